@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""Headline benchmark: DAE training cubes/s at |V|=22,000, d=256, B=512/GPU, BCE only, bf16
+(BASELINE.json configs[1]) on synthetic cubes, plus the recommend p50/p99 latency (configs[0]
+architecture: |V|=20,884, d=512, fp32, model resident).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+N>1 is launched by torch.distributed.run (one rank per GPU, RCCL); cubes shard data-parallel
+(weak scaling: B=512 per rank), gradients are all-reduced.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA (spec, no sparsity)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--V', type=int, default=22000)
+    ap.add_argument('--d', type=int, default=256)
+    ap.add_argument('--batch', type=int, default=512)
+    ap.add_argument('--cubes', type=int, default=65536)
+    ap.add_argument('--reg', type=float, default=0.0)
+    ap.add_argument('--dtype', default='bf16')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-steps', type=int, default=3)
+    ap.add_argument('--no-recommend', action='store_true')
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def roofline_for(name, ms, tr):
+    """Algorithmic bytes/flops per launch of the instrumented kernel."""
+    cfg = tr.cfg
+    V, d, B = cfg.V, cfg.d, cfg.batch_size
+    if name == 'cc_adam_dense':
+        n = tr.layout.total if tr.use_reg else tr.layout.main_total
+        byt = n * (16 + 12 + 2)                    # read p,m,v,g; write p,m,v; write bf16 shadow
+        return {'bound': 'hbm', 'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s', 'bytes_per_launch': byt}
+    if name in ('dec_bce_fwd', 'dec_dW', 'dec_dX'):
+        fl = 2.0 * B * d * V
+        return {'bound': 'mfma', 'achieved': fl / (ms * 1e-3) / 1e12, 'peak': BF16_PEAK_TFLOPS,
+                'unit': 'TFLOP/s', 'flops_per_launch': fl}
+    if name == 'cc_embed_gather_fwd':
+        xs = tr.x_cnt.float().mean().item()
+        byt = tr.R * xs * d * 2 + tr.R * d * 2
+        return {'bound': 'hbm', 'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s', 'bytes_per_launch': byt}
+    if name == 'cc_embed_scatter_bwd':
+        byt = V * d * 4 + V * ((tr.R + 31) // 32) * 4
+        return {'bound': 'hbm', 'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s', 'bytes_per_launch': byt}
+    return None
+
+
+def cpu_baseline(args, seconds_cap=30.0):
+    """The CPU oracle (numpy restatement of generator.py + model.py/train.py) on a bounded sample
+    of the same workload: a few B=512 steps at |V|=22k, d=256 (oracle is test infra; used here
+    only as the timed CPU baseline)."""
+    from threadpoolctl import threadpool_info
+    from oracle import model_ref, noise_ref
+    from cubecobrarecommender_amd.synthetic import synthetic_cubes, neg_sampler_from_csr
+    V, d, B = args.V, args.d, args.batch
+    C = max(B * args.cpu_steps, 1024)
+    indptr, indices = synthetic_cubes(C, V, seed=7, device='cuda' if torch.cuda.is_available() else 'cpu')
+    ns = neg_sampler_from_csr(indptr, indices, V)
+    lists = [indices[indptr[c]:indptr[c + 1]] for c in range(C)]
+    P = model_ref.init_params(V, d, seed=1)
+    Mo = {k: np.zeros_like(v) for k, v in P.items()}
+    Vo = {k: np.zeros_like(v) for k, v in P.items()}
+    rs = np.random.RandomState(0)
+    mt = noise_ref.MTNoise(rs, ns, V)
+    t0 = time.perf_counter()
+    done = 0
+    for s in range(args.cpu_steps):
+        xs, ys, _ = mt.batch(lists[s * B:(s + 1) * B])            # generator.py F (MT19937 replay)
+        _, G = model_ref.train_forward_backward(P, xs, ys, V, d, reg=0.0, mode='fp32')
+        P, Mo, Vo = model_ref.adam_tf(P, Mo, Vo, G, t=s + 1)
+        done += B
+        if time.perf_counter() - t0 > seconds_cap:
+            break
+    dt = time.perf_counter() - t0
+    threads = max([i.get('num_threads', 1) for i in threadpool_info()] + [1])
+    return {'value': done / dt, 'unit': 'cubes/s', 'cores': int(threads), 'kind': 'port',
+            'sample': f'{done} cubes ({done // B} steps of B={B}) at V={V}, d={d}: oracle numpy '
+                      f'generator (MT19937 replay of generator.py) + fp32 numpy fwd/bwd + TF-Adam'}
+
+
+def recommend_latency(n_req=1000):
+    from cubecobrarecommender_amd.layout import Layout
+    from cubecobrarecommender_amd.recommender import Recommender
+    V, d = 20884, 512
+    rng = np.random.default_rng(0)
+    lay = Layout(V, d)
+    flat = (rng.standard_normal(lay.total).astype(np.float32) * 0.02)
+    rec = Recommender(flat, V, d)
+    out = {}
+    for amount in (100, 30000):
+        lat = []
+        for i in range(n_req // 2 + 20):
+            cube = rng.choice(V, 360, replace=False)
+            t0 = time.perf_counter()
+            rec.recommend(cube, amount)
+            lat.append(time.perf_counter() - t0)
+        lat = np.array(lat[20:]) * 1e3
+        out[f'amount_{amount}'] = {'p50_ms': float(np.percentile(lat, 50)),
+                                   'p99_ms': float(np.percentile(lat, 99)), 'requests': len(lat)}
+    out['config'] = 'V=20884 d=512 fp32 resident model, cube n=360, index list in -> top-N indices out'
+    return out
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+    from cubecobrarecommender_amd.synthetic import synthetic_cubes, neg_sampler_from_csr
+    from cubecobrarecommender_amd.trainer import DeviceDataset, TrainConfig, Trainer
+    from cubecobrarecommender_amd.layout import Layout, glorot_flat
+    V, d, B = args.V, args.d, args.batch
+    t_setup = time.perf_counter()
+    indptr, indices = synthetic_cubes(args.cubes, V, seed=20250301, device=dev)
+    ns = neg_sampler_from_csr(indptr, indices, V)
+    y_mtx = None
+    if args.reg > 0:
+        from cubecobrarecommender_amd.adjacency import adjacency_normalised_gpu
+        y_mtx = adjacency_normalised_gpu(indptr, indices, V, device=dev)
+    data = DeviceDataset(csr=(indptr, indices), num_cards=V, neg_sampler=ns, y_mtx=y_mtx, device=dev)
+    cfg = TrainConfig(V=V, d=d, batch_size=B, reg=args.reg, dtype=args.dtype, seed=1234,
+                      rank=rank, world=world)
+    tr = Trainer(cfg, data, params_flat=glorot_flat(V, d, seed=42), device=dev)
+    rng = np.random.default_rng(99)      # same permutations on every rank
+    tr.set_epoch_permutations(np.stack([rng.permutation(args.cubes) for _ in range(4)]))
+    setup_s = time.perf_counter() - t_setup
+
+    def step():
+        tr.forward_backward()
+        if world > 1:
+            import torch.distributed as dist
+            n = tr.layout.total if tr.use_reg else tr.layout.main_total
+            dist.all_reduce(tr.grads[:n], op=dist.ReduceOp.AVG)
+        tr.apply()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    tr.timing = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier(world)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    tr.timing = False
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ktimes = tr.kernel_times_ms()
+    losses = tr.losses()
+    if rank != 0:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+    value = B * world * args.steps / dt
+    dom = max(ktimes, key=lambda k: ktimes[k] * (2 if k.startswith('dec_') and tr.use_reg else 1))
+    roof = roofline_for(dom, ktimes[dom], tr)
+    roof['frac'] = roof['achieved'] / roof['peak']
+    roof['kernel'] = dom
+    roof['avg_ms'] = ktimes[dom]
+    roof['traffic'] = None
+    out = {
+        'metric': 'training cubes/sec at |V|~22k d=256; top-N recommend p50 latency',
+        'value': value, 'unit': 'cubes/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype,
+        'data': 'synthetic cubes (SURVEY §8(d): Zipf popularity, sizes 180-720, C=65536), random-init weights',
+        'config': {'workload': 'DAE training step (F noise + E + D1/BCE' + (' + D2/KL' if args.reg > 0 else '')
+                               + ' + backward + Adam), BASELINE configs[1]',
+                   'V': V, 'd': d, 'batch_per_gpu': B, 'global_batch': B * world, 'reg': args.reg,
+                   'cubes': args.cubes, 'parallelism': f'dp{world}'},
+        'roofline': roof,
+        'kernel_ms': ktimes,
+        'final_loss': losses,
+        'setup_s': setup_s,
+    }
+    if not args.no_recommend and world == 1:
+        out['recommend'] = recommend_latency()
+    if not args.no_cpu_baseline and world == 1:
+        out['cpu_baseline'] = cpu_baseline(args)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

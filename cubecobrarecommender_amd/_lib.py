@@ -1,0 +1,110 @@
+"""ctypes binding of libccrec_hip.so (include/ccrec.h).  Fails loudly when the library is missing:
+there is no CPU fallback anywhere in the product path."""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('CCREC_LIB', os.path.join(_HERE, 'libccrec_hip.so'))
+
+CC_F32, CC_BF16 = 0, 1
+CC_EPI_STORE, CC_EPI_BCE, CC_EPI_MASK, CC_EPI_SPLITK = 0, 1, 2, 3
+CC_NUM_TENSORS = 24
+
+
+class CCError(RuntimeError):
+    pass
+
+
+class NoiseArgs(C.Structure):
+    _fields_ = [
+        ('V', C.c_int32), ('B', C.c_int32), ('x_cap', C.c_int32), ('with_reg', C.c_int32),
+        ('seed', C.c_uint64), ('slot_base', C.c_uint32), ('batch_stride', C.c_int32),
+        ('batch_offset', C.c_int32), ('noise_mean', C.c_double), ('noise_std', C.c_double),
+        ('cube_ptr', C.c_void_p), ('cube_idx', C.c_void_p), ('perm', C.c_void_p),
+        ('cdf', C.c_void_p), ('neg_sampler', C.c_void_p), ('state', C.c_void_p),
+        ('x_cnt', C.c_void_p), ('x_idx', C.c_void_p), ('y_bits', C.c_void_p),
+        ('xt_bits', C.c_void_p), ('reg_idx', C.c_void_p), ('status', C.c_void_p),
+    ]
+
+
+class GemmArgs(C.Structure):
+    _fields_ = [
+        ('dtype', C.c_int32), ('ta', C.c_int32), ('tb', C.c_int32), ('epilogue', C.c_int32),
+        ('M', C.c_int32), ('N', C.c_int32), ('K', C.c_int32), ('lda', C.c_int32),
+        ('ldb', C.c_int32), ('ldc', C.c_int32), ('splits', C.c_int32), ('relu', C.c_int32),
+        ('A', C.c_void_p), ('B', C.c_void_p), ('bias', C.c_void_p), ('C', C.c_void_p),
+        ('Cf', C.c_void_p), ('H', C.c_void_p), ('y_bits', C.c_void_p), ('scale', C.c_float),
+        ('loss_partials', C.c_void_p),
+    ]
+
+
+_P, _I32, _I64, _F32, _F64, _SZ = C.c_void_p, C.c_int32, C.c_int64, C.c_float, C.c_double, C.c_size_t
+
+# name -> (restype, argtypes); every symbol include/ccrec.h declares
+SIGNATURES = {
+    'cc_abi_version': (C.c_int, []),
+    'cc_last_error_string': (C.c_char_p, []),
+    'cc_param_layout': (C.c_int, [_I32, _I32, _P, _P, _P, _P]),
+    'cc_noise_fwd': (C.c_int, [C.POINTER(NoiseArgs), _P]),
+    'cc_embed_gather_fwd': (C.c_int, [_I32, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P]),
+    'cc_embed_scatter_bwd': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P]),
+    'cc_gemm': (C.c_int, [C.POINTER(GemmArgs), _P]),
+    'cc_gemm_grid': (C.c_int, [_I32, _I32, _P]),
+    'cc_splitk_reduce': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
+    'cc_colsum': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P]),
+    'cc_dec_bce_fused': (C.c_int, [_I32, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
+    'cc_dec_softmax_kl_fused': (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _F32, _P, _P, _P]),
+    'cc_reduce_loss': (C.c_int, [_P, _I32, _F64, _P, _P]),
+    'cc_adam_dense': (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _F32, _F32, _F32, _F32, _P]),
+    'cc_to_bf16': (C.c_int, [_P, _P, _I64, _P]),
+    'cc_state_advance': (C.c_int, [_P, _P]),
+    'cc_infer_encode_fp32': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
+    'cc_infer_decode_fp32': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
+    'cc_topn_workspace_size': (_SZ, [_I32]),
+    'cc_topn': (C.c_int, [_P, _I32, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the library with typed entry points."""
+    global _lib
+    if _lib is None:
+        # Load torch (and with it PyTorch's HIP runtime) first so libccrec_hip binds to the same
+        # libamdhip64 instance as the tensors it is handed; a second HIP runtime in the process
+        # sees no device.
+        import torch  # noqa: F401
+        if not os.path.exists(LIB_PATH):
+            raise CCError(f'libccrec_hip.so not found at {LIB_PATH}; build it with '
+                          f'`python -m cubecobrarecommender_amd.build` (no CPU fallback exists)')
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.cc_abi_version() != 1:
+            raise CCError('libccrec_hip ABI version mismatch')
+        _lib = L
+    return _lib
+
+
+def check(rc, what=''):
+    if rc != 0:
+        msg = lib().cc_last_error_string()
+        raise CCError(f'{what} failed ({rc}): {msg.decode() if msg else ""}')
+
+
+def call(name, *args):
+    check(getattr(lib(), name)(*args), name)
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (None -> NULL)."""
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)

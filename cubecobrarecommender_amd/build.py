@@ -1,0 +1,57 @@
+"""Build libccrec_hip.so in-tree for gfx950 with hipcc (no CUDA, no hipify, no JIT cache).
+
+Usage: python -m cubecobrarecommender_amd.build [--force]
+The .so lands next to this file so gpurun snapshots carry it to the GPU box.
+"""
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, 'csrc')
+INC = os.path.join(ROOT, 'include')
+OBJ = os.path.join(PKG, 'build_obj')
+LIB = os.path.join(PKG, 'libccrec_hip.so')
+ARCH = os.environ.get('CCREC_ARCH', 'gfx950')
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+FLAGS = ['-O3', '-fPIC', '-std=c++17', f'--offload-arch={ARCH}', '-I', INC, '-I', CSRC,
+         '-Wall', '-Wno-unused-function', '-Wno-unused-variable']
+
+
+def sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(('.hip', '.cpp')))
+
+
+def _headers_mtime():
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(('.hpp', '.h'))]
+    hs.append(os.path.join(INC, 'ccrec.h'))
+    return max(os.path.getmtime(h) for h in hs)
+
+
+def _compile(src, force):
+    obj = os.path.join(OBJ, os.path.basename(src) + '.o')
+    if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(src), _headers_mtime()):
+        return obj
+    cmd = [HIPCC, *FLAGS, '-c', src, '-o', obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f'hipcc failed for {src}:\n{r.stderr}')
+    return obj
+
+
+def build(force=False, jobs=8):
+    os.makedirs(OBJ, exist_ok=True)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force), sources()))
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        cmd = [HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', *objs, '-o', LIB]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f'link failed:\n{r.stderr}')
+    return LIB
+
+
+if __name__ == '__main__':
+    print(build(force='--force' in sys.argv))

@@ -1,0 +1,321 @@
+// Generic LDS-staged MFMA GEMM with fused epilogues — the Dense layers of the encoder and
+// decoder towers (model.py:29-33, 58-62), the decoder output layers (model.py:64) and their
+// backward products.  C[M,N] = op(A)[M,K] op(B)[K,N], fp32 accumulation.
+//
+//   bf16 operands: v_mfma_f32_32x32x16_bf16   (lane l: A[l&31][8(l>>5)+j], B[8(l>>5)+j][l&31])
+//   fp32 operands: v_mfma_f32_32x32x2_f32     (lane l: A[l&31][l>>5],       B[l>>5][l&31]) —
+//                  exact fp32 (a k-ordered fmaf chain), used for the fp32 parity mode.
+// Workgroup = 4 waves (256 threads), 64x64 output tile, 2x2 waves of 32x32, BK = 32.
+// Both LDS images are K-contiguous ([row][k] / [col][k]); transposed global layouts are
+// transposed during staging so every fragment read is one ds_read_b128 (bf16) / b32 (fp32).
+// Accumulator map (32x32): row = (r&3) + 8(r>>2) + 4(l>>5), col = l&31.
+#include "common.hpp"
+
+namespace {
+
+constexpr int BM = 64, BN = 64, BK = 32, NT = 256;
+
+struct GemmParams {
+  int M, N, K, lda, ldb, ldc, splits, relu;
+  int vec_a, vec_b;
+  const void *A, *B;
+  const float *bias;
+  void *C;
+  float *Cf;
+  const void *H;
+  const uint32_t *y_bits;
+  float scale;
+  double *loss_partials;
+};
+
+template <typename T> struct Mma;
+template <> struct Mma<bf16_t> {
+  static constexpr int KM = 16;
+  static __device__ __forceinline__ void step(const bf16_t *a_row, const bf16_t *b_row, int kk,
+                                              int half, f32x16_t &acc) {
+    const bf16x8_t a = *reinterpret_cast<const bf16x8_t *>(a_row + kk + 8 * half);
+    const bf16x8_t b = *reinterpret_cast<const bf16x8_t *>(b_row + kk + 8 * half);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+  }
+};
+template <> struct Mma<float> {
+  static constexpr int KM = 2;
+  static __device__ __forceinline__ void step(const float *a_row, const float *b_row, int kk,
+                                              int half, f32x16_t &acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a_row[kk + half], b_row[kk + half], acc, 0, 0, 0);
+  }
+};
+
+// Stage a ROWS x BK tile of the logical operand X[row][k] (row in [r0, r0+ROWS), k in [k0, kend))
+// into LDS image S[row][k].  KCONTIG: storage X[row*ld + k]; else storage X[k*ld + row].
+template <typename T, bool KCONTIG, int ROWS, int LDK>
+__device__ __forceinline__ void stage(T (*S)[LDK], const T *__restrict__ X, int ld, int r0,
+                                      int rlim, int k0, int kend, bool vec_ok) {
+  constexpr int VW = 16 / sizeof(T);
+  using V16 = uint4;
+  if constexpr (KCONTIG) {
+    constexpr int PER_ROW = BK / VW;
+    for (int v = threadIdx.x; v < ROWS * PER_ROW; v += NT) {
+      const int r = v / PER_ROW, kv = (v % PER_ROW) * VW;
+      const int gr = r0 + r, gk = k0 + kv;
+      if (vec_ok && gr < rlim && gk + VW <= kend) {
+        *reinterpret_cast<V16 *>(&S[r][kv]) =
+            *reinterpret_cast<const V16 *>(X + (int64_t)gr * ld + gk);
+      } else {
+#pragma unroll
+        for (int e = 0; e < VW; ++e)
+          S[r][kv + e] = (gr < rlim && gk + e < kend) ? X[(int64_t)gr * ld + gk + e] : T(0);
+      }
+    }
+  } else {
+    constexpr int PER_K = ROWS / VW;
+    for (int v = threadIdx.x; v < BK * PER_K; v += NT) {
+      const int k = v / PER_K, rv = (v % PER_K) * VW;
+      const int gk = k0 + k, gr = r0 + rv;
+      T tmp[VW];
+      if (vec_ok && gk < kend && gr + VW <= rlim) {
+        *reinterpret_cast<V16 *>(tmp) = *reinterpret_cast<const V16 *>(X + (int64_t)gk * ld + gr);
+      } else {
+#pragma unroll
+        for (int e = 0; e < VW; ++e)
+          tmp[e] = (gk < kend && gr + e < rlim) ? X[(int64_t)gk * ld + gr + e] : T(0);
+      }
+#pragma unroll
+      for (int e = 0; e < VW; ++e) S[rv + e][k] = tmp[e];
+    }
+  }
+}
+
+__device__ __forceinline__ double block_sum_double(double v, double *red) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  const int wave = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < NT / 64; ++w) s += red[w];
+  return s;
+}
+
+template <typename T, bool TA, bool TB, int EPI>
+__global__ __launch_bounds__(NT) void gemm_kernel(GemmParams p) {
+  constexpr int PADK = 16 / sizeof(T);
+  constexpr int LDK = BK + PADK;
+  __shared__ __attribute__((aligned(16))) T As[BM][LDK];
+  __shared__ __attribute__((aligned(16))) T Bs[BN][LDK];
+  __shared__ double red[NT / 64];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int bm = blockIdx.y * BM, bn = blockIdx.x * BN;
+  int kbeg = 0, kend = p.K;
+  if constexpr (EPI == CC_EPI_SPLITK) {
+    const int kchunk = (int)cdiv(cdiv(p.K, p.splits), BK) * BK;
+    kbeg = blockIdx.z * kchunk;
+    kend = min(p.K, kbeg + kchunk);
+  }
+  const T *__restrict__ A = reinterpret_cast<const T *>(p.A);
+  const T *__restrict__ B = reinterpret_cast<const T *>(p.B);
+  f32x16_t acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const T *a_row = &As[wm * 32 + (lane & 31)][0];
+  const T *b_row = &Bs[wn * 32 + (lane & 31)][0];
+  const int half = lane >> 5;
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    stage<T, !TA, BM, LDK>(As, A, p.lda, bm, p.M, k0, kend, p.vec_a);
+    stage<T, TB, BN, LDK>(Bs, B, p.ldb, bn, p.N, k0, kend, p.vec_b);
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += Mma<T>::KM) Mma<T>::step(a_row, b_row, kk, half, acc);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------------ epilogues
+  const int gn = bn + wn * 32 + (lane & 31);
+  double loss = 0.0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int gm = bm + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+    if (gm >= p.M || gn >= p.N) continue;
+    const float a = acc[r];
+    if constexpr (EPI == CC_EPI_SPLITK) {
+      p.Cf[((int64_t)blockIdx.z * p.M + gm) * p.N + gn] = a;
+    } else if constexpr (EPI == CC_EPI_STORE) {
+      float v = a + (p.bias ? p.bias[gn] : 0.f);
+      if (p.relu) v = v > 0.f ? v : 0.f;
+      const int64_t o = (int64_t)gm * p.ldc + gn;
+      if (p.C) DT<T>::st(reinterpret_cast<T *>(p.C) + o, v);
+      if (p.Cf) p.Cf[o] = v;
+    } else if constexpr (EPI == CC_EPI_MASK) {
+      const int64_t o = (int64_t)gm * p.ldc + gn;
+      const float h = DT<T>::ld(reinterpret_cast<const T *>(p.H) + o);
+      const float v = h > 0.f ? a : 0.f;
+      if (p.C) DT<T>::st(reinterpret_cast<T *>(p.C) + o, v);
+      if (p.Cf) p.Cf[o] = v;
+    } else if constexpr (EPI == CC_EPI_BCE) {
+      // sigmoid_cross_entropy_with_logits (TF 2.5 Keras BCE on a Sigmoid output)
+      const float z = a + p.bias[gn];
+      const int YW = (p.N + 31) >> 5;
+      const float y = (float)((p.y_bits[(int64_t)gm * YW + (gn >> 5)] >> (gn & 31)) & 1u);
+      const float az = fabsf(z);
+      loss += (double)(fmaxf(z, 0.f) - z * y + log1pf(expf(-az)));
+      const float e = expf(-az);
+      const float sig = z >= 0.f ? 1.f / (1.f + e) : e / (1.f + e);
+      const float dz = (sig - y) * p.scale;
+      const int64_t o = (int64_t)gm * p.ldc + gn;
+      if (p.C) DT<T>::st(reinterpret_cast<T *>(p.C) + o, dz);
+      if (p.Cf) p.Cf[o] = dz;
+    }
+  }
+  if constexpr (EPI == CC_EPI_BCE) {
+    const double s = block_sum_double(loss, red);
+    if (threadIdx.x == 0) p.loss_partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+template <typename T, int EPI>
+int launch_t(const cc_gemm_args *g, const GemmParams &p, hipStream_t s) {
+  const dim3 grid((unsigned)cdiv(g->N, BN), (unsigned)cdiv(g->M, BM),
+                  EPI == CC_EPI_SPLITK ? (unsigned)g->splits : 1u);
+  const dim3 block(NT);
+  if (g->ta && g->tb)
+    hipLaunchKernelGGL((gemm_kernel<T, true, true, EPI>), grid, block, 0, s, p);
+  else if (g->ta)
+    hipLaunchKernelGGL((gemm_kernel<T, true, false, EPI>), grid, block, 0, s, p);
+  else if (g->tb)
+    hipLaunchKernelGGL((gemm_kernel<T, false, true, EPI>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_kernel<T, false, false, EPI>), grid, block, 0, s, p);
+  CC_LAUNCH_CHECK("gemm_kernel");
+  return CC_OK;
+}
+
+template <typename T>
+int launch_epi(const cc_gemm_args *g, const GemmParams &p, hipStream_t s) {
+  switch (g->epilogue) {
+    case CC_EPI_STORE: return launch_t<T, CC_EPI_STORE>(g, p, s);
+    case CC_EPI_BCE: return launch_t<T, CC_EPI_BCE>(g, p, s);
+    case CC_EPI_MASK: return launch_t<T, CC_EPI_MASK>(g, p, s);
+    case CC_EPI_SPLITK: return launch_t<T, CC_EPI_SPLITK>(g, p, s);
+  }
+  return cc::fail(CC_ERR_ARG, "cc_gemm: unknown epilogue");
+}
+
+// ---------------------------------------------------------------- split-K reduce / colsum / loss
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restrict__ part,
+                                                            int splits, int M, int N,
+                                                            const T *__restrict__ H, T *C,
+                                                            float *Cf) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t MN = (int64_t)M * N;
+  if (i >= MN) return;
+  float s = 0.f;
+  for (int z = 0; z < splits; ++z) s += part[z * MN + i];
+  if (H) s = DT<T>::ld(H + i) > 0.f ? s : 0.f;
+  if (C) DT<T>::st(C + i, s);
+  if (Cf) Cf[i] = s;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(const T *__restrict__ X, int R, int N, int ld,
+                                                     float *__restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += DT<T>::ld(X + (int64_t)r * ld + n);
+  out[n] = s;
+}
+
+__global__ void reduce_loss_kernel(const double *__restrict__ part, int n, double scale,
+                                   double *out) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += part[i];
+  const double t = block_sum_double(s, red);
+  if (threadIdx.x == 0) out[0] = t * scale;
+}
+
+}  // namespace
+
+extern "C" int cc_gemm_grid(int32_t M, int32_t N, int32_t *tiles) {
+  CC_REQUIRE(tiles, "cc_gemm_grid: null");
+  *tiles = (int32_t)(cdiv(M, BM) * cdiv(N, BN));
+  return CC_OK;
+}
+
+extern "C" int cc_gemm(const cc_gemm_args *g, void *stream) {
+  CC_REQUIRE(g && g->A && g->B, "cc_gemm: null operand");
+  CC_REQUIRE(g->M >= 0 && g->N >= 0 && g->K >= 0, "cc_gemm: negative size");
+  CC_REQUIRE(g->dtype == CC_BF16 || g->dtype == CC_F32, "cc_gemm: dtype");
+  if (g->M == 0 || g->N == 0) return CC_OK;
+  if (g->epilogue == CC_EPI_SPLITK) CC_REQUIRE(g->splits >= 1 && g->Cf, "cc_gemm: split-K needs Cf, splits>=1");
+  if (g->epilogue == CC_EPI_BCE)
+    CC_REQUIRE(g->bias && g->y_bits && g->loss_partials, "cc_gemm: BCE needs bias, y_bits, loss_partials");
+  if (g->epilogue == CC_EPI_MASK) CC_REQUIRE(g->H, "cc_gemm: MASK needs H");
+  const int vw = g->dtype == CC_BF16 ? 8 : 4;
+  GemmParams p;
+  p.M = g->M; p.N = g->N; p.K = g->K;
+  p.lda = g->lda; p.ldb = g->ldb; p.ldc = g->ldc;
+  p.splits = g->splits; p.relu = g->relu;
+  p.vec_a = (g->lda % vw == 0) && ((uintptr_t)g->A % 16 == 0);
+  p.vec_b = (g->ldb % vw == 0) && ((uintptr_t)g->B % 16 == 0);
+  p.A = g->A; p.B = g->B; p.bias = g->bias; p.C = g->C; p.Cf = g->Cf; p.H = g->H;
+  p.y_bits = g->y_bits; p.scale = g->scale; p.loss_partials = g->loss_partials;
+  hipStream_t s = as_stream(stream);
+  return g->dtype == CC_BF16 ? launch_epi<bf16_t>(g, p, s) : launch_epi<float>(g, p, s);
+}
+
+extern "C" int cc_splitk_reduce(int32_t dtype, const float *partials, int32_t splits, int32_t M,
+                                int32_t N, const void *H, void *C, float *Cf, void *stream) {
+  CC_REQUIRE(partials && splits >= 1, "cc_splitk_reduce: args");
+  const int64_t MN = (int64_t)M * N;
+  if (MN == 0) return CC_OK;
+  const dim3 grid((unsigned)cdiv(MN, 256)), block(256);
+  if (dtype == CC_BF16)
+    hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, grid, block, 0, as_stream(stream), partials,
+                       splits, M, N, (const bf16_t *)H, (bf16_t *)C, Cf);
+  else
+    hipLaunchKernelGGL(splitk_reduce_kernel<float>, grid, block, 0, as_stream(stream), partials,
+                       splits, M, N, (const float *)H, (float *)C, Cf);
+  CC_LAUNCH_CHECK("splitk_reduce_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_colsum(int32_t dtype, const void *X, int32_t R, int32_t N, int32_t ld,
+                         float *out, void *stream) {
+  CC_REQUIRE(X && out, "cc_colsum: null");
+  if (N == 0) return CC_OK;
+  const dim3 grid((unsigned)cdiv(N, 256)), block(256);
+  if (dtype == CC_BF16)
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, block, 0, as_stream(stream), (const bf16_t *)X, R, N, ld, out);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, block, 0, as_stream(stream), (const float *)X, R, N, ld, out);
+  CC_LAUNCH_CHECK("colsum_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_reduce_loss(const double *partials, int32_t n, double scale, double *loss_out,
+                              void *stream) {
+  CC_REQUIRE(partials && loss_out && n >= 0, "cc_reduce_loss: args");
+  hipLaunchKernelGGL(reduce_loss_kernel, dim3(1), dim3(256), 0, as_stream(stream), partials, n,
+                     scale, loss_out);
+  CC_LAUNCH_CHECK("reduce_loss_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_dec_bce_fused(int32_t dtype, const void *H3, const void *Wo, const float *bo,
+                                int32_t B, int32_t d, int32_t V, const uint32_t *y_bits, void *dZ,
+                                double *loss_partials, int32_t *n_partials, void *stream) {
+  cc_gemm_args g = {};
+  g.dtype = dtype; g.ta = 0; g.tb = 0; g.epilogue = CC_EPI_BCE;
+  g.M = B; g.N = V; g.K = d; g.lda = d; g.ldb = V; g.ldc = V;
+  g.A = H3; g.B = Wo; g.bias = bo; g.C = dZ; g.y_bits = y_bits;
+  g.scale = 1.0f / ((float)B * (float)V);
+  g.loss_partials = loss_partials;
+  if (n_partials) *n_partials = (int32_t)(cdiv(B, BM) * cdiv(V, BN));
+  return cc_gemm(&g, stream);
+}

@@ -1,0 +1,214 @@
+// cc_noise_fwd — the DAE input-noise function F and regulariser-row sampling on the GPU.
+//
+// Replaces src/ml/generator.py:38-103 (DataGenerator.__getitem__ / generate_data).  One
+// 256-thread workgroup per cube; every draw is a pure function of
+// (seed, step, slot, kind, index, try) through Philox4x32-10, so the whole batch is
+// deterministic and bit-identical to oracle/noise_ref.py::philox_noise_batch.
+//
+// Per cube (n sorted card ids, LDS bitmasks over V):
+//   noise = clip(mean + std * BoxMuller, .05, .8)          generator.py:86-90
+//   k     = int(n * noise)                                  :91
+//   cut   : k draws w/ replacement from the includes        :92
+//   ycut  : k//4 draws w/ replacement from the cut multiset :95
+//   add   : k draws, rejection against the global CDF of neg_sampler until the card is not
+//           in the cube (== the renormalised law of :93-94), exact fallback after 256 tries
+//   x = (cube \ cut) U add  (sorted CSR row),  y = cube \ ycut  (bitmask)     :96-101
+// The B reg rows (generator.py:47-51) are drawn by thread 0 of each block into rows B..2B-1.
+#include "common.hpp"
+#include "detmath.hpp"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr uint32_t KIND_NOISE = 0, KIND_CUT = 1, KIND_YCUT = 2, KIND_ADD = 3, KIND_ADD_FB = 4,
+                   KIND_REG = 5;
+constexpr int ADD_MAX_TRIES = 256;
+
+__device__ __forceinline__ u32x4 rng(uint64_t seed, uint32_t step, uint32_t slot, uint32_t kind,
+                                     uint32_t idx, uint32_t tries) {
+  return philox4x32_10(idx, (kind << 24) | tries, slot, step, (uint32_t)seed,
+                       (uint32_t)(seed >> 32));
+}
+
+// first index j with cdf[j] > u  (numpy searchsorted side='right')
+__device__ __forceinline__ int search_right(const double *__restrict__ cdf, int V, double u) {
+  int lo = 0, hi = V;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (cdf[mid] <= u)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo < V ? lo : V - 1;
+}
+
+__device__ __forceinline__ double noise_level(double mean, double std, double z) {
+#pragma clang fp contract(off)
+  double lvl = mean + std * z;
+  lvl = lvl < 0.05 ? 0.05 : lvl;
+  return lvl > 0.8 ? 0.8 : lvl;
+}
+
+__device__ __forceinline__ bool bit_of(const uint32_t *bits, int j) {
+  return (bits[j >> 5] >> (j & 31)) & 1u;
+}
+
+// Exact (rare) fallback: inverse CDF over the excludes by a sequential fp64 scan.
+__device__ int add_fallback(const double *__restrict__ ns, int V, const uint32_t *cube_bits,
+                            double u01) {
+  double s = 0.0;
+  for (int j = 0; j < V; ++j)
+    if (!bit_of(cube_bits, j)) s += ns[j];
+  if (!(s > 0.0)) return -1;
+  const double u = u01 * s;
+  double acc = 0.0;
+  int last = -1;
+  for (int j = 0; j < V; ++j) {
+    if (bit_of(cube_bits, j)) continue;
+    if (ns[j] > 0.0) last = j;
+    acc += ns[j];
+    if (acc > u) return j;
+  }
+  return last;
+}
+
+__global__ __launch_bounds__(NT) void noise_kernel(cc_noise_args a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int VW = (a.V + 31) >> 5;
+  uint32_t *cube_bits = smem;
+  uint32_t *cut_bits = cube_bits + VW;
+  uint32_t *ycut_bits = cut_bits + VW;
+  uint32_t *add_bits = ycut_bits + VW;
+  int32_t *scan = (int32_t *)(add_bits + VW);  // [NT + 1]
+  int32_t *cut_card = scan + NT + 1;           // [x_cap]
+  __shared__ int s_k;
+
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const uint32_t slot = a.slot_base + (uint32_t)b;
+  const int64_t step64 = a.state[0];
+  const int64_t batch = a.state[1];
+  const uint32_t step = (uint32_t)step64;
+  const int R = a.with_reg ? 2 * a.B : a.B;
+  const int XW = (R + 31) >> 5;
+
+  const int32_t cube = a.perm[batch * (int64_t)a.batch_stride + a.batch_offset + b];
+  const int64_t beg = a.cube_ptr[cube];
+  const int n = (int)(a.cube_ptr[cube + 1] - beg);
+  const int32_t *__restrict__ inc = a.cube_idx + beg;
+
+  for (int w = tid; w < 4 * VW; w += NT) cube_bits[w] = 0u;
+  __syncthreads();
+  for (int i = tid; i < n; i += NT) {
+    const int j = inc[i];
+    atomicOr(&cube_bits[j >> 5], 1u << (j & 31));
+  }
+  if (tid == 0) {
+    const u32x4 o = rng(a.seed, step, slot, KIND_NOISE, 0, 0);
+    const double z = detm::det_normal(u53_open0(o.x, o.y), u53(o.z, o.w));
+    const double lvl = noise_level(a.noise_mean, a.noise_std, z);
+    int k = (int)((double)n * lvl);
+    if (n + k > a.x_cap) {  // cannot happen when x_cap >= 1.8 * max cube size
+      atomicOr(a.status, 1);
+      k = a.x_cap - n > 0 ? a.x_cap - n : 0;
+    }
+    s_k = k;
+  }
+  __syncthreads();
+  const int k = s_k;
+  // cut draws (with replacement from the includes)
+  for (int i = tid; i < k; i += NT) {
+    const uint32_t pos = mulhi_bound(rng(a.seed, step, slot, KIND_CUT, (uint32_t)i, 0).x, (uint32_t)n);
+    const int card = inc[pos];
+    cut_card[i] = card;
+    atomicOr(&cut_bits[card >> 5], 1u << (card & 31));
+  }
+  __syncthreads();
+  // ycut draws from the cut multiset
+  const int nq = k >> 2;
+  for (int q = tid; q < nq; q += NT) {
+    const uint32_t qq = mulhi_bound(rng(a.seed, step, slot, KIND_YCUT, (uint32_t)q, 0).x, (uint32_t)k);
+    const int card = cut_card[qq];
+    atomicOr(&ycut_bits[card >> 5], 1u << (card & 31));
+  }
+  // add draws (rejection against the global CDF)
+  for (int i = tid; i < k; i += NT) {
+    int pick = -1;
+    for (int t = 0; t < ADD_MAX_TRIES; ++t) {
+      const u32x4 o = rng(a.seed, step, slot, KIND_ADD, (uint32_t)i, (uint32_t)t);
+      const int j = search_right(a.cdf, a.V, u53(o.x, o.y));
+      if (!bit_of(cube_bits, j)) {
+        pick = j;
+        break;
+      }
+    }
+    if (pick < 0) {
+      const u32x4 o = rng(a.seed, step, slot, KIND_ADD_FB, (uint32_t)i, 0);
+      pick = add_fallback(a.neg_sampler, a.V, cube_bits, u53(o.x, o.y));
+    }
+    if (pick >= 0) atomicOr(&add_bits[pick >> 5], 1u << (pick & 31));
+  }
+  __syncthreads();
+  // y bitmask: cube \ ycut
+  uint32_t *yrow = a.y_bits + (int64_t)b * VW;
+  for (int w = tid; w < VW; w += NT) yrow[w] = cube_bits[w] & ~ycut_bits[w];
+  // x: sorted compaction of (cube \ cut) | add  — chunked block scan over the VW words
+  const int per = (VW + NT - 1) / NT;
+  const int w0 = tid * per, w1 = min(VW, w0 + per);
+  int cnt = 0;
+  for (int w = w0; w < w1; ++w) cnt += __popc((cube_bits[w] & ~cut_bits[w]) | add_bits[w]);
+  scan[tid] = cnt;
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int t = 0; t < NT; ++t) {
+      const int c = scan[t];
+      scan[t] = run;
+      run += c;
+    }
+    scan[NT] = run;
+  }
+  __syncthreads();
+  int pos = scan[tid];
+  int32_t *xrow = a.x_idx + (int64_t)b * a.x_cap;
+  for (int w = w0; w < w1; ++w) {
+    uint32_t m = (cube_bits[w] & ~cut_bits[w]) | add_bits[w];
+    while (m) {
+      const int bit = __ffs(m) - 1;
+      m &= m - 1;
+      const int j = (w << 5) + bit;
+      if (pos < a.x_cap) xrow[pos] = j;
+      if (a.xt_bits) atomicOr(&a.xt_bits[(int64_t)j * XW + (b >> 5)], 1u << (b & 31));
+      ++pos;
+    }
+  }
+  if (tid == 0) a.x_cnt[b] = min(scan[NT], a.x_cap);
+  // regulariser row for this slot (generator.py:47-51): one draw ∝ neg_sampler
+  if (a.with_reg && tid == 0) {
+    const u32x4 o = rng(a.seed, step, slot, KIND_REG, 0, 0);
+    const int j = search_right(a.cdf, a.V, u53(o.x, o.y));
+    a.reg_idx[b] = j;
+    const int r = a.B + b;
+    a.x_idx[(int64_t)r * a.x_cap] = j;
+    a.x_cnt[r] = 1;
+    if (a.xt_bits) atomicOr(&a.xt_bits[(int64_t)j * XW + (r >> 5)], 1u << (r & 31));
+  }
+}
+
+}  // namespace
+
+extern "C" int cc_noise_fwd(const cc_noise_args *a, void *stream) {
+  CC_REQUIRE(a != nullptr, "cc_noise_fwd: null args");
+  CC_REQUIRE(a->V > 0 && a->B > 0 && a->x_cap > 0, "cc_noise_fwd: bad V/B/x_cap");
+  CC_REQUIRE(a->cube_ptr && a->cube_idx && a->perm && a->cdf && a->neg_sampler && a->state,
+             "cc_noise_fwd: null input pointer");
+  CC_REQUIRE(a->x_cnt && a->x_idx && a->y_bits && a->status, "cc_noise_fwd: null output pointer");
+  CC_REQUIRE(!a->with_reg || a->reg_idx, "cc_noise_fwd: with_reg needs reg_idx");
+  const int VW = (a->V + 31) / 32;
+  const size_t lds = (size_t)(4 * VW + NT + 1 + a->x_cap) * 4;
+  CC_REQUIRE(lds <= 150 * 1024, "cc_noise_fwd: V / x_cap too large for LDS");
+  hipLaunchKernelGGL(noise_kernel, dim3(a->B), dim3(NT), lds, as_stream(stream), *a);
+  CC_LAUNCH_CHECK("noise_kernel");
+  return CC_OK;
+}

@@ -1,0 +1,71 @@
+"""Flat parameter layout shared by the kernels, Adam, the bf16 shadow and checkpoints.
+
+Tensor order is the Keras creation order of ``src/ml/model.py`` (:27-33 encoder, :58-64 decoder,
+:92-98 ``decoder`` then ``decoder_for_reg``).  Mirrors ``cc_param_layout`` (api.cpp); a CPU test
+checks the two agree.
+"""
+import numpy as np
+
+LAYERS = ('encoder/encoded_1', 'encoder/encoded_2', 'encoder/encoded_3', 'encoder/bottleneck',
+          'decoder/decoded_1', 'decoder/decoded_2', 'decoder/decoded_3', 'decoder/reconstruct',
+          'decoder_for_reg/decoded_1', 'decoder_for_reg/decoded_2', 'decoder_for_reg/decoded_3',
+          'decoder_for_reg/reconstruct')
+NAMES = tuple(n for l in LAYERS for n in (l + '/kernel', l + '/bias'))
+
+
+def layer_shapes(V, d):
+    return ((V, d), (d, 256), (256, 128), (128, 64),
+            (64, 128), (128, 256), (256, d), (d, V),
+            (64, 128), (128, 256), (256, d), (d, V))
+
+
+class Layout:
+    """name -> (offset, shape) in the flat fp32 buffer; 64-element aligned tensors."""
+
+    def __init__(self, V, d):
+        self.V, self.d = int(V), int(d)
+        self.entries = {}
+        o = 0
+        for li, (fi, fo) in enumerate(layer_shapes(V, d)):
+            for name, shape in ((LAYERS[li] + '/kernel', (fi, fo)), (LAYERS[li] + '/bias', (fo,))):
+                self.entries[name] = (o, shape)
+                o += (int(np.prod(shape)) + 63) // 64 * 64
+            if li == 7:
+                self.main_total = o
+        self.total = o
+
+    def offset(self, name):
+        return self.entries[name][0]
+
+    def shape(self, name):
+        return self.entries[name][1]
+
+    def view(self, flat, name):
+        o, shape = self.entries[name]
+        n = int(np.prod(shape))
+        return flat[o:o + n].reshape(shape)
+
+    def pack(self, params, out=None):
+        """dict name -> array  ->  flat float32 numpy buffer (padding zero)."""
+        flat = np.zeros(self.total, np.float32) if out is None else out
+        for name in NAMES:
+            if name in params:
+                o, shape = self.entries[name]
+                flat[o:o + int(np.prod(shape))] = np.asarray(params[name], np.float32).reshape(-1)
+        return flat
+
+    def unpack(self, flat):
+        flat = np.asarray(flat)
+        return {name: self.view(flat, name).copy() for name in NAMES}
+
+
+def glorot_flat(V, d, seed=0):
+    """Keras Dense defaults: glorot_uniform kernels, zero biases — as one flat float32 buffer."""
+    lay = Layout(V, d)
+    rng = np.random.default_rng(seed)
+    flat = np.zeros(lay.total, np.float32)
+    for li, (fi, fo) in enumerate(layer_shapes(V, d)):
+        o, shape = lay.entries[LAYERS[li] + '/kernel']
+        lim = np.sqrt(6.0 / (fi + fo))
+        flat[o:o + fi * fo] = rng.uniform(-lim, lim, fi * fo).astype(np.float32)
+    return flat

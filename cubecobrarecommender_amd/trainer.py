@@ -1,0 +1,340 @@
+"""Device-resident DAE training step — host orchestration of the libccrec_hip kernels.
+
+Replaces one Keras ``train_step`` of ``autoencoder.fit(generator)`` (src/ml/train.py:99-102):
+    F (generator.py:74-103) -> E (model.py:35-42) -> D1 + BCE and D2 + KL (model.py:117-125,
+    train.py:83-88) -> backward -> Adam (train.py:84).
+Everything stays in HBM: the dataset as a CSR of card ids, the noised batch as a CSR + bitmasks,
+activations in the GEMM operand dtype (bf16 or fp32), fp32 master weights + Adam moments in one
+flat buffer (cubecobrarecommender_amd.layout), a bf16 shadow of the weights for the MFMA path.
+torch is used only to own device memory and the stream; every computation is a HIP kernel.
+"""
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .layout import Layout
+
+
+@dataclass
+class TrainConfig:
+    V: int
+    d: int = 256
+    batch_size: int = 512          # per rank
+    reg: float = 0.0               # train.py:86 loss_weights=[1.0, reg]
+    noise: float = 0.2             # generator.py:13
+    noise_std: float = 0.1         # generator.py:14
+    lr: float = 1e-3               # Keras 'adam' defaults (train.py:84)
+    beta1: float = 0.9
+    beta2: float = 0.999
+    eps: float = 1e-7
+    dtype: str = 'bf16'            # GEMM operand dtype: 'bf16' (MFMA bf16) or 'fp32' (exact f32 MFMA)
+    seed: int = 0
+    rank: int = 0
+    world: int = 1
+
+
+class DeviceDataset:
+    """Cubes as a device CSR (sorted card ids), neg_sampler / CDF and optional M~ (fp32)."""
+
+    def __init__(self, cube_lists=None, num_cards=None, y_mtx=None, neg_sampler=None,
+                 device='cuda', csr=None):
+        if csr is not None:
+            indptr, indices = csr
+            indptr = np.asarray(indptr, np.int64)
+            indices = np.asarray(indices, np.int32)
+        else:
+            lens = np.array([len(c) for c in cube_lists], np.int64)
+            indptr = np.zeros(len(cube_lists) + 1, np.int64)
+            indptr[1:] = np.cumsum(lens)
+            indices = (np.concatenate([np.sort(np.asarray(c, np.int64)) for c in cube_lists])
+                       .astype(np.int32) if len(cube_lists) else np.zeros(0, np.int32))
+        self.V = int(num_cards)
+        self.C = len(indptr) - 1
+        self.max_n = int(np.max(np.diff(indptr))) if self.C else 0
+        self.cube_ptr = torch.from_numpy(indptr).to(device)
+        self.cube_idx = torch.from_numpy(indices).to(device)
+        if neg_sampler is None:
+            if y_mtx is None:
+                raise ValueError('need y_mtx (M~) or neg_sampler')
+            neg_sampler = _neg_sampler(y_mtx)
+        ns = np.asarray(neg_sampler, np.float64)
+        cdf = np.cumsum(ns)
+        cdf /= cdf[-1]
+        self.neg_sampler_host = ns
+        self.neg_sampler = torch.from_numpy(ns).to(device)
+        self.cdf = torch.from_numpy(cdf).to(device)
+        self.y_reg = None
+        if y_mtx is not None:
+            y = y_mtx if torch.is_tensor(y_mtx) else torch.from_numpy(np.asarray(y_mtx, np.float32))
+            self.y_reg = y.to(device=device, dtype=torch.float32).contiguous()
+
+
+def _neg_sampler(y_mtx):
+    """generator.py:30: neg_sampler = M~.sum(0) / M~.sum() (float64)."""
+    if torch.is_tensor(y_mtx):
+        y = y_mtx.to(torch.float64)
+        return (y.sum(0) / y.sum()).cpu().numpy()
+    y = np.asarray(y_mtx, np.float64)
+    return y.sum(0) / y.sum()
+
+
+class Trainer:
+    def __init__(self, cfg: TrainConfig, data: DeviceDataset, params_flat=None, device='cuda'):
+        L.lib()  # fail loudly before allocating anything
+        self.cfg, self.data = cfg, data
+        V, d, B = cfg.V, cfg.d, cfg.batch_size
+        assert data.V == V, 'dataset V mismatch'
+        assert d % 64 == 0 and (d // 64) & (d // 64 - 1) == 0, 'd must be 64 * 2^k'
+        self.dev = torch.device(device)
+        self.layout = Layout(V, d)
+        self.use_reg = cfg.reg > 0
+        if self.use_reg and data.y_reg is None:
+            raise ValueError('reg > 0 needs the M~ matrix on the device')
+        self.R = 2 * B if self.use_reg else B
+        self.dtype = L.CC_BF16 if cfg.dtype == 'bf16' else L.CC_F32
+        self.tdt = torch.bfloat16 if cfg.dtype == 'bf16' else torch.float32
+        P = self.layout.total
+        f32 = dict(device=self.dev, dtype=torch.float32)
+        self.params = torch.zeros(P, **f32)
+        if params_flat is not None:
+            self.params.copy_(torch.as_tensor(params_flat, dtype=torch.float32))
+        self.m = torch.zeros(P, **f32)
+        self.v = torch.zeros(P, **f32)
+        self.grads = torch.zeros(P, **f32)
+        self.shadow = torch.zeros(P, device=self.dev, dtype=torch.bfloat16) if self.dtype == L.CC_BF16 else None
+        self.refresh_shadow()
+        self.state = torch.zeros(2, device=self.dev, dtype=torch.int64)   # {step, batch_in_epoch}
+        self.x_cap = max(1, data.max_n + int(data.max_n * 0.8) + 1)
+        R, VW, XW = self.R, (V + 31) // 32, (self.R + 31) // 32
+        i32 = dict(device=self.dev, dtype=torch.int32)
+        self.x_cnt = torch.zeros(R, **i32)
+        self.x_idx = torch.zeros(R, self.x_cap, **i32)
+        self.y_bits = torch.zeros(B, VW, **i32)
+        self.xt_bits = torch.zeros(V, XW, **i32)
+        self.reg_idx = torch.zeros(B, **i32)
+        self.status = torch.zeros(1, **i32)
+        T = dict(device=self.dev, dtype=self.tdt)
+        self.H1 = torch.zeros(R, d, **T)
+        self.H2 = torch.zeros(R, 256, **T)
+        self.H3 = torch.zeros(R, 128, **T)
+        self.Zl = torch.zeros(R, 64, **T)
+        self.D1 = torch.zeros(R, 128, **T)
+        self.D2 = torch.zeros(R, 256, **T)
+        self.D3 = torch.zeros(R, d, **T)
+        self.dZout = torch.zeros(R, V, **T)       # rows [0,B): D1 dZ, rows [B,2B): D2 dZ
+        self.gD3 = torch.zeros(R, d, **T)
+        self.gD2 = torch.zeros(R, 256, **T)
+        self.gD1 = torch.zeros(R, 128, **T)
+        self.gZl = torch.zeros(R, 64, **T)
+        self.gH3 = torch.zeros(R, 128, **T)
+        self.gH2 = torch.zeros(R, 256, **T)
+        self.gPre1 = torch.zeros(R, d, **f32)
+        self.Z2 = torch.zeros(B, V, **f32) if self.use_reg else None
+        self.splits = max(1, min(16, V // 512))
+        self.split_buf = torch.zeros(self.splits, B, d, **f32)
+        tiles = ((B + 63) // 64) * ((V + 63) // 64)
+        self.bce_part = torch.zeros(tiles, device=self.dev, dtype=torch.float64)
+        self.kl_part = torch.zeros(B, device=self.dev, dtype=torch.float64)
+        self.loss_dev = torch.zeros(2, device=self.dev, dtype=torch.float64)
+        self.perm = None
+        self.batches_per_epoch = data.C // (B * cfg.world)
+        self.timing = False          # bench.py: HIP events around the main kernels
+        self.events = {}
+
+    def _tick(self, name):
+        """Record a HIP event on the current stream (bench timing); returns a closer."""
+        if not self.timing:
+            return lambda: None
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+
+        def close():
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.events.setdefault(name, []).append((e0, e1))
+        return close
+
+    def kernel_times_ms(self):
+        """Average duration (ms) per instrumented kernel over the recorded launches."""
+        torch.cuda.synchronize()
+        return {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in self.events.items()}
+
+    # ------------------------------------------------------------------ helpers
+    def w(self, name):
+        """Operand pointer of a weight: bf16 shadow or fp32 master."""
+        src = self.shadow if self.shadow is not None else self.params
+        return L.ptr(src[self.layout.offset(name):])
+
+    def pf(self, name):
+        return L.ptr(self.params[self.layout.offset(name):])
+
+    def gp(self, name):
+        return L.ptr(self.grads[self.layout.offset(name):])
+
+    def refresh_shadow(self):
+        if self.shadow is not None:
+            L.call('cc_to_bf16', L.ptr(self.params), L.ptr(self.shadow), self.layout.total, L.stream_ptr())
+
+    def set_epoch_permutation(self, perm):
+        """Upload one epoch's cube order (generator.py:63-72) and reset the batch counter."""
+        self.set_epoch_permutations(np.asarray(perm)[None, :])
+
+    def set_epoch_permutations(self, perms):
+        """Upload E epoch orders [E, C] (reset_indices / on_epoch_end, generator.py:63-72); epochs
+        cycle through them.  The batch counter lives on the device (state[1]) so the step needs no
+        host round trip; the host mirrors it to pick the epoch's permutation."""
+        p = torch.as_tensor(np.ascontiguousarray(perms, np.int32))
+        self.perms = p.to(self.dev)
+        self.epoch, self.host_batch = 0, 0
+        self.perm = self.perms[0]
+        self.state[1].zero_()
+
+    def _advance_epoch_if_needed(self):
+        if self.host_batch >= self.batches_per_epoch:
+            self.epoch += 1
+            self.perm = self.perms[self.epoch % self.perms.shape[0]]
+            self.state[1].zero_()          # on_epoch_end (generator.py:68-72)
+            self.host_batch = 0
+
+    def _gemm(self, M, N, K, A, lda, B, ldb, ta=0, tb=0, epi=L.CC_EPI_STORE, ldc=None, bias=None,
+              relu=0, C=None, Cf=None, H=None, y_bits=None, scale=0.0, partials=None, splits=1):
+        g = L.GemmArgs(dtype=self.dtype, ta=ta, tb=tb, epilogue=epi, M=M, N=N, K=K, lda=lda,
+                       ldb=ldb, ldc=ldc if ldc is not None else N, splits=splits, relu=relu,
+                       A=A, B=B, bias=bias, C=C, Cf=Cf, H=H, y_bits=y_bits, scale=scale,
+                       loss_partials=partials)
+        L.call('cc_gemm', L.C.byref(g), self._s)
+
+    def _dense_fwd(self, X, rows, K, N, name, out):
+        """out[rows] = relu(X[rows] @ W + b) (model.py Dense(relu))."""
+        r0, r1 = rows
+        self._gemm(r1 - r0, N, K, L.ptr(X[r0:]), K, self.w(name + '/kernel'), N,
+                   bias=self.pf(name + '/bias'), relu=1, C=L.ptr(out[r0:]))
+
+    def _dense_bwd(self, Xin, gOut, rows, K, N, name, gIn=None, gIn_f32=None, mask=None):
+        """dW = Xin^T gOut, db = colsum(gOut), gIn = (gOut W^T) * [mask > 0]."""
+        r0, r1 = rows
+        R = r1 - r0
+        self._gemm(K, N, R, L.ptr(Xin[r0:]), K, L.ptr(gOut[r0:]), N, ta=1, tb=0,
+                   Cf=self.gp(name + '/kernel'))
+        L.call('cc_colsum', self.dtype, L.ptr(gOut[r0:]), R, N, N, self.gp(name + '/bias'), self._s)
+        if gIn is not None or gIn_f32 is not None:
+            self._gemm(R, K, N, L.ptr(gOut[r0:]), N, self.w(name + '/kernel'), N, ta=0, tb=1,
+                       epi=L.CC_EPI_MASK, H=L.ptr(mask[r0:]),
+                       C=L.ptr(gIn[r0:]) if gIn is not None else None,
+                       Cf=L.ptr(gIn_f32[r0:]) if gIn_f32 is not None else None)
+
+    # ------------------------------------------------------------------ the step
+    def forward_backward(self, stream=None):
+        cfg, lay = self.cfg, self.layout
+        V, d, B, R = cfg.V, cfg.d, cfg.batch_size, self.R
+        self._s = L.stream_ptr(stream)
+        s = self._s
+        self._advance_epoch_if_needed()
+        # ---- F: noise + reg rows (generator.py:38-103)
+        self.xt_bits.zero_()
+        na = L.NoiseArgs(V=V, B=B, x_cap=self.x_cap, with_reg=int(self.use_reg), seed=cfg.seed,
+                         slot_base=cfg.rank * B, batch_stride=B * cfg.world, batch_offset=cfg.rank * B,
+                         noise_mean=cfg.noise, noise_std=cfg.noise_std,
+                         cube_ptr=self.data.cube_ptr.data_ptr(), cube_idx=self.data.cube_idx.data_ptr(),
+                         perm=self.perm.data_ptr(), cdf=self.data.cdf.data_ptr(),
+                         neg_sampler=self.data.neg_sampler.data_ptr(), state=self.state.data_ptr(),
+                         x_cnt=self.x_cnt.data_ptr(), x_idx=self.x_idx.data_ptr(),
+                         y_bits=self.y_bits.data_ptr(), xt_bits=self.xt_bits.data_ptr(),
+                         reg_idx=self.reg_idx.data_ptr(), status=self.status.data_ptr())
+        t = self._tick('cc_noise_fwd')
+        L.call('cc_noise_fwd', L.C.byref(na), s)
+        t()
+        # ---- E (model.py:35-42) on R rows: gather + 3 Dense
+        t = self._tick('cc_embed_gather_fwd')
+        L.call('cc_embed_gather_fwd', self.dtype, self.w('encoder/encoded_1/kernel'),
+               self.pf('encoder/encoded_1/bias'), V, d, R, L.ptr(self.x_cnt), L.ptr(self.x_idx),
+               self.x_cap, L.ptr(self.H1), s)
+        t()
+        self._dense_fwd(self.H1, (0, R), d, 256, 'encoder/encoded_2', self.H2)
+        self._dense_fwd(self.H2, (0, R), 256, 128, 'encoder/encoded_3', self.H3)
+        self._dense_fwd(self.H3, (0, R), 128, 64, 'encoder/bottleneck', self.Zl)
+        branches = [('decoder', (0, B))] + ([('decoder_for_reg', (B, 2 * B))] if self.use_reg else [])
+        for pre, rows in branches:
+            self._dense_fwd(self.Zl, rows, 64, 128, pre + '/decoded_1', self.D1)
+            self._dense_fwd(self.D1, rows, 128, 256, pre + '/decoded_2', self.D2)
+            self._dense_fwd(self.D2, rows, 256, d, pre + '/decoded_3', self.D3)
+        # ---- D1 output + sigmoid + BCE -> dZ (model.py:64,94; train.py:85)
+        t = self._tick('dec_bce_fwd')
+        self._gemm(B, V, d, L.ptr(self.D3), d, self.w('decoder/reconstruct/kernel'), V,
+                   epi=L.CC_EPI_BCE, bias=self.pf('decoder/reconstruct/bias'), C=L.ptr(self.dZout),
+                   y_bits=L.ptr(self.y_bits), scale=1.0 / (B * V), partials=L.ptr(self.bce_part))
+        t()
+        L.call('cc_reduce_loss', L.ptr(self.bce_part), self.bce_part.numel(), 1.0 / (B * V),
+               L.ptr(self.loss_dev), s)
+        # ---- D2 output + softmax + KL vs M~ rows (model.py:98; train.py:85)
+        if self.use_reg:
+            self._gemm(B, V, d, L.ptr(self.D3[B:]), d, self.w('decoder_for_reg/reconstruct/kernel'), V,
+                       bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2))
+            L.call('cc_dec_softmax_kl_fused', self.dtype, L.ptr(self.Z2), B, V, L.ptr(self.data.y_reg),
+                   L.ptr(self.reg_idx), float(cfg.reg), L.ptr(self.dZout[B:]), L.ptr(self.kl_part), s)
+            L.call('cc_reduce_loss', L.ptr(self.kl_part), B, 1.0 / B, L.ptr(self.loss_dev[1:]), s)
+        # ---- backward through the output layers and decoder towers
+        for pre, (r0, r1) in branches:
+            dz = self.dZout[r0:]
+            t = self._tick('dec_dW')
+            self._gemm(d, V, B, L.ptr(self.D3[r0:]), d, L.ptr(dz), V, ta=1, tb=0,
+                       Cf=self.gp(pre + '/reconstruct/kernel'))
+            t()
+            L.call('cc_colsum', self.dtype, L.ptr(dz), B, V, V, self.gp(pre + '/reconstruct/bias'), s)
+            t = self._tick('dec_dX')
+            self._gemm(B, d, V, L.ptr(dz), V, self.w(pre + '/reconstruct/kernel'), V, ta=0, tb=1,
+                       epi=L.CC_EPI_SPLITK, Cf=L.ptr(self.split_buf), splits=self.splits)
+            t()
+            L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), self.splits, B, d,
+                   L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, s)
+            rows = (r0, r1)
+            self._dense_bwd(self.D2, self.gD3, rows, 256, d, pre + '/decoded_3', gIn=self.gD2, mask=self.D2)
+            self._dense_bwd(self.D1, self.gD2, rows, 128, 256, pre + '/decoded_2', gIn=self.gD1, mask=self.D1)
+            self._dense_bwd(self.Zl, self.gD1, rows, 64, 128, pre + '/decoded_1', gIn=self.gZl, mask=self.Zl)
+        # ---- encoder backward (both branches' rows together)
+        self._dense_bwd(self.H3, self.gZl, (0, R), 128, 64, 'encoder/bottleneck', gIn=self.gH3, mask=self.H3)
+        self._dense_bwd(self.H2, self.gH3, (0, R), 256, 128, 'encoder/encoded_3', gIn=self.gH2, mask=self.H2)
+        self._dense_bwd(self.H1, self.gH2, (0, R), d, 256, 'encoder/encoded_2', gIn_f32=self.gPre1, mask=self.H1)
+        t = self._tick('cc_embed_scatter_bwd')
+        L.call('cc_embed_scatter_bwd', L.ptr(self.gPre1), V, d, R, L.ptr(self.xt_bits),
+               self.gp('encoder/encoded_1/kernel'), s)
+        t()
+        L.call('cc_colsum', L.CC_F32, L.ptr(self.gPre1), R, d, d, self.gp('encoder/encoded_1/bias'), s)
+
+    def apply(self, stream=None):
+        cfg = self.cfg
+        s = L.stream_ptr(stream)
+        n = self.layout.total if self.use_reg else self.layout.main_total
+        t = self._tick('cc_adam_dense')
+        L.call('cc_adam_dense', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v), L.ptr(self.grads),
+               L.ptr(self.shadow), n, L.ptr(self.state), cfg.lr, cfg.beta1, cfg.beta2, cfg.eps, s)
+        t()
+        L.call('cc_state_advance', L.ptr(self.state), s)
+        self.host_batch += 1
+
+    def step(self, stream=None):
+        self.forward_backward(stream)
+        self.apply(stream)
+
+    # ------------------------------------------------------------------ inspection (tests)
+    def losses(self):
+        l = self.loss_dev.cpu().numpy()
+        bce, kl = float(l[0]), float(l[1]) if self.use_reg else 0.0
+        return {'bce': bce, 'kl': kl, 'loss': bce + self.cfg.reg * kl}
+
+    def batch_lists(self):
+        """The last noised batch as host lists: (x lists (R rows), y lists (B rows), reg idx)."""
+        cnt = self.x_cnt.cpu().numpy()
+        idx = self.x_idx.cpu().numpy()
+        xs = [idx[r, :cnt[r]].copy() for r in range(self.R)]
+        yb = self.y_bits.cpu().numpy().view(np.uint32)
+        ys = []
+        for b in range(self.cfg.batch_size):
+            bits = np.unpackbits(yb[b].view(np.uint8), bitorder='little')[:self.cfg.V]
+            ys.append(np.nonzero(bits)[0])
+        return xs, ys, self.reg_idx.cpu().numpy().copy()
+
+    def params_dict(self):
+        return self.layout.unpack(self.params.cpu().numpy())

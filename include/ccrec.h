@@ -1,0 +1,198 @@
+/*
+ * ccrec.h — C ABI of libccrec_hip.so, the MI355X (gfx950) hot path of the CubeCobra
+ * denoising-autoencoder recommender.
+ *
+ * The reference has no FFI: its hot path sits behind Keras/TF Python objects
+ * (SURVEY.md §8(b)).  Each entry point below names the reference code it replaces.
+ * The Python host package (cubecobrarecommender_amd) binds these with ctypes; see
+ * INTEGRATION.md for the binding a maintainer would add on the reference side.
+ *
+ * Conventions
+ *   - All tensors are caller-owned DEVICE pointers (the library allocates nothing on
+ *     the device except what a cc_trainer/cc_recommender is handed in its workspace).
+ *   - Every call is stream-ordered on the given hipStream_t (passed as void*; NULL =
+ *     default stream) and does not synchronise.
+ *   - Return 0 on success, a negative CC_ERR_* code otherwise; no exceptions or aborts
+ *     cross the ABI.  cc_last_error_string() gives the calling thread's last message.
+ *   - Re-entrant: no global mutable state besides the thread-local error string.
+ *   - Deterministic: given (seed, step) every kernel produces bit-identical outputs
+ *     run to run (no float atomics on any output).
+ */
+#ifndef CCREC_H
+#define CCREC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CC_ABI_VERSION 1
+
+enum cc_status {
+  CC_OK = 0,
+  CC_ERR_ARG = -1,         /* invalid argument / shape */
+  CC_ERR_HIP = -2,         /* a HIP runtime call failed */
+  CC_ERR_UNSUPPORTED = -3, /* shape or dtype this build does not handle */
+  CC_ERR_CAPACITY = -4     /* a caller-provided buffer is too small */
+};
+
+enum cc_dtype { CC_F32 = 0, CC_BF16 = 1 };
+
+/* Number of tensors in the model (model.py: encoder 4 layers + 2 decoders x 4 layers, kernel+bias). */
+#define CC_NUM_TENSORS 24
+
+int cc_abi_version(void);
+const char *cc_last_error_string(void);
+
+/* ----------------------------------------------------------------------------------
+ * Parameter layout.  All weights live in ONE flat fp32 buffer (Adam m/v and the bf16
+ * shadow use the same offsets).  Tensor order = Keras creation order (model.py:27-33,
+ * 58-64, 92-98): encoder e1,e2,e3,bottleneck; decoder d1,d2,d3,reconstruct;
+ * decoder_for_reg d1,d2,d3,reconstruct; each as (kernel [in,out] row-major, bias [out]).
+ * offsets/sizes receive CC_NUM_TENSORS entries (elements); *total gets the flat size.
+ * *main_total = elements of the encoder + decoder (D1) part, which comes first.
+ * ---------------------------------------------------------------------------------- */
+int cc_param_layout(int32_t V, int32_t d, int64_t *offsets, int64_t *sizes,
+                    int64_t *total, int64_t *main_total);
+
+/* ----------------------------------------------------------------------------------
+ * F: noise + regulariser-row sampling.  Replaces DataGenerator.__getitem__ /
+ * generate_data (src/ml/generator.py:38-103) — the law is restated in
+ * oracle/noise_ref.py::philox_noise_batch (bit-exact).
+ * ---------------------------------------------------------------------------------- */
+typedef struct cc_noise_args {
+  int32_t V;             /* cards */
+  int32_t B;             /* cubes in this rank's batch */
+  int32_t x_cap;         /* per-row capacity of x_idx (>= max cube size * 1.8) */
+  int32_t with_reg;      /* also draw B reg rows (rows B..2B-1 of x) */
+  uint64_t seed;
+  uint32_t slot_base;    /* rank * B: decorrelates ranks */
+  int32_t batch_stride;  /* cubes consumed per global batch (B * world) */
+  int32_t batch_offset;  /* rank * B */
+  double noise_mean, noise_std;              /* generator.py:13-14 */
+  const int64_t *cube_ptr;                   /* [C+1] CSR of the dataset */
+  const int32_t *cube_idx;                   /* [nnz] sorted card ids per cube */
+  const int32_t *perm;                       /* [C] epoch permutation (generator.py:63-66) */
+  const double *cdf;                         /* [V] normalised cumsum of neg_sampler */
+  const double *neg_sampler;                 /* [V] generator.py:30 */
+  const int64_t *state;                      /* device {step, batch_in_epoch} */
+  int32_t *x_cnt;                            /* [R] R = B (+B with reg) */
+  int32_t *x_idx;                            /* [R, x_cap] sorted card ids of x */
+  uint32_t *y_bits;                          /* [B, ceil(V/32)] target bitmask */
+  uint32_t *xt_bits;                         /* [V, ceil(R/32)] transposed x bits (zeroed) or NULL */
+  int32_t *reg_idx;                          /* [B] or NULL */
+  int32_t *status;                           /* [1] device error flags (0 = ok) */
+} cc_noise_args;
+int cc_noise_fwd(const cc_noise_args *a, void *stream);
+
+/* ----------------------------------------------------------------------------------
+ * E1 forward: H[r] = ReLU(sum_{j in x_r} W1[j] + b1).  Replaces Dense(d)(x) on the 0/1
+ * cube (model.py:27,36): a coalesced row gather instead of a dense [R,V]x[V,d] GEMM.
+ * table is bf16 (CC_BF16) or fp32 (CC_F32) [V, d]; out is the same dtype [R, d].
+ * ---------------------------------------------------------------------------------- */
+int cc_embed_gather_fwd(int32_t dtype, const void *table, const float *bias, int32_t V,
+                        int32_t d, int32_t R, const int32_t *x_cnt, const int32_t *x_idx,
+                        int32_t x_cap, void *out, void *stream);
+
+/* ----------------------------------------------------------------------------------
+ * E1 backward: dW1[r] = sum_{b : r in x_b} dpre[b] (ascending b, deterministic), for every
+ * row r of W1 (dense, as TF's MatMul gradient is dense).  xt_bits [V, ceil(R/32)].
+ * Writes grad [V, d] fp32.  Replaces the MatMul gradient of model.py:27 inside fit.
+ * ---------------------------------------------------------------------------------- */
+int cc_embed_scatter_bwd(const float *dpre, int32_t V, int32_t d, int32_t R,
+                         const uint32_t *xt_bits, float *grad, void *stream);
+
+/* ----------------------------------------------------------------------------------
+ * Generic MFMA GEMM with fused epilogues — the Dense layers of the E/D towers and the
+ * decoder output layers (model.py:29-33, 58-64).  C[M,N] = op(A)[M,K] op(B)[K,N].
+ *   ta: A stored [K, M] (else [M, K]);  tb: B stored [N, K] (else [K, N]).  Row-major.
+ *   dtype: operand dtype (CC_BF16 -> v_mfma_f32_32x32x16_bf16, CC_F32 -> v_mfma_f32_32x32x2_f32);
+ *   accumulation always fp32.
+ * ---------------------------------------------------------------------------------- */
+enum cc_epilogue {
+  CC_EPI_STORE = 0,     /* out = act(acc + bias) -> C (dtype) and/or Cf (fp32) */
+  CC_EPI_BCE = 1,       /* D1 logits -> BCE loss partials + dZ (train.py:85) */
+  CC_EPI_MASK = 2,      /* out = acc * (H[m,n] > 0) -> C (dtype) and/or Cf: ReLU backward */
+  CC_EPI_SPLITK = 3     /* raw fp32 partial per K split -> Cf + split*M*N */
+};
+typedef struct cc_gemm_args {
+  int32_t dtype, ta, tb, epilogue;
+  int32_t M, N, K, lda, ldb, ldc;
+  int32_t splits;       /* K splits (CC_EPI_SPLITK only) */
+  int32_t relu;         /* CC_EPI_STORE */
+  const void *A, *B;
+  const float *bias;    /* [N] or NULL */
+  void *C;              /* dtype output or NULL */
+  float *Cf;            /* fp32 output or NULL */
+  const void *H;        /* CC_EPI_MASK: [M, ldc] dtype activations whose sign gates the gradient */
+  const uint32_t *y_bits; /* CC_EPI_BCE: [M, ceil(N/32)] targets */
+  float scale;          /* CC_EPI_BCE: 1/(B*V) */
+  double *loss_partials;  /* CC_EPI_BCE: [gridDim.x*gridDim.y] */
+} cc_gemm_args;
+int cc_gemm(const cc_gemm_args *g, void *stream);
+/* workspace bound for cc_gemm's loss partials: ceil(M/64)*ceil(N/64) doubles */
+int cc_gemm_grid(int32_t M, int32_t N, int32_t *tiles);
+
+/* Sum K-split partials (in split order) and apply the MASK/STORE epilogue. */
+int cc_splitk_reduce(int32_t dtype, const float *partials, int32_t splits, int32_t M, int32_t N,
+                     const void *H, void *C, float *Cf, void *stream);
+
+/* out[n] (+)= sum_r X[r, n] (fp32 accumulate, ascending r). db of every Dense layer. */
+int cc_colsum(int32_t dtype, const void *X, int32_t R, int32_t N, int32_t ld, float *out,
+              void *stream);
+
+/* ----------------------------------------------------------------------------------
+ * D1 output layer fused with sigmoid+BCE (model.py:64,94; train.py:85): logits
+ * z = H3 Wo + bo are never written; dZ = (sigmoid(z) - y)/(B*V) is.
+ * D2 softmax + KL (model.py:98; train.py:85): per reg row, row-softmax of z2, KL against the
+ * M~ row, dZ2 = reg/B * p (g - <p,g>) with the clip semantics of SURVEY §8(a) A9.
+ * ---------------------------------------------------------------------------------- */
+int cc_dec_bce_fused(int32_t dtype, const void *H3, const void *Wo, const float *bo,
+                     int32_t B, int32_t d, int32_t V, const uint32_t *y_bits, void *dZ,
+                     double *loss_partials, int32_t *n_partials, void *stream);
+int cc_dec_softmax_kl_fused(int32_t dtype, const float *Z2, int32_t B, int32_t V,
+                            const float *y_reg, const int32_t *reg_idx, float reg, void *dZ,
+                            double *kl_partials, void *stream);
+/* loss_out[0] = sum(partials[0:n]) * scale (fixed order, fp64) */
+int cc_reduce_loss(const double *partials, int32_t n, double scale, double *loss_out, void *stream);
+
+/* ----------------------------------------------------------------------------------
+ * Adam (train.py:84 'adam' -> TF ResourceApplyAdam): dense over [0, n) of the flat buffers,
+ * step t = state[0] + 1.  shadow (bf16) refreshed when non-NULL.
+ * ---------------------------------------------------------------------------------- */
+int cc_adam_dense(float *p, float *m, float *v, const float *g, uint16_t *shadow, int64_t n,
+                  const int64_t *state, float lr, float beta1, float beta2, float eps,
+                  void *stream);
+/* shadow[i] = bf16(x[i]) (round-to-nearest-even): refresh the bf16 weight shadow */
+int cc_to_bf16(const float *x, uint16_t *y, int64_t n, void *stream);
+/* state[0] += 1 (step), state[1] += 1 (batch in epoch) */
+int cc_state_advance(int64_t *state, void *stream);
+
+/* ----------------------------------------------------------------------------------
+ * Recommend forward (ml_recommend.py:78-87, ml_recommend_web.py:39-46), fp32, with the
+ * pinned summation order of oracle/infer_ref.py (bit-exact).  R cubes per call.
+ *   cc_infer_encode_fp32: zlat [R, 64]   (model.encoder(x))
+ *   cc_infer_decode_fp32: probs [R, V]   (model.decoder(z)) — sigmoid in fp64 -> fp32
+ * ---------------------------------------------------------------------------------- */
+int cc_infer_encode_fp32(const float *params, int32_t V, int32_t d, int32_t R,
+                         const int32_t *row_ptr, const int32_t *idx, float *zlat, void *stream);
+int cc_infer_decode_fp32(const float *params, int32_t V, int32_t d, int32_t R,
+                         const float *zlat, float *h3_ws, float *probs, void *stream);
+
+/* ----------------------------------------------------------------------------------
+ * Top-N (ml_recommend.py:87-108): rank all V probabilities descending, ties -> higher
+ * index first (= numpy argsort(kind='stable')[::-1]); additions = first max(amount,1)
+ * indices not in the cube; cut_vals[i] = probs[cube_idx[i]].
+ * ws: cc_topn_workspace_size(V) bytes.  order (optional, [V]) receives the full ranking.
+ * ---------------------------------------------------------------------------------- */
+size_t cc_topn_workspace_size(int32_t V);
+int cc_topn(const float *probs, int32_t V, const int32_t *cube_idx, int32_t n, int32_t amount,
+            int32_t *additions, int32_t *n_additions, float *add_vals, float *cut_vals,
+            int32_t *order, void *ws, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CCREC_H */

@@ -58,6 +58,8 @@ def bf16_round(a):
 def _rq(mode):
     if mode == 'bf16':
         return lambda a: bf16_round(a).astype(np.float64)
+    if mode == 'fp32':   # plain fp32 numpy (the CPU-baseline leg of bench.py)
+        return lambda a: np.asarray(a, np.float32)
     return lambda a: np.asarray(a, np.float64)
 
 
@@ -81,10 +83,11 @@ def train_forward_backward(P, x_lists, y_lists, V, d, reg=0.0, reg_idx=None, y_r
     """
     rq = _rq(mode)
     B = len(x_lists)
-    W = {k: (rq(v) if k.endswith('/kernel') else np.asarray(v, np.float64)) for k, v in P.items()}
+    bdt = np.float32 if mode == 'fp32' else np.float64
+    W = {k: (rq(v) if k.endswith('/kernel') else np.asarray(v, bdt)) for k, v in P.items()}
     use_reg = reg > 0
     R = 2 * B if use_reg else B
-    Xs = _csr(list(x_lists) + ([[int(i)] for i in reg_idx] if use_reg else []), V)
+    Xs = _csr(list(x_lists) + ([[int(i)] for i in reg_idx] if use_reg else []), V).astype(bdt)
     # E1: sparse gather-sum of the (bf16 shadow) rows + bias, ReLU
     pre1 = Xs @ W['encoder/encoded_1/kernel'] + W['encoder/encoded_1/bias']
     h1 = rq(_relu(pre1))
@@ -95,7 +98,7 @@ def train_forward_backward(P, x_lists, y_lists, V, d, reg=0.0, reg_idx=None, y_r
         acts.append(hs)
     zlat = hs
     losses = {}
-    grads = {k: np.zeros(v.shape, np.float64) for k, v in P.items()}
+    grads = {k: np.zeros(v.shape, bdt) for k, v in P.items()}
     dzlat = np.zeros_like(zlat)
 
     def decoder_branch(prefix, rows, out_grad_fn):
@@ -119,7 +122,7 @@ def train_forward_backward(P, x_lists, y_lists, V, d, reg=0.0, reg_idx=None, y_r
         dzlat[rows] += dh
         return loss
 
-    Y = _csr(y_lists, V).toarray()
+    Y = _csr(y_lists, V).toarray().astype(bdt)
 
     def bce(z):
         l = np.maximum(z, 0) - z * Y + np.log1p(np.exp(-np.abs(z)))

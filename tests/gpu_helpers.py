@@ -1,0 +1,30 @@
+"""Shared helpers for the GPU parity tests (synthetic data, oracle plumbing)."""
+import numpy as np
+
+from oracle import adjacency_ref, noise_ref
+
+
+def synthetic_lists(rng, C, V, sizes=(20, 40, 60), never_seen=3):
+    live = V - never_seen
+    pop = 1.0 / (1.0 + rng.permutation(live))
+    out = []
+    for _ in range(C):
+        n = int(rng.choice(sizes))
+        g = np.log(pop) + rng.gumbel(size=live)
+        out.append(np.sort(np.argsort(-g)[:n]))
+    return out
+
+
+def problem(seed, C, V, sizes):
+    rng = np.random.default_rng(seed)
+    lists = synthetic_lists(rng, C, V, sizes)
+    M = adjacency_ref.adjacency_from_lists(lists, V)
+    Mt = adjacency_ref.normalise(M)
+    ns = noise_ref.neg_sampler_of(Mt)
+    return lists, Mt, ns
+
+
+def rel_err(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))

@@ -1,0 +1,51 @@
+"""CPU tests: the C-ABI library loads, exports every symbol include/ccrec.h declares, and its
+parameter layout agrees with the Python mirror.  No compute calls (no GPU here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+
+from cubecobrarecommender_amd import _lib as L
+from cubecobrarecommender_amd.layout import Layout, NAMES
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    hdr = open(os.path.join(ROOT, 'include', 'ccrec.h')).read()
+    hdr = re.sub(r'/\*.*?\*/', '', hdr, flags=re.S)
+    return sorted(set(re.findall(r'\b(cc_[a-z0-9_]+)\s*\(', hdr)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = L.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 18
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in L.SIGNATURES, f'{s} not bound in _lib.SIGNATURES'
+    assert lib.cc_abi_version() == 1
+
+
+def test_param_layout_matches_python_mirror():
+    lib = L.lib()
+    for V, d in ((20884, 512), (22000, 256), (700, 64), (22000, 1024)):
+        off = (ctypes.c_int64 * 24)()
+        size = (ctypes.c_int64 * 24)()
+        tot, main = ctypes.c_int64(), ctypes.c_int64()
+        L.check(lib.cc_param_layout(V, d, off, size, ctypes.byref(tot), ctypes.byref(main)))
+        lay = Layout(V, d)
+        assert tot.value == lay.total and main.value == lay.main_total
+        for i, n in enumerate(NAMES):
+            assert off[i] == lay.offset(n) and size[i] == int(np.prod(lay.shape(n)))
+    # the reference checkpoint's parameter count: 32,638,440 at V=20,884, d=512
+    lay = Layout(20884, 512)
+    assert sum(int(np.prod(lay.shape(n))) for n in NAMES) == 32638440
+
+
+def test_error_reporting_without_gpu():
+    lib = L.lib()
+    rc = lib.cc_param_layout(0, 0, None, None, None, None)
+    assert rc == -1
+    assert b'null' in lib.cc_last_error_string() or b'positive' in lib.cc_last_error_string()

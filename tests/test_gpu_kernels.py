@@ -1,0 +1,221 @@
+"""GPU parity tests of the individual kernels against the CPU oracle (run on an MI355X)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from cubecobrarecommender_amd import _lib as L
+from oracle import noise_ref
+from tests.gpu_helpers import problem, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), 'GPU tests need a GPU'
+    L.lib()
+
+
+def _run_noise(lists, V, B, ns, seed, step, with_reg=True, slot_rank=0):
+    dev = 'cuda'
+    lens = np.array([len(c) for c in lists])
+    indptr = np.zeros(len(lists) + 1, np.int64)
+    indptr[1:] = np.cumsum(lens)
+    idx = np.concatenate(lists).astype(np.int32)
+    cdf = noise_ref.cdf_of(ns)
+    max_n = int(lens.max())
+    x_cap = max_n + int(max_n * 0.8) + 1
+    R = 2 * B if with_reg else B
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+    cube_ptr, cube_idx = t(indptr, torch.int64), t(idx, torch.int32)
+    perm = t(np.arange(len(lists), dtype=np.int32), torch.int32)
+    cdf_d, ns_d = t(cdf, torch.float64), t(ns, torch.float64)
+    state = t(np.array([step, 0], np.int64), torch.int64)
+    x_cnt = torch.zeros(R, device=dev, dtype=torch.int32)
+    x_idx = torch.zeros(R, x_cap, device=dev, dtype=torch.int32)
+    VW = (V + 31) // 32
+    y_bits = torch.zeros(B, VW, device=dev, dtype=torch.int32)
+    xt = torch.zeros(V, (R + 31) // 32, device=dev, dtype=torch.int32)
+    reg = torch.zeros(B, device=dev, dtype=torch.int32)
+    status = torch.zeros(1, device=dev, dtype=torch.int32)
+    a = L.NoiseArgs(V=V, B=B, x_cap=x_cap, with_reg=int(with_reg), seed=seed, slot_base=slot_rank * B,
+                    batch_stride=B, batch_offset=0, noise_mean=0.2, noise_std=0.1,
+                    cube_ptr=cube_ptr.data_ptr(), cube_idx=cube_idx.data_ptr(), perm=perm.data_ptr(),
+                    cdf=cdf_d.data_ptr(), neg_sampler=ns_d.data_ptr(), state=state.data_ptr(),
+                    x_cnt=x_cnt.data_ptr(), x_idx=x_idx.data_ptr(), y_bits=y_bits.data_ptr(),
+                    xt_bits=xt.data_ptr(), reg_idx=reg.data_ptr(), status=status.data_ptr())
+    L.call('cc_noise_fwd', ctypes.byref(a), L.stream_ptr())
+    torch.cuda.synchronize()
+    assert int(status.item()) == 0
+    cnt = x_cnt.cpu().numpy()
+    xi = x_idx.cpu().numpy()
+    xs = [xi[r, :cnt[r]] for r in range(R)]
+    yb = y_bits.cpu().numpy().view(np.uint32)
+    ys = [np.nonzero(np.unpackbits(yb[b].view(np.uint8), bitorder='little')[:V])[0] for b in range(B)]
+    xtb = xt.cpu().numpy().view(np.uint32)
+    return xs, ys, reg.cpu().numpy(), xtb, cdf
+
+
+@pytest.mark.parametrize('V,B,sizes,seed,step', [
+    (300, 16, (5, 30, 60), 1, 0),
+    (1500, 64, (40, 200, 400), 2, 7),
+    (22000, 64, (180, 360, 450, 540, 720), 20250301, 123456),
+])
+def test_noise_bit_exact_vs_oracle(V, B, sizes, seed, step):
+    lists, Mt, ns = problem(seed, B, V, sizes)
+    xs, ys, reg, xt, cdf = _run_noise(lists, V, B, ns, seed, step)
+    oxs, oys, oreg, ks = noise_ref.philox_noise_batch(lists, cdf, ns, seed, step, slot_base=0)
+    assert np.array_equal(reg, oreg)
+    for b in range(B):
+        assert np.array_equal(xs[b], oxs[b]), f'x row {b}'
+        assert np.array_equal(ys[b], oys[b]), f'y row {b}'
+        assert list(xs[B + b]) == [oreg[b]]
+    # transposed bitmask == x rows
+    R = 2 * B
+    for r in range(0, R, max(1, R // 7)):
+        col = (xt[:, r // 32] >> np.uint32(r % 32)) & 1
+        assert np.array_equal(np.nonzero(col)[0], xs[r])
+
+
+def test_noise_edge_cases():
+    V, B = 200, 8
+    rng = np.random.default_rng(5)
+    ns = rng.dirichlet(np.ones(V))
+    ns[190:] = 1e-6          # cube 2 holds ~all the mass: forces the exact fallback path
+    ns[20] = 0.0             # a zero-probability card is never added
+    ns /= ns.sum()
+    lists = [np.zeros(0, np.int64), np.array([3]), np.arange(0, 190),  # empty, 1 card, nearly all mass
+             np.array([0, 199]), np.arange(50, 60), np.arange(100, 150), np.array([7, 8]), np.arange(0, 200, 2)]
+    xs, ys, reg, xt, cdf = _run_noise(lists, V, B, ns, seed=9, step=1)
+    oxs, oys, oreg, _ = noise_ref.philox_noise_batch(lists, cdf, ns, 9, 1)
+    for b in range(B):
+        assert np.array_equal(xs[b], oxs[b]) and np.array_equal(ys[b], oys[b])
+    assert len(xs[0]) == 0 and len(ys[0]) == 0
+
+
+def _gemm_case(dtype, ta, tb, M, N, K, epi, rng):
+    tdt = torch.bfloat16 if dtype == L.CC_BF16 else torch.float32
+    A = torch.from_numpy(rng.standard_normal((K, M) if ta else (M, K)).astype(np.float32)).to('cuda', tdt)
+    Bm = torch.from_numpy(rng.standard_normal((N, K) if tb else (K, N)).astype(np.float32)).to('cuda', tdt)
+    Ad = A.double().cpu().numpy()
+    Bd = Bm.double().cpu().numpy()
+    ref = (Ad.T if ta else Ad) @ (Bd.T if tb else Bd)
+    bias = torch.from_numpy(rng.standard_normal(N).astype(np.float32)).cuda()
+    Cf = torch.zeros(M, N, device='cuda')
+    g = L.GemmArgs(dtype=dtype, ta=ta, tb=tb, epilogue=epi, M=M, N=N, K=K, lda=M if ta else K,
+                   ldb=K if tb else N, ldc=N, splits=1, relu=0, A=A.data_ptr(), B=Bm.data_ptr())
+    return A, Bm, ref, bias, Cf, g
+
+
+@pytest.mark.parametrize('dtype', [L.CC_F32, L.CC_BF16])
+@pytest.mark.parametrize('ta,tb', [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize('M,N,K', [(64, 64, 32), (100, 72, 50), (512, 256, 256), (37, 130, 1000)])
+def test_gemm_store_vs_fp64(dtype, ta, tb, M, N, K):
+    rng = np.random.default_rng(M * 7 + N + K)
+    A, Bm, ref, bias, Cf, g = _gemm_case(dtype, ta, tb, M, N, K, L.CC_EPI_STORE, rng)
+    g.bias = bias.data_ptr()
+    g.relu = 1
+    g.Cf = Cf.data_ptr()
+    L.call('cc_gemm', ctypes.byref(g), L.stream_ptr())
+    torch.cuda.synchronize()
+    want = np.maximum(ref + bias.double().cpu().numpy(), 0)
+    assert rel_err(Cf.cpu().numpy(), want) < 2e-6
+
+
+@pytest.mark.parametrize('dtype', [L.CC_F32, L.CC_BF16])
+def test_gemm_splitk_and_mask(dtype):
+    rng = np.random.default_rng(11)
+    M, N, K, S = 96, 80, 3000, 7
+    A, Bm, ref, bias, Cf, g = _gemm_case(dtype, 0, 1, M, N, K, L.CC_EPI_SPLITK, rng)
+    part = torch.zeros(S, M, N, device='cuda')
+    g.splits = S
+    g.Cf = part.data_ptr()
+    L.call('cc_gemm', ctypes.byref(g), L.stream_ptr())
+    tdt = torch.bfloat16 if dtype == L.CC_BF16 else torch.float32
+    H = torch.from_numpy(rng.standard_normal((M, N)).astype(np.float32)).to('cuda', tdt)
+    out = torch.zeros(M, N, device='cuda', dtype=tdt)
+    L.call('cc_splitk_reduce', dtype, L.ptr(part), S, M, N, L.ptr(H), L.ptr(out), L.ptr(Cf), L.stream_ptr())
+    torch.cuda.synchronize()
+    want = ref * (H.double().cpu().numpy() > 0)
+    assert rel_err(Cf.cpu().numpy(), want) < 2e-6
+    # MASK epilogue directly (no split)
+    g2 = L.GemmArgs(dtype=dtype, ta=0, tb=1, epilogue=L.CC_EPI_MASK, M=M, N=N, K=K, lda=K, ldb=K, ldc=N,
+                    splits=1, A=A.data_ptr(), B=Bm.data_ptr(), H=H.data_ptr(), Cf=Cf.data_ptr())
+    Cf.zero_()
+    L.call('cc_gemm', ctypes.byref(g2), L.stream_ptr())
+    torch.cuda.synchronize()
+    assert rel_err(Cf.cpu().numpy(), want) < 2e-6
+
+
+@pytest.mark.parametrize('dtype', [L.CC_F32, L.CC_BF16])
+def test_bce_epilogue(dtype):
+    rng = np.random.default_rng(3)
+    B, d, V = 70, 64, 333
+    tdt = torch.bfloat16 if dtype == L.CC_BF16 else torch.float32
+    H = torch.from_numpy(rng.standard_normal((B, d)).astype(np.float32)).to('cuda', tdt)
+    W = torch.from_numpy(rng.standard_normal((d, V)).astype(np.float32) * 0.3).to('cuda', tdt)
+    bo = torch.from_numpy(rng.standard_normal(V).astype(np.float32)).cuda()
+    Y = (rng.random((B, V)) < 0.1)
+    VW = (V + 31) // 32
+    yb = np.zeros((B, VW * 32), np.uint8)
+    yb[:, :V] = Y
+    ybits = torch.from_numpy(np.packbits(yb, axis=1, bitorder='little').view(np.int32).copy()).cuda()
+    dZ = torch.zeros(B, V, device='cuda', dtype=torch.float32)
+    tiles = ((B + 63) // 64) * ((V + 63) // 64)
+    part = torch.zeros(tiles, device='cuda', dtype=torch.float64)
+    loss = torch.zeros(1, device='cuda', dtype=torch.float64)
+    n = ctypes.c_int32()
+    L.call('cc_dec_bce_fused', dtype, L.ptr(H), L.ptr(W), L.ptr(bo), B, d, V, L.ptr(ybits), None,
+           L.ptr(part), ctypes.byref(n), L.stream_ptr())
+    L.call('cc_reduce_loss', L.ptr(part), n.value, 1.0 / (B * V), L.ptr(loss), L.stream_ptr())
+    g = L.GemmArgs(dtype=dtype, ta=0, tb=0, epilogue=L.CC_EPI_BCE, M=B, N=V, K=d, lda=d, ldb=V, ldc=V,
+                   A=H.data_ptr(), B=W.data_ptr(), bias=bo.data_ptr(), Cf=dZ.data_ptr(),
+                   y_bits=ybits.data_ptr(), scale=1.0 / (B * V), loss_partials=part.data_ptr())
+    L.call('cc_gemm', ctypes.byref(g), L.stream_ptr())
+    torch.cuda.synchronize()
+    z = H.double().cpu().numpy() @ W.double().cpu().numpy() + bo.double().cpu().numpy()
+    l = np.maximum(z, 0) - z * Y + np.log1p(np.exp(-np.abs(z)))
+    assert abs(loss.item() - l.mean()) / l.mean() < 1e-6
+    want = (1 / (1 + np.exp(-z)) - Y) / (B * V)
+    assert rel_err(dZ.cpu().numpy(), want) < 1e-5
+
+
+@pytest.mark.parametrize('dtype', [L.CC_F32, L.CC_BF16])
+@pytest.mark.parametrize('d', [64, 256, 512])
+def test_gather_and_scatter(dtype, d):
+    rng = np.random.default_rng(d)
+    V, R, cap = 3000, 50, 120
+    tdt = torch.bfloat16 if dtype == L.CC_BF16 else torch.float32
+    W = torch.from_numpy(rng.standard_normal((V, d)).astype(np.float32)).to('cuda', tdt)
+    b = torch.from_numpy(rng.standard_normal(d).astype(np.float32)).cuda()
+    lists = [np.sort(rng.choice(V, int(rng.integers(0, cap)), replace=False)) for _ in range(R)]
+    xi = np.zeros((R, cap), np.int32)
+    for r, l in enumerate(lists):
+        xi[r, :len(l)] = l
+    cnt = torch.from_numpy(np.array([len(l) for l in lists], np.int32)).cuda()
+    xid = torch.from_numpy(xi).cuda()
+    out = torch.zeros(R, d, device='cuda', dtype=tdt)
+    L.call('cc_embed_gather_fwd', dtype, L.ptr(W), L.ptr(b), V, d, R, L.ptr(cnt), L.ptr(xid), cap, L.ptr(out),
+           L.stream_ptr())
+    Wd = W.double().cpu().numpy()
+    want = np.stack([np.maximum(Wd[l].sum(0) + b.double().cpu().numpy(), 0) for l in lists])
+    torch.cuda.synchronize()
+    tol = 1e-2 if dtype == L.CC_BF16 else 1e-6
+    assert rel_err(out.double().cpu().numpy(), want) < tol
+    # backward: dW[r] = sum_{b: r in x_b} dpre[b]
+    dpre = torch.from_numpy(rng.standard_normal((R, d)).astype(np.float32)).cuda()
+    XW = (R + 31) // 32
+    xt = np.zeros((V, XW), np.uint32)
+    for r, l in enumerate(lists):
+        xt[l, r // 32] |= np.uint32(1 << (r % 32))
+    xtd = torch.from_numpy(xt.view(np.int32)).cuda()
+    grad = torch.full((V, d), 7.0, device='cuda')
+    L.call('cc_embed_scatter_bwd', L.ptr(dpre), V, d, R, L.ptr(xtd), L.ptr(grad), L.stream_ptr())
+    torch.cuda.synchronize()
+    gw = np.zeros((V, d))
+    dp = dpre.double().cpu().numpy()
+    for r, l in enumerate(lists):
+        gw[l] += dp[r]
+    assert rel_err(grad.cpu().numpy(), gw) < 1e-6

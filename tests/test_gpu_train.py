@@ -1,0 +1,92 @@
+"""GPU training-step parity vs the CPU oracle (oracle/model_ref.py): loss within 1e-4 relative at
+fp32; the bf16 MFMA path vs the oracle emulating the same bf16 operand rounding."""
+import numpy as np
+import pytest
+import torch
+
+from cubecobrarecommender_amd.layout import Layout
+from cubecobrarecommender_amd.trainer import DeviceDataset, TrainConfig, Trainer
+from oracle import model_ref, noise_ref
+from tests.gpu_helpers import problem, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(V, d, B, C, reg, dtype, seed=3, sizes=(20, 40, 80)):
+    lists, Mt, ns = problem(seed, C, V, sizes)
+    P = model_ref.init_params(V, d, seed=seed, bias_std=0.01)
+    lay = Layout(V, d)
+    cfg = TrainConfig(V=V, d=d, batch_size=B, reg=reg, dtype=dtype, seed=seed)
+    data = DeviceDataset(lists, V, y_mtx=Mt.astype(np.float32) if reg > 0 else None, neg_sampler=ns)
+    tr = Trainer(cfg, data, params_flat=lay.pack(P))
+    perm = np.random.default_rng(seed).permutation(C).astype(np.int32)
+    tr.set_epoch_permutation(perm)
+    return tr, lists, Mt, ns, P, perm
+
+
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
+@pytest.mark.parametrize('reg', [0.0, 0.1])
+@pytest.mark.parametrize('V,d,B', [(700, 64, 32), (2500, 128, 64)])
+def test_train_steps_match_oracle(dtype, reg, V, d, B):
+    C = 4 * B
+    tr, lists, Mt, ns, P, perm = _setup(V, d, B, C, reg, dtype)
+    cdf = noise_ref.cdf_of(ns)
+    Mo = {k: np.zeros_like(v) for k, v in P.items()}
+    Vo = {k: np.zeros_like(v) for k, v in P.items()}
+    mode = 'bf16' if dtype == 'bf16' else 'fp64'
+    loss_tol = 1e-4 if dtype == 'fp32' else 2e-4
+    for step in range(3):
+        tr.forward_backward()
+        torch.cuda.synchronize()
+        xs, ys, reg_idx = tr.batch_lists()
+        cubes = [lists[c] for c in perm[step * B:(step + 1) * B]]
+        oxs, oys, oreg, _ = noise_ref.philox_noise_batch(cubes, cdf, ns, tr.cfg.seed, step)
+        for b in range(B):   # F is bit-exact
+            assert np.array_equal(xs[b], oxs[b]) and np.array_equal(ys[b], oys[b])
+        if reg > 0:
+            assert np.array_equal(reg_idx, oreg)
+        losses, grads = model_ref.train_forward_backward(
+            P, oxs, oys, V, d, reg=reg, reg_idx=oreg, y_reg=Mt[oreg] if reg > 0 else None, mode=mode)
+        got = tr.losses()
+        assert abs(got['bce'] - losses['bce']) / losses['bce'] < loss_tol, (step, got, losses)
+        if reg > 0:
+            assert abs(got['kl'] - losses['kl']) / losses['kl'] < loss_tol, (step, got, losses)
+        gflat = tr.layout.unpack(tr.grads.cpu().numpy())
+        gtol = 1e-4 if dtype == 'fp32' else 2e-2
+        for k in grads:
+            if not reg and k.startswith('decoder_for_reg'):
+                continue
+            assert rel_err(gflat[k], grads[k]) < gtol, (step, k, rel_err(gflat[k], grads[k]))
+        tr.apply()
+        # advance the oracle with the oracle's own gradients (TF Adam in fp32)
+        G = {k: grads[k] for k in grads}
+        P, Mo, Vo = model_ref.adam_tf(P, Mo, Vo, G, t=step + 1)
+        torch.cuda.synchronize()
+        # keep the two trajectories on identical weights (Adam sign-noise on ~0 grads otherwise
+        # diverges the comparison, not the math): copy oracle params into the GPU trainer
+        got_p = tr.layout.unpack(tr.params.cpu().numpy())
+        for k in ('encoder/encoded_2/kernel', 'decoder/reconstruct/kernel'):
+            assert rel_err(got_p[k], P[k]) < (1e-3 if dtype == 'fp32' else 5e-2)
+        tr.params.copy_(torch.from_numpy(tr.layout.pack(P)))
+        tr.m.copy_(torch.from_numpy(tr.layout.pack(Mo)))
+        tr.v.copy_(torch.from_numpy(tr.layout.pack(Vo)))
+        tr.refresh_shadow()
+
+
+def test_adam_matches_tf_formula():
+    import ctypes
+    from cubecobrarecommender_amd import _lib as L
+    rng = np.random.default_rng(0)
+    n = 10007
+    p = rng.standard_normal(n).astype(np.float32)
+    g = rng.standard_normal(n).astype(np.float32)
+    m = np.zeros(n, np.float32)
+    v = np.zeros(n, np.float32)
+    dp, dm, dv, dg = (torch.from_numpy(a.copy()).cuda() for a in (p, m, v, g))
+    st = torch.tensor([4, 0], dtype=torch.int64, device='cuda')   # t = 5
+    L.call('cc_adam_dense', L.ptr(dp), L.ptr(dm), L.ptr(dv), L.ptr(dg), None, n, L.ptr(st),
+           1e-3, 0.9, 0.999, 1e-7, L.stream_ptr())
+    torch.cuda.synchronize()
+    P, Mo, Vo = model_ref.adam_tf({'a': p}, {'a': m}, {'a': v}, {'a': g}, t=5)
+    assert np.max(np.abs(dp.cpu().numpy() - P['a'])) < 1e-6
+    assert rel_err(dm.cpu().numpy(), Mo['a']) < 1e-6 and rel_err(dv.cpu().numpy(), Vo['a']) < 1e-6
