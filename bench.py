@@ -159,33 +159,45 @@ def main():
     tr.set_epoch_permutations(np.stack([rng.permutation(args.cubes) for _ in range(4)]))
     setup_s = time.perf_counter() - t_setup
 
-    def step():
-        tr.forward_backward()
+    n_grad = tr.layout.total if tr.use_reg else tr.layout.main_total
+
+    def step(graphed):
+        if graphed:
+            tr.graphs[0].replay()
+        else:
+            tr.forward_backward()
         if world > 1:
             import torch.distributed as dist
-            n = tr.layout.total if tr.use_reg else tr.layout.main_total
-            dist.all_reduce(tr.grads[:n], op=dist.ReduceOp.AVG)
-        tr.apply()
+            dist.all_reduce(tr.grads[:n_grad], op=dist.ReduceOp.AVG)
+        if graphed:
+            tr.graphs[1].replay()
+        else:
+            tr.apply()
+
+    # per-kernel durations (HIP events, eager launches of the same step) for the roofline
+    tr.timing = True
+    for _ in range(10):
+        step(False)
+    ktimes = tr.kernel_times_ms()
+    tr.timing = False
+    tr.capture()
 
     for _ in range(args.warmup):
-        step()
+        step(True)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
-    tr.timing = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(True)
     barrier(world)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    tr.timing = False
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    ktimes = tr.kernel_times_ms()
     losses = tr.losses()
     if rank != 0:
         if world > 1:

@@ -19,7 +19,8 @@ class NoiseArgs(C.Structure):
     _fields_ = [
         ('V', C.c_int32), ('B', C.c_int32), ('x_cap', C.c_int32), ('with_reg', C.c_int32),
         ('seed', C.c_uint64), ('slot_base', C.c_uint32), ('batch_stride', C.c_int32),
-        ('batch_offset', C.c_int32), ('noise_mean', C.c_double), ('noise_std', C.c_double),
+        ('batch_offset', C.c_int32), ('num_perms', C.c_int32), ('num_cubes', C.c_int32),
+        ('noise_mean', C.c_double), ('noise_std', C.c_double),
         ('cube_ptr', C.c_void_p), ('cube_idx', C.c_void_p), ('perm', C.c_void_p),
         ('cdf', C.c_void_p), ('neg_sampler', C.c_void_p), ('state', C.c_void_p),
         ('x_cnt', C.c_void_p), ('x_idx', C.c_void_p), ('y_bits', C.c_void_p),
@@ -57,7 +58,7 @@ SIGNATURES = {
     'cc_reduce_loss': (C.c_int, [_P, _I32, _F64, _P, _P]),
     'cc_adam_dense': (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _F32, _F32, _F32, _F32, _P]),
     'cc_to_bf16': (C.c_int, [_P, _P, _I64, _P]),
-    'cc_state_advance': (C.c_int, [_P, _P]),
+    'cc_state_advance': (C.c_int, [_P, _I64, _P]),
     'cc_infer_encode_fp32': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_infer_decode_fp32': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_topn_workspace_size': (_SZ, [_I32]),

@@ -120,9 +120,13 @@ __global__ __launch_bounds__(NT) void adam_kernel(float *__restrict__ p, float *
   }
 }
 
-__global__ void state_advance_kernel(int64_t *state) {
+__global__ void state_advance_kernel(int64_t *state, int64_t bpe) {
   state[0] += 1;
   state[1] += 1;
+  if (state[1] >= bpe) {
+    state[1] = 0;
+    state[2] += 1;
+  }
 }
 
 __global__ __launch_bounds__(NT) void to_bf16_kernel(const float *__restrict__ x,
@@ -165,9 +169,10 @@ extern "C" int cc_adam_dense(float *p, float *m, float *v, const float *g, uint1
   return CC_OK;
 }
 
-extern "C" int cc_state_advance(int64_t *state, void *stream) {
-  CC_REQUIRE(state, "cc_state_advance: null");
-  hipLaunchKernelGGL(state_advance_kernel, dim3(1), dim3(1), 0, as_stream(stream), state);
+extern "C" int cc_state_advance(int64_t *state, int64_t batches_per_epoch, void *stream) {
+  CC_REQUIRE(state && batches_per_epoch >= 1, "cc_state_advance: args");
+  hipLaunchKernelGGL(state_advance_kernel, dim3(1), dim3(1), 0, as_stream(stream), state,
+                     batches_per_epoch);
   CC_LAUNCH_CHECK("state_advance_kernel");
   return CC_OK;
 }

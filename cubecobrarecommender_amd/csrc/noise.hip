@@ -93,7 +93,9 @@ __global__ __launch_bounds__(NT) void noise_kernel(cc_noise_args a) {
   const int R = a.with_reg ? 2 * a.B : a.B;
   const int XW = (R + 31) >> 5;
 
-  const int32_t cube = a.perm[batch * (int64_t)a.batch_stride + a.batch_offset + b];
+  const int64_t epoch = a.state[2];
+  const int32_t *perm = a.perm + (epoch % a.num_perms) * (int64_t)a.num_cubes;
+  const int32_t cube = perm[batch * (int64_t)a.batch_stride + a.batch_offset + b];
   const int64_t beg = a.cube_ptr[cube];
   const int n = (int)(a.cube_ptr[cube + 1] - beg);
   const int32_t *__restrict__ inc = a.cube_idx + beg;
@@ -205,6 +207,7 @@ extern "C" int cc_noise_fwd(const cc_noise_args *a, void *stream) {
              "cc_noise_fwd: null input pointer");
   CC_REQUIRE(a->x_cnt && a->x_idx && a->y_bits && a->status, "cc_noise_fwd: null output pointer");
   CC_REQUIRE(!a->with_reg || a->reg_idx, "cc_noise_fwd: with_reg needs reg_idx");
+  CC_REQUIRE(a->num_perms >= 1 && a->num_cubes >= a->batch_stride, "cc_noise_fwd: num_perms/num_cubes");
   const int VW = (a->V + 31) / 32;
   const size_t lds = (size_t)(4 * VW + NT + 1 + a->x_cap) * 4;
   CC_REQUIRE(lds <= 150 * 1024, "cc_noise_fwd: V / x_cap too large for LDS");

@@ -105,7 +105,7 @@ class Trainer:
         self.grads = torch.zeros(P, **f32)
         self.shadow = torch.zeros(P, device=self.dev, dtype=torch.bfloat16) if self.dtype == L.CC_BF16 else None
         self.refresh_shadow()
-        self.state = torch.zeros(2, device=self.dev, dtype=torch.int64)   # {step, batch_in_epoch}
+        self.state = torch.zeros(4, device=self.dev, dtype=torch.int64)   # {step, batch, epoch, 0}
         self.x_cap = max(1, data.max_n + int(data.max_n * 0.8) + 1)
         R, VW, XW = self.R, (V + 31) // 32, (self.R + 31) // 32
         i32 = dict(device=self.dev, dtype=torch.int32)
@@ -138,8 +138,9 @@ class Trainer:
         self.bce_part = torch.zeros(tiles, device=self.dev, dtype=torch.float64)
         self.kl_part = torch.zeros(B, device=self.dev, dtype=torch.float64)
         self.loss_dev = torch.zeros(2, device=self.dev, dtype=torch.float64)
-        self.perm = None
-        self.batches_per_epoch = data.C // (B * cfg.world)
+        self.perms = None
+        self.batches_per_epoch = max(1, data.C // (B * cfg.world))   # generator.py:36 (__len__)
+        self.graphs = None
         self.timing = False          # bench.py: HIP events around the main kernels
         self.events = {}
 
@@ -183,20 +184,14 @@ class Trainer:
 
     def set_epoch_permutations(self, perms):
         """Upload E epoch orders [E, C] (reset_indices / on_epoch_end, generator.py:63-72); epochs
-        cycle through them.  The batch counter lives on the device (state[1]) so the step needs no
-        host round trip; the host mirrors it to pick the epoch's permutation."""
+        cycle through them.  Batch and epoch counters live on the device (state[1], state[2]) and
+        are advanced by cc_state_advance, so a step has no host round trip and replays as a graph."""
         p = torch.as_tensor(np.ascontiguousarray(perms, np.int32))
-        self.perms = p.to(self.dev)
-        self.epoch, self.host_batch = 0, 0
-        self.perm = self.perms[0]
-        self.state[1].zero_()
-
-    def _advance_epoch_if_needed(self):
-        if self.host_batch >= self.batches_per_epoch:
-            self.epoch += 1
-            self.perm = self.perms[self.epoch % self.perms.shape[0]]
-            self.state[1].zero_()          # on_epoch_end (generator.py:68-72)
-            self.host_batch = 0
+        assert p.shape[1] == self.data.C
+        if self.perms is None or self.perms.shape != p.shape:
+            self.perms = torch.empty(p.shape, device=self.dev, dtype=torch.int32)
+        self.perms.copy_(p)
+        self.state[1:3].zero_()
 
     def _gemm(self, M, N, K, A, lda, B, ldb, ta=0, tb=0, epi=L.CC_EPI_STORE, ldc=None, bias=None,
               relu=0, C=None, Cf=None, H=None, y_bits=None, scale=0.0, partials=None, splits=1):
@@ -231,14 +226,14 @@ class Trainer:
         V, d, B, R = cfg.V, cfg.d, cfg.batch_size, self.R
         self._s = L.stream_ptr(stream)
         s = self._s
-        self._advance_epoch_if_needed()
         # ---- F: noise + reg rows (generator.py:38-103)
         self.xt_bits.zero_()
         na = L.NoiseArgs(V=V, B=B, x_cap=self.x_cap, with_reg=int(self.use_reg), seed=cfg.seed,
                          slot_base=cfg.rank * B, batch_stride=B * cfg.world, batch_offset=cfg.rank * B,
                          noise_mean=cfg.noise, noise_std=cfg.noise_std,
                          cube_ptr=self.data.cube_ptr.data_ptr(), cube_idx=self.data.cube_idx.data_ptr(),
-                         perm=self.perm.data_ptr(), cdf=self.data.cdf.data_ptr(),
+                         num_perms=self.perms.shape[0], num_cubes=self.data.C,
+                         perm=self.perms.data_ptr(), cdf=self.data.cdf.data_ptr(),
                          neg_sampler=self.data.neg_sampler.data_ptr(), state=self.state.data_ptr(),
                          x_cnt=self.x_cnt.data_ptr(), x_idx=self.x_idx.data_ptr(),
                          y_bits=self.y_bits.data_ptr(), xt_bits=self.xt_bits.data_ptr(),
@@ -311,12 +306,38 @@ class Trainer:
         L.call('cc_adam_dense', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v), L.ptr(self.grads),
                L.ptr(self.shadow), n, L.ptr(self.state), cfg.lr, cfg.beta1, cfg.beta2, cfg.eps, s)
         t()
-        L.call('cc_state_advance', L.ptr(self.state), s)
-        self.host_batch += 1
+        L.call('cc_state_advance', L.ptr(self.state), self.batches_per_epoch, s)
 
     def step(self, stream=None):
+        if self.graphs is not None:
+            self.graphs[0].replay()
+            self.graphs[1].replay()
+            return
         self.forward_backward(stream)
         self.apply(stream)
+
+    def capture(self):
+        """Capture forward_backward and apply as two hipGraphs (torch.cuda.CUDAGraph over our
+        own kernel launches): one graph launch per phase instead of ~40 host launches.  Every
+        buffer is preallocated and the step/epoch counters are device-resident, so replays are
+        exact repeats of the eager step (the data-parallel all-reduce runs between the two)."""
+        timing, self.timing = self.timing, False
+        s = torch.cuda.Stream(device=self.dev)
+        s.wait_stream(torch.cuda.current_stream())
+        saved = self.state.clone()
+        with torch.cuda.stream(s):           # warm-up launch outside capture (lazy module loads)
+            self.forward_backward()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g_fb, g_ap = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_fb):
+            self.forward_backward()
+        with torch.cuda.graph(g_ap):
+            self.apply()
+        torch.cuda.synchronize()
+        self.state.copy_(saved)
+        self.graphs = (g_fb, g_ap)
+        self.timing = timing
 
     # ------------------------------------------------------------------ inspection (tests)
     def losses(self):

@@ -71,13 +71,15 @@ typedef struct cc_noise_args {
   uint32_t slot_base;    /* rank * B: decorrelates ranks */
   int32_t batch_stride;  /* cubes consumed per global batch (B * world) */
   int32_t batch_offset;  /* rank * B */
+  int32_t num_perms;     /* epochs cycle through num_perms permutations */
+  int32_t num_cubes;     /* C */
   double noise_mean, noise_std;              /* generator.py:13-14 */
   const int64_t *cube_ptr;                   /* [C+1] CSR of the dataset */
   const int32_t *cube_idx;                   /* [nnz] sorted card ids per cube */
-  const int32_t *perm;                       /* [C] epoch permutation (generator.py:63-66) */
+  const int32_t *perm;                       /* [num_perms, C] epoch permutations (generator.py:63-66) */
   const double *cdf;                         /* [V] normalised cumsum of neg_sampler */
   const double *neg_sampler;                 /* [V] generator.py:30 */
-  const int64_t *state;                      /* device {step, batch_in_epoch} */
+  const int64_t *state;                      /* device {step, batch_in_epoch, epoch, 0} */
   int32_t *x_cnt;                            /* [R] R = B (+B with reg) */
   int32_t *x_idx;                            /* [R, x_cap] sorted card ids of x */
   uint32_t *y_bits;                          /* [B, ceil(V/32)] target bitmask */
@@ -167,8 +169,10 @@ int cc_adam_dense(float *p, float *m, float *v, const float *g, uint16_t *shadow
                   void *stream);
 /* shadow[i] = bf16(x[i]) (round-to-nearest-even): refresh the bf16 weight shadow */
 int cc_to_bf16(const float *x, uint16_t *y, int64_t n, void *stream);
-/* state[0] += 1 (step), state[1] += 1 (batch in epoch) */
-int cc_state_advance(int64_t *state, void *stream);
+/* Device step state {step, batch_in_epoch, epoch, 0}: step += 1, batch += 1, and on reaching
+ * batches_per_epoch: batch = 0, epoch += 1 (on_epoch_end, generator.py:68-72).  Keeping the
+ * counters on the device makes a whole training step replayable as one hipGraph. */
+int cc_state_advance(int64_t *state, int64_t batches_per_epoch, void *stream);
 
 /* ----------------------------------------------------------------------------------
  * Recommend forward (ml_recommend.py:78-87, ml_recommend_web.py:39-46), fp32, with the

@@ -32,7 +32,7 @@ def _run_noise(lists, V, B, ns, seed, step, with_reg=True, slot_rank=0):
     cube_ptr, cube_idx = t(indptr, torch.int64), t(idx, torch.int32)
     perm = t(np.arange(len(lists), dtype=np.int32), torch.int32)
     cdf_d, ns_d = t(cdf, torch.float64), t(ns, torch.float64)
-    state = t(np.array([step, 0], np.int64), torch.int64)
+    state = t(np.array([step, 0, 0, 0], np.int64), torch.int64)
     x_cnt = torch.zeros(R, device=dev, dtype=torch.int32)
     x_idx = torch.zeros(R, x_cap, device=dev, dtype=torch.int32)
     VW = (V + 31) // 32
@@ -41,7 +41,7 @@ def _run_noise(lists, V, B, ns, seed, step, with_reg=True, slot_rank=0):
     reg = torch.zeros(B, device=dev, dtype=torch.int32)
     status = torch.zeros(1, device=dev, dtype=torch.int32)
     a = L.NoiseArgs(V=V, B=B, x_cap=x_cap, with_reg=int(with_reg), seed=seed, slot_base=slot_rank * B,
-                    batch_stride=B, batch_offset=0, noise_mean=0.2, noise_std=0.1,
+                    batch_stride=B, batch_offset=0, num_perms=1, num_cubes=len(lists), noise_mean=0.2, noise_std=0.1,
                     cube_ptr=cube_ptr.data_ptr(), cube_idx=cube_idx.data_ptr(), perm=perm.data_ptr(),
                     cdf=cdf_d.data_ptr(), neg_sampler=ns_d.data_ptr(), state=state.data_ptr(),
                     x_cnt=x_cnt.data_ptr(), x_idx=x_idx.data_ptr(), y_bits=y_bits.data_ptr(),

@@ -83,10 +83,34 @@ def test_adam_matches_tf_formula():
     m = np.zeros(n, np.float32)
     v = np.zeros(n, np.float32)
     dp, dm, dv, dg = (torch.from_numpy(a.copy()).cuda() for a in (p, m, v, g))
-    st = torch.tensor([4, 0], dtype=torch.int64, device='cuda')   # t = 5
+    st = torch.tensor([4, 0, 0, 0], dtype=torch.int64, device='cuda')   # t = 5
     L.call('cc_adam_dense', L.ptr(dp), L.ptr(dm), L.ptr(dv), L.ptr(dg), None, n, L.ptr(st),
            1e-3, 0.9, 0.999, 1e-7, L.stream_ptr())
     torch.cuda.synchronize()
     P, Mo, Vo = model_ref.adam_tf({'a': p}, {'a': m}, {'a': v}, {'a': g}, t=5)
     assert np.max(np.abs(dp.cpu().numpy() - P['a'])) < 1e-6
     assert rel_err(dm.cpu().numpy(), Mo['a']) < 1e-6 and rel_err(dv.cpu().numpy(), Vo['a']) < 1e-6
+
+
+def test_graph_replay_matches_eager_and_epochs_roll_over():
+    V, d, B, C = 700, 64, 32, 128          # 4 batches per epoch
+    tr_e, lists, Mt, ns, P, _ = _setup(V, d, B, C, 0.1, 'bf16')
+    tr_g, *_ = _setup(V, d, B, C, 0.1, 'bf16')
+    rng = np.random.default_rng(1)
+    perms = np.stack([rng.permutation(C) for _ in range(2)]).astype(np.int32)
+    tr_e.set_epoch_permutations(perms)
+    tr_g.set_epoch_permutations(perms)
+    tr_g.capture()
+    cdf = noise_ref.cdf_of(ns)
+    for step in range(6):
+        tr_e.step()
+        tr_g.step()
+        torch.cuda.synchronize()
+        assert tr_e.losses() == tr_g.losses()
+        xs, ys, _ = tr_g.batch_lists()
+        ep, bi = divmod(step, 4)
+        cubes = [lists[c] for c in perms[ep % 2][bi * B:(bi + 1) * B]]
+        oxs, oys, _, _ = noise_ref.philox_noise_batch(cubes, cdf, ns, tr_g.cfg.seed, step)
+        assert all(np.array_equal(a, b) for a, b in zip(xs[:B], oxs))
+    assert torch.equal(tr_e.params, tr_g.params)
+    assert tr_g.state.cpu().tolist()[:3] == [6, 2, 1]
