@@ -22,7 +22,8 @@ class NoiseArgs(C.Structure):
         ('batch_offset', C.c_int32), ('num_perms', C.c_int32), ('num_cubes', C.c_int32),
         ('noise_mean', C.c_double), ('noise_std', C.c_double),
         ('cube_ptr', C.c_void_p), ('cube_idx', C.c_void_p), ('perm', C.c_void_p),
-        ('cdf', C.c_void_p), ('neg_sampler', C.c_void_p), ('state', C.c_void_p),
+        ('cdf', C.c_void_p), ('neg_sampler', C.c_void_p), ('guide', C.c_void_p),
+        ('guide_log2', C.c_int32), ('state', C.c_void_p),
         ('x_cnt', C.c_void_p), ('x_idx', C.c_void_p), ('y_bits', C.c_void_p),
         ('xt_bits', C.c_void_p), ('reg_idx', C.c_void_p), ('status', C.c_void_p),
     ]
@@ -35,7 +36,7 @@ class GemmArgs(C.Structure):
         ('ldb', C.c_int32), ('ldc', C.c_int32), ('splits', C.c_int32), ('relu', C.c_int32),
         ('A', C.c_void_p), ('B', C.c_void_p), ('bias', C.c_void_p), ('C', C.c_void_p),
         ('Cf', C.c_void_p), ('H', C.c_void_p), ('y_bits', C.c_void_p), ('scale', C.c_float),
-        ('loss_partials', C.c_void_p),
+        ('loss_partials', C.c_void_p), ('colsum', C.c_void_p),
     ]
 
 
@@ -48,10 +49,10 @@ SIGNATURES = {
     'cc_param_layout': (C.c_int, [_I32, _I32, _P, _P, _P, _P]),
     'cc_noise_fwd': (C.c_int, [C.POINTER(NoiseArgs), _P]),
     'cc_embed_gather_fwd': (C.c_int, [_I32, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P]),
-    'cc_embed_scatter_bwd': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P]),
+    'cc_embed_scatter_bwd': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_gemm': (C.c_int, [C.POINTER(GemmArgs), _P]),
     'cc_gemm_grid': (C.c_int, [_I32, _I32, _P]),
-    'cc_splitk_reduce': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
+    'cc_splitk_reduce': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     'cc_colsum': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P]),
     'cc_dec_bce_fused': (C.c_int, [_I32, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     'cc_dec_softmax_kl_fused': (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _F32, _P, _P, _P]),

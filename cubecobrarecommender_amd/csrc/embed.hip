@@ -14,79 +14,174 @@
 
 namespace {
 
+// EPL consecutive elements of one table row -> fp32, with the widest aligned vector loads.
+template <typename T, int EPL>
+__device__ __forceinline__ void load_row(const T *__restrict__ p, float (&v)[EPL]) {
+  constexpr int BYTES = EPL * (int)sizeof(T);
+  if constexpr (BYTES % 16 == 0) {
+#pragma unroll
+    for (int q = 0; q < BYTES / 16; ++q) {
+      const uint4 u = reinterpret_cast<const uint4 *>(p)[q];
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if constexpr (sizeof(T) == 2) {
+          v[q * 8 + 2 * e] = __uint_as_float(w[e] << 16);
+          v[q * 8 + 2 * e + 1] = __uint_as_float(w[e] & 0xFFFF0000u);
+        } else {
+          v[q * 4 + e] = __uint_as_float(w[e]);
+        }
+      }
+    }
+  } else if constexpr (BYTES == 8) {
+    const uint2 u = *reinterpret_cast<const uint2 *>(p);
+    if constexpr (sizeof(T) == 2) {
+      v[0] = __uint_as_float(u.x << 16);
+      v[1] = __uint_as_float(u.x & 0xFFFF0000u);
+      v[2] = __uint_as_float(u.y << 16);
+      v[3] = __uint_as_float(u.y & 0xFFFF0000u);
+    } else {
+      v[0] = __uint_as_float(u.x);
+      v[1] = __uint_as_float(u.y);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) v[e] = DT<T>::ld(p + e);
+  }
+}
+
+// Forward: 4 waves per cube row, wave w sums the w-th quarter of the row's (sorted) card list
+// with U row loads in flight per lane; the four partials are added in wave order (deterministic).
+constexpr int GW = 4;
+
 template <typename T, int EPL>
 __global__ __launch_bounds__(256) void gather_kernel(const T *__restrict__ table,
                                                      const float *__restrict__ bias, int d, int R,
                                                      const int32_t *__restrict__ x_cnt,
                                                      const int32_t *__restrict__ x_idx, int x_cap,
                                                      T *__restrict__ out) {
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (wave >= R) return;
+  constexpr int U = 8;
+  __shared__ float part[GW - 1][64 * EPL];
+  const int row = blockIdx.x;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int c0 = lane * EPL;
   float acc[EPL];
 #pragma unroll
   for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
-  const int n = x_cnt[wave];
-  const int32_t *__restrict__ lst = x_idx + (int64_t)wave * x_cap;
-  int i = 0;
-  for (; i + 4 <= n; i += 4) {
-    const int j0 = lst[i], j1 = lst[i + 1], j2 = lst[i + 2], j3 = lst[i + 3];
-    const T *r0 = table + (int64_t)j0 * d + c0;
-    const T *r1 = table + (int64_t)j1 * d + c0;
-    const T *r2 = table + (int64_t)j2 * d + c0;
-    const T *r3 = table + (int64_t)j3 * d + c0;
-    float v0[EPL], v1[EPL], v2[EPL], v3[EPL];
+  const int n = x_cnt[row];
+  const int q = (n + GW - 1) / GW;
+  const int i0 = min(n, w * q), i1 = min(n, i0 + q);
+  const int32_t *__restrict__ lst = x_idx + (int64_t)row * x_cap;
+  int i = i0;
+  for (; i + U <= i1; i += U) {
+    int j[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) j[u] = lst[i + u];
+    float v[U][EPL];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load_row<T, EPL>(table + (int64_t)j[u] * d + c0, v[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) acc[e] += v[u][e];
+  }
+  for (; i < i1; ++i) {
+    float v[EPL];
+    load_row<T, EPL>(table + (int64_t)lst[i] * d + c0, v);
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) acc[e] += v[e];
+  }
+  if (w > 0) {
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) part[w - 1][c0 + e] = acc[e];
+  }
+  __syncthreads();
+  if (w == 0) {
+    T *o = out + (int64_t)row * d + c0;
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
-      v0[e] = DT<T>::ld(r0 + e);
-      v1[e] = DT<T>::ld(r1 + e);
-      v2[e] = DT<T>::ld(r2 + e);
-      v3[e] = DT<T>::ld(r3 + e);
+      float v = acc[e];
+#pragma unroll
+      for (int p = 0; p < GW - 1; ++p) v += part[p][c0 + e];
+      v += bias[c0 + e];
+      DT<T>::st(o + e, v > 0.f ? v : 0.f);
     }
-#pragma unroll
-    for (int e = 0; e < EPL; ++e) acc[e] = (((acc[e] + v0[e]) + v1[e]) + v2[e]) + v3[e];
-  }
-  for (; i < n; ++i) {
-    const T *r0 = table + (int64_t)lst[i] * d + c0;
-#pragma unroll
-    for (int e = 0; e < EPL; ++e) acc[e] += DT<T>::ld(r0 + e);
-  }
-  T *o = out + (int64_t)wave * d + c0;
-#pragma unroll
-  for (int e = 0; e < EPL; ++e) {
-    const float v = acc[e] + bias[c0 + e];
-    DT<T>::st(o + e, v > 0.f ? v : 0.f);
   }
 }
 
+// Backward: 4 waves per W1 row (row V = the bias when bias_grad is given); wave w walks the w-th
+// quarter of the row's bit words, collecting up to U set bits before issuing their dPre loads
+// together (heavy Zipf rows have a set bit for nearly every batch row).  Partials added in wave order.
 template <int EPL>
 __global__ __launch_bounds__(256) void scatter_bwd_kernel(const float *__restrict__ dpre, int V,
                                                           int d, int R,
                                                           const uint32_t *__restrict__ xt,
-                                                          float *__restrict__ grad) {
-  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (row >= V) return;
+                                                          float *__restrict__ grad,
+                                                          float *__restrict__ bias_grad) {
+  constexpr int U = 8;
+  __shared__ float part[GW - 1][64 * EPL];
+  const int row = blockIdx.x;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int XW = (R + 31) >> 5;
   const int c0 = lane * EPL;
   float acc[EPL];
 #pragma unroll
   for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
   const uint32_t *bits = xt + (int64_t)row * XW;
-  for (int w = 0; w < XW; ++w) {
-    uint32_t m = bits[w];
+  const int q = (XW + GW - 1) / GW;
+  const int w0 = min(XW, w * q), w1 = min(XW, w0 + q);
+  int pend[U];
+  int np = 0;
+  for (int wd = w0; wd < w1; ++wd) {
+    uint32_t m = row == V ? (wd == XW - 1 && (R & 31) ? (1u << (R & 31)) - 1u : 0xFFFFFFFFu) : bits[wd];
     while (m) {
-      const int b = (w << 5) + __ffs(m) - 1;
-      m &= m - 1;
-      const float *src = dpre + (int64_t)b * d + c0;
+      // static-indexed shift register (a runtime-indexed array would live in scratch)
 #pragma unroll
-      for (int e = 0; e < EPL; ++e) acc[e] += src[e];
+      for (int u = U - 1; u > 0; --u) pend[u] = pend[u - 1];
+      pend[0] = (wd << 5) + __ffs(m) - 1;
+      m &= m - 1;
+      if (++np == U) {
+        float v[U][EPL];
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_row<float, EPL>(dpre + (int64_t)pend[u] * d + c0, v[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int e = 0; e < EPL; ++e) acc[e] += v[u][e];
+        np = 0;
+      }
     }
   }
-  float *g = grad + (int64_t)row * d + c0;
 #pragma unroll
-  for (int e = 0; e < EPL; ++e) g[e] = acc[e];
+  for (int u = 0; u < U; ++u) {
+    if (u < np) {
+      float v[EPL];
+      load_row<float, EPL>(dpre + (int64_t)pend[u] * d + c0, v);
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) acc[e] += v[e];
+    }
+  }
+  if (w > 0) {
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) part[w - 1][c0 + e] = acc[e];
+  }
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int e = 0; e < EPL; ++e)
+#pragma unroll
+      for (int p = 0; p < GW - 1; ++p) acc[e] += part[p][c0 + e];
+    float *g = row == V ? bias_grad + c0 : grad + (int64_t)row * d + c0;
+    if constexpr (EPL % 4 == 0) {
+#pragma unroll
+      for (int qq = 0; qq < EPL / 4; ++qq)
+        reinterpret_cast<float4 *>(g)[qq] =
+            make_float4(acc[4 * qq], acc[4 * qq + 1], acc[4 * qq + 2], acc[4 * qq + 3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) g[e] = acc[e];
+    }
+  }
 }
 
 }  // namespace
@@ -98,7 +193,7 @@ extern "C" int cc_embed_gather_fwd(int32_t dtype, const void *table, const float
   CC_REQUIRE(d % 64 == 0 && d >= 64 && d <= 1024, "cc_embed_gather_fwd: d must be 64..1024, %64");
   CC_REQUIRE(V > 0 && R >= 0 && x_cap > 0, "cc_embed_gather_fwd: bad sizes");
   if (R == 0) return CC_OK;
-  const dim3 grid((unsigned)cdiv((int64_t)R * 64, 256)), block(256);
+  const dim3 grid((unsigned)R), block(256);
   const int epl = d / 64;
   hipStream_t s = as_stream(stream);
 #define GATHER_CASE(E)                                                                          \
@@ -125,17 +220,18 @@ extern "C" int cc_embed_gather_fwd(int32_t dtype, const void *table, const float
 }
 
 extern "C" int cc_embed_scatter_bwd(const float *dpre, int32_t V, int32_t d, int32_t R,
-                                    const uint32_t *xt_bits, float *grad, void *stream) {
+                                    const uint32_t *xt_bits, float *grad, float *bias_grad,
+                                    void *stream) {
   CC_REQUIRE(dpre && xt_bits && grad, "cc_embed_scatter_bwd: null pointer");
   CC_REQUIRE(d % 64 == 0 && d >= 64 && d <= 1024, "cc_embed_scatter_bwd: d must be 64..1024, %64");
-  const dim3 grid((unsigned)cdiv((int64_t)V * 64, 256)), block(256);
+  const dim3 grid((unsigned)(bias_grad ? V + 1 : V)), block(256);
   hipStream_t s = as_stream(stream);
   switch (d / 64) {
-    case 1: hipLaunchKernelGGL((scatter_bwd_kernel<1>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad); break;
-    case 2: hipLaunchKernelGGL((scatter_bwd_kernel<2>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad); break;
-    case 4: hipLaunchKernelGGL((scatter_bwd_kernel<4>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad); break;
-    case 8: hipLaunchKernelGGL((scatter_bwd_kernel<8>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad); break;
-    case 16: hipLaunchKernelGGL((scatter_bwd_kernel<16>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad); break;
+    case 1: hipLaunchKernelGGL((scatter_bwd_kernel<1>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
+    case 2: hipLaunchKernelGGL((scatter_bwd_kernel<2>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
+    case 4: hipLaunchKernelGGL((scatter_bwd_kernel<4>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
+    case 8: hipLaunchKernelGGL((scatter_bwd_kernel<8>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
+    case 16: hipLaunchKernelGGL((scatter_bwd_kernel<16>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
     default: return cc::fail(CC_ERR_UNSUPPORTED, "cc_embed_scatter_bwd: d/64 must be a power of two");
   }
   CC_LAUNCH_CHECK("scatter_bwd_kernel");

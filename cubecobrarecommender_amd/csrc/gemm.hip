@@ -26,6 +26,7 @@ struct GemmParams {
   const uint32_t *y_bits;
   float scale;
   double *loss_partials;
+  float *colsum;
 };
 
 template <typename T> struct Mma;
@@ -46,45 +47,74 @@ template <> struct Mma<float> {
   }
 };
 
-// Stage a ROWS x BK tile of the logical operand X[row][k] (row in [r0, r0+ROWS), k in [k0, kend))
-// into LDS image S[row][k].  KCONTIG: storage X[row*ld + k]; else storage X[k*ld + row].
-template <typename T, bool KCONTIG, int ROWS, int LDK>
-__device__ __forceinline__ void stage(T (*S)[LDK], const T *__restrict__ X, int ld, int r0,
-                                      int rlim, int k0, int kend, bool vec_ok) {
-  constexpr int VW = 16 / sizeof(T);
-  using V16 = uint4;
-  if constexpr (KCONTIG) {
-    constexpr int PER_ROW = BK / VW;
-    for (int v = threadIdx.x; v < ROWS * PER_ROW; v += NT) {
-      const int r = v / PER_ROW, kv = (v % PER_ROW) * VW;
-      const int gr = r0 + r, gk = k0 + kv;
-      if (vec_ok && gr < rlim && gk + VW <= kend) {
-        *reinterpret_cast<V16 *>(&S[r][kv]) =
-            *reinterpret_cast<const V16 *>(X + (int64_t)gr * ld + gk);
+// Register-staged tile loader for a ROWS x BK tile of the logical operand X[row][k]
+// (row in [r0, r0+ROWS), k in [k0, kend)) into the K-contiguous LDS image S[row][k].
+//   KCONTIG: storage X[row*ld + k] (16-B vectors along k, stored to LDS as one b128);
+//   else   : storage X[k*ld + row] (16-B vectors along row, transposed into LDS element-wise).
+// load() issues the global loads into registers; store() writes them to LDS — split so the next
+// tile's loads are in flight while the current tile's MFMAs run.
+template <typename T, bool KCONTIG, int ROWS>
+struct Stager {
+  static constexpr int VW = 16 / sizeof(T);
+  static constexpr int NVEC = ROWS * BK / VW;
+  static constexpr int NV = (NVEC + NT - 1) / NT;
+  uint4 r[NV];
+
+  __device__ __forceinline__ void load(const T *__restrict__ X, int ld, int r0, int rlim, int k0,
+                                       int kend, bool vec_ok) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = threadIdx.x + i * NT;
+      if (v >= NVEC) break;
+      int gr, gk;
+      bool full;
+      const T *src;
+      if constexpr (KCONTIG) {
+        constexpr int PER = BK / VW;
+        gr = r0 + v / PER;
+        gk = k0 + (v % PER) * VW;
+        full = vec_ok && gr < rlim && gk + VW <= kend;
+        src = X + (int64_t)gr * ld + gk;
       } else {
-#pragma unroll
-        for (int e = 0; e < VW; ++e)
-          S[r][kv + e] = (gr < rlim && gk + e < kend) ? X[(int64_t)gr * ld + gk + e] : T(0);
+        constexpr int PER = ROWS / VW;
+        gk = k0 + v / PER;
+        gr = r0 + (v % PER) * VW;
+        full = vec_ok && gk < kend && gr + VW <= rlim;
+        src = X + (int64_t)gk * ld + gr;
       }
-    }
-  } else {
-    constexpr int PER_K = ROWS / VW;
-    for (int v = threadIdx.x; v < BK * PER_K; v += NT) {
-      const int k = v / PER_K, rv = (v % PER_K) * VW;
-      const int gk = k0 + k, gr = r0 + rv;
-      T tmp[VW];
-      if (vec_ok && gk < kend && gr + VW <= rlim) {
-        *reinterpret_cast<V16 *>(tmp) = *reinterpret_cast<const V16 *>(X + (int64_t)gk * ld + gr);
+      if (full) {
+        r[i] = *reinterpret_cast<const uint4 *>(src);
       } else {
+        T tmp[VW];
 #pragma unroll
-        for (int e = 0; e < VW; ++e)
-          tmp[e] = (gk < kend && gr + e < rlim) ? X[(int64_t)gk * ld + gr + e] : T(0);
+        for (int e = 0; e < VW; ++e) {
+          const bool ok = KCONTIG ? (gr < rlim && gk + e < kend) : (gk < kend && gr + e < rlim);
+          tmp[e] = ok ? src[e * (KCONTIG ? 1 : 1)] : T(0);
+        }
+        r[i] = *reinterpret_cast<const uint4 *>(tmp);
       }
-#pragma unroll
-      for (int e = 0; e < VW; ++e) S[rv + e][k] = tmp[e];
     }
   }
-}
+
+  template <int LDK>
+  __device__ __forceinline__ void store(T (*S)[LDK]) const {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = threadIdx.x + i * NT;
+      if (v >= NVEC) break;
+      if constexpr (KCONTIG) {
+        constexpr int PER = BK / VW;
+        *reinterpret_cast<uint4 *>(&S[v / PER][(v % PER) * VW]) = r[i];
+      } else {
+        constexpr int PER = ROWS / VW;
+        const int k = v / PER, rv = (v % PER) * VW;
+        const T *tmp = reinterpret_cast<const T *>(&r[i]);
+#pragma unroll
+        for (int e = 0; e < VW; ++e) S[rv + e][k] = tmp[e];
+      }
+    }
+  }
+};
 
 __device__ __forceinline__ double block_sum_double(double v, double *red) {
 #pragma unroll
@@ -124,13 +154,35 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams p) {
   const T *a_row = &As[wm * 32 + (lane & 31)][0];
   const T *b_row = &Bs[wn * 32 + (lane & 31)][0];
   const int half = lane >> 5;
+  // fused bias gradient: the first row of blocks sums the staged op(B) tile over k (ascending)
+  const bool do_cs = p.colsum != nullptr && blockIdx.y == 0 && threadIdx.x < BN;
+  float cs = 0.f;
+  Stager<T, !TA, BM> sa;
+  Stager<T, TB, BN> sb;
+  if (kbeg < kend) {
+    sa.load(A, p.lda, bm, p.M, kbeg, kend, p.vec_a);
+    sb.load(B, p.ldb, bn, p.N, kbeg, kend, p.vec_b);
+  }
   for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    stage<T, !TA, BM, LDK>(As, A, p.lda, bm, p.M, k0, kend, p.vec_a);
-    stage<T, TB, BN, LDK>(Bs, B, p.ldb, bn, p.N, k0, kend, p.vec_b);
+    sa.store(As);
+    sb.store(Bs);
     __syncthreads();
+    if (k0 + BK < kend) {  // next tile's global loads fly while this tile's MFMAs run
+      sa.load(A, p.lda, bm, p.M, k0 + BK, kend, p.vec_a);
+      sb.load(B, p.ldb, bn, p.N, k0 + BK, kend, p.vec_b);
+    }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += Mma<T>::KM) Mma<T>::step(a_row, b_row, kk, half, acc);
+    if (do_cs) {
+#pragma unroll 8
+      for (int k = 0; k < BK; ++k) cs += DT<T>::ld(&Bs[threadIdx.x][k]);
+    }
     __syncthreads();
+  }
+  if (do_cs && bn + (int)threadIdx.x < p.N) {
+    // split-K: one partial row per split (reduced in cc_splitk_reduce)
+    const int64_t zo = EPI == CC_EPI_SPLITK ? (int64_t)blockIdx.z * p.N : 0;
+    p.colsum[zo + bn + threadIdx.x] = cs;
   }
 
   // ------------------------------------------------------------------ epilogues
@@ -209,9 +261,15 @@ template <typename T>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restrict__ part,
                                                             int splits, int M, int N,
                                                             const T *__restrict__ H, T *C,
-                                                            float *Cf) {
+                                                            float *Cf, const float *cs_part,
+                                                            float *cs_out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t MN = (int64_t)M * N;
+  if (cs_out && i < N) {
+    float c = 0.f;
+    for (int z = 0; z < splits; ++z) c += cs_part[(int64_t)z * N + i];
+    cs_out[i] = c;
+  }
   if (i >= MN) return;
   float s = 0.f;
   for (int z = 0; z < splits; ++z) s += part[z * MN + i];
@@ -265,22 +323,25 @@ extern "C" int cc_gemm(const cc_gemm_args *g, void *stream) {
   p.vec_b = (g->ldb % vw == 0) && ((uintptr_t)g->B % 16 == 0);
   p.A = g->A; p.B = g->B; p.bias = g->bias; p.C = g->C; p.Cf = g->Cf; p.H = g->H;
   p.y_bits = g->y_bits; p.scale = g->scale; p.loss_partials = g->loss_partials;
+  p.colsum = g->colsum;
+
   hipStream_t s = as_stream(stream);
   return g->dtype == CC_BF16 ? launch_epi<bf16_t>(g, p, s) : launch_epi<float>(g, p, s);
 }
 
 extern "C" int cc_splitk_reduce(int32_t dtype, const float *partials, int32_t splits, int32_t M,
-                                int32_t N, const void *H, void *C, float *Cf, void *stream) {
+                                int32_t N, const void *H, void *C, float *Cf,
+                                const float *colsum_partials, float *colsum_out, void *stream) {
   CC_REQUIRE(partials && splits >= 1, "cc_splitk_reduce: args");
   const int64_t MN = (int64_t)M * N;
   if (MN == 0) return CC_OK;
   const dim3 grid((unsigned)cdiv(MN, 256)), block(256);
   if (dtype == CC_BF16)
     hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, grid, block, 0, as_stream(stream), partials,
-                       splits, M, N, (const bf16_t *)H, (bf16_t *)C, Cf);
+                       splits, M, N, (const bf16_t *)H, (bf16_t *)C, Cf, colsum_partials, colsum_out);
   else
     hipLaunchKernelGGL(splitk_reduce_kernel<float>, grid, block, 0, as_stream(stream), partials,
-                       splits, M, N, (const float *)H, (float *)C, Cf);
+                       splits, M, N, (const float *)H, (float *)C, Cf, colsum_partials, colsum_out);
   CC_LAUNCH_CHECK("splitk_reduce_kernel");
   return CC_OK;
 }

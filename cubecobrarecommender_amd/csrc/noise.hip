@@ -30,9 +30,17 @@ __device__ __forceinline__ u32x4 rng(uint64_t seed, uint32_t step, uint32_t slot
                        (uint32_t)(seed >> 32));
 }
 
-// first index j with cdf[j] > u  (numpy searchsorted side='right')
-__device__ __forceinline__ int search_right(const double *__restrict__ cdf, int V, double u) {
+// first index j with cdf[j] > u  (numpy searchsorted side='right').  With a guide table the search
+// is restricted to [guide[g], guide[g+1]], g = floor(u 2^G) — the same answer (cdf is monotone and
+// g/2^G <= u < (g+1)/2^G), in ~log2(V/2^G) instead of log2(V) dependent loads.
+__device__ __forceinline__ int search_right(const double *__restrict__ cdf, int V, double u,
+                                            const int32_t *__restrict__ guide, int glog2) {
   int lo = 0, hi = V;
+  if (guide) {
+    const int g = (int)(u * (double)(1 << glog2));
+    lo = guide[g];
+    hi = min(guide[g + 1], V - 1) + 1;
+  }
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
     if (cdf[mid] <= u)
@@ -139,7 +147,7 @@ __global__ __launch_bounds__(NT) void noise_kernel(cc_noise_args a) {
     int pick = -1;
     for (int t = 0; t < ADD_MAX_TRIES; ++t) {
       const u32x4 o = rng(a.seed, step, slot, KIND_ADD, (uint32_t)i, (uint32_t)t);
-      const int j = search_right(a.cdf, a.V, u53(o.x, o.y));
+      const int j = search_right(a.cdf, a.V, u53(o.x, o.y), a.guide, a.guide_log2);
       if (!bit_of(cube_bits, j)) {
         pick = j;
         break;
@@ -189,7 +197,7 @@ __global__ __launch_bounds__(NT) void noise_kernel(cc_noise_args a) {
   // regulariser row for this slot (generator.py:47-51): one draw ∝ neg_sampler
   if (a.with_reg && tid == 0) {
     const u32x4 o = rng(a.seed, step, slot, KIND_REG, 0, 0);
-    const int j = search_right(a.cdf, a.V, u53(o.x, o.y));
+    const int j = search_right(a.cdf, a.V, u53(o.x, o.y), a.guide, a.guide_log2);
     a.reg_idx[b] = j;
     const int r = a.B + b;
     a.x_idx[(int64_t)r * a.x_cap] = j;

@@ -65,6 +65,9 @@ class DeviceDataset:
         self.neg_sampler_host = ns
         self.neg_sampler = torch.from_numpy(ns).to(device)
         self.cdf = torch.from_numpy(cdf).to(device)
+        self.guide_log2 = 12   # CDF search guide table: 4097 entries
+        guide = np.searchsorted(cdf, np.arange((1 << self.guide_log2) + 1) / float(1 << self.guide_log2), side='right')
+        self.guide = torch.from_numpy(guide.astype(np.int32)).to(device)
         self.y_reg = None
         if y_mtx is not None:
             y = y_mtx if torch.is_tensor(y_mtx) else torch.from_numpy(np.asarray(y_mtx, np.float32))
@@ -132,8 +135,10 @@ class Trainer:
         self.gH2 = torch.zeros(R, 256, **T)
         self.gPre1 = torch.zeros(R, d, **f32)
         self.Z2 = torch.zeros(B, V, **f32) if self.use_reg else None
-        self.splits = max(1, min(16, V // 512))
-        self.split_buf = torch.zeros(self.splits, B, d, **f32)
+        self.splits = max(1, min(16, V // 512))            # decoder dX: K = V
+        self.tsplits = max(1, min(8, B // 128))             # tower dW: K = rows (B or 2B)
+        self.split_buf = torch.zeros(max(self.splits * B * d, 2 * self.tsplits * max(d, 256) * 256), **f32)
+        self.cs_buf = torch.zeros(2 * self.tsplits * max(d, 256), **f32)
         tiles = ((B + 63) // 64) * ((V + 63) // 64)
         self.bce_part = torch.zeros(tiles, device=self.dev, dtype=torch.float64)
         self.kl_part = torch.zeros(B, device=self.dev, dtype=torch.float64)
@@ -194,11 +199,12 @@ class Trainer:
         self.state[1:3].zero_()
 
     def _gemm(self, M, N, K, A, lda, B, ldb, ta=0, tb=0, epi=L.CC_EPI_STORE, ldc=None, bias=None,
-              relu=0, C=None, Cf=None, H=None, y_bits=None, scale=0.0, partials=None, splits=1):
+              relu=0, C=None, Cf=None, H=None, y_bits=None, scale=0.0, partials=None, splits=1,
+              colsum=None):
         g = L.GemmArgs(dtype=self.dtype, ta=ta, tb=tb, epilogue=epi, M=M, N=N, K=K, lda=lda,
                        ldb=ldb, ldc=ldc if ldc is not None else N, splits=splits, relu=relu,
                        A=A, B=B, bias=bias, C=C, Cf=Cf, H=H, y_bits=y_bits, scale=scale,
-                       loss_partials=partials)
+                       loss_partials=partials, colsum=colsum)
         L.call('cc_gemm', L.C.byref(g), self._s)
 
     def _dense_fwd(self, X, rows, K, N, name, out):
@@ -208,12 +214,18 @@ class Trainer:
                    bias=self.pf(name + '/bias'), relu=1, C=L.ptr(out[r0:]))
 
     def _dense_bwd(self, Xin, gOut, rows, K, N, name, gIn=None, gIn_f32=None, mask=None):
-        """dW = Xin^T gOut, db = colsum(gOut), gIn = (gOut W^T) * [mask > 0]."""
+        """dW = Xin^T gOut with db = colsum(gOut) fused; gIn = (gOut W^T) * [mask > 0]."""
         r0, r1 = rows
         R = r1 - r0
-        self._gemm(K, N, R, L.ptr(Xin[r0:]), K, L.ptr(gOut[r0:]), N, ta=1, tb=0,
-                   Cf=self.gp(name + '/kernel'))
-        L.call('cc_colsum', self.dtype, L.ptr(gOut[r0:]), R, N, N, self.gp(name + '/bias'), self._s)
+        S = self.tsplits * (R // self.cfg.batch_size)
+        if S > 1:   # K = R rows: split-K for parallelism, partials summed in split order
+            self._gemm(K, N, R, L.ptr(Xin[r0:]), K, L.ptr(gOut[r0:]), N, ta=1, tb=0,
+                       epi=L.CC_EPI_SPLITK, Cf=L.ptr(self.split_buf), splits=S, colsum=L.ptr(self.cs_buf))
+            L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), S, K, N, None, None,
+                   self.gp(name + '/kernel'), L.ptr(self.cs_buf), self.gp(name + '/bias'), self._s)
+        else:
+            self._gemm(K, N, R, L.ptr(Xin[r0:]), K, L.ptr(gOut[r0:]), N, ta=1, tb=0,
+                       Cf=self.gp(name + '/kernel'), colsum=self.gp(name + '/bias'))
         if gIn is not None or gIn_f32 is not None:
             self._gemm(R, K, N, L.ptr(gOut[r0:]), N, self.w(name + '/kernel'), N, ta=0, tb=1,
                        epi=L.CC_EPI_MASK, H=L.ptr(mask[r0:]),
@@ -234,7 +246,8 @@ class Trainer:
                          cube_ptr=self.data.cube_ptr.data_ptr(), cube_idx=self.data.cube_idx.data_ptr(),
                          num_perms=self.perms.shape[0], num_cubes=self.data.C,
                          perm=self.perms.data_ptr(), cdf=self.data.cdf.data_ptr(),
-                         neg_sampler=self.data.neg_sampler.data_ptr(), state=self.state.data_ptr(),
+                         neg_sampler=self.data.neg_sampler.data_ptr(), guide=self.data.guide.data_ptr(),
+                         guide_log2=self.data.guide_log2, state=self.state.data_ptr(),
                          x_cnt=self.x_cnt.data_ptr(), x_idx=self.x_idx.data_ptr(),
                          y_bits=self.y_bits.data_ptr(), xt_bits=self.xt_bits.data_ptr(),
                          reg_idx=self.reg_idx.data_ptr(), status=self.status.data_ptr())
@@ -275,15 +288,14 @@ class Trainer:
             dz = self.dZout[r0:]
             t = self._tick('dec_dW')
             self._gemm(d, V, B, L.ptr(self.D3[r0:]), d, L.ptr(dz), V, ta=1, tb=0,
-                       Cf=self.gp(pre + '/reconstruct/kernel'))
+                       Cf=self.gp(pre + '/reconstruct/kernel'), colsum=self.gp(pre + '/reconstruct/bias'))
             t()
-            L.call('cc_colsum', self.dtype, L.ptr(dz), B, V, V, self.gp(pre + '/reconstruct/bias'), s)
             t = self._tick('dec_dX')
             self._gemm(B, d, V, L.ptr(dz), V, self.w(pre + '/reconstruct/kernel'), V, ta=0, tb=1,
                        epi=L.CC_EPI_SPLITK, Cf=L.ptr(self.split_buf), splits=self.splits)
             t()
             L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), self.splits, B, d,
-                   L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, s)
+                   L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
             rows = (r0, r1)
             self._dense_bwd(self.D2, self.gD3, rows, 256, d, pre + '/decoded_3', gIn=self.gD2, mask=self.D2)
             self._dense_bwd(self.D1, self.gD2, rows, 128, 256, pre + '/decoded_2', gIn=self.gD1, mask=self.D1)
@@ -294,9 +306,8 @@ class Trainer:
         self._dense_bwd(self.H1, self.gH2, (0, R), d, 256, 'encoder/encoded_2', gIn_f32=self.gPre1, mask=self.H1)
         t = self._tick('cc_embed_scatter_bwd')
         L.call('cc_embed_scatter_bwd', L.ptr(self.gPre1), V, d, R, L.ptr(self.xt_bits),
-               self.gp('encoder/encoded_1/kernel'), s)
+               self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
         t()
-        L.call('cc_colsum', L.CC_F32, L.ptr(self.gPre1), R, d, d, self.gp('encoder/encoded_1/bias'), s)
 
     def apply(self, stream=None):
         cfg = self.cfg

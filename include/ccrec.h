@@ -79,6 +79,9 @@ typedef struct cc_noise_args {
   const int32_t *perm;                       /* [num_perms, C] epoch permutations (generator.py:63-66) */
   const double *cdf;                         /* [V] normalised cumsum of neg_sampler */
   const double *neg_sampler;                 /* [V] generator.py:30 */
+  const int32_t *guide;                      /* optional [2^guide_log2 + 1]: guide[g] =
+                                                searchsorted_right(cdf, g / 2^guide_log2) */
+  int32_t guide_log2;                        /* 0 = no guide table (full binary search) */
   const int64_t *state;                      /* device {step, batch_in_epoch, epoch, 0} */
   int32_t *x_cnt;                            /* [R] R = B (+B with reg) */
   int32_t *x_idx;                            /* [R, x_cap] sorted card ids of x */
@@ -101,10 +104,11 @@ int cc_embed_gather_fwd(int32_t dtype, const void *table, const float *bias, int
 /* ----------------------------------------------------------------------------------
  * E1 backward: dW1[r] = sum_{b : r in x_b} dpre[b] (ascending b, deterministic), for every
  * row r of W1 (dense, as TF's MatMul gradient is dense).  xt_bits [V, ceil(R/32)].
- * Writes grad [V, d] fp32.  Replaces the MatMul gradient of model.py:27 inside fit.
+ * Writes grad [V, d] fp32 and, when bias_grad != NULL, bias_grad[c] = sum_b dpre[b, c] (db1).
+ * Replaces the MatMul/BiasAdd gradients of model.py:27 inside fit.
  * ---------------------------------------------------------------------------------- */
 int cc_embed_scatter_bwd(const float *dpre, int32_t V, int32_t d, int32_t R,
-                         const uint32_t *xt_bits, float *grad, void *stream);
+                         const uint32_t *xt_bits, float *grad, float *bias_grad, void *stream);
 
 /* ----------------------------------------------------------------------------------
  * Generic MFMA GEMM with fused epilogues — the Dense layers of the E/D towers and the
@@ -132,14 +136,19 @@ typedef struct cc_gemm_args {
   const uint32_t *y_bits; /* CC_EPI_BCE: [M, ceil(N/32)] targets */
   float scale;          /* CC_EPI_BCE: 1/(B*V) */
   double *loss_partials;  /* CC_EPI_BCE: [gridDim.x*gridDim.y] */
+  float *colsum;        /* optional [N] ([splits, N] with CC_EPI_SPLITK): colsum[n] = sum_k op(B)[k, n]
+                           (fp32, ascending k) — the bias gradient of a Dense layer fused into its
+                           dW = X^T dPre product */
 } cc_gemm_args;
 int cc_gemm(const cc_gemm_args *g, void *stream);
 /* workspace bound for cc_gemm's loss partials: ceil(M/64)*ceil(N/64) doubles */
 int cc_gemm_grid(int32_t M, int32_t N, int32_t *tiles);
 
-/* Sum K-split partials (in split order) and apply the MASK/STORE epilogue. */
+/* Sum K-split partials (in split order) and apply the MASK/STORE epilogue; when colsum_out is
+ * given, also colsum_out[n] = sum_z colsum_partials[z*N + n] (cc_gemm's split-K colsum rows). */
 int cc_splitk_reduce(int32_t dtype, const float *partials, int32_t splits, int32_t M, int32_t N,
-                     const void *H, void *C, float *Cf, void *stream);
+                     const void *H, void *C, float *Cf, const float *colsum_partials,
+                     float *colsum_out, void *stream);
 
 /* out[n] (+)= sum_r X[r, n] (fp32 accumulate, ascending r). db of every Dense layer. */
 int cc_colsum(int32_t dtype, const void *X, int32_t R, int32_t N, int32_t ld, float *out,

@@ -18,7 +18,7 @@ def _gpu():
     L.lib()
 
 
-def _run_noise(lists, V, B, ns, seed, step, with_reg=True, slot_rank=0):
+def _run_noise(lists, V, B, ns, seed, step, with_reg=True, slot_rank=0, guide_log2=0):
     dev = 'cuda'
     lens = np.array([len(c) for c in lists])
     indptr = np.zeros(len(lists) + 1, np.int64)
@@ -32,6 +32,8 @@ def _run_noise(lists, V, B, ns, seed, step, with_reg=True, slot_rank=0):
     cube_ptr, cube_idx = t(indptr, torch.int64), t(idx, torch.int32)
     perm = t(np.arange(len(lists), dtype=np.int32), torch.int32)
     cdf_d, ns_d = t(cdf, torch.float64), t(ns, torch.float64)
+    guide = t(np.searchsorted(cdf, np.arange((1 << guide_log2) + 1) / float(1 << guide_log2),
+                              side='right').astype(np.int32), torch.int32) if guide_log2 else None
     state = t(np.array([step, 0, 0, 0], np.int64), torch.int64)
     x_cnt = torch.zeros(R, device=dev, dtype=torch.int32)
     x_idx = torch.zeros(R, x_cap, device=dev, dtype=torch.int32)
@@ -44,6 +46,7 @@ def _run_noise(lists, V, B, ns, seed, step, with_reg=True, slot_rank=0):
                     batch_stride=B, batch_offset=0, num_perms=1, num_cubes=len(lists), noise_mean=0.2, noise_std=0.1,
                     cube_ptr=cube_ptr.data_ptr(), cube_idx=cube_idx.data_ptr(), perm=perm.data_ptr(),
                     cdf=cdf_d.data_ptr(), neg_sampler=ns_d.data_ptr(), state=state.data_ptr(),
+                    guide=guide.data_ptr() if guide is not None else None, guide_log2=guide_log2,
                     x_cnt=x_cnt.data_ptr(), x_idx=x_idx.data_ptr(), y_bits=y_bits.data_ptr(),
                     xt_bits=xt.data_ptr(), reg_idx=reg.data_ptr(), status=status.data_ptr())
     L.call('cc_noise_fwd', ctypes.byref(a), L.stream_ptr())
@@ -58,14 +61,16 @@ def _run_noise(lists, V, B, ns, seed, step, with_reg=True, slot_rank=0):
     return xs, ys, reg.cpu().numpy(), xtb, cdf
 
 
-@pytest.mark.parametrize('V,B,sizes,seed,step', [
-    (300, 16, (5, 30, 60), 1, 0),
-    (1500, 64, (40, 200, 400), 2, 7),
-    (22000, 64, (180, 360, 450, 540, 720), 20250301, 123456),
+@pytest.mark.parametrize('V,B,sizes,seed,step,glog2', [
+    (300, 16, (5, 30, 60), 1, 0, 0),
+    (1500, 64, (40, 200, 400), 2, 7, 0),
+    (1500, 64, (40, 200, 400), 2, 7, 12),
+    (22000, 64, (180, 360, 450, 540, 720), 20250301, 123456, 0),
+    (22000, 64, (180, 360, 450, 540, 720), 20250301, 123456, 12),
 ])
-def test_noise_bit_exact_vs_oracle(V, B, sizes, seed, step):
+def test_noise_bit_exact_vs_oracle(V, B, sizes, seed, step, glog2):
     lists, Mt, ns = problem(seed, B, V, sizes)
-    xs, ys, reg, xt, cdf = _run_noise(lists, V, B, ns, seed, step)
+    xs, ys, reg, xt, cdf = _run_noise(lists, V, B, ns, seed, step, guide_log2=glog2)
     oxs, oys, oreg, ks = noise_ref.philox_noise_batch(lists, cdf, ns, seed, step, slot_base=0)
     assert np.array_equal(reg, oreg)
     for b in range(B):
@@ -118,10 +123,14 @@ def test_gemm_store_vs_fp64(dtype, ta, tb, M, N, K):
     g.bias = bias.data_ptr()
     g.relu = 1
     g.Cf = Cf.data_ptr()
+    cs = torch.zeros(N, device='cuda')
+    g.colsum = cs.data_ptr()
     L.call('cc_gemm', ctypes.byref(g), L.stream_ptr())
     torch.cuda.synchronize()
     want = np.maximum(ref + bias.double().cpu().numpy(), 0)
     assert rel_err(Cf.cpu().numpy(), want) < 2e-6
+    Bd = Bm.double().cpu().numpy()
+    assert rel_err(cs.cpu().numpy(), (Bd.T if tb else Bd).sum(0)) < 2e-6   # fused bias gradient
 
 
 @pytest.mark.parametrize('dtype', [L.CC_F32, L.CC_BF16])
@@ -130,16 +139,21 @@ def test_gemm_splitk_and_mask(dtype):
     M, N, K, S = 96, 80, 3000, 7
     A, Bm, ref, bias, Cf, g = _gemm_case(dtype, 0, 1, M, N, K, L.CC_EPI_SPLITK, rng)
     part = torch.zeros(S, M, N, device='cuda')
+    cs_part = torch.zeros(S, N, device='cuda')
+    cs = torch.zeros(N, device='cuda')
     g.splits = S
     g.Cf = part.data_ptr()
+    g.colsum = cs_part.data_ptr()
     L.call('cc_gemm', ctypes.byref(g), L.stream_ptr())
     tdt = torch.bfloat16 if dtype == L.CC_BF16 else torch.float32
     H = torch.from_numpy(rng.standard_normal((M, N)).astype(np.float32)).to('cuda', tdt)
     out = torch.zeros(M, N, device='cuda', dtype=tdt)
-    L.call('cc_splitk_reduce', dtype, L.ptr(part), S, M, N, L.ptr(H), L.ptr(out), L.ptr(Cf), L.stream_ptr())
+    L.call('cc_splitk_reduce', dtype, L.ptr(part), S, M, N, L.ptr(H), L.ptr(out), L.ptr(Cf),
+           L.ptr(cs_part), L.ptr(cs), L.stream_ptr())
     torch.cuda.synchronize()
     want = ref * (H.double().cpu().numpy() > 0)
     assert rel_err(Cf.cpu().numpy(), want) < 2e-6
+    assert rel_err(cs.cpu().numpy(), Bm.double().cpu().numpy().T.sum(0)) < 2e-6
     # MASK epilogue directly (no split)
     g2 = L.GemmArgs(dtype=dtype, ta=0, tb=1, epilogue=L.CC_EPI_MASK, M=M, N=N, K=K, lda=K, ldb=K, ldc=N,
                     splits=1, A=A.data_ptr(), B=Bm.data_ptr(), H=H.data_ptr(), Cf=Cf.data_ptr())
@@ -212,8 +226,10 @@ def test_gather_and_scatter(dtype, d):
         xt[l, r // 32] |= np.uint32(1 << (r % 32))
     xtd = torch.from_numpy(xt.view(np.int32)).cuda()
     grad = torch.full((V, d), 7.0, device='cuda')
-    L.call('cc_embed_scatter_bwd', L.ptr(dpre), V, d, R, L.ptr(xtd), L.ptr(grad), L.stream_ptr())
+    bgrad = torch.full((d,), 7.0, device='cuda')
+    L.call('cc_embed_scatter_bwd', L.ptr(dpre), V, d, R, L.ptr(xtd), L.ptr(grad), L.ptr(bgrad), L.stream_ptr())
     torch.cuda.synchronize()
+    assert rel_err(bgrad.cpu().numpy(), dpre.double().cpu().numpy().sum(0)) < 1e-6
     gw = np.zeros((V, d))
     dp = dpre.double().cpu().numpy()
     for r, l in enumerate(lists):
