@@ -40,6 +40,15 @@ class GemmArgs(C.Structure):
     ]
 
 
+class TowerArgs(C.Structure):
+    _fields_ = [
+        ('dtype', C.c_int32), ('d', C.c_int32), ('B', C.c_int32), ('R', C.c_int32),
+        ('w', C.c_void_p * 9), ('wt', C.c_void_p * 9), ('b', C.c_void_p * 9), ('act', C.c_void_p * 7),
+        ('gD3', C.c_void_p), ('gpre1', C.c_void_p), ('slab', C.c_void_p),
+        ('gw', C.c_void_p * 9), ('gb', C.c_void_p * 9),
+    ]
+
+
 _P, _I32, _I64, _F32, _F64, _SZ = C.c_void_p, C.c_int32, C.c_int64, C.c_float, C.c_double, C.c_size_t
 
 # name -> (restype, argtypes); every symbol include/ccrec.h declares
@@ -62,6 +71,11 @@ SIGNATURES = {
     'cc_state_advance': (C.c_int, [_P, _I64, _P]),
     'cc_infer_encode_fp32': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_infer_decode_fp32': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
+    'cc_tower_slab_elems': (_I64, [_I32]),
+    'cc_tower_fwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
+    'cc_tower_bwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
+    'cc_tower_reduce': (C.c_int, [C.POINTER(TowerArgs), _P]),
+    'cc_tower_transpose': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_topn_workspace_size': (_SZ, [_I32]),
     'cc_topn': (C.c_int, [_P, _I32, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
 }

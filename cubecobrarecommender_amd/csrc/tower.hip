@@ -1,0 +1,358 @@
+// Fused E/D towers on 32-row blocks (model.py:29-33 encoder Dense 256/128/64, :58-62 decoder Dense
+// 128/256/d, both decoders) — forward and backward chains in ONE launch each instead of ~20 small
+// GEMM launches.  Rows are independent through the towers, so a block owns RB = 32 rows of the
+// batch and carries them through every layer with the activations in LDS; the weights (0.4 MB)
+// stream from L2.  MFMA: v_mfma_f32_32x32x16_bf16 (bf16) / v_mfma_f32_32x32x2_f32 (fp32 parity).
+//
+// Forward layer  : out[32][N] = relu(X[32][K] W[K][N] + b);  A = X (LDS, row-major),
+//                  B fragments from W^T [N][K] (global, k-contiguous) — cc_tower_transpose.
+// Backward layer : dW_partial[K][N] = H^T G over the block's 32 rows (A = H^T, B = G from the
+//                  transposed LDS images), db_partial = colsum G  -> slab[blk] (no atomics);
+//                  dH[32][K] = G W^T (B fragments straight from W [K][N]) masked by H > 0.
+// cc_tower_reduce sums the slabs in block order: deterministic dW/db for all 9 layers.
+#include "common.hpp"
+
+namespace {
+
+constexpr int RB = 32;   // rows per block
+constexpr int NT = 256;  // 4 waves
+
+struct TowerP {
+  int d, B, R, maxw;
+  const void *w[9];
+  void *wt[9];
+  const float *b[9];
+  void *act[7];
+  const void *gD3;
+  float *gpre1;
+  float *slab;
+  int64_t slab_elems;
+  float *gw[9];
+  float *gb[9];
+};
+
+__host__ __device__ inline void chain_dims(int d, int i, int &K, int &N) {
+  const int Ks[6] = {d, 256, 128, 64, 128, 256};
+  const int Ns[6] = {256, 128, 64, 128, 256, d};
+  K = Ks[i];
+  N = Ns[i];
+}
+__host__ __device__ inline int64_t slab_off(int d, int i) {  // chain layer i (0..5): kernel, bias
+  int64_t o = 0;
+  for (int j = 0; j < i; ++j) {
+    int K, N;
+    chain_dims(d, j, K, N);
+    o += (int64_t)K * N + N;
+  }
+  return o;
+}
+
+template <typename T> struct TMma;
+template <> struct TMma<bf16_t> {
+  static constexpr int KM = 16;
+  using frag = bf16x8_t;
+  static __device__ __forceinline__ frag ld(const bf16_t *p, int kk, int half) {
+    return *reinterpret_cast<const bf16x8_t *>(p + kk + 8 * half);
+  }
+  static __device__ __forceinline__ void mma(const frag &a, const frag &b, f32x16_t &c) {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct TMma<float> {
+  static constexpr int KM = 2;
+  using frag = float;
+  static __device__ __forceinline__ frag ld(const float *p, int kk, int half) { return p[kk + half]; }
+  static __device__ __forceinline__ void mma(const frag &a, const frag &b, f32x16_t &c) {
+    c = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+  }
+};
+
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// C tile (32 rows x 32 cols starting at column n0) = A[32][K] (LDS row-major, lda) . Bt[n][K]
+// (global, row n0+(lane&31) of a [N][K] k-contiguous matrix).  Loads for UB k-steps are issued
+// before their MFMAs.
+template <typename T>
+__device__ __forceinline__ void tile_mm(const T *A, int lda, const T *__restrict__ Bt, int K, int n0,
+                                        f32x16_t &acc) {
+  using M = TMma<T>;
+  constexpr int UB = 8;
+  const int lane = threadIdx.x & 63, half = lane >> 5;
+  const T *arow = A + (lane & 31) * lda;
+  const T *brow = Bt + (int64_t)(n0 + (lane & 31)) * K;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  int kk = 0;
+  for (; kk + UB * M::KM <= K; kk += UB * M::KM) {
+    typename M::frag b[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) b[u] = M::ld(brow, kk + u * M::KM, half);
+#pragma unroll
+    for (int u = 0; u < UB; ++u) M::mma(M::ld(arow, kk + u * M::KM, half), b[u], acc);
+  }
+  for (; kk < K; kk += M::KM) M::mma(M::ld(arow, kk, half), M::ld(brow, kk, half), acc);
+}
+
+template <typename T>
+__device__ __forceinline__ void lds_store_rows(T *Xr, int ldx, T *Xt, int ldt, int row, int col, float v) {
+  T tv;
+  DT<T>::st(&tv, v);
+  Xr[row * ldx + col] = tv;
+  if (Xt) Xt[col * ldt + row] = tv;
+}
+
+// copy a [32][W] block of a global [R][W] activation into LDS row-major (+ transposed) images
+template <typename T>
+__device__ void load_block(const T *__restrict__ g, int W, int r0, T *Xr, int ldx, T *Xt, int ldt) {
+  for (int i = threadIdx.x; i < RB * W; i += NT) {
+    const int row = i / W, col = i % W;
+    const T v = g[(int64_t)(r0 + row) * W + col];
+    Xr[row * ldx + col] = v;
+    if (Xt) Xt[col * ldt + row] = v;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void tower_fwd_kernel(TowerP p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int ldx = p.maxw + 16 / (int)sizeof(T);
+  T *X0 = reinterpret_cast<T *>(smem);
+  T *X1 = X0 + RB * ldx;
+  const int blk = blockIdx.x, r0 = blk * RB;
+  const bool reg = r0 >= p.B;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  load_block<T>(reinterpret_cast<const T *>(p.act[0]), p.d, r0, X0, ldx, (T *)nullptr, 0);
+  __syncthreads();
+  T *xin = X0, *xout = X1;
+  for (int i = 0; i < 6; ++i) {
+    const int l = i < 3 ? i : i + (reg ? 3 : 0);  // layer index 0..8
+    int K, N;
+    chain_dims(p.d, i, K, N);
+    const T *Wt = reinterpret_cast<const T *>(p.wt[l]);
+    const float *bias = p.b[l];
+    T *gout = reinterpret_cast<T *>(p.act[i + 1]);
+    for (int t = wave; t < N / 32; t += 4) {
+      f32x16_t acc;
+      tile_mm<T>(xin, ldx, Wt, K, 32 * t, acc);
+      const int col = 32 * t + (lane & 31);
+      const float bb = bias[col];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = acc_row(r, lane);
+        float v = acc[r] + bb;
+        v = v > 0.f ? v : 0.f;
+        T tv;
+        DT<T>::st(&tv, v);
+        xout[row * ldx + col] = tv;
+        gout[(int64_t)(r0 + row) * N + col] = tv;
+      }
+    }
+    __syncthreads();
+    T *tmp = xin;
+    xin = xout;
+    xout = tmp;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void tower_bwd_kernel(TowerP p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int MAXT = 4;  // dX tiles per wave (K <= 512)
+  const int ldx = p.maxw + 16 / (int)sizeof(T);
+  const int ldt = RB + 16 / (int)sizeof(T);
+  T *Hr = reinterpret_cast<T *>(smem);
+  T *Gr = Hr + RB * ldx;
+  T *Ht = Gr + RB * ldx;
+  T *Gt = Ht + p.maxw * ldt;
+  const int blk = blockIdx.x, r0 = blk * RB;
+  const bool reg = r0 >= p.B;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5;
+  float *slab = p.slab + (int64_t)blk * p.slab_elems;
+  load_block<T>(reinterpret_cast<const T *>(p.gD3), p.d, r0, Gr, ldx, Gt, ldt);
+  for (int i = 5; i >= 0; --i) {
+    const int l = i < 3 ? i : i + (reg ? 3 : 0);
+    int K, N;
+    chain_dims(p.d, i, K, N);
+    load_block<T>(reinterpret_cast<const T *>(p.act[i]), K, r0, Hr, ldx, Ht, ldt);
+    __syncthreads();
+    // ---- dW partial [K][N] = H^T G over 32 rows; db partial = colsum G
+    float *sw = slab + slab_off(p.d, i);
+    const int ntn = N / 32, nt = (K / 32) * ntn;
+    for (int t = wave; t < nt; t += 4) {
+      const int k0 = 32 * (t / ntn), n0 = 32 * (t % ntn);
+      f32x16_t acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const T *arow = Ht + (k0 + (lane & 31)) * ldt;
+      const T *brow = Gt + (n0 + (lane & 31)) * ldt;
+#pragma unroll
+      for (int kk = 0; kk < RB; kk += TMma<T>::KM)
+        TMma<T>::mma(TMma<T>::ld(arow, kk, half), TMma<T>::ld(brow, kk, half), acc);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sw[(int64_t)(k0 + acc_row(r, lane)) * N + n0 + (lane & 31)] = acc[r];
+    }
+    for (int n = threadIdx.x; n < N; n += NT) {
+      float s = 0.f;
+      for (int b = 0; b < RB; ++b) s += DT<T>::ld(&Gr[b * ldx + n]);
+      sw[(int64_t)K * N + n] = s;
+    }
+    // ---- dH[32][K] = G W^T, masked by H > 0
+    const T *W = reinterpret_cast<const T *>(p.w[l]);  // [K][N]: row k is k-contiguous over N
+    f32x16_t accs[MAXT];
+#pragma unroll
+    for (int q = 0; q < MAXT; ++q) {
+      const int t = wave + 4 * q;
+      if (t < K / 32) tile_mm<T>(Gr, ldx, W, N, 32 * t, accs[q]);
+    }
+    __syncthreads();  // every wave has finished reading Gr/Gt/Ht
+#pragma unroll
+    for (int q = 0; q < MAXT; ++q) {
+      const int t = wave + 4 * q;
+      if (t >= K / 32) continue;
+      const int col = 32 * t + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = acc_row(r, lane);
+        const float h = DT<T>::ld(&Hr[row * ldx + col]);
+        const float v = h > 0.f ? accs[q][r] : 0.f;
+        if (i == 0)
+          p.gpre1[(int64_t)(r0 + row) * K + col] = v;
+        else
+          lds_store_rows<T>(Gr, ldx, Gt, ldt, row, col, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// grads[l] = sum over the blocks that touched layer l of their slab partials, in block order.
+__global__ __launch_bounds__(256) void tower_reduce_kernel(TowerP p) {
+  const int nb = p.R / RB, nbB = p.B / RB;
+  const int64_t E = p.slab_elems;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+    int i = 0;
+    while (i < 5 && e >= slab_off(p.d, i + 1)) ++i;
+    int K, N;
+    chain_dims(p.d, i, K, N);
+    const int64_t o = e - slab_off(p.d, i);
+    const bool is_b = o >= (int64_t)K * N;
+    if (i < 3) {
+      float s = 0.f;
+      for (int bk = 0; bk < nb; ++bk) s += p.slab[(int64_t)bk * E + e];
+      if (is_b) p.gb[i][o - (int64_t)K * N] = s; else p.gw[i][o] = s;
+    } else {
+      float s1 = 0.f, s2 = 0.f;
+      for (int bk = 0; bk < nbB; ++bk) s1 += p.slab[(int64_t)bk * E + e];
+      for (int bk = nbB; bk < nb; ++bk) s2 += p.slab[(int64_t)bk * E + e];
+      const int l1 = i, l2 = i + 3;
+      if (is_b) {
+        p.gb[l1][o - (int64_t)K * N] = s1;
+        if (nb > nbB) p.gb[l2][o - (int64_t)K * N] = s2;
+      } else {
+        p.gw[l1][o] = s1;
+        if (nb > nbB) p.gw[l2][o] = s2;
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void tower_transpose_kernel(TowerP p) {
+  __shared__ T tile[32][33];
+  const int l = blockIdx.y;
+  const int i = l < 3 ? l : (l < 6 ? l : l - 3);
+  int K, N;
+  chain_dims(p.d, i, K, N);
+  const int tn = N / 32, ntile = (K / 32) * tn;
+  const T *w = reinterpret_cast<const T *>(p.w[l]);
+  T *wt = reinterpret_cast<T *>(p.wt[l]);
+  for (int t = blockIdx.x; t < ntile; t += gridDim.x) {
+    const int k0 = 32 * (t / tn), n0 = 32 * (t % tn);
+    for (int e = threadIdx.x; e < 1024; e += 256) tile[e / 32][e % 32] = w[(int64_t)(k0 + e / 32) * N + n0 + e % 32];
+    __syncthreads();
+    for (int e = threadIdx.x; e < 1024; e += 256) wt[(int64_t)(n0 + e / 32) * K + k0 + e % 32] = tile[e % 32][e / 32];
+    __syncthreads();
+  }
+}
+
+int make_params(const cc_tower_args *t, TowerP &p) {
+  if (!t) return cc::fail(CC_ERR_ARG, "cc_tower: null args");
+  if (t->dtype != CC_BF16 && t->dtype != CC_F32) return cc::fail(CC_ERR_ARG, "cc_tower: dtype");
+  const int maxd = t->dtype == CC_BF16 ? 512 : 256;
+  if (t->d < 64 || t->d > maxd || t->d % 64) return cc::fail(CC_ERR_UNSUPPORTED, "cc_tower: d out of range for the fused towers");
+  if (t->B % RB || t->R % RB || t->R < t->B || t->B <= 0) return cc::fail(CC_ERR_ARG, "cc_tower: B and R must be multiples of 32");
+  p.d = t->d;
+  p.B = t->B;
+  p.R = t->R;
+  p.maxw = t->d > 256 ? t->d : 256;
+  for (int l = 0; l < 9; ++l) {
+    p.w[l] = t->w[l];
+    p.wt[l] = t->wt[l];
+    p.b[l] = t->b[l];
+    p.gw[l] = t->gw[l];
+    p.gb[l] = t->gb[l];
+  }
+  for (int a = 0; a < 7; ++a) p.act[a] = t->act[a];
+  p.gD3 = t->gD3;
+  p.gpre1 = t->gpre1;
+  p.slab = t->slab;
+  p.slab_elems = slab_off(t->d, 6);
+  return CC_OK;
+}
+
+}  // namespace
+
+extern "C" int64_t cc_tower_slab_elems(int32_t d) { return slab_off(d, 6); }
+
+extern "C" int cc_tower_fwd(const cc_tower_args *t, void *stream) {
+  TowerP p;
+  int rc = make_params(t, p);
+  if (rc) return rc;
+  const int es = t->dtype == CC_BF16 ? 2 : 4;
+  const size_t lds = (size_t)2 * RB * (p.maxw + 16 / es) * es;
+  if (t->dtype == CC_BF16)
+    hipLaunchKernelGGL(tower_fwd_kernel<bf16_t>, dim3(p.R / RB), dim3(NT), lds, as_stream(stream), p);
+  else
+    hipLaunchKernelGGL(tower_fwd_kernel<float>, dim3(p.R / RB), dim3(NT), lds, as_stream(stream), p);
+  CC_LAUNCH_CHECK("tower_fwd_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_tower_bwd(const cc_tower_args *t, void *stream) {
+  TowerP p;
+  int rc = make_params(t, p);
+  if (rc) return rc;
+  CC_REQUIRE(t->gD3 && t->gpre1 && t->slab, "cc_tower_bwd: null gD3/gpre1/slab");
+  const int es = t->dtype == CC_BF16 ? 2 : 4;
+  const size_t lds = (size_t)(2 * RB * (p.maxw + 16 / es) + 2 * p.maxw * (RB + 16 / es)) * es;
+  CC_REQUIRE(lds <= 160 * 1024, "cc_tower_bwd: LDS");
+  if (t->dtype == CC_BF16)
+    hipLaunchKernelGGL(tower_bwd_kernel<bf16_t>, dim3(p.R / RB), dim3(NT), lds, as_stream(stream), p);
+  else
+    hipLaunchKernelGGL(tower_bwd_kernel<float>, dim3(p.R / RB), dim3(NT), lds, as_stream(stream), p);
+  CC_LAUNCH_CHECK("tower_bwd_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_tower_reduce(const cc_tower_args *t, void *stream) {
+  TowerP p;
+  int rc = make_params(t, p);
+  if (rc) return rc;
+  const unsigned blocks = (unsigned)std::min<int64_t>(cdiv(p.slab_elems, 256), 2048);
+  hipLaunchKernelGGL(tower_reduce_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), p);
+  CC_LAUNCH_CHECK("tower_reduce_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_tower_transpose(const cc_tower_args *t, void *stream) {
+  TowerP p;
+  int rc = make_params(t, p);
+  if (rc) return rc;
+  const int layers = t->R > t->B ? 9 : 6;
+  if (t->dtype == CC_BF16)
+    hipLaunchKernelGGL(tower_transpose_kernel<bf16_t>, dim3(64, layers), dim3(256), 0, as_stream(stream), p);
+  else
+    hipLaunchKernelGGL(tower_transpose_kernel<float>, dim3(64, layers), dim3(256), 0, as_stream(stream), p);
+  CC_LAUNCH_CHECK("tower_transpose_kernel");
+  return CC_OK;
+}

@@ -33,6 +33,7 @@ class TrainConfig:
     seed: int = 0
     rank: int = 0
     world: int = 1
+    fused_tower: bool = True       # tower.hip row-block kernels (else per-layer cc_gemm launches)
 
 
 class DeviceDataset:
@@ -143,6 +144,22 @@ class Trainer:
         self.bce_part = torch.zeros(tiles, device=self.dev, dtype=torch.float64)
         self.kl_part = torch.zeros(B, device=self.dev, dtype=torch.float64)
         self.loss_dev = torch.zeros(2, device=self.dev, dtype=torch.float64)
+        # fused 32-row-block towers (tower.hip) when the widths fit; generic GEMMs otherwise
+        self.fused_tower = cfg.fused_tower and (B % 32 == 0) and d <= (512 if self.dtype == L.CC_BF16 else 256)
+        if self.fused_tower:
+            self.tower_layers = ('encoder/encoded_2', 'encoder/encoded_3', 'encoder/bottleneck',
+                                 'decoder/decoded_1', 'decoder/decoded_2', 'decoder/decoded_3',
+                                 'decoder_for_reg/decoded_1', 'decoder_for_reg/decoded_2',
+                                 'decoder_for_reg/decoded_3')
+            sizes = [int(np.prod(self.layout.shape(n + '/kernel'))) for n in self.tower_layers]
+            self.wt_off = np.concatenate([[0], np.cumsum([(n + 63) // 64 * 64 for n in sizes])])
+            self.wt = torch.zeros(int(self.wt_off[-1]), **T)
+            slab = int(L.lib().cc_tower_slab_elems(d))
+            self.slab = torch.zeros((R // 32) * slab, **f32)
+            self.targs = self._tower_args()
+            self.transpose_tower()
+        else:
+            self.targs = None
         self.perms = None
         self.batches_per_epoch = max(1, data.C // (B * cfg.world))   # generator.py:36 (__len__)
         self.graphs = None
@@ -179,9 +196,32 @@ class Trainer:
     def gp(self, name):
         return L.ptr(self.grads[self.layout.offset(name):])
 
+    def _tower_args(self):
+        t = L.TowerArgs(dtype=self.dtype, d=self.cfg.d, B=self.cfg.batch_size, R=self.R)
+        src = self.shadow if self.shadow is not None else self.params
+        for l, name in enumerate(self.tower_layers):
+            t.w[l] = src[self.layout.offset(name + '/kernel'):].data_ptr()
+            t.wt[l] = self.wt[int(self.wt_off[l]):].data_ptr()
+            t.b[l] = self.params[self.layout.offset(name + '/bias'):].data_ptr()
+            t.gw[l] = self.grads[self.layout.offset(name + '/kernel'):].data_ptr()
+            t.gb[l] = self.grads[self.layout.offset(name + '/bias'):].data_ptr()
+        for a, buf in enumerate((self.H1, self.H2, self.H3, self.Zl, self.D1, self.D2, self.D3)):
+            t.act[a] = buf.data_ptr()
+        t.gD3 = self.gD3.data_ptr()
+        t.gpre1 = self.gPre1.data_ptr()
+        t.slab = self.slab.data_ptr()
+        return t
+
+    def transpose_tower(self, stream=None):
+        if self.fused_tower:
+            L.call('cc_tower_transpose', L.C.byref(self.targs), L.stream_ptr(stream))
+
     def refresh_shadow(self):
+        """Re-derive the bf16 shadow (and the transposed tower operands) from the fp32 master."""
         if self.shadow is not None:
             L.call('cc_to_bf16', L.ptr(self.params), L.ptr(self.shadow), self.layout.total, L.stream_ptr())
+        if getattr(self, 'targs', None) is not None:
+            self.transpose_tower()
 
     def set_epoch_permutation(self, perm):
         """Upload one epoch's cube order (generator.py:63-72) and reset the batch counter."""
@@ -260,14 +300,19 @@ class Trainer:
                self.pf('encoder/encoded_1/bias'), V, d, R, L.ptr(self.x_cnt), L.ptr(self.x_idx),
                self.x_cap, L.ptr(self.H1), s)
         t()
-        self._dense_fwd(self.H1, (0, R), d, 256, 'encoder/encoded_2', self.H2)
-        self._dense_fwd(self.H2, (0, R), 256, 128, 'encoder/encoded_3', self.H3)
-        self._dense_fwd(self.H3, (0, R), 128, 64, 'encoder/bottleneck', self.Zl)
         branches = [('decoder', (0, B))] + ([('decoder_for_reg', (B, 2 * B))] if self.use_reg else [])
-        for pre, rows in branches:
-            self._dense_fwd(self.Zl, rows, 64, 128, pre + '/decoded_1', self.D1)
-            self._dense_fwd(self.D1, rows, 128, 256, pre + '/decoded_2', self.D2)
-            self._dense_fwd(self.D2, rows, 256, d, pre + '/decoded_3', self.D3)
+        if self.fused_tower:
+            t = self._tick('cc_tower_fwd')
+            L.call('cc_tower_fwd', L.C.byref(self.targs), s)
+            t()
+        else:
+            self._dense_fwd(self.H1, (0, R), d, 256, 'encoder/encoded_2', self.H2)
+            self._dense_fwd(self.H2, (0, R), 256, 128, 'encoder/encoded_3', self.H3)
+            self._dense_fwd(self.H3, (0, R), 128, 64, 'encoder/bottleneck', self.Zl)
+            for pre, rows in branches:
+                self._dense_fwd(self.Zl, rows, 64, 128, pre + '/decoded_1', self.D1)
+                self._dense_fwd(self.D1, rows, 128, 256, pre + '/decoded_2', self.D2)
+                self._dense_fwd(self.D2, rows, 256, d, pre + '/decoded_3', self.D3)
         # ---- D1 output + sigmoid + BCE -> dZ (model.py:64,94; train.py:85)
         t = self._tick('dec_bce_fwd')
         self._gemm(B, V, d, L.ptr(self.D3), d, self.w('decoder/reconstruct/kernel'), V,
@@ -296,14 +341,21 @@ class Trainer:
             t()
             L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), self.splits, B, d,
                    L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
-            rows = (r0, r1)
-            self._dense_bwd(self.D2, self.gD3, rows, 256, d, pre + '/decoded_3', gIn=self.gD2, mask=self.D2)
-            self._dense_bwd(self.D1, self.gD2, rows, 128, 256, pre + '/decoded_2', gIn=self.gD1, mask=self.D1)
-            self._dense_bwd(self.Zl, self.gD1, rows, 64, 128, pre + '/decoded_1', gIn=self.gZl, mask=self.Zl)
-        # ---- encoder backward (both branches' rows together)
-        self._dense_bwd(self.H3, self.gZl, (0, R), 128, 64, 'encoder/bottleneck', gIn=self.gH3, mask=self.H3)
-        self._dense_bwd(self.H2, self.gH3, (0, R), 256, 128, 'encoder/encoded_3', gIn=self.gH2, mask=self.H2)
-        self._dense_bwd(self.H1, self.gH2, (0, R), d, 256, 'encoder/encoded_2', gIn_f32=self.gPre1, mask=self.H1)
+            if not self.fused_tower:
+                rows = (r0, r1)
+                self._dense_bwd(self.D2, self.gD3, rows, 256, d, pre + '/decoded_3', gIn=self.gD2, mask=self.D2)
+                self._dense_bwd(self.D1, self.gD2, rows, 128, 256, pre + '/decoded_2', gIn=self.gD1, mask=self.D1)
+                self._dense_bwd(self.Zl, self.gD1, rows, 64, 128, pre + '/decoded_1', gIn=self.gZl, mask=self.Zl)
+        # ---- towers backward (both branches' rows together through the shared encoder)
+        if self.fused_tower:
+            t = self._tick('cc_tower_bwd')
+            L.call('cc_tower_bwd', L.C.byref(self.targs), s)
+            t()
+            L.call('cc_tower_reduce', L.C.byref(self.targs), s)
+        else:
+            self._dense_bwd(self.H3, self.gZl, (0, R), 128, 64, 'encoder/bottleneck', gIn=self.gH3, mask=self.H3)
+            self._dense_bwd(self.H2, self.gH3, (0, R), 256, 128, 'encoder/encoded_3', gIn=self.gH2, mask=self.H2)
+            self._dense_bwd(self.H1, self.gH2, (0, R), d, 256, 'encoder/encoded_2', gIn_f32=self.gPre1, mask=self.H1)
         t = self._tick('cc_embed_scatter_bwd')
         L.call('cc_embed_scatter_bwd', L.ptr(self.gPre1), V, d, R, L.ptr(self.xt_bits),
                self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
@@ -318,6 +370,7 @@ class Trainer:
                L.ptr(self.shadow), n, L.ptr(self.state), cfg.lr, cfg.beta1, cfg.beta2, cfg.eps, s)
         t()
         L.call('cc_state_advance', L.ptr(self.state), self.batches_per_epoch, s)
+        self.transpose_tower(stream)
 
     def step(self, stream=None):
         if self.graphs is not None:

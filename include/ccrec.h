@@ -155,6 +155,35 @@ int cc_colsum(int32_t dtype, const void *X, int32_t R, int32_t N, int32_t ld, fl
               void *stream);
 
 /* ----------------------------------------------------------------------------------
+ * Fused towers (model.py:29-33 E2..E4, :58-62 D1..D3 of both decoders) on 32-row blocks.
+ * Rows [0,B) use `decoder`, rows [B,R) `decoder_for_reg`; one block never straddles B.
+ * Layer order l = 0..8: e2, e3, e4 | d1, d2, d3 (decoder) | d1, d2, d3 (decoder_for_reg).
+ *   cc_tower_fwd: act[0] = H1 (input) -> act[1..6] = H2, H3, Zl, D1, D2, D3 (bias+ReLU fused).
+ *   cc_tower_bwd: from gD3 = dPre of d3 [R,d] down to gpre1 = dPre of e1 [R,d] fp32, with the
+ *                 per-block partial dW/db of all 6 layers a block touches in slab[blk][...].
+ *   cc_tower_reduce: grads of the 9 layers = sum of the slabs in block order (deterministic).
+ *   cc_tower_transpose: wt[l] = w[l]^T ([N][K]) — the k-contiguous operand the forward reads.
+ * d <= 512 (bf16) / <= 256 (fp32); the generic cc_gemm path covers larger widths.
+ * ---------------------------------------------------------------------------------- */
+typedef struct cc_tower_args {
+  int32_t dtype, d, B, R;
+  const void *w[9];      /* [K][N] dtype */
+  void *wt[9];           /* [N][K] dtype */
+  const float *b[9];     /* [N] */
+  void *act[7];          /* H1, H2, H3, Zl, D1, D2, D3: [R, width] dtype */
+  const void *gD3;       /* [R, d] dtype */
+  float *gpre1;          /* [R, d] fp32 */
+  float *slab;           /* [R/32, cc_tower_slab_elems(d)] fp32 */
+  float *gw[9];          /* reduce outputs: kernel grads [K][N] */
+  float *gb[9];          /* bias grads [N] */
+} cc_tower_args;
+int64_t cc_tower_slab_elems(int32_t d);
+int cc_tower_fwd(const cc_tower_args *t, void *stream);
+int cc_tower_bwd(const cc_tower_args *t, void *stream);
+int cc_tower_reduce(const cc_tower_args *t, void *stream);
+int cc_tower_transpose(const cc_tower_args *t, void *stream);
+
+/* ----------------------------------------------------------------------------------
  * D1 output layer fused with sigmoid+BCE (model.py:64,94; train.py:85): logits
  * z = H3 Wo + bo are never written; dZ = (sigmoid(z) - y)/(B*V) is.
  * D2 softmax + KL (model.py:98; train.py:85): per reg row, row-softmax of z2, KL against the

@@ -1,0 +1,113 @@
+"""GPU: fused tower kernels (tower.hip) vs a numpy restatement of the same layer chain."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from cubecobrarecommender_amd import _lib as L
+from tests.gpu_helpers import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _dims(d):
+    return [(d, 256), (256, 128), (128, 64), (64, 128), (128, 256), (256, d)]
+
+
+@pytest.mark.parametrize('dtype', [L.CC_F32, L.CC_BF16])
+@pytest.mark.parametrize('d,B,R', [(64, 32, 64), (256, 64, 128), (256, 64, 64), (64, 32, 32), (512, 64, 128)])
+def test_tower_fwd_bwd_vs_numpy(dtype, d, B, R):
+    if dtype == L.CC_F32 and d > 256:
+        pytest.skip('fp32 fused towers cover d <= 256')
+    rng = np.random.default_rng(d + R)
+    tdt = torch.bfloat16 if dtype == L.CC_BF16 else torch.float32
+    rnd = lambda *s: torch.from_numpy((rng.standard_normal(s) * 0.2).astype(np.float32)).to('cuda', tdt)
+    dims = _dims(d)
+    W = [rnd(*dims[l if l < 6 else l - 3]) for l in range(9)]
+    Wt = [torch.zeros(w.shape[1], w.shape[0], device='cuda', dtype=tdt) for w in W]
+    bias = [torch.from_numpy(rng.standard_normal(w.shape[1]).astype(np.float32) * 0.1).cuda() for w in W]
+    widths = [d, 256, 128, 64, 128, 256, d]
+    act = [rnd(R, widths[0])] + [torch.zeros(R, w, device='cuda', dtype=tdt) for w in widths[1:]]
+    gD3 = rnd(R, d)
+    gpre1 = torch.zeros(R, d, device='cuda')
+    slab = torch.zeros((R // 32) * int(L.lib().cc_tower_slab_elems(d)), device='cuda')
+    gw = [torch.zeros(w.shape, device='cuda') for w in W]
+    gb = [torch.zeros(w.shape[1], device='cuda') for w in W]
+    t = L.TowerArgs(dtype=dtype, d=d, B=B, R=R)
+    for l in range(9):
+        t.w[l], t.wt[l], t.b[l] = W[l].data_ptr(), Wt[l].data_ptr(), bias[l].data_ptr()
+        t.gw[l], t.gb[l] = gw[l].data_ptr(), gb[l].data_ptr()
+    for a in range(7):
+        t.act[a] = act[a].data_ptr()
+    t.gD3, t.gpre1, t.slab = gD3.data_ptr(), gpre1.data_ptr(), slab.data_ptr()
+    s = L.stream_ptr()
+    for fn in ('cc_tower_transpose', 'cc_tower_fwd', 'cc_tower_bwd', 'cc_tower_reduce'):
+        L.call(fn, ctypes.byref(t), s)
+    torch.cuda.synchronize()
+    f = lambda x: x.double().cpu().numpy()
+    q = (lambda a: torch.from_numpy(np.asarray(a, np.float32)).to(tdt).double().numpy())
+    for l in range(9 if R > B else 6):
+        assert np.array_equal(f(Wt[l]), f(W[l]).T), f'transpose {l}'
+    # forward
+    h = f(act[0])
+    errs = {}
+    acts = [h]
+    for i in range(6):
+        rows_l = [(np.arange(R) < B), (np.arange(R) >= B)]
+        out = np.zeros((R, widths[i + 1]))
+        for br, rows in enumerate(rows_l):
+            l = i if i < 3 else i + 3 * br
+            if rows.any():
+                out[rows] = q(np.maximum(h[rows] @ f(W[l]) + f(bias[l]), 0))
+        errs[f'act{i + 1}'] = rel_err(f(act[i + 1]), out)
+        h = f(act[i + 1])          # continue from the GPU's own activations
+        acts.append(h)
+    # backward
+    g = f(gD3)
+    gW = [np.zeros(w.shape) for w in W]
+    gB = [np.zeros(w.shape[1]) for w in W]
+    for i in range(5, -1, -1):
+        H = acts[i]
+        dX = np.zeros((R, widths[i]))
+        for br, rows in enumerate([(np.arange(R) < B), (np.arange(R) >= B)]):
+            l = i if i < 3 else i + 3 * br
+            if not rows.any():
+                continue
+            gW[l] += H[rows].T @ g[rows]
+            gB[l] += g[rows].sum(0)
+            dX[rows] = (g[rows] @ f(W[l]).T) * (H[rows] > 0)
+        g = dX if i == 0 else q(dX)
+    errs['gpre1'] = rel_err(f(gpre1), g)
+    for l in range(9):
+        if l >= 6 and R == B:
+            continue
+        errs[f'gw{l}'] = rel_err(f(gw[l]), gW[l])
+        errs[f'gb{l}'] = rel_err(f(gb[l]), gB[l])
+    tol = 1e-5 if dtype == L.CC_F32 else 2e-2
+    bad = {k: v for k, v in errs.items() if not v < tol}
+    assert not bad, bad
+
+
+def test_device_lds_limits():
+    p = torch.cuda.get_device_properties(0)
+    print('LDS per block', getattr(p, 'shared_memory_per_block', None),
+          'optin', getattr(p, 'shared_memory_per_block_optin', None),
+          'per CU', getattr(p, 'shared_memory_per_multiprocessor', None))
+
+
+
+def test_fused_towers_match_generic_gemm_path():
+    """The fused tower kernels and the per-layer cc_gemm path give the same step (bf16 & fp32)."""
+    from tests.test_gpu_train import _setup
+    for dtype in ('fp32', 'bf16'):
+        res = {}
+        for fused in (True, False):
+            tr, *_ = _setup(700, 64, 32, 128, 0.1, dtype, fused_tower=fused)
+            tr.forward_backward()
+            torch.cuda.synchronize()
+            res[fused] = tr.layout.unpack(tr.grads.cpu().numpy())
+        tol = 1e-5 if dtype == 'fp32' else 1e-2
+        bad = {k: rel_err(res[True][k], res[False][k]) for k in res[True]
+               if not rel_err(res[True][k], res[False][k]) < tol}
+        assert not bad, (dtype, bad)
