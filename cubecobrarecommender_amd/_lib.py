@@ -36,7 +36,7 @@ class GemmArgs(C.Structure):
         ('ldb', C.c_int32), ('ldc', C.c_int32), ('splits', C.c_int32), ('relu', C.c_int32),
         ('A', C.c_void_p), ('B', C.c_void_p), ('bias', C.c_void_p), ('C', C.c_void_p),
         ('Cf', C.c_void_p), ('H', C.c_void_p), ('y_bits', C.c_void_p), ('scale', C.c_float),
-        ('loss_partials', C.c_void_p), ('colsum', C.c_void_p),
+        ('loss_partials', C.c_void_p), ('colsum', C.c_void_p), ('Ct', C.c_void_p), ('ldct', C.c_int32),
     ]
 
 
@@ -44,7 +44,8 @@ class TowerArgs(C.Structure):
     _fields_ = [
         ('dtype', C.c_int32), ('d', C.c_int32), ('B', C.c_int32), ('R', C.c_int32),
         ('w', C.c_void_p * 9), ('wt', C.c_void_p * 9), ('b', C.c_void_p * 9), ('act', C.c_void_p * 7),
-        ('gD3', C.c_void_p), ('gpre1', C.c_void_p), ('slab', C.c_void_p),
+        ('act6t', C.c_void_p),
+        ('gD3', C.c_void_p), ('gact', C.c_void_p * 5), ('gpre1', C.c_void_p), ('slab', C.c_void_p),
         ('gw', C.c_void_p * 9), ('gb', C.c_void_p * 9),
     ]
 
@@ -63,6 +64,7 @@ SIGNATURES = {
     'cc_gemm_grid': (C.c_int, [_I32, _I32, _P]),
     'cc_splitk_reduce': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     'cc_colsum': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P]),
+    'cc_transpose': (C.c_int, [_I32, _P, _I32, _I32, _P, _P]),
     'cc_dec_bce_fused': (C.c_int, [_I32, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     'cc_dec_softmax_kl_fused': (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _F32, _P, _P, _P]),
     'cc_reduce_loss': (C.c_int, [_P, _I32, _F64, _P, _P]),

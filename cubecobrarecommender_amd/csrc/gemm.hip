@@ -5,7 +5,7 @@
 //   bf16 operands: v_mfma_f32_32x32x16_bf16   (lane l: A[l&31][8(l>>5)+j], B[8(l>>5)+j][l&31])
 //   fp32 operands: v_mfma_f32_32x32x2_f32     (lane l: A[l&31][l>>5],       B[l>>5][l&31]) —
 //                  exact fp32 (a k-ordered fmaf chain), used for the fp32 parity mode.
-// Workgroup = 4 waves (256 threads), 64x64 output tile, 2x2 waves of 32x32, BK = 32.
+// Workgroup = 4 waves (256 threads), 64x64 output tile, 2x2 waves of 32x32, BK = 32/64/128 by K.
 // Both LDS images are K-contiguous ([row][k] / [col][k]); transposed global layouts are
 // transposed during staging so every fragment read is one ds_read_b128 (bf16) / b32 (fp32).
 // Accumulator map (32x32): row = (r&3) + 8(r>>2) + 4(l>>5), col = l&31.
@@ -13,7 +13,7 @@
 
 namespace {
 
-constexpr int BM = 64, BN = 64, BK = 32, NT = 256;
+constexpr int BM = 64, BN = 64, NT = 256;
 
 struct GemmParams {
   int M, N, K, lda, ldb, ldc, splits, relu;
@@ -27,6 +27,8 @@ struct GemmParams {
   float scale;
   double *loss_partials;
   float *colsum;
+  void *Ct;
+  int ldct;
 };
 
 template <typename T> struct Mma;
@@ -53,7 +55,7 @@ template <> struct Mma<float> {
 //   else   : storage X[k*ld + row] (16-B vectors along row, transposed into LDS element-wise).
 // load() issues the global loads into registers; store() writes them to LDS — split so the next
 // tile's loads are in flight while the current tile's MFMAs run.
-template <typename T, bool KCONTIG, int ROWS>
+template <typename T, bool KCONTIG, int ROWS, int BK>
 struct Stager {
   static constexpr int VW = 16 / sizeof(T);
   static constexpr int NVEC = ROWS * BK / VW;
@@ -129,7 +131,7 @@ __device__ __forceinline__ double block_sum_double(double v, double *red) {
   return s;
 }
 
-template <typename T, bool TA, bool TB, int EPI>
+template <typename T, bool TA, bool TB, int EPI, int BK>
 __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams p) {
   constexpr int PADK = 16 / sizeof(T);
   constexpr int LDK = BK + PADK;
@@ -157,8 +159,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams p) {
   // fused bias gradient: the first row of blocks sums the staged op(B) tile over k (ascending)
   const bool do_cs = p.colsum != nullptr && blockIdx.y == 0 && threadIdx.x < BN;
   float cs = 0.f;
-  Stager<T, !TA, BM> sa;
-  Stager<T, TB, BN> sb;
+  Stager<T, !TA, BM, BK> sa;
+  Stager<T, TB, BN, BK> sb;
   if (kbeg < kend) {
     sa.load(A, p.lda, bm, p.M, kbeg, kend, p.vec_a);
     sb.load(B, p.ldb, bn, p.N, kbeg, kend, p.vec_b);
@@ -187,7 +189,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams p) {
 
   // ------------------------------------------------------------------ epilogues
   const int gn = bn + wn * 32 + (lane & 31);
-  double loss = 0.0;
+  float lossf = 0.f;
+  float dzv[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int gm = bm + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
@@ -212,37 +215,69 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams p) {
       const float z = a + p.bias[gn];
       const int YW = (p.N + 31) >> 5;
       const float y = (float)((p.y_bits[(int64_t)gm * YW + (gn >> 5)] >> (gn & 31)) & 1u);
-      const float az = fabsf(z);
-      loss += (double)(fmaxf(z, 0.f) - z * y + log1pf(expf(-az)));
-      const float e = expf(-az);
-      const float sig = z >= 0.f ? 1.f / (1.f + e) : e / (1.f + e);
+      const float e = __expf(-fabsf(z));               // in (0, 1]
+      const float rp = __fdividef(1.f, 1.f + e);
+      lossf += fmaxf(z, 0.f) - z * y + __logf(1.f + e);   // log1p(exp(-|z|))
+      const float sig = z >= 0.f ? rp : e * rp;
       const float dz = (sig - y) * p.scale;
+      dzv[r] = dz;
       const int64_t o = (int64_t)gm * p.ldc + gn;
       if (p.C) DT<T>::st(reinterpret_cast<T *>(p.C) + o, dz);
       if (p.Cf) p.Cf[o] = dz;
     }
   }
   if constexpr (EPI == CC_EPI_BCE) {
-    const double s = block_sum_double(loss, red);
+    // transposed copy dZ^T [N][M] (k-contiguous operand of the dW = H^T dZ product): registers
+    // 4g..4g+3 hold 4 consecutive rows of one column -> one 8-byte (bf16) / 16-byte (fp32) store
+    if (p.Ct && gn < p.N) {
+      T *ct = reinterpret_cast<T *>(p.Ct) + (int64_t)gn * p.ldct;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int row0 = bm + wm * 32 + 8 * g + 4 * half;
+        if (row0 + 3 < p.M && (p.ldct & 3) == 0) {
+          T v4[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) DT<T>::st(&v4[e], dzv[4 * g + e]);
+          if constexpr (sizeof(T) == 2)
+            *reinterpret_cast<uint2 *>(ct + row0) = *reinterpret_cast<const uint2 *>(v4);
+          else
+            *reinterpret_cast<uint4 *>(ct + row0) = *reinterpret_cast<const uint4 *>(v4);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (row0 + e < p.M) DT<T>::st(ct + row0 + e, dzv[4 * g + e]);
+        }
+      }
+    }
+    const double s = block_sum_double((double)lossf, red);
     if (threadIdx.x == 0) p.loss_partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
   }
 }
 
-template <typename T, int EPI>
-int launch_t(const cc_gemm_args *g, const GemmParams &p, hipStream_t s) {
+template <typename T, int EPI, int BK>
+int launch_bk(const cc_gemm_args *g, const GemmParams &p, hipStream_t s) {
   const dim3 grid((unsigned)cdiv(g->N, BN), (unsigned)cdiv(g->M, BM),
                   EPI == CC_EPI_SPLITK ? (unsigned)g->splits : 1u);
   const dim3 block(NT);
   if (g->ta && g->tb)
-    hipLaunchKernelGGL((gemm_kernel<T, true, true, EPI>), grid, block, 0, s, p);
+    hipLaunchKernelGGL((gemm_kernel<T, true, true, EPI, BK>), grid, block, 0, s, p);
   else if (g->ta)
-    hipLaunchKernelGGL((gemm_kernel<T, true, false, EPI>), grid, block, 0, s, p);
+    hipLaunchKernelGGL((gemm_kernel<T, true, false, EPI, BK>), grid, block, 0, s, p);
   else if (g->tb)
-    hipLaunchKernelGGL((gemm_kernel<T, false, true, EPI>), grid, block, 0, s, p);
+    hipLaunchKernelGGL((gemm_kernel<T, false, true, EPI, BK>), grid, block, 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_kernel<T, false, false, EPI>), grid, block, 0, s, p);
+    hipLaunchKernelGGL((gemm_kernel<T, false, false, EPI, BK>), grid, block, 0, s, p);
   CC_LAUNCH_CHECK("gemm_kernel");
   return CC_OK;
+}
+
+// K-tile depth: a deeper BK puts more bytes in flight per iteration of the latency-bound K loop.
+template <typename T, int EPI>
+int launch_t(const cc_gemm_args *g, const GemmParams &p, hipStream_t s) {
+  const int kc = EPI == CC_EPI_SPLITK ? (int)cdiv(g->K, g->splits) : g->K;
+  if (sizeof(T) == 2 && kc >= 512) return launch_bk<T, EPI, 128>(g, p, s);
+  if (kc >= 128) return launch_bk<T, EPI, 64>(g, p, s);
+  return launch_bk<T, EPI, 32>(g, p, s);
 }
 
 template <typename T>
@@ -288,6 +323,22 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T *__restrict__ X, in
   out[n] = s;
 }
 
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_kernel(const T *__restrict__ src, int rows, int cols,
+                                                        T *__restrict__ dst) {
+  __shared__ T tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int r = r0 + e / 64, c = c0 + e % 64;
+    if (r < rows && c < cols) tile[e / 64][e % 64] = src[(int64_t)r * cols + c];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int c = c0 + e / 64, r = r0 + e % 64;
+    if (r < rows && c < cols) dst[(int64_t)c * rows + r] = tile[e % 64][e / 64];
+  }
+}
+
 __global__ void reduce_loss_kernel(const double *__restrict__ part, int n, double scale,
                                    double *out) {
   __shared__ double red[4];
@@ -324,6 +375,9 @@ extern "C" int cc_gemm(const cc_gemm_args *g, void *stream) {
   p.A = g->A; p.B = g->B; p.bias = g->bias; p.C = g->C; p.Cf = g->Cf; p.H = g->H;
   p.y_bits = g->y_bits; p.scale = g->scale; p.loss_partials = g->loss_partials;
   p.colsum = g->colsum;
+  p.Ct = g->Ct;
+  p.ldct = g->ldct;
+  CC_REQUIRE(!g->Ct || g->epilogue == CC_EPI_BCE, "cc_gemm: Ct only with the BCE epilogue");
 
   hipStream_t s = as_stream(stream);
   return g->dtype == CC_BF16 ? launch_epi<bf16_t>(g, p, s) : launch_epi<float>(g, p, s);
@@ -356,6 +410,19 @@ extern "C" int cc_colsum(int32_t dtype, const void *X, int32_t R, int32_t N, int
   else
     hipLaunchKernelGGL(colsum_kernel<float>, grid, block, 0, as_stream(stream), (const float *)X, R, N, ld, out);
   CC_LAUNCH_CHECK("colsum_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_transpose(int32_t dtype, const void *src, int32_t rows, int32_t cols, void *dst,
+                            void *stream) {
+  CC_REQUIRE(src && dst && rows >= 0 && cols >= 0, "cc_transpose: args");
+  if (rows == 0 || cols == 0) return CC_OK;
+  const dim3 grid((unsigned)cdiv(cols, 64), (unsigned)cdiv(rows, 64)), block(256);
+  if (dtype == CC_BF16)
+    hipLaunchKernelGGL(transpose_kernel<bf16_t>, grid, block, 0, as_stream(stream), (const bf16_t *)src, rows, cols, (bf16_t *)dst);
+  else
+    hipLaunchKernelGGL(transpose_kernel<float>, grid, block, 0, as_stream(stream), (const float *)src, rows, cols, (float *)dst);
+  CC_LAUNCH_CHECK("transpose_kernel");
   return CC_OK;
 }
 

@@ -23,7 +23,9 @@ struct TowerP {
   void *wt[9];
   const float *b[9];
   void *act[7];
+  void *act6t;
   const void *gD3;
+  void *gact[5];
   float *gpre1;
   float *slab;
   int64_t slab_elems;
@@ -136,15 +138,25 @@ __global__ __launch_bounds__(NT) void tower_fwd_kernel(TowerP p) {
       tile_mm<T>(xin, ldx, Wt, K, 32 * t, acc);
       const int col = 32 * t + (lane & 31);
       const float bb = bias[col];
+      T tv[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = acc_row(r, lane);
         float v = acc[r] + bb;
         v = v > 0.f ? v : 0.f;
-        T tv;
-        DT<T>::st(&tv, v);
-        xout[row * ldx + col] = tv;
-        gout[(int64_t)(r0 + row) * N + col] = tv;
+        DT<T>::st(&tv[r], v);
+        xout[row * ldx + col] = tv[r];
+        gout[(int64_t)(r0 + row) * N + col] = tv[r];
+      }
+      if (i == 5 && p.act6t) {  // D3^T [d][R]: registers 4g..4g+3 = 4 consecutive rows
+        T *dt = reinterpret_cast<T *>(p.act6t) + (int64_t)col * p.R + r0 + 4 * (lane >> 5);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          if constexpr (sizeof(T) == 2)
+            *reinterpret_cast<uint2 *>(dt + 8 * g) = *reinterpret_cast<const uint2 *>(&tv[4 * g]);
+          else
+            *reinterpret_cast<uint4 *>(dt + 8 * g) = *reinterpret_cast<const uint4 *>(&tv[4 * g]);
+        }
       }
     }
     __syncthreads();
@@ -154,57 +166,35 @@ __global__ __launch_bounds__(NT) void tower_fwd_kernel(TowerP p) {
   }
 }
 
+// dX chain: one block per 32 rows carries dPre from d3 down to e1; every layer's dPre is written
+// to global (gact) for the dW kernel.  H (the layer input) is needed only as the ReLU mask.
 template <typename T>
-__global__ __launch_bounds__(NT) void tower_bwd_kernel(TowerP p) {
+__global__ __launch_bounds__(NT) void tower_bwd_chain_kernel(TowerP p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int MAXT = 4;  // dX tiles per wave (K <= 512)
   const int ldx = p.maxw + 16 / (int)sizeof(T);
-  const int ldt = RB + 16 / (int)sizeof(T);
-  T *Hr = reinterpret_cast<T *>(smem);
-  T *Gr = Hr + RB * ldx;
-  T *Ht = Gr + RB * ldx;
-  T *Gt = Ht + p.maxw * ldt;
+  T *Gr = reinterpret_cast<T *>(smem);
+  T *Hr = Gr + RB * ldx;
   const int blk = blockIdx.x, r0 = blk * RB;
   const bool reg = r0 >= p.B;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5;
-  float *slab = p.slab + (int64_t)blk * p.slab_elems;
-  load_block<T>(reinterpret_cast<const T *>(p.gD3), p.d, r0, Gr, ldx, Gt, ldt);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  load_block<T>(reinterpret_cast<const T *>(p.gD3), p.d, r0, Gr, ldx, (T *)nullptr, 0);
   for (int i = 5; i >= 0; --i) {
     const int l = i < 3 ? i : i + (reg ? 3 : 0);
     int K, N;
     chain_dims(p.d, i, K, N);
-    load_block<T>(reinterpret_cast<const T *>(p.act[i]), K, r0, Hr, ldx, Ht, ldt);
+    // layer input H (only its ReLU mask is needed): coalesced block copy into LDS
+    load_block<T>(reinterpret_cast<const T *>(p.act[i]), K, r0, Hr, ldx, (T *)nullptr, 0);
     __syncthreads();
-    // ---- dW partial [K][N] = H^T G over 32 rows; db partial = colsum G
-    float *sw = slab + slab_off(p.d, i);
-    const int ntn = N / 32, nt = (K / 32) * ntn;
-    for (int t = wave; t < nt; t += 4) {
-      const int k0 = 32 * (t / ntn), n0 = 32 * (t % ntn);
-      f32x16_t acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      const T *arow = Ht + (k0 + (lane & 31)) * ldt;
-      const T *brow = Gt + (n0 + (lane & 31)) * ldt;
-#pragma unroll
-      for (int kk = 0; kk < RB; kk += TMma<T>::KM)
-        TMma<T>::mma(TMma<T>::ld(arow, kk, half), TMma<T>::ld(brow, kk, half), acc);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sw[(int64_t)(k0 + acc_row(r, lane)) * N + n0 + (lane & 31)] = acc[r];
-    }
-    for (int n = threadIdx.x; n < N; n += NT) {
-      float s = 0.f;
-      for (int b = 0; b < RB; ++b) s += DT<T>::ld(&Gr[b * ldx + n]);
-      sw[(int64_t)K * N + n] = s;
-    }
-    // ---- dH[32][K] = G W^T, masked by H > 0
-    const T *W = reinterpret_cast<const T *>(p.w[l]);  // [K][N]: row k is k-contiguous over N
+    const T *W = reinterpret_cast<const T *>(p.w[l]);    // [K][N]: row k is k-contiguous over N
     f32x16_t accs[MAXT];
 #pragma unroll
     for (int q = 0; q < MAXT; ++q) {
       const int t = wave + 4 * q;
       if (t < K / 32) tile_mm<T>(Gr, ldx, W, N, 32 * t, accs[q]);
     }
-    __syncthreads();  // every wave has finished reading Gr/Gt/Ht
+    __syncthreads();  // every wave has finished reading Gr
+    T *gout = i > 0 ? reinterpret_cast<T *>(p.gact[i - 1]) : nullptr;
 #pragma unroll
     for (int q = 0; q < MAXT; ++q) {
       const int t = wave + 4 * q;
@@ -213,15 +203,62 @@ __global__ __launch_bounds__(NT) void tower_bwd_kernel(TowerP p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = acc_row(r, lane);
+        const int64_t go = (int64_t)(r0 + row) * K + col;
         const float h = DT<T>::ld(&Hr[row * ldx + col]);
         const float v = h > 0.f ? accs[q][r] : 0.f;
-        if (i == 0)
-          p.gpre1[(int64_t)(r0 + row) * K + col] = v;
-        else
-          lds_store_rows<T>(Gr, ldx, Gt, ldt, row, col, v);
+        if (i == 0) {
+          p.gpre1[go] = v;
+        } else {
+          T tv;
+          DT<T>::st(&tv, v);
+          Gr[row * ldx + col] = tv;
+          gout[go] = tv;
+        }
       }
     }
     __syncthreads();
+  }
+}
+
+// dW partials: one block per (chain layer i, 32-row block): slab[blk][i] = H^T G over the block's
+// rows (A = H^T, B = G from transposed LDS images, MFMA), db = colsum G.  Spreads the slab writes
+// over 6x more CUs than the chain.
+template <typename T>
+__global__ __launch_bounds__(NT) void tower_dw_kernel(TowerP p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int ldt = RB + 16 / (int)sizeof(T);
+  T *Ht = reinterpret_cast<T *>(smem);
+  T *Gt = Ht + p.maxw * ldt;
+  const int nb = p.R / RB;
+  const int i = blockIdx.x / nb, blk = blockIdx.x % nb, r0 = blk * RB;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5;
+  int K, N;
+  chain_dims(p.d, i, K, N);
+  const T *H = reinterpret_cast<const T *>(p.act[i]);
+  const T *G = reinterpret_cast<const T *>(i == 5 ? p.gD3 : p.gact[i]);
+  for (int e = threadIdx.x; e < RB * K; e += NT) Ht[(e % K) * ldt + e / K] = H[(int64_t)(r0 + e / K) * K + e % K];
+  for (int e = threadIdx.x; e < RB * N; e += NT) Gt[(e % N) * ldt + e / N] = G[(int64_t)(r0 + e / N) * N + e % N];
+  __syncthreads();
+  float *sw = p.slab + (int64_t)blk * p.slab_elems + slab_off(p.d, i);
+  const int ntn = N / 32, nt = (K / 32) * ntn;
+  for (int t = wave; t < nt; t += 4) {
+    const int k0 = 32 * (t / ntn), n0 = 32 * (t % ntn);
+    f32x16_t acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const T *arow = Ht + (k0 + (lane & 31)) * ldt;
+    const T *brow = Gt + (n0 + (lane & 31)) * ldt;
+#pragma unroll
+    for (int kk = 0; kk < RB; kk += TMma<T>::KM)
+      TMma<T>::mma(TMma<T>::ld(arow, kk, half), TMma<T>::ld(brow, kk, half), acc);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sw[(int64_t)(k0 + acc_row(r, lane)) * N + n0 + (lane & 31)] = acc[r];
+  }
+  for (int n = threadIdx.x; n < N; n += NT) {
+    float s = 0.f;
+    const T *g = Gt + n * ldt;
+    for (int b = 0; b < RB; ++b) s += DT<T>::ld(&g[b]);
+    sw[(int64_t)K * N + n] = s;
   }
 }
 
@@ -293,7 +330,9 @@ int make_params(const cc_tower_args *t, TowerP &p) {
     p.gb[l] = t->gb[l];
   }
   for (int a = 0; a < 7; ++a) p.act[a] = t->act[a];
+  p.act6t = t->act6t;
   p.gD3 = t->gD3;
+  for (int a = 0; a < 5; ++a) p.gact[a] = t->gact[a];
   p.gpre1 = t->gpre1;
   p.slab = t->slab;
   p.slab_elems = slab_off(t->d, 6);
@@ -323,14 +362,19 @@ extern "C" int cc_tower_bwd(const cc_tower_args *t, void *stream) {
   int rc = make_params(t, p);
   if (rc) return rc;
   CC_REQUIRE(t->gD3 && t->gpre1 && t->slab, "cc_tower_bwd: null gD3/gpre1/slab");
+  for (int a = 0; a < 5; ++a) CC_REQUIRE(t->gact[a], "cc_tower_bwd: null gact");
   const int es = t->dtype == CC_BF16 ? 2 : 4;
-  const size_t lds = (size_t)(2 * RB * (p.maxw + 16 / es) + 2 * p.maxw * (RB + 16 / es)) * es;
-  CC_REQUIRE(lds <= 160 * 1024, "cc_tower_bwd: LDS");
-  if (t->dtype == CC_BF16)
-    hipLaunchKernelGGL(tower_bwd_kernel<bf16_t>, dim3(p.R / RB), dim3(NT), lds, as_stream(stream), p);
-  else
-    hipLaunchKernelGGL(tower_bwd_kernel<float>, dim3(p.R / RB), dim3(NT), lds, as_stream(stream), p);
-  CC_LAUNCH_CHECK("tower_bwd_kernel");
+  const size_t lds_chain = (size_t)2 * RB * (p.maxw + 16 / es) * es;
+  const size_t lds_dw = (size_t)2 * p.maxw * (RB + 16 / es) * es;
+  const dim3 gc(p.R / RB), gd(6 * (p.R / RB));
+  if (t->dtype == CC_BF16) {
+    hipLaunchKernelGGL(tower_bwd_chain_kernel<bf16_t>, gc, dim3(NT), lds_chain, as_stream(stream), p);
+    hipLaunchKernelGGL(tower_dw_kernel<bf16_t>, gd, dim3(NT), lds_dw, as_stream(stream), p);
+  } else {
+    hipLaunchKernelGGL(tower_bwd_chain_kernel<float>, gc, dim3(NT), lds_chain, as_stream(stream), p);
+    hipLaunchKernelGGL(tower_dw_kernel<float>, gd, dim3(NT), lds_dw, as_stream(stream), p);
+  }
+  CC_LAUNCH_CHECK("tower_bwd kernels");
   return CC_OK;
 }
 

@@ -75,6 +75,10 @@ class DeviceDataset:
             self.y_reg = y.to(device=device, dtype=torch.float32).contiguous()
 
 
+def branches_of(use_reg):
+    return ('decoder', 'decoder_for_reg') if use_reg else ('decoder',)
+
+
 def _neg_sampler(y_mtx):
     """generator.py:30: neg_sampler = M~.sum(0) / M~.sum() (float64)."""
     if torch.is_tensor(y_mtx):
@@ -156,6 +160,10 @@ class Trainer:
             self.wt = torch.zeros(int(self.wt_off[-1]), **T)
             slab = int(L.lib().cc_tower_slab_elems(d))
             self.slab = torch.zeros((R // 32) * slab, **f32)
+            # decoder operands kept k-contiguous: D3^T (tower fwd), dZ^T (BCE epilogue), Wo^T shadow
+            self.D3t = torch.zeros(d, R, **T)
+            self.dZt = torch.zeros(V, B, **T)
+            self.WoT = torch.zeros(len(branches_of(self.use_reg)), V, d, **T)
             self.targs = self._tower_args()
             self.transpose_tower()
         else:
@@ -207,14 +215,22 @@ class Trainer:
             t.gb[l] = self.grads[self.layout.offset(name + '/bias'):].data_ptr()
         for a, buf in enumerate((self.H1, self.H2, self.H3, self.Zl, self.D1, self.D2, self.D3)):
             t.act[a] = buf.data_ptr()
+        t.act6t = self.D3t.data_ptr()
         t.gD3 = self.gD3.data_ptr()
+        for a, buf in enumerate((self.gH2, self.gH3, self.gZl, self.gD1, self.gD2)):
+            t.gact[a] = buf.data_ptr()      # dPre of e2, e3, e4, d1, d2
         t.gpre1 = self.gPre1.data_ptr()
         t.slab = self.slab.data_ptr()
         return t
 
     def transpose_tower(self, stream=None):
+        """Refresh the transposed operand copies (tower W^T, decoder Wo^T) from the current weights."""
         if self.fused_tower:
-            L.call('cc_tower_transpose', L.C.byref(self.targs), L.stream_ptr(stream))
+            s = L.stream_ptr(stream)
+            L.call('cc_tower_transpose', L.C.byref(self.targs), s)
+            for k, pre in enumerate(branches_of(self.use_reg)):
+                L.call('cc_transpose', self.dtype, self.w(pre + '/reconstruct/kernel'), self.cfg.d, self.cfg.V,
+                       L.ptr(self.WoT[k]), s)
 
     def refresh_shadow(self):
         """Re-derive the bf16 shadow (and the transposed tower operands) from the fp32 master."""
@@ -240,11 +256,11 @@ class Trainer:
 
     def _gemm(self, M, N, K, A, lda, B, ldb, ta=0, tb=0, epi=L.CC_EPI_STORE, ldc=None, bias=None,
               relu=0, C=None, Cf=None, H=None, y_bits=None, scale=0.0, partials=None, splits=1,
-              colsum=None):
+              colsum=None, Ct=None, ldct=0):
         g = L.GemmArgs(dtype=self.dtype, ta=ta, tb=tb, epilogue=epi, M=M, N=N, K=K, lda=lda,
                        ldb=ldb, ldc=ldc if ldc is not None else N, splits=splits, relu=relu,
                        A=A, B=B, bias=bias, C=C, Cf=Cf, H=H, y_bits=y_bits, scale=scale,
-                       loss_partials=partials, colsum=colsum)
+                       loss_partials=partials, colsum=colsum, Ct=Ct, ldct=ldct)
         L.call('cc_gemm', L.C.byref(g), self._s)
 
     def _dense_fwd(self, X, rows, K, N, name, out):
@@ -315,16 +331,26 @@ class Trainer:
                 self._dense_fwd(self.D2, rows, 256, d, pre + '/decoded_3', self.D3)
         # ---- D1 output + sigmoid + BCE -> dZ (model.py:64,94; train.py:85)
         t = self._tick('dec_bce_fwd')
-        self._gemm(B, V, d, L.ptr(self.D3), d, self.w('decoder/reconstruct/kernel'), V,
-                   epi=L.CC_EPI_BCE, bias=self.pf('decoder/reconstruct/bias'), C=L.ptr(self.dZout),
-                   y_bits=L.ptr(self.y_bits), scale=1.0 / (B * V), partials=L.ptr(self.bce_part))
+        if self.fused_tower:   # Wo^T [V][d]: k-contiguous B operand; also writes dZ^T [V][B]
+            self._gemm(B, V, d, L.ptr(self.D3), d, L.ptr(self.WoT[0]), d, tb=1,
+                       epi=L.CC_EPI_BCE, bias=self.pf('decoder/reconstruct/bias'), C=L.ptr(self.dZout),
+                       y_bits=L.ptr(self.y_bits), scale=1.0 / (B * V), partials=L.ptr(self.bce_part),
+                       Ct=L.ptr(self.dZt), ldct=B)
+        else:
+            self._gemm(B, V, d, L.ptr(self.D3), d, self.w('decoder/reconstruct/kernel'), V,
+                       epi=L.CC_EPI_BCE, bias=self.pf('decoder/reconstruct/bias'), C=L.ptr(self.dZout),
+                       y_bits=L.ptr(self.y_bits), scale=1.0 / (B * V), partials=L.ptr(self.bce_part))
         t()
         L.call('cc_reduce_loss', L.ptr(self.bce_part), self.bce_part.numel(), 1.0 / (B * V),
                L.ptr(self.loss_dev), s)
         # ---- D2 output + softmax + KL vs M~ rows (model.py:98; train.py:85)
         if self.use_reg:
-            self._gemm(B, V, d, L.ptr(self.D3[B:]), d, self.w('decoder_for_reg/reconstruct/kernel'), V,
-                       bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2))
+            if self.fused_tower:
+                self._gemm(B, V, d, L.ptr(self.D3[B:]), d, L.ptr(self.WoT[1]), d, tb=1,
+                           bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2))
+            else:
+                self._gemm(B, V, d, L.ptr(self.D3[B:]), d, self.w('decoder_for_reg/reconstruct/kernel'), V,
+                           bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2))
             L.call('cc_dec_softmax_kl_fused', self.dtype, L.ptr(self.Z2), B, V, L.ptr(self.data.y_reg),
                    L.ptr(self.reg_idx), float(cfg.reg), L.ptr(self.dZout[B:]), L.ptr(self.kl_part), s)
             L.call('cc_reduce_loss', L.ptr(self.kl_part), B, 1.0 / B, L.ptr(self.loss_dev[1:]), s)
@@ -332,8 +358,12 @@ class Trainer:
         for pre, (r0, r1) in branches:
             dz = self.dZout[r0:]
             t = self._tick('dec_dW')
-            self._gemm(d, V, B, L.ptr(self.D3[r0:]), d, L.ptr(dz), V, ta=1, tb=0,
-                       Cf=self.gp(pre + '/reconstruct/kernel'), colsum=self.gp(pre + '/reconstruct/bias'))
+            if self.fused_tower and r0 == 0:   # dW = D3^T dZ with both operands k-contiguous
+                self._gemm(d, V, B, L.ptr(self.D3t), R, L.ptr(self.dZt), B, ta=0, tb=1,
+                           Cf=self.gp(pre + '/reconstruct/kernel'), colsum=self.gp(pre + '/reconstruct/bias'))
+            else:
+                self._gemm(d, V, B, L.ptr(self.D3[r0:]), d, L.ptr(dz), V, ta=1, tb=0,
+                           Cf=self.gp(pre + '/reconstruct/kernel'), colsum=self.gp(pre + '/reconstruct/bias'))
             t()
             t = self._tick('dec_dX')
             self._gemm(B, d, V, L.ptr(dz), V, self.w(pre + '/reconstruct/kernel'), V, ta=0, tb=1,
@@ -361,30 +391,39 @@ class Trainer:
                self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
         t()
 
-    def apply(self, stream=None):
+    def apply_adam(self, stream=None):
+        """TF Adam over every trained parameter (+ bf16 shadow refresh)."""
         cfg = self.cfg
-        s = L.stream_ptr(stream)
         n = self.layout.total if self.use_reg else self.layout.main_total
         t = self._tick('cc_adam_dense')
         L.call('cc_adam_dense', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v), L.ptr(self.grads),
-               L.ptr(self.shadow), n, L.ptr(self.state), cfg.lr, cfg.beta1, cfg.beta2, cfg.eps, s)
+               L.ptr(self.shadow), n, L.ptr(self.state), cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,
+               L.stream_ptr(stream))
         t()
-        L.call('cc_state_advance', L.ptr(self.state), self.batches_per_epoch, s)
+
+    def apply_rest(self, stream=None):
+        """Advance the device step/epoch counters and refresh the transposed operand copies."""
+        L.call('cc_state_advance', L.ptr(self.state), self.batches_per_epoch, L.stream_ptr(stream))
         self.transpose_tower(stream)
+
+    def apply(self, stream=None):
+        self.apply_adam(stream)
+        self.apply_rest(stream)
 
     def step(self, stream=None):
         if self.graphs is not None:
-            self.graphs[0].replay()
-            self.graphs[1].replay()
+            for g in self.graphs:
+                g.replay()
             return
         self.forward_backward(stream)
         self.apply(stream)
 
     def capture(self):
-        """Capture forward_backward and apply as two hipGraphs (torch.cuda.CUDAGraph over our
-        own kernel launches): one graph launch per phase instead of ~40 host launches.  Every
-        buffer is preallocated and the step/epoch counters are device-resident, so replays are
-        exact repeats of the eager step (the data-parallel all-reduce runs between the two)."""
+        """Capture the step as three hipGraphs (torch.cuda.CUDAGraph over our own kernel launches):
+        forward_backward | Adam | counters+transposes.  Every buffer is preallocated and the
+        step/epoch counters are device-resident, so replays are exact repeats of the eager step.
+        The data-parallel all-reduce runs between the first two; bench.py brackets the Adam graph
+        with HIP events to time the step's bytes-dominant kernel inside the timed region."""
         timing, self.timing = self.timing, False
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream())
@@ -393,14 +432,16 @@ class Trainer:
             self.forward_backward()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        g_fb, g_ap = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        g_fb, g_adam, g_rest = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_fb):
             self.forward_backward()
-        with torch.cuda.graph(g_ap):
-            self.apply()
+        with torch.cuda.graph(g_adam):
+            self.apply_adam()
+        with torch.cuda.graph(g_rest):
+            self.apply_rest()
         torch.cuda.synchronize()
         self.state.copy_(saved)
-        self.graphs = (g_fb, g_ap)
+        self.graphs = (g_fb, g_adam, g_rest)
         self.timing = timing
 
     # ------------------------------------------------------------------ inspection (tests)

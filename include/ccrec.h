@@ -139,6 +139,9 @@ typedef struct cc_gemm_args {
   float *colsum;        /* optional [N] ([splits, N] with CC_EPI_SPLITK): colsum[n] = sum_k op(B)[k, n]
                            (fp32, ascending k) — the bias gradient of a Dense layer fused into its
                            dW = X^T dPre product */
+  void *Ct;             /* CC_EPI_BCE, optional: dZ^T [N][ldct] (dtype) — the k-contiguous operand of
+                           dW = H^T dZ, written with packed stores from the accumulator registers */
+  int32_t ldct;
 } cc_gemm_args;
 int cc_gemm(const cc_gemm_args *g, void *stream);
 /* workspace bound for cc_gemm's loss partials: ceil(M/64)*ceil(N/64) doubles */
@@ -150,6 +153,9 @@ int cc_splitk_reduce(int32_t dtype, const float *partials, int32_t splits, int32
                      const void *H, void *C, float *Cf, const float *colsum_partials,
                      float *colsum_out, void *stream);
 
+/* dst[c][r] = src[r][c] for a [rows, cols] row-major matrix (dtype elements). */
+int cc_transpose(int32_t dtype, const void *src, int32_t rows, int32_t cols, void *dst, void *stream);
+
 /* out[n] (+)= sum_r X[r, n] (fp32 accumulate, ascending r). db of every Dense layer. */
 int cc_colsum(int32_t dtype, const void *X, int32_t R, int32_t N, int32_t ld, float *out,
               void *stream);
@@ -159,8 +165,9 @@ int cc_colsum(int32_t dtype, const void *X, int32_t R, int32_t N, int32_t ld, fl
  * Rows [0,B) use `decoder`, rows [B,R) `decoder_for_reg`; one block never straddles B.
  * Layer order l = 0..8: e2, e3, e4 | d1, d2, d3 (decoder) | d1, d2, d3 (decoder_for_reg).
  *   cc_tower_fwd: act[0] = H1 (input) -> act[1..6] = H2, H3, Zl, D1, D2, D3 (bias+ReLU fused).
- *   cc_tower_bwd: from gD3 = dPre of d3 [R,d] down to gpre1 = dPre of e1 [R,d] fp32, with the
- *                 per-block partial dW/db of all 6 layers a block touches in slab[blk][...].
+ *   cc_tower_bwd: from gD3 = dPre of d3 [R,d] down to gpre1 = dPre of e1 [R,d] fp32 (the dX
+ *                 chain, writing every layer's dPre to gact), then the per-(layer, 32-row block)
+ *                 partial dW/db of the 6 layers each block touches into slab[blk][...].
  *   cc_tower_reduce: grads of the 9 layers = sum of the slabs in block order (deterministic).
  *   cc_tower_transpose: wt[l] = w[l]^T ([N][K]) — the k-contiguous operand the forward reads.
  * d <= 512 (bf16) / <= 256 (fp32); the generic cc_gemm path covers larger widths.
@@ -171,7 +178,9 @@ typedef struct cc_tower_args {
   void *wt[9];           /* [N][K] dtype */
   const float *b[9];     /* [N] */
   void *act[7];          /* H1, H2, H3, Zl, D1, D2, D3: [R, width] dtype */
+  void *act6t;           /* optional: D3^T [d][R] dtype (k-contiguous operand of the decoder dW) */
   const void *gD3;       /* [R, d] dtype */
+  void *gact[5];         /* bwd outputs, dPre of e2, e3, e4, d1, d2: [R, N_l] dtype */
   float *gpre1;          /* [R, d] fp32 */
   float *slab;           /* [R/32, cc_tower_slab_elems(d)] fp32 */
   float *gw[9];          /* reduce outputs: kernel grads [K][N] */

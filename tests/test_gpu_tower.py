@@ -30,6 +30,7 @@ def test_tower_fwd_bwd_vs_numpy(dtype, d, B, R):
     widths = [d, 256, 128, 64, 128, 256, d]
     act = [rnd(R, widths[0])] + [torch.zeros(R, w, device='cuda', dtype=tdt) for w in widths[1:]]
     gD3 = rnd(R, d)
+    gact = [torch.zeros(R, w, device='cuda', dtype=tdt) for w in (256, 128, 64, 128, 256)]
     gpre1 = torch.zeros(R, d, device='cuda')
     slab = torch.zeros((R // 32) * int(L.lib().cc_tower_slab_elems(d)), device='cuda')
     gw = [torch.zeros(w.shape, device='cuda') for w in W]
@@ -41,6 +42,8 @@ def test_tower_fwd_bwd_vs_numpy(dtype, d, B, R):
     for a in range(7):
         t.act[a] = act[a].data_ptr()
     t.gD3, t.gpre1, t.slab = gD3.data_ptr(), gpre1.data_ptr(), slab.data_ptr()
+    for a in range(5):
+        t.gact[a] = gact[a].data_ptr()
     s = L.stream_ptr()
     for fn in ('cc_tower_transpose', 'cc_tower_fwd', 'cc_tower_bwd', 'cc_tower_reduce'):
         L.call(fn, ctypes.byref(t), s)
