@@ -32,7 +32,7 @@ def parse():
     ap.add_argument('--reg', type=float, default=0.0)
     ap.add_argument('--dtype', default='bf16')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-steps', type=int, default=3)
+    ap.add_argument('--cpu-steps', type=int, default=16)
     ap.add_argument('--no-recommend', action='store_true')
     ap.add_argument('--traffic-json', default=os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                            'profiles', 'traffic_r01.json'))

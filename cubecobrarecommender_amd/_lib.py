@@ -57,6 +57,7 @@ SIGNATURES = {
     'cc_abi_version': (C.c_int, []),
     'cc_last_error_string': (C.c_char_p, []),
     'cc_param_layout': (C.c_int, [_I32, _I32, _P, _P, _P, _P]),
+    'cc_crc32c': (C.c_uint32, [C.c_uint32, _P, _SZ]),
     'cc_noise_fwd': (C.c_int, [C.POINTER(NoiseArgs), _P]),
     'cc_embed_gather_fwd': (C.c_int, [_I32, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P]),
     'cc_embed_scatter_bwd': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),

@@ -1,0 +1,56 @@
+"""Data parallelism over the GPUs of one node: one process per GPU,
+torch.distributed with backend "nccl" (= RCCL over xGMI on ROCm), gloo for CPU tests.
+
+Each rank takes its own B cubes of every global batch (disjoint slices of the shared epoch
+permutation: cubes perm[g*B*W + r*B : g*B*W + (r+1)*B]) and draws F and its B regulariser rows with
+Philox slots r*B..r*B+B-1, so the W ranks together process exactly the batch a single process with
+batch W*B would (tests/test_gpu_train.py::test_data_parallel_equivalence).  The only exchange is the
+all-reduce (average) of the fp32 gradient buffer before Adam; every rank then applies the same
+update, so weights stay replicated.  M~ is replicated (1.9 GB at |V|=22k fits every GPU); the
+row-sharded KL of §8(e) is a later-round optimisation."""
+import os
+
+import numpy as np
+import torch
+
+
+def init(backend=None):
+    """Read RANK/LOCAL_RANK/WORLD_SIZE; init the process group when WORLD_SIZE > 1.
+    Returns (world, rank, device)."""
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    cuda = torch.cuda.is_available()
+    dev = torch.device('cuda', local) if cuda else torch.device('cpu')
+    if cuda:
+        torch.cuda.set_device(dev)
+    if world > 1 and not torch.distributed.is_initialized():
+        backend = backend or ('nccl' if cuda else 'gloo')
+        kw = {'device_id': dev} if backend == 'nccl' else {}
+        torch.distributed.init_process_group(backend, **kw)
+    return world, rank, dev
+
+
+def finish():
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        torch.distributed.destroy_process_group()
+
+
+def rank_cubes(perm, batch_in_epoch, B, rank, world):
+    """Host mirror of the cube selection in cc_noise_fwd: this rank's cube ids for a global batch."""
+    base = batch_in_epoch * B * world + rank * B
+    return np.asarray(perm)[base:base + B]
+
+
+def allreduce_grads(grads, n=None, world=None):
+    """Average the first n gradient entries over ranks (gradient of the mean loss over W*B cubes)."""
+    world = world or (torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1)
+    if world == 1:
+        return grads
+    g = grads[:n] if n is not None else grads
+    if g.is_cuda:
+        torch.distributed.all_reduce(g, op=torch.distributed.ReduceOp.AVG)
+    else:  # gloo has no AVG
+        torch.distributed.all_reduce(g, op=torch.distributed.ReduceOp.SUM)
+        g.div_(world)
+    return grads

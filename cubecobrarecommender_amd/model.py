@@ -1,0 +1,182 @@
+"""Keras-shaped host mirror of ``src/ml/model.py`` / ``src/ml/train.py`` over the HIP hot path.
+
+    model = CC_Recommender(num_cards)                                   # model.py:89-98
+    model.compile(optimizer='adam', loss=['binary_crossentropy', 'kullback_leibler_divergence'],
+                  loss_weights=[1.0, reg], metrics=['accuracy'])        # train.py:83-88
+    model.fit(generator, epochs=epochs)                                # train.py:99-102
+    model.save(dest, save_format='tf')                                  # train.py:112-115
+    model = load_model(dest)                                            # ml_recommend.py:54
+    model.decoder(model.encoder(x)).numpy()                             # ml_recommend.py:78-85
+
+encoder/decoder run the fp32 pinned-order inference kernels (bit-exact vs oracle/infer_ref.py);
+fit runs the device-resident training step (trainer.py) with TF Adam semantics.  There is no CPU
+fallback: every compute call goes through libccrec_hip.so.
+"""
+import time
+
+import numpy as np
+import torch
+
+from . import checkpoint
+from .layout import Layout, glorot_flat
+from .recommender import Recommender
+
+_LOSSES = ('binary_crossentropy', 'kullback_leibler_divergence')
+
+
+class Tensor:
+    """What model.encoder(...) returns: supports .numpy() like a TF EagerTensor."""
+
+    def __init__(self, t):
+        self._t = t
+
+    def numpy(self):
+        return self._t.detach().cpu().numpy()
+
+    def __array__(self, dtype=None):
+        a = self.numpy()
+        return a.astype(dtype) if dtype is not None else a
+
+    def __getitem__(self, i):
+        return Tensor(self._t[i])
+
+    @property
+    def shape(self):
+        return tuple(self._t.shape)
+
+
+def _rows_of(x):
+    """Dense 0/1 input [R, V] (numpy/torch/Tensor) or a list of index lists -> list of index arrays."""
+    if isinstance(x, Tensor):
+        x = x.numpy()
+    if isinstance(x, (list, tuple)) and (len(x) == 0 or not np.isscalar(x[0])):
+        return [np.asarray(r, np.int64) for r in x]
+    a = x.detach().cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
+    if a.ndim == 1:
+        a = a[None, :]
+    return [np.nonzero(r == 1)[0] for r in a]
+
+
+class _Encoder:
+    def __init__(self, model):
+        self.m = model
+
+    def __call__(self, x, training=None):
+        return Tensor(self.m._rec().encode_lists(_rows_of(x)))
+
+
+class _Decoder:
+    def __init__(self, model):
+        self.m = model
+
+    def __call__(self, z, training=None):
+        zt = z._t if isinstance(z, Tensor) else torch.as_tensor(np.asarray(z, np.float32))
+        return Tensor(self.m._rec().decode(zt))
+
+
+class CC_Recommender:
+    def __init__(self, num_cards, d=512, dtype='bf16', seed=0, params_flat=None):
+        self.N = int(num_cards)
+        self.d = int(d)
+        self.dtype = dtype
+        self.seed = seed
+        self.layout = Layout(self.N, self.d)
+        self._flat = params_flat if params_flat is not None else glorot_flat(self.N, self.d, seed)
+        self._m = self._v = None
+        self._step = 0
+        self.reg = 0.0
+        self.lr = 1e-3
+        self.trainer = None
+        self._recommender = None
+        self.encoder = _Encoder(self)
+        self.decoder = _Decoder(self)
+        self.history = []
+
+    # --------------------------------------------------------------- Keras surface
+    def compile(self, optimizer='adam', loss=_LOSSES, loss_weights=(1.0, 0.0), metrics=None,
+                learning_rate=1e-3):
+        if optimizer != 'adam':
+            raise ValueError("only optimizer='adam' (train.py:84) is implemented")
+        if tuple(loss) != _LOSSES:
+            raise ValueError(f'loss must be {list(_LOSSES)} (train.py:85)')
+        if float(loss_weights[0]) != 1.0:
+            raise ValueError('loss_weights[0] must be 1.0 (train.py:86)')
+        self.reg = float(loss_weights[1])
+        self.lr = float(learning_rate)
+
+    def fit(self, generator, epochs=1, verbose=1, rank=0, world=1, graphs=True, log=print):
+        from .trainer import TrainConfig, Trainer
+        cfg = TrainConfig(V=self.N, d=self.d, batch_size=generator.batch_size, reg=self.reg,
+                          noise=generator.noise, noise_std=generator.noise_std, lr=self.lr,
+                          dtype=self.dtype, seed=self.seed, rank=rank, world=world)
+        tr = Trainer(cfg, generator.data, params_flat=self._current_flat())
+        if self._m is not None:
+            tr.m.copy_(torch.from_numpy(self._m))
+            tr.v.copy_(torch.from_numpy(self._v))
+            tr.state[0] = self._step
+        tr.set_epoch_permutations(generator.epoch_permutations(epochs))
+        steps = tr.batches_per_epoch
+        if graphs:
+            tr.capture()
+        for ep in range(epochs):
+            t0 = time.perf_counter()
+            acc = 0.0
+            for _ in range(steps):
+                if world > 1:
+                    import torch.distributed as dist
+                    tr.forward_backward()
+                    n = tr.layout.total if tr.use_reg else tr.layout.main_total
+                    dist.all_reduce(tr.grads[:n], op=dist.ReduceOp.AVG)
+                    tr.apply()
+                else:
+                    tr.step()
+            torch.cuda.synchronize()
+            l = tr.losses()
+            self.history.append(l)
+            if verbose and rank == 0:
+                dt = time.perf_counter() - t0
+                log(f'Epoch {ep + 1}/{epochs} - {steps} steps - {dt:.3f}s - loss: {l["loss"]:.6f} '
+                    f'- bce: {l["bce"]:.6f} - kl: {l["kl"]:.6f} - {steps * cfg.batch_size * world / dt:.0f} cubes/s')
+
+        self.trainer = tr
+        self._recommender = None
+        self._step = int(tr.state[0].item())
+        return self
+
+    def save(self, dest, save_format='tf'):
+        lay = self.layout
+        P = lay.unpack(self._current_flat())
+        if self.trainer is not None:
+            m = lay.unpack(self.trainer.m.cpu().numpy())
+            v = lay.unpack(self.trainer.v.cpu().numpy())
+        elif self._m is not None:
+            m, v = lay.unpack(self._m), lay.unpack(self._v)
+        else:
+            m = v = None
+        checkpoint.save_model(dest, self.N, self.d, P, m, v, step=self._step, lr=self.lr)
+
+    # --------------------------------------------------------------- internals
+    def _current_flat(self):
+        if self.trainer is not None:
+            return self.trainer.params.cpu().numpy()
+        return np.asarray(self._flat, np.float32)
+
+    def _rec(self):
+        if self._recommender is None:
+            self._recommender = Recommender(self._current_flat(), self.N, self.d)
+        return self._recommender
+
+    def recommender(self):
+        """The resident single-cube recommend engine (fp32 forward + GPU top-N)."""
+        return self._rec()
+
+
+def load_model(path, dtype='bf16'):
+    """keras.models.load_model('ml_files/<name>') (ml_recommend.py:54, ml_recommend_web.py:37)."""
+    V, d, params, m, v, step = checkpoint.load_variables(path)
+    lay = Layout(V, d)
+    model = CC_Recommender(V, d=d, dtype=dtype, params_flat=lay.pack(params))
+    if m is not None and v is not None:
+        model._m, model._v = lay.pack(m), lay.pack(v)
+    model._step = step
+    return model

@@ -254,6 +254,20 @@ class Trainer:
         self.perms.copy_(p)
         self.state[1:3].zero_()
 
+    def _noise_args(self):
+        cfg, V, B = self.cfg, self.cfg.V, self.cfg.batch_size
+        return L.NoiseArgs(V=V, B=B, x_cap=self.x_cap, with_reg=int(self.use_reg), seed=cfg.seed,
+                           slot_base=cfg.rank * B, batch_stride=B * cfg.world, batch_offset=cfg.rank * B,
+                           noise_mean=cfg.noise, noise_std=cfg.noise_std,
+                           cube_ptr=self.data.cube_ptr.data_ptr(), cube_idx=self.data.cube_idx.data_ptr(),
+                           num_perms=self.perms.shape[0], num_cubes=self.data.C,
+                           perm=self.perms.data_ptr(), cdf=self.data.cdf.data_ptr(),
+                           neg_sampler=self.data.neg_sampler.data_ptr(), guide=self.data.guide.data_ptr(),
+                           guide_log2=self.data.guide_log2, state=self.state.data_ptr(),
+                           x_cnt=self.x_cnt.data_ptr(), x_idx=self.x_idx.data_ptr(),
+                           y_bits=self.y_bits.data_ptr(), xt_bits=self.xt_bits.data_ptr(),
+                           reg_idx=self.reg_idx.data_ptr(), status=self.status.data_ptr())
+
     def _gemm(self, M, N, K, A, lda, B, ldb, ta=0, tb=0, epi=L.CC_EPI_STORE, ldc=None, bias=None,
               relu=0, C=None, Cf=None, H=None, y_bits=None, scale=0.0, partials=None, splits=1,
               colsum=None, Ct=None, ldct=0):
@@ -296,17 +310,7 @@ class Trainer:
         s = self._s
         # ---- F: noise + reg rows (generator.py:38-103)
         self.xt_bits.zero_()
-        na = L.NoiseArgs(V=V, B=B, x_cap=self.x_cap, with_reg=int(self.use_reg), seed=cfg.seed,
-                         slot_base=cfg.rank * B, batch_stride=B * cfg.world, batch_offset=cfg.rank * B,
-                         noise_mean=cfg.noise, noise_std=cfg.noise_std,
-                         cube_ptr=self.data.cube_ptr.data_ptr(), cube_idx=self.data.cube_idx.data_ptr(),
-                         num_perms=self.perms.shape[0], num_cubes=self.data.C,
-                         perm=self.perms.data_ptr(), cdf=self.data.cdf.data_ptr(),
-                         neg_sampler=self.data.neg_sampler.data_ptr(), guide=self.data.guide.data_ptr(),
-                         guide_log2=self.data.guide_log2, state=self.state.data_ptr(),
-                         x_cnt=self.x_cnt.data_ptr(), x_idx=self.x_idx.data_ptr(),
-                         y_bits=self.y_bits.data_ptr(), xt_bits=self.xt_bits.data_ptr(),
-                         reg_idx=self.reg_idx.data_ptr(), status=self.status.data_ptr())
+        na = self._noise_args()
         t = self._tick('cc_noise_fwd')
         L.call('cc_noise_fwd', L.C.byref(na), s)
         t()

@@ -46,6 +46,10 @@ enum cc_dtype { CC_F32 = 0, CC_BF16 = 1 };
 int cc_abi_version(void);
 const char *cc_last_error_string(void);
 
+/* Host utility: CRC32C (Castagnoli) of [data, data+n) continuing from crc (0 to start) — the
+ * checksum of TF tensor-bundle checkpoints (ml_files/<name>/variables). */
+uint32_t cc_crc32c(uint32_t crc, const void *data, size_t n);
+
 /* ----------------------------------------------------------------------------------
  * Parameter layout.  All weights live in ONE flat fp32 buffer (Adam m/v and the bf16
  * shadow use the same offsets).  Tensor order = Keras creation order (model.py:27-33,

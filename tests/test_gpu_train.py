@@ -116,3 +116,43 @@ def test_graph_replay_matches_eager_and_epochs_roll_over():
         assert all(np.array_equal(a, b) for a, b in zip(xs[:B], oxs))
     assert torch.equal(tr_e.params, tr_g.params)
     assert tr_g.state.cpu().tolist()[:3] == [6, 2, 1]
+
+
+@pytest.mark.parametrize('reg', [0.0, 0.1])
+def test_data_parallel_equivalence(reg):
+    """W ranks of batch B == one process of batch W*B: same cubes, same F draws (Philox slots),
+    averaged gradients equal the single-process gradients (the all-reduce is the only exchange)."""
+    V, d, B, C, W = 700, 64, 32, 256, 2
+    lists, Mt, ns = problem(3, C, V, (20, 40, 80))
+    P = model_ref.init_params(V, d, seed=3, bias_std=0.01)
+    lay = Layout(V, d)
+    perms = np.random.default_rng(4).permutation(C)[None, :]
+
+    def make(b, rank, world):
+        cfg = TrainConfig(V=V, d=d, batch_size=b, reg=reg, dtype='fp32', seed=3, rank=rank, world=world)
+        data = DeviceDataset(lists, V, y_mtx=Mt.astype(np.float32) if reg else None, neg_sampler=ns)
+        tr = Trainer(cfg, data, params_flat=lay.pack(P))
+        tr.set_epoch_permutations(perms)
+        return tr
+
+    single = make(W * B, 0, 1)
+    ranks = [make(B, r, W) for r in range(W)]
+    for step in range(2):
+        single.forward_backward()
+        for t in ranks:
+            t.forward_backward()
+        torch.cuda.synchronize()
+        xs, _, _ = single.batch_lists()
+        got = [t.batch_lists()[0][:B] for t in ranks]
+        assert all(np.array_equal(a, b) for a, b in zip(xs[:W * B], got[0] + got[1]))
+        avg = (ranks[0].grads + ranks[1].grads) / W
+        n = lay.total if reg else lay.main_total
+        assert rel_err(avg[:n].cpu().numpy(), single.grads[:n].cpu().numpy()) < 1e-5
+        lw = [t.losses()['loss'] for t in ranks]
+        assert abs(np.mean(lw) - single.losses()['loss']) / single.losses()['loss'] < 1e-6
+        for t in ranks:          # every rank applies the same averaged update
+            t.grads.copy_(avg)
+            t.apply()
+        single.apply()
+        torch.cuda.synchronize()
+        assert rel_err(ranks[0].params.cpu().numpy(), single.params.cpu().numpy()) < 1e-5
