@@ -72,7 +72,8 @@ SIGNATURES = {
     'cc_adam_dense': (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _F32, _F32, _F32, _F32, _P]),
     'cc_to_bf16': (C.c_int, [_P, _P, _I64, _P]),
     'cc_state_advance': (C.c_int, [_P, _I64, _P]),
-    'cc_infer_encode_fp32': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
+    'cc_infer_encode_ws_size': (_SZ, [_I32, _I32, _I32]),
+    'cc_infer_encode_fp32': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _P]),
     'cc_infer_decode_fp32': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_tower_slab_elems': (_I64, [_I32]),
     'cc_tower_fwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
@@ -81,6 +82,11 @@ SIGNATURES = {
     'cc_tower_transpose': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_topn_workspace_size': (_SZ, [_I32]),
     'cc_topn': (C.c_int, [_P, _I32, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
+    'cc_recommend_ws_size': (_SZ, [_I32, _I32]),
+    'cc_recommend_fp32': (C.c_int, [_P, _I32, _I32, _P, _I32, _P, _P, _P, _P]),
+    'cc_recommend_graph_create': (C.c_int, [_P, _I32, _I32, _P, _P, _I32, _P, _P, _P, C.POINTER(C.c_void_p)]),
+    'cc_recommend_graph_run': (C.c_int, [_P, _P, _I32]),
+    'cc_recommend_graph_destroy': (C.c_int, [_P]),
 }
 
 _lib = None

@@ -43,8 +43,13 @@ def _compile(src, force):
 
 def build(force=False, jobs=8):
     os.makedirs(OBJ, exist_ok=True)
-    with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), sources()))
+    try:
+        with cf.ThreadPoolExecutor(jobs) as ex:
+            objs = list(ex.map(lambda s: _compile(s, force), sources()))
+    except RuntimeError:
+        if os.path.exists(LIB):
+            os.remove(LIB)        # never leave a stale library behind a failed build
+        raise
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
         cmd = [HIPCC, '-shared', '-fPIC', f'--offload-arch={ARCH}', *objs, '-o', LIB]
         r = subprocess.run(cmd, capture_output=True, text=True)

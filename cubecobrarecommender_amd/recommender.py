@@ -14,6 +14,8 @@ import torch
 from . import _lib as L
 from .layout import Layout
 
+GRAPH_MAX_IDS = 4096   # cube ids per request the captured graph's H2D carries
+
 
 class Recommender:
     def __init__(self, params_flat, V, d, device='cuda'):
@@ -26,26 +28,38 @@ class Recommender:
         assert self.params.numel() >= self.layout.main_total
         self.stream = torch.cuda.Stream(device=self.dev)
         self.lock = threading.Lock()
-        self._alloc(1)
-        self.topn_ws = torch.zeros(int(L.lib().cc_topn_workspace_size(V)) // 4 + 1,
-                                   device=self.dev, dtype=torch.int32)
-        self.additions = torch.zeros(V, device=self.dev, dtype=torch.int32)
-        self.add_vals = torch.zeros(V, device=self.dev, dtype=torch.float32)
-        self.cut_vals = torch.zeros(V, device=self.dev, dtype=torch.float32)
-        self.n_add = torch.zeros(1, device=self.dev, dtype=torch.int32)
-        self.order = torch.zeros(V, device=self.dev, dtype=torch.int32)
-        self.idx_dev = torch.zeros(V + 2, device=self.dev, dtype=torch.int32)
-        self.pin_in = torch.zeros(V + 2, dtype=torch.int32).pin_memory()
-        self.pin_add = torch.zeros(V, dtype=torch.int32).pin_memory()
-        self.pin_addv = torch.zeros(V, dtype=torch.float32).pin_memory()
-        self.pin_cut = torch.zeros(V, dtype=torch.float32).pin_memory()
-        self.pin_nadd = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self.probs_dev = torch.zeros(V, device=self.dev, dtype=torch.float32)
+        self.ws = torch.zeros(int(L.lib().cc_recommend_ws_size(V, d)) // 4 + 64,
+                              device=self.dev, dtype=torch.int32)
+        # request I/O: req = {n, amount, ids[n]}, res = {n_add, additions, add_vals, cut_vals}
+        self.cap = min(V, GRAPH_MAX_IDS)
+        self.req_dev = torch.zeros(2 + V, device=self.dev, dtype=torch.int32)
+        self.res_dev = torch.zeros(1 + 2 * V + V, device=self.dev, dtype=torch.int32)
+        self.pin_req = torch.zeros(2 + V, dtype=torch.int32).pin_memory()
+        self.pin_res = torch.zeros(1 + 2 * V + V, dtype=torch.int32).pin_memory()
+        self._req_np = self.pin_req.numpy()
+        self._res_np = self.pin_res.numpy()
+        self._graph = None
+        # the request graph runs on the library's own non-blocking stream: every allocation and
+        # fill above (issued on torch's stream) must be complete before it can run
+        torch.cuda.synchronize(self.dev)
 
-    def _alloc(self, R):
-        self.cap = R
-        self.zlat = torch.zeros(R, 64, device=self.dev, dtype=torch.float32)
-        self.h3 = torch.zeros(R, self.d, device=self.dev, dtype=torch.float32)
-        self.probs_dev = torch.zeros(R, self.V, device=self.dev, dtype=torch.float32)
+    def __del__(self):
+        g = getattr(self, '_graph', None)
+        if g is not None:
+            try:
+                L.lib().cc_recommend_graph_destroy(g)
+            except Exception:
+                pass
+
+    def _graph_handle(self):
+        if self._graph is None:
+            h = L.C.c_void_p()
+            L.call('cc_recommend_graph_create', L.ptr(self.params), self.V, self.d, L.ptr(self.pin_req),
+                   L.ptr(self.req_dev), self.cap, L.ptr(self.ws), L.ptr(self.probs_dev), L.ptr(self.res_dev),
+                   L.C.byref(h))
+            self._graph = h
+        return self._graph
 
     # ------------------------------------------------------------------ batched encoder / decoder
     def encode_lists(self, lists):
@@ -54,13 +68,16 @@ class Recommender:
         lists = [np.unique(np.asarray(l, np.int64)).astype(np.int32) for l in lists]
         row_ptr = np.zeros(R + 1, np.int32)
         row_ptr[1:] = np.cumsum([len(l) for l in lists])
+        max_n = max([len(l) for l in lists], default=0)
         idx = np.concatenate(lists) if R else np.zeros(0, np.int32)
         with torch.cuda.stream(self.stream):
             rp = torch.from_numpy(row_ptr).to(self.dev, non_blocking=True)
             ix = torch.from_numpy(idx if len(idx) else np.zeros(1, np.int32)).to(self.dev, non_blocking=True)
             z = torch.zeros(R, 64, device=self.dev, dtype=torch.float32)
+            ws = torch.empty(int(L.lib().cc_infer_encode_ws_size(R, self.d, max_n)) // 4 + 4,
+                             device=self.dev, dtype=torch.float32)
             L.call('cc_infer_encode_fp32', L.ptr(self.params), self.V, self.d, R, L.ptr(rp), L.ptr(ix),
-                   L.ptr(z), L.stream_ptr(self.stream))
+                   max_n, L.ptr(ws), L.ptr(z), L.stream_ptr(self.stream))
         self.stream.synchronize()
         return z
 
@@ -78,45 +95,62 @@ class Recommender:
 
     # ------------------------------------------------------------------ single-cube request
     def recommend(self, cube_indices, amount, want_probs=False, want_order=False):
-        """ml_recommend.py:78-108 for one cube.  Returns dict with
-        additions (card idx, descending), add_vals, cut_vals (per cube index, input order),
-        and optionally the full probability vector / ranking."""
+        """ml_recommend.py:78-108 for one cube.  Returns dict with additions (card idx,
+        descending), add_vals, cut_vals (per cube index, input order), and optionally the full
+        probability vector / ranking.  Cubes of up to GRAPH_MAX_IDS distinct cards replay the
+        captured request graph (one launch, one D2H); larger ones run the same kernels directly."""
         ci = np.asarray(cube_indices, np.int64)
         uniq = np.unique(ci).astype(np.int32)
         n = len(uniq)
         amount = int(amount)
-        want = min(max(amount, 1), self.V)
+        want = min(max(amount, 1), self.V - n)
+        words = 1 + 2 * want + n
         with self.lock:
-            s = L.stream_ptr(self.stream)
-            with torch.cuda.stream(self.stream):
-                self.pin_in[0] = 0
-                self.pin_in[1] = n
-                self.pin_in[2:2 + n] = torch.from_numpy(uniq)
-                self.idx_dev[:2 + n].copy_(self.pin_in[:2 + n], non_blocking=True)
-                L.call('cc_infer_encode_fp32', L.ptr(self.params), self.V, self.d, 1, L.ptr(self.idx_dev),
-                       L.ptr(self.idx_dev[2:]), L.ptr(self.zlat), s)
-                L.call('cc_infer_decode_fp32', L.ptr(self.params), self.V, self.d, 1, L.ptr(self.zlat),
-                       L.ptr(self.h3), L.ptr(self.probs_dev), s)
-                L.call('cc_topn', L.ptr(self.probs_dev), self.V, L.ptr(self.idx_dev[2:]), n, amount,
-                       L.ptr(self.additions), L.ptr(self.n_add), L.ptr(self.add_vals), L.ptr(self.cut_vals),
-                       L.ptr(self.order) if want_order else None, L.ptr(self.topn_ws), s)
-                self.pin_nadd.copy_(self.n_add, non_blocking=True)
-                self.pin_add[:want].copy_(self.additions[:want], non_blocking=True)
-                self.pin_addv[:want].copy_(self.add_vals[:want], non_blocking=True)
-                if n:
-                    self.pin_cut[:n].copy_(self.cut_vals[:n], non_blocking=True)
-                probs = self.probs_dev[0].clone() if want_probs else None
-                order = self.order.clone() if want_order else None
-            self.stream.synchronize()
-            k = int(self.pin_nadd[0])
-            cut_by_card = dict(zip(uniq.tolist(), self.pin_cut[:n].tolist()))
+            req = self._req_np
+            req[0] = n
+            req[1] = amount
+            req[2:2 + n] = uniq
+            if n <= self.cap:
+                L.call('cc_recommend_graph_run', self._graph_handle(), L.ptr(self.pin_res), words)
+            else:
+                with torch.cuda.stream(self.stream):
+                    self.req_dev[:2 + n].copy_(self.pin_req[:2 + n], non_blocking=True)
+                    L.call('cc_recommend_fp32', L.ptr(self.params), self.V, self.d, L.ptr(self.req_dev), n,
+                           L.ptr(self.ws), L.ptr(self.probs_dev), L.ptr(self.res_dev), L.stream_ptr(self.stream))
+                    self.pin_res[:words].copy_(self.res_dev[:words], non_blocking=True)
+                self.stream.synchronize()
+            r = self._res_np
+            k = int(r[0])
+            cut = r[1 + 2 * want:1 + 2 * want + n].view(np.float32)
             out = {
-                'additions': self.pin_add[:k].numpy().copy(),
-                'add_vals': self.pin_addv[:k].numpy().copy(),
-                'cut_vals': np.array([cut_by_card[int(c)] for c in ci], np.float32),
+                'additions': r[1:1 + k].copy(),
+                'add_vals': r[1 + want:1 + want + k].view(np.float32).copy(),
+                'cut_vals': cut[np.searchsorted(uniq, ci)].copy() if n else np.zeros(0, np.float32),
             }
+            probs = order = None
+            if want_probs or want_order:
+                probs = self.probs_dev.clone()   # the graph ran on its own stream and was waited for
+            if want_order:
+                order = self._full_order(probs, uniq, amount)
         if want_probs:
             out['probs'] = probs.cpu().numpy()
         if want_order:
-            out['order'] = order.cpu().numpy()
+            out['order'] = order
         return out
+
+    def _full_order(self, probs, uniq, amount):
+        """The complete ranking (cc_topn with `order`; tests and tools only)."""
+        V, dev = self.V, self.dev
+        n = len(uniq)
+        want = min(max(amount, 1), V)
+        ci = torch.from_numpy(uniq if n else np.zeros(1, np.int32)).to(dev)
+        adds = torch.zeros(want, device=dev, dtype=torch.int32)
+        addv = torch.zeros(want, device=dev)
+        cutv = torch.zeros(max(n, 1), device=dev)
+        nadd = torch.zeros(1, device=dev, dtype=torch.int32)
+        order = torch.zeros(V, device=dev, dtype=torch.int32)
+        ws = torch.zeros(int(L.lib().cc_topn_workspace_size(V)) // 4 + 64, device=dev, dtype=torch.int32)
+        L.call('cc_topn', L.ptr(probs), V, L.ptr(ci), n, amount, L.ptr(adds), L.ptr(nadd), L.ptr(addv),
+               L.ptr(cutv), L.ptr(order), L.ptr(ws), L.stream_ptr())
+        torch.cuda.synchronize()
+        return order.cpu().numpy()

@@ -228,24 +228,51 @@ int cc_state_advance(int64_t *state, int64_t batches_per_epoch, void *stream);
 /* ----------------------------------------------------------------------------------
  * Recommend forward (ml_recommend.py:78-87, ml_recommend_web.py:39-46), fp32, with the
  * pinned summation order of oracle/infer_ref.py (bit-exact).  R cubes per call.
- *   cc_infer_encode_fp32: zlat [R, 64]   (model.encoder(x))
- *   cc_infer_decode_fp32: probs [R, V]   (model.decoder(z)) — sigmoid in fp64 -> fp32
+ *   cc_infer_encode_fp32: zlat [R, 64]   (model.encoder(x)); row_ptr/idx = CSR of sorted unique
+ *                         card ids, max_n >= the longest row; ws: cc_infer_encode_ws_size bytes.
+ *   cc_infer_decode_fp32: probs [R, V]   (model.decoder(z)) — sigmoid in fp64 -> fp32;
+ *                         h3_ws: [R, d] floats.
  * ---------------------------------------------------------------------------------- */
+size_t cc_infer_encode_ws_size(int32_t R, int32_t d, int32_t max_n);
 int cc_infer_encode_fp32(const float *params, int32_t V, int32_t d, int32_t R,
-                         const int32_t *row_ptr, const int32_t *idx, float *zlat, void *stream);
+                         const int32_t *row_ptr, const int32_t *idx, int32_t max_n, void *ws,
+                         float *zlat, void *stream);
 int cc_infer_decode_fp32(const float *params, int32_t V, int32_t d, int32_t R,
                          const float *zlat, float *h3_ws, float *probs, void *stream);
 
 /* ----------------------------------------------------------------------------------
  * Top-N (ml_recommend.py:87-108): rank all V probabilities descending, ties -> higher
  * index first (= numpy argsort(kind='stable')[::-1]); additions = first max(amount,1)
- * indices not in the cube; cut_vals[i] = probs[cube_idx[i]].
- * ws: cc_topn_workspace_size(V) bytes.  order (optional, [V]) receives the full ranking.
+ * indices not in the cube; cut_vals[i] = probs[cube_idx[i]].  cube_idx: n DISTINCT card ids.
+ * ws: cc_topn_workspace_size(V) bytes.
+ * order == NULL: the request path (tiled multi-workgroup radix sort, 5 launches).
+ * order != NULL: additionally the full ranking [V] (single-workgroup sort; tests and tools).
  * ---------------------------------------------------------------------------------- */
 size_t cc_topn_workspace_size(int32_t V);
 int cc_topn(const float *probs, int32_t V, const int32_t *cube_idx, int32_t n, int32_t amount,
             int32_t *additions, int32_t *n_additions, float *add_vals, float *cut_vals,
             int32_t *order, void *ws, void *stream);
+
+/* ----------------------------------------------------------------------------------
+ * One single-cube request end to end (ml_recommend.py:78-108 / ml_recommend_web.py:39-64):
+ * encode + decode + top-N, no host round trip, fixed launch grids (graph-replayable).
+ *   req (device):  {n, amount, ids[n]}  — the cube's sorted distinct card ids, n <= max_n
+ *   res (device):  {n_add, additions[w], add_vals[w] (fp32 bits), cut_vals[n] (fp32 bits)}
+ *                  with w = n_add = min(max(amount, 1), V - n)
+ *   probs [V] receives the probabilities; ws: cc_recommend_ws_size(V, d) bytes, 256-B aligned.
+ * ---------------------------------------------------------------------------------- */
+size_t cc_recommend_ws_size(int32_t V, int32_t d);
+int cc_recommend_fp32(const float *params, int32_t V, int32_t d, const int32_t *req,
+                      int32_t max_n, void *ws, float *probs, int32_t *res, void *stream);
+
+/* The same request captured once as a hipGraph: [H2D of (2 + max_n) words req_host -> req_dev]
+ * + the kernels.  cc_recommend_graph_run replays it, copies res_words words of res back to
+ * res_host (pinned) and waits.  Buffers stay owned by the caller and must outlive the handle. */
+int cc_recommend_graph_create(const float *params, int32_t V, int32_t d, const int32_t *req_host,
+                              int32_t *req_dev, int32_t max_n, void *ws, float *probs,
+                              int32_t *res_dev, void **handle);
+int cc_recommend_graph_run(void *handle, int32_t *res_host, int32_t res_words);
+int cc_recommend_graph_destroy(void *handle);
 
 #ifdef __cplusplus
 }
