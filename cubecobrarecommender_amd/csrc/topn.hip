@@ -144,18 +144,15 @@ __global__ __launch_bounds__(tiles::NT) void topn_pass_kernel(int pass, int V, i
     id[it] = pos < V ? isrc[pos] : 0u;
   }
   for (int i = threadIdx.x; i < (NT / 64) * R; i += NT) (&wcnt[0][0])[i] = 0u;
-  if (local) {  // stage this pass's histograms: ntiles*R words, 16 B per load, all in flight
-    const uint4 *src = reinterpret_cast<const uint4 *>(Hp);
-    uint4 *dst = reinterpret_cast<uint4 *>(hs);
-    const int n4 = ntiles * R / 4;
-    uint4 v[LOCAL_TILES];
+  if (local && !last)  // hs: the next pass's [dest tile][digit] counts of this tile
+    for (int i = threadIdx.x; i < ntiles * R; i += NT) hs[i] = 0u;
+  // every tile's counts of my 4 digits (4*tid..4*tid+3): the first HB tiles' loads are issued
+  // now and land during the ranking below
+  constexpr int HB = 16;
+  const uint4 *Hq = reinterpret_cast<const uint4 *>(Hp) + threadIdx.x;
+  uint4 hc[HB];
 #pragma unroll
-    for (int k = 0; k < LOCAL_TILES; ++k)
-      if (threadIdx.x + k * NT < n4) v[k] = src[threadIdx.x + k * NT];
-#pragma unroll
-    for (int k = 0; k < LOCAL_TILES; ++k)
-      if (threadIdx.x + k * NT < n4) dst[threadIdx.x + k * NT] = v[k];
-  }
+  for (int u = 0; u < HB; ++u) hc[u] = u < ntiles ? Hq[(int64_t)u * (R / 4)] : make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
@@ -166,24 +163,27 @@ __global__ __launch_bounds__(tiles::NT) void topn_pass_kernel(int pass, int V, i
     rk[it] = r + (uint32_t)__popcll(m & lt);
     if (valid && (m & lt) == 0) wcnt[wv][d] = r + (uint32_t)__popcll(m);
   }
-  // digit bases: thread owns digits 4*tid .. 4*tid+3
   {
     constexpr int PER = R / NT;
     int tot[PER], before[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) tot[j] = before[j] = 0;
-    for (int u = 0; u < ntiles; ++u) {
-      uint4 c;
-      if (local)
-        c = reinterpret_cast<const uint4 *>(hs + (int64_t)u * R)[threadIdx.x];
-      else
-        c = reinterpret_cast<const uint4 *>(Hp + (int64_t)u * R)[threadIdx.x];
+    auto acc = [&](const uint4 c, int u) {
       const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
       for (int j = 0; j < PER; ++j) {
         tot[j] += (int)cc[j];
         before[j] += u < t ? (int)cc[j] : 0;
       }
+    };
+#pragma unroll
+    for (int u = 0; u < HB; ++u) acc(hc[u], u);
+    for (int u0 = HB; u0 < ntiles; u0 += HB) {
+#pragma unroll
+      for (int u = 0; u < HB; ++u)
+        hc[u] = u0 + u < ntiles ? Hq[(int64_t)(u0 + u) * (R / 4)] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int u = 0; u < HB; ++u) acc(hc[u], u0 + u);
     }
     int sum = 0;
 #pragma unroll
@@ -195,9 +195,6 @@ __global__ __launch_bounds__(tiles::NT) void topn_pass_kernel(int pass, int V, i
       off += tot[j];
     }
   }
-  // hs becomes the next pass's local histogram
-  if (local && !last)
-    for (int i = threadIdx.x; i < ntiles * R; i += NT) hs[i] = 0u;
   __syncthreads();
   for (int dd = threadIdx.x; dd < R; dd += NT) {  // fold per-wave prefixes into the bases
     const uint32_t c0 = wcnt[0][dd], c1 = wcnt[1][dd], c2 = wcnt[2][dd];
