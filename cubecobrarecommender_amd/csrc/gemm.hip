@@ -9,6 +9,8 @@
 // Both LDS images are K-contiguous ([row][k] / [col][k]); transposed global layouts are
 // transposed during staging so every fragment read is one ds_read_b128 (bf16) / b32 (fp32).
 // Accumulator map (32x32): row = (r&3) + 8(r>>2) + 4(l>>5), col = l&31.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace {
@@ -254,6 +256,257 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams p) {
   }
 }
 
+// ------------------------------------------------------------------ NT bf16 kernel
+// C = A B^T with both operands K-contiguous (A [M][K], B [N][K]) — the decoder output layer's
+// forward (D3 Wo^T), weight gradient (D3^T dZ via D3^T and dZ^T images) and input gradient
+// (dZ Wo^T, split-K).  128x128x64 tiles, 4 waves each owning 64x64 (2x2 blocks of
+// v_mfma_f32_32x32x16_bf16), LDS double-buffered (one barrier per K-step; the next K-tile's
+// global loads are in flight during the current tile's MFMAs).  LDS rows are 64 bf16 = 8 x 16 B
+// chunks stored at chunk ^ (row & 7), so the 32 rows a fragment read touches spread over all
+// banks.  Tiles are assigned XCD-aware: each XCD gets a contiguous run of tiles, and the tile
+// order walks M fastest, so the M-tiles sharing one B panel (a slab of Wo or dZ^T) hit the same L2.
+constexpr int NBM = 128, NBN = 128, NBK = 64;
+#ifndef NT_RING
+#define NT_RING 2
+#endif
+
+__device__ __forceinline__ int xcd_tile(int b, int nb) {
+  const int q = nb / 8, r = nb % 8, x = b % 8, slot = b / 8;
+  return x < r ? x * (q + 1) + slot : r * (q + 1) + (x - r) * q + slot;
+}
+
+struct NtStage {
+  uint4 a[4], b[4];
+  // thread t, i < 4: chunk v = t + 256 i -> row v >> 3, 16-B chunk v & 7 of the 64-wide K tile
+  __device__ __forceinline__ static uint4 ld(const bf16_t *X, int ld, int row, int rlim, int k,
+                                             int kend) {
+    row = min(row, rlim - 1);  // rows past the edge compute discarded outputs
+    const bf16_t *src = X + (int64_t)row * ld + k;
+    if (k + 8 <= kend) return *reinterpret_cast<const uint4 *>(src);
+    bf16_t tmp[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tmp[e] = k + e < kend ? src[e] : (bf16_t)0;
+    return *reinterpret_cast<const uint4 *>(tmp);
+  }
+  __device__ __forceinline__ void load(const GemmParams &p, const bf16_t *A, const bf16_t *B,
+                                       int bm, int bn, int k0, int kend) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int v = threadIdx.x + 256 * i, row = v >> 3, k = k0 + (v & 7) * 8;
+      a[i] = ld(A, p.lda, bm + row, p.M, k, kend);
+      b[i] = ld(B, p.ldb, bn + row, p.N, k, kend);
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t *As, bf16_t *Bs) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int v = threadIdx.x + 256 * i, row = v >> 3, ch = (v & 7) ^ (row & 7);
+      *reinterpret_cast<uint4 *>(As + row * NBK + ch * 8) = a[i];
+      *reinterpret_cast<uint4 *>(Bs + row * NBK + ch * 8) = b[i];
+    }
+  }
+};
+
+__device__ __forceinline__ bf16x8_t nt_frag(const bf16_t *S, int row, int c) {
+  return *reinterpret_cast<const bf16x8_t *>(S + row * NBK + ((c ^ (row & 7)) * 8));
+}
+
+// Output staging: the finished 128x128 tile (post-epilogue fp32) goes through LDS so that
+// every global store is a full 16-B segment of a row of C / Cf, or of a row of C^T.
+constexpr int SLD = NBN + 1;  // odd row pitch: column reads for C^T spread over the banks
+constexpr int NT_LDS_BYTES = NBM * SLD * 4 > 2 * (NBM + NBN) * NBK * 2 ? NBM * SLD * 4
+                                                                       : 2 * (NBM + NBN) * NBK * 2;
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_nt_bf16_kernel(GemmParams p, int tiles_m) {
+  __shared__ __attribute__((aligned(16))) char smem[NT_LDS_BYTES];
+  __shared__ uint32_t ys[NBM][NBN / 32];  // BCE targets of the tile
+  __shared__ double red[4];
+  bf16_t(*As)[NBM * NBK] = reinterpret_cast<bf16_t(*)[NBM * NBK]>(smem);
+  bf16_t(*Bs)[NBN * NBK] = reinterpret_cast<bf16_t(*)[NBN * NBK]>(smem + 2 * NBM * NBK * 2);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int bm = (tile % tiles_m) * NBM, bn = (tile / tiles_m) * NBN;
+  int kbeg = 0, kend = p.K;
+  if constexpr (EPI == CC_EPI_SPLITK) {
+    const int kchunk = (int)cdiv(cdiv(p.K, p.splits), NBK) * NBK;
+    kbeg = blockIdx.y * kchunk;
+    kend = min(p.K, kbeg + kchunk);
+  }
+  if constexpr (EPI == CC_EPI_BCE) {  // lands during the K loop
+    const int YW = (p.N + 31) >> 5;
+    for (int i = threadIdx.x; i < NBM * (NBN / 32); i += 256) {
+      const int r = i / (NBN / 32), w = i % (NBN / 32);
+      const int gm = bm + r, gw = (bn >> 5) + w;
+      ys[r][w] = gm < p.M && gw < YW ? p.y_bits[(int64_t)gm * YW + gw] : 0u;
+    }
+  }
+  const bf16_t *__restrict__ A = reinterpret_cast<const bf16_t *>(p.A);
+  const bf16_t *__restrict__ B = reinterpret_cast<const bf16_t *>(p.B);
+  f32x16_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const bool do_cs = p.colsum != nullptr && bm == 0 && threadIdx.x < NBN;
+  float cs = 0.f;
+  // D-deep register ring: K-tiles t+1 .. t+D-1 are in flight while tile t's MFMAs run (a tile's
+  // compute is far shorter than a global round trip, so one tile of look-ahead leaves the loop
+  // latency-bound).  LDS stays double-buffered: tile t lives in buffer t & 1.
+  constexpr int D = NT_RING;
+  NtStage st[D];
+  const int nk = kbeg < kend ? (int)cdiv(kend - kbeg, NBK) : 0;
+#pragma unroll
+  for (int q = 0; q < D; ++q)
+    if (q < nk) st[q].load(p, A, B, bm, bn, kbeg + q * NBK, kend);
+  if (nk > 0) st[0].store(As[0], Bs[0]);
+  __syncthreads();
+  const int ar = wm * 64 + (lane & 31), br = wn * 64 + (lane & 31);
+  for (int t0 = 0; t0 < nk; t0 += D) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      const int t = t0 + q;
+      if (t >= nk) break;
+      const bf16_t *as = As[t & 1], *bs = Bs[t & 1];
+#pragma unroll
+      for (int kk = 0; kk < NBK / 16; ++kk) {
+        const int c = 2 * kk + half;
+        const bf16x8_t a0 = nt_frag(as, ar, c), a1 = nt_frag(as, ar + 32, c);
+        const bf16x8_t b0 = nt_frag(bs, br, c), b1 = nt_frag(bs, br + 32, c);
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+      }
+      if (do_cs) {  // bias gradient: sum of B row n over k, ascending k
+        const int n = threadIdx.x;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const bf16_t *qq = bs + n * NBK + ((c ^ (n & 7)) * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs += bf2f(qq[e]);
+        }
+      }
+      // slot q held tile t (already in LDS); refill it with tile t + D, publish tile t + 1
+      if (t + D < nk) st[q].load(p, A, B, bm, bn, kbeg + (t + D) * NBK, kend);
+      if (t + 1 < nk) st[(q + 1) % D].store(As[(t + 1) & 1], Bs[(t + 1) & 1]);
+      __syncthreads();
+    }
+  }
+  if (do_cs && bn + (int)threadIdx.x < p.N) {
+    const int64_t zo = EPI == CC_EPI_SPLITK ? (int64_t)blockIdx.y * p.N : 0;
+    p.colsum[zo + bn + threadIdx.x] = cs;
+  }
+
+  // ---- epilogue: post-op fp32 tile -> LDS -> coalesced stores
+  float *S = reinterpret_cast<float *>(smem);  // [NBM][SLD] (the K loop's buffers are done)
+  float lossf = 0.f;
+  const float scale = p.scale;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int lc = wn * 64 + j * 32 + (lane & 31), gn = bn + lc;
+      const int lr0 = wm * 64 + i * 32 + 4 * half;
+      float bias = 0.f;
+      if constexpr (EPI == CC_EPI_STORE || EPI == CC_EPI_BCE)
+        bias = p.bias && gn < p.N ? p.bias[gn] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int lr = lr0 + (r & 3) + 8 * (r >> 2);
+        float v = acc[i][j][r];
+        if constexpr (EPI == CC_EPI_STORE) {
+          v += bias;
+          if (p.relu) v = v > 0.f ? v : 0.f;
+        } else if constexpr (EPI == CC_EPI_BCE) {
+          // sigmoid_cross_entropy_with_logits (TF 2.5 Keras BCE on a Sigmoid output)
+          const float z = v + bias;
+          const float y = (float)((ys[lr][lc >> 5] >> (lc & 31)) & 1u);
+          const float e = __expf(-fabsf(z));
+          const float rp = __fdividef(1.f, 1.f + e);
+          if (bm + lr < p.M && gn < p.N) lossf += fmaxf(z, 0.f) - z * y + __logf(1.f + e);
+          const float sig = z >= 0.f ? rp : e * rp;
+          v = (sig - y) * scale;
+        }
+        S[lr * SLD + lc] = v;
+      }
+    }
+  }
+  __syncthreads();
+  // rows of C / Cf: thread -> 4 consecutive columns
+  {
+    float *Cf = p.Cf;
+    int64_t ldf = p.ldc;
+    if constexpr (EPI == CC_EPI_SPLITK) {
+      Cf = p.Cf + (int64_t)blockIdx.y * p.M * p.N;
+      ldf = p.N;
+    }
+    bf16_t *Cb = EPI == CC_EPI_SPLITK ? nullptr : reinterpret_cast<bf16_t *>(p.C);
+    const bool vec = ((ldf & 3) == 0) && ((p.ldc & 3) == 0);
+    for (int idx = threadIdx.x; idx < NBM * (NBN / 4); idx += 256) {
+      const int lr = idx / (NBN / 4), lc = (idx % (NBN / 4)) * 4;
+      const int gm = bm + lr, gn = bn + lc;
+      if (gm >= p.M || gn >= p.N) continue;
+      const float v0 = S[lr * SLD + lc], v1 = S[lr * SLD + lc + 1];
+      const float v2 = S[lr * SLD + lc + 2], v3 = S[lr * SLD + lc + 3];
+      if (vec && gn + 3 < p.N) {
+        if (Cf) *reinterpret_cast<float4 *>(Cf + (int64_t)gm * ldf + gn) = make_float4(v0, v1, v2, v3);
+        if (Cb) {
+          const uint2 pk = make_uint2((uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16),
+                                      (uint32_t)f2bf(v2) | ((uint32_t)f2bf(v3) << 16));
+          *reinterpret_cast<uint2 *>(Cb + (int64_t)gm * p.ldc + gn) = pk;
+        }
+      } else {
+        const float vv[4] = {v0, v1, v2, v3};
+        for (int e = 0; e < 4 && gn + e < p.N; ++e) {
+          if (Cf) Cf[(int64_t)gm * ldf + gn + e] = vv[e];
+          if (Cb) Cb[(int64_t)gm * p.ldc + gn + e] = f2bf(vv[e]);
+        }
+      }
+    }
+  }
+  if constexpr (EPI == CC_EPI_BCE) {
+    // rows of C^T [N][M] (the k-contiguous operand of dW = D3^T dZ): thread -> 8 consecutive m
+    if (p.Ct) {
+      bf16_t *Ct = reinterpret_cast<bf16_t *>(p.Ct);
+      const bool vec = (p.ldct & 7) == 0;
+      for (int idx = threadIdx.x; idx < NBN * (NBM / 8); idx += 256) {
+        const int lc = idx / (NBM / 8), lr = (idx % (NBM / 8)) * 8;
+        const int gn = bn + lc, gm = bm + lr;
+        if (gn >= p.N || gm >= p.M) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = S[(lr + e) * SLD + lc];
+        bf16_t *dst = Ct + (int64_t)gn * p.ldct + gm;
+        if (vec && gm + 7 < p.M) {
+          uint4 pk;
+          pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          pk.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+          pk.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+          *reinterpret_cast<uint4 *>(dst) = pk;
+        } else {
+          for (int e = 0; e < 8 && gm + e < p.M; ++e) dst[e] = f2bf(v[e]);
+        }
+      }
+    }
+    const double sum = block_sum_double((double)lossf, red);
+    if (threadIdx.x == 0) p.loss_partials[tile] = sum;
+  }
+}
+
+template <int EPI>
+int launch_nt(const cc_gemm_args *g, const GemmParams &p, hipStream_t s) {
+  const int tm = (int)cdiv(g->M, NBM), tn = (int)cdiv(g->N, NBN);
+  const dim3 grid((unsigned)(tm * tn), EPI == CC_EPI_SPLITK ? (unsigned)g->splits : 1u);
+  hipLaunchKernelGGL(gemm_nt_bf16_kernel<EPI>, grid, dim3(256), 0, s, p, tm);
+  CC_LAUNCH_CHECK("gemm_nt_bf16_kernel");
+  return CC_OK;
+}
+
 template <typename T, int EPI, int BK>
 int launch_bk(const cc_gemm_args *g, const GemmParams &p, hipStream_t s) {
   const dim3 grid((unsigned)cdiv(g->N, BN), (unsigned)cdiv(g->M, BM),
@@ -380,6 +633,19 @@ extern "C" int cc_gemm(const cc_gemm_args *g, void *stream) {
   CC_REQUIRE(!g->Ct || g->epilogue == CC_EPI_BCE, "cc_gemm: Ct only with the BCE epilogue");
 
   hipStream_t s = as_stream(stream);
+  // bf16 with both operands K-contiguous and 16-B aligned rows: the 128x128 NT kernel
+  static const bool nt_enabled = [] {
+    const char *e = getenv("CCREC_GEMM_NT");  // A/B switch for benchmarking the generic kernel
+    return !(e && e[0] == '0');
+  }();
+  if (nt_enabled && g->dtype == CC_BF16 && !g->ta && g->tb && p.vec_a && p.vec_b &&
+      g->epilogue != CC_EPI_MASK) {
+    switch (g->epilogue) {
+      case CC_EPI_STORE: return launch_nt<CC_EPI_STORE>(g, p, s);
+      case CC_EPI_BCE: return launch_nt<CC_EPI_BCE>(g, p, s);
+      case CC_EPI_SPLITK: return launch_nt<CC_EPI_SPLITK>(g, p, s);
+    }
+  }
   return g->dtype == CC_BF16 ? launch_epi<bf16_t>(g, p, s) : launch_epi<float>(g, p, s);
 }
 
