@@ -106,12 +106,57 @@ __device__ __forceinline__ void lds_store_rows(T *Xr, int ldx, T *Xt, int ldt, i
 // copy a [32][W] block of a global [R][W] activation into LDS row-major (+ transposed) images
 template <typename T>
 __device__ void load_block(const T *__restrict__ g, int W, int r0, T *Xr, int ldx, T *Xt, int ldt) {
+  constexpr int VW = 16 / sizeof(T);
+  if (!Xt && W % VW == 0 && ldx % VW == 0) {
+    // 16-B vectors: the block's rows are contiguous in global memory ([R][W] row-major)
+    const int per = W / VW, nv = RB * per;
+    const uint4 *src = reinterpret_cast<const uint4 *>(g + (int64_t)r0 * W);
+    for (int i0 = 0; i0 < nv; i0 += 4 * NT) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + u * NT + (int)threadIdx.x < nv) v[u] = src[i0 + u * NT + threadIdx.x];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * NT + threadIdx.x;
+        if (i < nv) *reinterpret_cast<uint4 *>(Xr + (i / per) * ldx + (i % per) * VW) = v[u];
+      }
+    }
+    return;
+  }
   for (int i = threadIdx.x; i < RB * W; i += NT) {
     const int row = i / W, col = i % W;
     const T v = g[(int64_t)(r0 + row) * W + col];
     Xr[row * ldx + col] = v;
     if (Xt) Xt[col * ldt + row] = v;
   }
+}
+
+// transposed copy: Xt[col][row] = g[r0 + row][col] for the block's RB rows (16-B global loads)
+template <typename T>
+__device__ void load_block_t(const T *__restrict__ g, int W, int r0, T *Xt, int ldt) {
+  constexpr int VW = 16 / sizeof(T);
+  if (W % VW == 0) {
+    const int per = W / VW, nv = RB * per;
+    const uint4 *src = reinterpret_cast<const uint4 *>(g + (int64_t)r0 * W);
+    for (int i0 = 0; i0 < nv; i0 += 4 * NT) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + u * NT + (int)threadIdx.x < nv) v[u] = src[i0 + u * NT + threadIdx.x];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * NT + threadIdx.x;
+        if (i >= nv) continue;
+        const int row = i / per, c0 = (i % per) * VW;
+        const T *e = reinterpret_cast<const T *>(&v[u]);
+#pragma unroll
+        for (int q = 0; q < VW; ++q) Xt[(c0 + q) * ldt + row] = e[q];
+      }
+    }
+    return;
+  }
+  for (int e = threadIdx.x; e < RB * W; e += NT) Xt[(e % W) * ldt + e / W] = g[(int64_t)(r0 + e / W) * W + e % W];
 }
 
 template <typename T>
@@ -236,8 +281,8 @@ __global__ __launch_bounds__(NT) void tower_dw_kernel(TowerP p) {
   chain_dims(p.d, i, K, N);
   const T *H = reinterpret_cast<const T *>(p.act[i]);
   const T *G = reinterpret_cast<const T *>(i == 5 ? p.gD3 : p.gact[i]);
-  for (int e = threadIdx.x; e < RB * K; e += NT) Ht[(e % K) * ldt + e / K] = H[(int64_t)(r0 + e / K) * K + e % K];
-  for (int e = threadIdx.x; e < RB * N; e += NT) Gt[(e % N) * ldt + e / N] = G[(int64_t)(r0 + e / N) * N + e % N];
+  load_block_t<T>(H, K, r0, Ht, ldt);
+  load_block_t<T>(G, N, r0, Gt, ldt);
   __syncthreads();
   float *sw = p.slab + (int64_t)blk * p.slab_elems + slab_off(p.d, i);
   const int ntn = N / 32, nt = (K / 32) * ntn;
