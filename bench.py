@@ -34,6 +34,9 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-steps', type=int, default=16)
     ap.add_argument('--no-recommend', action='store_true')
+    ap.add_argument('--backend', default='nccl',
+                    help="collective backend for --gpus > 1 (nccl = RCCL; gloo only to rehearse the "
+                         "data-parallel path with several ranks on one GPU)")
     ap.add_argument('--traffic-json', default=os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                            'profiles', 'traffic_r01.json'))
     return ap.parse_args()
@@ -45,8 +48,12 @@ def setup_dist(args):
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
         import torch.distributed as dist
+        local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(args.backend)
     return world, rank, local
 
 
@@ -166,13 +173,18 @@ def main():
     adam_ev = []
 
     def step(graphed, timed=False):
+        if world > 1:   # bucketed reduce-scatter + sharded Adam + all-gather (zero.py)
+            if not graphed:
+                saved, tr.graphs = tr.graphs, None
+                tr.step_dp()
+                tr.graphs = saved
+            else:
+                tr.step_dp(timing=timed)
+            return
         if graphed:
             tr.graphs[0].replay()
         else:
             tr.forward_backward()
-        if world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(tr.grads[:n_grad], op=dist.ReduceOp.AVG)
         if graphed:
             if timed:
                 # HIP events on the stream, bracketing the Adam kernel launched right behind the
@@ -220,15 +232,25 @@ def main():
             dist.destroy_process_group()
         return
     value = B * world * args.steps / dt
-    adam_ms = float(np.mean([a.elapsed_time(b) for a, b in adam_ev]))
-    roof = roofline_for('cc_adam_dense', adam_ms, tr)
+    if world == 1:
+        adam_ms = float(np.mean([a.elapsed_time(b) for a, b in adam_ev]))
+        roof = roofline_for('cc_adam_dense', adam_ms, tr)
+        roof['measured'] = 'HIP events around the Adam kernel in every timed step (same stream)'
+        roof['traffic'] = None
+        if args.traffic_json and os.path.exists(args.traffic_json):
+            roof['traffic'] = json.load(open(args.traffic_json)).get('adam_kernel')
+    else:   # sharded Adam: this rank's 1/world shard of every bucket, per step
+        torch.cuda.synchronize()
+        ev = tr.sharded.adam_events
+        n_sh = sum(n for _, _, n in ev) / args.steps
+        adam_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / args.steps
+        byt = n_sh * (16 + 12 + 2)
+        roof = {'bound': 'hbm', 'achieved': byt / (adam_ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s', 'bytes_per_launch': byt, 'traffic': None,
+                'measured': 'HIP events around the sharded Adam kernels on the comm stream (sum per step)'}
     roof['frac'] = roof['achieved'] / roof['peak']
     roof['kernel'] = 'adam_kernel (cc_adam_dense)'
     roof['avg_ms'] = adam_ms
-    roof['measured'] = 'HIP events around the Adam kernel in every timed step (same stream)'
-    roof['traffic'] = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        roof['traffic'] = json.load(open(args.traffic_json)).get('adam_kernel')
     out = {
         'metric': 'training cubes/sec at |V|~22k d=256; top-N recommend p50 latency',
         'value': value, 'unit': 'cubes/s', 'n_gpus': world, 'steps': args.steps,

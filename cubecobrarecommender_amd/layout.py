@@ -19,20 +19,44 @@ def layer_shapes(V, d):
             (64, 128), (128, 256), (256, d), (d, V))
 
 
-class Layout:
-    """name -> (offset, shape) in the flat fp32 buffer; 64-element aligned tensors."""
+def _round_up(x, a):
+    return (x + a - 1) // a * a
 
-    def __init__(self, V, d):
-        self.V, self.d = int(V), int(d)
+
+class Layout:
+    """name -> (offset, shape) in the flat fp32 buffer; 64-element aligned tensors.
+
+    align > 1 (data-parallel training, align = world * 64) additionally starts the decoder output
+    layer and the decoder_for_reg block on multiples of `align` and pads every block to one, so the
+    three gradient buckets (towers + E1 | decoder output layer | decoder_for_reg) split into equal
+    per-rank shards (zero.py).  align == 1 is exactly cc_param_layout."""
+
+    def __init__(self, V, d, align=1):
+        self.V, self.d, self.align = int(V), int(d), int(align)
         self.entries = {}
         o = 0
         for li, (fi, fo) in enumerate(layer_shapes(V, d)):
+            if li in (7, 8):
+                o = _round_up(o, self.align)
             for name, shape in ((LAYERS[li] + '/kernel', (fi, fo)), (LAYERS[li] + '/bias', (fo,))):
                 self.entries[name] = (o, shape)
                 o += (int(np.prod(shape)) + 63) // 64 * 64
             if li == 7:
+                o = _round_up(o, self.align)
                 self.main_total = o
-        self.total = o
+        self.total = _round_up(o, self.align)
+
+    def buckets(self, with_reg):
+        """Gradient buckets in the order backward produces them: (name, lo, hi)."""
+        out = [('decoder_output', self.offset('decoder/reconstruct/kernel'), self.main_total),
+               ('towers_e1', 0, self.offset('decoder/reconstruct/kernel'))]
+        if with_reg:
+            out.append(('decoder_for_reg', self.main_total, self.total))
+        return out
+
+    def convert(self, flat, other):
+        """Re-lay a flat buffer written in layout `other` into this layout (numpy)."""
+        return self.pack(other.unpack(flat))
 
     def offset(self, name):
         return self.entries[name][0]

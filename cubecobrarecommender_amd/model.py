@@ -111,8 +111,8 @@ class CC_Recommender:
                           dtype=self.dtype, seed=self.seed, rank=rank, world=world)
         tr = Trainer(cfg, generator.data, params_flat=self._current_flat())
         if self._m is not None:
-            tr.m.copy_(torch.from_numpy(self._m))
-            tr.v.copy_(torch.from_numpy(self._v))
+            tr.load_standard(tr.m, self._m)
+            tr.load_standard(tr.v, self._v)
             tr.state[0] = self._step
         tr.set_epoch_permutations(generator.epoch_permutations(epochs))
         steps = tr.batches_per_epoch
@@ -122,14 +122,7 @@ class CC_Recommender:
             t0 = time.perf_counter()
             acc = 0.0
             for _ in range(steps):
-                if world > 1:
-                    import torch.distributed as dist
-                    tr.forward_backward()
-                    n = tr.layout.total if tr.use_reg else tr.layout.main_total
-                    dist.all_reduce(tr.grads[:n], op=dist.ReduceOp.AVG)
-                    tr.apply()
-                else:
-                    tr.step()
+                tr.step()          # data-parallel: bucketed reduce-scatter + sharded Adam (zero.py)
             torch.cuda.synchronize()
             l = tr.losses()
             self.history.append(l)
@@ -147,8 +140,10 @@ class CC_Recommender:
         lay = self.layout
         P = lay.unpack(self._current_flat())
         if self.trainer is not None:
-            m = lay.unpack(self.trainer.m.cpu().numpy())
-            v = lay.unpack(self.trainer.v.cpu().numpy())
+            if getattr(self.trainer, 'sharded', None) is not None:   # data parallel: m, v sharded
+                self.trainer.sharded.gather_state()
+            m = lay.unpack(self.trainer.standard(self.trainer.m))
+            v = lay.unpack(self.trainer.standard(self.trainer.v))
         elif self._m is not None:
             m, v = lay.unpack(self._m), lay.unpack(self._v)
         else:
@@ -158,7 +153,7 @@ class CC_Recommender:
     # --------------------------------------------------------------- internals
     def _current_flat(self):
         if self.trainer is not None:
-            return self.trainer.params.cpu().numpy()
+            return self.trainer.standard(self.trainer.params)
         return np.asarray(self._flat, np.float32)
 
     def _rec(self):

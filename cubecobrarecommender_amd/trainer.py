@@ -96,7 +96,9 @@ class Trainer:
         assert data.V == V, 'dataset V mismatch'
         assert d % 64 == 0 and (d // 64) & (d // 64 - 1) == 0, 'd must be 64 * 2^k'
         self.dev = torch.device(device)
-        self.layout = Layout(V, d)
+        # data-parallel: gradient buckets aligned to world*64 so every rank owns an equal shard
+        self.std_layout = Layout(V, d)
+        self.layout = Layout(V, d, align=cfg.world * 64) if cfg.world > 1 else self.std_layout
         self.use_reg = cfg.reg > 0
         if self.use_reg and data.y_reg is None:
             raise ValueError('reg > 0 needs the M~ matrix on the device')
@@ -106,8 +108,8 @@ class Trainer:
         P = self.layout.total
         f32 = dict(device=self.dev, dtype=torch.float32)
         self.params = torch.zeros(P, **f32)
-        if params_flat is not None:
-            self.params.copy_(torch.as_tensor(params_flat, dtype=torch.float32))
+        if params_flat is not None:   # given in the standard (cc_param_layout) layout
+            self.load_standard(self.params, params_flat)
         self.m = torch.zeros(P, **f32)
         self.v = torch.zeros(P, **f32)
         self.grads = torch.zeros(P, **f32)
@@ -304,6 +306,14 @@ class Trainer:
 
     # ------------------------------------------------------------------ the step
     def forward_backward(self, stream=None):
+        """One step's gradients into self.grads (no optimizer): F, E, D1/D2 + losses, backward."""
+        self.forward_backward_a(stream)
+        self.forward_backward_b(stream)
+
+    def forward_backward_a(self, stream=None):
+        """F, E, towers forward, both output layers with their losses and weight/input gradients.
+        After it the 'decoder_output' gradient bucket is final (zero.py overlaps its reduction
+        with forward_backward_b)."""
         cfg, lay = self.cfg, self.layout
         V, d, B, R = cfg.V, cfg.d, cfg.batch_size, self.R
         self._s = L.stream_ptr(stream)
@@ -380,7 +390,13 @@ class Trainer:
                 self._dense_bwd(self.D2, self.gD3, rows, 256, d, pre + '/decoded_3', gIn=self.gD2, mask=self.D2)
                 self._dense_bwd(self.D1, self.gD2, rows, 128, 256, pre + '/decoded_2', gIn=self.gD1, mask=self.D1)
                 self._dense_bwd(self.Zl, self.gD1, rows, 64, 128, pre + '/decoded_1', gIn=self.gZl, mask=self.Zl)
-        # ---- towers backward (both branches' rows together through the shared encoder)
+
+    def forward_backward_b(self, stream=None):
+        """Towers backward (both branches' rows together through the shared encoder) and the E1
+        row-gather backward."""
+        cfg, V, d, R = self.cfg, self.cfg.V, self.cfg.d, self.R
+        self._s = L.stream_ptr(stream)
+        s = self._s
         if self.fused_tower:
             t = self._tick('cc_tower_bwd')
             L.call('cc_tower_bwd', L.C.byref(self.targs), s)
@@ -414,7 +430,38 @@ class Trainer:
         self.apply_adam(stream)
         self.apply_rest(stream)
 
+    # ------------------------------------------------------------------ data parallel (zero.py)
+    def adam_range(self, lo, n, g, stream=None):
+        """TF Adam over [lo, lo+n) of the flat buffers with the gradient slice g (a tensor)."""
+        cfg = self.cfg
+        L.call('cc_adam_dense', L.ptr(self.params[lo:]), L.ptr(self.m[lo:]), L.ptr(self.v[lo:]),
+               L.ptr(g), L.ptr(self.shadow[lo:]) if self.shadow is not None else None, n,
+               L.ptr(self.state), cfg.lr, cfg.beta1, cfg.beta2, cfg.eps, L.stream_ptr(stream))
+
+    def refresh_range(self, lo, hi, stream=None):
+        if self.shadow is not None:
+            L.call('cc_to_bf16', L.ptr(self.params[lo:]), L.ptr(self.shadow[lo:]), hi - lo,
+                   L.stream_ptr(stream))
+
+    def step_dp(self, timing=False):
+        """One data-parallel step: bucketed reduce-scatter overlapped with the towers' backward,
+        Adam on this rank's shards, all-gathered parameters (zero.py)."""
+        if getattr(self, 'sharded', None) is None:
+            from .zero import ShardedStep
+            self.sharded = ShardedStep(self)
+        g = self.graphs
+        self.sharded.step(
+            phase_a=g[0].replay if g else self.forward_backward_a,
+            phase_b=g[1].replay if g else self.forward_backward_b,
+            rest=g[2].replay if g else self.apply_rest,
+            adam_fn=lambda lo, n, gs: self.adam_range(lo, n, gs),
+            refresh_fn=lambda lo, hi: self.refresh_range(lo, hi),
+            timing=timing)
+
     def step(self, stream=None):
+        if self.cfg.world > 1:
+            self.step_dp()
+            return
         if self.graphs is not None:
             for g in self.graphs:
                 g.replay()
@@ -424,10 +471,11 @@ class Trainer:
 
     def capture(self):
         """Capture the step as three hipGraphs (torch.cuda.CUDAGraph over our own kernel launches):
-        forward_backward | Adam | counters+transposes.  Every buffer is preallocated and the
-        step/epoch counters are device-resident, so replays are exact repeats of the eager step.
-        The data-parallel all-reduce runs between the first two; bench.py brackets the Adam graph
-        with HIP events to time the step's bytes-dominant kernel inside the timed region."""
+        forward_backward | Adam | counters+transposes (data parallel: forward_backward_a |
+        forward_backward_b | counters+transposes, with zero.py's collectives and sharded Adam
+        between them).  Every buffer is preallocated and the step/epoch counters are
+        device-resident, so replays are exact repeats of the eager step.  bench.py brackets the
+        Adam kernel with HIP events to time the step's bytes-dominant kernel in the timed region."""
         timing, self.timing = self.timing, False
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream())
@@ -437,10 +485,16 @@ class Trainer:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g_fb, g_adam, g_rest = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_fb):
-            self.forward_backward()
-        with torch.cuda.graph(g_adam):
-            self.apply_adam()
+        if self.cfg.world > 1:   # (forward_backward_a | forward_backward_b | counters): the
+            with torch.cuda.graph(g_fb):       # sharded optimizer's collectives run between them
+                self.forward_backward_a()
+            with torch.cuda.graph(g_adam):
+                self.forward_backward_b()
+        else:
+            with torch.cuda.graph(g_fb):
+                self.forward_backward()
+            with torch.cuda.graph(g_adam):
+                self.apply_adam()
         with torch.cuda.graph(g_rest):
             self.apply_rest()
         torch.cuda.synchronize()
@@ -468,3 +522,15 @@ class Trainer:
 
     def params_dict(self):
         return self.layout.unpack(self.params.cpu().numpy())
+
+    # ------------------------------------------------------------------ standard-layout views
+    def standard(self, buf):
+        """A device flat buffer (params / m / v / grads) in the standard cc_param_layout (numpy)."""
+        flat = buf.detach().cpu().numpy()
+        return flat if self.layout is self.std_layout else self.std_layout.convert(flat, self.layout)
+
+    def load_standard(self, buf, flat):
+        flat = np.asarray(flat, np.float32)
+        if self.layout is not self.std_layout:
+            flat = self.layout.convert(flat, self.std_layout)
+        buf.copy_(torch.as_tensor(flat, dtype=torch.float32))

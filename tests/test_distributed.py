@@ -40,3 +40,67 @@ def test_gloo_world2_allreduce_and_sharding():
     for bi in range(8):
         both = res[0][1][bi] + res[1][1][bi]
         assert both == perm[bi * 8:(bi + 1) * 8].tolist()
+
+
+def _adam(p, m, v, g, t, lr=1e-3, b1=0.9, b2=0.999, eps=1e-7):
+    """TF ResourceApplyAdam in float32 torch ops, in place."""
+    m.add_((g - m) * (1 - b1))
+    v.add_((g * g - v) * (1 - b2))
+    lr_t = lr * (1 - b2 ** t) ** 0.5 / (1 - b1 ** t)
+    p.sub_(lr_t * m / (v.sqrt() + eps))
+
+
+class _FakeTrainer:
+    def __init__(self, world, rank, with_reg):
+        from types import SimpleNamespace
+        from cubecobrarecommender_amd.layout import Layout
+        self.cfg = SimpleNamespace(world=world, rank=rank)
+        self.layout = Layout(300, 64, align=world * 64)
+        self.use_reg = with_reg
+        n = self.layout.total
+        gen = torch.Generator().manual_seed(7)
+        self.params = torch.randn(n, generator=gen)
+        self.m = torch.zeros(n)
+        self.v = torch.zeros(n)
+        self.grads = torch.randn(n, generator=torch.Generator().manual_seed(100 + rank))
+
+
+def _zero_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from cubecobrarecommender_amd import distributed as D
+    from cubecobrarecommender_amd.zero import ShardedStep
+    D.init(backend='gloo')
+    tr = _FakeTrainer(world, rank, with_reg=True)
+    zs = ShardedStep(tr)
+    for t in (1, 2):
+        def adam_fn(lo, n, g, t=t):
+            _adam(tr.params[lo:lo + n], tr.m[lo:lo + n], tr.v[lo:lo + n], g, t)
+        zs.step(lambda: None, lambda: None, lambda: None, adam_fn, lambda lo, hi: None)
+    zs.gather_state()
+    q.put((rank, tr.params.numpy().copy(), tr.m.numpy().copy(), tr.v.numpy().copy()))
+    D.finish()
+
+
+def test_gloo_world2_sharded_adam_equals_allreduce_adam():
+    """ZeRO-1 step (bucketed reduce-scatter, Adam on the rank's shard, all-gather; zero.py)
+    leaves every rank with exactly the parameters of a full Adam on the averaged gradient."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() + 7) % 1000
+    ps = [ctx.Process(target=_zero_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {r: (pp, mm, vv) for r, pp, mm, vv in [q.get(timeout=120) for _ in ps]}
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    ref = _FakeTrainer(world, 0, with_reg=True)
+    g = sum(_FakeTrainer(world, r, True).grads for r in range(world)) * (1.0 / world)
+    for t in (1, 2):
+        _adam(ref.params, ref.m, ref.v, g, t)
+    for r in range(world):
+        np.testing.assert_array_equal(res[r][0], ref.params.numpy())
+        np.testing.assert_array_equal(res[r][1], ref.m.numpy())
+        np.testing.assert_array_equal(res[r][2], ref.v.numpy())
