@@ -259,89 +259,151 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmParams p) {
 // ------------------------------------------------------------------ NT bf16 kernel
 // C = A B^T with both operands K-contiguous (A [M][K], B [N][K]) — the decoder output layer's
 // forward (D3 Wo^T), weight gradient (D3^T dZ via D3^T and dZ^T images) and input gradient
-// (dZ Wo^T, split-K).  128x128x64 tiles, 4 waves each owning 64x64 (2x2 blocks of
-// v_mfma_f32_32x32x16_bf16), LDS double-buffered (one barrier per K-step; the next K-tile's
-// global loads are in flight during the current tile's MFMAs).  LDS rows are 64 bf16 = 8 x 16 B
-// chunks stored at chunk ^ (row & 7), so the 32 rows a fragment read touches spread over all
-// banks.  Tiles are assigned XCD-aware: each XCD gets a contiguous run of tiles, and the tile
-// order walks M fastest, so the M-tiles sharing one B panel (a slab of Wo or dZ^T) hit the same L2.
-constexpr int NBM = 128, NBN = 128, NBK = 64;
+// (dZ Wo^T, split-K).  BM x 128 tiles (BM = 128/256/512), BM/32 waves each owning 64x64 (2x2
+// blocks of v_mfma_f32_32x32x16_bf16); with the decoder's M <= 512 one workgroup covers every row
+// of a 128-column panel, so each panel of Wo / dZ^T is read once and the per-tile fixed cost
+// (prologue, epilogue) is paid BM/128 times less often.  LDS double-buffered (one barrier per
+// K-step; the next K-tile's global loads are in flight during the current tile's MFMAs).  LDS
+// rows hold BK bf16 = CH x 16 B chunks stored at chunk ^ (row & (CH-1)), so the rows a fragment
+// read touches spread over the banks.  Tiles are assigned XCD-aware: each XCD gets a contiguous
+// run, walking M fastest, so the M-tiles sharing one B panel hit the same L2.
+// Epilogue: post-op fp32 tile -> LDS (in passes of <= 256 rows) -> 16-B coalesced stores of
+// C / Cf rows and of C^T rows (BCE: dZ^T, the k-contiguous operand of dW = D3^T dZ).
+constexpr int NBN = 128;
+constexpr int SLD = NBN + 1;  // odd row pitch: column reads for C^T spread over the banks
 #ifndef NT_RING
 #define NT_RING 2
 #endif
+
+template <int BM>
+struct NtCfg {
+  static constexpr int NTH = BM * 2;         // BM/32 waves of 64x64 outputs
+  static constexpr int BK = BM >= 512 ? 32 : 64;
+  static constexpr int CH = BK / 8;           // 16-B chunks per LDS row
+  static constexpr int A_CH = BM * CH, B_CH = NBN * CH;
+  static constexpr int NA = (A_CH + NTH - 1) / NTH, NB = (B_CH + NTH - 1) / NTH;
+  static constexpr int STAGE = (BM + NBN) * BK * 2;  // bytes per K-tile (A + B)
+  static constexpr int SR = BM > 256 ? 256 : BM;     // rows per epilogue staging pass
+  static constexpr int LDS = 2 * STAGE > SR * SLD * 4 ? 2 * STAGE : SR * SLD * 4;
+};
 
 __device__ __forceinline__ int xcd_tile(int b, int nb) {
   const int q = nb / 8, r = nb % 8, x = b % 8, slot = b / 8;
   return x < r ? x * (q + 1) + slot : r * (q + 1) + (x - r) * q + slot;
 }
 
+// Per-thread staging plan, computed once: which 16-B chunks of the A/B tiles this thread moves,
+// their global element offsets at k = 0 (rows clamped at the edge: those rows only feed
+// discarded outputs) and their swizzled LDS offsets.  The K loop then only adds k0.
+template <int BM>
+struct NtPlan {
+  using C = NtCfg<BM>;
+  int64_t ga[C::NA], gb[C::NB];
+  int la[C::NA], lb[C::NB];
+  __device__ __forceinline__ NtPlan(const GemmParams &p, int bm, int bn) {
+#pragma unroll
+    for (int i = 0; i < C::NA; ++i) {
+      const int v = min((int)threadIdx.x + C::NTH * i, C::A_CH - 1), row = v / C::CH, ch = v % C::CH;
+      ga[i] = (int64_t)min(bm + row, p.M - 1) * p.lda + ch * 8;
+      la[i] = row * C::BK + ((ch ^ (row & (C::CH - 1))) * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < C::NB; ++i) {
+      const int v = min((int)threadIdx.x + C::NTH * i, C::B_CH - 1), row = v / C::CH, ch = v % C::CH;
+      gb[i] = (int64_t)min(bn + row, p.N - 1) * p.ldb + ch * 8;
+      lb[i] = row * C::BK + ((ch ^ (row & (C::CH - 1))) * 8);
+    }
+  }
+};
+
+template <int BM>
 struct NtStage {
-  uint4 a[4], b[4];
-  // thread t, i < 4: chunk v = t + 256 i -> row v >> 3, 16-B chunk v & 7 of the 64-wide K tile
-  __device__ __forceinline__ static uint4 ld(const bf16_t *X, int ld, int row, int rlim, int k,
-                                             int kend) {
-    row = min(row, rlim - 1);  // rows past the edge compute discarded outputs
-    const bf16_t *src = X + (int64_t)row * ld + k;
-    if (k + 8 <= kend) return *reinterpret_cast<const uint4 *>(src);
+  using C = NtCfg<BM>;
+  uint4 a[C::NA], b[C::NB];
+  static __device__ __forceinline__ uint4 edge(const bf16_t *src, int k, int kend) {
     bf16_t tmp[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) tmp[e] = k + e < kend ? src[e] : (bf16_t)0;
     return *reinterpret_cast<const uint4 *>(tmp);
   }
-  __device__ __forceinline__ void load(const GemmParams &p, const bf16_t *A, const bf16_t *B,
-                                       int bm, int bn, int k0, int kend) {
+  __device__ __forceinline__ void load(const NtPlan<BM> &pl, const bf16_t *A, const bf16_t *B,
+                                       int k0, int kend) {
+    if (k0 + C::BK <= kend) {  // whole K-tile inside [.., kend): plain 16-B loads
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int v = threadIdx.x + 256 * i, row = v >> 3, k = k0 + (v & 7) * 8;
-      a[i] = ld(A, p.lda, bm + row, p.M, k, kend);
-      b[i] = ld(B, p.ldb, bn + row, p.N, k, kend);
+      for (int i = 0; i < C::NA; ++i) a[i] = *reinterpret_cast<const uint4 *>(A + pl.ga[i] + k0);
+#pragma unroll
+      for (int i = 0; i < C::NB; ++i) b[i] = *reinterpret_cast<const uint4 *>(B + pl.gb[i] + k0);
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < C::NA; ++i) {
+      const int kc = k0 + (int)((threadIdx.x + C::NTH * i) % C::CH) * 8;
+      a[i] = kc + 8 <= kend ? *reinterpret_cast<const uint4 *>(A + pl.ga[i] + k0)
+                            : edge(A + pl.ga[i] + k0, kc, kend);
+    }
+#pragma unroll
+    for (int i = 0; i < C::NB; ++i) {
+      const int kc = k0 + (int)((threadIdx.x + C::NTH * i) % C::CH) * 8;
+      b[i] = kc + 8 <= kend ? *reinterpret_cast<const uint4 *>(B + pl.gb[i] + k0)
+                            : edge(B + pl.gb[i] + k0, kc, kend);
     }
   }
-  __device__ __forceinline__ void store(bf16_t *As, bf16_t *Bs) const {
+  __device__ __forceinline__ void store(const NtPlan<BM> &pl, bf16_t *As, bf16_t *Bs) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int v = threadIdx.x + 256 * i, row = v >> 3, ch = (v & 7) ^ (row & 7);
-      *reinterpret_cast<uint4 *>(As + row * NBK + ch * 8) = a[i];
-      *reinterpret_cast<uint4 *>(Bs + row * NBK + ch * 8) = b[i];
-    }
+    for (int i = 0; i < C::NA; ++i)
+      if (C::A_CH % C::NTH == 0 || (int)threadIdx.x + C::NTH * i < C::A_CH)
+        *reinterpret_cast<uint4 *>(As + pl.la[i]) = a[i];
+#pragma unroll
+    for (int i = 0; i < C::NB; ++i)
+      if (C::B_CH % C::NTH == 0 || (int)threadIdx.x + C::NTH * i < C::B_CH)
+        *reinterpret_cast<uint4 *>(Bs + pl.lb[i]) = b[i];
   }
 };
 
+template <int BK>
 __device__ __forceinline__ bf16x8_t nt_frag(const bf16_t *S, int row, int c) {
-  return *reinterpret_cast<const bf16x8_t *>(S + row * NBK + ((c ^ (row & 7)) * 8));
+  return *reinterpret_cast<const bf16x8_t *>(S + row * BK + ((c ^ (row & (BK / 8 - 1))) * 8));
 }
 
-// Output staging: the finished 128x128 tile (post-epilogue fp32) goes through LDS so that
-// every global store is a full 16-B segment of a row of C / Cf, or of a row of C^T.
-constexpr int SLD = NBN + 1;  // odd row pitch: column reads for C^T spread over the banks
-constexpr int NT_LDS_BYTES = NBM * SLD * 4 > 2 * (NBM + NBN) * NBK * 2 ? NBM * SLD * 4
-                                                                       : 2 * (NBM + NBN) * NBK * 2;
+// sigmoid_cross_entropy_with_logits (TF 2.5 Keras BCE on a Sigmoid output): returns
+// dz = (sigmoid(z) - y) * scale and adds the element's loss when `live`.
+__device__ __forceinline__ float bce_dz(float z, uint32_t ybit, float scale, float &loss, bool live) {
+  const float y = (float)ybit;
+  const float e = __expf(-fabsf(z));  // in (0, 1]
+  const float rp = __fdividef(1.f, 1.f + e);
+  if (live) loss += fmaxf(z, 0.f) - z * y + __logf(1.f + e);  // log1p(exp(-|z|))
+  const float sig = z >= 0.f ? rp : e * rp;
+  return (sig - y) * scale;
+}
 
-template <int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_nt_bf16_kernel(GemmParams p, int tiles_m) {
-  __shared__ __attribute__((aligned(16))) char smem[NT_LDS_BYTES];
-  __shared__ uint32_t ys[NBM][NBN / 32];  // BCE targets of the tile
-  __shared__ double red[4];
-  bf16_t(*As)[NBM * NBK] = reinterpret_cast<bf16_t(*)[NBM * NBK]>(smem);
-  bf16_t(*Bs)[NBN * NBK] = reinterpret_cast<bf16_t(*)[NBN * NBK]>(smem + 2 * NBM * NBK * 2);
+template <int EPI, int BM>
+__global__ __launch_bounds__(NtCfg<BM>::NTH) void gemm_nt_bf16_kernel(GemmParams p, int tiles_m) {
+  using C = NtCfg<BM>;
+  constexpr bool kBceRegs = BM <= 128;  // BCE math on the accumulators (no register pressure)
+  constexpr int BK = C::BK, NTH = C::NTH;
+  __shared__ __attribute__((aligned(16))) char smem[C::LDS];
+  __shared__ uint32_t ys[BM][NBN / 32];  // BCE targets of the tile
+  __shared__ double red[NTH / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
-  const int bm = (tile % tiles_m) * NBM, bn = (tile / tiles_m) * NBN;
+  const int bm = (tile % tiles_m) * BM, bn = (tile / tiles_m) * NBN;
   int kbeg = 0, kend = p.K;
   if constexpr (EPI == CC_EPI_SPLITK) {
-    const int kchunk = (int)cdiv(cdiv(p.K, p.splits), NBK) * NBK;
+    const int kchunk = (int)cdiv(cdiv(p.K, p.splits), BK) * BK;
     kbeg = blockIdx.y * kchunk;
     kend = min(p.K, kbeg + kchunk);
   }
   if constexpr (EPI == CC_EPI_BCE) {  // lands during the K loop
     const int YW = (p.N + 31) >> 5;
-    for (int i = threadIdx.x; i < NBM * (NBN / 32); i += 256) {
+    for (int i = threadIdx.x; i < BM * (NBN / 32); i += NTH) {
       const int r = i / (NBN / 32), w = i % (NBN / 32);
       const int gm = bm + r, gw = (bn >> 5) + w;
       ys[r][w] = gm < p.M && gw < YW ? p.y_bits[(int64_t)gm * YW + gw] : 0u;
     }
   }
+  bf16_t *AsBase = reinterpret_cast<bf16_t *>(smem);
+  bf16_t *BsBase = AsBase + 2 * BM * BK;
   const bf16_t *__restrict__ A = reinterpret_cast<const bf16_t *>(p.A);
   const bf16_t *__restrict__ B = reinterpret_cast<const bf16_t *>(p.B);
   f32x16_t acc[2][2];
@@ -353,16 +415,16 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_bf16_kernel(GemmParams p, int 
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   const bool do_cs = p.colsum != nullptr && bm == 0 && threadIdx.x < NBN;
   float cs = 0.f;
-  // D-deep register ring: K-tiles t+1 .. t+D-1 are in flight while tile t's MFMAs run (a tile's
-  // compute is far shorter than a global round trip, so one tile of look-ahead leaves the loop
-  // latency-bound).  LDS stays double-buffered: tile t lives in buffer t & 1.
+  // D-deep register ring: K-tiles t+1 .. t+D-1 are in flight while tile t's MFMAs run; LDS is
+  // double-buffered: tile t lives in buffer t & 1.
   constexpr int D = NT_RING;
-  NtStage st[D];
-  const int nk = kbeg < kend ? (int)cdiv(kend - kbeg, NBK) : 0;
+  const NtPlan<BM> pl(p, bm, bn);
+  NtStage<BM> st[D];
+  const int nk = kbeg < kend ? (int)cdiv(kend - kbeg, BK) : 0;
 #pragma unroll
   for (int q = 0; q < D; ++q)
-    if (q < nk) st[q].load(p, A, B, bm, bn, kbeg + q * NBK, kend);
-  if (nk > 0) st[0].store(As[0], Bs[0]);
+    if (q < nk) st[q].load(pl, A, B, kbeg + q * BK, kend);
+  if (nk > 0) st[0].store(pl, AsBase, BsBase);
   __syncthreads();
   const int ar = wm * 64 + (lane & 31), br = wn * 64 + (lane & 31);
   for (int t0 = 0; t0 < nk; t0 += D) {
@@ -370,12 +432,12 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_bf16_kernel(GemmParams p, int 
     for (int q = 0; q < D; ++q) {
       const int t = t0 + q;
       if (t >= nk) break;
-      const bf16_t *as = As[t & 1], *bs = Bs[t & 1];
+      const bf16_t *as = AsBase + (t & 1) * BM * BK, *bs = BsBase + (t & 1) * NBN * BK;
 #pragma unroll
-      for (int kk = 0; kk < NBK / 16; ++kk) {
+      for (int kk = 0; kk < BK / 16; ++kk) {
         const int c = 2 * kk + half;
-        const bf16x8_t a0 = nt_frag(as, ar, c), a1 = nt_frag(as, ar + 32, c);
-        const bf16x8_t b0 = nt_frag(bs, br, c), b1 = nt_frag(bs, br + 32, c);
+        const bf16x8_t a0 = nt_frag<BK>(as, ar, c), a1 = nt_frag<BK>(as, ar + 32, c);
+        const bf16x8_t b0 = nt_frag<BK>(bs, br, c), b1 = nt_frag<BK>(bs, br + 32, c);
         acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
         acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
         acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
@@ -384,15 +446,16 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_bf16_kernel(GemmParams p, int 
       if (do_cs) {  // bias gradient: sum of B row n over k, ascending k
         const int n = threadIdx.x;
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const bf16_t *qq = bs + n * NBK + ((c ^ (n & 7)) * 8);
+        for (int c = 0; c < BK / 8; ++c) {
+          const bf16_t *qq = bs + n * BK + ((c ^ (n & (BK / 8 - 1))) * 8);
 #pragma unroll
           for (int e = 0; e < 8; ++e) cs += bf2f(qq[e]);
         }
       }
       // slot q held tile t (already in LDS); refill it with tile t + D, publish tile t + 1
-      if (t + D < nk) st[q].load(p, A, B, bm, bn, kbeg + (t + D) * NBK, kend);
-      if (t + 1 < nk) st[(q + 1) % D].store(As[(t + 1) & 1], Bs[(t + 1) & 1]);
+      if (t + D < nk) st[q].load(pl, A, B, kbeg + (t + D) * BK, kend);
+      if (t + 1 < nk)
+        st[(q + 1) % D].store(pl, AsBase + ((t + 1) & 1) * BM * BK, BsBase + ((t + 1) & 1) * NBN * BK);
       __syncthreads();
     }
   }
@@ -401,54 +464,61 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_bf16_kernel(GemmParams p, int 
     p.colsum[zo + bn + threadIdx.x] = cs;
   }
 
-  // ---- epilogue: post-op fp32 tile -> LDS -> coalesced stores
-  float *S = reinterpret_cast<float *>(smem);  // [NBM][SLD] (the K loop's buffers are done)
+  // ---- epilogue: post-op fp32 tile -> LDS (passes of SR rows) -> coalesced stores
+  float *S = reinterpret_cast<float *>(smem);  // [SR][SLD] (the K loop's buffers are done)
   float lossf = 0.f;
   const float scale = p.scale;
+  float *Cf = p.Cf;
+  int64_t ldf = p.ldc;
+  if constexpr (EPI == CC_EPI_SPLITK) {
+    Cf = p.Cf + (int64_t)blockIdx.y * p.M * p.N;
+    ldf = p.N;
+  }
+  bf16_t *Cb = EPI == CC_EPI_SPLITK ? nullptr : reinterpret_cast<bf16_t *>(p.C);
+  const bool vec = ((ldf & 3) == 0) && ((p.ldc & 3) == 0);
+#pragma unroll 1
+  for (int r0 = 0; r0 < BM; r0 += C::SR) {
+    if (wm * 64 >= r0 && wm * 64 < r0 + C::SR) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < 2; ++i) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int lc = wn * 64 + j * 32 + (lane & 31), gn = bn + lc;
-      const int lr0 = wm * 64 + i * 32 + 4 * half;
-      float bias = 0.f;
-      if constexpr (EPI == CC_EPI_STORE || EPI == CC_EPI_BCE)
-        bias = p.bias && gn < p.N ? p.bias[gn] : 0.f;
+        for (int j = 0; j < 2; ++j) {
+          const int lc = wn * 64 + j * 32 + (lane & 31), gn = bn + lc;
+          const int lr0 = wm * 64 + i * 32 + 4 * half;
+          float bias = 0.f;
+          if constexpr (EPI == CC_EPI_STORE || EPI == CC_EPI_BCE)
+            bias = p.bias && gn < p.N ? p.bias[gn] : 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int lr = lr0 + (r & 3) + 8 * (r >> 2);
-        float v = acc[i][j][r];
-        if constexpr (EPI == CC_EPI_STORE) {
-          v += bias;
-          if (p.relu) v = v > 0.f ? v : 0.f;
-        } else if constexpr (EPI == CC_EPI_BCE) {
-          // sigmoid_cross_entropy_with_logits (TF 2.5 Keras BCE on a Sigmoid output)
-          const float z = v + bias;
-          const float y = (float)((ys[lr][lc >> 5] >> (lc & 31)) & 1u);
-          const float e = __expf(-fabsf(z));
-          const float rp = __fdividef(1.f, 1.f + e);
-          if (bm + lr < p.M && gn < p.N) lossf += fmaxf(z, 0.f) - z * y + __logf(1.f + e);
-          const float sig = z >= 0.f ? rp : e * rp;
-          v = (sig - y) * scale;
+          for (int r = 0; r < 16; ++r) {
+            const int lr = lr0 + (r & 3) + 8 * (r >> 2);
+            float v = acc[i][j][r] + bias;
+            if constexpr (EPI == CC_EPI_STORE) {
+              if (p.relu) v = v > 0.f ? v : 0.f;
+            } else if constexpr (EPI == CC_EPI_BCE && kBceRegs) {
+              v = bce_dz(v, (ys[lr][lc >> 5] >> (lc & 31)) & 1u, scale, lossf,
+                         bm + lr < p.M && gn < p.N);
+            }
+            S[(lr - r0) * SLD + lc] = v;        // BCE (!kBceRegs): the logit, transformed below
+          }
         }
-        S[lr * SLD + lc] = v;
       }
     }
-  }
-  __syncthreads();
-  // rows of C / Cf: thread -> 4 consecutive columns
-  {
-    float *Cf = p.Cf;
-    int64_t ldf = p.ldc;
-    if constexpr (EPI == CC_EPI_SPLITK) {
-      Cf = p.Cf + (int64_t)blockIdx.y * p.M * p.N;
-      ldf = p.N;
+    __syncthreads();
+    if constexpr (EPI == CC_EPI_BCE && !kBceRegs) {
+      // taller tiles: the transcendental work runs from LDS so it does not hold the
+      // accumulators' registers (z -> dz in place)
+      for (int idx = threadIdx.x; idx < C::SR * NBN; idx += NTH) {
+        const int lr = idx / NBN, lc = idx % NBN;
+        float &z = S[lr * SLD + lc];
+        z = bce_dz(z, (ys[r0 + lr][lc >> 5] >> (lc & 31)) & 1u, scale, lossf,
+                   bm + r0 + lr < p.M && bn + lc < p.N);
+      }
+      __syncthreads();
     }
-    bf16_t *Cb = EPI == CC_EPI_SPLITK ? nullptr : reinterpret_cast<bf16_t *>(p.C);
-    const bool vec = ((ldf & 3) == 0) && ((p.ldc & 3) == 0);
-    for (int idx = threadIdx.x; idx < NBM * (NBN / 4); idx += 256) {
+    // rows of C / Cf: thread -> 4 consecutive columns
+    for (int idx = threadIdx.x; idx < C::SR * (NBN / 4); idx += NTH) {
       const int lr = idx / (NBN / 4), lc = (idx % (NBN / 4)) * 4;
-      const int gm = bm + lr, gn = bn + lc;
+      const int gm = bm + r0 + lr, gn = bn + lc;
       if (gm >= p.M || gn >= p.N) continue;
       const float v0 = S[lr * SLD + lc], v1 = S[lr * SLD + lc + 1];
       const float v2 = S[lr * SLD + lc + 2], v3 = S[lr * SLD + lc + 3];
@@ -467,44 +537,70 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_bf16_kernel(GemmParams p, int 
         }
       }
     }
-  }
-  if constexpr (EPI == CC_EPI_BCE) {
-    // rows of C^T [N][M] (the k-contiguous operand of dW = D3^T dZ): thread -> 8 consecutive m
-    if (p.Ct) {
-      bf16_t *Ct = reinterpret_cast<bf16_t *>(p.Ct);
-      const bool vec = (p.ldct & 7) == 0;
-      for (int idx = threadIdx.x; idx < NBN * (NBM / 8); idx += 256) {
-        const int lc = idx / (NBM / 8), lr = (idx % (NBM / 8)) * 8;
-        const int gn = bn + lc, gm = bm + lr;
-        if (gn >= p.N || gm >= p.M) continue;
-        float v[8];
+    if constexpr (EPI == CC_EPI_BCE) {
+      // rows of C^T [N][M] for this pass's rows: thread -> 8 consecutive m
+      if (p.Ct) {
+        bf16_t *Ct = reinterpret_cast<bf16_t *>(p.Ct);
+        const bool vt = (p.ldct & 7) == 0;
+        for (int idx = threadIdx.x; idx < NBN * (C::SR / 8); idx += NTH) {
+          const int lc = idx / (C::SR / 8), lr = (idx % (C::SR / 8)) * 8;
+          const int gn = bn + lc, gm = bm + r0 + lr;
+          if (gn >= p.N || gm >= p.M) continue;
+          float v[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = S[(lr + e) * SLD + lc];
-        bf16_t *dst = Ct + (int64_t)gn * p.ldct + gm;
-        if (vec && gm + 7 < p.M) {
-          uint4 pk;
-          pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          pk.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-          pk.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-          *reinterpret_cast<uint4 *>(dst) = pk;
-        } else {
-          for (int e = 0; e < 8 && gm + e < p.M; ++e) dst[e] = f2bf(v[e]);
+          for (int e = 0; e < 8; ++e) v[e] = S[(lr + e) * SLD + lc];
+          bf16_t *dst = Ct + (int64_t)gn * p.ldct + gm;
+          if (vt && gm + 7 < p.M) {
+            uint4 pk;
+            pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+            pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+            pk.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+            pk.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+            *reinterpret_cast<uint4 *>(dst) = pk;
+          } else {
+            for (int e = 0; e < 8 && gm + e < p.M; ++e) dst[e] = f2bf(v[e]);
+          }
         }
       }
     }
-    const double sum = block_sum_double((double)lossf, red);
-    if (threadIdx.x == 0) p.loss_partials[tile] = sum;
+    __syncthreads();
+  }
+  if constexpr (EPI == CC_EPI_BCE) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) lossf += __shfl_xor(lossf, off);
+    double lv = (double)lossf;
+    if (lane == 0) red[wave] = lv;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double sum = 0.0;
+      for (int w = 0; w < NTH / 64; ++w) sum += red[w];
+      p.loss_partials[tile] = sum;
+    }
   }
 }
 
-template <int EPI>
-int launch_nt(const cc_gemm_args *g, const GemmParams &p, hipStream_t s) {
-  const int tm = (int)cdiv(g->M, NBM), tn = (int)cdiv(g->N, NBN);
+template <int EPI, int BM>
+int launch_nt_bm(const cc_gemm_args *g, const GemmParams &p, hipStream_t s) {
+  const int tm = (int)cdiv(g->M, BM), tn = (int)cdiv(g->N, NBN);
   const dim3 grid((unsigned)(tm * tn), EPI == CC_EPI_SPLITK ? (unsigned)g->splits : 1u);
-  hipLaunchKernelGGL(gemm_nt_bf16_kernel<EPI>, grid, dim3(256), 0, s, p, tm);
+  hipLaunchKernelGGL((gemm_nt_bf16_kernel<EPI, BM>), grid, dim3(NtCfg<BM>::NTH), 0, s, p, tm);
   CC_LAUNCH_CHECK("gemm_nt_bf16_kernel");
   return CC_OK;
+}
+
+// Tile height: 128 rows by default (taller tiles read each B panel fewer times but measured
+// slower on the decoder shapes, tools/micro/gemm_bench.py); CCREC_NT_BM=256/512 selects them.
+template <int EPI>
+int launch_nt(const cc_gemm_args *g, const GemmParams &p, hipStream_t s) {
+  static const int forced = [] {  // A/B switch for benchmarking tile heights
+    const char *e = getenv("CCREC_NT_BM");
+    return e ? atoi(e) : 0;
+  }();
+  int bm = 128;  // measured fastest for the decoder shapes (K = 256 / 512 / split V)
+  if (forced == 128 || forced == 256 || forced == 512) bm = forced;
+  if (bm == 512) return launch_nt_bm<EPI, 512>(g, p, s);
+  if (bm == 256) return launch_nt_bm<EPI, 256>(g, p, s);
+  return launch_nt_bm<EPI, 128>(g, p, s);
 }
 
 template <typename T, int EPI, int BK>

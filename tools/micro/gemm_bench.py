@@ -5,7 +5,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, '.')
+sys.path.insert(0, __import__('os').path.join(__import__('os').path.dirname(__import__('os').path.abspath(__file__)), '..', '..'))
 from cubecobrarecommender_amd import _lib as L  # noqa: E402
 
 B, V, d, SPL = 512, 22000, 256, 16
@@ -40,41 +40,50 @@ def gemm(M, N, K, A, lda, Bp, ldb, epi, **kw):
     L.call('cc_gemm', C.byref(g), L.stream_ptr())
 
 
-variants = {
-    'bce+C+Ct': lambda: gemm(B, V, d, D3, d, WoT, d, L.CC_EPI_BCE, bias=bias, C=Cb, y_bits=ybits,
-                             loss_partials=part, Ct=Ct, ldct=B),
-    'bce+C': lambda: gemm(B, V, d, D3, d, WoT, d, L.CC_EPI_BCE, bias=bias, C=Cb, y_bits=ybits,
-                          loss_partials=part),
-    'store_bf16': lambda: gemm(B, V, d, D3, d, WoT, d, L.CC_EPI_STORE, C=Cb),
-    'compute_only': lambda: gemm(B, V, d, D3, d, WoT, d, L.CC_EPI_STORE),
-    'dW+colsum': lambda: gemm(d, V, B, D3t, B, dZt, B, L.CC_EPI_STORE, Cf=gW, colsum=gb),
-    'dX_splitk': lambda: gemm(B, d, V, dZ, V, Wo, V, L.CC_EPI_SPLITK, Cf=split, splits=SPL),
-}
-for name, fn in variants.items():
-    for _ in range(3):
-        fn()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(50):
-        fn()
-    e1.record()
-    torch.cuda.synchronize()
-    print(f'{name:14s} {e0.elapsed_time(e1) / 50 * 1000:8.1f} us', flush=True)
+def main(only=None):
+    variants = {
+        'bce+C+Ct': lambda: gemm(B, V, d, D3, d, WoT, d, L.CC_EPI_BCE, bias=bias, C=Cb, y_bits=ybits,
+                                 loss_partials=part, Ct=Ct, ldct=B),
+        'bce+C': lambda: gemm(B, V, d, D3, d, WoT, d, L.CC_EPI_BCE, bias=bias, C=Cb, y_bits=ybits,
+                              loss_partials=part),
+        'store_bf16': lambda: gemm(B, V, d, D3, d, WoT, d, L.CC_EPI_STORE, C=Cb),
+        'compute_only': lambda: gemm(B, V, d, D3, d, WoT, d, L.CC_EPI_STORE),
+        'dW+colsum': lambda: gemm(d, V, B, D3t, B, dZt, B, L.CC_EPI_STORE, Cf=gW, colsum=gb),
+        'dX_splitk': lambda: gemm(B, d, V, dZ, V, Wo, V, L.CC_EPI_SPLITK, Cf=split, splits=SPL),
+    }
+    for name, fn in variants.items():
+        if only and name != only:
+            continue
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(50):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        print(f'{name:14s} {e0.elapsed_time(e1) / 50 * 1000:8.1f} us', flush=True)
 
-# steady-state reference shapes (compute only)
-for (M, N, K) in ((512, 22016, 2048), (4096, 4096, 4096), (512, 22016, 256)):
-    A = torch.randn(M, K, **bf)
-    Bt = torch.randn(N, K, **bf)
-    fn = lambda: gemm(M, N, K, A, K, Bt, K, L.CC_EPI_STORE)
-    for _ in range(3):
-        fn()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(20):
-        fn()
-    e1.record()
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) / 20 * 1000
-    print(f'{M}x{N}x{K} compute-only {us:8.1f} us  {2 * M * N * K / us / 1e6:7.1f} TFLOP/s', flush=True)
+    if only:
+        return
+    # steady-state reference shapes (compute only)
+    for (M, N, K) in ((512, 22016, 2048), (4096, 4096, 4096), (512, 22016, 256)):
+        A = torch.randn(M, K, **bf)
+        Bt = torch.randn(N, K, **bf)
+        fn = lambda: gemm(M, N, K, A, K, Bt, K, L.CC_EPI_STORE)
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / 20 * 1000
+        print(f'{M}x{N}x{K} compute-only {us:8.1f} us  {2 * M * N * K / us / 1e6:7.1f} TFLOP/s', flush=True)
+
+
+if __name__ == '__main__':
+    main(sys.argv[1] if len(sys.argv) > 1 else None)
