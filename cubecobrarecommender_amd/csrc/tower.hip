@@ -132,6 +132,16 @@ __device__ void load_block(const T *__restrict__ g, int W, int r0, T *Xr, int ld
   }
 }
 
+// row-major block copy with a given block size (16-B vectors; W % 8 == 0, ldx % 8 == 0)
+template <typename T, int THREADS>
+__device__ void load_block_n(const T *__restrict__ g, int W, int r0, T *Xr, int ldx) {
+  constexpr int VW = 16 / sizeof(T);
+  const int per = W / VW, nv = RB * per;
+  const uint4 *src = reinterpret_cast<const uint4 *>(g + (int64_t)r0 * W);
+  for (int i = threadIdx.x; i < nv; i += THREADS)
+    *reinterpret_cast<uint4 *>(Xr + (i / per) * ldx + (i % per) * VW) = src[i];
+}
+
 // transposed copy: Xt[col][row] = g[r0 + row][col] for the block's RB rows (16-B global loads)
 template <typename T>
 __device__ void load_block_t(const T *__restrict__ g, int W, int r0, T *Xt, int ldt) {
@@ -256,6 +266,149 @@ __global__ __launch_bounds__(NT) void tower_bwd_chain_kernel(TowerP p) {
         } else {
           T tv;
           DT<T>::st(&tv, v);
+          Gr[row * ldx + col] = tv;
+          gout[go] = tv;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ bf16 fast path (d <= 256)
+// Same math as the kernels above, shaped for latency: 8 waves, one 32-column output tile per
+// wave per layer, and the NEXT layer's weight fragments are loaded into registers while the
+// current layer's MFMAs run — weights do not depend on the activations, so every layer after
+// the first starts with its operands already in flight.
+constexpr int FNT = 512;  // 8 waves
+constexpr int FB = 16;    // fragments per tile: reduction length <= 256
+
+struct Frags {
+  bf16x8_t f[FB];
+};
+// B fragments of the 32-column tile n0 of a [rows][K] k-contiguous matrix (rows = output cols)
+__device__ __forceinline__ void issue_frags(Frags &F, const bf16_t *__restrict__ W, int K, int n0) {
+  const int lane = threadIdx.x & 63;
+  const bf16_t *row = W + (int64_t)(n0 + (lane & 31)) * K + 8 * (lane >> 5);
+#pragma unroll
+  for (int j = 0; j < FB; ++j)
+    if (16 * j < K) F.f[j] = *reinterpret_cast<const bf16x8_t *>(row + 16 * j);
+}
+__device__ __forceinline__ void consume_frags(const Frags &F, const bf16_t *A, int lda, int K,
+                                              f32x16_t &acc) {
+  const int lane = threadIdx.x & 63;
+  const bf16_t *arow = A + (lane & 31) * lda + 8 * (lane >> 5);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int j = 0; j < FB; ++j)
+    if (16 * j < K)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8_t *>(arow + 16 * j),
+                                                    F.f[j], acc, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int ldx = p.maxw + 8;
+  bf16_t *X0 = reinterpret_cast<bf16_t *>(smem);
+  bf16_t *X1 = X0 + RB * ldx;
+  const int r0 = blockIdx.x * RB;
+  const bool reg = r0 >= p.B;
+  const int t = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  Frags fr[2];
+  {
+    int K, N;
+    chain_dims(p.d, 0, K, N);
+    if (t < N / 32) issue_frags(fr[0], reinterpret_cast<const bf16_t *>(p.wt[0]), K, 32 * t);
+  }
+  load_block_n<bf16_t, FNT>(reinterpret_cast<const bf16_t *>(p.act[0]), p.d, r0, X0, ldx);
+  __syncthreads();
+  bf16_t *xin = X0, *xout = X1;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int l = i < 3 ? i : i + (reg ? 3 : 0);
+    int K, N;
+    chain_dims(p.d, i, K, N);
+    if (i < 5) {  // next layer's weights fly during this layer
+      const int ln = i + 1 < 3 ? i + 1 : i + 1 + (reg ? 3 : 0);
+      int Kn, Nn;
+      chain_dims(p.d, i + 1, Kn, Nn);
+      if (t < Nn / 32) issue_frags(fr[(i + 1) & 1], reinterpret_cast<const bf16_t *>(p.wt[ln]), Kn, 32 * t);
+    }
+    if (t < N / 32) {
+      f32x16_t acc;
+      consume_frags(fr[i & 1], xin, ldx, K, acc);
+      const int col = 32 * t + (lane & 31);
+      const float bb = p.b[l][col];
+      bf16_t *gout = reinterpret_cast<bf16_t *>(p.act[i + 1]);
+      bf16_t tv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = acc_row(r, lane);
+        float v = acc[r] + bb;
+        v = v > 0.f ? v : 0.f;
+        tv[r] = f2bf(v);
+        xout[row * ldx + col] = tv[r];
+        gout[(int64_t)(r0 + row) * N + col] = tv[r];
+      }
+      if (i == 5 && p.act6t) {  // D3^T [d][R]: registers 4g..4g+3 = 4 consecutive rows
+        bf16_t *dt = reinterpret_cast<bf16_t *>(p.act6t) + (int64_t)col * p.R + r0 + 4 * (lane >> 5);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<uint2 *>(dt + 8 * g) = *reinterpret_cast<const uint2 *>(&tv[4 * g]);
+      }
+    }
+    __syncthreads();
+    bf16_t *tmp = xin;
+    xin = xout;
+    xout = tmp;
+  }
+}
+
+__global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int ldx = p.maxw + 8;
+  bf16_t *Gr = reinterpret_cast<bf16_t *>(smem);
+  const int r0 = blockIdx.x * RB;
+  const bool reg = r0 >= p.B;
+  const int t = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  Frags fr[2];
+  auto issue_layer = [&](int i, int slot) {
+    const int l = i < 3 ? i : i + (reg ? 3 : 0);
+    int K, N;
+    chain_dims(p.d, i, K, N);
+    if (t < K / 32) issue_frags(fr[slot], reinterpret_cast<const bf16_t *>(p.w[l]), N, 32 * t);
+  };
+  issue_layer(5, 1);
+  load_block_n<bf16_t, FNT>(reinterpret_cast<const bf16_t *>(p.gD3), p.d, r0, Gr, ldx);
+  __syncthreads();
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    int K, N;
+    chain_dims(p.d, i, K, N);
+    if (i > 0) issue_layer(i - 1, (i - 1) & 1);
+    // the layer input's ReLU mask at this lane's accumulator positions: lands during the MFMAs
+    const int col = 32 * t + (lane & 31);
+    bf16_t hm[16];
+    if (t < K / 32) {
+      const bf16_t *H = reinterpret_cast<const bf16_t *>(p.act[i]);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) hm[r] = H[(int64_t)(r0 + acc_row(r, lane)) * K + col];
+    }
+    f32x16_t acc;
+    if (t < K / 32) consume_frags(fr[i & 1], Gr, ldx, N, acc);
+    __syncthreads();  // every wave has finished reading Gr
+    if (t < K / 32) {
+      bf16_t *gout = i > 0 ? reinterpret_cast<bf16_t *>(p.gact[i - 1]) : nullptr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = acc_row(r, lane);
+        const int64_t go = (int64_t)(r0 + row) * K + col;
+        const float v = bf2f(hm[r]) > 0.f ? acc[r] : 0.f;
+        if (i == 0) {
+          p.gpre1[go] = v;
+        } else {
+          const bf16_t tv = f2bf(v);
           Gr[row * ldx + col] = tv;
           gout[go] = tv;
         }
@@ -394,7 +547,9 @@ extern "C" int cc_tower_fwd(const cc_tower_args *t, void *stream) {
   if (rc) return rc;
   const int es = t->dtype == CC_BF16 ? 2 : 4;
   const size_t lds = (size_t)2 * RB * (p.maxw + 16 / es) * es;
-  if (t->dtype == CC_BF16)
+  if (t->dtype == CC_BF16 && p.d <= 256)
+    hipLaunchKernelGGL(tower_fwd_fast_kernel, dim3(p.R / RB), dim3(FNT), lds, as_stream(stream), p);
+  else if (t->dtype == CC_BF16)
     hipLaunchKernelGGL(tower_fwd_kernel<bf16_t>, dim3(p.R / RB), dim3(NT), lds, as_stream(stream), p);
   else
     hipLaunchKernelGGL(tower_fwd_kernel<float>, dim3(p.R / RB), dim3(NT), lds, as_stream(stream), p);
@@ -413,7 +568,10 @@ extern "C" int cc_tower_bwd(const cc_tower_args *t, void *stream) {
   const size_t lds_dw = (size_t)2 * p.maxw * (RB + 16 / es) * es;
   const dim3 gc(p.R / RB), gd(6 * (p.R / RB));
   if (t->dtype == CC_BF16) {
-    hipLaunchKernelGGL(tower_bwd_chain_kernel<bf16_t>, gc, dim3(NT), lds_chain, as_stream(stream), p);
+    if (p.d <= 256)
+      hipLaunchKernelGGL(tower_bwd_chain_fast_kernel, gc, dim3(FNT), lds_chain, as_stream(stream), p);
+    else
+      hipLaunchKernelGGL(tower_bwd_chain_kernel<bf16_t>, gc, dim3(NT), lds_chain, as_stream(stream), p);
     hipLaunchKernelGGL(tower_dw_kernel<bf16_t>, gd, dim3(NT), lds_dw, as_stream(stream), p);
   } else {
     hipLaunchKernelGGL(tower_bwd_chain_kernel<float>, gc, dim3(NT), lds_chain, as_stream(stream), p);
