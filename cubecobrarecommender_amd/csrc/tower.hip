@@ -316,30 +316,36 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
   const bool reg = r0 >= p.B;
   const int t = threadIdx.x >> 6, lane = threadIdx.x & 63;
   Frags fr[2];
+  float bias[2] = {0.f, 0.f};
   {
     int K, N;
     chain_dims(p.d, 0, K, N);
-    if (t < N / 32) issue_frags(fr[0], reinterpret_cast<const bf16_t *>(p.wt[0]), K, 32 * t);
+    if (t < N / 32) {
+      issue_frags(fr[0], reinterpret_cast<const bf16_t *>(p.wt[0]), K, 32 * t);
+      bias[0] = p.b[0][32 * t + (lane & 31)];
+    }
   }
   load_block_n<bf16_t, FNT>(reinterpret_cast<const bf16_t *>(p.act[0]), p.d, r0, X0, ldx);
   __syncthreads();
   bf16_t *xin = X0, *xout = X1;
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    const int l = i < 3 ? i : i + (reg ? 3 : 0);
     int K, N;
     chain_dims(p.d, i, K, N);
     if (i < 5) {  // next layer's weights fly during this layer
       const int ln = i + 1 < 3 ? i + 1 : i + 1 + (reg ? 3 : 0);
       int Kn, Nn;
       chain_dims(p.d, i + 1, Kn, Nn);
-      if (t < Nn / 32) issue_frags(fr[(i + 1) & 1], reinterpret_cast<const bf16_t *>(p.wt[ln]), Kn, 32 * t);
+      if (t < Nn / 32) {
+        issue_frags(fr[(i + 1) & 1], reinterpret_cast<const bf16_t *>(p.wt[ln]), Kn, 32 * t);
+        bias[(i + 1) & 1] = p.b[ln][32 * t + (lane & 31)];
+      }
     }
     if (t < N / 32) {
       f32x16_t acc;
       consume_frags(fr[i & 1], xin, ldx, K, acc);
       const int col = 32 * t + (lane & 31);
-      const float bb = p.b[l][col];
+      const float bb = bias[i & 1];
       bf16_t *gout = reinterpret_cast<bf16_t *>(p.act[i + 1]);
       bf16_t tv[16];
 #pragma unroll
