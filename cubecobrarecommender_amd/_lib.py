@@ -78,6 +78,8 @@ SIGNATURES = {
     'cc_tower_slab_elems': (_I64, [_I32]),
     'cc_tower_fwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_bwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
+    'cc_tower_bwd_chain': (C.c_int, [C.POINTER(TowerArgs), _P]),
+    'cc_tower_bwd_dw': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_reduce': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_transpose': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_topn_workspace_size': (_SZ, [_I32]),

@@ -115,7 +115,7 @@ __global__ __launch_bounds__(256) void gather_kernel(const T *__restrict__ table
 template <int EPL>
 __global__ __launch_bounds__(256) void scatter_bwd_kernel(const float *__restrict__ dpre, int V,
                                                           int d, int R,
-                                                          const uint32_t *__restrict__ xt,
+                                                          const uint32_t *xt,
                                                           float *__restrict__ grad,
                                                           float *__restrict__ bias_grad) {
   constexpr int U = 8;
@@ -161,6 +161,10 @@ __global__ __launch_bounds__(256) void scatter_bwd_kernel(const float *__restric
       for (int e = 0; e < EPL; ++e) acc[e] += v[e];
     }
   }
+  // consume the bitmask: this wave is the only reader of words [w0, w1) of the row, and every
+  // one of its loads above has been used, so clearing leaves xt zeroed for the next step's F
+  if (row < V)
+    for (int wd = w0 + lane; wd < w1; wd += 64) const_cast<uint32_t *>(bits)[wd] = 0u;
   if (w > 0) {
 #pragma unroll
     for (int e = 0; e < EPL; ++e) part[w - 1][c0 + e] = acc[e];

@@ -563,7 +563,7 @@ extern "C" int cc_tower_fwd(const cc_tower_args *t, void *stream) {
   return CC_OK;
 }
 
-extern "C" int cc_tower_bwd(const cc_tower_args *t, void *stream) {
+static int tower_bwd_launch(const cc_tower_args *t, void *stream, bool chain, bool dw) {
   TowerP p;
   int rc = make_params(t, p);
   if (rc) return rc;
@@ -573,18 +573,29 @@ extern "C" int cc_tower_bwd(const cc_tower_args *t, void *stream) {
   const size_t lds_chain = (size_t)2 * RB * (p.maxw + 16 / es) * es;
   const size_t lds_dw = (size_t)2 * p.maxw * (RB + 16 / es) * es;
   const dim3 gc(p.R / RB), gd(6 * (p.R / RB));
+  hipStream_t s = as_stream(stream);
   if (t->dtype == CC_BF16) {
-    if (p.d <= 256)
-      hipLaunchKernelGGL(tower_bwd_chain_fast_kernel, gc, dim3(FNT), lds_chain, as_stream(stream), p);
-    else
-      hipLaunchKernelGGL(tower_bwd_chain_kernel<bf16_t>, gc, dim3(NT), lds_chain, as_stream(stream), p);
-    hipLaunchKernelGGL(tower_dw_kernel<bf16_t>, gd, dim3(NT), lds_dw, as_stream(stream), p);
+    if (chain && p.d <= 256)
+      hipLaunchKernelGGL(tower_bwd_chain_fast_kernel, gc, dim3(FNT), lds_chain, s, p);
+    else if (chain)
+      hipLaunchKernelGGL(tower_bwd_chain_kernel<bf16_t>, gc, dim3(NT), lds_chain, s, p);
+    if (dw) hipLaunchKernelGGL(tower_dw_kernel<bf16_t>, gd, dim3(NT), lds_dw, s, p);
   } else {
-    hipLaunchKernelGGL(tower_bwd_chain_kernel<float>, gc, dim3(NT), lds_chain, as_stream(stream), p);
-    hipLaunchKernelGGL(tower_dw_kernel<float>, gd, dim3(NT), lds_dw, as_stream(stream), p);
+    if (chain) hipLaunchKernelGGL(tower_bwd_chain_kernel<float>, gc, dim3(NT), lds_chain, s, p);
+    if (dw) hipLaunchKernelGGL(tower_dw_kernel<float>, gd, dim3(NT), lds_dw, s, p);
   }
   CC_LAUNCH_CHECK("tower_bwd kernels");
   return CC_OK;
+}
+
+extern "C" int cc_tower_bwd(const cc_tower_args *t, void *stream) {
+  return tower_bwd_launch(t, stream, true, true);
+}
+extern "C" int cc_tower_bwd_chain(const cc_tower_args *t, void *stream) {
+  return tower_bwd_launch(t, stream, true, false);
+}
+extern "C" int cc_tower_bwd_dw(const cc_tower_args *t, void *stream) {
+  return tower_bwd_launch(t, stream, false, true);
 }
 
 extern "C" int cc_tower_reduce(const cc_tower_args *t, void *stream) {

@@ -10,6 +10,8 @@ torch is used only to own device memory and the stream; every computation is a H
 """
 from dataclasses import dataclass
 
+import os
+
 import numpy as np
 import torch
 
@@ -173,21 +175,40 @@ class Trainer:
         self.perms = None
         self.batches_per_epoch = max(1, data.C // (B * cfg.world))   # generator.py:36 (__len__)
         self.graphs = None
+        self.side = torch.cuda.Stream(device=self.dev)   # dW / slab reduce / losses / transposes
+        self.overlap = os.environ.get('CCREC_OVERLAP', '0') == '1'   # measured slower (graph branches), off
         self.timing = False          # bench.py: HIP events around the main kernels
         self.events = {}
 
-    def _tick(self, name):
-        """Record a HIP event on the current stream (bench timing); returns a closer."""
+    def _tick(self, name, stream=None):
+        """Record a HIP event on the launching stream (bench timing); returns a closer."""
         if not self.timing:
             return lambda: None
         e0 = torch.cuda.Event(enable_timing=True)
-        e0.record()
+        e0.record(stream)
 
         def close():
             e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
+            e1.record(stream)
             self.events.setdefault(name, []).append((e0, e1))
         return close
+
+    # ---- a second stream for work off the critical path (graph branches when captured)
+    def _fork(self):
+        """The side stream starts after everything issued so far on the current stream."""
+        if not self.overlap:
+            return L.stream_ptr(None)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self.side.wait_event(ev)
+        return L.stream_ptr(self.side)
+
+    def _join(self):
+        if not self.overlap:
+            return
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        torch.cuda.current_stream().wait_event(ev)
 
     def kernel_times_ms(self):
         """Average duration (ms) per instrumented kernel over the recorded launches."""
@@ -272,12 +293,12 @@ class Trainer:
 
     def _gemm(self, M, N, K, A, lda, B, ldb, ta=0, tb=0, epi=L.CC_EPI_STORE, ldc=None, bias=None,
               relu=0, C=None, Cf=None, H=None, y_bits=None, scale=0.0, partials=None, splits=1,
-              colsum=None, Ct=None, ldct=0):
+              colsum=None, Ct=None, ldct=0, stream=None):
         g = L.GemmArgs(dtype=self.dtype, ta=ta, tb=tb, epilogue=epi, M=M, N=N, K=K, lda=lda,
                        ldb=ldb, ldc=ldc if ldc is not None else N, splits=splits, relu=relu,
                        A=A, B=B, bias=bias, C=C, Cf=Cf, H=H, y_bits=y_bits, scale=scale,
                        loss_partials=partials, colsum=colsum, Ct=Ct, ldct=ldct)
-        L.call('cc_gemm', L.C.byref(g), self._s)
+        L.call('cc_gemm', L.C.byref(g), stream if stream is not None else self._s)
 
     def _dense_fwd(self, X, rows, K, N, name, out):
         """out[rows] = relu(X[rows] @ W + b) (model.py Dense(relu))."""
@@ -318,8 +339,8 @@ class Trainer:
         V, d, B, R = cfg.V, cfg.d, cfg.batch_size, self.R
         self._s = L.stream_ptr(stream)
         s = self._s
-        # ---- F: noise + reg rows (generator.py:38-103)
-        self.xt_bits.zero_()
+        # ---- F: noise + reg rows (generator.py:38-103); xt_bits arrives zeroed (the previous
+        # step's cc_embed_scatter_bwd consumes it)
         na = self._noise_args()
         t = self._tick('cc_noise_fwd')
         L.call('cc_noise_fwd', L.C.byref(na), s)
@@ -355,8 +376,9 @@ class Trainer:
                        epi=L.CC_EPI_BCE, bias=self.pf('decoder/reconstruct/bias'), C=L.ptr(self.dZout),
                        y_bits=L.ptr(self.y_bits), scale=1.0 / (B * V), partials=L.ptr(self.bce_part))
         t()
+        ss = self._fork()          # off the critical path: loss reductions, output-layer dW
         L.call('cc_reduce_loss', L.ptr(self.bce_part), self.bce_part.numel(), 1.0 / (B * V),
-               L.ptr(self.loss_dev), s)
+               L.ptr(self.loss_dev), ss)
         # ---- D2 output + softmax + KL vs M~ rows (model.py:98; train.py:85)
         if self.use_reg:
             if self.fused_tower:
@@ -367,17 +389,21 @@ class Trainer:
                            bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2))
             L.call('cc_dec_softmax_kl_fused', self.dtype, L.ptr(self.Z2), B, V, L.ptr(self.data.y_reg),
                    L.ptr(self.reg_idx), float(cfg.reg), L.ptr(self.dZout[B:]), L.ptr(self.kl_part), s)
-            L.call('cc_reduce_loss', L.ptr(self.kl_part), B, 1.0 / B, L.ptr(self.loss_dev[1:]), s)
-        # ---- backward through the output layers and decoder towers
+            ss = self._fork()
+            L.call('cc_reduce_loss', L.ptr(self.kl_part), B, 1.0 / B, L.ptr(self.loss_dev[1:]), ss)
+        # ---- backward through the output layers and decoder towers.  The output layers' dW
+        # (side stream) and dX -> towers (this stream) only share read-only inputs.
         for pre, (r0, r1) in branches:
             dz = self.dZout[r0:]
-            t = self._tick('dec_dW')
+            t = self._tick('dec_dW', self.side if self.overlap else None)
             if self.fused_tower and r0 == 0:   # dW = D3^T dZ with both operands k-contiguous
                 self._gemm(d, V, B, L.ptr(self.D3t), R, L.ptr(self.dZt), B, ta=0, tb=1,
-                           Cf=self.gp(pre + '/reconstruct/kernel'), colsum=self.gp(pre + '/reconstruct/bias'))
+                           Cf=self.gp(pre + '/reconstruct/kernel'), colsum=self.gp(pre + '/reconstruct/bias'),
+                           stream=ss)
             else:
                 self._gemm(d, V, B, L.ptr(self.D3[r0:]), d, L.ptr(dz), V, ta=1, tb=0,
-                           Cf=self.gp(pre + '/reconstruct/kernel'), colsum=self.gp(pre + '/reconstruct/bias'))
+                           Cf=self.gp(pre + '/reconstruct/kernel'), colsum=self.gp(pre + '/reconstruct/bias'),
+                           stream=ss)
             t()
             t = self._tick('dec_dX')
             self._gemm(B, d, V, L.ptr(dz), V, self.w(pre + '/reconstruct/kernel'), V, ta=0, tb=1,
@@ -390,6 +416,7 @@ class Trainer:
                 self._dense_bwd(self.D2, self.gD3, rows, 256, d, pre + '/decoded_3', gIn=self.gD2, mask=self.D2)
                 self._dense_bwd(self.D1, self.gD2, rows, 128, 256, pre + '/decoded_2', gIn=self.gD1, mask=self.D1)
                 self._dense_bwd(self.Zl, self.gD1, rows, 64, 128, pre + '/decoded_1', gIn=self.gZl, mask=self.Zl)
+        self._join()
 
     def forward_backward_b(self, stream=None):
         """Towers backward (both branches' rows together through the shared encoder) and the E1
@@ -399,9 +426,11 @@ class Trainer:
         s = self._s
         if self.fused_tower:
             t = self._tick('cc_tower_bwd')
-            L.call('cc_tower_bwd', L.C.byref(self.targs), s)
+            L.call('cc_tower_bwd_chain', L.C.byref(self.targs), s)
             t()
-            L.call('cc_tower_reduce', L.C.byref(self.targs), s)
+            ss = self._fork()      # per-block dW slabs + their reduce overlap the E1 scatter
+            L.call('cc_tower_bwd_dw', L.C.byref(self.targs), ss)
+            L.call('cc_tower_reduce', L.C.byref(self.targs), ss)
         else:
             self._dense_bwd(self.H3, self.gZl, (0, R), 128, 64, 'encoder/bottleneck', gIn=self.gH3, mask=self.H3)
             self._dense_bwd(self.H2, self.gH3, (0, R), 256, 128, 'encoder/encoded_3', gIn=self.gH2, mask=self.H2)
@@ -410,6 +439,8 @@ class Trainer:
         L.call('cc_embed_scatter_bwd', L.ptr(self.gPre1), V, d, R, L.ptr(self.xt_bits),
                self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
         t()
+        if self.fused_tower:
+            self._join()
 
     def apply_adam(self, stream=None):
         """TF Adam over every trained parameter (+ bf16 shadow refresh)."""
@@ -422,7 +453,17 @@ class Trainer:
         t()
 
     def apply_rest(self, stream=None):
-        """Advance the device step/epoch counters and refresh the transposed operand copies."""
+        """Advance the device step/epoch counters and refresh the transposed operand copies
+        (the decoder's Wo^T on the side stream, concurrently)."""
+        if self.fused_tower and stream is None:
+            ss = self._fork()
+            for k, pre in enumerate(branches_of(self.use_reg)):
+                L.call('cc_transpose', self.dtype, self.w(pre + '/reconstruct/kernel'), self.cfg.d, self.cfg.V,
+                       L.ptr(self.WoT[k]), ss)
+            L.call('cc_state_advance', L.ptr(self.state), self.batches_per_epoch, L.stream_ptr(None))
+            L.call('cc_tower_transpose', L.C.byref(self.targs), L.stream_ptr(None))
+            self._join()
+            return
         L.call('cc_state_advance', L.ptr(self.state), self.batches_per_epoch, L.stream_ptr(stream))
         self.transpose_tower(stream)
 

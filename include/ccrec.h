@@ -107,7 +107,8 @@ int cc_embed_gather_fwd(int32_t dtype, const void *table, const float *bias, int
 
 /* ----------------------------------------------------------------------------------
  * E1 backward: dW1[r] = sum_{b : r in x_b} dpre[b] (ascending b, deterministic), for every
- * row r of W1 (dense, as TF's MatMul gradient is dense).  xt_bits [V, ceil(R/32)].
+ * row r of W1 (dense, as TF's MatMul gradient is dense).  xt_bits [V, ceil(R/32)] is CONSUMED:
+ * it is left all-zero, ready for the next step's cc_noise_fwd (which ORs bits into it).
  * Writes grad [V, d] fp32 and, when bias_grad != NULL, bias_grad[c] = sum_b dpre[b, c] (db1).
  * Replaces the MatMul/BiasAdd gradients of model.py:27 inside fit.
  * ---------------------------------------------------------------------------------- */
@@ -193,6 +194,10 @@ typedef struct cc_tower_args {
 int64_t cc_tower_slab_elems(int32_t d);
 int cc_tower_fwd(const cc_tower_args *t, void *stream);
 int cc_tower_bwd(const cc_tower_args *t, void *stream);
+/* cc_tower_bwd = cc_tower_bwd_chain (dX chain; writes gpre1 and every layer's dPre) followed by
+ * cc_tower_bwd_dw (per-block dW/db slabs); split so the slabs can overlap the E1 scatter. */
+int cc_tower_bwd_chain(const cc_tower_args *t, void *stream);
+int cc_tower_bwd_dw(const cc_tower_args *t, void *stream);
 int cc_tower_reduce(const cc_tower_args *t, void *stream);
 int cc_tower_transpose(const cc_tower_args *t, void *stream);
 
