@@ -4,7 +4,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get('CCREC_LIB', os.path.join(_HERE, 'libccrec_hip.so'))
+LIB_PATH = os.environ.get('CCREC_LIB') or os.path.join(_HERE, 'libccrec_hip.so')
 
 CC_F32, CC_BF16 = 0, 1
 CC_EPI_STORE, CC_EPI_BCE, CC_EPI_MASK, CC_EPI_SPLITK = 0, 1, 2, 3

@@ -53,6 +53,11 @@ __device__ __forceinline__ void load_row(const T *__restrict__ p, float (&v)[EPL
 // Forward: 4 waves per cube row, wave w sums the w-th quarter of the row's (sorted) card list
 // with U row loads in flight per lane; the four partials are added in wave order (deterministic).
 constexpr int GW = 4;
+// E1 backward: waves per W1 row (measured: 2 -> 49 us, 4 -> 46, 8 -> 62, 16 -> 130 at cfg 2).
+#ifndef CCREC_SCATTER_GW
+#define CCREC_SCATTER_GW 4
+#endif
+constexpr int SGW = CCREC_SCATTER_GW;
 
 template <typename T, int EPL>
 __global__ __launch_bounds__(256) void gather_kernel(const T *__restrict__ table,
@@ -113,13 +118,13 @@ __global__ __launch_bounds__(256) void gather_kernel(const T *__restrict__ table
 // quarter of the row's bit words, collecting up to U set bits before issuing their dPre loads
 // together (heavy Zipf rows have a set bit for nearly every batch row).  Partials added in wave order.
 template <int EPL>
-__global__ __launch_bounds__(256) void scatter_bwd_kernel(const float *__restrict__ dpre, int V,
+__global__ __launch_bounds__(64 * SGW) void scatter_bwd_kernel(const float *__restrict__ dpre, int V,
                                                           int d, int R,
                                                           const uint32_t *xt,
                                                           float *__restrict__ grad,
                                                           float *__restrict__ bias_grad) {
   constexpr int U = 8;
-  __shared__ float part[GW - 1][64 * EPL];
+  __shared__ float part[SGW - 1][64 * EPL];
   const int row = blockIdx.x;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int XW = (R + 31) >> 5;
@@ -128,7 +133,7 @@ __global__ __launch_bounds__(256) void scatter_bwd_kernel(const float *__restric
 #pragma unroll
   for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
   const uint32_t *bits = xt + (int64_t)row * XW;
-  const int q = (XW + GW - 1) / GW;
+  const int q = (XW + SGW - 1) / SGW;
   const int w0 = min(XW, w * q), w1 = min(XW, w0 + q);
   int pend[U];
   int np = 0;
@@ -174,7 +179,7 @@ __global__ __launch_bounds__(256) void scatter_bwd_kernel(const float *__restric
 #pragma unroll
     for (int e = 0; e < EPL; ++e)
 #pragma unroll
-      for (int p = 0; p < GW - 1; ++p) acc[e] += part[p][c0 + e];
+      for (int p = 0; p < SGW - 1; ++p) acc[e] += part[p][c0 + e];
     float *g = row == V ? bias_grad + c0 : grad + (int64_t)row * d + c0;
     if constexpr (EPL % 4 == 0) {
 #pragma unroll
@@ -228,7 +233,7 @@ extern "C" int cc_embed_scatter_bwd(const float *dpre, int32_t V, int32_t d, int
                                     void *stream) {
   CC_REQUIRE(dpre && xt_bits && grad, "cc_embed_scatter_bwd: null pointer");
   CC_REQUIRE(d % 64 == 0 && d >= 64 && d <= 1024, "cc_embed_scatter_bwd: d must be 64..1024, %64");
-  const dim3 grid((unsigned)(bias_grad ? V + 1 : V)), block(256);
+  const dim3 grid((unsigned)(bias_grad ? V + 1 : V)), block(64 * SGW);
   hipStream_t s = as_stream(stream);
   switch (d / 64) {
     case 1: hipLaunchKernelGGL((scatter_bwd_kernel<1>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
