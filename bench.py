@@ -238,7 +238,12 @@ def main():
         roof['measured'] = 'HIP events around the Adam kernel in every timed step (same stream)'
         roof['traffic'] = None
         if args.traffic_json and os.path.exists(args.traffic_json):
-            roof['traffic'] = json.load(open(args.traffic_json)).get('adam_kernel')
+            # PMC bytes were collected on one configuration: attach them only to the same launch
+            tj = json.load(open(args.traffic_json)).get('adam_kernel') or {}
+            tb = tj.get('bytes_per_launch')
+            if tb and abs(tb - roof['bytes_per_launch']) <= 0.02 * roof['bytes_per_launch']:
+                roof['traffic'] = tb
+                roof['traffic_detail'] = tj
     else:   # sharded Adam: this rank's 1/world shard of every bucket, per step
         torch.cuda.synchronize()
         ev = tr.sharded.adam_events

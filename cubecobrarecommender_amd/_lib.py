@@ -89,6 +89,8 @@ SIGNATURES = {
     'cc_recommend_graph_create': (C.c_int, [_P, _I32, _I32, _P, _P, _I32, _P, _P, _P, C.POINTER(C.c_void_p)]),
     'cc_recommend_graph_run': (C.c_int, [_P, _P, _I32]),
     'cc_recommend_graph_destroy': (C.c_int, [_P]),
+    'cc_adjacency_ws_size': (_SZ, [_I32, _I32, _I32, _I32]),
+    'cc_adjacency': (C.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
 }
 
 _lib = None

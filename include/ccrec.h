@@ -279,6 +279,24 @@ int cc_recommend_graph_create(const float *params, int32_t V, int32_t d, const i
 int cc_recommend_graph_run(void *handle, int32_t *res_host, int32_t res_words);
 int cc_recommend_graph_destroy(void *handle);
 
+/* ---------------------------------------------------------------- card co-occurrence graph (N1)
+ * Replaces src/non_ml/utils.py:75-91 (create_adjacency_matrix, called by
+ * src/non_ml/create_mtx.py:19) and the M~ normalisation of src/ml/train.py:69-71.
+ * Cubes arrive as CSR lists on the device: cube c holds card ids idx[row_ptr[c] .. row_ptr[c+1])
+ * (ids in [0, V), validated by the caller; duplicates collapse like the reference's dense 0/1
+ * matrix).  Outputs (any subset, each row-major [V][V], device):
+ *   counts   int32: |{cubes containing i and j}|                         (exact)
+ *   adj      f64:   M  = counts[i,j] / counts[i,i], unseen rows 0, diag := *force_diag if given
+ *                   (bit-exact with the reference's f64 M, the output/full_adj_mtx.npy format)
+ *   adj_norm f32:   M~ = (M, diag := 1) / rowsum, an unseen row e_i (train.py:69-71)
+ * chunk_cubes > 0 bounds the transposed 0/1 matrix held in the workspace to V x chunk bytes;
+ * <= 0 processes all cubes at once.  with_counts says whether `counts` will be passed (it then
+ * doubles as the accumulator across chunks). */
+size_t cc_adjacency_ws_size(int32_t V, int32_t C, int32_t chunk_cubes, int32_t with_counts);
+int cc_adjacency(const int32_t *row_ptr, const int32_t *idx, int32_t C, int32_t V,
+                 int32_t chunk_cubes, const double *force_diag, void *ws, int32_t *counts,
+                 double *adj, float *adj_norm, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
