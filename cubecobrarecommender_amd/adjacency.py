@@ -2,8 +2,8 @@
 
 Replaces ``create_adjacency_matrix`` (src/non_ml/utils.py:75-91, run by
 src/non_ml/create_mtx.py:19) and the M~ normalisation of src/ml/train.py:69-71 with one C-ABI
-call, ``cc_adjacency`` (csrc/cooccur.hip): an int8 MFMA GEMM of the transposed 0/1 cube matrix
-with itself (exact int32 counts, upper-triangle tiles only) whose epilogue writes
+call, ``cc_adjacency`` (csrc/cooccur.hip): an FP4 (MX-scaled) MFMA GEMM of the transposed 0/1 cube matrix
+with itself (exact counts, upper-triangle tiles only) whose epilogue writes
 
     counts  int32  |{cubes containing i and j}|
     M       f64    counts[i, j] / counts[i, i]; rows of unseen cards 0; diag := force_diag
@@ -45,16 +45,20 @@ def _device_lists(indptr, indices, V, device):
     return rp, ix, len(indptr) - 1
 
 
-def adjacency_gpu(indptr, indices, V, outputs=('M',), force_diag=None, chunk_cubes=0,
-                  device='cuda', stream=None):
-    """Returns a dict with the requested outputs among 'counts', 'M', 'Mt' (device tensors)."""
+def upload_lists(indptr, indices, V, device='cuda'):
+    """Validate CSR cube lists on the host and copy them to the device (int32)."""
+    return _device_lists(indptr, indices, int(V), device)
+
+
+def adjacency_device(rp, ix, C, V, outputs=('M',), force_diag=None, chunk_cubes=0, stream=None):
+    """cc_adjacency on already-uploaded lists (see upload_lists); returns device tensors."""
     outputs = set(outputs)
     if not outputs or not outputs <= {'counts', 'M', 'Mt'}:
         raise ValueError("outputs must be a non-empty subset of {'counts', 'M', 'Mt'}")
     V = int(V)
     if V <= 0:
         raise ValueError('V must be positive')
-    rp, ix, C = _device_lists(indptr, indices, V, device)
+    device = rp.device
     L = _lib.lib()
     with_counts = 'counts' in outputs
     ws_bytes = L.cc_adjacency_ws_size(V, C, int(chunk_cubes), int(with_counts))
@@ -72,6 +76,15 @@ def adjacency_gpu(indptr, indices, V, outputs=('M',), force_diag=None, chunk_cub
                               _lib.ptr(out.get('Mt')), _lib.stream_ptr(stream)), 'cc_adjacency')
     del ws   # stream-ordered reuse by the caching allocator is safe
     return out
+
+
+def adjacency_gpu(indptr, indices, V, outputs=('M',), force_diag=None, chunk_cubes=0,
+                  device='cuda', stream=None):
+    """Returns a dict with the requested outputs among 'counts', 'M', 'Mt' (device tensors)."""
+    if int(V) <= 0:
+        raise ValueError('V must be positive')
+    rp, ix, C = upload_lists(indptr, indices, V, device)
+    return adjacency_device(rp, ix, C, V, outputs, force_diag, chunk_cubes, stream)
 
 
 def create_adjacency_matrix(cubes, verbose=False, force_diag=None, device='cuda'):
