@@ -70,6 +70,8 @@ def roofline_for(name, ms, tr):
     if name == 'cc_adam_dense':
         n = tr.layout.total if tr.use_reg else tr.layout.main_total
         byt = n * (16 + 12 + 2)                    # read p,m,v,g; write p,m,v; write bf16 shadow
+        if getattr(tr, 'fused_adam', False):      # + the transposed bf16 operand copies
+            byt += 2 * sum(int(r.rows) * int(r.cols) for r in tr.adam_regions)
         return {'bound': 'hbm', 'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s', 'bytes_per_launch': byt}
     if name in ('dec_bce_fwd', 'dec_dW', 'dec_dX'):
@@ -181,25 +183,18 @@ def main():
             else:
                 tr.step_dp(timing=timed)
             return
-        if graphed:
-            tr.graphs[0].replay()
+        if timed and graphed:
+            # HIP events on the stream, bracketing the Adam kernel launched right behind the
+            # forward/backward graph: the host is far ahead of the GPU here, so the kernel is
+            # already queued when e0 fires and the interval is the kernel's own duration.
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            tr.run_fb()
+            tr.run_adam(events=(e0, e1))
+            adam_ev.append((e0, e1))
         else:
-            tr.forward_backward()
-        if graphed:
-            if timed:
-                # HIP events on the stream, bracketing the Adam kernel launched right behind the
-                # forward/backward graph: the host is far ahead of the GPU here, so the kernel is
-                # already queued when e0 fires and the interval is the kernel's own duration.
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                tr.apply_adam()
-                e1.record()
-                adam_ev.append((e0, e1))
-            else:
-                tr.graphs[1].replay()
-            tr.graphs[2].replay()
-        else:
-            tr.apply()
+            saved, tr.graphs = tr.graphs, (tr.graphs if graphed else None)
+            tr.step()
+            tr.graphs = saved
 
     # per-kernel durations (HIP events, eager launches of the same step) for the roofline
     tr.timing = True

@@ -37,7 +37,12 @@ class GemmArgs(C.Structure):
         ('A', C.c_void_p), ('B', C.c_void_p), ('bias', C.c_void_p), ('C', C.c_void_p),
         ('Cf', C.c_void_p), ('H', C.c_void_p), ('y_bits', C.c_void_p), ('scale', C.c_float),
         ('loss_partials', C.c_void_p), ('colsum', C.c_void_p), ('Ct', C.c_void_p), ('ldct', C.c_int32),
+        ('loss_out', C.c_void_p), ('loss_scale', C.c_double), ('ticket', C.c_void_p),
     ]
+
+
+class AdamTRegion(C.Structure):
+    _fields_ = [('off', C.c_int64), ('rows', C.c_int32), ('cols', C.c_int32), ('dst', C.c_void_p)]
 
 
 class TowerArgs(C.Structure):
@@ -70,6 +75,8 @@ SIGNATURES = {
     'cc_dec_softmax_kl_fused': (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _F32, _P, _P, _P]),
     'cc_reduce_loss': (C.c_int, [_P, _I32, _F64, _P, _P]),
     'cc_adam_dense': (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _F32, _F32, _F32, _F32, _P]),
+    'cc_adam_dense_t': (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _F32, _F32, _F32, _F32, _P, _I32,
+                                  _I64, _P]),
     'cc_to_bf16': (C.c_int, [_P, _P, _I64, _P]),
     'cc_state_advance': (C.c_int, [_P, _I64, _P]),
     'cc_infer_encode_ws_size': (_SZ, [_I32, _I32, _I32]),

@@ -75,6 +75,13 @@ __global__ __launch_bounds__(NT) void softmax_kl_kernel(const float *__restrict_
 
 // TF ResourceApplyAdam: alpha = lr sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1); v += (g^2-v)(1-b2);
 // p -= m*alpha/(sqrt(v)+eps).  t = state[0] + 1.
+__device__ __forceinline__ void adam_elem(float &p, float &m, float &v, float g, float alpha,
+                                          float omb1, float omb2, float eps) {
+  m += (g - m) * omb1;
+  v += (g * g - v) * omb2;
+  p -= (m * alpha) / (sqrtf(v) + eps);
+}
+
 __global__ __launch_bounds__(NT) void adam_kernel(float *__restrict__ p, float *__restrict__ m,
                                                   float *__restrict__ v,
                                                   const float *__restrict__ g,
@@ -95,11 +102,7 @@ __global__ __launch_bounds__(NT) void adam_kernel(float *__restrict__ p, float *
     float *pe = &pp.x, *me = &mm.x, *ve = &vv.x;
     const float *ge = &gg.x;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      me[e] += (ge[e] - me[e]) * omb1;
-      ve[e] += (ge[e] * ge[e] - ve[e]) * omb2;
-      pe[e] -= (me[e] * alpha) / (sqrtf(ve[e]) + eps);
-    }
+    for (int e = 0; e < 4; ++e) adam_elem(pe[e], me[e], ve[e], ge[e], alpha, omb1, omb2, eps);
     reinterpret_cast<float4 *>(p)[i] = pp;
     reinterpret_cast<float4 *>(m)[i] = mm;
     reinterpret_cast<float4 *>(v)[i] = vv;
@@ -113,10 +116,163 @@ __global__ __launch_bounds__(NT) void adam_kernel(float *__restrict__ p, float *
     }
   }
   for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    m[i] += (g[i] - m[i]) * omb1;
-    v[i] += (g[i] * g[i] - v[i]) * omb2;
-    p[i] -= (m[i] * alpha) / (sqrtf(v[i]) + eps);
-    if (shadow) shadow[i] = f2bf(p[i]);
+    float pp = p[i], mm = m[i], vv = v[i];
+    adam_elem(pp, mm, vv, g[i], alpha, omb1, omb2, eps);
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+    if (shadow) shadow[i] = f2bf(pp);
+  }
+}
+
+// Adam fused with the transposed bf16 operand copies (Wo^T, tower W^T): the flat blocks update
+// every element outside the regions; each tile block updates one 64x64 tile of a region's
+// [rows][cols] matrix, writes p/m/v and the bf16 shadow row-major, and the bf16 values
+// transposed to dst [cols][rows] through LDS (both stores coalesced).  Replaces cc_adam_dense
+// followed by cc_transpose / cc_tower_transpose (one launch, no re-read of the shadow).
+constexpr int MAXR = 12;
+struct TRegs {
+  int n;
+  int64_t off[MAXR], size[MAXR];
+  int rows[MAXR], cols[MAXR], tcols[MAXR];
+  int64_t tile0[MAXR + 1];
+  bf16_t *dst[MAXR];
+};
+
+__device__ __forceinline__ void adam_tile(float *__restrict__ p, float *__restrict__ m,
+                                          float *__restrict__ v, const float *__restrict__ g,
+                                          bf16_t *__restrict__ shadow, const TRegs &tr,
+                                          int flat_blocks, float alpha, float omb1, float omb2,
+                                          float eps);
+
+__global__ __launch_bounds__(NT) void adam_fused_kernel(float *__restrict__ p, float *__restrict__ m,
+                                                        float *__restrict__ v,
+                                                        const float *__restrict__ g,
+                                                        bf16_t *__restrict__ shadow, int64_t n4v,
+                                                        int64_t *state, float lr,
+                                                        float b1, float b2, float eps, TRegs tr,
+                                                        int flat_blocks, int64_t advance_bpe) {
+  const float t = (float)(state[0] + 1);
+  const float b1p = powf(b1, t), b2p = powf(b2, t);
+  const float alpha = lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  const float omb1 = 1.f - b1, omb2 = 1.f - b2;
+  if ((int)blockIdx.x < flat_blocks) {
+    const int64_t stride = (int64_t)flat_blocks * blockDim.x;
+    for (int64_t vi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; vi < n4v; vi += stride) {
+      int64_t e = vi << 2;  // virtual (regions removed) -> physical element index
+      for (int k = 0; k < tr.n; ++k)
+        if (e >= tr.off[k]) e += tr.size[k];
+      const int64_t i = e >> 2;
+      float4 pp = reinterpret_cast<float4 *>(p)[i];
+      float4 mm = reinterpret_cast<float4 *>(m)[i];
+      float4 vv = reinterpret_cast<float4 *>(v)[i];
+      const float4 gg = reinterpret_cast<const float4 *>(g)[i];
+      float *pe = &pp.x, *me = &mm.x, *ve = &vv.x;
+      const float *ge = &gg.x;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) adam_elem(pe[q], me[q], ve[q], ge[q], alpha, omb1, omb2, eps);
+      reinterpret_cast<float4 *>(p)[i] = pp;
+      reinterpret_cast<float4 *>(m)[i] = mm;
+      reinterpret_cast<float4 *>(v)[i] = vv;
+      ushort4 sh;
+      sh.x = f2bf(pp.x);
+      sh.y = f2bf(pp.y);
+      sh.z = f2bf(pp.z);
+      sh.w = f2bf(pp.w);
+      reinterpret_cast<ushort4 *>(shadow)[i] = sh;
+    }
+  } else {
+    adam_tile(p, m, v, g, shadow, tr, flat_blocks, alpha, omb1, omb2, eps);
+  }
+  if (advance_bpe > 0) {  // the last block to finish advances {step, batch, epoch}
+    __syncthreads();
+    if (threadIdx.x == 0) {  // no data hand-off: the ticket alone orders the counter update
+      const unsigned long long tk = atomicAdd(reinterpret_cast<unsigned long long *>(state + 3), 1ull);
+      if (tk == (unsigned long long)gridDim.x - 1) {  // every block has read state[0]
+        state[0] += 1;
+        state[1] += 1;
+        if (state[1] >= advance_bpe) {
+          state[1] = 0;
+          state[2] += 1;
+        }
+        state[3] = 0;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void adam_tile(float *__restrict__ p, float *__restrict__ m,
+                                          float *__restrict__ v, const float *__restrict__ g,
+                                          bf16_t *__restrict__ shadow, const TRegs &tr,
+                                          int flat_blocks, float alpha, float omb1, float omb2,
+                                          float eps) {
+  __shared__ bf16_t T[64][66];
+  const int64_t tb = (int64_t)blockIdx.x - flat_blocks;
+  int k = 0;
+  while (k + 1 < tr.n && tb >= tr.tile0[k + 1]) ++k;
+  const int64_t tl = tb - tr.tile0[k];
+  const int rows = tr.rows[k], cols = tr.cols[k];
+  const int r0 = (int)(tl / tr.tcols[k]) * 64, c0 = (int)(tl % tr.tcols[k]) * 64;
+  const int64_t base = tr.off[k];
+  // 64 x 64 tile as 1024 float4 (16 per row): every load of the thread is issued before any
+  // math (a load -> math -> store chain per element would expose the memory latency 16 times)
+  constexpr int Q = 64 * 16 / NT;
+  float4 P4[Q], M4[Q], V4[Q], G4[Q];
+  bool ok[Q];
+#pragma unroll
+  for (int qq = 0; qq < Q; ++qq) {
+    const int q = threadIdx.x + NT * qq, rr = q >> 4, c = c0 + (q & 15) * 4, r = r0 + rr;
+    ok[qq] = r < rows && c + 3 < cols && (cols & 3) == 0;
+    if (ok[qq]) {
+      const int64_t i4 = (base + (int64_t)r * cols + c) >> 2;
+      P4[qq] = reinterpret_cast<const float4 *>(p)[i4];
+      M4[qq] = reinterpret_cast<const float4 *>(m)[i4];
+      V4[qq] = reinterpret_cast<const float4 *>(v)[i4];
+      G4[qq] = reinterpret_cast<const float4 *>(g)[i4];
+    }
+  }
+#pragma unroll
+  for (int qq = 0; qq < Q; ++qq) {
+    const int q = threadIdx.x + NT * qq, rr = q >> 4, cl = (q & 15) * 4, c = c0 + cl, r = r0 + rr;
+    if (ok[qq]) {
+      float *pe = &P4[qq].x, *me = &M4[qq].x, *ve = &V4[qq].x;
+      const float *ge = &G4[qq].x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) adam_elem(pe[e], me[e], ve[e], ge[e], alpha, omb1, omb2, eps);
+      const int64_t i4 = (base + (int64_t)r * cols + c) >> 2;
+      reinterpret_cast<float4 *>(p)[i4] = P4[qq];
+      reinterpret_cast<float4 *>(m)[i4] = M4[qq];
+      reinterpret_cast<float4 *>(v)[i4] = V4[qq];
+      ushort4 sh;
+      sh.x = f2bf(pe[0]);
+      sh.y = f2bf(pe[1]);
+      sh.z = f2bf(pe[2]);
+      sh.w = f2bf(pe[3]);
+      reinterpret_cast<ushort4 *>(shadow)[i4] = sh;
+      T[rr][cl] = sh.x;
+      T[rr][cl + 1] = sh.y;
+      T[rr][cl + 2] = sh.z;
+      T[rr][cl + 3] = sh.w;
+    } else if (r < rows) {  // ragged edge (or cols % 4 != 0): element by element
+      for (int e = 0; e < 4 && c + e < cols; ++e) {
+        const int64_t i = base + (int64_t)r * cols + c + e;
+        float pp = p[i], mm = m[i], vv = v[i];
+        adam_elem(pp, mm, vv, g[i], alpha, omb1, omb2, eps);
+        p[i] = pp;
+        m[i] = mm;
+        v[i] = vv;
+        const bf16_t b = f2bf(pp);
+        shadow[i] = b;
+        T[rr][cl + e] = b;
+      }
+    }
+  }
+  __syncthreads();
+  bf16_t *dst = tr.dst[k];
+  for (int e = threadIdx.x; e < 64 * 64; e += NT) {  // dst row c0 + e/64: 64 consecutive rows
+    const int cc = e >> 6, rr = e & 63;
+    const int c = c0 + cc, r = r0 + rr;
+    if (r < rows && c < cols) dst[(int64_t)c * rows + r] = T[rr][cc];
   }
 }
 
@@ -166,6 +322,49 @@ extern "C" int cc_adam_dense(float *p, float *m, float *v, const float *g, uint1
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(NT), 0, as_stream(stream), p, m, v,
                      g, (bf16_t *)shadow, n, state, lr, beta1, beta2, eps);
   CC_LAUNCH_CHECK("adam_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_adam_dense_t(float *p, float *m, float *v, const float *g, uint16_t *shadow,
+                               int64_t n, int64_t *state, float lr, float beta1,
+                               float beta2, float eps, const cc_adam_tregion *regions,
+                               int32_t nregions, int64_t advance_bpe, void *stream) {
+  CC_REQUIRE(p && m && v && g && state && shadow, "cc_adam_dense_t: null pointer");
+  CC_REQUIRE(((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g) % 16 == 0,
+             "cc_adam_dense_t: buffers must be 16-byte aligned");
+  CC_REQUIRE((uintptr_t)shadow % 8 == 0, "cc_adam_dense_t: shadow must be 8-byte aligned");
+  CC_REQUIRE(n % 4 == 0, "cc_adam_dense_t: n must be a multiple of 4");
+  CC_REQUIRE(nregions >= 0 && nregions <= MAXR && (nregions == 0 || regions),
+             "cc_adam_dense_t: 0..12 regions");
+  TRegs tr{};
+  tr.n = nregions;
+  int64_t covered = 0, prev_end = 0, tiles = 0;
+  for (int k = 0; k < nregions; ++k) {
+    const cc_adam_tregion &r = regions[k];
+    const int64_t size = (int64_t)r.rows * r.cols;
+    CC_REQUIRE(r.dst && r.rows > 0 && r.cols > 0, "cc_adam_dense_t: empty region");
+    CC_REQUIRE(r.off >= prev_end && r.off + size <= n, "cc_adam_dense_t: regions must be sorted, disjoint, in range");
+    CC_REQUIRE(r.off % 4 == 0 && size % 4 == 0, "cc_adam_dense_t: regions must be 4-element aligned");
+    tr.off[k] = r.off;
+    tr.size[k] = size;
+    tr.rows[k] = r.rows;
+    tr.cols[k] = r.cols;
+    tr.tcols[k] = (int)cdiv(r.cols, 64);
+    tr.dst[k] = (bf16_t *)r.dst;
+    tr.tile0[k] = tiles;
+    tiles += cdiv(r.rows, 64) * tr.tcols[k];
+    covered += size;
+    prev_end = r.off + size;
+  }
+  tr.tile0[nregions] = tiles;
+  const int64_t n4v = (n - covered) / 4;
+  const int flat_blocks = n4v > 0 ? (int)std::min<int64_t>(cdiv(n4v, NT), 256 * 8) : 0;
+  const int64_t blocks = flat_blocks + tiles;
+  if (blocks == 0) return CC_OK;
+  hipLaunchKernelGGL(adam_fused_kernel, dim3((unsigned)blocks), dim3(NT), 0, as_stream(stream), p,
+                     m, v, g, (bf16_t *)shadow, n4v, state, lr, beta1, beta2, eps, tr, flat_blocks,
+                     advance_bpe);
+  CC_LAUNCH_CHECK("adam_fused_kernel");
   return CC_OK;
 }
 

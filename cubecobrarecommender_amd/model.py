@@ -131,6 +131,7 @@ class CC_Recommender:
                 log(f'Epoch {ep + 1}/{epochs} - {steps} steps - {dt:.3f}s - loss: {l["loss"]:.6f} '
                     f'- bce: {l["bce"]:.6f} - kl: {l["kl"]:.6f} - {steps * cfg.batch_size * world / dt:.0f} cubes/s')
 
+        tr.flush()
         self.trainer = tr
         self._recommender = None
         self._step = int(tr.state[0].item())

@@ -117,7 +117,8 @@ class Trainer:
         self.grads = torch.zeros(P, **f32)
         self.shadow = torch.zeros(P, device=self.dev, dtype=torch.bfloat16) if self.dtype == L.CC_BF16 else None
         self.refresh_shadow()
-        self.state = torch.zeros(4, device=self.dev, dtype=torch.int64)   # {step, batch, epoch, 0}
+        self.state = torch.zeros(4, device=self.dev, dtype=torch.int64)   # {step, batch, epoch, ticket}
+        self.tickets = torch.zeros(4, device=self.dev, dtype=torch.int32)  # last-block hand-offs
         self.x_cap = max(1, data.max_n + int(data.max_n * 0.8) + 1)
         R, VW, XW = self.R, (V + 31) // 32, (self.R + 31) // 32
         i32 = dict(device=self.dev, dtype=torch.int32)
@@ -172,9 +173,19 @@ class Trainer:
             self.transpose_tower()
         else:
             self.targs = None
+        # one process: Adam also writes the transposed operand copies and advances the step
+        # counters (cc_adam_dense_t), so a step is two launches of graphs: fwd/bwd | Adam
+        # (measured: in the step the fused kernel ran 77 us against 56 + 8 + 4 + 5 for Adam,
+        # Wo^T, tower W^T and the counters — its 64x64 tiles read Wo with poor DRAM locality —
+        # so it is opt-in: CCREC_FUSED_ADAM=1)
+        self.fused_adam = (self.fused_tower and cfg.world == 1 and self.dtype == L.CC_BF16
+                           and os.environ.get('CCREC_FUSED_ADAM', '0') == '1')
+        self.adam_regions = self._adam_regions() if self.fused_adam else None
         self.perms = None
         self.batches_per_epoch = max(1, data.C // (B * cfg.world))   # generator.py:36 (__len__)
         self.graphs = None
+        self.pending_rest = False    # one process: step k's counters/transposes run at the head
+        #                              of step k+1's forward graph (one graph launch less per step)
         self.side = torch.cuda.Stream(device=self.dev)   # dW / slab reduce / losses / transposes
         self.overlap = os.environ.get('CCREC_OVERLAP', '0') == '1'   # measured slower (graph branches), off
         self.timing = False          # bench.py: HIP events around the main kernels
@@ -246,6 +257,25 @@ class Trainer:
         t.slab = self.slab.data_ptr()
         return t
 
+    def _adam_regions(self):
+        """Row-major weights whose bf16 values the forward reads transposed: the six (nine)
+        tower kernels -> wt, the output layers' kernels -> Wo^T; sorted by flat offset."""
+        n = self.layout.total if self.use_reg else self.layout.main_total
+        regs = []
+        for l, name in enumerate(self.tower_layers):
+            off = self.layout.offset(name + '/kernel')
+            K, N = self.layout.shape(name + '/kernel')
+            if off + K * N <= n:
+                regs.append((off, K, N, self.wt[int(self.wt_off[l]):].data_ptr()))
+        for k, pre in enumerate(branches_of(self.use_reg)):
+            off = self.layout.offset(pre + '/reconstruct/kernel')
+            regs.append((off, self.cfg.d, self.cfg.V, self.WoT[k].data_ptr()))
+        regs.sort()
+        arr = (L.AdamTRegion * len(regs))()
+        for i, (off, r, c, dst) in enumerate(regs):
+            arr[i].off, arr[i].rows, arr[i].cols, arr[i].dst = off, r, c, dst
+        return arr
+
     def transpose_tower(self, stream=None):
         """Refresh the transposed operand copies (tower W^T, decoder Wo^T) from the current weights."""
         if self.fused_tower:
@@ -293,11 +323,12 @@ class Trainer:
 
     def _gemm(self, M, N, K, A, lda, B, ldb, ta=0, tb=0, epi=L.CC_EPI_STORE, ldc=None, bias=None,
               relu=0, C=None, Cf=None, H=None, y_bits=None, scale=0.0, partials=None, splits=1,
-              colsum=None, Ct=None, ldct=0, stream=None):
+              colsum=None, Ct=None, ldct=0, stream=None, loss_out=None, loss_scale=0.0, ticket=None):
         g = L.GemmArgs(dtype=self.dtype, ta=ta, tb=tb, epilogue=epi, M=M, N=N, K=K, lda=lda,
                        ldb=ldb, ldc=ldc if ldc is not None else N, splits=splits, relu=relu,
                        A=A, B=B, bias=bias, C=C, Cf=Cf, H=H, y_bits=y_bits, scale=scale,
-                       loss_partials=partials, colsum=colsum, Ct=Ct, ldct=ldct)
+                       loss_partials=partials, colsum=colsum, Ct=Ct, ldct=ldct,
+                       loss_out=loss_out, loss_scale=loss_scale, ticket=ticket)
         L.call('cc_gemm', L.C.byref(g), stream if stream is not None else self._s)
 
     def _dense_fwd(self, X, rows, K, N, name, out):
@@ -328,6 +359,7 @@ class Trainer:
     # ------------------------------------------------------------------ the step
     def forward_backward(self, stream=None):
         """One step's gradients into self.grads (no optimizer): F, E, D1/D2 + losses, backward."""
+        self.flush(stream)
         self.forward_backward_a(stream)
         self.forward_backward_b(stream)
 
@@ -370,15 +402,16 @@ class Trainer:
             self._gemm(B, V, d, L.ptr(self.D3), d, L.ptr(self.WoT[0]), d, tb=1,
                        epi=L.CC_EPI_BCE, bias=self.pf('decoder/reconstruct/bias'), C=L.ptr(self.dZout),
                        y_bits=L.ptr(self.y_bits), scale=1.0 / (B * V), partials=L.ptr(self.bce_part),
-                       Ct=L.ptr(self.dZt), ldct=B)
+                       Ct=L.ptr(self.dZt), ldct=B, loss_out=L.ptr(self.loss_dev),
+                       loss_scale=1.0 / (B * V), ticket=L.ptr(self.tickets))
         else:
             self._gemm(B, V, d, L.ptr(self.D3), d, self.w('decoder/reconstruct/kernel'), V,
                        epi=L.CC_EPI_BCE, bias=self.pf('decoder/reconstruct/bias'), C=L.ptr(self.dZout),
-                       y_bits=L.ptr(self.y_bits), scale=1.0 / (B * V), partials=L.ptr(self.bce_part))
+                       y_bits=L.ptr(self.y_bits), scale=1.0 / (B * V), partials=L.ptr(self.bce_part),
+                       loss_out=L.ptr(self.loss_dev), loss_scale=1.0 / (B * V),
+                       ticket=L.ptr(self.tickets))
         t()
         ss = self._fork()          # off the critical path: loss reductions, output-layer dW
-        L.call('cc_reduce_loss', L.ptr(self.bce_part), self.bce_part.numel(), 1.0 / (B * V),
-               L.ptr(self.loss_dev), ss)
         # ---- D2 output + softmax + KL vs M~ rows (model.py:98; train.py:85)
         if self.use_reg:
             if self.fused_tower:
@@ -447,14 +480,23 @@ class Trainer:
         cfg = self.cfg
         n = self.layout.total if self.use_reg else self.layout.main_total
         t = self._tick('cc_adam_dense')
-        L.call('cc_adam_dense', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v), L.ptr(self.grads),
-               L.ptr(self.shadow), n, L.ptr(self.state), cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,
-               L.stream_ptr(stream))
+        if self.fused_adam:   # + transposed operand copies + step counters
+            L.call('cc_adam_dense_t', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v),
+                   L.ptr(self.grads), L.ptr(self.shadow), n, L.ptr(self.state), cfg.lr, cfg.beta1,
+                   cfg.beta2, cfg.eps, self.adam_regions, len(self.adam_regions),
+                   self.batches_per_epoch, L.stream_ptr(stream))
+        else:
+            L.call('cc_adam_dense', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v), L.ptr(self.grads),
+                   L.ptr(self.shadow), n, L.ptr(self.state), cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,
+                   L.stream_ptr(stream))
         t()
 
     def apply_rest(self, stream=None):
         """Advance the device step/epoch counters and refresh the transposed operand copies
-        (the decoder's Wo^T on the side stream, concurrently)."""
+        (the decoder's Wo^T on the side stream, concurrently).  With the fused Adam both are
+        already done."""
+        if self.fused_adam:
+            return
         if self.fused_tower and stream is None:
             ss = self._fork()
             for k, pre in enumerate(branches_of(self.use_reg)):
@@ -499,16 +541,41 @@ class Trainer:
             refresh_fn=lambda lo, hi: self.refresh_range(lo, hi),
             timing=timing)
 
+    def flush(self, stream=None):
+        """Run the previous step's deferred counters/transposes (before reading state or the
+        transposed operands from outside the step)."""
+        if self.pending_rest:
+            self.pending_rest = False
+            self.apply_rest(stream)
+
+    def run_fb(self, stream=None):
+        """Forward/backward of one step (graph replay or eager), preceded by the previous step's
+        deferred counters/transposes."""
+        if self.graphs is not None:
+            g_fb, _, _, g_main = self.graphs
+            (g_main if self.pending_rest and g_main is not None else g_fb).replay()
+            self.pending_rest = False
+        else:
+            self.forward_backward(stream)
+
+    def run_adam(self, stream=None, events=None):
+        """Adam (graph replay, or an eager launch bracketed by `events` = (e0, e1))."""
+        if events is not None:
+            events[0].record()
+            self.apply_adam(stream)
+            events[1].record()
+        elif self.graphs is not None:
+            self.graphs[1].replay()
+        else:
+            self.apply_adam(stream)
+        self.pending_rest = not self.fused_adam
+
     def step(self, stream=None):
         if self.cfg.world > 1:
             self.step_dp()
             return
-        if self.graphs is not None:
-            for g in self.graphs:
-                g.replay()
-            return
-        self.forward_backward(stream)
-        self.apply(stream)
+        self.run_fb(stream)
+        self.run_adam(stream)
 
     def capture(self):
         """Capture the step as three hipGraphs (torch.cuda.CUDAGraph over our own kernel launches):
@@ -518,6 +585,7 @@ class Trainer:
         device-resident, so replays are exact repeats of the eager step.  bench.py brackets the
         Adam kernel with HIP events to time the step's bytes-dominant kernel in the timed region."""
         timing, self.timing = self.timing, False
+        self.flush()
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream())
         saved = self.state.clone()
@@ -536,11 +604,20 @@ class Trainer:
                 self.forward_backward()
             with torch.cuda.graph(g_adam):
                 self.apply_adam()
-        with torch.cuda.graph(g_rest):
-            self.apply_rest()
+        g_main = None
+        if self.fused_adam:
+            g_rest = None
+        else:
+            with torch.cuda.graph(g_rest):
+                self.apply_rest()
+            if self.cfg.world == 1:   # rest of step k + forward/backward of step k+1
+                g_main = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g_main):
+                    self.apply_rest()
+                    self.forward_backward()
         torch.cuda.synchronize()
         self.state.copy_(saved)
-        self.graphs = (g_fb, g_adam, g_rest)
+        self.graphs = (g_fb, g_adam, g_rest, g_main)
         self.timing = timing
 
     # ------------------------------------------------------------------ inspection (tests)

@@ -147,6 +147,11 @@ typedef struct cc_gemm_args {
   void *Ct;             /* CC_EPI_BCE, optional: dZ^T [N][ldct] (dtype) — the k-contiguous operand of
                            dW = H^T dZ, written with packed stores from the accumulator registers */
   int32_t ldct;
+  double *loss_out;     /* CC_EPI_BCE, optional: loss_out[0] = sum(loss_partials) * loss_scale, in
+                           tile order (the same as cc_reduce_loss would give), computed by the
+                           kernel's last tile block */
+  double loss_scale;
+  uint32_t *ticket;     /* with loss_out: one zeroed word, left zeroed */
 } cc_gemm_args;
 int cc_gemm(const cc_gemm_args *g, void *stream);
 /* workspace bound for cc_gemm's loss partials: ceil(M/64)*ceil(N/64) doubles */
@@ -228,6 +233,22 @@ int cc_to_bf16(const float *x, uint16_t *y, int64_t n, void *stream);
 /* Device step state {step, batch_in_epoch, epoch, 0}: step += 1, batch += 1, and on reaching
  * batches_per_epoch: batch = 0, epoch += 1 (on_epoch_end, generator.py:68-72).  Keeping the
  * counters on the device makes a whole training step replayable as one hipGraph. */
+/* cc_adam_dense_t: cc_adam_dense over [0, n) (n % 4 == 0, shadow required) that also writes,
+ * for each region k (sorted, disjoint, 4-aligned), the updated bf16 values of the row-major
+ * [rows][cols] matrix at p + off transposed to dst [cols][rows] — the k-contiguous operand
+ * copies (decoder Wo^T, tower W^T) the forward reads.  One launch replaces cc_adam_dense +
+ * cc_transpose + cc_tower_transpose; identical values.  advance_bpe > 0 also performs
+ * cc_state_advance(state, advance_bpe) once every block has read the step (state[3] is the
+ * kernel's completion ticket and must be 0 between launches). */
+typedef struct cc_adam_tregion {
+  int64_t off;
+  int32_t rows, cols;
+  uint16_t *dst;
+} cc_adam_tregion;
+int cc_adam_dense_t(float *p, float *m, float *v, const float *g, uint16_t *shadow, int64_t n,
+                    int64_t *state, float lr, float beta1, float beta2, float eps,
+                    const cc_adam_tregion *regions, int32_t nregions, int64_t advance_bpe,
+                    void *stream);
 int cc_state_advance(int64_t *state, int64_t batches_per_epoch, void *stream);
 
 /* ----------------------------------------------------------------------------------

@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 import torch
 
+from cubecobrarecommender_amd import _lib as L
 from cubecobrarecommender_amd.layout import Layout
 from cubecobrarecommender_amd.trainer import DeviceDataset, TrainConfig, Trainer
 from oracle import model_ref, noise_ref
@@ -94,6 +95,46 @@ def test_adam_matches_tf_formula():
     assert rel_err(dm.cpu().numpy(), Mo['a']) < 1e-6 and rel_err(dv.cpu().numpy(), Vo['a']) < 1e-6
 
 
+@pytest.mark.parametrize('bpe', [0, 3])
+def test_adam_fused_transposes_and_counters(bpe):
+    """cc_adam_dense_t == cc_adam_dense + bf16 shadow + transposed copies of the regions
+    (bit-exact), and the completion-ticket state advance."""
+    rng = np.random.default_rng(7)
+    shapes = [(64, 256), (256, 130), (128, 64), (256, 700)]     # partial 64-tiles included
+    gap = 68
+    offs, n = [], 100
+    for r, c in shapes:
+        offs.append(n)
+        n += r * c + gap
+    n = (n + 3) // 4 * 4
+    p, m, g = (rng.standard_normal(n).astype(np.float32) for _ in range(3))
+    v = rng.random(n).astype(np.float32)
+    outs = []
+    for fused in (False, True):
+        dp, dm, dv, dg = (torch.from_numpy(a.copy()).cuda() for a in (p, m, v, g))
+        sh = torch.zeros(n, dtype=torch.int16, device='cuda')
+        st = torch.tensor([4, 2, 0, 0], dtype=torch.int64, device='cuda')
+        dsts = [torch.zeros(c, r, dtype=torch.int16, device='cuda') for r, c in shapes]
+        if fused:
+            arr = (L.AdamTRegion * len(shapes))()
+            for i, ((r, c), o) in enumerate(zip(shapes, offs)):
+                arr[i].off, arr[i].rows, arr[i].cols, arr[i].dst = o, r, c, dsts[i].data_ptr()
+            L.call('cc_adam_dense_t', L.ptr(dp), L.ptr(dm), L.ptr(dv), L.ptr(dg), L.ptr(sh), n,
+                   L.ptr(st), 1e-3, 0.9, 0.999, 1e-7, arr, len(shapes), bpe, L.stream_ptr())
+        else:
+            L.call('cc_adam_dense', L.ptr(dp), L.ptr(dm), L.ptr(dv), L.ptr(dg), L.ptr(sh), n,
+                   L.ptr(st), 1e-3, 0.9, 0.999, 1e-7, L.stream_ptr())
+            for (r, c), o, dst in zip(shapes, offs, dsts):
+                dst.copy_(sh[o:o + r * c].view(r, c).t())
+            if bpe:
+                L.call('cc_state_advance', L.ptr(st), bpe, L.stream_ptr())
+        torch.cuda.synchronize()
+        outs.append([t.cpu().numpy() for t in (dp, dm, dv, sh, st, *dsts)])
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+    assert outs[1][4].tolist() == ([5, 0, 1, 0] if bpe else [4, 2, 0, 0])
+
+
 def test_graph_replay_matches_eager_and_epochs_roll_over():
     V, d, B, C = 700, 64, 32, 128          # 4 batches per epoch
     tr_e, lists, Mt, ns, P, _ = _setup(V, d, B, C, 0.1, 'bf16')
@@ -115,6 +156,7 @@ def test_graph_replay_matches_eager_and_epochs_roll_over():
         oxs, oys, _, _ = noise_ref.philox_noise_batch(cubes, cdf, ns, tr_g.cfg.seed, step)
         assert all(np.array_equal(a, b) for a, b in zip(xs[:B], oxs))
     assert torch.equal(tr_e.params, tr_g.params)
+    tr_g.flush()            # the last step's counters run at the head of the next step
     assert tr_g.state.cpu().tolist()[:3] == [6, 2, 1]
 
 
