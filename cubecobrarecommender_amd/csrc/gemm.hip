@@ -701,6 +701,43 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T *__restrict__ X, in
   out[n] = s;
 }
 
+// bf16 transpose with 16-B accesses on both sides (rows, cols multiples of 8, 16-B aligned):
+// a 64 x 64 tile moves as 512 chunks of 8 elements in and 512 out (2 per thread).
+__global__ __launch_bounds__(256) void transpose_b16v_kernel(const bf16_t *__restrict__ src, int rows,
+                                                            int cols, bf16_t *__restrict__ dst) {
+  __shared__ bf16_t tile[64][64 + 2];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  uint4 in[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = threadIdx.x + 256 * k, r = r0 + q / 8, c = c0 + (q % 8) * 8;
+    in[k] = r < rows && c < cols ? *reinterpret_cast<const uint4 *>(src + (int64_t)r * cols + c)
+                                 : make_uint4(0u, 0u, 0u, 0u);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = threadIdx.x + 256 * k, rr = q / 8, cc = (q % 8) * 8;
+    const uint32_t w[4] = {in[k].x, in[k].y, in[k].z, in[k].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      tile[rr][cc + 2 * e] = (bf16_t)(w[e] & 0xFFFFu);
+      tile[rr][cc + 2 * e + 1] = (bf16_t)(w[e] >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = threadIdx.x + 256 * k, cc = q / 8, rr = (q % 8) * 8;
+    const int c = c0 + cc, r = r0 + rr;
+    if (c >= cols || r >= rows) continue;
+    uint32_t w[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      w[e] = (uint32_t)tile[rr + 2 * e][cc] | ((uint32_t)tile[rr + 2 * e + 1][cc] << 16);
+    *reinterpret_cast<uint4 *>(dst + (int64_t)c * rows + r) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void transpose_kernel(const T *__restrict__ src, int rows, int cols,
                                                         T *__restrict__ dst) {
@@ -819,6 +856,12 @@ extern "C" int cc_transpose(int32_t dtype, const void *src, int32_t rows, int32_
   CC_REQUIRE(src && dst && rows >= 0 && cols >= 0, "cc_transpose: args");
   if (rows == 0 || cols == 0) return CC_OK;
   const dim3 grid((unsigned)cdiv(cols, 64), (unsigned)cdiv(rows, 64)), block(256);
+  if (dtype == CC_BF16 && rows % 8 == 0 && cols % 8 == 0 && ((uintptr_t)src | (uintptr_t)dst) % 16 == 0) {
+    hipLaunchKernelGGL(transpose_b16v_kernel, grid, block, 0, as_stream(stream), (const bf16_t *)src,
+                       rows, cols, (bf16_t *)dst);
+    CC_LAUNCH_CHECK("transpose_b16v_kernel");
+    return CC_OK;
+  }
   if (dtype == CC_BF16)
     hipLaunchKernelGGL(transpose_kernel<bf16_t>, grid, block, 0, as_stream(stream), (const bf16_t *)src, rows, cols, (bf16_t *)dst);
   else

@@ -498,8 +498,16 @@ __global__ __launch_bounds__(256) void tower_reduce_kernel(TowerP p) {
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void tower_transpose_kernel(TowerP p) {
+__global__ __launch_bounds__(256) void tower_transpose_kernel(TowerP p, int64_t *state, int64_t bpe) {
   __shared__ T tile[32][33];
+  if (state && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {  // cc_state_advance
+    state[0] += 1;
+    state[1] += 1;
+    if (state[1] >= bpe) {
+      state[1] = 0;
+      state[2] += 1;
+    }
+  }
   const int l = blockIdx.y;
   const int i = l < 3 ? l : (l < 6 ? l : l - 3);
   int K, N;
@@ -608,15 +616,23 @@ extern "C" int cc_tower_reduce(const cc_tower_args *t, void *stream) {
   return CC_OK;
 }
 
-extern "C" int cc_tower_transpose(const cc_tower_args *t, void *stream) {
+extern "C" int cc_tower_transpose_advance(const cc_tower_args *t, int64_t *state,
+                                          int64_t batches_per_epoch, void *stream) {
   TowerP p;
   int rc = make_params(t, p);
   if (rc) return rc;
+  CC_REQUIRE(!state || batches_per_epoch >= 1, "cc_tower_transpose_advance: batches_per_epoch");
   const int layers = t->R > t->B ? 9 : 6;
   if (t->dtype == CC_BF16)
-    hipLaunchKernelGGL(tower_transpose_kernel<bf16_t>, dim3(64, layers), dim3(256), 0, as_stream(stream), p);
+    hipLaunchKernelGGL(tower_transpose_kernel<bf16_t>, dim3(64, layers), dim3(256), 0, as_stream(stream), p,
+                       state, batches_per_epoch);
   else
-    hipLaunchKernelGGL(tower_transpose_kernel<float>, dim3(64, layers), dim3(256), 0, as_stream(stream), p);
+    hipLaunchKernelGGL(tower_transpose_kernel<float>, dim3(64, layers), dim3(256), 0, as_stream(stream), p,
+                       state, batches_per_epoch);
   CC_LAUNCH_CHECK("tower_transpose_kernel");
   return CC_OK;
+}
+
+extern "C" int cc_tower_transpose(const cc_tower_args *t, void *stream) {
+  return cc_tower_transpose_advance(t, nullptr, 1, stream);
 }

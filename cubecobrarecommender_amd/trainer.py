@@ -145,7 +145,7 @@ class Trainer:
         self.gH2 = torch.zeros(R, 256, **T)
         self.gPre1 = torch.zeros(R, d, **f32)
         self.Z2 = torch.zeros(B, V, **f32) if self.use_reg else None
-        self.splits = max(1, min(16, V // 512))            # decoder dX: K = V
+        self.splits = max(1, min(32, V // 512))            # decoder dX: K = V (32: 22.4 us vs 29.5 at 16)
         self.tsplits = max(1, min(8, B // 128))             # tower dW: K = rows (B or 2B)
         self.split_buf = torch.zeros(max(self.splits * B * d, 2 * self.tsplits * max(d, 256) * 256), **f32)
         self.cs_buf = torch.zeros(2 * self.tsplits * max(d, 256), **f32)
@@ -502,8 +502,8 @@ class Trainer:
             for k, pre in enumerate(branches_of(self.use_reg)):
                 L.call('cc_transpose', self.dtype, self.w(pre + '/reconstruct/kernel'), self.cfg.d, self.cfg.V,
                        L.ptr(self.WoT[k]), ss)
-            L.call('cc_state_advance', L.ptr(self.state), self.batches_per_epoch, L.stream_ptr(None))
-            L.call('cc_tower_transpose', L.C.byref(self.targs), L.stream_ptr(None))
+            L.call('cc_tower_transpose_advance', L.C.byref(self.targs), L.ptr(self.state),
+                   self.batches_per_epoch, L.stream_ptr(None))
             self._join()
             return
         L.call('cc_state_advance', L.ptr(self.state), self.batches_per_epoch, L.stream_ptr(stream))

@@ -205,6 +205,9 @@ int cc_tower_bwd_chain(const cc_tower_args *t, void *stream);
 int cc_tower_bwd_dw(const cc_tower_args *t, void *stream);
 int cc_tower_reduce(const cc_tower_args *t, void *stream);
 int cc_tower_transpose(const cc_tower_args *t, void *stream);
+/* cc_tower_transpose + cc_state_advance(state, batches_per_epoch) in the same launch */
+int cc_tower_transpose_advance(const cc_tower_args *t, int64_t *state, int64_t batches_per_epoch,
+                               void *stream);
 
 /* ----------------------------------------------------------------------------------
  * D1 output layer fused with sigmoid+BCE (model.py:64,94; train.py:85): logits

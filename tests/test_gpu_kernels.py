@@ -235,3 +235,15 @@ def test_gather_and_scatter(dtype, d):
     for r, l in enumerate(lists):
         gw[l] += dp[r]
     assert rel_err(grad.cpu().numpy(), gw) < 1e-6
+
+
+@pytest.mark.parametrize('rows,cols', [(256, 22000), (64, 700), (256, 20884), (13, 7), (24, 40)])
+def test_transpose_bf16_and_fp32(rows, cols):
+    """cc_transpose (the Wo^T refresh): vector bf16 path (rows, cols % 8 == 0) and scalar paths."""
+    from cubecobrarecommender_amd import _lib as L
+    for dt, tdt in ((L.CC_BF16, torch.bfloat16), (L.CC_F32, torch.float32)):
+        src = torch.randn(rows, cols, device='cuda').to(tdt)
+        dst = torch.zeros(cols, rows, device='cuda', dtype=tdt)
+        L.call('cc_transpose', dt, L.ptr(src), rows, cols, L.ptr(dst), L.stream_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(dst, src.t().contiguous())

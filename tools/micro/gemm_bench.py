@@ -24,7 +24,7 @@ Cb = torch.empty(B, V, **bf)
 Ct = torch.empty(V, B, **bf)
 gW = torch.empty(d, V, device=dev)
 gb = torch.empty(V, device=dev)
-split = torch.empty(SPL * B * d, device=dev)
+split = torch.empty(64 * B * d, device=dev)
 
 
 def gemm(M, N, K, A, lda, Bp, ldb, epi, **kw):
@@ -50,6 +50,12 @@ def main(only=None):
         'compute_only': lambda: gemm(B, V, d, D3, d, WoT, d, L.CC_EPI_STORE),
         'dW+colsum': lambda: gemm(d, V, B, D3t, B, dZt, B, L.CC_EPI_STORE, Cf=gW, colsum=gb),
         'dX_splitk': lambda: gemm(B, d, V, dZ, V, Wo, V, L.CC_EPI_SPLITK, Cf=split, splits=SPL),
+        'dX_splitk8': lambda: gemm(B, d, V, dZ, V, Wo, V, L.CC_EPI_SPLITK, Cf=split, splits=8),
+        'dX_splitk32': lambda: gemm(B, d, V, dZ, V, Wo, V, L.CC_EPI_SPLITK, Cf=split, splits=32),
+        'dX_splitk64': lambda: gemm(B, d, V, dZ, V, Wo, V, L.CC_EPI_SPLITK, Cf=split, splits=64),
+        'reduce16': lambda: L.call('cc_splitk_reduce', L.CC_BF16, L.ptr(split), 16, B, d, None, L.ptr(Cb), None, None, None, L.stream_ptr()),
+        'reduce32': lambda: L.call('cc_splitk_reduce', L.CC_BF16, L.ptr(split), 32, B, d, None, L.ptr(Cb), None, None, None, L.stream_ptr()),
+        'reduce64': lambda: L.call('cc_splitk_reduce', L.CC_BF16, L.ptr(split), 64, B, d, None, L.ptr(Cb), None, None, None, L.stream_ptr()),
     }
     for name, fn in variants.items():
         if only and name != only:
