@@ -387,9 +387,32 @@ __global__ __launch_bounds__(NtCfg<BM>::NTH) void gemm_nt_bf16_kernel(GemmParams
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   __shared__ uint32_t ys[BM][NBN / 32];  // BCE targets of the tile
   __shared__ double red[NTH / 64];
+  __shared__ int lastflag;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  // BCE: block-sum the loss and publish it as this tile's partial; with loss_out, an sc1 store
+  // + agent ticket (MI355X guide hand-off: no L2 writeback fence) tells the last block to reduce.
+  // Called before the epilogue's global stores, so the vmcnt wait has nothing else to drain.
+  auto bce_publish = [&](float lf) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) lf += __shfl_xor(lf, off);
+    if (lane == 0) red[wave] = (double)lf;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double sum = 0.0;
+      for (int w = 0; w < NTH / 64; ++w) sum += red[w];
+      lastflag = 0;
+      if (!p.loss_out) {
+        p.loss_partials[tile] = sum;
+      } else {
+        __hip_atomic_store(&p.loss_partials[tile], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t tk = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lastflag = tk == gridDim.x - 1;
+      }
+    }
+  };
   const int bm = (tile % tiles_m) * BM, bn = (tile / tiles_m) * NBN;
   int kbeg = 0, kend = p.K;
   if constexpr (EPI == CC_EPI_SPLITK) {
@@ -507,6 +530,9 @@ __global__ __launch_bounds__(NtCfg<BM>::NTH) void gemm_nt_bf16_kernel(GemmParams
       }
     }
     __syncthreads();
+    if constexpr (EPI == CC_EPI_BCE && kBceRegs) {
+      if (r0 == 0) bce_publish(lossf);  // the loss is final after the register pass
+    }
     if constexpr (EPI == CC_EPI_BCE && !kBceRegs) {
       // taller tiles: the transcendental work runs from LDS so it does not hold the
       // accumulators' registers (z -> dz in place)
@@ -569,27 +595,10 @@ __global__ __launch_bounds__(NtCfg<BM>::NTH) void gemm_nt_bf16_kernel(GemmParams
     __syncthreads();
   }
   if constexpr (EPI == CC_EPI_BCE) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) lossf += __shfl_xor(lossf, off);
-    double lv = (double)lossf;
-    if (lane == 0) red[wave] = lv;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double sum = 0.0;
-      for (int w = 0; w < NTH / 64; ++w) sum += red[w];
-      if (!p.loss_out) {
-        p.loss_partials[tile] = sum;
-      } else {  // hand-off by sc1 store + ticket (MI355X guide: no L2 writeback fence needed)
-        __hip_atomic_store(&p.loss_partials[tile], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t tk = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        red[0] = tk == gridDim.x - 1 ? 1.0 : 0.0;
-      }
-    }
+    if constexpr (!kBceRegs) bce_publish(lossf);
     if (p.loss_out) {  // the last tile block reduces the partials in tile order: the loss, no
       __syncthreads();  // separate reduce launch
-      if (red[0] != 0.0) {
-        __syncthreads();
+      if (lastflag) {
         double s2 = 0.0;
         for (int i = threadIdx.x; i < (int)gridDim.x; i += NTH)
           s2 += __hip_atomic_load(&p.loss_partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -684,8 +693,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restr
     cs_out[i] = c;
   }
   if (i >= MN) return;
+  // the splits' loads are independent: issue 8 at a time, add in split order
   float s = 0.f;
-  for (int z = 0; z < splits; ++z) s += part[z * MN + i];
+  int z = 0;
+  for (; z + 8 <= splits; z += 8) {
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = part[(int64_t)(z + u) * MN + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += x[u];
+  }
+  for (; z < splits; ++z) s += part[(int64_t)z * MN + i];
   if (H) s = DT<T>::ld(H + i) > 0.f ? s : 0.f;
   if (C) DT<T>::st(C + i, s);
   if (Cf) Cf[i] = s;
