@@ -89,6 +89,7 @@ SIGNATURES = {
     'cc_tower_bwd_dw': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_reduce': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_transpose': (C.c_int, [C.POINTER(TowerArgs), _P]),
+    'cc_tower_bwd_dw_direct': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_transpose_advance': (C.c_int, [C.POINTER(TowerArgs), _P, _I64, _P]),
     'cc_topn_workspace_size': (_SZ, [_I32]),
     'cc_topn': (C.c_int, [_P, _I32, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),

@@ -10,6 +10,8 @@
 //   the batch rows containing card r; their dPre rows (L2-resident, [R, d] fp32) are summed in
 //   ascending row order — deterministic, and dense over every row (rows absent from the batch
 //   get an exact zero gradient, as TF's dense MatMul gradient gives).
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace {
@@ -59,14 +61,18 @@ constexpr int GW = 4;
 #endif
 constexpr int SGW = CCREC_SCATTER_GW;
 
-template <typename T, int EPL>
+// The row's index list is staged in LDS first (one coalesced read), so each batch of U row
+// loads costs one dependent global round trip instead of two.
+constexpr int GIDX = 2048;
+
+template <typename T, int EPL, int U>
 __global__ __launch_bounds__(256) void gather_kernel(const T *__restrict__ table,
                                                      const float *__restrict__ bias, int d, int R,
                                                      const int32_t *__restrict__ x_cnt,
                                                      const int32_t *__restrict__ x_idx, int x_cap,
                                                      T *__restrict__ out) {
-  constexpr int U = 8;
   __shared__ float part[GW - 1][64 * EPL];
+  __shared__ int32_t ls[GIDX];
   const int row = blockIdx.x;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int c0 = lane * EPL;
@@ -76,7 +82,12 @@ __global__ __launch_bounds__(256) void gather_kernel(const T *__restrict__ table
   const int n = x_cnt[row];
   const int q = (n + GW - 1) / GW;
   const int i0 = min(n, w * q), i1 = min(n, i0 + q);
-  const int32_t *__restrict__ lst = x_idx + (int64_t)row * x_cap;
+  const int32_t *__restrict__ glst = x_idx + (int64_t)row * x_cap;
+  const bool staged = n <= GIDX;
+  if (staged)
+    for (int t = threadIdx.x; t < n; t += 256) ls[t] = glst[t];
+  __syncthreads();
+  const int32_t *lst = staged ? ls : glst;
   int i = i0;
   for (; i + U <= i1; i += U) {
     int j[U];
@@ -117,13 +128,13 @@ __global__ __launch_bounds__(256) void gather_kernel(const T *__restrict__ table
 // Backward: 4 waves per W1 row (row V = the bias when bias_grad is given); wave w walks the w-th
 // quarter of the row's bit words, collecting up to U set bits before issuing their dPre loads
 // together (heavy Zipf rows have a set bit for nearly every batch row).  Partials added in wave order.
-template <int EPL>
+template <int EPL, int U>
 __global__ __launch_bounds__(64 * SGW) void scatter_bwd_kernel(const float *__restrict__ dpre, int V,
                                                           int d, int R,
                                                           const uint32_t *xt,
                                                           float *__restrict__ grad,
                                                           float *__restrict__ bias_grad) {
-  constexpr int U = 8;
+  
   __shared__ float part[SGW - 1][64 * EPL];
   const int row = blockIdx.x;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -205,14 +216,28 @@ extern "C" int cc_embed_gather_fwd(int32_t dtype, const void *table, const float
   const dim3 grid((unsigned)R), block(256);
   const int epl = d / 64;
   hipStream_t s = as_stream(stream);
-#define GATHER_CASE(E)                                                                          \
-  case E:                                                                                       \
-    if (dtype == CC_BF16)                                                                       \
-      hipLaunchKernelGGL((gather_kernel<bf16_t, E>), grid, block, 0, s, (const bf16_t *)table, \
-                         bias, d, R, x_cnt, x_idx, x_cap, (bf16_t *)out);                      \
-    else                                                                                        \
-      hipLaunchKernelGGL((gather_kernel<float, E>), grid, block, 0, s, (const float *)table,   \
-                         bias, d, R, x_cnt, x_idx, x_cap, (float *)out);                       \
+  static const int gu = [] {  // A/B switch: row loads in flight per lane (bf16, d = 256)
+    const char *e = getenv("CCREC_GATHER_U");
+    return e ? atoi(e) : 8;  // measured at cfg 2: 8 -> 328.5 us/step, 16 -> 337, 32 -> 341
+  }();
+  if (dtype == CC_BF16 && epl == 4 && (gu == 16 || gu == 32)) {
+    if (gu == 16)
+      hipLaunchKernelGGL((gather_kernel<bf16_t, 4, 16>), grid, block, 0, s, (const bf16_t *)table,
+                         bias, d, R, x_cnt, x_idx, x_cap, (bf16_t *)out);
+    else
+      hipLaunchKernelGGL((gather_kernel<bf16_t, 4, 32>), grid, block, 0, s, (const bf16_t *)table,
+                         bias, d, R, x_cnt, x_idx, x_cap, (bf16_t *)out);
+    CC_LAUNCH_CHECK("gather_kernel");
+    return CC_OK;
+  }
+#define GATHER_CASE(E)                                                                              \
+  case E:                                                                                           \
+    if (dtype == CC_BF16)                                                                           \
+      hipLaunchKernelGGL((gather_kernel<bf16_t, E, 8>), grid, block, 0, s, (const bf16_t *)table, \
+                         bias, d, R, x_cnt, x_idx, x_cap, (bf16_t *)out);                          \
+    else                                                                                            \
+      hipLaunchKernelGGL((gather_kernel<float, E, 8>), grid, block, 0, s, (const float *)table,   \
+                         bias, d, R, x_cnt, x_idx, x_cap, (float *)out);                           \
     break;
   switch (epl) {
     GATHER_CASE(1)
@@ -235,12 +260,21 @@ extern "C" int cc_embed_scatter_bwd(const float *dpre, int32_t V, int32_t d, int
   CC_REQUIRE(d % 64 == 0 && d >= 64 && d <= 1024, "cc_embed_scatter_bwd: d must be 64..1024, %64");
   const dim3 grid((unsigned)(bias_grad ? V + 1 : V)), block(64 * SGW);
   hipStream_t s = as_stream(stream);
+  static const int su = [] {  // A/B switch: dPre row loads in flight per lane (d = 256)
+    const char *e = getenv("CCREC_SCATTER_U");
+    return e ? atoi(e) : 8;  // measured at cfg 2: 8 -> 45.5 us, 16 -> 54.8
+  }();
+  if (d == 256 && su == 16) {
+    hipLaunchKernelGGL((scatter_bwd_kernel<4, 16>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad);
+    CC_LAUNCH_CHECK("scatter_bwd_kernel");
+    return CC_OK;
+  }
   switch (d / 64) {
-    case 1: hipLaunchKernelGGL((scatter_bwd_kernel<1>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
-    case 2: hipLaunchKernelGGL((scatter_bwd_kernel<2>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
-    case 4: hipLaunchKernelGGL((scatter_bwd_kernel<4>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
-    case 8: hipLaunchKernelGGL((scatter_bwd_kernel<8>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
-    case 16: hipLaunchKernelGGL((scatter_bwd_kernel<16>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
+    case 1: hipLaunchKernelGGL((scatter_bwd_kernel<1, 8>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
+    case 2: hipLaunchKernelGGL((scatter_bwd_kernel<2, 8>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
+    case 4: hipLaunchKernelGGL((scatter_bwd_kernel<4, 8>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
+    case 8: hipLaunchKernelGGL((scatter_bwd_kernel<8, 8>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
+    case 16: hipLaunchKernelGGL((scatter_bwd_kernel<16, 8>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad); break;
     default: return cc::fail(CC_ERR_UNSUPPORTED, "cc_embed_scatter_bwd: d/64 must be a power of two");
   }
   CC_LAUNCH_CHECK("scatter_bwd_kernel");

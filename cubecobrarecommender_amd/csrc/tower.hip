@@ -10,6 +10,8 @@
 //                  transposed LDS images), db_partial = colsum G  -> slab[blk] (no atomics);
 //                  dH[32][K] = G W^T (B fragments straight from W [K][N]) masked by H > 0.
 // cc_tower_reduce sums the slabs in block order: deterministic dW/db for all 9 layers.
+#include <algorithm>
+
 #include "common.hpp"
 
 namespace {
@@ -467,6 +469,95 @@ __global__ __launch_bounds__(NT) void tower_dw_kernel(TowerP p) {
 }
 
 // grads[l] = sum over the blocks that touched layer l of their slab partials, in block order.
+// Tower weight gradients without slabs (bf16 operands): one workgroup per 32 x 32 tile of one
+// layer's dW = H^T G over all of that layer's rows (encoder: R rows; each decoder branch: its B
+// rows).  The 4 waves split the rows; each stages its rows of H[:, k0:k0+32] and G[:, n0:n0+32]
+// transposed in LDS ([col][row], 16-B MFMA fragment reads), accumulates with 32x32x16 MFMAs in
+// row order, and the 4 partial tiles are added in wave order (deterministic).  Tiles of the
+// first k-block also sum G's columns: the bias gradient.  Replaces tower_dw + tower_reduce.
+constexpr int DW_NT = 256;
+
+__device__ __forceinline__ bool dw_job(const TowerP &p, int bid, int &l, int &i, int &k0, int &n0,
+                                       int &row0, int &nrows) {
+  const int L = p.R > p.B ? 9 : 6;
+  for (l = 0; l < L; ++l) {
+    i = l < 6 ? l : l - 3;
+    int K, N;
+    chain_dims(p.d, i, K, N);
+    const int tn = N / 32, nt = (K / 32) * tn;
+    if (bid < nt) {
+      k0 = 32 * (bid / tn);
+      n0 = 32 * (bid % tn);
+      row0 = l < 6 ? 0 : p.B;
+      nrows = l < 3 ? p.R : p.B;
+      return true;
+    }
+    bid -= nt;
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(DW_NT) void tower_dw_tiled_kernel(TowerP p, int rpw) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int l, i, k0, n0, row0, nrows;
+  if (!dw_job(p, blockIdx.x, l, i, k0, n0, row0, nrows)) return;
+  int K, N;
+  chain_dims(p.d, i, K, N);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5;
+  const int ldr = rpw + 8;  // LDS row pitch (bf16): 16-B aligned, spreads the banks
+  bf16_t *Ht = reinterpret_cast<bf16_t *>(smem) + (size_t)wave * 2 * 32 * ldr;
+  bf16_t *Gt = Ht + 32 * ldr;
+  const bf16_t *H = reinterpret_cast<const bf16_t *>(p.act[i]);
+  const bf16_t *G = reinterpret_cast<const bf16_t *>(i == 5 ? p.gD3 : p.gact[i]);
+  const int wr0 = wave * rpw;  // this wave's rows: [wr0, wr0 + rpw) of the layer's rows
+  // stage: 4 lanes per row (8 bf16 = 16 B each), 16 rows per pass; rows past nrows are zeros
+  for (int rr = lane >> 2; rr < rpw; rr += 16) {
+    const int r = wr0 + rr, c8 = (lane & 3) * 8;
+    uint4 hv = make_uint4(0u, 0u, 0u, 0u), gv = make_uint4(0u, 0u, 0u, 0u);
+    if (r < nrows) {
+      hv = *reinterpret_cast<const uint4 *>(H + (int64_t)(row0 + r) * K + k0 + c8);
+      gv = *reinterpret_cast<const uint4 *>(G + (int64_t)(row0 + r) * N + n0 + c8);
+    }
+    const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w}, gw[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      Ht[(c8 + 2 * e) * ldr + rr] = (bf16_t)(hw[e] & 0xFFFFu);
+      Ht[(c8 + 2 * e + 1) * ldr + rr] = (bf16_t)(hw[e] >> 16);
+      Gt[(c8 + 2 * e) * ldr + rr] = (bf16_t)(gw[e] & 0xFFFFu);
+      Gt[(c8 + 2 * e + 1) * ldr + rr] = (bf16_t)(gw[e] >> 16);
+    }
+  }
+  __syncthreads();
+  f32x16_t acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const bf16_t *arow = Ht + (lane & 31) * ldr;
+  const bf16_t *brow = Gt + (lane & 31) * ldr;
+  for (int kk = 0; kk < rpw; kk += 16)
+    TMma<bf16_t>::mma(TMma<bf16_t>::ld(arow, kk, half), TMma<bf16_t>::ld(brow, kk, half), acc);
+  float cs = 0.f;  // bias: this wave's rows of G column n0 + lane (lanes 0..31)
+  if (k0 == 0 && lane < 32)
+    for (int rr = 0; rr < rpw; ++rr) cs += bf2f(Gt[lane * ldr + rr]);
+  __syncthreads();  // the staged operands are consumed: reuse the LDS for the partial tiles
+  float *part = reinterpret_cast<float *>(smem);  // [4][32][33] + [4][32]
+  float *pcs = part + 4 * 32 * 33;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) part[(wave * 32 + acc_row(r, lane)) * 33 + (lane & 31)] = acc[r];
+  if (lane < 32) pcs[wave * 32 + lane] = cs;
+  __syncthreads();
+  float *gw = p.gw[l];
+  for (int e = threadIdx.x; e < 32 * 32; e += DW_NT) {
+    const int kr = e >> 5, nc = e & 31;
+    float v = part[(0 * 32 + kr) * 33 + nc];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) v += part[(w * 32 + kr) * 33 + nc];
+    gw[(int64_t)(k0 + kr) * N + n0 + nc] = v;
+  }
+  if (k0 == 0 && threadIdx.x < 32)
+    p.gb[l][n0 + threadIdx.x] = pcs[threadIdx.x] + pcs[32 + threadIdx.x] + pcs[64 + threadIdx.x] +
+                                pcs[96 + threadIdx.x];
+}
+
 __global__ __launch_bounds__(256) void tower_reduce_kernel(TowerP p) {
   const int nb = p.R / RB, nbB = p.B / RB;
   const int64_t E = p.slab_elems;
@@ -613,6 +704,30 @@ extern "C" int cc_tower_reduce(const cc_tower_args *t, void *stream) {
   const unsigned blocks = (unsigned)std::min<int64_t>(cdiv(p.slab_elems, 256), 2048);
   hipLaunchKernelGGL(tower_reduce_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), p);
   CC_LAUNCH_CHECK("tower_reduce_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_tower_bwd_dw_direct(const cc_tower_args *t, void *stream) {
+  TowerP p;
+  int rc = make_params(t, p);
+  if (rc) return rc;
+  CC_REQUIRE(t->dtype == CC_BF16, "cc_tower_bwd_dw_direct: bf16 only");
+  CC_REQUIRE(t->gD3, "cc_tower_bwd_dw_direct: null gD3");
+  for (int a = 0; a < 5; ++a) CC_REQUIRE(t->gact[a], "cc_tower_bwd_dw_direct: null gact");
+  for (int l = 0; l < (t->R > t->B ? 9 : 6); ++l)
+    CC_REQUIRE(t->gw[l] && t->gb[l], "cc_tower_bwd_dw_direct: null gw/gb");
+  const int rmax = t->R > t->B ? t->R : t->B;
+  const int rpw = ((rmax + 3) / 4 + 15) / 16 * 16;
+  const size_t lds = std::max((size_t)4 * 2 * 32 * (rpw + 8) * 2, (size_t)(4 * 32 * 33 + 4 * 32) * 4);
+  CC_REQUIRE(lds <= 160 * 1024, "cc_tower_bwd_dw_direct: too many rows for one LDS stage");
+  int jobs = 0;
+  for (int l = 0; l < (t->R > t->B ? 9 : 6); ++l) {
+    int K, N;
+    chain_dims(t->d, l < 6 ? l : l - 3, K, N);
+    jobs += (K / 32) * (N / 32);
+  }
+  hipLaunchKernelGGL(tower_dw_tiled_kernel, dim3(jobs), dim3(DW_NT), lds, as_stream(stream), p, rpw);
+  CC_LAUNCH_CHECK("tower_dw_tiled_kernel");
   return CC_OK;
 }
 

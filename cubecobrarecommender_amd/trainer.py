@@ -462,8 +462,11 @@ class Trainer:
             L.call('cc_tower_bwd_chain', L.C.byref(self.targs), s)
             t()
             ss = self._fork()      # per-block dW slabs + their reduce overlap the E1 scatter
-            L.call('cc_tower_bwd_dw', L.C.byref(self.targs), ss)
-            L.call('cc_tower_reduce', L.C.byref(self.targs), ss)
+            if self.dtype == L.CC_BF16 and os.environ.get('CCREC_TOWER_DW_DIRECT', '1') != '0':
+                L.call('cc_tower_bwd_dw_direct', L.C.byref(self.targs), ss)
+            else:
+                L.call('cc_tower_bwd_dw', L.C.byref(self.targs), ss)
+                L.call('cc_tower_reduce', L.C.byref(self.targs), ss)
         else:
             self._dense_bwd(self.H3, self.gZl, (0, R), 128, 64, 'encoder/bottleneck', gIn=self.gH3, mask=self.H3)
             self._dense_bwd(self.H2, self.gH3, (0, R), 256, 128, 'encoder/encoded_3', gIn=self.gH2, mask=self.H2)

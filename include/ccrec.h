@@ -204,6 +204,9 @@ int cc_tower_bwd(const cc_tower_args *t, void *stream);
 int cc_tower_bwd_chain(const cc_tower_args *t, void *stream);
 int cc_tower_bwd_dw(const cc_tower_args *t, void *stream);
 int cc_tower_reduce(const cc_tower_args *t, void *stream);
+/* bf16: every layer's dW/db written directly (no slabs, no reduce): cc_tower_bwd_dw +
+ * cc_tower_reduce in one launch; row-order MFMA sums, deterministic. */
+int cc_tower_bwd_dw_direct(const cc_tower_args *t, void *stream);
 int cc_tower_transpose(const cc_tower_args *t, void *stream);
 /* cc_tower_transpose + cc_state_advance(state, batches_per_epoch) in the same launch */
 int cc_tower_transpose_advance(const cc_tower_args *t, int64_t *state, int64_t batches_per_epoch,
