@@ -168,19 +168,22 @@ __global__ __launch_bounds__(NT) void noise_kernel(cc_noise_args a) {
   const int w0 = tid * per, w1 = min(VW, w0 + per);
   int cnt = 0;
   for (int w = w0; w < w1; ++w) cnt += __popc((cube_bits[w] & ~cut_bits[w]) | add_bits[w]);
-  scan[tid] = cnt;
-  __syncthreads();
-  if (tid == 0) {
-    int run = 0;
-    for (int t = 0; t < NT; ++t) {
-      const int c = scan[t];
-      scan[t] = run;
-      run += c;
-    }
-    scan[NT] = run;
+  // exclusive block scan of cnt: inclusive wave scan by shuffles, then the wave totals
+  const int lane = tid & 63, wv = tid >> 6;
+  int inc_sum = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(inc_sum, off);
+    if (lane >= off) inc_sum += y;
   }
+  if (lane == 63) scan[wv] = inc_sum;
   __syncthreads();
-  int pos = scan[tid];
+  int wbase = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) wbase += w < wv ? scan[w] : 0;
+  const int total = scan[0] + scan[1] + scan[2] + scan[3];
+  static_assert(NT == 256, "block scan assumes 4 waves");
+  int pos = wbase + inc_sum - cnt;
   int32_t *xrow = a.x_idx + (int64_t)b * a.x_cap;
   for (int w = w0; w < w1; ++w) {
     uint32_t m = (cube_bits[w] & ~cut_bits[w]) | add_bits[w];
@@ -193,7 +196,7 @@ __global__ __launch_bounds__(NT) void noise_kernel(cc_noise_args a) {
       ++pos;
     }
   }
-  if (tid == 0) a.x_cnt[b] = min(scan[NT], a.x_cap);
+  if (tid == 0) a.x_cnt[b] = min(total, a.x_cap);
   // regulariser row for this slot (generator.py:47-51): one draw ∝ neg_sampler
   if (a.with_reg && tid == 0) {
     const u32x4 o = rng(a.seed, step, slot, KIND_REG, 0, 0);

@@ -563,8 +563,8 @@ class Trainer:
 
     def run_adam(self, stream=None, events=None):
         """Adam (graph replay, or an eager launch bracketed by `events` = (e0, e1))."""
-        if events is not None:
-            events[0].record()
+        if events is not None:   # the Adam kernel alone between the events (an eager launch:
+            events[0].record()   # a graph replay there would add its launch edge to the interval)
             self.apply_adam(stream)
             events[1].record()
         elif self.graphs is not None:
