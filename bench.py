@@ -249,7 +249,13 @@ def main():
                 'unit': 'GB/s', 'bytes_per_launch': byt, 'traffic': None,
                 'measured': 'HIP events around the sharded Adam kernels on the comm stream (sum per step)'}
     roof['frac'] = roof['achieved'] / roof['peak']
-    roof['kernel'] = 'adam_kernel (cc_adam_dense)'
+    if world == 1 and getattr(tr, 'prefetch', False):
+        roof['kernel'] = ('adam_noise_kernel (cc_adam_noise: TF Adam over all parameters + F of the '
+                          'next step in the same launch; bytes counted are Adam\'s only, F adds <2%)')
+    elif world == 1 and getattr(tr, 'fused_adam', False):
+        roof['kernel'] = 'adam_fused_kernel (cc_adam_dense_t)'
+    else:
+        roof['kernel'] = 'adam_kernel (cc_adam_dense)'
     roof['avg_ms'] = adam_ms
     out = {
         'metric': 'training cubes/sec at |V|~22k d=256; top-N recommend p50 latency',

@@ -74,6 +74,7 @@ SIGNATURES = {
     'cc_dec_bce_fused': (C.c_int, [_I32, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     'cc_dec_softmax_kl_fused': (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _F32, _P, _P, _P]),
     'cc_reduce_loss': (C.c_int, [_P, _I32, _F64, _P, _P]),
+    'cc_adam_noise': (C.c_int, [_P, _P, _P, _P, _P, _I64, _F32, _F32, _F32, _F32, C.POINTER(NoiseArgs), _I64, _P]),
     'cc_adam_dense': (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _F32, _F32, _F32, _F32, _P]),
     'cc_adam_dense_t': (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _F32, _F32, _F32, _F32, _P, _I32,
                                   _I64, _P]),

@@ -1,0 +1,64 @@
+// TF ResourceApplyAdam element update and its flat-range loop, shared by the plain Adam kernel
+// (loss_adam.hip) and the Adam + next-step-F kernel (noise.hip).
+//   alpha = lr sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1); v += (g^2-v)(1-b2);
+//   p -= m*alpha/(sqrt(v)+eps);  t = state[0] + 1.
+#pragma once
+#include "common.hpp"
+
+namespace cc_adam {
+
+__device__ __forceinline__ void elem(float &p, float &m, float &v, float g, float alpha,
+                                     float omb1, float omb2, float eps) {
+  m += (g - m) * omb1;
+  v += (g * g - v) * omb2;
+  p -= (m * alpha) / (sqrtf(v) + eps);
+}
+
+struct Args {
+  float *p, *m, *v;
+  const float *g;
+  bf16_t *shadow;
+  int64_t n;
+  float lr, b1, b2, eps;
+};
+
+// Blocks [0, nblocks) of whatever grid run this cover [0, n) grid-stride (float4 body + tail).
+__device__ __forceinline__ void range(const Args &a, int64_t step, int bid, int nblocks) {
+  const float t = (float)(step + 1);
+  const float b1p = powf(a.b1, t), b2p = powf(a.b2, t);
+  const float alpha = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  const float omb1 = 1.f - a.b1, omb2 = 1.f - a.b2;
+  const int64_t n4 = a.n >> 2;
+  const int64_t stride = (int64_t)nblocks * blockDim.x;
+  for (int64_t i = (int64_t)bid * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pp = reinterpret_cast<float4 *>(a.p)[i];
+    float4 mm = reinterpret_cast<float4 *>(a.m)[i];
+    float4 vv = reinterpret_cast<float4 *>(a.v)[i];
+    const float4 gg = reinterpret_cast<const float4 *>(a.g)[i];
+    float *pe = &pp.x, *me = &mm.x, *ve = &vv.x;
+    const float *ge = &gg.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) elem(pe[e], me[e], ve[e], ge[e], alpha, omb1, omb2, a.eps);
+    reinterpret_cast<float4 *>(a.p)[i] = pp;
+    reinterpret_cast<float4 *>(a.m)[i] = mm;
+    reinterpret_cast<float4 *>(a.v)[i] = vv;
+    if (a.shadow) {
+      ushort4 s;
+      s.x = f2bf(pp.x);
+      s.y = f2bf(pp.y);
+      s.z = f2bf(pp.z);
+      s.w = f2bf(pp.w);
+      reinterpret_cast<ushort4 *>(a.shadow)[i] = s;
+    }
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)bid * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    float pp = a.p[i], mm = a.m[i], vv = a.v[i];
+    elem(pp, mm, vv, a.g[i], alpha, omb1, omb2, a.eps);
+    a.p[i] = pp;
+    a.m[i] = mm;
+    a.v[i] = vv;
+    if (a.shadow) a.shadow[i] = f2bf(pp);
+  }
+}
+
+}  // namespace cc_adam

@@ -1,5 +1,6 @@
 // D2 softmax + KL regulariser (model.py:98, train.py:85 'kullback_leibler_divergence'),
 // TF-Adam (train.py:84 'adam' -> ResourceApplyAdam) and the device step counter.
+#include "adam.hpp"
 #include "common.hpp"
 
 namespace {
@@ -75,54 +76,9 @@ __global__ __launch_bounds__(NT) void softmax_kl_kernel(const float *__restrict_
 
 // TF ResourceApplyAdam: alpha = lr sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1); v += (g^2-v)(1-b2);
 // p -= m*alpha/(sqrt(v)+eps).  t = state[0] + 1.
-__device__ __forceinline__ void adam_elem(float &p, float &m, float &v, float g, float alpha,
-                                          float omb1, float omb2, float eps) {
-  m += (g - m) * omb1;
-  v += (g * g - v) * omb2;
-  p -= (m * alpha) / (sqrtf(v) + eps);
-}
 
-__global__ __launch_bounds__(NT) void adam_kernel(float *__restrict__ p, float *__restrict__ m,
-                                                  float *__restrict__ v,
-                                                  const float *__restrict__ g,
-                                                  bf16_t *__restrict__ shadow, int64_t n,
-                                                  const int64_t *__restrict__ state, float lr,
-                                                  float b1, float b2, float eps) {
-  const float t = (float)(state[0] + 1);
-  const float b1p = powf(b1, t), b2p = powf(b2, t);
-  const float alpha = lr * sqrtf(1.f - b2p) / (1.f - b1p);
-  const float omb1 = 1.f - b1, omb2 = 1.f - b2;
-  const int64_t n4 = n >> 2;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 pp = reinterpret_cast<float4 *>(p)[i];
-    float4 mm = reinterpret_cast<float4 *>(m)[i];
-    float4 vv = reinterpret_cast<float4 *>(v)[i];
-    const float4 gg = reinterpret_cast<const float4 *>(g)[i];
-    float *pe = &pp.x, *me = &mm.x, *ve = &vv.x;
-    const float *ge = &gg.x;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) adam_elem(pe[e], me[e], ve[e], ge[e], alpha, omb1, omb2, eps);
-    reinterpret_cast<float4 *>(p)[i] = pp;
-    reinterpret_cast<float4 *>(m)[i] = mm;
-    reinterpret_cast<float4 *>(v)[i] = vv;
-    if (shadow) {
-      ushort4 s;
-      s.x = f2bf(pp.x);
-      s.y = f2bf(pp.y);
-      s.z = f2bf(pp.z);
-      s.w = f2bf(pp.w);
-      reinterpret_cast<ushort4 *>(shadow)[i] = s;
-    }
-  }
-  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float pp = p[i], mm = m[i], vv = v[i];
-    adam_elem(pp, mm, vv, g[i], alpha, omb1, omb2, eps);
-    p[i] = pp;
-    m[i] = mm;
-    v[i] = vv;
-    if (shadow) shadow[i] = f2bf(pp);
-  }
+__global__ __launch_bounds__(NT) void adam_kernel(cc_adam::Args a, const int64_t *__restrict__ state) {
+  cc_adam::range(a, state[0], blockIdx.x, gridDim.x);
 }
 
 // Adam fused with the transposed bf16 operand copies (Wo^T, tower W^T): the flat blocks update
@@ -170,7 +126,7 @@ __global__ __launch_bounds__(NT) void adam_fused_kernel(float *__restrict__ p, f
       float *pe = &pp.x, *me = &mm.x, *ve = &vv.x;
       const float *ge = &gg.x;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) adam_elem(pe[q], me[q], ve[q], ge[q], alpha, omb1, omb2, eps);
+      for (int q = 0; q < 4; ++q) cc_adam::elem(pe[q], me[q], ve[q], ge[q], alpha, omb1, omb2, eps);
       reinterpret_cast<float4 *>(p)[i] = pp;
       reinterpret_cast<float4 *>(m)[i] = mm;
       reinterpret_cast<float4 *>(v)[i] = vv;
@@ -238,7 +194,7 @@ __device__ __forceinline__ void adam_tile(float *__restrict__ p, float *__restri
       float *pe = &P4[qq].x, *me = &M4[qq].x, *ve = &V4[qq].x;
       const float *ge = &G4[qq].x;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) adam_elem(pe[e], me[e], ve[e], ge[e], alpha, omb1, omb2, eps);
+      for (int e = 0; e < 4; ++e) cc_adam::elem(pe[e], me[e], ve[e], ge[e], alpha, omb1, omb2, eps);
       const int64_t i4 = (base + (int64_t)r * cols + c) >> 2;
       reinterpret_cast<float4 *>(p)[i4] = P4[qq];
       reinterpret_cast<float4 *>(m)[i4] = M4[qq];
@@ -257,7 +213,7 @@ __device__ __forceinline__ void adam_tile(float *__restrict__ p, float *__restri
       for (int e = 0; e < 4 && c + e < cols; ++e) {
         const int64_t i = base + (int64_t)r * cols + c + e;
         float pp = p[i], mm = m[i], vv = v[i];
-        adam_elem(pp, mm, vv, g[i], alpha, omb1, omb2, eps);
+        cc_adam::elem(pp, mm, vv, g[i], alpha, omb1, omb2, eps);
         p[i] = pp;
         m[i] = mm;
         v[i] = vv;
@@ -319,8 +275,8 @@ extern "C" int cc_adam_dense(float *p, float *m, float *v, const float *g, uint1
   CC_REQUIRE(!shadow || (uintptr_t)shadow % 8 == 0, "cc_adam_dense: shadow must be 8-byte aligned");
   if (n <= 0) return CC_OK;
   const int64_t blocks = std::min<int64_t>(cdiv(cdiv(n, 4), NT), 256 * 8);
-  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(NT), 0, as_stream(stream), p, m, v,
-                     g, (bf16_t *)shadow, n, state, lr, beta1, beta2, eps);
+  const cc_adam::Args a{p, m, v, g, (bf16_t *)shadow, n, lr, beta1, beta2, eps};
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(NT), 0, as_stream(stream), a, state);
   CC_LAUNCH_CHECK("adam_kernel");
   return CC_OK;
 }

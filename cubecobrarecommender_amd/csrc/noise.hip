@@ -14,6 +14,9 @@
 //           in the cube (== the renormalised law of :93-94), exact fallback after 256 tries
 //   x = (cube \ cut) U add  (sorted CSR row),  y = cube \ ycut  (bitmask)     :96-101
 // The B reg rows (generator.py:47-51) are drawn by thread 0 of each block into rows B..2B-1.
+#include <algorithm>
+
+#include "adam.hpp"
 #include "common.hpp"
 #include "detmath.hpp"
 
@@ -81,8 +84,10 @@ __device__ int add_fallback(const double *__restrict__ ns, int V, const uint32_t
   return last;
 }
 
-__global__ __launch_bounds__(NT) void noise_kernel(cc_noise_args a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+// F for cube slot b of the batch at (step, batch-in-epoch, epoch); smem: the dynamic LDS of
+// cc_noise_fwd's launch.
+__device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *smem, int &s_k,
+                                            int b, int64_t step64, int64_t batch, int64_t epoch) {
   const int VW = (a.V + 31) >> 5;
   uint32_t *cube_bits = smem;
   uint32_t *cut_bits = cube_bits + VW;
@@ -90,18 +95,13 @@ __global__ __launch_bounds__(NT) void noise_kernel(cc_noise_args a) {
   uint32_t *add_bits = ycut_bits + VW;
   int32_t *scan = (int32_t *)(add_bits + VW);  // [NT + 1]
   int32_t *cut_card = scan + NT + 1;           // [x_cap]
-  __shared__ int s_k;
 
-  const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const uint32_t slot = a.slot_base + (uint32_t)b;
-  const int64_t step64 = a.state[0];
-  const int64_t batch = a.state[1];
   const uint32_t step = (uint32_t)step64;
   const int R = a.with_reg ? 2 * a.B : a.B;
   const int XW = (R + 31) >> 5;
 
-  const int64_t epoch = a.state[2];
   const int32_t *perm = a.perm + (epoch % a.num_perms) * (int64_t)a.num_cubes;
   const int32_t cube = perm[batch * (int64_t)a.batch_stride + a.batch_offset + b];
   const int64_t beg = a.cube_ptr[cube];
@@ -209,9 +209,38 @@ __global__ __launch_bounds__(NT) void noise_kernel(cc_noise_args a) {
   }
 }
 
+__global__ __launch_bounds__(NT) void noise_kernel(cc_noise_args a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  __shared__ int s_k;
+  noise_block(a, smem, s_k, blockIdx.x, a.state[0], a.state[1], a.state[2]);
+}
+
+// Adam over the flat buffers in blocks [0, nadam) and, in blocks [nadam, nadam + B), F for the
+// NEXT step (its {step, batch, epoch} = this step's advanced as cc_state_advance will): Adam is
+// HBM-bound, F latency-bound, and F touches only the batch buffers this step's backward has
+// released — one launch instead of F on the next step's critical path.
+__global__ __launch_bounds__(NT) void adam_noise_kernel(cc_adam::Args ad, cc_noise_args a,
+                                                        int nadam, int64_t bpe) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  __shared__ int s_k;
+  // F's blocks come first: they are latency-bound chains that should start at once, the Adam
+  // blocks stream around them
+  const int64_t step = a.state[0];
+  if ((int)blockIdx.x >= a.B) {
+    cc_adam::range(ad, step, (int)blockIdx.x - a.B, nadam);
+    return;
+  }
+  int64_t batch = a.state[1] + 1, epoch = a.state[2];
+  if (batch >= bpe) {
+    batch = 0;
+    epoch += 1;
+  }
+  noise_block(a, smem, s_k, blockIdx.x, step + 1, batch, epoch);
+}
+
 }  // namespace
 
-extern "C" int cc_noise_fwd(const cc_noise_args *a, void *stream) {
+static int noise_check(const cc_noise_args *a, size_t &lds) {
   CC_REQUIRE(a != nullptr, "cc_noise_fwd: null args");
   CC_REQUIRE(a->V > 0 && a->B > 0 && a->x_cap > 0, "cc_noise_fwd: bad V/B/x_cap");
   CC_REQUIRE(a->cube_ptr && a->cube_idx && a->perm && a->cdf && a->neg_sampler && a->state,
@@ -220,9 +249,33 @@ extern "C" int cc_noise_fwd(const cc_noise_args *a, void *stream) {
   CC_REQUIRE(!a->with_reg || a->reg_idx, "cc_noise_fwd: with_reg needs reg_idx");
   CC_REQUIRE(a->num_perms >= 1 && a->num_cubes >= a->batch_stride, "cc_noise_fwd: num_perms/num_cubes");
   const int VW = (a->V + 31) / 32;
-  const size_t lds = (size_t)(4 * VW + NT + 1 + a->x_cap) * 4;
+  lds = (size_t)(4 * VW + NT + 1 + a->x_cap) * 4;
   CC_REQUIRE(lds <= 150 * 1024, "cc_noise_fwd: V / x_cap too large for LDS");
+  return CC_OK;
+}
+
+extern "C" int cc_noise_fwd(const cc_noise_args *a, void *stream) {
+  size_t lds = 0;
+  if (int rc = noise_check(a, lds)) return rc;
   hipLaunchKernelGGL(noise_kernel, dim3(a->B), dim3(NT), lds, as_stream(stream), *a);
   CC_LAUNCH_CHECK("noise_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_adam_noise(float *p, float *m, float *v, const float *g, uint16_t *shadow,
+                             int64_t n, float lr, float beta1, float beta2, float eps,
+                             const cc_noise_args *next, int64_t batches_per_epoch, void *stream) {
+  CC_REQUIRE(p && m && v && g, "cc_adam_noise: null pointer");
+  CC_REQUIRE(((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g) % 16 == 0,
+             "cc_adam_noise: buffers must be 16-byte aligned");
+  CC_REQUIRE(!shadow || (uintptr_t)shadow % 8 == 0, "cc_adam_noise: shadow must be 8-byte aligned");
+  CC_REQUIRE(batches_per_epoch >= 1, "cc_adam_noise: batches_per_epoch");
+  size_t lds = 0;
+  if (int rc = noise_check(next, lds)) return rc;
+  const int nadam = n > 0 ? (int)std::min<int64_t>(cdiv(cdiv(n, 4), NT), 256 * 8) : 0;
+  const cc_adam::Args ad{p, m, v, g, (bf16_t *)shadow, n, lr, beta1, beta2, eps};
+  hipLaunchKernelGGL(adam_noise_kernel, dim3((unsigned)(nadam + next->B)), dim3(NT), lds,
+                     as_stream(stream), ad, *next, nadam, batches_per_epoch);
+  CC_LAUNCH_CHECK("adam_noise_kernel");
   return CC_OK;
 }

@@ -36,6 +36,7 @@ class TrainConfig:
     rank: int = 0
     world: int = 1
     fused_tower: bool = True       # tower.hip row-block kernels (else per-layer cc_gemm launches)
+    prefetch_noise: bool = True    # one process: F of step k+1 rides in step k's Adam launch
 
 
 class DeviceDataset:
@@ -181,6 +182,12 @@ class Trainer:
         self.fused_adam = (self.fused_tower and cfg.world == 1 and self.dtype == L.CC_BF16
                            and os.environ.get('CCREC_FUSED_ADAM', '0') == '1')
         self.adam_regions = self._adam_regions() if self.fused_adam else None
+        # F for the next step in the Adam launch (cc_adam_noise): Adam is HBM-bound, F latency-
+        # bound; F then leaves the forward's critical path.  noise_ready: the batch buffers
+        # already hold the batch the next forward_backward consumes.
+        self.prefetch = (cfg.prefetch_noise and cfg.world == 1 and not self.fused_adam
+                         and os.environ.get('CCREC_PREFETCH_NOISE', '1') != '0')
+        self.noise_ready = False
         self.perms = None
         self.batches_per_epoch = max(1, data.C // (B * cfg.world))   # generator.py:36 (__len__)
         self.graphs = None
@@ -306,6 +313,7 @@ class Trainer:
             self.perms = torch.empty(p.shape, device=self.dev, dtype=torch.int32)
         self.perms.copy_(p)
         self.state[1:3].zero_()
+        self.noise_ready = False   # a prefetched batch was drawn from the old order
 
     def _noise_args(self):
         cfg, V, B = self.cfg, self.cfg.V, self.cfg.batch_size
@@ -373,10 +381,13 @@ class Trainer:
         s = self._s
         # ---- F: noise + reg rows (generator.py:38-103); xt_bits arrives zeroed (the previous
         # step's cc_embed_scatter_bwd consumes it)
-        na = self._noise_args()
-        t = self._tick('cc_noise_fwd')
-        L.call('cc_noise_fwd', L.C.byref(na), s)
-        t()
+        if self.noise_ready:       # drawn by the previous step's Adam launch (cc_adam_noise)
+            self.noise_ready = False
+        else:
+            na = self._noise_args()
+            t = self._tick('cc_noise_fwd')
+            L.call('cc_noise_fwd', L.C.byref(na), s)
+            t()
         # ---- E (model.py:35-42) on R rows: gather + 3 Dense
         t = self._tick('cc_embed_gather_fwd')
         L.call('cc_embed_gather_fwd', self.dtype, self.w('encoder/encoded_1/kernel'),
@@ -483,7 +494,13 @@ class Trainer:
         cfg = self.cfg
         n = self.layout.total if self.use_reg else self.layout.main_total
         t = self._tick('cc_adam_dense')
-        if self.fused_adam:   # + transposed operand copies + step counters
+        if self.prefetch:     # + F for the next step in the same launch
+            na = self._noise_args()
+            L.call('cc_adam_noise', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v),
+                   L.ptr(self.grads), L.ptr(self.shadow), n, cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,
+                   L.C.byref(na), self.batches_per_epoch, L.stream_ptr(stream))
+            self.noise_ready = True
+        elif self.fused_adam:   # + transposed operand copies + step counters
             L.call('cc_adam_dense_t', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v),
                    L.ptr(self.grads), L.ptr(self.shadow), n, L.ptr(self.state), cfg.lr, cfg.beta1,
                    cfg.beta2, cfg.eps, self.adam_regions, len(self.adam_regions),
@@ -556,8 +573,15 @@ class Trainer:
         deferred counters/transposes."""
         if self.graphs is not None:
             g_fb, _, _, g_main = self.graphs
-            (g_main if self.pending_rest and g_main is not None else g_fb).replay()
+            if self.pending_rest and g_main is not None and (self.noise_ready or not self.prefetch):
+                g_main.replay()     # previous step's rest + this forward/backward
+            else:
+                self.flush()
+                if self.noise_ready:   # (captured with F inside; redraw, identically)
+                    self.noise_ready = False
+                g_fb.replay()
             self.pending_rest = False
+            self.noise_ready = False
         else:
             self.forward_backward(stream)
 
@@ -603,9 +627,10 @@ class Trainer:
             with torch.cuda.graph(g_adam):
                 self.forward_backward_b()
         else:
-            with torch.cuda.graph(g_fb):
+            self.noise_ready = False
+            with torch.cuda.graph(g_fb):       # F inside
                 self.forward_backward()
-            with torch.cuda.graph(g_adam):
+            with torch.cuda.graph(g_adam):     # (with prefetch: + the next step's F)
                 self.apply_adam()
         g_main = None
         if self.fused_adam:
@@ -615,11 +640,13 @@ class Trainer:
                 self.apply_rest()
             if self.cfg.world == 1:   # rest of step k + forward/backward of step k+1
                 g_main = torch.cuda.CUDAGraph()
+                self.noise_ready = self.prefetch   # F already drawn by step k's Adam launch
                 with torch.cuda.graph(g_main):
                     self.apply_rest()
                     self.forward_backward()
         torch.cuda.synchronize()
         self.state.copy_(saved)
+        self.noise_ready = False
         self.graphs = (g_fb, g_adam, g_rest, g_main)
         self.timing = timing
 

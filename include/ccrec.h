@@ -95,6 +95,13 @@ typedef struct cc_noise_args {
   int32_t *status;                           /* [1] device error flags (0 = ok) */
 } cc_noise_args;
 int cc_noise_fwd(const cc_noise_args *a, void *stream);
+/* cc_adam_dense(p, m, v, g, shadow, n, next->state, ...) and, in the same launch, cc_noise_fwd
+ * for the step AFTER next->state (step + 1, batch advanced with epoch roll-over as
+ * cc_state_advance(batches_per_epoch) would) — the batch buffers must be free (this step's
+ * backward done).  The state itself is not modified. */
+int cc_adam_noise(float *p, float *m, float *v, const float *g, uint16_t *shadow, int64_t n,
+                  float lr, float beta1, float beta2, float eps, const cc_noise_args *next,
+                  int64_t batches_per_epoch, void *stream);
 
 /* ----------------------------------------------------------------------------------
  * E1 forward: H[r] = ReLU(sum_{j in x_r} W1[j] + b1).  Replaces Dense(d)(x) on the 0/1

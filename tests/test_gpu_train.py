@@ -13,11 +13,12 @@ from tests.gpu_helpers import problem, rel_err
 pytestmark = pytest.mark.gpu
 
 
-def _setup(V, d, B, C, reg, dtype, seed=3, sizes=(20, 40, 80), fused_tower=True):
+def _setup(V, d, B, C, reg, dtype, seed=3, sizes=(20, 40, 80), fused_tower=True, prefetch=True):
     lists, Mt, ns = problem(seed, C, V, sizes)
     P = model_ref.init_params(V, d, seed=seed, bias_std=0.01)
     lay = Layout(V, d)
-    cfg = TrainConfig(V=V, d=d, batch_size=B, reg=reg, dtype=dtype, seed=seed, fused_tower=fused_tower)
+    cfg = TrainConfig(V=V, d=d, batch_size=B, reg=reg, dtype=dtype, seed=seed, fused_tower=fused_tower,
+                      prefetch_noise=prefetch)
     data = DeviceDataset(lists, V, y_mtx=Mt.astype(np.float32) if reg > 0 else None, neg_sampler=ns)
     tr = Trainer(cfg, data, params_flat=lay.pack(P))
     perm = np.random.default_rng(seed).permutation(C).astype(np.int32)
@@ -137,8 +138,9 @@ def test_adam_fused_transposes_and_counters(bpe):
 
 def test_graph_replay_matches_eager_and_epochs_roll_over():
     V, d, B, C = 700, 64, 32, 128          # 4 batches per epoch
-    tr_e, lists, Mt, ns, P, _ = _setup(V, d, B, C, 0.1, 'bf16')
-    tr_g, *_ = _setup(V, d, B, C, 0.1, 'bf16')
+    # batch_lists() after step() must show that step's batch: no F prefetch here
+    tr_e, lists, Mt, ns, P, _ = _setup(V, d, B, C, 0.1, 'bf16', prefetch=False)
+    tr_g, *_ = _setup(V, d, B, C, 0.1, 'bf16', prefetch=False)
     rng = np.random.default_rng(1)
     perms = np.stack([rng.permutation(C) for _ in range(2)]).astype(np.int32)
     tr_e.set_epoch_permutations(perms)
@@ -158,6 +160,32 @@ def test_graph_replay_matches_eager_and_epochs_roll_over():
     assert torch.equal(tr_e.params, tr_g.params)
     tr_g.flush()            # the last step's counters run at the head of the next step
     assert tr_g.state.cpu().tolist()[:3] == [6, 2, 1]
+
+
+@pytest.mark.parametrize('reg', [0.0, 0.1])
+def test_noise_prefetch_is_exact(reg):
+    """F drawn in the previous step's Adam launch (cc_adam_noise) == F at the head of the step:
+    identical parameters and losses over epoch roll-overs, eager and as graph replays."""
+    V, d, B, C = 700, 64, 32, 128          # 4 batches per epoch
+    perms = np.stack([np.random.default_rng(s).permutation(C) for s in (1, 2)]).astype(np.int32)
+    trs = []
+    for prefetch, graphs in ((False, False), (True, False), (True, True)):
+        tr, *_ = _setup(V, d, B, C, reg, 'bf16', prefetch=prefetch)
+        assert tr.prefetch == prefetch
+        tr.set_epoch_permutations(perms)
+        if graphs:
+            tr.capture()
+        trs.append(tr)
+    for step in range(7):
+        for tr in trs:
+            tr.step()
+        torch.cuda.synchronize()
+        assert trs[0].losses() == trs[1].losses() == trs[2].losses()
+    for tr in trs:
+        tr.flush()
+    for tr in trs[1:]:
+        assert torch.equal(tr.params, trs[0].params)
+        assert torch.equal(tr.state, trs[0].state)
 
 
 @pytest.mark.parametrize('reg', [0.0, 0.1])
