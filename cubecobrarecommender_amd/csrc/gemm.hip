@@ -379,18 +379,19 @@ __device__ __forceinline__ float bce_dz(float z, uint32_t ybit, float scale, flo
   return (sig - y) * scale;
 }
 
+// One output tile of one problem: block `bid` of the problem's `nblk` tile blocks, K split
+// `split`; the LDS arrays come from the launching kernel (so two problems sharing a launch do
+// not double the LDS).
 template <int EPI, int BM>
-__global__ __launch_bounds__(NtCfg<BM>::NTH) void gemm_nt_bf16_kernel(GemmParams p, int tiles_m) {
+__device__ __forceinline__ void nt_body(const GemmParams &p, int tiles_m, int bid, int nblk,
+                                        int split, char *smem, uint32_t (*ys)[NBN / 32],
+                                        double *red, int &lastflag) {
   using C = NtCfg<BM>;
   constexpr bool kBceRegs = BM <= 128;  // BCE math on the accumulators (no register pressure)
   constexpr int BK = C::BK, NTH = C::NTH;
-  __shared__ __attribute__((aligned(16))) char smem[C::LDS];
-  __shared__ uint32_t ys[BM][NBN / 32];  // BCE targets of the tile
-  __shared__ double red[NTH / 64];
-  __shared__ int lastflag;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int tile = xcd_tile(bid, nblk);
   // BCE: block-sum the loss and publish it as this tile's partial; with loss_out, an sc1 store
   // + agent ticket (MI355X guide hand-off: no L2 writeback fence) tells the last block to reduce.
   // Called before the epilogue's global stores, so the vmcnt wait has nothing else to drain.
@@ -409,7 +410,7 @@ __global__ __launch_bounds__(NtCfg<BM>::NTH) void gemm_nt_bf16_kernel(GemmParams
         __hip_atomic_store(&p.loss_partials[tile], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint32_t tk = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        lastflag = tk == gridDim.x - 1;
+        lastflag = tk == (uint32_t)nblk - 1;
       }
     }
   };
@@ -417,7 +418,7 @@ __global__ __launch_bounds__(NtCfg<BM>::NTH) void gemm_nt_bf16_kernel(GemmParams
   int kbeg = 0, kend = p.K;
   if constexpr (EPI == CC_EPI_SPLITK) {
     const int kchunk = (int)cdiv(cdiv(p.K, p.splits), BK) * BK;
-    kbeg = blockIdx.y * kchunk;
+    kbeg = split * kchunk;
     kend = min(p.K, kbeg + kchunk);
   }
   if constexpr (EPI == CC_EPI_BCE) {  // lands during the K loop
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(NtCfg<BM>::NTH) void gemm_nt_bf16_kernel(GemmParams
     }
   }
   if (do_cs && bn + (int)threadIdx.x < p.N) {
-    const int64_t zo = EPI == CC_EPI_SPLITK ? (int64_t)blockIdx.y * p.N : 0;
+    const int64_t zo = EPI == CC_EPI_SPLITK ? (int64_t)split * p.N : 0;
     p.colsum[zo + bn + threadIdx.x] = cs;
   }
 
@@ -497,7 +498,7 @@ __global__ __launch_bounds__(NtCfg<BM>::NTH) void gemm_nt_bf16_kernel(GemmParams
   float *Cf = p.Cf;
   int64_t ldf = p.ldc;
   if constexpr (EPI == CC_EPI_SPLITK) {
-    Cf = p.Cf + (int64_t)blockIdx.y * p.M * p.N;
+    Cf = p.Cf + (int64_t)split * p.M * p.N;
     ldf = p.N;
   }
   bf16_t *Cb = EPI == CC_EPI_SPLITK ? nullptr : reinterpret_cast<bf16_t *>(p.C);
@@ -600,7 +601,7 @@ __global__ __launch_bounds__(NtCfg<BM>::NTH) void gemm_nt_bf16_kernel(GemmParams
       __syncthreads();  // separate reduce launch
       if (lastflag) {
         double s2 = 0.0;
-        for (int i = threadIdx.x; i < (int)gridDim.x; i += NTH)
+        for (int i = threadIdx.x; i < nblk; i += NTH)
           s2 += __hip_atomic_load(&p.loss_partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) s2 += __shfl_xor(s2, off);
@@ -614,6 +615,36 @@ __global__ __launch_bounds__(NtCfg<BM>::NTH) void gemm_nt_bf16_kernel(GemmParams
         }
       }
     }
+  }
+}
+
+template <int EPI, int BM>
+__global__ __launch_bounds__(NtCfg<BM>::NTH) void gemm_nt_bf16_kernel(GemmParams p, int tiles_m) {
+  __shared__ __attribute__((aligned(16))) char smem[NtCfg<BM>::LDS];
+  __shared__ uint32_t ys[EPI == CC_EPI_BCE ? BM : 1][NBN / 32];  // BCE targets of the tile
+  __shared__ double red[NtCfg<BM>::NTH / 64];
+  __shared__ int lastflag;
+  nt_body<EPI, BM>(p, tiles_m, blockIdx.x, gridDim.x, blockIdx.y, smem, ys, red, lastflag);
+}
+
+// Two independent NT problems in one launch (grouped GEMM): blocks [0, nb0*s0) are problem 0's
+// (tile, split) pairs, the rest problem 1's — the decoder's dX (split-K) and dW products fill
+// the chip together instead of one after the other.
+template <int E0, int E1>
+__global__ __launch_bounds__(NtCfg<128>::NTH) void gemm_nt_pair_kernel(GemmParams p0, int tm0, int nb0,
+                                                                       int s0, GemmParams p1, int tm1,
+                                                                       int nb1) {
+  static_assert(E0 != CC_EPI_BCE && E1 != CC_EPI_BCE, "pair: no loss hand-off");
+  __shared__ __attribute__((aligned(16))) char smem[NtCfg<128>::LDS];
+  __shared__ uint32_t ys[1][NBN / 32];
+  __shared__ double red[NtCfg<128>::NTH / 64];
+  __shared__ int lastflag;
+  const int b = blockIdx.x;
+  if (b < nb0 * s0) {
+    nt_body<E0, 128>(p0, tm0, b % nb0, nb0, b / nb0, smem, ys, red, lastflag);
+  } else {
+    const int c = b - nb0 * s0;
+    nt_body<E1, 128>(p1, tm1, c % nb1, nb1, c / nb1, smem, ys, red, lastflag);
   }
 }
 
@@ -789,17 +820,15 @@ extern "C" int cc_gemm_grid(int32_t M, int32_t N, int32_t *tiles) {
   return CC_OK;
 }
 
-extern "C" int cc_gemm(const cc_gemm_args *g, void *stream) {
+static int gemm_params(const cc_gemm_args *g, GemmParams &p) {
   CC_REQUIRE(g && g->A && g->B, "cc_gemm: null operand");
   CC_REQUIRE(g->M >= 0 && g->N >= 0 && g->K >= 0, "cc_gemm: negative size");
   CC_REQUIRE(g->dtype == CC_BF16 || g->dtype == CC_F32, "cc_gemm: dtype");
-  if (g->M == 0 || g->N == 0) return CC_OK;
   if (g->epilogue == CC_EPI_SPLITK) CC_REQUIRE(g->splits >= 1 && g->Cf, "cc_gemm: split-K needs Cf, splits>=1");
   if (g->epilogue == CC_EPI_BCE)
     CC_REQUIRE(g->bias && g->y_bits && g->loss_partials, "cc_gemm: BCE needs bias, y_bits, loss_partials");
   if (g->epilogue == CC_EPI_MASK) CC_REQUIRE(g->H, "cc_gemm: MASK needs H");
   const int vw = g->dtype == CC_BF16 ? 8 : 4;
-  GemmParams p;
   p.M = g->M; p.N = g->N; p.K = g->K;
   p.lda = g->lda; p.ldb = g->ldb; p.ldc = g->ldc;
   p.splits = g->splits; p.relu = g->relu;
@@ -815,15 +844,25 @@ extern "C" int cc_gemm(const cc_gemm_args *g, void *stream) {
   p.ticket = g->ticket;
   CC_REQUIRE(!p.loss_out || p.ticket, "cc_gemm: loss_out needs a ticket word");
   CC_REQUIRE(!g->Ct || g->epilogue == CC_EPI_BCE, "cc_gemm: Ct only with the BCE epilogue");
+  return CC_OK;
+}
 
-  hipStream_t s = as_stream(stream);
-  // bf16 with both operands K-contiguous and 16-B aligned rows: the 128x128 NT kernel
+// bf16 with both operands K-contiguous and 16-B aligned rows: the 128x128 NT kernel
+static bool nt_path(const cc_gemm_args *g, const GemmParams &p) {
   static const bool nt_enabled = [] {
     const char *e = getenv("CCREC_GEMM_NT");  // A/B switch for benchmarking the generic kernel
     return !(e && e[0] == '0');
   }();
-  if (nt_enabled && g->dtype == CC_BF16 && !g->ta && g->tb && p.vec_a && p.vec_b &&
-      g->epilogue != CC_EPI_MASK) {
+  return nt_enabled && g->dtype == CC_BF16 && !g->ta && g->tb && p.vec_a && p.vec_b &&
+         g->epilogue != CC_EPI_MASK;
+}
+
+extern "C" int cc_gemm(const cc_gemm_args *g, void *stream) {
+  GemmParams p;
+  if (int rc = gemm_params(g, p)) return rc;
+  if (g->M == 0 || g->N == 0) return CC_OK;
+  hipStream_t s = as_stream(stream);
+  if (nt_path(g, p)) {
     switch (g->epilogue) {
       case CC_EPI_STORE: return launch_nt<CC_EPI_STORE>(g, p, s);
       case CC_EPI_BCE: return launch_nt<CC_EPI_BCE>(g, p, s);  // reduces the loss itself
@@ -837,6 +876,34 @@ extern "C" int cc_gemm(const cc_gemm_args *g, void *stream) {
   int32_t tiles = 0;
   cc_gemm_grid(g->M, g->N, &tiles);
   return cc_reduce_loss(g->loss_partials, tiles, g->loss_scale, g->loss_out, stream);
+}
+
+extern "C" int cc_gemm_pair(const cc_gemm_args *g0, const cc_gemm_args *g1, void *stream) {
+  GemmParams p0, p1;
+  if (int rc = gemm_params(g0, p0)) return rc;
+  if (int rc = gemm_params(g1, p1)) return rc;
+  auto pairable = [](const cc_gemm_args *g, const GemmParams &p) {
+    return nt_path(g, p) && g->M > 0 && g->N > 0 &&
+           (g->epilogue == CC_EPI_STORE || g->epilogue == CC_EPI_SPLITK);
+  };
+  if (!pairable(g0, p0) || !pairable(g1, p1)) {  // one after the other
+    if (int rc = cc_gemm(g0, stream)) return rc;
+    return cc_gemm(g1, stream);
+  }
+  const int tm0 = (int)cdiv(g0->M, 128), nb0 = tm0 * (int)cdiv(g0->N, NBN);
+  const int tm1 = (int)cdiv(g1->M, 128), nb1 = tm1 * (int)cdiv(g1->N, NBN);
+  const int s0 = g0->epilogue == CC_EPI_SPLITK ? g0->splits : 1;
+  const int s1 = g1->epilogue == CC_EPI_SPLITK ? g1->splits : 1;
+  const dim3 grid((unsigned)(nb0 * s0 + nb1 * s1)), block(NtCfg<128>::NTH);
+  hipStream_t s = as_stream(stream);
+#define PAIR(E0, E1) hipLaunchKernelGGL((gemm_nt_pair_kernel<E0, E1>), grid, block, 0, s, p0, tm0, nb0, s0, p1, tm1, nb1)
+  if (g0->epilogue == CC_EPI_SPLITK && g1->epilogue == CC_EPI_STORE) PAIR(CC_EPI_SPLITK, CC_EPI_STORE);
+  else if (g0->epilogue == CC_EPI_STORE && g1->epilogue == CC_EPI_SPLITK) PAIR(CC_EPI_STORE, CC_EPI_SPLITK);
+  else if (g0->epilogue == CC_EPI_STORE) PAIR(CC_EPI_STORE, CC_EPI_STORE);
+  else PAIR(CC_EPI_SPLITK, CC_EPI_SPLITK);
+#undef PAIR
+  CC_LAUNCH_CHECK("gemm_nt_pair_kernel");
+  return CC_OK;
 }
 
 extern "C" int cc_splitk_reduce(int32_t dtype, const float *partials, int32_t splits, int32_t M,

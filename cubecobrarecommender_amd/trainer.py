@@ -331,13 +331,16 @@ class Trainer:
 
     def _gemm(self, M, N, K, A, lda, B, ldb, ta=0, tb=0, epi=L.CC_EPI_STORE, ldc=None, bias=None,
               relu=0, C=None, Cf=None, H=None, y_bits=None, scale=0.0, partials=None, splits=1,
-              colsum=None, Ct=None, ldct=0, stream=None, loss_out=None, loss_scale=0.0, ticket=None):
+              colsum=None, Ct=None, ldct=0, stream=None, loss_out=None, loss_scale=0.0, ticket=None,
+              launch=True):
         g = L.GemmArgs(dtype=self.dtype, ta=ta, tb=tb, epilogue=epi, M=M, N=N, K=K, lda=lda,
                        ldb=ldb, ldc=ldc if ldc is not None else N, splits=splits, relu=relu,
                        A=A, B=B, bias=bias, C=C, Cf=Cf, H=H, y_bits=y_bits, scale=scale,
                        loss_partials=partials, colsum=colsum, Ct=Ct, ldct=ldct,
                        loss_out=loss_out, loss_scale=loss_scale, ticket=ticket)
-        L.call('cc_gemm', L.C.byref(g), stream if stream is not None else self._s)
+        if launch:
+            L.call('cc_gemm', L.C.byref(g), stream if stream is not None else self._s)
+        return g
 
     def _dense_fwd(self, X, rows, K, N, name, out):
         """out[rows] = relu(X[rows] @ W + b) (model.py Dense(relu))."""
@@ -439,6 +442,18 @@ class Trainer:
         # (side stream) and dX -> towers (this stream) only share read-only inputs.
         for pre, (r0, r1) in branches:
             dz = self.dZout[r0:]
+            if self.fused_tower and r0 == 0 and not self.timing and not self.overlap:
+                # dX (split-K) and dW = D3^T dZ (+ dbo) in one grouped launch
+                gx = self._gemm(B, d, V, L.ptr(dz), V, self.w(pre + '/reconstruct/kernel'), V, ta=0, tb=1,
+                                epi=L.CC_EPI_SPLITK, Cf=L.ptr(self.split_buf), splits=self.splits,
+                                launch=False)
+                gw = self._gemm(d, V, B, L.ptr(self.D3t), R, L.ptr(self.dZt), B, ta=0, tb=1,
+                                Cf=self.gp(pre + '/reconstruct/kernel'),
+                                colsum=self.gp(pre + '/reconstruct/bias'), launch=False)
+                L.call('cc_gemm_pair', L.C.byref(gx), L.C.byref(gw), s)
+                L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), self.splits, B, d,
+                       L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
+                continue
             t = self._tick('dec_dW', self.side if self.overlap else None)
             if self.fused_tower and r0 == 0:   # dW = D3^T dZ with both operands k-contiguous
                 self._gemm(d, V, B, L.ptr(self.D3t), R, L.ptr(self.dZt), B, ta=0, tb=1,

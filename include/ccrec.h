@@ -161,6 +161,9 @@ typedef struct cc_gemm_args {
   uint32_t *ticket;     /* with loss_out: one zeroed word, left zeroed */
 } cc_gemm_args;
 int cc_gemm(const cc_gemm_args *g, void *stream);
+/* Two independent products in one launch (grouped GEMM) when both take the bf16 NT path with
+ * the STORE or SPLITK epilogue; otherwise cc_gemm(g0) then cc_gemm(g1).  Same results. */
+int cc_gemm_pair(const cc_gemm_args *g0, const cc_gemm_args *g1, void *stream);
 /* workspace bound for cc_gemm's loss partials: ceil(M/64)*ceil(N/64) doubles */
 int cc_gemm_grid(int32_t M, int32_t N, int32_t *tiles);
 

@@ -247,3 +247,38 @@ def test_transpose_bf16_and_fp32(rows, cols):
         L.call('cc_transpose', dt, L.ptr(src), rows, cols, L.ptr(dst), L.stream_ptr())
         torch.cuda.synchronize()
         assert torch.equal(dst, src.t().contiguous())
+
+
+@pytest.mark.parametrize('B,d,V,splits', [(128, 64, 700, 4), (512, 256, 2500, 8)])
+def test_gemm_pair_equals_two_launches(B, d, V, splits):
+    """cc_gemm_pair (grouped dX split-K + dW with colsum) == the two cc_gemm launches, bitwise."""
+    bf = dict(device='cuda', dtype=torch.bfloat16)
+    dZ = (torch.randn(B, V, device='cuda') * 1e-3).to(torch.bfloat16)
+    Wo = torch.randn(d, V, **bf)
+    D3t = torch.randn(d, B, **bf)
+    dZt = dZ.t().contiguous()
+
+    def args(out_split, gW, gb):
+        gx = L.GemmArgs(dtype=L.CC_BF16, ta=0, tb=1, epilogue=L.CC_EPI_SPLITK, M=B, N=d, K=V, lda=V, ldb=V,
+                        ldc=d, splits=splits, A=dZ.data_ptr(), B=Wo.data_ptr(), Cf=out_split.data_ptr())
+        gw = L.GemmArgs(dtype=L.CC_BF16, ta=0, tb=1, epilogue=L.CC_EPI_STORE, M=d, N=V, K=B, lda=B, ldb=B,
+                        ldc=V, splits=1, A=D3t.data_ptr(), B=dZt.data_ptr(), Cf=gW.data_ptr(), colsum=gb.data_ptr())
+        return gx, gw
+
+    outs = []
+    for pair in (False, True):
+        sp = torch.zeros(splits * B * d, device='cuda')
+        gW = torch.zeros(d, V, device='cuda')
+        gb = torch.zeros(V, device='cuda')
+        gx, gw = args(sp, gW, gb)
+        if pair:
+            L.call('cc_gemm_pair', ctypes.byref(gx), ctypes.byref(gw), L.stream_ptr())
+        else:
+            L.call('cc_gemm', ctypes.byref(gx), L.stream_ptr())
+            L.call('cc_gemm', ctypes.byref(gw), L.stream_ptr())
+        torch.cuda.synchronize()
+        outs.append((sp.cpu(), gW.cpu(), gb.cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    ref = (D3t.float() @ dZt.float().t())
+    assert rel_err(outs[1][1].numpy(), ref.cpu().numpy()) < 1e-5
