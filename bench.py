@@ -173,8 +173,10 @@ def main():
     n_grad = tr.layout.total if tr.use_reg else tr.layout.main_total
 
     adam_ev = []
+    ADAM_SAMPLE = 8
 
     def step(graphed, timed=False):
+        step.count = getattr(step, 'count', -1) + 1 if timed else -1
         if world > 1:   # bucketed reduce-scatter + sharded Adam + all-gather (zero.py)
             if not graphed:
                 saved, tr.graphs = tr.graphs, None
@@ -183,10 +185,11 @@ def main():
             else:
                 tr.step_dp(timing=timed)
             return
-        if timed and graphed:
-            # HIP events on the stream, bracketing the Adam kernel launched right behind the
-            # forward/backward graph: the host is far ahead of the GPU here, so the kernel is
-            # already queued when e0 fires and the interval is the kernel's own duration.
+        if timed and graphed and (len(adam_ev) == 0 or step.count % ADAM_SAMPLE == 0):
+            # every ADAM_SAMPLE-th timed step: HIP events on the stream bracketing the Adam kernel,
+            # launched eagerly right behind the forward/backward graph (the host is far ahead of
+            # the GPU, so the kernel is queued when e0 fires: the interval is its own duration).
+            # The other steps replay the whole step as one graph.
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             tr.run_fb()
             tr.run_adam(events=(e0, e1))

@@ -587,7 +587,7 @@ class Trainer:
         """Forward/backward of one step (graph replay or eager), preceded by the previous step's
         deferred counters/transposes."""
         if self.graphs is not None:
-            g_fb, _, _, g_main = self.graphs
+            g_fb, _, _, g_main, _ = self.graphs
             if self.pending_rest and g_main is not None and (self.noise_ready or not self.prefetch):
                 g_main.replay()     # previous step's rest + this forward/backward
             else:
@@ -615,6 +615,12 @@ class Trainer:
     def step(self, stream=None):
         if self.cfg.world > 1:
             self.step_dp()
+            return
+        if (self.graphs is not None and self.graphs[4] is not None and self.pending_rest
+                and (self.noise_ready or not self.prefetch)):
+            self.graphs[4].replay()    # steady state: rest(k-1) + fwd/bwd(k) + Adam(k) in one graph
+            self.pending_rest = True
+            self.noise_ready = self.prefetch
             return
         self.run_fb(stream)
         self.run_adam(stream)
@@ -647,22 +653,27 @@ class Trainer:
                 self.forward_backward()
             with torch.cuda.graph(g_adam):     # (with prefetch: + the next step's F)
                 self.apply_adam()
-        g_main = None
+        g_main = g_all = None
         if self.fused_adam:
             g_rest = None
         else:
             with torch.cuda.graph(g_rest):
                 self.apply_rest()
-            if self.cfg.world == 1:   # rest of step k + forward/backward of step k+1
-                g_main = torch.cuda.CUDAGraph()
+            if self.cfg.world == 1:   # rest of step k + forward/backward of step k+1 (+ its Adam)
+                g_main, g_all = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
                 self.noise_ready = self.prefetch   # F already drawn by step k's Adam launch
                 with torch.cuda.graph(g_main):
                     self.apply_rest()
                     self.forward_backward()
+                self.noise_ready = self.prefetch
+                with torch.cuda.graph(g_all):
+                    self.apply_rest()
+                    self.forward_backward()
+                    self.apply_adam()
         torch.cuda.synchronize()
         self.state.copy_(saved)
         self.noise_ready = False
-        self.graphs = (g_fb, g_adam, g_rest, g_main)
+        self.graphs = (g_fb, g_adam, g_rest, g_main, g_all)
         self.timing = timing
 
     # ------------------------------------------------------------------ inspection (tests)
