@@ -38,7 +38,7 @@ def parse():
                     help="collective backend for --gpus > 1 (nccl = RCCL; gloo only to rehearse the "
                          "data-parallel path with several ranks on one GPU)")
     ap.add_argument('--traffic-json', default=os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                                           'profiles', 'traffic_r01.json'))
+                                                           'profiles', 'traffic_r01c.json'))
     return ap.parse_args()
 
 
@@ -237,9 +237,10 @@ def main():
         roof['traffic'] = None
         if args.traffic_json and os.path.exists(args.traffic_json):
             # PMC bytes were collected on one configuration: attach them only to the same launch
-            tj = json.load(open(args.traffic_json)).get('adam_kernel') or {}
+            key = 'adam_noise_kernel' if getattr(tr, 'prefetch', False) else 'adam_kernel'
+            tj = json.load(open(args.traffic_json)).get(key) or {}
             tb = tj.get('bytes_per_launch')
-            if tb and abs(tb - roof['bytes_per_launch']) <= 0.02 * roof['bytes_per_launch']:
+            if tb and abs(tb - roof['bytes_per_launch']) <= 0.05 * roof['bytes_per_launch']:
                 roof['traffic'] = tb
                 roof['traffic_detail'] = tj
     else:   # sharded Adam: this rank's 1/world shard of every bucket, per step

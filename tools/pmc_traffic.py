@@ -16,6 +16,13 @@ import sys
 def per_dispatch(d, counter, kname):
     files = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)
     vals = {}
+    for db in glob.glob(os.path.join(d, '**', '*.db'), recursive=True):   # rocprofv3 rocpd output
+        import sqlite3
+        c = sqlite3.connect(db)
+        for disp, name, cn, v in c.execute(
+                'select dispatch_id, kernel_name, counter_name, value from counters_collection'):
+            if counter in cn and kname in name:
+                vals[(db, disp)] = vals.get((db, disp), 0.0) + float(v)
     for f in files:
         for r in csv.DictReader(open(f)):
             if counter not in r.get('Counter_Name', '') or kname not in r.get('Kernel_Name', ''):
