@@ -74,6 +74,100 @@ __global__ __launch_bounds__(NT) void softmax_kl_kernel(const float *__restrict_
   if (threadIdx.x == 0) kl_part[b] = kl;
 }
 
+// The same row computation with the row held in registers: one 1024-thread workgroup per row,
+// z and t read from HBM exactly once as float4s (NV per thread, V <= 4096 NV), so the kernel
+// moves 8 B/element in and sizeof(T) out — the HBM floor of the regulariser loss — instead of
+// re-reading the row four times.  Same element formulas as softmax_kl_kernel.
+constexpr int NTR = 1024;
+
+template <typename Tv, int W>
+__device__ __forceinline__ Tv rows_reduce(Tv v, Tv *red, bool is_max) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const Tv o = __shfl_xor(v, off);
+    v = is_max ? (v > o ? v : o) : v + o;
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  Tv r = red[0];
+#pragma unroll
+  for (int w = 1; w < W; ++w) r = is_max ? (r > red[w] ? r : red[w]) : r + red[w];
+  return r;
+}
+
+template <typename T, int NV>
+__global__ __launch_bounds__(NTR) void softmax_kl_rows_kernel(const float *__restrict__ Z2, int V,
+                                                              const float *__restrict__ Mt,
+                                                              const int32_t *__restrict__ reg_idx,
+                                                              float scale, T *__restrict__ dZ,
+                                                              double *__restrict__ kl_part) {
+  __shared__ float redf[NTR / 64];
+  __shared__ double redd[NTR / 64];
+  const int b = blockIdx.x, V4 = V >> 2;
+  const float4 *z4 = reinterpret_cast<const float4 *>(Z2 + (int64_t)b * V);
+  const float4 *t4 = reinterpret_cast<const float4 *>(Mt + (int64_t)reg_idx[b] * V);
+  float z[NV][4], t[NV][4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int j = threadIdx.x + i * NTR;
+    const float4 zz = j < V4 ? z4[j] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    const float4 tt = j < V4 ? t4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    z[i][0] = zz.x, z[i][1] = zz.y, z[i][2] = zz.z, z[i][3] = zz.w;
+    t[i][0] = tt.x, t[i][1] = tt.y, t[i][2] = tt.z, t[i][3] = tt.w;
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) mx = fmaxf(mx, z[i][e]);
+  mx = rows_reduce<float, NTR / 64>(mx, redf, true);
+  float se = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      z[i][e] = expf(z[i][e] - mx);  // padding: exp(-inf) = 0
+      se += z[i][e];
+    }
+  se = rows_reduce<float, NTR / 64>(se, redf, false);
+  const float inv = 1.f / se;
+  double kl = 0.0, S = 0.0;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    if ((int)threadIdx.x + i * NTR >= V4) break;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float p = z[i][e] * inv;
+      const float tc = fminf(fmaxf(t[i][e], 1e-7f), 1.f);
+      const float q = fminf(fmaxf(p, 1e-7f), 1.f);
+      kl += (double)(tc * logf(tc / q));
+      if (p >= 1e-7f) S += (double)tc;
+      z[i][e] = p;
+      t[i][e] = p >= 1e-7f ? -tc : 0.f;
+    }
+  }
+  kl = rows_reduce<double, NTR / 64>(kl, redd, false);
+  S = rows_reduce<double, NTR / 64>(S, redd, false);
+  const float Sf = (float)S;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int j = threadIdx.x + i * NTR;
+    if (j >= V4) break;
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = scale * (t[i][e] + z[i][e] * Sf);
+    if constexpr (sizeof(T) == 2) {
+      uint2 pk = make_uint2((uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16),
+                            (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16));
+      reinterpret_cast<uint2 *>(dZ + (int64_t)b * V)[j] = pk;
+    } else {
+      reinterpret_cast<float4 *>(dZ + (int64_t)b * V)[j] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  if (threadIdx.x == 0) kl_part[b] = kl;
+}
+
 // TF ResourceApplyAdam: alpha = lr sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1); v += (g^2-v)(1-b2);
 // p -= m*alpha/(sqrt(v)+eps).  t = state[0] + 1.
 
@@ -256,6 +350,29 @@ extern "C" int cc_dec_softmax_kl_fused(int32_t dtype, const float *Z2, int32_t B
   CC_REQUIRE(Z2 && y_reg && reg_idx && dZ && kl_partials, "cc_dec_softmax_kl_fused: null pointer");
   if (B == 0) return CC_OK;
   const float scale = reg / (float)B;
+  const bool aligned = (V % 4 == 0) && ((uintptr_t)Z2 % 16 == 0) && ((uintptr_t)y_reg % 16 == 0) &&
+                       ((uintptr_t)dZ % 16 == 0);
+  const int nv = (int)cdiv(V, 4 * NTR);
+  if (aligned && nv <= 8 && getenv("CCREC_KL_ROWS") == nullptr) {  // register-resident rows
+    const hipStream_t s = as_stream(stream);
+#define KL_ROWS(NVV)                                                                            \
+  if (nv <= NVV) {                                                                              \
+    if (dtype == CC_BF16)                                                                       \
+      hipLaunchKernelGGL((softmax_kl_rows_kernel<bf16_t, NVV>), dim3(B), dim3(NTR), 0, s, Z2, V, \
+                         y_reg, reg_idx, scale, (bf16_t *)dZ, kl_partials);                     \
+    else                                                                                        \
+      hipLaunchKernelGGL((softmax_kl_rows_kernel<float, NVV>), dim3(B), dim3(NTR), 0, s, Z2, V,  \
+                         y_reg, reg_idx, scale, (float *)dZ, kl_partials);                      \
+    CC_LAUNCH_CHECK("softmax_kl_rows_kernel");                                                  \
+    return CC_OK;                                                                               \
+  }
+    KL_ROWS(1)
+    KL_ROWS(2)
+    KL_ROWS(4)
+    KL_ROWS(6)
+    KL_ROWS(8)
+#undef KL_ROWS
+  }
   if (dtype == CC_BF16)
     hipLaunchKernelGGL(softmax_kl_kernel<bf16_t>, dim3(B), dim3(NT), 0, as_stream(stream), Z2, V,
                        y_reg, reg_idx, scale, (bf16_t *)dZ, kl_partials);

@@ -168,7 +168,7 @@ class Trainer:
             self.slab = torch.zeros((R // 32) * slab, **f32)
             # decoder operands kept k-contiguous: D3^T (tower fwd), dZ^T (BCE epilogue), Wo^T shadow
             self.D3t = torch.zeros(d, R, **T)
-            self.dZt = torch.zeros(V, B, **T)
+            self.dZt = torch.zeros(len(branches_of(self.use_reg)), V, B, **T)   # [branch][V][B]
             self.WoT = torch.zeros(len(branches_of(self.use_reg)), V, d, **T)
             self.targs = self._tower_args()
             self.transpose_tower()
@@ -416,7 +416,7 @@ class Trainer:
             self._gemm(B, V, d, L.ptr(self.D3), d, L.ptr(self.WoT[0]), d, tb=1,
                        epi=L.CC_EPI_BCE, bias=self.pf('decoder/reconstruct/bias'), C=L.ptr(self.dZout),
                        y_bits=L.ptr(self.y_bits), scale=1.0 / (B * V), partials=L.ptr(self.bce_part),
-                       Ct=L.ptr(self.dZt), ldct=B, loss_out=L.ptr(self.loss_dev),
+                       Ct=L.ptr(self.dZt[0]), ldct=B, loss_out=L.ptr(self.loss_dev),
                        loss_scale=1.0 / (B * V), ticket=L.ptr(self.tickets))
         else:
             self._gemm(B, V, d, L.ptr(self.D3), d, self.w('decoder/reconstruct/kernel'), V,
@@ -434,20 +434,24 @@ class Trainer:
             else:
                 self._gemm(B, V, d, L.ptr(self.D3[B:]), d, self.w('decoder_for_reg/reconstruct/kernel'), V,
                            bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2))
+            t = self._tick('dec_softmax_kl')
             L.call('cc_dec_softmax_kl_fused', self.dtype, L.ptr(self.Z2), B, V, L.ptr(self.data.y_reg),
                    L.ptr(self.reg_idx), float(cfg.reg), L.ptr(self.dZout[B:]), L.ptr(self.kl_part), s)
+            t()
+            if self.fused_tower:   # dZ2^T [V][B]: the k-contiguous operand of the reg branch's dW
+                L.call('cc_transpose', self.dtype, L.ptr(self.dZout[B:]), B, V, L.ptr(self.dZt[1]), s)
             ss = self._fork()
             L.call('cc_reduce_loss', L.ptr(self.kl_part), B, 1.0 / B, L.ptr(self.loss_dev[1:]), ss)
         # ---- backward through the output layers and decoder towers.  The output layers' dW
         # (side stream) and dX -> towers (this stream) only share read-only inputs.
-        for pre, (r0, r1) in branches:
+        for k, (pre, (r0, r1)) in enumerate(branches):
             dz = self.dZout[r0:]
-            if self.fused_tower and r0 == 0 and not self.timing and not self.overlap:
+            if self.fused_tower and not self.timing and not self.overlap:
                 # dX (split-K) and dW = D3^T dZ (+ dbo) in one grouped launch
                 gx = self._gemm(B, d, V, L.ptr(dz), V, self.w(pre + '/reconstruct/kernel'), V, ta=0, tb=1,
                                 epi=L.CC_EPI_SPLITK, Cf=L.ptr(self.split_buf), splits=self.splits,
                                 launch=False)
-                gw = self._gemm(d, V, B, L.ptr(self.D3t), R, L.ptr(self.dZt), B, ta=0, tb=1,
+                gw = self._gemm(d, V, B, L.ptr(self.D3t[:, r0:]), R, L.ptr(self.dZt[k]), B, ta=0, tb=1,
                                 Cf=self.gp(pre + '/reconstruct/kernel'),
                                 colsum=self.gp(pre + '/reconstruct/bias'), launch=False)
                 L.call('cc_gemm_pair', L.C.byref(gx), L.C.byref(gw), s)
@@ -455,8 +459,8 @@ class Trainer:
                        L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
                 continue
             t = self._tick('dec_dW', self.side if self.overlap else None)
-            if self.fused_tower and r0 == 0:   # dW = D3^T dZ with both operands k-contiguous
-                self._gemm(d, V, B, L.ptr(self.D3t), R, L.ptr(self.dZt), B, ta=0, tb=1,
+            if self.fused_tower:   # dW = D3^T dZ with both operands k-contiguous
+                self._gemm(d, V, B, L.ptr(self.D3t[:, r0:]), R, L.ptr(self.dZt[k]), B, ta=0, tb=1,
                            Cf=self.gp(pre + '/reconstruct/kernel'), colsum=self.gp(pre + '/reconstruct/bias'),
                            stream=ss)
             else:

@@ -282,3 +282,46 @@ def test_gemm_pair_equals_two_launches(B, d, V, splits):
         assert torch.equal(a, b)
     ref = (D3t.float() @ dZt.float().t())
     assert rel_err(outs[1][1].numpy(), ref.cpu().numpy()) < 1e-5
+
+
+def _softmax_kl_ref(Z, T, reg, B):
+    """fp64 statement of the KL term: loss rows and dZ = reg/B p (g - <p,g>)."""
+    Z = Z.astype(np.float64)
+    p = np.exp(Z - Z.max(1, keepdims=True))
+    p /= p.sum(1, keepdims=True)
+    t = np.clip(T.astype(np.float64), 1e-7, 1.0)
+    q = np.clip(p, 1e-7, 1.0)
+    kl = (t * np.log(t / q)).sum(1)
+    live = p >= 1e-7
+    S = (t * live).sum(1, keepdims=True)
+    dz = reg / B * (np.where(live, -t, 0.0) + p * S)
+    return kl, dz
+
+
+@pytest.mark.parametrize('V', [701, 2500, 22000, 33000])
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
+def test_softmax_kl_rows(V, dtype):
+    """cc_dec_softmax_kl_fused: register-resident rows (V % 4 == 0, V <= 32768) and the generic
+    row kernel (V = 701, 33000) against fp64; rows with very negative logits exercise the
+    p < 1e-7 clip."""
+    rng = np.random.default_rng(V)
+    B, reg = 24, 0.1
+    Z = (rng.standard_normal((B, V)) * 3).astype(np.float32)
+    Z[::5, : V // 3] -= 40.0                    # p below the 1e-7 clip on a third of the row
+    Mt = rng.random((B + 3, V)).astype(np.float32) ** 8
+    Mt /= Mt.sum(1, keepdims=True)
+    Mt[:, ::7] = 0.0
+    ridx = rng.integers(0, B + 3, B).astype(np.int32)
+    dt = L.CC_BF16 if dtype == 'bf16' else L.CC_F32
+    tdt = torch.bfloat16 if dtype == 'bf16' else torch.float32
+    Zd = torch.from_numpy(Z).cuda()
+    Md = torch.from_numpy(Mt).cuda()
+    rd = torch.from_numpy(ridx).cuda()
+    dZ = torch.zeros(B, V, device='cuda', dtype=tdt)
+    part = torch.zeros(B, device='cuda', dtype=torch.float64)
+    L.call('cc_dec_softmax_kl_fused', dt, L.ptr(Zd), B, V, L.ptr(Md), L.ptr(rd), reg, L.ptr(dZ),
+           L.ptr(part), L.stream_ptr())
+    torch.cuda.synchronize()
+    kl, dz = _softmax_kl_ref(Z, Mt[ridx], reg, B)
+    np.testing.assert_allclose(part.cpu().numpy(), kl, rtol=1e-4)
+    assert rel_err(dZ.float().cpu().numpy(), dz) < (1e-5 if dtype == 'fp32' else 4e-3)
