@@ -6,7 +6,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('CCREC_LIB') or os.path.join(_HERE, 'libccrec_hip.so')
 
-CC_F32, CC_BF16 = 0, 1
+CC_F32, CC_BF16, CC_MX8 = 0, 1, 2
 CC_EPI_STORE, CC_EPI_BCE, CC_EPI_MASK, CC_EPI_SPLITK = 0, 1, 2, 3
 CC_NUM_TENSORS = 24
 
@@ -38,6 +38,7 @@ class GemmArgs(C.Structure):
         ('Cf', C.c_void_p), ('H', C.c_void_p), ('y_bits', C.c_void_p), ('scale', C.c_float),
         ('loss_partials', C.c_void_p), ('colsum', C.c_void_p), ('Ct', C.c_void_p), ('ldct', C.c_int32),
         ('loss_out', C.c_void_p), ('loss_scale', C.c_double), ('ticket', C.c_void_p),
+        ('a_scale', C.c_void_p), ('b_scale', C.c_void_p),
     ]
 
 
@@ -72,6 +73,7 @@ SIGNATURES = {
     'cc_splitk_reduce': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     'cc_colsum': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P]),
     'cc_transpose': (C.c_int, [_I32, _P, _I32, _I32, _P, _P]),
+    'cc_quant_mx8': (C.c_int, [_I32, _P, _I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P]),
     'cc_dec_bce_fused': (C.c_int, [_I32, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     'cc_dec_softmax_kl_fused': (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _F32, _P, _P, _P]),
     'cc_reduce_loss': (C.c_int, [_P, _I32, _F64, _P, _P]),

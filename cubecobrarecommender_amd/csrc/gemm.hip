@@ -34,6 +34,7 @@ struct GemmParams {
   double *loss_out;
   double loss_scale;
   uint32_t *ticket;
+  const uint8_t *sa, *sb;  // MX-FP8: E8M0 block scales [M][lda/32], [N][ldb/32]
 };
 
 template <typename T> struct Mma;
@@ -278,16 +279,23 @@ constexpr int SLD = NBN + 1;  // odd row pitch: column reads for C^T spread over
 #define NT_RING 2
 #endif
 
-template <int BM>
+// T = bf16_t (v_mfma_f32_32x32x16_bf16) or uint8_t = MX-FP8 e4m3 codes with one E8M0 scale per
+// 32 K-elements of a row (v_mfma_scale_f32_32x32x64_f8f6f4).  A K-tile is 128 bytes of every row
+// either way (64 bf16 / 128 fp8), so staging, swizzle and LDS footprint are shared.
+template <int BM, typename T = bf16_t>
 struct NtCfg {
+  static constexpr bool MX = sizeof(T) == 1;
   static constexpr int NTH = BM * 2;         // BM/32 waves of 64x64 outputs
-  static constexpr int BK = BM >= 512 ? 32 : 64;
-  static constexpr int CH = BK / 8;           // 16-B chunks per LDS row
+  static constexpr int BKB = BM >= 512 ? 64 : 128;   // bytes per row per K-tile
+  static constexpr int EPC = 16 / (int)sizeof(T);    // elements per 16-B chunk
+  static constexpr int BK = BKB / (int)sizeof(T);    // elements per K-tile
+  static constexpr int CH = BKB / 16;         // 16-B chunks per LDS row
   static constexpr int A_CH = BM * CH, B_CH = NBN * CH;
   static constexpr int NA = (A_CH + NTH - 1) / NTH, NB = (B_CH + NTH - 1) / NTH;
-  static constexpr int STAGE = (BM + NBN) * BK * 2;  // bytes per K-tile (A + B)
+  static constexpr int STAGE = (BM + NBN) * BKB;    // bytes per K-tile (A + B)
+  static constexpr int SCL = MX ? 2 * (BM + NBN) * 4 : 0;  // scale words, double-buffered
   static constexpr int SR = BM > 256 ? 256 : BM;     // rows per epilogue staging pass
-  static constexpr int LDS = 2 * STAGE > SR * SLD * 4 ? 2 * STAGE : SR * SLD * 4;
+  static constexpr int LDS = 2 * STAGE + SCL > SR * SLD * 4 ? 2 * STAGE + SCL : SR * SLD * 4;
 };
 
 __device__ __forceinline__ int xcd_tile(int b, int nb) {
@@ -297,40 +305,52 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
 
 // Per-thread staging plan, computed once: which 16-B chunks of the A/B tiles this thread moves,
 // their global element offsets at k = 0 (rows clamped at the edge: those rows only feed
-// discarded outputs) and their swizzled LDS offsets.  The K loop then only adds k0.
-template <int BM>
+// discarded outputs) and their swizzled LDS offsets.  The K loop then only adds k0.  MX: thread
+// t < BM (< 128) also moves row t's scale word of A (B) — the 4 E8M0 bytes of the K-tile.
+template <int BM, typename T = bf16_t>
 struct NtPlan {
-  using C = NtCfg<BM>;
+  using C = NtCfg<BM, T>;
   int64_t ga[C::NA], gb[C::NB];
   int la[C::NA], lb[C::NB];
+  int64_t gsa, gsb;
   __device__ __forceinline__ NtPlan(const GemmParams &p, int bm, int bn) {
 #pragma unroll
     for (int i = 0; i < C::NA; ++i) {
       const int v = min((int)threadIdx.x + C::NTH * i, C::A_CH - 1), row = v / C::CH, ch = v % C::CH;
-      ga[i] = (int64_t)min(bm + row, p.M - 1) * p.lda + ch * 8;
-      la[i] = row * C::BK + ((ch ^ (row & (C::CH - 1))) * 8);
+      ga[i] = (int64_t)min(bm + row, p.M - 1) * p.lda + ch * C::EPC;
+      la[i] = row * C::BK + ((ch ^ (row & (C::CH - 1))) * C::EPC);
     }
 #pragma unroll
     for (int i = 0; i < C::NB; ++i) {
       const int v = min((int)threadIdx.x + C::NTH * i, C::B_CH - 1), row = v / C::CH, ch = v % C::CH;
-      gb[i] = (int64_t)min(bn + row, p.N - 1) * p.ldb + ch * 8;
-      lb[i] = row * C::BK + ((ch ^ (row & (C::CH - 1))) * 8);
+      gb[i] = (int64_t)min(bn + row, p.N - 1) * p.ldb + ch * C::EPC;
+      lb[i] = row * C::BK + ((ch ^ (row & (C::CH - 1))) * C::EPC);
+    }
+    if constexpr (C::MX) {
+      const int t = (int)threadIdx.x;
+      gsa = (int64_t)min(bm + min(t, BM - 1), p.M - 1) * (p.lda / 32);
+      gsb = (int64_t)min(bn + min(t, NBN - 1), p.N - 1) * (p.ldb / 32);
     }
   }
 };
 
-template <int BM>
+template <int BM, typename T = bf16_t>
 struct NtStage {
-  using C = NtCfg<BM>;
+  using C = NtCfg<BM, T>;
   uint4 a[C::NA], b[C::NB];
-  static __device__ __forceinline__ uint4 edge(const bf16_t *src, int k, int kend) {
-    bf16_t tmp[8];
+  uint32_t sa, sb;
+  static __device__ __forceinline__ uint4 edge(const T *src, int k, int kend) {
+    T tmp[C::EPC];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) tmp[e] = k + e < kend ? src[e] : (bf16_t)0;
+    for (int e = 0; e < C::EPC; ++e) tmp[e] = k + e < kend ? src[e] : (T)0;
     return *reinterpret_cast<const uint4 *>(tmp);
   }
-  __device__ __forceinline__ void load(const NtPlan<BM> &pl, const bf16_t *A, const bf16_t *B,
-                                       int k0, int kend) {
+  __device__ __forceinline__ void load(const NtPlan<BM, T> &pl, const T *A, const T *B,
+                                       const GemmParams &p, int k0, int kend) {
+    if constexpr (C::MX) {  // K % 128 == 0 on this path: whole K-tiles, whole scale words
+      if ((int)threadIdx.x < BM) sa = *reinterpret_cast<const uint32_t *>(p.sa + pl.gsa + k0 / 32);
+      if ((int)threadIdx.x < NBN) sb = *reinterpret_cast<const uint32_t *>(p.sb + pl.gsb + k0 / 32);
+    }
     if (k0 + C::BK <= kend) {  // whole K-tile inside [.., kend): plain 16-B loads
 #pragma unroll
       for (int i = 0; i < C::NA; ++i) a[i] = *reinterpret_cast<const uint4 *>(A + pl.ga[i] + k0);
@@ -340,18 +360,18 @@ struct NtStage {
     }
 #pragma unroll
     for (int i = 0; i < C::NA; ++i) {
-      const int kc = k0 + (int)((threadIdx.x + C::NTH * i) % C::CH) * 8;
-      a[i] = kc + 8 <= kend ? *reinterpret_cast<const uint4 *>(A + pl.ga[i] + k0)
-                            : edge(A + pl.ga[i] + k0, kc, kend);
+      const int kc = k0 + (int)((threadIdx.x + C::NTH * i) % C::CH) * C::EPC;
+      a[i] = kc + C::EPC <= kend ? *reinterpret_cast<const uint4 *>(A + pl.ga[i] + k0)
+                                 : edge(A + pl.ga[i] + k0, kc, kend);
     }
 #pragma unroll
     for (int i = 0; i < C::NB; ++i) {
-      const int kc = k0 + (int)((threadIdx.x + C::NTH * i) % C::CH) * 8;
-      b[i] = kc + 8 <= kend ? *reinterpret_cast<const uint4 *>(B + pl.gb[i] + k0)
-                            : edge(B + pl.gb[i] + k0, kc, kend);
+      const int kc = k0 + (int)((threadIdx.x + C::NTH * i) % C::CH) * C::EPC;
+      b[i] = kc + C::EPC <= kend ? *reinterpret_cast<const uint4 *>(B + pl.gb[i] + k0)
+                                 : edge(B + pl.gb[i] + k0, kc, kend);
     }
   }
-  __device__ __forceinline__ void store(const NtPlan<BM> &pl, bf16_t *As, bf16_t *Bs) const {
+  __device__ __forceinline__ void store(const NtPlan<BM, T> &pl, T *As, T *Bs, uint32_t *Ss) const {
 #pragma unroll
     for (int i = 0; i < C::NA; ++i)
       if (C::A_CH % C::NTH == 0 || (int)threadIdx.x + C::NTH * i < C::A_CH)
@@ -360,8 +380,27 @@ struct NtStage {
     for (int i = 0; i < C::NB; ++i)
       if (C::B_CH % C::NTH == 0 || (int)threadIdx.x + C::NTH * i < C::B_CH)
         *reinterpret_cast<uint4 *>(Bs + pl.lb[i]) = b[i];
+    if constexpr (C::MX) {
+      if ((int)threadIdx.x < BM) Ss[threadIdx.x] = sa;
+      if ((int)threadIdx.x < NBN) Ss[BM + threadIdx.x] = sb;
+    }
   }
 };
+
+// MX-FP8 fragment of the 32x32x64 block-scaled MFMA.  The instruction's K order (probed on
+// gfx950, tools/debug/mx8_probe.py): lane half h holds k 16h .. 16h+15 in its low 16 bytes and
+// 32+16h .. 32+16h+15 in its high 16 bytes, and lane half h's scale byte covers k 32h .. 32h+31.
+// So for scale block b = 2kk + h of the K-tile, lane half g loads 16-B chunks 4kk + g (low) and
+// 4kk + 2 + g (high): chunks {4kk, 4kk+1} form block 2kk, {4kk+2, 4kk+3} block 2kk + 1.
+typedef __attribute__((ext_vector_type(4))) int nt_i32x4_t;
+typedef __attribute__((ext_vector_type(8))) int nt_i32x8_t;
+__device__ __forceinline__ nt_i32x8_t nt_frag8(const uint8_t *S, int row, int c0) {
+  constexpr int BKB = 128, CH = 8;
+  const nt_i32x4_t lo = *reinterpret_cast<const nt_i32x4_t *>(S + row * BKB + ((c0 ^ (row & (CH - 1))) * 16));
+  const nt_i32x4_t hi =
+      *reinterpret_cast<const nt_i32x4_t *>(S + row * BKB + (((c0 + 2) ^ (row & (CH - 1))) * 16));
+  return nt_i32x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
 
 template <int BK>
 __device__ __forceinline__ bf16x8_t nt_frag(const bf16_t *S, int row, int c) {
@@ -382,11 +421,11 @@ __device__ __forceinline__ float bce_dz(float z, uint32_t ybit, float scale, flo
 // One output tile of one problem: block `bid` of the problem's `nblk` tile blocks, K split
 // `split`; the LDS arrays come from the launching kernel (so two problems sharing a launch do
 // not double the LDS).
-template <int EPI, int BM>
+template <int EPI, int BM, typename T = bf16_t>
 __device__ __forceinline__ void nt_body(const GemmParams &p, int tiles_m, int bid, int nblk,
                                         int split, char *smem, uint32_t (*ys)[NBN / 32],
                                         double *red, int &lastflag) {
-  using C = NtCfg<BM>;
+  using C = NtCfg<BM, T>;
   constexpr bool kBceRegs = BM <= 128;  // BCE math on the accumulators (no register pressure)
   constexpr int BK = C::BK, NTH = C::NTH;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
@@ -429,10 +468,11 @@ __device__ __forceinline__ void nt_body(const GemmParams &p, int tiles_m, int bi
       ys[r][w] = gm < p.M && gw < YW ? p.y_bits[(int64_t)gm * YW + gw] : 0u;
     }
   }
-  bf16_t *AsBase = reinterpret_cast<bf16_t *>(smem);
-  bf16_t *BsBase = AsBase + 2 * BM * BK;
-  const bf16_t *__restrict__ A = reinterpret_cast<const bf16_t *>(p.A);
-  const bf16_t *__restrict__ B = reinterpret_cast<const bf16_t *>(p.B);
+  T *AsBase = reinterpret_cast<T *>(smem);
+  T *BsBase = AsBase + 2 * BM * BK;
+  uint32_t *SsBase = reinterpret_cast<uint32_t *>(smem + 2 * C::STAGE);  // MX: [2][BM + NBN]
+  const T *__restrict__ A = reinterpret_cast<const T *>(p.A);
+  const T *__restrict__ B = reinterpret_cast<const T *>(p.B);
   f32x16_t acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -440,18 +480,18 @@ __device__ __forceinline__ void nt_body(const GemmParams &p, int tiles_m, int bi
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  const bool do_cs = p.colsum != nullptr && bm == 0 && threadIdx.x < NBN;
+  const bool do_cs = !C::MX && p.colsum != nullptr && bm == 0 && threadIdx.x < NBN;
   float cs = 0.f;
   // D-deep register ring: K-tiles t+1 .. t+D-1 are in flight while tile t's MFMAs run; LDS is
   // double-buffered: tile t lives in buffer t & 1.
   constexpr int D = NT_RING;
-  const NtPlan<BM> pl(p, bm, bn);
-  NtStage<BM> st[D];
+  const NtPlan<BM, T> pl(p, bm, bn);
+  NtStage<BM, T> st[D];
   const int nk = kbeg < kend ? (int)cdiv(kend - kbeg, BK) : 0;
 #pragma unroll
   for (int q = 0; q < D; ++q)
-    if (q < nk) st[q].load(pl, A, B, kbeg + q * BK, kend);
-  if (nk > 0) st[0].store(pl, AsBase, BsBase);
+    if (q < nk) st[q].load(pl, A, B, p, kbeg + q * BK, kend);
+  if (nk > 0) st[0].store(pl, AsBase, BsBase, SsBase);
   __syncthreads();
   const int ar = wm * 64 + (lane & 31), br = wn * 64 + (lane & 31);
   for (int t0 = 0; t0 < nk; t0 += D) {
@@ -459,30 +499,50 @@ __device__ __forceinline__ void nt_body(const GemmParams &p, int tiles_m, int bi
     for (int q = 0; q < D; ++q) {
       const int t = t0 + q;
       if (t >= nk) break;
-      const bf16_t *as = AsBase + (t & 1) * BM * BK, *bs = BsBase + (t & 1) * NBN * BK;
+      const T *as = AsBase + (t & 1) * BM * BK, *bs = BsBase + (t & 1) * NBN * BK;
+      if constexpr (C::MX) {
+        const uint32_t *ss = SsBase + (t & 1) * (BM + NBN);
+        const uint32_t wa0 = ss[ar], wa1 = ss[ar + 32], wb0 = ss[BM + br], wb1 = ss[BM + br + 32];
 #pragma unroll
-      for (int kk = 0; kk < BK / 16; ++kk) {
-        const int c = 2 * kk + half;
-        const bf16x8_t a0 = nt_frag<BK>(as, ar, c), a1 = nt_frag<BK>(as, ar + 32, c);
-        const bf16x8_t b0 = nt_frag<BK>(bs, br, c), b1 = nt_frag<BK>(bs, br + 32, c);
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
-      }
-      if (do_cs) {  // bias gradient: sum of B row n over k, ascending k
-        const int n = threadIdx.x;
+        for (int kk = 0; kk < BK / 64; ++kk) {
+          const int c0 = 4 * kk + half, sh = 8 * (2 * kk + half);
+          const uint8_t *as8 = reinterpret_cast<const uint8_t *>(as);
+          const uint8_t *bs8 = reinterpret_cast<const uint8_t *>(bs);
+          const nt_i32x8_t a0 = nt_frag8(as8, ar, c0), a1 = nt_frag8(as8, ar + 32, c0);
+          const nt_i32x8_t b0 = nt_frag8(bs8, br, c0), b1 = nt_frag8(bs8, br + 32, c0);
+          const int sa0 = (int)((wa0 >> sh) & 0xFFu), sa1 = (int)((wa1 >> sh) & 0xFFu);
+          const int sb0 = (int)((wb0 >> sh) & 0xFFu), sb1 = (int)((wb1 >> sh) & 0xFFu);
+          acc[0][0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a0, b0, acc[0][0], 0, 0, 0, sa0, 0, sb0);
+          acc[0][1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a0, b1, acc[0][1], 0, 0, 0, sa0, 0, sb1);
+          acc[1][0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a1, b0, acc[1][0], 0, 0, 0, sa1, 0, sb0);
+          acc[1][1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a1, b1, acc[1][1], 0, 0, 0, sa1, 0, sb1);
+        }
+      } else {
 #pragma unroll
-        for (int c = 0; c < BK / 8; ++c) {
-          const bf16_t *qq = bs + n * BK + ((c ^ (n & (BK / 8 - 1))) * 8);
+        for (int kk = 0; kk < BK / 16; ++kk) {
+          const int c = 2 * kk + half;
+          const bf16x8_t a0 = nt_frag<BK>(as, ar, c), a1 = nt_frag<BK>(as, ar + 32, c);
+          const bf16x8_t b0 = nt_frag<BK>(bs, br, c), b1 = nt_frag<BK>(bs, br + 32, c);
+          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+        }
+        if (do_cs) {  // bias gradient: sum of B row n over k, ascending k
+          const int n = threadIdx.x;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) cs += bf2f(qq[e]);
+          for (int c = 0; c < BK / 8; ++c) {
+            const bf16_t *qq = reinterpret_cast<const bf16_t *>(bs) + n * BK + ((c ^ (n & (BK / 8 - 1))) * 8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cs += bf2f(qq[e]);
+          }
         }
       }
       // slot q held tile t (already in LDS); refill it with tile t + D, publish tile t + 1
-      if (t + D < nk) st[q].load(pl, A, B, kbeg + (t + D) * BK, kend);
+      if (t + D < nk) st[q].load(pl, A, B, p, kbeg + (t + D) * BK, kend);
       if (t + 1 < nk)
-        st[(q + 1) % D].store(pl, AsBase + ((t + 1) & 1) * BM * BK, BsBase + ((t + 1) & 1) * NBN * BK);
+        st[(q + 1) % D].store(pl, AsBase + ((t + 1) & 1) * BM * BK, BsBase + ((t + 1) & 1) * NBN * BK,
+                              SsBase + ((t + 1) & 1) * (BM + NBN));
       __syncthreads();
     }
   }
@@ -627,25 +687,44 @@ __global__ __launch_bounds__(NtCfg<BM>::NTH) void gemm_nt_bf16_kernel(GemmParams
   nt_body<EPI, BM>(p, tiles_m, blockIdx.x, gridDim.x, blockIdx.y, smem, ys, red, lastflag);
 }
 
+// The same tiles on MX-FP8 operands (128 x 128, K % 128 == 0).
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_nt_mx8_kernel(GemmParams p, int tiles_m) {
+  __shared__ __attribute__((aligned(16))) char smem[NtCfg<128, uint8_t>::LDS];
+  __shared__ uint32_t ys[EPI == CC_EPI_BCE ? 128 : 1][NBN / 32];
+  __shared__ double red[NtCfg<128, uint8_t>::NTH / 64];
+  __shared__ int lastflag;
+  nt_body<EPI, 128, uint8_t>(p, tiles_m, blockIdx.x, gridDim.x, blockIdx.y, smem, ys, red, lastflag);
+}
+
 // Two independent NT problems in one launch (grouped GEMM): blocks [0, nb0*s0) are problem 0's
 // (tile, split) pairs, the rest problem 1's — the decoder's dX (split-K) and dW products fill
 // the chip together instead of one after the other.
-template <int E0, int E1>
-__global__ __launch_bounds__(NtCfg<128>::NTH) void gemm_nt_pair_kernel(GemmParams p0, int tm0, int nb0,
-                                                                       int s0, GemmParams p1, int tm1,
-                                                                       int nb1) {
+template <int E0, int E1, typename T = bf16_t>
+__global__ __launch_bounds__(256) void gemm_nt_pair_kernel(GemmParams p0, int tm0, int nb0,
+                                                                          int s0, GemmParams p1, int tm1,
+                                                                          int nb1) {
   static_assert(E0 != CC_EPI_BCE && E1 != CC_EPI_BCE, "pair: no loss hand-off");
-  __shared__ __attribute__((aligned(16))) char smem[NtCfg<128>::LDS];
+  __shared__ __attribute__((aligned(16))) char smem[NtCfg<128, T>::LDS];
   __shared__ uint32_t ys[1][NBN / 32];
-  __shared__ double red[NtCfg<128>::NTH / 64];
+  __shared__ double red[NtCfg<128, T>::NTH / 64];
   __shared__ int lastflag;
   const int b = blockIdx.x;
   if (b < nb0 * s0) {
-    nt_body<E0, 128>(p0, tm0, b % nb0, nb0, b / nb0, smem, ys, red, lastflag);
+    nt_body<E0, 128, T>(p0, tm0, b % nb0, nb0, b / nb0, smem, ys, red, lastflag);
   } else {
     const int c = b - nb0 * s0;
-    nt_body<E1, 128>(p1, tm1, c % nb1, nb1, c / nb1, smem, ys, red, lastflag);
+    nt_body<E1, 128, T>(p1, tm1, c % nb1, nb1, c / nb1, smem, ys, red, lastflag);
   }
+}
+
+template <int EPI>
+int launch_nt_mx8(const cc_gemm_args *g, const GemmParams &p, hipStream_t s) {
+  const int tm = (int)cdiv(g->M, 128), tn = (int)cdiv(g->N, NBN);
+  const dim3 grid((unsigned)(tm * tn), EPI == CC_EPI_SPLITK ? (unsigned)g->splits : 1u);
+  hipLaunchKernelGGL((gemm_nt_mx8_kernel<EPI>), grid, dim3(NtCfg<128, uint8_t>::NTH), 0, s, p, tm);
+  CC_LAUNCH_CHECK("gemm_nt_mx8_kernel");
+  return CC_OK;
 }
 
 template <int EPI, int BM>
@@ -823,12 +902,21 @@ extern "C" int cc_gemm_grid(int32_t M, int32_t N, int32_t *tiles) {
 static int gemm_params(const cc_gemm_args *g, GemmParams &p) {
   CC_REQUIRE(g && g->A && g->B, "cc_gemm: null operand");
   CC_REQUIRE(g->M >= 0 && g->N >= 0 && g->K >= 0, "cc_gemm: negative size");
-  CC_REQUIRE(g->dtype == CC_BF16 || g->dtype == CC_F32, "cc_gemm: dtype");
+  CC_REQUIRE(g->dtype == CC_BF16 || g->dtype == CC_F32 || g->dtype == CC_MX8, "cc_gemm: dtype");
+  if (g->dtype == CC_MX8) {
+    CC_REQUIRE(!g->ta && g->tb, "cc_gemm: MX8 is NT only (ta = 0, tb = 1)");
+    CC_REQUIRE(g->K % 128 == 0 && g->lda % 128 == 0 && g->ldb % 128 == 0,
+               "cc_gemm: MX8 needs K, lda, ldb multiples of 128");
+    CC_REQUIRE(g->a_scale && g->b_scale && ((uintptr_t)g->a_scale | (uintptr_t)g->b_scale) % 4 == 0,
+               "cc_gemm: MX8 needs 4-byte aligned a_scale / b_scale");
+    CC_REQUIRE(((uintptr_t)g->A | (uintptr_t)g->B) % 16 == 0, "cc_gemm: MX8 operands 16-byte aligned");
+    CC_REQUIRE(g->epilogue != CC_EPI_MASK && !g->colsum, "cc_gemm: MX8 epilogues STORE/BCE/SPLITK, no colsum");
+  }
   if (g->epilogue == CC_EPI_SPLITK) CC_REQUIRE(g->splits >= 1 && g->Cf, "cc_gemm: split-K needs Cf, splits>=1");
   if (g->epilogue == CC_EPI_BCE)
     CC_REQUIRE(g->bias && g->y_bits && g->loss_partials, "cc_gemm: BCE needs bias, y_bits, loss_partials");
   if (g->epilogue == CC_EPI_MASK) CC_REQUIRE(g->H, "cc_gemm: MASK needs H");
-  const int vw = g->dtype == CC_BF16 ? 8 : 4;
+  const int vw = g->dtype == CC_MX8 ? 16 : g->dtype == CC_BF16 ? 8 : 4;
   p.M = g->M; p.N = g->N; p.K = g->K;
   p.lda = g->lda; p.ldb = g->ldb; p.ldc = g->ldc;
   p.splits = g->splits; p.relu = g->relu;
@@ -842,6 +930,8 @@ static int gemm_params(const cc_gemm_args *g, GemmParams &p) {
   p.loss_out = g->epilogue == CC_EPI_BCE ? g->loss_out : nullptr;
   p.loss_scale = g->loss_scale;
   p.ticket = g->ticket;
+  p.sa = g->a_scale;
+  p.sb = g->b_scale;
   CC_REQUIRE(!p.loss_out || p.ticket, "cc_gemm: loss_out needs a ticket word");
   CC_REQUIRE(!g->Ct || g->epilogue == CC_EPI_BCE, "cc_gemm: Ct only with the BCE epilogue");
   return CC_OK;
@@ -862,6 +952,14 @@ extern "C" int cc_gemm(const cc_gemm_args *g, void *stream) {
   if (int rc = gemm_params(g, p)) return rc;
   if (g->M == 0 || g->N == 0) return CC_OK;
   hipStream_t s = as_stream(stream);
+  if (g->dtype == CC_MX8) {
+    switch (g->epilogue) {
+      case CC_EPI_STORE: return launch_nt_mx8<CC_EPI_STORE>(g, p, s);
+      case CC_EPI_BCE: return launch_nt_mx8<CC_EPI_BCE>(g, p, s);
+      case CC_EPI_SPLITK: return launch_nt_mx8<CC_EPI_SPLITK>(g, p, s);
+    }
+    return cc::fail(CC_ERR_ARG, "cc_gemm: MX8 epilogue");
+  }
   if (nt_path(g, p)) {
     switch (g->epilogue) {
       case CC_EPI_STORE: return launch_nt<CC_EPI_STORE>(g, p, s);
@@ -883,10 +981,10 @@ extern "C" int cc_gemm_pair(const cc_gemm_args *g0, const cc_gemm_args *g1, void
   if (int rc = gemm_params(g0, p0)) return rc;
   if (int rc = gemm_params(g1, p1)) return rc;
   auto pairable = [](const cc_gemm_args *g, const GemmParams &p) {
-    return nt_path(g, p) && g->M > 0 && g->N > 0 &&
+    return (nt_path(g, p) || g->dtype == CC_MX8) && g->M > 0 && g->N > 0 &&
            (g->epilogue == CC_EPI_STORE || g->epilogue == CC_EPI_SPLITK);
   };
-  if (!pairable(g0, p0) || !pairable(g1, p1)) {  // one after the other
+  if (!pairable(g0, p0) || !pairable(g1, p1) || (g0->dtype == CC_MX8) != (g1->dtype == CC_MX8)) {
     if (int rc = cc_gemm(g0, stream)) return rc;
     return cc_gemm(g1, stream);
   }
@@ -896,7 +994,13 @@ extern "C" int cc_gemm_pair(const cc_gemm_args *g0, const cc_gemm_args *g1, void
   const int s1 = g1->epilogue == CC_EPI_SPLITK ? g1->splits : 1;
   const dim3 grid((unsigned)(nb0 * s0 + nb1 * s1)), block(NtCfg<128>::NTH);
   hipStream_t s = as_stream(stream);
-#define PAIR(E0, E1) hipLaunchKernelGGL((gemm_nt_pair_kernel<E0, E1>), grid, block, 0, s, p0, tm0, nb0, s0, p1, tm1, nb1)
+#define PAIR(E0, E1)                                                                                     \
+  do {                                                                                                   \
+    if (g0->dtype == CC_MX8)                                                                             \
+      hipLaunchKernelGGL((gemm_nt_pair_kernel<E0, E1, uint8_t>), grid, block, 0, s, p0, tm0, nb0, s0, p1, tm1, nb1); \
+    else                                                                                                 \
+      hipLaunchKernelGGL((gemm_nt_pair_kernel<E0, E1>), grid, block, 0, s, p0, tm0, nb0, s0, p1, tm1, nb1); \
+  } while (0)
   if (g0->epilogue == CC_EPI_SPLITK && g1->epilogue == CC_EPI_STORE) PAIR(CC_EPI_SPLITK, CC_EPI_STORE);
   else if (g0->epilogue == CC_EPI_STORE && g1->epilogue == CC_EPI_SPLITK) PAIR(CC_EPI_STORE, CC_EPI_SPLITK);
   else if (g0->epilogue == CC_EPI_STORE) PAIR(CC_EPI_STORE, CC_EPI_STORE);

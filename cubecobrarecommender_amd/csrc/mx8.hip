@@ -1,0 +1,152 @@
+// MX-FP8 quantisation of GEMM operands (config 5, SURVEY §8(d): the decoder output layer and the
+// regulariser GEMM of model.py:64,94,98 on v_mfma_scale_f32_32x32x64_f8f6f4).  One E8M0 scale per
+// 32 elements along the GEMM's K axis; the rule is restated in oracle/mx8_ref.py (bit-exact):
+//   e = min{e : amax <= 448 * 2^e} (= x - 9 + (m > 0.875) for amax = m 2^x), e in [-127, 127];
+//   code = OCP e4m3fn round-to-nearest-even of v * 2^-e (v_cvt_pk_fp8_f32); never saturates.
+// Row blocks: one lane per 32-element block (two 16-B stores per lane).  Transposed blocks: a
+// workgroup stages a [32 rows][256 cols] tile in LDS and each lane emits one output row's block.
+#include "common.hpp"
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ float ldf(const T *p, int64_t i) { return DT<T>::ld(p + i); }
+
+__device__ __forceinline__ int block_exp(float amax) {
+  if (!(amax > 0.f)) return 0;
+  int x;
+  const float m = frexpf(amax, &x);
+  int e = x - 9 + (m > 0.875f ? 1 : 0);
+  return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+
+// 32 values -> 32 e4m3 codes (little-endian bytes in w[8]) at scale 2^-e
+__device__ __forceinline__ void encode32(const float *v, int e, uint32_t *w) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    int word = 0;
+    word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4 * q], -e), ldexpf(v[4 * q + 1], -e), word, false);
+    word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4 * q + 2], -e), ldexpf(v[4 * q + 3], -e), word, true);
+    w[q] = (uint32_t)word;
+  }
+}
+
+// grid (ceil(nb / 64), rows), block 64: lane -> block j of row r; with rowsum (gridDim.x == 1) the
+// wave also sums the row (per-lane ascending partials, then a fixed xor tree: deterministic).
+template <typename T>
+__global__ __launch_bounds__(64) void quant_rows_kernel(const T *__restrict__ src, int cols, int ld_src,
+                                                        uint8_t *__restrict__ dst, int ld_dst,
+                                                        uint8_t *__restrict__ scales,
+                                                        float *__restrict__ rowsum) {
+  const int r = blockIdx.y, nb = ld_dst / 32;
+  const T *row = src + (int64_t)r * ld_src;
+  float part = 0.f;
+  for (int j = blockIdx.x * 64 + threadIdx.x; j < nb; j += gridDim.x * 64) {
+    float v[32];
+    const int c0 = 32 * j;
+    if (c0 + 32 <= cols && sizeof(T) == 2 && (ld_src % 8) == 0 && ((uintptr_t)src % 16) == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 u = *reinterpret_cast<const uint4 *>(row + c0 + 8 * q);
+        const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[8 * q + 2 * e] = __uint_as_float(uw[e] << 16);
+          v[8 * q + 2 * e + 1] = __uint_as_float(uw[e] & 0xFFFF0000u);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 32; ++e) v[e] = c0 + e < cols ? ldf(row, c0 + e) : 0.f;
+    }
+    float amax = 0.f;
+#pragma unroll
+    for (int e = 0; e < 32; ++e) {
+      amax = fmaxf(amax, fabsf(v[e]));
+      part += v[e];
+    }
+    const int ex = block_exp(amax);
+    uint32_t w[8];
+    encode32(v, ex, w);
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst + (int64_t)r * ld_dst + c0);
+    d4[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    d4[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    scales[(int64_t)r * nb + j] = (uint8_t)(ex + 127);
+  }
+  if (rowsum) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) part += __shfl_xor(part, off);
+    if (threadIdx.x == 0) rowsum[r] = part;
+  }
+}
+
+// Transposed: dst[c][r] = q(src[r][c]); K axis = r.  grid (ceil(cols / 256), ld_dst / 32), block
+// 256: tile rows [32 by, 32 by + 32), cols [256 bx, +256); lane c emits dst row (256 bx + c)'s block by.
+constexpr int QT_C = 256;
+template <typename T>
+__global__ __launch_bounds__(QT_C) void quant_t_kernel(const T *__restrict__ src, int rows, int cols,
+                                                       int ld_src, uint8_t *__restrict__ dst, int ld_dst,
+                                                       uint8_t *__restrict__ scales) {
+  __shared__ float tile[32][QT_C + 1];
+  const int c0 = blockIdx.x * QT_C, r0 = blockIdx.y * 32;
+  for (int i = threadIdx.x; i < 32 * QT_C; i += QT_C) {
+    const int rr = i / QT_C, cc = i % QT_C;
+    const int gr = r0 + rr, gc = c0 + cc;
+    tile[rr][cc] = gr < rows && gc < cols ? ldf(src, (int64_t)gr * ld_src + gc) : 0.f;
+  }
+  __syncthreads();
+  const int c = c0 + threadIdx.x;
+  if (c >= cols) return;
+  float v[32];
+  float amax = 0.f;
+#pragma unroll
+  for (int e = 0; e < 32; ++e) {
+    v[e] = tile[e][threadIdx.x];
+    amax = fmaxf(amax, fabsf(v[e]));
+  }
+  const int ex = block_exp(amax);
+  uint32_t w[8];
+  encode32(v, ex, w);
+  uint4 *d4 = reinterpret_cast<uint4 *>(dst + (int64_t)c * ld_dst + r0);
+  d4[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  d4[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  scales[(int64_t)c * (ld_dst / 32) + blockIdx.y] = (uint8_t)(ex + 127);
+}
+
+}  // namespace
+
+extern "C" int cc_quant_mx8(int32_t dtype, const void *src, int32_t rows, int32_t cols, int32_t ld_src,
+                            int32_t transpose, uint8_t *dst, int32_t ld_dst, uint8_t *scales,
+                            float *rowsum, void *stream) {
+  CC_REQUIRE(src && dst && scales, "cc_quant_mx8: null pointer");
+  CC_REQUIRE(dtype == CC_BF16 || dtype == CC_F32, "cc_quant_mx8: dtype");
+  CC_REQUIRE(rows >= 0 && cols >= 0 && ld_src >= cols, "cc_quant_mx8: shape");
+  CC_REQUIRE(ld_dst % 128 == 0 && (uintptr_t)dst % 16 == 0, "cc_quant_mx8: ld_dst % 128, dst 16-B aligned");
+  if (rows == 0 || cols == 0) return CC_OK;
+  hipStream_t s = as_stream(stream);
+  if (!transpose) {
+    CC_REQUIRE(ld_dst >= cols, "cc_quant_mx8: ld_dst < cols");
+    const int nb = ld_dst / 32;
+    CC_REQUIRE(!rowsum || nb <= 64, "cc_quant_mx8: rowsum needs ld_dst <= 2048");
+    const dim3 grid(rowsum ? 1u : (unsigned)cdiv(nb, 64), (unsigned)rows);
+    if (dtype == CC_BF16)
+      hipLaunchKernelGGL(quant_rows_kernel<bf16_t>, grid, dim3(64), 0, s, (const bf16_t *)src, cols, ld_src,
+                         dst, ld_dst, scales, rowsum);
+    else
+      hipLaunchKernelGGL(quant_rows_kernel<float>, grid, dim3(64), 0, s, (const float *)src, cols, ld_src,
+                         dst, ld_dst, scales, rowsum);
+    CC_LAUNCH_CHECK("quant_rows_kernel");
+    return CC_OK;
+  }
+  CC_REQUIRE(!rowsum, "cc_quant_mx8: rowsum only without transpose");
+  CC_REQUIRE(ld_dst >= rows, "cc_quant_mx8: ld_dst < rows");
+  const dim3 grid((unsigned)cdiv(cols, QT_C), (unsigned)(ld_dst / 32));
+  if (dtype == CC_BF16)
+    hipLaunchKernelGGL(quant_t_kernel<bf16_t>, grid, dim3(QT_C), 0, s, (const bf16_t *)src, rows, cols, ld_src,
+                       dst, ld_dst, scales);
+  else
+    hipLaunchKernelGGL(quant_t_kernel<float>, grid, dim3(QT_C), 0, s, (const float *)src, rows, cols, ld_src,
+                       dst, ld_dst, scales);
+  CC_LAUNCH_CHECK("quant_t_kernel");
+  return CC_OK;
+}

@@ -228,7 +228,7 @@ __global__ __launch_bounds__(NT) void tower_fwd_kernel(TowerP p) {
 template <typename T>
 __global__ __launch_bounds__(NT) void tower_bwd_chain_kernel(TowerP p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int MAXT = 4;  // dX tiles per wave (K <= 512)
+  constexpr int MAXT = 8;  // dX tiles per wave (K <= 1024)
   const int ldx = p.maxw + 16 / (int)sizeof(T);
   T *Gr = reinterpret_cast<T *>(smem);
   T *Hr = Gr + RB * ldx;
@@ -618,7 +618,7 @@ __global__ __launch_bounds__(256) void tower_transpose_kernel(TowerP p, int64_t 
 int make_params(const cc_tower_args *t, TowerP &p) {
   if (!t) return cc::fail(CC_ERR_ARG, "cc_tower: null args");
   if (t->dtype != CC_BF16 && t->dtype != CC_F32) return cc::fail(CC_ERR_ARG, "cc_tower: dtype");
-  const int maxd = t->dtype == CC_BF16 ? 512 : 256;
+  const int maxd = t->dtype == CC_BF16 ? 1024 : 256;
   if (t->d < 64 || t->d > maxd || t->d % 64) return cc::fail(CC_ERR_UNSUPPORTED, "cc_tower: d out of range for the fused towers");
   if (t->B % RB || t->R % RB || t->R < t->B || t->B <= 0) return cc::fail(CC_ERR_ARG, "cc_tower: B and R must be multiples of 32");
   p.d = t->d;

@@ -31,7 +31,8 @@ class TrainConfig:
     beta1: float = 0.9
     beta2: float = 0.999
     eps: float = 1e-7
-    dtype: str = 'bf16'            # GEMM operand dtype: 'bf16' (MFMA bf16) or 'fp32' (exact f32 MFMA)
+    dtype: str = 'bf16'            # GEMM operand dtype: 'bf16' (MFMA bf16), 'fp32' (exact f32 MFMA) or
+    #                                'fp8' (bf16 + MX-FP8 decoder output / regulariser GEMMs, config 5)
     seed: int = 0
     rank: int = 0
     world: int = 1
@@ -106,8 +107,13 @@ class Trainer:
         if self.use_reg and data.y_reg is None:
             raise ValueError('reg > 0 needs the M~ matrix on the device')
         self.R = 2 * B if self.use_reg else B
-        self.dtype = L.CC_BF16 if cfg.dtype == 'bf16' else L.CC_F32
-        self.tdt = torch.bfloat16 if cfg.dtype == 'bf16' else torch.float32
+        if cfg.dtype not in ('bf16', 'fp32', 'fp8'):
+            raise ValueError(f'dtype {cfg.dtype!r}: bf16, fp32 or fp8')
+        self.mx8 = cfg.dtype == 'fp8'
+        self.dtype = L.CC_F32 if cfg.dtype == 'fp32' else L.CC_BF16
+        self.tdt = torch.float32 if cfg.dtype == 'fp32' else torch.bfloat16
+        if self.mx8 and (d % 128 or self.R % 128 or B % 32):
+            raise ValueError('fp8 (MX) decoder GEMMs need d and the row count (B, 2B with reg) multiples of 128')
         P = self.layout.total
         f32 = dict(device=self.dev, dtype=torch.float32)
         self.params = torch.zeros(P, **f32)
@@ -155,7 +161,9 @@ class Trainer:
         self.kl_part = torch.zeros(B, device=self.dev, dtype=torch.float64)
         self.loss_dev = torch.zeros(2, device=self.dev, dtype=torch.float64)
         # fused 32-row-block towers (tower.hip) when the widths fit; generic GEMMs otherwise
-        self.fused_tower = cfg.fused_tower and (B % 32 == 0) and d <= (512 if self.dtype == L.CC_BF16 else 256)
+        self.fused_tower = cfg.fused_tower and (B % 32 == 0) and d <= (1024 if self.dtype == L.CC_BF16 else 256)
+        if self.mx8 and not self.fused_tower:
+            raise ValueError('fp8 needs the fused towers (fused_tower=True, B % 32 == 0)')
         if self.fused_tower:
             self.tower_layers = ('encoder/encoded_2', 'encoder/encoded_3', 'encoder/bottleneck',
                                  'decoder/decoded_1', 'decoder/decoded_2', 'decoder/decoded_3',
@@ -170,6 +178,21 @@ class Trainer:
             self.D3t = torch.zeros(d, R, **T)
             self.dZt = torch.zeros(len(branches_of(self.use_reg)), V, B, **T)   # [branch][V][B]
             self.WoT = torch.zeros(len(branches_of(self.use_reg)), V, d, **T)
+            if self.mx8:   # MX-FP8 operand images of the decoder output layers (csrc/mx8.hip)
+                nbr, u8 = len(branches_of(self.use_reg)), dict(device=self.dev, dtype=torch.uint8)
+                self.Vp = (V + 127) // 128 * 128
+                self.WoT8 = torch.zeros(nbr, V, d, **u8)                  # fwd B operand [V][d]
+                self.WoT8s = torch.zeros(nbr, V, d // 32, **u8)
+                self.Wo8 = torch.zeros(nbr, d, self.Vp, **u8)             # dX B operand [d][Vp]
+                self.Wo8s = torch.zeros(nbr, d, self.Vp // 32, **u8)
+                self.D3q = torch.zeros(R, d, **u8)                        # fwd A operand
+                self.D3qs = torch.zeros(R, d // 32, **u8)
+                self.D3tq = torch.zeros(d, R, **u8)                       # dW A operand (K = rows)
+                self.D3tqs = torch.zeros(d, R // 32, **u8)
+                self.dZq = torch.zeros(R, self.Vp, **u8)                  # dX A operand
+                self.dZqs = torch.zeros(R, self.Vp // 32, **u8)
+                self.dZtq = torch.zeros(nbr, V, B, **u8)                  # dW B operand (K = rows)
+                self.dZtqs = torch.zeros(nbr, V, B // 32, **u8)
             self.targs = self._tower_args()
             self.transpose_tower()
         else:
@@ -179,7 +202,7 @@ class Trainer:
         # (measured: in the step the fused kernel ran 77 us against 56 + 8 + 4 + 5 for Adam,
         # Wo^T, tower W^T and the counters — its 64x64 tiles read Wo with poor DRAM locality —
         # so it is opt-in: CCREC_FUSED_ADAM=1)
-        self.fused_adam = (self.fused_tower and cfg.world == 1 and self.dtype == L.CC_BF16
+        self.fused_adam = (self.fused_tower and cfg.world == 1 and self.dtype == L.CC_BF16 and not self.mx8
                            and os.environ.get('CCREC_FUSED_ADAM', '0') == '1')
         self.adam_regions = self._adam_regions() if self.fused_adam else None
         # F for the next step in the Adam launch (cc_adam_noise): Adam is HBM-bound, F latency-
@@ -283,14 +306,26 @@ class Trainer:
             arr[i].off, arr[i].rows, arr[i].cols, arr[i].dst = off, r, c, dst
         return arr
 
+    def refresh_decoder_operands(self, s):
+        """Decoder output-layer operands from the current (bf16 shadow) weights Wo [d][V]: Wo^T
+        (bf16), or with fp8 the MX-FP8 images Wo^T [V][d] (forward) and Wo [d][Vp] (dX)."""
+        d, V = self.cfg.d, self.cfg.V
+        for k, pre in enumerate(branches_of(self.use_reg)):
+            if self.mx8:
+                L.call('cc_quant_mx8', L.CC_BF16, self.w(pre + '/reconstruct/kernel'), d, V, V, 1,
+                       L.ptr(self.WoT8[k]), d, L.ptr(self.WoT8s[k]), None, s)
+                L.call('cc_quant_mx8', L.CC_BF16, self.w(pre + '/reconstruct/kernel'), d, V, V, 0,
+                       L.ptr(self.Wo8[k]), self.Vp, L.ptr(self.Wo8s[k]), None, s)
+            else:
+                L.call('cc_transpose', self.dtype, self.w(pre + '/reconstruct/kernel'), d, V,
+                       L.ptr(self.WoT[k]), s)
+
     def transpose_tower(self, stream=None):
         """Refresh the transposed operand copies (tower W^T, decoder Wo^T) from the current weights."""
         if self.fused_tower:
             s = L.stream_ptr(stream)
             L.call('cc_tower_transpose', L.C.byref(self.targs), s)
-            for k, pre in enumerate(branches_of(self.use_reg)):
-                L.call('cc_transpose', self.dtype, self.w(pre + '/reconstruct/kernel'), self.cfg.d, self.cfg.V,
-                       L.ptr(self.WoT[k]), s)
+            self.refresh_decoder_operands(s)
 
     def refresh_shadow(self):
         """Re-derive the bf16 shadow (and the transposed tower operands) from the fp32 master."""
@@ -332,12 +367,13 @@ class Trainer:
     def _gemm(self, M, N, K, A, lda, B, ldb, ta=0, tb=0, epi=L.CC_EPI_STORE, ldc=None, bias=None,
               relu=0, C=None, Cf=None, H=None, y_bits=None, scale=0.0, partials=None, splits=1,
               colsum=None, Ct=None, ldct=0, stream=None, loss_out=None, loss_scale=0.0, ticket=None,
-              launch=True):
-        g = L.GemmArgs(dtype=self.dtype, ta=ta, tb=tb, epilogue=epi, M=M, N=N, K=K, lda=lda,
-                       ldb=ldb, ldc=ldc if ldc is not None else N, splits=splits, relu=relu,
+              launch=True, dtype=None, a_scale=None, b_scale=None):
+        g = L.GemmArgs(dtype=self.dtype if dtype is None else dtype, ta=ta, tb=tb, epilogue=epi, M=M, N=N,
+                       K=K, lda=lda, ldb=ldb, ldc=ldc if ldc is not None else N, splits=splits, relu=relu,
                        A=A, B=B, bias=bias, C=C, Cf=Cf, H=H, y_bits=y_bits, scale=scale,
                        loss_partials=partials, colsum=colsum, Ct=Ct, ldct=ldct,
-                       loss_out=loss_out, loss_scale=loss_scale, ticket=ticket)
+                       loss_out=loss_out, loss_scale=loss_scale, ticket=ticket,
+                       a_scale=a_scale, b_scale=b_scale)
         if launch:
             L.call('cc_gemm', L.C.byref(g), stream if stream is not None else self._s)
         return g
@@ -411,9 +447,14 @@ class Trainer:
                 self._dense_fwd(self.D1, rows, 128, 256, pre + '/decoded_2', self.D2)
                 self._dense_fwd(self.D2, rows, 256, d, pre + '/decoded_3', self.D3)
         # ---- D1 output + sigmoid + BCE -> dZ (model.py:64,94; train.py:85)
+        if self.mx8:   # MX-FP8 images of D3: rows (forward A) and transposed (dW A, K = rows)
+            L.call('cc_quant_mx8', L.CC_BF16, L.ptr(self.D3), R, d, d, 0, L.ptr(self.D3q), d,
+                   L.ptr(self.D3qs), None, s)
+            L.call('cc_quant_mx8', L.CC_BF16, L.ptr(self.D3), R, d, d, 1, L.ptr(self.D3tq), R,
+                   L.ptr(self.D3tqs), None, s)
         t = self._tick('dec_bce_fwd')
         if self.fused_tower:   # Wo^T [V][d]: k-contiguous B operand; also writes dZ^T [V][B]
-            self._gemm(B, V, d, L.ptr(self.D3), d, L.ptr(self.WoT[0]), d, tb=1,
+            self._gemm(B, V, d, **self._dec_fwd(0, 0), tb=1,
                        epi=L.CC_EPI_BCE, bias=self.pf('decoder/reconstruct/bias'), C=L.ptr(self.dZout),
                        y_bits=L.ptr(self.y_bits), scale=1.0 / (B * V), partials=L.ptr(self.bce_part),
                        Ct=L.ptr(self.dZt[0]), ldct=B, loss_out=L.ptr(self.loss_dev),
@@ -429,7 +470,7 @@ class Trainer:
         # ---- D2 output + softmax + KL vs M~ rows (model.py:98; train.py:85)
         if self.use_reg:
             if self.fused_tower:
-                self._gemm(B, V, d, L.ptr(self.D3[B:]), d, L.ptr(self.WoT[1]), d, tb=1,
+                self._gemm(B, V, d, **self._dec_fwd(1, B), tb=1,
                            bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2))
             else:
                 self._gemm(B, V, d, L.ptr(self.D3[B:]), d, self.w('decoder_for_reg/reconstruct/kernel'), V,
@@ -446,27 +487,34 @@ class Trainer:
         # (side stream) and dX -> towers (this stream) only share read-only inputs.
         for k, (pre, (r0, r1)) in enumerate(branches):
             dz = self.dZout[r0:]
-            if self.fused_tower and not self.timing and not self.overlap:
-                # dX (split-K) and dW = D3^T dZ (+ dbo) in one grouped launch
-                gx = self._gemm(B, d, V, L.ptr(dz), V, self.w(pre + '/reconstruct/kernel'), V, ta=0, tb=1,
+            if self.fused_tower:
+                if self.mx8:   # MX-FP8 dZ (dX A, K = V) and dZ^T (dW B, K = rows) + the bias grad
+                    L.call('cc_quant_mx8', L.CC_BF16, L.ptr(dz), B, V, V, 0, L.ptr(self.dZq[r0:]), self.Vp,
+                           L.ptr(self.dZqs[r0:]), None, s)
+                    L.call('cc_quant_mx8', L.CC_BF16, L.ptr(self.dZt[k]), V, B, B, 0, L.ptr(self.dZtq[k]), B,
+                           L.ptr(self.dZtqs[k]), self.gp(pre + '/reconstruct/bias'), s)
+                gx = self._gemm(B, d, self.Vp if self.mx8 else V, **self._dec_dx(k, r0, pre), ta=0, tb=1,
                                 epi=L.CC_EPI_SPLITK, Cf=L.ptr(self.split_buf), splits=self.splits,
                                 launch=False)
-                gw = self._gemm(d, V, B, L.ptr(self.D3t[:, r0:]), R, L.ptr(self.dZt[k]), B, ta=0, tb=1,
+                gw = self._gemm(d, V, B, **self._dec_dw(k, r0), ta=0, tb=1,
                                 Cf=self.gp(pre + '/reconstruct/kernel'),
-                                colsum=self.gp(pre + '/reconstruct/bias'), launch=False)
-                L.call('cc_gemm_pair', L.C.byref(gx), L.C.byref(gw), s)
+                                colsum=None if self.mx8 else self.gp(pre + '/reconstruct/bias'), launch=False)
+                if not self.timing and not self.overlap:   # dX (split-K) and dW in one grouped launch
+                    L.call('cc_gemm_pair', L.C.byref(gx), L.C.byref(gw), s)
+                else:
+                    t = self._tick('dec_dW', self.side if self.overlap else None)
+                    L.call('cc_gemm', L.C.byref(gw), ss)
+                    t()
+                    t = self._tick('dec_dX')
+                    L.call('cc_gemm', L.C.byref(gx), s)
+                    t()
                 L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), self.splits, B, d,
                        L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
                 continue
             t = self._tick('dec_dW', self.side if self.overlap else None)
-            if self.fused_tower:   # dW = D3^T dZ with both operands k-contiguous
-                self._gemm(d, V, B, L.ptr(self.D3t[:, r0:]), R, L.ptr(self.dZt[k]), B, ta=0, tb=1,
-                           Cf=self.gp(pre + '/reconstruct/kernel'), colsum=self.gp(pre + '/reconstruct/bias'),
-                           stream=ss)
-            else:
-                self._gemm(d, V, B, L.ptr(self.D3[r0:]), d, L.ptr(dz), V, ta=1, tb=0,
-                           Cf=self.gp(pre + '/reconstruct/kernel'), colsum=self.gp(pre + '/reconstruct/bias'),
-                           stream=ss)
+            self._gemm(d, V, B, L.ptr(self.D3[r0:]), d, L.ptr(dz), V, ta=1, tb=0,
+                       Cf=self.gp(pre + '/reconstruct/kernel'), colsum=self.gp(pre + '/reconstruct/bias'),
+                       stream=ss)
             t()
             t = self._tick('dec_dX')
             self._gemm(B, d, V, L.ptr(dz), V, self.w(pre + '/reconstruct/kernel'), V, ta=0, tb=1,
@@ -474,12 +522,34 @@ class Trainer:
             t()
             L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), self.splits, B, d,
                    L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
-            if not self.fused_tower:
-                rows = (r0, r1)
-                self._dense_bwd(self.D2, self.gD3, rows, 256, d, pre + '/decoded_3', gIn=self.gD2, mask=self.D2)
-                self._dense_bwd(self.D1, self.gD2, rows, 128, 256, pre + '/decoded_2', gIn=self.gD1, mask=self.D1)
-                self._dense_bwd(self.Zl, self.gD1, rows, 64, 128, pre + '/decoded_1', gIn=self.gZl, mask=self.Zl)
+            rows = (r0, r1)
+            self._dense_bwd(self.D2, self.gD3, rows, 256, d, pre + '/decoded_3', gIn=self.gD2, mask=self.D2)
+            self._dense_bwd(self.D1, self.gD2, rows, 128, 256, pre + '/decoded_2', gIn=self.gD1, mask=self.D1)
+            self._dense_bwd(self.Zl, self.gD1, rows, 64, 128, pre + '/decoded_1', gIn=self.gZl, mask=self.Zl)
         self._join()
+
+    # operands of the decoder output-layer products (branch k, rows [r0, r0 + B)): bf16 NT images
+    # (D3, Wo^T, dZ, Wo, D3^T, dZ^T) or their MX-FP8 codes + E8M0 scales
+    def _dec_fwd(self, k, r0):
+        d = self.cfg.d
+        if self.mx8:
+            return dict(A=L.ptr(self.D3q[r0:]), lda=d, B=L.ptr(self.WoT8[k]), ldb=d, dtype=L.CC_MX8,
+                        a_scale=L.ptr(self.D3qs[r0:]), b_scale=L.ptr(self.WoT8s[k]))
+        return dict(A=L.ptr(self.D3[r0:]), lda=d, B=L.ptr(self.WoT[k]), ldb=d)
+
+    def _dec_dx(self, k, r0, pre):
+        V = self.cfg.V
+        if self.mx8:
+            return dict(A=L.ptr(self.dZq[r0:]), lda=self.Vp, B=L.ptr(self.Wo8[k]), ldb=self.Vp,
+                        dtype=L.CC_MX8, a_scale=L.ptr(self.dZqs[r0:]), b_scale=L.ptr(self.Wo8s[k]))
+        return dict(A=L.ptr(self.dZout[r0:]), lda=V, B=self.w(pre + '/reconstruct/kernel'), ldb=V)
+
+    def _dec_dw(self, k, r0):
+        R, B = self.R, self.cfg.batch_size
+        if self.mx8:
+            return dict(A=L.ptr(self.D3tq[:, r0:]), lda=R, B=L.ptr(self.dZtq[k]), ldb=B, dtype=L.CC_MX8,
+                        a_scale=L.ptr(self.D3tqs[:, r0 // 32:]), b_scale=L.ptr(self.dZtqs[k]))
+        return dict(A=L.ptr(self.D3t[:, r0:]), lda=R, B=L.ptr(self.dZt[k]), ldb=B)
 
     def forward_backward_b(self, stream=None):
         """Towers backward (both branches' rows together through the shared encoder) and the E1
@@ -538,9 +608,7 @@ class Trainer:
             return
         if self.fused_tower and stream is None:
             ss = self._fork()
-            for k, pre in enumerate(branches_of(self.use_reg)):
-                L.call('cc_transpose', self.dtype, self.w(pre + '/reconstruct/kernel'), self.cfg.d, self.cfg.V,
-                       L.ptr(self.WoT[k]), ss)
+            self.refresh_decoder_operands(ss)
             L.call('cc_tower_transpose_advance', L.C.byref(self.targs), L.ptr(self.state),
                    self.batches_per_epoch, L.stream_ptr(None))
             self._join()

@@ -38,7 +38,9 @@ enum cc_status {
   CC_ERR_CAPACITY = -4     /* a caller-provided buffer is too small */
 };
 
-enum cc_dtype { CC_F32 = 0, CC_BF16 = 1 };
+/* CC_MX8: OCP MX-FP8 operands (cc_gemm only) — e4m3fn codes [rows][ld] + one E8M0 scale byte per
+ * 32 K-elements ([rows][ld/32]), quantised by cc_quant_mx8 (config 5). */
+enum cc_dtype { CC_F32 = 0, CC_BF16 = 1, CC_MX8 = 2 };
 
 /* Number of tensors in the model (model.py: encoder 4 layers + 2 decoders x 4 layers, kernel+bias). */
 #define CC_NUM_TENSORS 24
@@ -159,8 +161,12 @@ typedef struct cc_gemm_args {
                            kernel's last tile block */
   double loss_scale;
   uint32_t *ticket;     /* with loss_out: one zeroed word, left zeroed */
+  const uint8_t *a_scale, *b_scale;  /* CC_MX8: E8M0 scales [M][lda/32] of A, [N][ldb/32] of B */
 } cc_gemm_args;
 int cc_gemm(const cc_gemm_args *g, void *stream);
+/* CC_MX8 runs v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 x e4m3, block scales applied in the MFMA):
+ * NT only (ta = 0, tb = 1), K % 128 == 0, lda % 128 == ldb % 128 == 0, epilogues STORE / BCE /
+ * SPLITK without colsum; outputs as for CC_BF16 (C is bf16, Cf fp32). */
 /* Two independent products in one launch (grouped GEMM) when both take the bf16 NT path with
  * the STORE or SPLITK epilogue; otherwise cc_gemm(g0) then cc_gemm(g1).  Same results. */
 int cc_gemm_pair(const cc_gemm_args *g0, const cc_gemm_args *g1, void *stream);
@@ -172,6 +178,19 @@ int cc_gemm_grid(int32_t M, int32_t N, int32_t *tiles);
 int cc_splitk_reduce(int32_t dtype, const float *partials, int32_t splits, int32_t M, int32_t N,
                      const void *H, void *C, float *Cf, const float *colsum_partials,
                      float *colsum_out, void *stream);
+
+/* MX-FP8 quantisation (oracle/mx8_ref.py, bit-exact): blocks of 32 along the GEMM K axis, E8M0
+ * exponent e = min{e : amax <= 448 * 2^e}, codes = e4m3 RNE of x * 2^-e.  src is [rows][ld_src]
+ * (dtype CC_BF16 or CC_F32).
+ *   transpose = 0: dst [rows][ld_dst] codes, scales [rows][ld_dst/32]; K axis = cols (padded with
+ *                  zeros up to ld_dst); rowsum (optional, needs ld_dst <= 2048): rowsum[r] = fp32
+ *                  sum of src row r (the bias gradient when src is dZ^T).
+ *   transpose = 1: dst [cols][ld_dst] with dst[c][r] = q(src[r][c]), scales [cols][ld_dst/32];
+ *                  K axis = rows (padded up to ld_dst).  rowsum must be NULL.
+ * ld_dst % 128 == 0. */
+int cc_quant_mx8(int32_t dtype, const void *src, int32_t rows, int32_t cols, int32_t ld_src,
+                 int32_t transpose, uint8_t *dst, int32_t ld_dst, uint8_t *scales, float *rowsum,
+                 void *stream);
 
 /* dst[c][r] = src[r][c] for a [rows, cols] row-major matrix (dtype elements). */
 int cc_transpose(int32_t dtype, const void *src, int32_t rows, int32_t cols, void *dst, void *stream);
@@ -190,7 +209,7 @@ int cc_colsum(int32_t dtype, const void *X, int32_t R, int32_t N, int32_t ld, fl
  *                 partial dW/db of the 6 layers each block touches into slab[blk][...].
  *   cc_tower_reduce: grads of the 9 layers = sum of the slabs in block order (deterministic).
  *   cc_tower_transpose: wt[l] = w[l]^T ([N][K]) — the k-contiguous operand the forward reads.
- * d <= 512 (bf16) / <= 256 (fp32); the generic cc_gemm path covers larger widths.
+ * d <= 1024 (bf16) / <= 256 (fp32); the generic cc_gemm path covers larger widths.
  * ---------------------------------------------------------------------------------- */
 typedef struct cc_tower_args {
   int32_t dtype, d, B, R;

@@ -16,7 +16,8 @@ def _dims(d):
 
 
 @pytest.mark.parametrize('dtype', [L.CC_F32, L.CC_BF16])
-@pytest.mark.parametrize('d,B,R', [(64, 32, 64), (256, 64, 128), (256, 64, 64), (64, 32, 32), (512, 64, 128)])
+@pytest.mark.parametrize('d,B,R', [(64, 32, 64), (256, 64, 128), (256, 64, 64), (64, 32, 32), (512, 64, 128),
+                                   (1024, 64, 128)])
 def test_tower_fwd_bwd_vs_numpy(dtype, d, B, R):
     if dtype == L.CC_F32 and d > 256:
         pytest.skip('fp32 fused towers cover d <= 256')

@@ -227,3 +227,59 @@ def test_data_parallel_equivalence(reg):
         single.apply()
         torch.cuda.synchronize()
         assert rel_err(ranks[0].standard(ranks[0].params), single.params.cpu().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize('reg', [0.0, 0.1])
+@pytest.mark.parametrize('V,d,B', [(1500, 128, 128), (2500, 1024, 128)])
+def test_fp8_decoder_steps_track_oracle(reg, V, d, B):
+    """Config 5: MX-FP8 decoder output / regulariser GEMMs, everything else bf16.
+    Parity is claimed at fp32 only (§8(d)); here F is bit-exact, the losses track the bf16-emulating
+    oracle within the fp8 element precision (3 mantissa bits) and the gradients within 10 % L2."""
+    C = 4 * B
+    tr, lists, Mt, ns, P, perm = _setup(V, d, B, C, reg, 'fp8')
+    assert tr.mx8 and tr.fused_tower
+    cdf = noise_ref.cdf_of(ns)
+    for step in range(2):
+        tr.forward_backward()
+        torch.cuda.synchronize()
+        xs, ys, reg_idx = tr.batch_lists()
+        cubes = [lists[c] for c in perm[step * B:(step + 1) * B]]
+        oxs, oys, oreg, _ = noise_ref.philox_noise_batch(cubes, cdf, ns, tr.cfg.seed, step)
+        for b in range(B):
+            assert np.array_equal(xs[b], oxs[b]) and np.array_equal(ys[b], oys[b])
+        losses, grads = model_ref.train_forward_backward(
+            P, oxs, oys, V, d, reg=reg, reg_idx=oreg, y_reg=Mt[oreg] if reg > 0 else None, mode='bf16')
+        got = tr.losses()
+        assert abs(got['bce'] - losses['bce']) / losses['bce'] < 1e-2, (step, got, losses)
+        if reg > 0:
+            assert abs(got['kl'] - losses['kl']) / losses['kl'] < 1e-2, (step, got, losses)
+        gflat = tr.layout.unpack(tr.grads.cpu().numpy())
+        errs = {k: rel_err(gflat[k], grads[k]) for k in grads if reg or not k.startswith('decoder_for_reg')}
+        bad = {k: v for k, v in errs.items() if not v < 0.1}
+        assert not bad, (step, bad)
+        tr.apply()
+        torch.cuda.synchronize()
+        P = tr.layout.unpack(tr.params.cpu().numpy())   # follow the GPU trajectory
+
+
+@pytest.mark.parametrize('reg', [0.0, 0.1])
+def test_wide_d1024_bf16_steps_match_oracle(reg):
+    """d = 1024 (config 5's width) through the fused towers at bf16."""
+    V, d, B = 2500, 1024, 64
+    tr, lists, Mt, ns, P, perm = _setup(V, d, B, 4 * B, reg, 'bf16')
+    assert tr.fused_tower
+    cdf = noise_ref.cdf_of(ns)
+    tr.forward_backward()
+    torch.cuda.synchronize()
+    cubes = [lists[c] for c in perm[:B]]
+    oxs, oys, oreg, _ = noise_ref.philox_noise_batch(cubes, cdf, ns, tr.cfg.seed, 0)
+    losses, grads = model_ref.train_forward_backward(
+        P, oxs, oys, V, d, reg=reg, reg_idx=oreg, y_reg=Mt[oreg] if reg > 0 else None, mode='bf16')
+    got = tr.losses()
+    assert abs(got['bce'] - losses['bce']) / losses['bce'] < 2e-4
+    if reg > 0:
+        assert abs(got['kl'] - losses['kl']) / losses['kl'] < 2e-4
+    gflat = tr.layout.unpack(tr.grads.cpu().numpy())
+    bad = {k: rel_err(gflat[k], grads[k]) for k in grads if (reg or not k.startswith('decoder_for_reg'))
+           and not rel_err(gflat[k], grads[k]) < 2e-2}
+    assert not bad, bad
