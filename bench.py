@@ -31,6 +31,9 @@ def parse():
     ap.add_argument('--cubes', type=int, default=65536)
     ap.add_argument('--reg', type=float, default=0.0)
     ap.add_argument('--dtype', default='bf16')
+    ap.add_argument('--reg-shard', type=int, default=1,
+                    help='with --reg > 0 on N > 1 ranks: M~ row-sharded at equal neg_sampler mass, '
+                         'owner computes (SURVEY 8(e)); 0 = every rank holds all of M~')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-steps', type=int, default=16)
     ap.add_argument('--no-recommend', action='store_true')
@@ -158,13 +161,21 @@ def main():
     t_setup = time.perf_counter()
     indptr, indices = synthetic_cubes(args.cubes, V, seed=20250301, device=dev)
     ns = neg_sampler_from_csr(indptr, indices, V)
-    y_mtx = None
+    y_mtx, reg_rows = None, None
+    reg_shard = bool(args.reg_shard) and world > 1 and args.reg > 0
     if args.reg > 0:
         from cubecobrarecommender_amd.adjacency import adjacency_normalised_gpu
         y_mtx = adjacency_normalised_gpu(indptr, indices, V, device=dev)
-    data = DeviceDataset(csr=(indptr, indices), num_cards=V, neg_sampler=ns, y_mtx=y_mtx, device=dev)
+        if reg_shard:    # keep only this rank's rows of M~
+            from cubecobrarecommender_amd.trainer import reg_rows_for
+            reg_rows = reg_rows_for(ns, world, rank)
+            y_mtx = y_mtx[reg_rows[0]:reg_rows[1]].clone()
+            torch.cuda.empty_cache()
+    data = DeviceDataset(csr=(indptr, indices), num_cards=V, neg_sampler=ns, y_mtx=y_mtx, device=dev,
+                         reg_rows=reg_rows)
+    del y_mtx
     cfg = TrainConfig(V=V, d=d, batch_size=B, reg=args.reg, dtype=args.dtype, seed=1234,
-                      rank=rank, world=world)
+                      rank=rank, world=world, reg_shard=reg_shard)
     tr = Trainer(cfg, data, params_flat=glorot_flat(V, d, seed=42), device=dev)
     rng = np.random.default_rng(99)      # same permutations on every rank
     tr.set_epoch_permutations(np.stack([rng.permutation(args.cubes) for _ in range(4)]))

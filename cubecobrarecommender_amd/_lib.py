@@ -26,6 +26,7 @@ class NoiseArgs(C.Structure):
         ('guide_log2', C.c_int32), ('state', C.c_void_p),
         ('x_cnt', C.c_void_p), ('x_idx', C.c_void_p), ('y_bits', C.c_void_p),
         ('xt_bits', C.c_void_p), ('reg_idx', C.c_void_p), ('status', C.c_void_p),
+        ('reg_lo', C.c_int32), ('reg_hi', C.c_int32),
     ]
 
 

@@ -54,6 +54,15 @@ __device__ __forceinline__ int search_right(const double *__restrict__ cdf, int 
   return lo < V ? lo : V - 1;
 }
 
+// u in [0,1) -> [cdf[lo-1], cdf[hi-1]) (cdf[-1] = 0): the inverse-CDF draw restricted to cards
+// [lo, hi).  A product that rounds onto the upper edge is folded back to the lower one.
+__device__ __forceinline__ double shard_u(const double *__restrict__ cdf, int lo, int hi, double u) {
+#pragma clang fp contract(off)
+  const double ulo = lo > 0 ? cdf[lo - 1] : 0.0, uhi = cdf[hi - 1];
+  const double v = ulo + u * (uhi - ulo);
+  return v < uhi ? v : ulo;
+}
+
 __device__ __forceinline__ double noise_level(double mean, double std, double z) {
 #pragma clang fp contract(off)
   double lvl = mean + std * z;
@@ -200,7 +209,13 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
   // regulariser row for this slot (generator.py:47-51): one draw ∝ neg_sampler
   if (a.with_reg && tid == 0) {
     const u32x4 o = rng(a.seed, step, slot, KIND_REG, 0, 0);
-    const int j = search_right(a.cdf, a.V, u53(o.x, o.y), a.guide, a.guide_log2);
+    int j;
+    if (a.reg_hi > 0) {  // row-sharded M~: the draw conditioned on the rank's shard of cards
+      j = search_right(a.cdf, a.V, shard_u(a.cdf, a.reg_lo, a.reg_hi, u53(o.x, o.y)), a.guide, a.guide_log2);
+      j = j < a.reg_lo ? a.reg_lo : (j >= a.reg_hi ? a.reg_hi - 1 : j);
+    } else {
+      j = search_right(a.cdf, a.V, u53(o.x, o.y), a.guide, a.guide_log2);
+    }
     a.reg_idx[b] = j;
     const int r = a.B + b;
     a.x_idx[(int64_t)r * a.x_cap] = j;

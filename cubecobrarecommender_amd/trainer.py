@@ -38,13 +38,48 @@ class TrainConfig:
     world: int = 1
     fused_tower: bool = True       # tower.hip row-block kernels (else per-layer cc_gemm launches)
     prefetch_noise: bool = True    # one process: F of step k+1 rides in step k's Adam launch
+    reg_shard: bool = False        # data parallel + reg: M~ row-sharded, owner computes
+
+
+def reg_row_shards(cdf, world):
+    """Row shards of M~ for the regulariser (owner computes): boundaries b[0..world]
+    at equal cumulative neg_sampler mass — shard r = cards whose CDF value lies in
+    (r/world, (r+1)/world] — and each shard's mass m_r = cdf[b_{r+1}-1] - cdf[b_r-1].  Rank r holds
+    rows [b_r, b_{r+1}) of M~ only and draws its B reg rows from neg_sampler conditioned on them
+    (csrc/noise.hip shard_u); weighting its KL by world * m_r makes the averaged gradient the
+    stratified estimate of the same expectation the one-process step samples."""
+    cdf = np.asarray(cdf, np.float64)
+    V = len(cdf)
+    b = np.searchsorted(cdf, np.arange(world + 1) / float(world), side='right')
+    b[0], b[world] = 0, V
+    b = np.maximum.accumulate(np.minimum(b, V))
+    lo_mass = np.where(b[:-1] > 0, cdf[np.maximum(b[:-1] - 1, 0)], 0.0)
+    hi_mass = np.where(b[1:] > 0, cdf[np.maximum(b[1:] - 1, 0)], 0.0)
+    mass = hi_mass - lo_mass
+    if np.any(b[1:] <= b[:-1]) or np.any(mass <= 0):
+        raise ValueError(f'reg_row_shards: a shard of {world} is empty (one card holds > 1/{world} '
+                         'of the neg_sampler mass); use the replicated M~ (reg_shard=False)')
+    return b.astype(np.int64), mass
+
+
+def _cdf(neg_sampler):
+    cdf = np.cumsum(np.asarray(neg_sampler, np.float64))
+    return cdf / cdf[-1]
+
+
+def reg_rows_for(neg_sampler, world, rank):
+    """Rank's M~ row shard [lo, hi) (reg_row_shards on the dataset's CDF)."""
+    b, _ = reg_row_shards(_cdf(neg_sampler), world)
+    return int(b[rank]), int(b[rank + 1])
 
 
 class DeviceDataset:
-    """Cubes as a device CSR (sorted card ids), neg_sampler / CDF and optional M~ (fp32)."""
+    """Cubes as a device CSR (sorted card ids), neg_sampler / CDF and optional M~ (fp32).
+    ``reg_rows=(lo, hi)``: y_mtx holds (or is cut down to) rows [lo, hi) of M~ only — the
+    row-sharded regulariser of a data-parallel rank (reg_row_shards)."""
 
     def __init__(self, cube_lists=None, num_cards=None, y_mtx=None, neg_sampler=None,
-                 device='cuda', csr=None):
+                 device='cuda', csr=None, reg_rows=None):
         if csr is not None:
             indptr, indices = csr
             indptr = np.asarray(indptr, np.int64)
@@ -65,18 +100,25 @@ class DeviceDataset:
                 raise ValueError('need y_mtx (M~) or neg_sampler')
             neg_sampler = _neg_sampler(y_mtx)
         ns = np.asarray(neg_sampler, np.float64)
-        cdf = np.cumsum(ns)
-        cdf /= cdf[-1]
+        cdf = _cdf(ns)
         self.neg_sampler_host = ns
+        self.cdf_host = cdf
         self.neg_sampler = torch.from_numpy(ns).to(device)
         self.cdf = torch.from_numpy(cdf).to(device)
         self.guide_log2 = 12   # CDF search guide table: 4097 entries
         guide = np.searchsorted(cdf, np.arange((1 << self.guide_log2) + 1) / float(1 << self.guide_log2), side='right')
         self.guide = torch.from_numpy(guide.astype(np.int32)).to(device)
         self.y_reg = None
+        self.reg_rows = None
         if y_mtx is not None:
             y = y_mtx if torch.is_tensor(y_mtx) else torch.from_numpy(np.asarray(y_mtx, np.float32))
+            lo, hi = reg_rows if reg_rows is not None else (0, self.V)
+            if y.shape[0] == self.V and (lo, hi) != (0, self.V):
+                y = y[lo:hi]
+            if y.shape != (hi - lo, self.V):
+                raise ValueError(f'y_mtx rows {tuple(y.shape)}: expected ({hi - lo}, {self.V})')
             self.y_reg = y.to(device=device, dtype=torch.float32).contiguous()
+            self.reg_rows = (int(lo), int(hi))
 
 
 def branches_of(use_reg):
@@ -107,6 +149,17 @@ class Trainer:
         if self.use_reg and data.y_reg is None:
             raise ValueError('reg > 0 needs the M~ matrix on the device')
         self.R = 2 * B if self.use_reg else B
+        # regulariser rows: all of M~, or (data parallel, reg_shard) this rank's row shard
+        self.reg_rows, self.reg_weight = (0, V), 1.0
+        if self.use_reg and cfg.reg_shard and cfg.world > 1:
+            bnd, mass = reg_row_shards(data.cdf_host, cfg.world)
+            self.reg_rows = (int(bnd[cfg.rank]), int(bnd[cfg.rank + 1]))
+            self.reg_weight = float(cfg.world * mass[cfg.rank])
+        if self.use_reg and data.reg_rows != self.reg_rows:
+            if data.reg_rows != (0, V):
+                raise ValueError(f'dataset holds M~ rows {data.reg_rows}, rank needs {self.reg_rows}')
+            lo, hi = self.reg_rows
+            data.y_reg, data.reg_rows = data.y_reg[lo:hi].contiguous(), self.reg_rows
         if cfg.dtype not in ('bf16', 'fp32', 'fp8'):
             raise ValueError(f'dtype {cfg.dtype!r}: bf16, fp32 or fp8')
         self.mx8 = cfg.dtype == 'fp8'
@@ -362,7 +415,9 @@ class Trainer:
                            guide_log2=self.data.guide_log2, state=self.state.data_ptr(),
                            x_cnt=self.x_cnt.data_ptr(), x_idx=self.x_idx.data_ptr(),
                            y_bits=self.y_bits.data_ptr(), xt_bits=self.xt_bits.data_ptr(),
-                           reg_idx=self.reg_idx.data_ptr(), status=self.status.data_ptr())
+                           reg_idx=self.reg_idx.data_ptr(), status=self.status.data_ptr(),
+                           reg_lo=self.reg_rows[0],
+                           reg_hi=self.reg_rows[1] if self.reg_rows != (0, V) else 0)
 
     def _gemm(self, M, N, K, A, lda, B, ldb, ta=0, tb=0, epi=L.CC_EPI_STORE, ldc=None, bias=None,
               relu=0, C=None, Cf=None, H=None, y_bits=None, scale=0.0, partials=None, splits=1,
@@ -476,13 +531,17 @@ class Trainer:
                 self._gemm(B, V, d, L.ptr(self.D3[B:]), d, self.w('decoder_for_reg/reconstruct/kernel'), V,
                            bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2))
             t = self._tick('dec_softmax_kl')
-            L.call('cc_dec_softmax_kl_fused', self.dtype, L.ptr(self.Z2), B, V, L.ptr(self.data.y_reg),
-                   L.ptr(self.reg_idx), float(cfg.reg), L.ptr(self.dZout[B:]), L.ptr(self.kl_part), s)
+            # M~ row shard [lo, hi): the kernel indexes y_reg[reg_idx * V], so pass the base of
+            # row 0 (reg_idx lies in [lo, hi) by construction of the draw)
+            y_base = L.C.c_void_p(self.data.y_reg.data_ptr() - self.reg_rows[0] * V * 4)
+            L.call('cc_dec_softmax_kl_fused', self.dtype, L.ptr(self.Z2), B, V, y_base,
+                   L.ptr(self.reg_idx), float(cfg.reg * self.reg_weight), L.ptr(self.dZout[B:]),
+                   L.ptr(self.kl_part), s)
             t()
             if self.fused_tower:   # dZ2^T [V][B]: the k-contiguous operand of the reg branch's dW
                 L.call('cc_transpose', self.dtype, L.ptr(self.dZout[B:]), B, V, L.ptr(self.dZt[1]), s)
             ss = self._fork()
-            L.call('cc_reduce_loss', L.ptr(self.kl_part), B, 1.0 / B, L.ptr(self.loss_dev[1:]), ss)
+            L.call('cc_reduce_loss', L.ptr(self.kl_part), B, self.reg_weight / B, L.ptr(self.loss_dev[1:]), ss)
         # ---- backward through the output layers and decoder towers.  The output layers' dW
         # (side stream) and dX -> towers (this stream) only share read-only inputs.
         for k, (pre, (r0, r1)) in enumerate(branches):

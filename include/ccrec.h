@@ -95,6 +95,10 @@ typedef struct cc_noise_args {
   uint32_t *xt_bits;                         /* [V, ceil(R/32)] transposed x bits (zeroed) or NULL */
   int32_t *reg_idx;                          /* [B] or NULL */
   int32_t *status;                           /* [1] device error flags (0 = ok) */
+  int32_t reg_lo, reg_hi;                    /* M~ row shard [reg_lo, reg_hi) of this rank (SURVEY
+                                                8(e) owner computes): reg rows are drawn from
+                                                neg_sampler restricted to the shard (u mapped into
+                                                [cdf[lo-1], cdf[hi-1]) ); reg_hi == 0: all cards */
 } cc_noise_args;
 int cc_noise_fwd(const cc_noise_args *a, void *stream);
 /* cc_adam_dense(p, m, v, g, shadow, n, next->state, ...) and, in the same launch, cc_noise_fwd
