@@ -53,7 +53,7 @@ class TowerArgs(C.Structure):
         ('w', C.c_void_p * 9), ('wt', C.c_void_p * 9), ('b', C.c_void_p * 9), ('act', C.c_void_p * 7),
         ('act6t', C.c_void_p),
         ('gD3', C.c_void_p), ('gact', C.c_void_p * 5), ('gpre1', C.c_void_p), ('slab', C.c_void_p),
-        ('gw', C.c_void_p * 9), ('gb', C.c_void_p * 9),
+        ('gw', C.c_void_p * 9), ('gb', C.c_void_p * 9), ('gpre1t', C.c_void_p),
     ]
 
 
@@ -68,6 +68,7 @@ SIGNATURES = {
     'cc_noise_fwd': (C.c_int, [C.POINTER(NoiseArgs), _P]),
     'cc_embed_gather_fwd': (C.c_int, [_I32, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P]),
     'cc_embed_scatter_bwd': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
+    'cc_embed_grad_mfma': (C.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_gemm': (C.c_int, [C.POINTER(GemmArgs), _P]),
     'cc_gemm_pair': (C.c_int, [C.POINTER(GemmArgs), C.POINTER(GemmArgs), _P]),
     'cc_gemm_grid': (C.c_int, [_I32, _I32, _P]),
@@ -76,6 +77,8 @@ SIGNATURES = {
     'cc_transpose': (C.c_int, [_I32, _P, _I32, _I32, _P, _P]),
     'cc_quant_mx8': (C.c_int, [_I32, _P, _I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P]),
     'cc_dec_bce_fused': (C.c_int, [_I32, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
+    'cc_dec_bce_dw': (C.c_int, [_P, _P, _I32, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _F64, _P, _P]),
+    'cc_dec_bce_dw_blocks': (_I32, [_I32]),
     'cc_dec_softmax_kl_fused': (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _F32, _P, _P, _P]),
     'cc_reduce_loss': (C.c_int, [_P, _I32, _F64, _P, _P]),
     'cc_adam_noise': (C.c_int, [_P, _P, _P, _P, _P, _I64, _F32, _F32, _F32, _F32, C.POINTER(NoiseArgs), _I64, _P]),

@@ -1,0 +1,332 @@
+// D1 output layer, fused: logits -> sigmoid/BCE -> dZ -> dWo, dbo in ONE pass over a 96-column
+// slice of |V| (model.py:64 Dense(V) + :94 sigmoid; train.py:85 binary_crossentropy; the
+// MatMul/BiasAdd gradients of the reconstruct layer inside fit).
+//
+// A block owns output columns [n0, n0 + 96) for ALL B batch rows, so the output-layer weight
+// gradient of those columns is complete inside the block:
+//   phase 1  z[B][96] = D3[B][d] Wo^T[96][d]^T + bo   (Wo^T slice resident in LDS, D3 fragments
+//            loaded global -> registers), BCE on the accumulators, dZ written row-major for the dX
+//            product (cc_gemm split-K), and kept in LDS as dZ^T [96][B] (bf16, the rounded values
+//            the dX product also sees) — the dZ^T HBM round trip of the unfused path is gone;
+//   phase 2  dWo[d][96] = D3^T[d][B] dZ[B][96]          (D3^T fragments from global through a
+//            4-deep register ring, dZ^T from LDS), dbo = colsum.
+// bf16 MFMA v_mfma_f32_32x32x16_bf16 (fp32 accumulation), 8 waves; the loss is published per block
+// and the last block (agent-scope ticket) reduces the partials in block order — deterministic.
+#include "common.hpp"
+
+namespace {
+
+constexpr int NB = 96;      // V columns per block: ceil(22000 / 96) = 230 blocks <= 256 CUs, one round
+constexpr int NJ = NB / 32; // 32-column accumulators per wave
+constexpr int BK = 64;      // k per phase-2 ring chunk
+constexpr int NTH = 512;    // 8 waves
+constexpr int BMAX = 512;   // batch rows (B <= 512)
+constexpr int DMAX = 256;   // d <= 256
+// LDS map (bytes): the Wo^T slice [NB][d]; dZ^T [NB][B]; the target bits [B][NJ].
+constexpr int ZT_OFF = NB * DMAX * 2, ZT_BYTES = NB * BMAX * 2;
+constexpr int YS_OFF = ZT_OFF + ZT_BYTES, YS_BYTES = BMAX * NJ * 4;
+constexpr int LDS_BYTES = YS_OFF + YS_BYTES;
+constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+
+typedef __attribute__((ext_vector_type(4))) uint32_t v4u;  // staging registers (stay in VGPRs)
+
+struct DecOutP {
+  const bf16_t *D3;        // [B][d]
+  const bf16_t *D3t;       // [d][ldt]
+  const bf16_t *WoT;       // [V][d]
+  const float *bo;         // [V]
+  const uint32_t *y_bits;  // [B][ceil(V/32)]
+  bf16_t *dZ;              // [B][V]
+  float *gW;               // [d][V]
+  float *gb;               // [V]
+  double *loss_partials;   // [gridDim.x]
+  double *loss_out;        // [1] or null
+  uint32_t *ticket;
+  double loss_scale;
+  float scale;
+  int V, ldt;
+};
+
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// element offset of (row, k) in a k-contiguous LDS image with `chunks` 16-B chunks per row,
+// chunk index XOR-swizzled by the row's low 4 bits (conflict-free fragment reads)
+__device__ __forceinline__ int sw_off(int row, int k, int chunks) {
+  return row * chunks * 8 + ((((k >> 3) ^ (row & 15)) << 3) | (k & 7));
+}
+
+__device__ __forceinline__ bf16x8_t frag(const bf16_t *S, int off) {
+  return *reinterpret_cast<const bf16x8_t *>(S + off);
+}
+
+__device__ __forceinline__ uint16_t bf16_bits(float f) {  // RNE (v_cvt_pk_bf16_f32), finite inputs
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
+}
+
+template <int D, int BB>
+__global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
+  constexpr int d = D, B = BB;
+  constexpr int CHD = d / 8, CHB = B / 8;
+  constexpr int nkk = d / 16;                     // 16-k steps of phase 1
+  constexpr int npass = (B + 255) / 256;          // 256-row passes of phase 1
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+  __shared__ float red_cs[NTH / 64][NB];
+  __shared__ double red_loss[NTH / 64];
+  __shared__ int lastflag;
+  bf16_t *Wt = reinterpret_cast<bf16_t *>(smem);                 // [NB][d]
+  bf16_t *Zt = reinterpret_cast<bf16_t *>(smem + ZT_OFF);        // [NB][B]
+  uint32_t *ys = reinterpret_cast<uint32_t *>(smem + YS_OFF);    // [B][NJ]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
+  const int n0 = blockIdx.x * NB;
+  const int V = p.V;
+  const int VW = (V + 31) >> 5;
+
+  // ---- resident operands: Wo^T slice (rows clamped at the edge: they feed masked columns only)
+  // and the target bits; every load of the batch issued before the first LDS store
+  {
+    constexpr int NW = NB * CHD / NTH, NY = (B * NJ + NTH - 1) / NTH;
+    v4u wv[NW];
+    uint32_t yv[NY];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const int c = tid + NTH * q, n = c / CHD, ch = c % CHD;
+      wv[q] = *reinterpret_cast<const v4u *>(p.WoT + (int64_t)min(n0 + n, V - 1) * d + ch * 8);
+    }
+#pragma unroll
+    for (int q = 0; q < NY; ++q) {
+      const int i = tid + NTH * q, r = min(i / NJ, B - 1), gw = (n0 >> 5) + i % NJ;
+      yv[q] = gw < VW ? p.y_bits[(int64_t)r * VW + gw] : 0u;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const int c = tid + NTH * q, n = c / CHD, ch = c % CHD;
+      *reinterpret_cast<v4u *>(Wt + sw_off(n, ch * 8, CHD)) = wv[q];
+    }
+#pragma unroll
+    for (int q = 0; q < NY; ++q)
+      if (tid + NTH * q < B * NJ) ys[tid + NTH * q] = yv[q];
+  }
+
+  // ---- phase 1: logits, BCE, dZ (global + LDS dZ^T), bias-gradient partial, loss.  Wave w owns
+  // rows pass*256 + 32w .. +32 and all NB columns; its A fragments (16 B per lane per 16-k step)
+  // come straight from global/L2 into registers, the next pass's in flight during this one.
+  float rsum = 0.f, lsum = 0.f, cs[NJ];
+  float bias[NJ];
+  bool valid[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int gc = n0 + j * 32 + (lane & 31);
+    valid[j] = gc < V;
+    bias[j] = valid[j] ? p.bo[gc] : 0.f;
+    cs[j] = 0.f;
+  }
+  bf16x8_t af[2][nkk];
+  auto load_a = [&](bf16x8_t (&dst)[nkk], int pass) {
+    const int row = min(pass * 256 + w * 32 + (lane & 31), B - 1);
+    const bf16_t *src = p.D3 + (int64_t)row * d + 8 * half;
+#pragma unroll
+    for (int kk = 0; kk < nkk; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 16);
+    // keep the whole batch in flight: without this fence the scheduler sinks each load to its
+    // MFMA and the pass becomes a chain of dependent L2 round trips
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  load_a(af[0], 0);
+  __syncthreads();
+  const float scale = p.scale;
+#pragma unroll
+  for (int ps = 0; ps < npass; ++ps) {
+    if (ps + 1 < npass) load_a(af[(ps + 1) & 1], ps + 1);
+    if (ps * 256 + w * 32 >= B) continue;          // wave-uniform: rows beyond B
+    f32x16_t acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < nkk; ++kk) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const bf16x8_t b = frag(Wt, sw_off(j * 32 + (lane & 31), kk * 16 + 8 * half, CHD));
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ps & 1][kk], b, acc[j], 0, 0, 0);
+      }
+    }
+    const int rb = ps * 256 + w * 32;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = j * 32 + (lane & 31);
+      uint16_t tt[16];
+      if (valid[j]) {
+        // sigmoid_cross_entropy_with_logits (TF 2.5 Keras BCE on a sigmoid output):
+        //   loss = max(z, 0) - z y + log1p(exp(-|z|)),  dz = (sigmoid(z) - y) / (B V)
+        // a = exp(-|z|) once; log1p and 1/(1+a) from it; log2 summed, scaled by ln 2 at the end
+        bf16_t *dst = p.dZ + (int64_t)(rb + 4 * half) * V + n0 + col;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = rb + acc_row(r, lane);
+          const uint32_t yb = (ys[row * NJ + j] >> (lane & 31)) & 1u;
+          const float z = acc[j][r] + bias[j];
+          const float a = __builtin_amdgcn_exp2f(-fabsf(z) * LOG2E);
+          const float opa = 1.f + a;
+          const float rp = __builtin_amdgcn_rcpf(opa);
+          lsum += __builtin_amdgcn_logf(opa);
+          rsum += fmaxf(yb ? -z : z, 0.f);
+          const float sig = z >= 0.f ? rp : a * rp;
+          const uint16_t zb = bf16_bits(fmaf(sig, scale, yb ? -scale : 0.f));
+          tt[r] = zb;
+          cs[j] += __uint_as_float((uint32_t)zb << 16);
+          dst[(int64_t)((r & 3) + 8 * (r >> 2)) * V] = zb;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tt[r] = 0;
+      }
+      // dZ^T image: registers 4g..4g+3 = 4 consecutive rows -> one 8-byte LDS store
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<uint2 *>(Zt + sw_off(col, rb + 8 * g + 4 * half, CHB)) =
+            *reinterpret_cast<const uint2 *>(&tt[4 * g]);
+    }
+  }
+
+  // bias gradient: column sums of the rounded dZ in a fixed order (lane halves, then waves)
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const float c2 = cs[j] + __shfl_xor(cs[j], 32);
+    if (half == 0) red_cs[w][j * 32 + (lane & 31)] = c2;
+  }
+  // loss: block partial, published before phase 2's stores
+  float lossf = rsum + lsum * LN2;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) lossf += __shfl_xor(lossf, off);
+  if (lane == 0) red_loss[w] = (double)lossf;
+  __syncthreads();   // dZ^T image, red_cs, red_loss complete
+  if (tid < NB && n0 + tid < V) {
+    float g = 0.f;
+    for (int i = 0; i < NTH / 64; ++i) g += red_cs[i][tid];
+    p.gb[n0 + tid] = g;
+  }
+  if (tid == 0) {
+    double sum = 0.0;
+    for (int i = 0; i < NTH / 64; ++i) sum += red_loss[i];
+    lastflag = 0;
+    if (!p.loss_out) {
+      p.loss_partials[blockIdx.x] = sum;
+    } else {
+      __hip_atomic_store(&p.loss_partials[blockIdx.x], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t tk = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lastflag = tk == gridDim.x - 1;
+    }
+  }
+
+  // ---- phase 2: dWo[d][NB] = D3^T[d][B] . dZ[B][NB].  Wave w owns rows 32w .. +32 of d (waves
+  // beyond d idle) and all NB columns; A fragments from global through a ring P2D chunks of 64 k
+  // deep, B fragments from the dZ^T image.
+  if (w * 32 < d) {
+    constexpr int P2D = 4;
+    constexpr int nk2 = B / BK;
+    const bf16_t *arow = p.D3t + (int64_t)(w * 32 + (lane & 31)) * p.ldt + 8 * half;
+    bf16x8_t ring[P2D][4];
+#pragma unroll
+    for (int q = 0; q < P2D; ++q)
+      if (q < nk2)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) ring[q][kk] = *reinterpret_cast<const bf16x8_t *>(arow + q * BK + kk * 16);
+    __builtin_amdgcn_sched_barrier(0);
+    f32x16_t acc2[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
+#pragma unroll
+    for (int kc = 0; kc < nk2; ++kc) {
+      const int q = kc % P2D;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const bf16x8_t b = frag(Zt, sw_off(j * 32 + (lane & 31), kc * BK + kk * 16 + 8 * half, CHB));
+          acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[q][kk], b, acc2[j], 0, 0, 0);
+        }
+      }
+      if (kc + P2D < nk2) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+          ring[q][kk] = *reinterpret_cast<const bf16x8_t *>(arow + (kc + P2D) * BK + kk * 16);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int gc2 = n0 + j * 32 + (lane & 31);
+      if (gc2 < V) {
+        float *g = p.gW + (int64_t)(w * 32 + 4 * half) * V + gc2;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) g[(int64_t)((r & 3) + 8 * (r >> 2)) * V] = acc2[j][r];
+      }
+    }
+  }
+
+  // ---- the last block reduces the loss partials in block order
+  if (p.loss_out) {
+    __syncthreads();
+    if (lastflag) {
+      double s2d = 0.0;
+      for (int i = tid; i < (int)gridDim.x; i += NTH)
+        s2d += __hip_atomic_load(&p.loss_partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) s2d += __shfl_xor(s2d, off);
+      if (lane == 0) red_loss[w] = s2d;
+      __syncthreads();
+      if (tid == 0) {
+        double tot = 0.0;
+        for (int i = 0; i < NTH / 64; ++i) tot += red_loss[i];
+        p.loss_out[0] = tot * p.loss_scale;
+        __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const void *WoT,
+                             const float *bo, int32_t B, int32_t d, int32_t V, const uint32_t *y_bits,
+                             void *dZ, float *gW, float *gb, double *loss_partials, double *loss_out,
+                             double loss_scale, uint32_t *ticket, void *stream) {
+  CC_REQUIRE(D3 && D3t && WoT && bo && y_bits && dZ && gW && gb && loss_partials,
+             "cc_dec_bce_dw: null pointer");
+  CC_REQUIRE(B == 128 || B == 256 || B == 512, "cc_dec_bce_dw: B must be 128, 256 or 512");
+  CC_REQUIRE(d == 128 || d == 256, "cc_dec_bce_dw: d must be 128 or 256");
+  CC_REQUIRE(V > 0 && ldt >= B && ldt % 8 == 0, "cc_dec_bce_dw: V > 0, ldt >= B, ldt % 8 == 0");
+  CC_REQUIRE(!loss_out || ticket, "cc_dec_bce_dw: loss_out needs a ticket word");
+  CC_REQUIRE((((uintptr_t)D3 | (uintptr_t)D3t | (uintptr_t)WoT) & 15) == 0, "cc_dec_bce_dw: operands 16-B aligned");
+  DecOutP p;
+  p.D3 = (const bf16_t *)D3;
+  p.D3t = (const bf16_t *)D3t;
+  p.WoT = (const bf16_t *)WoT;
+  p.bo = bo;
+  p.y_bits = y_bits;
+  p.dZ = (bf16_t *)dZ;
+  p.gW = gW;
+  p.gb = gb;
+  p.loss_partials = loss_partials;
+  p.loss_out = loss_out;
+  p.ticket = ticket;
+  p.loss_scale = loss_scale;
+  p.scale = 1.0f / ((float)B * (float)V);
+  p.V = V;
+  p.ldt = ldt;
+  const dim3 grid((unsigned)cdiv(V, NB)), block(NTH);
+  hipStream_t s = as_stream(stream);
+#define DO_LAUNCH(DD, BBB) \
+  if (d == DD && B == BBB) hipLaunchKernelGGL((dec_bce_dw_kernel<DD, BBB>), grid, block, 0, s, p);
+  DO_LAUNCH(256, 512) DO_LAUNCH(256, 256) DO_LAUNCH(256, 128)
+  DO_LAUNCH(128, 512) DO_LAUNCH(128, 256) DO_LAUNCH(128, 128)
+#undef DO_LAUNCH
+  CC_LAUNCH_CHECK("dec_bce_dw_kernel");
+  return CC_OK;
+}
+
+extern "C" int32_t cc_dec_bce_dw_blocks(int32_t V) { return (int32_t)cdiv(V, NB); }

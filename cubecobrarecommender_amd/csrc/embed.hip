@@ -204,6 +204,108 @@ __global__ __launch_bounds__(64 * SGW) void scatter_bwd_kernel(const float *__re
   }
 }
 
+// Backward on bf16 MFMA (cc_embed_grad_mfma): dW1 = X^T dPre1 as a dense [V, R] x [R, d] product
+// whose A operand is the transposed x bitmask itself — each lane's 8-k A fragment is one byte of
+// the row's bit words expanded to bf16 0/1 in registers (exact), B = dPre1^T bf16 [d][RP] (written
+// by the tower backward chain).  Every row costs the same (no Zipf-heavy row latency chain, no
+// per-row dispatch); row V (with bias_grad) is the all-ones row: db1 = colsum dPre1.  A block owns
+// EG_ROWS rows of W1 and all d columns, so it also clears the bit words it consumed.
+constexpr int EG_ROWS = 64, EG_BK = 64, EG_XWMAX = 32;  // R <= 1024
+
+typedef __attribute__((ext_vector_type(4))) uint32_t eg_u32x4;  // ext vectors stay in VGPRs
+__device__ __forceinline__ bf16x8_t expand_bits8(uint32_t b) {
+  eg_u32x4 w;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = (((b >> (2 * i)) & 1u) * 0x3F80u) | (((b >> (2 * i + 1)) & 1u) * 0x3F800000u);
+  return __builtin_bit_cast(bf16x8_t, w);
+}
+
+template <int NC>
+__global__ __launch_bounds__(256, 2) void embed_grad_mfma_kernel(const bf16_t *__restrict__ gT, int V,
+                                                                int d, int R, int RP, uint32_t *xt,
+                                                                float *__restrict__ grad,
+                                                                float *__restrict__ bias_grad) {
+  constexpr int CH = EG_BK / 8;                 // 16-B chunks per B row per K-tile
+  constexpr int NCH = NC * CH / 256;            // chunks staged per thread
+  constexpr int NJ = NC / 64;                   // 32-col accumulators per wave (2 x 2 waves)
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][NC * EG_BK];
+  __shared__ uint32_t As[EG_ROWS][EG_XWMAX + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, half = lane >> 5;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int v0 = blockIdx.x * EG_ROWS;
+  const int XW = (R + 31) >> 5, XWP = RP >> 5;
+  for (int i = tid; i < EG_ROWS * XWP; i += 256) {
+    const int r = i / XWP, w = i % XWP, v = v0 + r;
+    uint32_t m = 0u;
+    if (w < XW) {
+      if (v < V) {
+        uint32_t *src = xt + (int64_t)v * XW + w;
+        m = *src;
+        *src = 0u;  // consumed: the next step's F finds xt zeroed
+      } else if (v == V && bias_grad) {
+        m = (w == XW - 1 && (R & 31)) ? (1u << (R & 31)) - 1u : 0xFFFFFFFFu;
+      }
+    }
+    As[r][w] = m;
+  }
+  const int nk = RP / EG_BK;
+  const int arow = wm * 32 + (lane & 31);
+  for (int nc0 = 0; nc0 < d; nc0 += NC) {
+    f32x16_t acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    eg_u32x4 st[NCH];
+#define EG_LOAD(KT)                                                                                   \
+  _Pragma("unroll") for (int q = 0; q < NCH; ++q) {                                                   \
+    const int c = tid + 256 * q, n = c / CH, ch = c % CH;                                             \
+    st[q] = *reinterpret_cast<const eg_u32x4 *>(gT + (int64_t)(nc0 + n) * RP + (KT) * EG_BK + ch * 8); \
+  }
+#define EG_STORE(BUF)                                                                          \
+  _Pragma("unroll") for (int q = 0; q < NCH; ++q) {                                            \
+    const int c = tid + 256 * q, n = c / CH, ch = c % CH;                                      \
+    *reinterpret_cast<eg_u32x4 *>(&Bs[BUF][n * EG_BK + ((ch ^ (n & (CH - 1))) * 8)]) = st[q];     \
+  }
+    EG_LOAD(0)
+    __syncthreads();  // As visible; previous chunk's readers of Bs are done
+    EG_STORE(0)
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) { EG_LOAD(kt + 1) }
+      const bf16_t *bs = Bs[kt & 1];
+#pragma unroll
+      for (int kk = 0; kk < EG_BK / 16; ++kk) {
+        const int k = kt * EG_BK + kk * 16 + 8 * half;
+        const bf16x8_t a = expand_bits8((As[arow][k >> 5] >> (k & 31)) & 0xFFu);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int n = wn * (NC / 2) + j * 32 + (lane & 31);
+          const bf16x8_t b = *reinterpret_cast<const bf16x8_t *>(bs + n * EG_BK + (((2 * kk + half) ^ (n & (CH - 1))) * 8));
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[j], 0, 0, 0);
+        }
+      }
+      if (kt + 1 < nk) { EG_STORE((kt + 1) & 1) }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = nc0 + wn * (NC / 2) + j * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int v = v0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        if (v < V)
+          grad[(int64_t)v * d + col] = acc[j][r];
+        else if (v == V && bias_grad)
+          bias_grad[col] = acc[j][r];
+      }
+    }
+  }
+#undef EG_LOAD
+#undef EG_STORE
+}
+
 }  // namespace
 
 extern "C" int cc_embed_gather_fwd(int32_t dtype, const void *table, const float *bias, int32_t V,
@@ -278,5 +380,25 @@ extern "C" int cc_embed_scatter_bwd(const float *dpre, int32_t V, int32_t d, int
     default: return cc::fail(CC_ERR_UNSUPPORTED, "cc_embed_scatter_bwd: d/64 must be a power of two");
   }
   CC_LAUNCH_CHECK("scatter_bwd_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_embed_grad_mfma(const void *dpre_t, int32_t V, int32_t d, int32_t R, int32_t ld_t,
+                                  uint32_t *xt_bits, float *grad, float *bias_grad, void *stream) {
+  CC_REQUIRE(dpre_t && xt_bits && grad, "cc_embed_grad_mfma: null pointer");
+  CC_REQUIRE(d % 128 == 0 && d >= 128 && d <= 1024, "cc_embed_grad_mfma: d must be 128..1024, %128");
+  CC_REQUIRE(R > 0 && R <= 32 * EG_XWMAX, "cc_embed_grad_mfma: R must be 1..1024");
+  CC_REQUIRE(ld_t % EG_BK == 0 && ld_t >= R && ((uintptr_t)dpre_t % 16) == 0,
+             "cc_embed_grad_mfma: ld_t must be a multiple of 64 covering R (zero padded), 16-B aligned");
+  const int rows = bias_grad ? V + 1 : V;
+  const dim3 grid((unsigned)cdiv(rows, EG_ROWS)), block(256);
+  hipStream_t s = as_stream(stream);
+  if (d % 256 == 0)
+    hipLaunchKernelGGL((embed_grad_mfma_kernel<256>), grid, block, 0, s, (const bf16_t *)dpre_t, V, d, R,
+                       ld_t, xt_bits, grad, bias_grad);
+  else
+    hipLaunchKernelGGL((embed_grad_mfma_kernel<128>), grid, block, 0, s, (const bf16_t *)dpre_t, V, d, R,
+                       ld_t, xt_bits, grad, bias_grad);
+  CC_LAUNCH_CHECK("embed_grad_mfma_kernel");
   return CC_OK;
 }

@@ -29,6 +29,7 @@ struct TowerP {
   const void *gD3;
   void *gact[5];
   float *gpre1;
+  void *gpre1t;  // optional bf16 dPre1^T [d][ceil64(R)]
   float *slab;
   int64_t slab_elems;
   float *gw[9];
@@ -72,6 +73,14 @@ template <> struct TMma<float> {
 };
 
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// dPre1^T [d][ceil64(R)] (bf16): accumulator registers 4g..4g+3 hold 4 consecutive rows of column
+// col, stored as one 8-byte word per g
+__device__ __forceinline__ void gpre1t_store(const TowerP &p, int col, int r0, int lane, const bf16_t (&tt)[16]) {
+  bf16_t *dt = reinterpret_cast<bf16_t *>(p.gpre1t) + (int64_t)col * ((p.R + 63) & ~63) + r0 + 4 * (lane >> 5);
+#pragma unroll
+  for (int g = 0; g < 4; ++g) *reinterpret_cast<uint2 *>(dt + 8 * g) = *reinterpret_cast<const uint2 *>(&tt[4 * g]);
+}
 
 // C tile (32 rows x 32 cols starting at column n0) = A[32][K] (LDS row-major, lda) . Bt[n][K]
 // (global, row n0+(lane&31) of a [N][K] k-contiguous matrix).  Loads for UB k-steps are issued
@@ -265,6 +274,10 @@ __global__ __launch_bounds__(NT) void tower_bwd_chain_kernel(TowerP p) {
         const float v = h > 0.f ? accs[q][r] : 0.f;
         if (i == 0) {
           p.gpre1[go] = v;
+          if constexpr (sizeof(T) == 2) {
+            if (p.gpre1t)
+              reinterpret_cast<bf16_t *>(p.gpre1t)[(int64_t)col * ((p.R + 63) & ~63) + r0 + row] = f2bf(v);
+          }
         } else {
           T tv;
           DT<T>::st(&tv, v);
@@ -408,6 +421,7 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
     __syncthreads();  // every wave has finished reading Gr
     if (t < K / 32) {
       bf16_t *gout = i > 0 ? reinterpret_cast<bf16_t *>(p.gact[i - 1]) : nullptr;
+      bf16_t tt[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = acc_row(r, lane);
@@ -415,12 +429,14 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
         const float v = bf2f(hm[r]) > 0.f ? acc[r] : 0.f;
         if (i == 0) {
           p.gpre1[go] = v;
+          tt[r] = f2bf(v);
         } else {
           const bf16_t tv = f2bf(v);
           Gr[row * ldx + col] = tv;
           gout[go] = tv;
         }
       }
+      if (i == 0 && p.gpre1t) gpre1t_store(p, col, r0, lane, tt);
     }
     __syncthreads();
   }
@@ -637,6 +653,7 @@ int make_params(const cc_tower_args *t, TowerP &p) {
   p.gD3 = t->gD3;
   for (int a = 0; a < 5; ++a) p.gact[a] = t->gact[a];
   p.gpre1 = t->gpre1;
+  p.gpre1t = t->dtype == CC_BF16 ? t->gpre1t : nullptr;
   p.slab = t->slab;
   p.slab_elems = slab_off(t->d, 6);
   return CC_OK;

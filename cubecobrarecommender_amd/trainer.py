@@ -215,6 +215,15 @@ class Trainer:
         self.loss_dev = torch.zeros(2, device=self.dev, dtype=torch.float64)
         # fused 32-row-block towers (tower.hip) when the widths fit; generic GEMMs otherwise
         self.fused_tower = cfg.fused_tower and (B % 32 == 0) and d <= (1024 if self.dtype == L.CC_BF16 else 256)
+        # bf16 path: the W1 gradient on MFMA (cc_embed_grad_mfma) from dPre1^T bf16 [d][RP]
+        # written by the tower backward chain (columns R..RP-1 stay zero)
+        self.embed_mfma = (self.dtype == L.CC_BF16 and self.fused_tower and d % 128 == 0 and R <= 1024
+                           and os.environ.get('CCREC_EMBED_MFMA', '1') != '0')
+        self.RP = (R + 63) // 64 * 64
+        # D1 output layer fused (logits + BCE + dZ + dWo, csrc/decout.hip) where its shape fits
+        self.fused_out = (self.dtype == L.CC_BF16 and self.fused_tower and not self.mx8 and d in (128, 256)
+                          and B in (128, 256, 512) and os.environ.get('CCREC_DEC_FUSED', '1') != '0')
+        self.gPre1T = torch.zeros(d, self.RP, **T) if self.embed_mfma else None
         if self.mx8 and not self.fused_tower:
             raise ValueError('fp8 needs the fused towers (fused_tower=True, B % 32 == 0)')
         if self.fused_tower:
@@ -337,6 +346,7 @@ class Trainer:
         for a, buf in enumerate((self.gH2, self.gH3, self.gZl, self.gD1, self.gD2)):
             t.gact[a] = buf.data_ptr()      # dPre of e2, e3, e4, d1, d2
         t.gpre1 = self.gPre1.data_ptr()
+        t.gpre1t = self.gPre1T.data_ptr() if self.gPre1T is not None else None
         t.slab = self.slab.data_ptr()
         return t
 
@@ -508,7 +518,12 @@ class Trainer:
             L.call('cc_quant_mx8', L.CC_BF16, L.ptr(self.D3), R, d, d, 1, L.ptr(self.D3tq), R,
                    L.ptr(self.D3tqs), None, s)
         t = self._tick('dec_bce_fwd')
-        if self.fused_tower:   # Wo^T [V][d]: k-contiguous B operand; also writes dZ^T [V][B]
+        if self.fused_out:     # logits + BCE + dZ + dWo/dbo in one pass (csrc/decout.hip)
+            L.call('cc_dec_bce_dw', L.ptr(self.D3), L.ptr(self.D3t), R, L.ptr(self.WoT[0]),
+                   self.pf('decoder/reconstruct/bias'), B, d, V, L.ptr(self.y_bits), L.ptr(self.dZout),
+                   self.gp('decoder/reconstruct/kernel'), self.gp('decoder/reconstruct/bias'),
+                   L.ptr(self.bce_part), L.ptr(self.loss_dev), 1.0 / (B * V), L.ptr(self.tickets), s)
+        elif self.fused_tower:   # Wo^T [V][d]: k-contiguous B operand; also writes dZ^T [V][B]
             self._gemm(B, V, d, **self._dec_fwd(0, 0), tb=1,
                        epi=L.CC_EPI_BCE, bias=self.pf('decoder/reconstruct/bias'), C=L.ptr(self.dZout),
                        y_bits=L.ptr(self.y_bits), scale=1.0 / (B * V), partials=L.ptr(self.bce_part),
@@ -555,6 +570,13 @@ class Trainer:
                 gx = self._gemm(B, d, self.Vp if self.mx8 else V, **self._dec_dx(k, r0, pre), ta=0, tb=1,
                                 epi=L.CC_EPI_SPLITK, Cf=L.ptr(self.split_buf), splits=self.splits,
                                 launch=False)
+                if k == 0 and self.fused_out:   # dWo/dbo came out of cc_dec_bce_dw: dX only
+                    t = self._tick('dec_dX')
+                    L.call('cc_gemm', L.C.byref(gx), s)
+                    t()
+                    L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), self.splits, B, d,
+                           L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
+                    continue
                 gw = self._gemm(d, V, B, **self._dec_dw(k, r0), ta=0, tb=1,
                                 Cf=self.gp(pre + '/reconstruct/kernel'),
                                 colsum=None if self.mx8 else self.gp(pre + '/reconstruct/bias'), launch=False)
@@ -631,8 +653,12 @@ class Trainer:
             self._dense_bwd(self.H2, self.gH3, (0, R), 256, 128, 'encoder/encoded_3', gIn=self.gH2, mask=self.H2)
             self._dense_bwd(self.H1, self.gH2, (0, R), d, 256, 'encoder/encoded_2', gIn_f32=self.gPre1, mask=self.H1)
         t = self._tick('cc_embed_scatter_bwd')
-        L.call('cc_embed_scatter_bwd', L.ptr(self.gPre1), V, d, R, L.ptr(self.xt_bits),
-               self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
+        if self.embed_mfma:
+            L.call('cc_embed_grad_mfma', L.ptr(self.gPre1T), V, d, R, self.RP, L.ptr(self.xt_bits),
+                   self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
+        else:
+            L.call('cc_embed_scatter_bwd', L.ptr(self.gPre1), V, d, R, L.ptr(self.xt_bits),
+                   self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
         t()
         if self.fused_tower:
             self._join()

@@ -127,6 +127,12 @@ int cc_embed_gather_fwd(int32_t dtype, const void *table, const float *bias, int
  * ---------------------------------------------------------------------------------- */
 int cc_embed_scatter_bwd(const float *dpre, int32_t V, int32_t d, int32_t R,
                          const uint32_t *xt_bits, float *grad, float *bias_grad, void *stream);
+/* The same gradient on bf16 MFMA (the bf16/fp8 training path): dW1 = X^T dPre1 with the x^T
+ * bitmask expanded to 0/1 bf16 A fragments in registers and dpre_t = dPre1^T bf16 [d][ld_t]
+ * (ld_t % 64 == 0, columns R..ld_t-1 zero; cc_tower_args.gpre1t).  d % 128 == 0, R <= 1024.
+ * Consumes (zeroes) xt_bits like cc_embed_scatter_bwd; deterministic. */
+int cc_embed_grad_mfma(const void *dpre_t, int32_t V, int32_t d, int32_t R, int32_t ld_t,
+                       uint32_t *xt_bits, float *grad, float *bias_grad, void *stream);
 
 /* ----------------------------------------------------------------------------------
  * Generic MFMA GEMM with fused epilogues — the Dense layers of the E/D towers and the
@@ -228,6 +234,7 @@ typedef struct cc_tower_args {
   float *slab;           /* [R/32, cc_tower_slab_elems(d)] fp32 */
   float *gw[9];          /* reduce outputs: kernel grads [K][N] */
   float *gb[9];          /* bias grads [N] */
+  void *gpre1t;          /* optional (bf16): dPre1^T [d][ceil64(R)] for cc_embed_grad_mfma */
 } cc_tower_args;
 int64_t cc_tower_slab_elems(int32_t d);
 int cc_tower_fwd(const cc_tower_args *t, void *stream);
@@ -254,6 +261,17 @@ int cc_tower_transpose_advance(const cc_tower_args *t, int64_t *state, int64_t b
 int cc_dec_bce_fused(int32_t dtype, const void *H3, const void *Wo, const float *bo,
                      int32_t B, int32_t d, int32_t V, const uint32_t *y_bits, void *dZ,
                      double *loss_partials, int32_t *n_partials, void *stream);
+/* D1 output layer in one pass (bf16; B in {128, 256, 512}, d in {128, 256}): per 96-column
+ * slice of V, logits z = D3 Wo + bo (Wo as Wo^T [V][d]), dZ = (sigmoid(z) - y)/(B*V) written
+ * row-major [B][V] (for the dX product), and dWo [d][V] = D3^T dZ (D3t = D3^T [d][ldt]) and
+ * dbo = colsum dZ from the block's LDS copy of dZ^T — no dZ^T in HBM, no separate dW launch.
+ * loss_partials: cc_dec_bce_dw_blocks(V) doubles; loss_out (optional, with ticket) =
+ * sum(partials) * loss_scale reduced by the last block. */
+int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const void *WoT, const float *bo,
+                  int32_t B, int32_t d, int32_t V, const uint32_t *y_bits, void *dZ, float *gW,
+                  float *gb, double *loss_partials, double *loss_out, double loss_scale,
+                  uint32_t *ticket, void *stream);
+int32_t cc_dec_bce_dw_blocks(int32_t V);
 int cc_dec_softmax_kl_fused(int32_t dtype, const float *Z2, int32_t B, int32_t V,
                             const float *y_reg, const int32_t *reg_idx, float reg, void *dZ,
                             double *kl_partials, void *stream);

@@ -156,7 +156,10 @@ def train_forward_backward(P, x_lists, y_lists, V, d, reg=0.0, reg_idx=None, y_r
         grads[names[li] + '/kernel'] += acts[li - 1].T @ dpre
         grads[names[li] + '/bias'] += dpre.sum(0)
         dh = dpre @ W[names[li] + '/kernel'].T
-    dpre1 = dh * (acts[0] > 0)          # fp32 on the GPU (feeds the row-scatter, not a GEMM)
+    # fp32 on the GPU's fp32 path (exact row-scatter); the bf16 path's W1 gradient is a bf16
+    # MFMA product (cc_embed_grad_mfma) whose B operand is dPre1 rounded to bf16, as for every
+    # other Dense layer's dW
+    dpre1 = rq(dh * (acts[0] > 0))
     grads['encoder/encoded_1/kernel'] += np.asarray(Xs.T @ dpre1)
     grads['encoder/encoded_1/bias'] += dpre1.sum(0)
     return losses, grads

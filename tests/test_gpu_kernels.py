@@ -325,3 +325,112 @@ def test_softmax_kl_rows(V, dtype):
     kl, dz = _softmax_kl_ref(Z, Mt[ridx], reg, B)
     np.testing.assert_allclose(part.cpu().numpy(), kl, rtol=1e-4)
     assert rel_err(dZ.float().cpu().numpy(), dz) < (1e-5 if dtype == 'fp32' else 4e-3)
+
+
+@pytest.mark.parametrize('V,R,d,heavy', [(3000, 512, 256, True), (1000, 96, 128, False),
+                                         (777, 1024, 512, True), (64, 40, 256, False)])
+def test_embed_grad_mfma(V, R, d, heavy):
+    """cc_embed_grad_mfma: dW1 = X^T dPre1 on bf16 MFMA with the x^T bitmask as the A operand.
+    Against the fp64 product of the bits and the bf16-rounded dPre1 (the only rounding), the bias
+    row (all-ones) = colsum, bit words zeroed after the call, R not a multiple of 64."""
+    rng = np.random.default_rng(V + R + d)
+    XW = (R + 31) // 32
+    RP = (R + 63) // 64 * 64
+    p = np.full(V, 0.02)
+    if heavy:
+        p[:8] = 0.97      # Zipf-heavy rows: a bit for nearly every batch row
+    X = rng.random((R, V)) < p
+    xt = np.zeros((V, XW), np.uint32)
+    for r in range(R):
+        cols = np.nonzero(X[r])[0]
+        xt[cols, r // 32] |= np.uint32(1 << (r % 32))
+    dpre = rng.standard_normal((R, d)).astype(np.float32)
+    dT = torch.zeros(d, RP, dtype=torch.bfloat16)
+    dT[:, :R] = torch.from_numpy(dpre.T.copy()).to(torch.bfloat16)
+    dTd = dT.cuda()                                # columns R..RP-1 zero (the contract)
+    xtd = torch.from_numpy(xt.view(np.int32)).cuda()
+    grad = torch.full((V, d), 7.0, device='cuda')
+    bgrad = torch.full((d,), 7.0, device='cuda')
+    L.call('cc_embed_grad_mfma', L.ptr(dTd), V, d, R, RP, L.ptr(xtd), L.ptr(grad), L.ptr(bgrad),
+           L.stream_ptr())
+    torch.cuda.synchronize()
+    dq = dT[:, :R].double().numpy().T            # bf16-rounded dPre1 [R, d]
+    want = X.T.astype(np.float64) @ dq
+    got = grad.cpu().numpy()
+    assert rel_err(got, want) < 1e-6
+    assert np.all(got[~X.any(0)] == 0.0)           # rows absent from the batch: exact zero
+    assert rel_err(bgrad.cpu().numpy(), dq.sum(0)) < 1e-6
+    assert int(xtd.abs().sum()) == 0               # consumed
+    # no bias row
+    xtd = torch.from_numpy(xt.view(np.int32)).cuda()
+    grad2 = torch.zeros(V, d, device='cuda')
+    L.call('cc_embed_grad_mfma', L.ptr(dTd), V, d, R, RP, L.ptr(xtd), L.ptr(grad2), None, L.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(grad2, grad)
+
+
+def _nt_gemm(M, N, K, A, lda, Bm, ldb, epi, **kw):
+    g = L.GemmArgs()
+    g.dtype, g.ta, g.tb, g.epilogue = L.CC_BF16, 0, 1, epi
+    g.M, g.N, g.K, g.lda, g.ldb, g.ldc, g.splits, g.relu = M, N, K, lda, ldb, kw.get('ldc', N), 1, 0
+    g.A, g.B = A.data_ptr(), Bm.data_ptr()
+    for k in ('bias', 'C', 'Cf', 'y_bits', 'loss_partials', 'colsum', 'Ct'):
+        v = kw.get(k)
+        setattr(g, k, v.data_ptr() if v is not None else None)
+    g.scale = kw.get('scale', 1.0)
+    g.ldct = kw.get('ldct', 0)
+    L.call('cc_gemm', ctypes.byref(g), L.stream_ptr())
+
+
+@pytest.mark.parametrize('B,d,V', [(512, 256, 2500), (128, 128, 700), (256, 256, 64)])
+def test_dec_bce_dw_matches_unfused(B, d, V):
+    """cc_dec_bce_dw (logits + BCE + dZ + dWo/dbo in one pass) vs the unfused NT-GEMM path (BCE
+    epilogue writing dZ and dZ^T, then dW = D3^T dZ^T with the colsum bias gradient): dZ and dWo
+    bitwise (same MFMA k order), dbo and the loss within fp32 summation-order error; the fp64
+    oracle of the same bf16 operands bounds both."""
+    torch.manual_seed(B + d + V)
+    bf = dict(device='cuda', dtype=torch.bfloat16)
+    D3 = (torch.randn(B, d, device='cuda') * 0.5).to(torch.bfloat16)
+    D3t = D3.t().contiguous()
+    WoT = (torch.randn(V, d, device='cuda') * 0.1).to(torch.bfloat16)
+    bo = torch.randn(V, device='cuda') * 0.1
+    VW = (V + 31) // 32
+    ybits = torch.randint(-2**31, 2**31 - 1, (B, VW), device='cuda', dtype=torch.int32)
+    scale = 1.0 / (B * V)
+    # fused
+    dZ = torch.zeros(B, V, **bf)
+    gW = torch.full((d, V), 7.0, device='cuda')
+    gb = torch.full((V,), 7.0, device='cuda')
+    nblk = L.lib().cc_dec_bce_dw_blocks(V)
+    part = torch.zeros(nblk, device='cuda', dtype=torch.float64)
+    loss = torch.zeros(1, device='cuda', dtype=torch.float64)
+    tick = torch.zeros(1, device='cuda', dtype=torch.int32)
+    L.call('cc_dec_bce_dw', L.ptr(D3), L.ptr(D3t), B, L.ptr(WoT), L.ptr(bo), B, d, V, L.ptr(ybits),
+           L.ptr(dZ), L.ptr(gW), L.ptr(gb), L.ptr(part), L.ptr(loss), scale, L.ptr(tick), L.stream_ptr())
+    # unfused
+    dZ2 = torch.zeros(B, V, **bf)
+    dZt = torch.zeros(V, B, **bf)
+    part2 = torch.zeros(4096, device='cuda', dtype=torch.float64)
+    _nt_gemm(B, V, d, D3, d, WoT, d, L.CC_EPI_BCE, bias=bo, C=dZ2, y_bits=ybits, loss_partials=part2,
+             scale=scale, Ct=dZt, ldct=B)
+    gW2 = torch.zeros(d, V, device='cuda')
+    gb2 = torch.zeros(V, device='cuda')
+    _nt_gemm(d, V, B, D3t, B, dZt, B, L.CC_EPI_STORE, Cf=gW2, colsum=gb2)
+    torch.cuda.synchronize()
+    # both round dz to bf16 (the fused kernel forms (sigmoid - y) * scale with one fma): equal up
+    # to a bf16 ulp, and the products built on them agree to that level
+    assert rel_err(dZ.float().cpu().numpy(), dZ2.float().cpu().numpy()) < 4e-3
+    assert rel_err(gW.cpu().numpy(), gW2.cpu().numpy()) < 4e-3
+    assert rel_err(gb.cpu().numpy(), gb2.cpu().numpy()) < 4e-3
+    assert int(tick.item()) == 0
+    # fp64 references of dZ (to bf16 rounding), dWo / dbo on the kernel's own rounded dZ, the loss
+    y = np.unpackbits(ybits.cpu().numpy().view(np.uint8), axis=1, bitorder='little')[:, :V].astype(np.float64)
+    z = D3.double().cpu().numpy() @ WoT.double().cpu().numpy().T + bo.double().cpu().numpy()
+    dz_ref = (1.0 / (1.0 + np.exp(-z)) - y) * scale
+    dzk = dZ.double().cpu().numpy()
+    assert np.max(np.abs(dzk - dz_ref) / np.maximum(np.abs(dz_ref), 1e-30)) < 2 ** -8 + 1e-5
+    assert rel_err(gW.cpu().numpy(), D3.double().cpu().numpy().T @ dzk) < 1e-5
+    assert rel_err(gb.cpu().numpy(), dzk.sum(0)) < 1e-5
+    want = (np.maximum(z, 0) - z * y + np.log1p(np.exp(-np.abs(z)))).mean()
+    assert abs(loss.item() - want) < 1e-5 * abs(want)
+    assert abs(part.sum().item() * scale - want) < 1e-5 * abs(want)
