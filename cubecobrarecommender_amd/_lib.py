@@ -54,6 +54,7 @@ class TowerArgs(C.Structure):
         ('act6t', C.c_void_p),
         ('gD3', C.c_void_p), ('gact', C.c_void_p * 5), ('gpre1', C.c_void_p), ('slab', C.c_void_p),
         ('gw', C.c_void_p * 9), ('gb', C.c_void_p * 9), ('gpre1t', C.c_void_p),
+        ('wpf', C.c_void_p * 9), ('wpb', C.c_void_p * 9), ('act6p', C.c_void_p), ('act6tp', C.c_void_p),
     ]
 
 
@@ -77,7 +78,7 @@ SIGNATURES = {
     'cc_transpose': (C.c_int, [_I32, _P, _I32, _I32, _P, _P]),
     'cc_quant_mx8': (C.c_int, [_I32, _P, _I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P]),
     'cc_dec_bce_fused': (C.c_int, [_I32, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
-    'cc_dec_bce_dw': (C.c_int, [_P, _P, _I32, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _F64, _P, _P]),
+    'cc_dec_bce_dw': (C.c_int, [_P, _P, _I32, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _F64, _P, _P]),
     'cc_dec_bce_dw_blocks': (_I32, [_I32]),
     'cc_dec_softmax_kl_fused': (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _F32, _P, _P, _P]),
     'cc_reduce_loss': (C.c_int, [_P, _I32, _F64, _P, _P]),

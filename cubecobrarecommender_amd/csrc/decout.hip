@@ -33,6 +33,8 @@ typedef __attribute__((ext_vector_type(4))) uint32_t v4u;  // staging registers 
 struct DecOutP {
   const bf16_t *D3;        // [B][d]
   const bf16_t *D3t;       // [d][ldt]
+  const bf16_t *D3p;       // optional packed A images (cc_tower_args.act6p / act6tp; ldt rows)
+  const bf16_t *D3tp;
   const bf16_t *WoT;       // [V][d]
   const float *bo;         // [V]
   const uint32_t *y_bits;  // [B][ceil(V/32)]
@@ -123,10 +125,17 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   }
   bf16x8_t af[2][nkk];
   auto load_a = [&](bf16x8_t (&dst)[nkk], int pass) {
-    const int row = min(pass * 256 + w * 32 + (lane & 31), B - 1);
-    const bf16_t *src = p.D3 + (int64_t)row * d + 8 * half;
+    if (p.D3p) {  // fragment (row block, kk) = 1 KB contiguous: whole cache lines per wave load
+      const int rb = min(pass * 8 + w, B / 32 - 1);
+      const bf16_t *src = p.D3p + ((int64_t)rb * nkk * 64 + lane) * 8;
 #pragma unroll
-    for (int kk = 0; kk < nkk; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 16);
+      for (int kk = 0; kk < nkk; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 512);
+    } else {
+      const int row = min(pass * 256 + w * 32 + (lane & 31), B - 1);
+      const bf16_t *src = p.D3 + (int64_t)row * d + 8 * half;
+#pragma unroll
+      for (int kk = 0; kk < nkk; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 16);
+    }
     // keep the whole batch in flight: without this fence the scheduler sinks each load to its
     // MFMA and the pass becomes a chain of dependent L2 round trips
     __builtin_amdgcn_sched_barrier(0);
@@ -226,13 +235,19 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   if (w * 32 < d) {
     constexpr int P2D = 4;
     constexpr int nk2 = B / BK;
-    const bf16_t *arow = p.D3t + (int64_t)(w * 32 + (lane & 31)) * p.ldt + 8 * half;
+    // A fragment (kc, kk): row-strided from D3^T, or 1 KB contiguous from the packed image
+    const bool pk = p.D3tp != nullptr;
+    const bf16_t *arow = pk ? p.D3tp + ((int64_t)w * (p.ldt / 16) * 64 + lane) * 8
+                            : p.D3t + (int64_t)(w * 32 + (lane & 31)) * p.ldt + 8 * half;
+    auto afrag = [&](int kc, int kk) {
+      return *reinterpret_cast<const bf16x8_t *>(arow + (pk ? (kc * 4 + kk) * 512 : kc * BK + kk * 16));
+    };
     bf16x8_t ring[P2D][4];
 #pragma unroll
     for (int q = 0; q < P2D; ++q)
       if (q < nk2)
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) ring[q][kk] = *reinterpret_cast<const bf16x8_t *>(arow + q * BK + kk * 16);
+        for (int kk = 0; kk < 4; ++kk) ring[q][kk] = afrag(q, kk);
     __builtin_amdgcn_sched_barrier(0);
     f32x16_t acc2[NJ];
 #pragma unroll
@@ -252,8 +267,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
       }
       if (kc + P2D < nk2) {
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-          ring[q][kk] = *reinterpret_cast<const bf16x8_t *>(arow + (kc + P2D) * BK + kk * 16);
+        for (int kk = 0; kk < 4; ++kk) ring[q][kk] = afrag(kc + P2D, kk);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -291,7 +305,8 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 
 }  // namespace
 
-extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const void *WoT,
+extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const void *D3p,
+                             const void *D3tp, const void *WoT,
                              const float *bo, int32_t B, int32_t d, int32_t V, const uint32_t *y_bits,
                              void *dZ, float *gW, float *gb, double *loss_partials, double *loss_out,
                              double loss_scale, uint32_t *ticket, void *stream) {
@@ -305,6 +320,10 @@ extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const
   DecOutP p;
   p.D3 = (const bf16_t *)D3;
   p.D3t = (const bf16_t *)D3t;
+  p.D3p = (const bf16_t *)D3p;
+  p.D3tp = (const bf16_t *)D3tp;
+  CC_REQUIRE(!D3tp || ldt % 16 == 0, "cc_dec_bce_dw: packed D3^T needs ldt % 16 == 0");
+  CC_REQUIRE((((uintptr_t)D3p | (uintptr_t)D3tp) & 15) == 0, "cc_dec_bce_dw: packed images 16-B aligned");
   p.WoT = (const bf16_t *)WoT;
   p.bo = bo;
   p.y_bits = y_bits;

@@ -14,6 +14,11 @@
 
 #include "common.hpp"
 
+// dev-only timing hook (tools/micro/tower_probe.hip defines it); compiled out of the library
+#ifndef TOWER_PROBE
+#define TOWER_PROBE(k)
+#endif
+
 namespace {
 
 constexpr int RB = 32;   // rows per block
@@ -34,13 +39,16 @@ struct TowerP {
   int64_t slab_elems;
   float *gw[9];
   float *gb[9];
+  const bf16_t *wpf[9];  // fragment-packed forward / backward weight images (cc_tower_args)
+  const bf16_t *wpb[9];
+  bf16_t *act6p, *act6tp;  // packed D3 operand images for cc_dec_bce_dw (fast forward only)
+  bool packed;
 };
 
 __host__ __device__ inline void chain_dims(int d, int i, int &K, int &N) {
-  const int Ks[6] = {d, 256, 128, 64, 128, 256};
-  const int Ns[6] = {256, 128, 64, 128, 256, d};
-  K = Ks[i];
-  N = Ns[i];
+  // K: d, 256, 128, 64, 128, 256;  N: 256, 128, 64, 128, 256, d  (no arrays: no scratch)
+  K = i == 0 ? d : i == 1 ? 256 : i == 2 ? 128 : i == 3 ? 64 : i == 4 ? 128 : 256;
+  N = i == 0 ? 256 : i == 1 ? 128 : i == 2 ? 64 : i == 3 ? 128 : i == 4 ? 256 : d;
 }
 __host__ __device__ inline int64_t slab_off(int d, int i) {  // chain layer i (0..5): kernel, bias
   int64_t o = 0;
@@ -309,6 +317,45 @@ __device__ __forceinline__ void issue_frags(Frags &F, const bf16_t *__restrict__
   for (int j = 0; j < FB; ++j)
     if (16 * j < K) F.f[j] = *reinterpret_cast<const bf16x8_t *>(row + 16 * j);
 }
+// the same fragments from a fragment-packed image (cc_tower_args.wpf / wpb): fragment (t, j) is
+// 64 lanes x 16 B contiguous, so each wave load reads 8 whole cache lines (the row-strided form
+// touches 32 lines per load and refetches each line once per 16-k step)
+__device__ __forceinline__ void issue_frags_packed(Frags &F, const bf16_t *__restrict__ P, int red, int t) {
+  const int lane = threadIdx.x & 63;
+  const bf16_t *base = P + ((int64_t)t * (red / 16) * 64 + lane) * 8;
+#pragma unroll
+  for (int j = 0; j < FB; ++j)
+    if (16 * j < red) F.f[j] = *reinterpret_cast<const bf16x8_t *>(base + j * 512);
+}
+// packed-image element offset of fragment (t, j), lane, element e
+__device__ __forceinline__ int64_t pack_off(int t, int j, int lane, int red) {
+  return (((int64_t)t * (red / 16) + j) * 64 + lane) * 8;
+}
+
+// 32 rows x W (bf16, W <= 256) of a [R][W] activation into registers: issue now, store to LDS later
+typedef __attribute__((ext_vector_type(4))) uint32_t u32v4;  // staging registers (HIP's uint4
+                                                              // struct would be spilled to scratch)
+struct RowRegs {
+  u32v4 v[2];
+};
+__device__ __forceinline__ void rows_issue(RowRegs &Rg, const bf16_t *__restrict__ g, int W, int r0) {
+  const int per = W / 8, nv = RB * per;
+  const u32v4 *src = reinterpret_cast<const u32v4 *>(g + (int64_t)r0 * W);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = (int)threadIdx.x + u * FNT;
+    if (i < nv) Rg.v[u] = src[i];
+  }
+}
+__device__ __forceinline__ void rows_store(const RowRegs &Rg, int W, bf16_t *Xr, int ldx) {
+  const int per = W / 8, nv = RB * per;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = (int)threadIdx.x + u * FNT;
+    if (i < nv) *reinterpret_cast<u32v4 *>(Xr + (i / per) * ldx + (i % per) * 8) = Rg.v[u];
+  }
+}
+
 __device__ __forceinline__ void consume_frags(const Frags &F, const bf16_t *A, int lda, int K,
                                               f32x16_t &acc) {
   const int lane = threadIdx.x & 63;
@@ -322,64 +369,142 @@ __device__ __forceinline__ void consume_frags(const Frags &F, const bf16_t *A, i
                                                     F.f[j], acc, 0, 0, 0);
 }
 
+// Transposed product: with the packed B fragments as the MFMA's A operand and the LDS activation
+// rows as its B operand the accumulators hold C^T — lane l owns batch row (l & 31) and columns
+// (r & 3) + 8 (r >> 2) + 4 (l >> 5) of the tile, i.e. four runs of 4 consecutive columns — so the
+// epilogue writes 8-B runs instead of 2-B scatters.  Same loads, same products.
+__device__ __forceinline__ void consume_frags_t(const Frags &F, const bf16_t *A, int lda, int K,
+                                                f32x16_t &acc) {
+  const int lane = threadIdx.x & 63;
+  const bf16_t *arow = A + (lane & 31) * lda + 8 * (lane >> 5);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int j = 0; j < FB; ++j)
+    if (16 * j < K)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.f[j], *reinterpret_cast<const bf16x8_t *>(arow + 16 * j),
+                                                    acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint2 pack4_bf16(float a, float b, float c, float d) {
+  return make_uint2((uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16), (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16));
+}
+
+// the block's 32 rows of an LDS image (pitch ldx) -> global [R][W] rows r0.., 16-B coalesced
+__device__ __forceinline__ void rows_copy_out(const bf16_t *X, int ldx, bf16_t *__restrict__ g, int W, int r0) {
+  const int per = W / 8, nv = RB * per;
+  for (int i = threadIdx.x; i < nv; i += FNT) {
+    const int row = i / per, c = (i % per) * 8;
+    *reinterpret_cast<uint4 *>(g + (int64_t)(r0 + row) * W + c) = *reinterpret_cast<const uint4 *>(X + row * ldx + c);
+  }
+}
+// ... transposed: dst [W][ld] (column c holds the block's rows r0..r0+31 contiguously), 16-B stores
+__device__ __forceinline__ void cols_copy_out(const bf16_t *X, int ldx, bf16_t *__restrict__ dt, int W, int ld, int r0) {
+  for (int i = threadIdx.x; i < W * 4; i += FNT) {
+    const int c = i >> 2, q = i & 3;
+    uint32_t w4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      w4[e] = (uint32_t)X[(8 * q + 2 * e) * ldx + c] | ((uint32_t)X[(8 * q + 2 * e + 1) * ldx + c] << 16);
+    *reinterpret_cast<uint4 *>(dt + (int64_t)c * ld + r0 + 8 * q) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+  }
+}
+
+constexpr int BIAS_MAX = 256 + 128 + 64 + 128 + 256 + 256;  // the six chain layers' widths, d <= 256
+// offset of chain layer i's bias in the block's LDS bias image (widths 256, 128, 64, 128, 256, d)
+__device__ __forceinline__ int bias_off(int i) {
+  return i <= 0 ? 0 : i == 1 ? 256 : i == 2 ? 384 : i == 3 ? 448 : i == 4 ? 576 : 832;
+}
+
 __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ __attribute__((aligned(16))) float bsm[BIAS_MAX];
   const int ldx = p.maxw + 8;
   bf16_t *X0 = reinterpret_cast<bf16_t *>(smem);
   bf16_t *X1 = X0 + RB * ldx;
   const int r0 = blockIdx.x * RB;
   const bool reg = r0 >= p.B;
-  const int t = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int t = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5;
+  const int nbias = bias_off(5) + p.d;
   Frags fr[2];
-  float bias[2] = {0.f, 0.f};
-  {
-    int K, N;
-    chain_dims(p.d, 0, K, N);
-    if (t < N / 32) {
-      issue_frags(fr[0], reinterpret_cast<const bf16_t *>(p.wt[0]), K, 32 * t);
-      bias[0] = p.b[0][32 * t + (lane & 31)];
+  TOWER_PROBE(0);
+  // the block's input rows first (they gate the first MFMA), then the biases, then the weights
+  RowRegs rg;
+  rows_issue(rg, reinterpret_cast<const bf16_t *>(p.act[0]), p.d, r0);
+  float bv[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int c = (int)threadIdx.x + q * FNT;
+    bv[q] = 0.f;
+    if (c < nbias) {
+      const int i = c < 256 ? 0 : c < 384 ? 1 : c < 448 ? 2 : c < 576 ? 3 : c < 832 ? 4 : 5;
+      const int l = i < 3 ? i : i + (reg ? 3 : 0);
+      bv[q] = p.b[l][c - bias_off(i)];
     }
   }
-  load_block_n<bf16_t, FNT>(reinterpret_cast<const bf16_t *>(p.act[0]), p.d, r0, X0, ldx);
+  auto issue = [&](int i, int slot) {
+    const int l = i < 3 ? i : i + (reg ? 3 : 0);
+    int K, N;
+    chain_dims(p.d, i, K, N);
+    if (t < N / 32) {
+      if (p.packed)
+        issue_frags_packed(fr[slot], p.wpf[l], K, t);
+      else
+        issue_frags(fr[slot], reinterpret_cast<const bf16_t *>(p.wt[l]), K, 32 * t);
+    }
+  };
+  issue(0, 0);
+  rows_store(rg, p.d, X0, ldx);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int c = (int)threadIdx.x + q * FNT;
+    if (c < nbias) bsm[c] = bv[q];
+  }
   __syncthreads();
+  TOWER_PROBE(1);
   bf16_t *xin = X0, *xout = X1;
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     int K, N;
     chain_dims(p.d, i, K, N);
-    if (i < 5) {  // next layer's weights fly during this layer
-      const int ln = i + 1 < 3 ? i + 1 : i + 1 + (reg ? 3 : 0);
-      int Kn, Nn;
-      chain_dims(p.d, i + 1, Kn, Nn);
-      if (t < Nn / 32) {
-        issue_frags(fr[(i + 1) & 1], reinterpret_cast<const bf16_t *>(p.wt[ln]), Kn, 32 * t);
-        bias[(i + 1) & 1] = p.b[ln][32 * t + (lane & 31)];
-      }
-    }
+    if (i < 5) issue(i + 1, (i + 1) & 1);  // next layer's weights fly during this layer
     if (t < N / 32) {
       f32x16_t acc;
-      consume_frags(fr[i & 1], xin, ldx, K, acc);
-      const int col = 32 * t + (lane & 31);
-      const float bb = bias[i & 1];
-      bf16_t *gout = reinterpret_cast<bf16_t *>(p.act[i + 1]);
-      bf16_t tv[16];
+      consume_frags_t(fr[i & 1], xin, ldx, K, acc);
+      TOWER_PROBE(2 + 3 * i);
+      const int row = lane & 31, cb = 32 * t + 4 * half;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = acc_row(r, lane);
-        float v = acc[r] + bb;
-        v = v > 0.f ? v : 0.f;
-        tv[r] = f2bf(v);
-        xout[row * ldx + col] = tv[r];
-        gout[(int64_t)(r0 + row) * N + col] = tv[r];
+      for (int g = 0; g < 4; ++g) {
+        const float4 b4 = *reinterpret_cast<const float4 *>(bsm + bias_off(i) + cb + 8 * g);
+        *reinterpret_cast<uint2 *>(xout + row * ldx + cb + 8 * g) =
+            pack4_bf16(fmaxf(acc[4 * g] + b4.x, 0.f), fmaxf(acc[4 * g + 1] + b4.y, 0.f),
+                       fmaxf(acc[4 * g + 2] + b4.z, 0.f), fmaxf(acc[4 * g + 3] + b4.w, 0.f));
       }
-      if (i == 5 && p.act6t) {  // D3^T [d][R]: registers 4g..4g+3 = 4 consecutive rows
-        bf16_t *dt = reinterpret_cast<bf16_t *>(p.act6t) + (int64_t)col * p.R + r0 + 4 * (lane >> 5);
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<uint2 *>(dt + 8 * g) = *reinterpret_cast<const uint2 *>(&tv[4 * g]);
-      }
+      TOWER_PROBE(3 + 3 * i);
     }
     __syncthreads();
+    TOWER_PROBE(4 + 3 * i);
+    // this layer's output rows to global (read by the backward and the dW kernel) while the next
+    // layer computes; D3^T [d][R] for the decoder's dW operand
+    rows_copy_out(xout, ldx, reinterpret_cast<bf16_t *>(p.act[i + 1]), N, r0);
+    if (i == 5 && p.act6t) cols_copy_out(xout, ldx, reinterpret_cast<bf16_t *>(p.act6t), N, p.R, r0);
+    if (i == 5 && p.act6p) {  // D3 as the logits' A operand: fragments (blockIdx.x, j)
+      for (int v = threadIdx.x; v < (N / 16) * 64; v += FNT) {
+        const int j = v >> 6, ln = v & 63;
+        *reinterpret_cast<u32v4 *>(p.act6p + pack_off(blockIdx.x, j, ln, N)) =
+            *reinterpret_cast<const u32v4 *>(xout + (ln & 31) * ldx + 16 * j + 8 * (ln >> 5));
+      }
+    }
+    if (i == 5 && p.act6tp) {  // D3^T as the dWo A operand: fragments (tt, r0/16 + jj), jj = 0, 1
+      for (int v = threadIdx.x; v < (N / 32) * 2 * 64; v += FNT) {
+        const int ln = v & 63, jj = (v >> 6) & 1, tt = v >> 7;
+        const bf16_t *src = xout + (16 * jj + 8 * (ln >> 5)) * ldx + 32 * tt + (ln & 31);
+        uint32_t w4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w4[e] = (uint32_t)src[(2 * e) * ldx] | ((uint32_t)src[(2 * e + 1) * ldx] << 16);
+        *reinterpret_cast<u32v4 *>(p.act6tp + pack_off(tt, r0 / 16 + jj, ln, p.R)) = u32v4{w4[0], w4[1], w4[2], w4[3]};
+      }
+    }
     bf16_t *tmp = xin;
     xin = xout;
     xout = tmp;
@@ -392,16 +517,24 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
   bf16_t *Gr = reinterpret_cast<bf16_t *>(smem);
   const int r0 = blockIdx.x * RB;
   const bool reg = r0 >= p.B;
-  const int t = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int t = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5;
+  const int row = lane & 31, cb = 32 * t + 4 * half;
   Frags fr[2];
   auto issue_layer = [&](int i, int slot) {
     const int l = i < 3 ? i : i + (reg ? 3 : 0);
     int K, N;
     chain_dims(p.d, i, K, N);
-    if (t < K / 32) issue_frags(fr[slot], reinterpret_cast<const bf16_t *>(p.w[l]), N, 32 * t);
+    if (t < K / 32) {
+      if (p.packed)
+        issue_frags_packed(fr[slot], p.wpb[l], N, t);
+      else
+        issue_frags(fr[slot], reinterpret_cast<const bf16_t *>(p.w[l]), N, 32 * t);
+    }
   };
+  RowRegs rg;
+  rows_issue(rg, reinterpret_cast<const bf16_t *>(p.gD3), p.d, r0);
   issue_layer(5, 1);
-  load_block_n<bf16_t, FNT>(reinterpret_cast<const bf16_t *>(p.gD3), p.d, r0, Gr, ldx);
+  rows_store(rg, p.d, Gr, ldx);
   __syncthreads();
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
@@ -409,36 +542,32 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
     chain_dims(p.d, i, K, N);
     if (i > 0) issue_layer(i - 1, (i - 1) & 1);
     // the layer input's ReLU mask at this lane's accumulator positions: lands during the MFMAs
-    const int col = 32 * t + (lane & 31);
-    bf16_t hm[16];
+    uint2 hm[4];
     if (t < K / 32) {
-      const bf16_t *H = reinterpret_cast<const bf16_t *>(p.act[i]);
+      const bf16_t *H = reinterpret_cast<const bf16_t *>(p.act[i]) + (int64_t)(r0 + row) * K + cb;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) hm[r] = H[(int64_t)(r0 + acc_row(r, lane)) * K + col];
+      for (int g = 0; g < 4; ++g) hm[g] = *reinterpret_cast<const uint2 *>(H + 8 * g);
     }
     f32x16_t acc;
-    if (t < K / 32) consume_frags(fr[i & 1], Gr, ldx, N, acc);
+    if (t < K / 32) consume_frags_t(fr[i & 1], Gr, ldx, N, acc);
     __syncthreads();  // every wave has finished reading Gr
     if (t < K / 32) {
-      bf16_t *gout = i > 0 ? reinterpret_cast<bf16_t *>(p.gact[i - 1]) : nullptr;
-      bf16_t tt[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = acc_row(r, lane);
-        const int64_t go = (int64_t)(r0 + row) * K + col;
-        const float v = bf2f(hm[r]) > 0.f ? acc[r] : 0.f;
-        if (i == 0) {
-          p.gpre1[go] = v;
-          tt[r] = f2bf(v);
-        } else {
-          const bf16_t tv = f2bf(v);
-          Gr[row * ldx + col] = tv;
-          gout[go] = tv;
-        }
+      for (int g = 0; g < 4; ++g) {
+        const float v0 = __uint_as_float(hm[g].x << 16) > 0.f ? acc[4 * g] : 0.f;
+        const float v1 = __uint_as_float(hm[g].x & 0xFFFF0000u) > 0.f ? acc[4 * g + 1] : 0.f;
+        const float v2 = __uint_as_float(hm[g].y << 16) > 0.f ? acc[4 * g + 2] : 0.f;
+        const float v3 = __uint_as_float(hm[g].y & 0xFFFF0000u) > 0.f ? acc[4 * g + 3] : 0.f;
+        if (i == 0)
+          *reinterpret_cast<float4 *>(p.gpre1 + (int64_t)(r0 + row) * K + cb + 8 * g) = make_float4(v0, v1, v2, v3);
+        *reinterpret_cast<uint2 *>(Gr + row * ldx + cb + 8 * g) = pack4_bf16(v0, v1, v2, v3);
       }
-      if (i == 0 && p.gpre1t) gpre1t_store(p, col, r0, lane, tt);
     }
     __syncthreads();
+    if (i > 0)
+      rows_copy_out(Gr, ldx, reinterpret_cast<bf16_t *>(p.gact[i - 1]), K, r0);
+    else if (p.gpre1t)  // dPre1^T [d][ceil64(R)] (bf16) for cc_embed_grad_mfma
+      cols_copy_out(Gr, ldx, reinterpret_cast<bf16_t *>(p.gpre1t), K, (p.R + 63) & ~63, r0);
   }
 }
 
@@ -629,6 +758,30 @@ __global__ __launch_bounds__(256) void tower_transpose_kernel(TowerP p, int64_t 
     for (int e = threadIdx.x; e < 1024; e += 256) wt[(int64_t)(n0 + e / 32) * K + k0 + e % 32] = tile[e % 32][e / 32];
     __syncthreads();
   }
+  if constexpr (sizeof(T) == 2) {
+    if (p.packed) {  // fragment-packed forward (rows n, reduction k) and backward (rows k, red. n)
+      const bf16_t *wb = reinterpret_cast<const bf16_t *>(p.w[l]);
+      bf16_t *pf = const_cast<bf16_t *>(p.wpf[l]), *pb = const_cast<bf16_t *>(p.wpb[l]);
+      const int nfr = K * N / 8;
+      for (int f = blockIdx.x * 256 + threadIdx.x; f < nfr; f += gridDim.x * 256) {
+        const int lane = f & 63, q = f >> 6;
+        {  // forward: fragment (t, j) over K/16 reduction steps
+          const int j = q % (K / 16), tt = q / (K / 16);
+          const int n = 32 * tt + (lane & 31), k0 = 16 * j + 8 * (lane >> 5);
+          uint16_t e8[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) e8[e] = wb[(int64_t)(k0 + e) * N + n];
+          *reinterpret_cast<uint4 *>(pf + pack_off(tt, j, lane, K)) = *reinterpret_cast<const uint4 *>(e8);
+        }
+        {  // backward: fragment (t, j) over N/16 reduction steps, rows are W's rows
+          const int j = q % (N / 16), tt = q / (N / 16);
+          const int k = 32 * tt + (lane & 31), n0 = 16 * j + 8 * (lane >> 5);
+          *reinterpret_cast<uint4 *>(pb + pack_off(tt, j, lane, N)) =
+              *reinterpret_cast<const uint4 *>(wb + (int64_t)k * N + n0);
+        }
+      }
+    }
+  }
 }
 
 int make_params(const cc_tower_args *t, TowerP &p) {
@@ -656,6 +809,21 @@ int make_params(const cc_tower_args *t, TowerP &p) {
   p.gpre1t = t->dtype == CC_BF16 ? t->gpre1t : nullptr;
   p.slab = t->slab;
   p.slab_elems = slab_off(t->d, 6);
+  p.packed = t->dtype == CC_BF16 && t->d <= 256;
+  const bool fast = p.packed;
+  p.act6p = fast ? static_cast<bf16_t *>(t->act6p) : nullptr;
+  p.act6tp = fast ? static_cast<bf16_t *>(t->act6tp) : nullptr;
+  if (((uintptr_t)p.act6p | (uintptr_t)p.act6tp) & 15)
+    return cc::fail(CC_ERR_ARG, "cc_tower: packed D3 images must be 16-B aligned");
+  for (int l = 0; l < 9; ++l) {
+    p.wpf[l] = static_cast<const bf16_t *>(t->wpf[l]);
+    p.wpb[l] = static_cast<const bf16_t *>(t->wpb[l]);
+    if (l < (t->R > t->B ? 9 : 6) && (!t->wpf[l] || !t->wpb[l])) p.packed = false;
+  }
+  if (p.packed)
+    for (int l = 0; l < 9; ++l)
+      if ((((uintptr_t)t->wpf[l] | (uintptr_t)t->wpb[l]) & 15) != 0)
+        return cc::fail(CC_ERR_ARG, "cc_tower: packed weight images must be 16-B aligned");
   return CC_OK;
 }
 

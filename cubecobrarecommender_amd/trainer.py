@@ -226,6 +226,7 @@ class Trainer:
         self.gPre1T = torch.zeros(d, self.RP, **T) if self.embed_mfma else None
         if self.mx8 and not self.fused_tower:
             raise ValueError('fp8 needs the fused towers (fused_tower=True, B % 32 == 0)')
+        self.wpack = self.D3p = self.D3tp = None
         if self.fused_tower:
             self.tower_layers = ('encoder/encoded_2', 'encoder/encoded_3', 'encoder/bottleneck',
                                  'decoder/decoded_1', 'decoder/decoded_2', 'decoder/decoded_3',
@@ -234,6 +235,14 @@ class Trainer:
             sizes = [int(np.prod(self.layout.shape(n + '/kernel'))) for n in self.tower_layers]
             self.wt_off = np.concatenate([[0], np.cumsum([(n + 63) // 64 * 64 for n in sizes])])
             self.wt = torch.zeros(int(self.wt_off[-1]), **T)
+            # fragment-packed forward/backward weight images for the d <= 256 bf16 tower kernels
+            # (written with wt by cc_tower_transpose; the opt-in fused Adam writes only wt)
+            pack = (self.dtype == L.CC_BF16 and d <= 256 and os.environ.get('CCREC_FUSED_ADAM', '0') != '1'
+                    and os.environ.get('CCREC_TOWER_PACK', '1') != '0')
+            self.wpack = torch.zeros(2, int(self.wt_off[-1]), **T) if pack else None
+            # ... and D3 as packed operand images of the fused D1 output kernel (cc_dec_bce_dw)
+            self.D3p = torch.zeros(R * d, **T) if pack else None
+            self.D3tp = torch.zeros(d * R, **T) if pack else None
             slab = int(L.lib().cc_tower_slab_elems(d))
             self.slab = torch.zeros((R // 32) * slab, **f32)
             # decoder operands kept k-contiguous: D3^T (tower fwd), dZ^T (BCE epilogue), Wo^T shadow
@@ -336,12 +345,17 @@ class Trainer:
         for l, name in enumerate(self.tower_layers):
             t.w[l] = src[self.layout.offset(name + '/kernel'):].data_ptr()
             t.wt[l] = self.wt[int(self.wt_off[l]):].data_ptr()
+            if self.wpack is not None:
+                t.wpf[l] = self.wpack[0, int(self.wt_off[l]):].data_ptr()
+                t.wpb[l] = self.wpack[1, int(self.wt_off[l]):].data_ptr()
             t.b[l] = self.params[self.layout.offset(name + '/bias'):].data_ptr()
             t.gw[l] = self.grads[self.layout.offset(name + '/kernel'):].data_ptr()
             t.gb[l] = self.grads[self.layout.offset(name + '/bias'):].data_ptr()
         for a, buf in enumerate((self.H1, self.H2, self.H3, self.Zl, self.D1, self.D2, self.D3)):
             t.act[a] = buf.data_ptr()
         t.act6t = self.D3t.data_ptr()
+        if self.D3p is not None:
+            t.act6p, t.act6tp = self.D3p.data_ptr(), self.D3tp.data_ptr()
         t.gD3 = self.gD3.data_ptr()
         for a, buf in enumerate((self.gH2, self.gH3, self.gZl, self.gD1, self.gD2)):
             t.gact[a] = buf.data_ptr()      # dPre of e2, e3, e4, d1, d2
@@ -519,7 +533,9 @@ class Trainer:
                    L.ptr(self.D3tqs), None, s)
         t = self._tick('dec_bce_fwd')
         if self.fused_out:     # logits + BCE + dZ + dWo/dbo in one pass (csrc/decout.hip)
-            L.call('cc_dec_bce_dw', L.ptr(self.D3), L.ptr(self.D3t), R, L.ptr(self.WoT[0]),
+            L.call('cc_dec_bce_dw', L.ptr(self.D3), L.ptr(self.D3t), R,
+                   L.ptr(self.D3p) if self.D3p is not None else None,
+                   L.ptr(self.D3tp) if self.D3p is not None else None, L.ptr(self.WoT[0]),
                    self.pf('decoder/reconstruct/bias'), B, d, V, L.ptr(self.y_bits), L.ptr(self.dZout),
                    self.gp('decoder/reconstruct/kernel'), self.gp('decoder/reconstruct/bias'),
                    L.ptr(self.bce_part), L.ptr(self.loss_dev), 1.0 / (B * V), L.ptr(self.tickets), s)

@@ -235,6 +235,20 @@ typedef struct cc_tower_args {
   float *gw[9];          /* reduce outputs: kernel grads [K][N] */
   float *gb[9];          /* bias grads [N] */
   void *gpre1t;          /* optional (bf16): dPre1^T [d][ceil64(R)] for cc_embed_grad_mfma */
+  /* optional (bf16, d <= 256): MFMA-fragment-packed weight images, K*N elements each, written by
+   * cc_tower_transpose.  Fragment (t, j) of a [rows][red] operand = 64 lanes x 8 consecutive
+   * elements, lane l holding row 32t + (l & 31), reduction 16j + 8(l >> 5) .. +8, stored as one
+   * contiguous 1 KB run: every wave load reads whole cache lines.
+   *   wpf: forward B operand (rows = N outputs, reduction K): element W[k][n];
+   *   wpb: backward B operand (rows = K outputs, reduction N): element W[k][n].
+   * Used by the fast tower kernels when all of them are set. */
+  void *wpf[9];
+  void *wpb[9];
+  /* optional (bf16, d <= 256, fast kernels): D3 as fragment-packed MFMA operand images for
+   * cc_dec_bce_dw — act6p: rows = batch rows, reduction d ([R/32][d/16][64][8]); act6tp: rows = d,
+   * reduction = batch rows ([d/32][R/16][64][8]).  Same fragment order as wpf. */
+  void *act6p;
+  void *act6tp;
 } cc_tower_args;
 int64_t cc_tower_slab_elems(int32_t d);
 int cc_tower_fwd(const cc_tower_args *t, void *stream);
@@ -267,7 +281,8 @@ int cc_dec_bce_fused(int32_t dtype, const void *H3, const void *Wo, const float 
  * dbo = colsum dZ from the block's LDS copy of dZ^T — no dZ^T in HBM, no separate dW launch.
  * loss_partials: cc_dec_bce_dw_blocks(V) doubles; loss_out (optional, with ticket) =
  * sum(partials) * loss_scale reduced by the last block. */
-int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const void *WoT, const float *bo,
+int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const void *D3p, const void *D3tp,
+                  const void *WoT, const float *bo,
                   int32_t B, int32_t d, int32_t V, const uint32_t *y_bits, void *dZ, float *gW,
                   float *gb, double *loss_partials, double *loss_out, double loss_scale,
                   uint32_t *ticket, void *stream);

@@ -115,3 +115,61 @@ def test_fused_towers_match_generic_gemm_path():
         bad = {k: rel_err(res[True][k], res[False][k]) for k in res[True]
                if not rel_err(res[True][k], res[False][k]) < tol}
         assert not bad, (dtype, bad)
+
+
+@pytest.mark.parametrize('d,B,R', [(256, 64, 128), (256, 512, 512), (128, 32, 64), (64, 32, 32)])
+def test_packed_weight_images_bit_exact(d, B, R):
+    """The fragment-packed weight images (cc_tower_args.wpf/wpb, written by cc_tower_transpose)
+    feed the fast bf16 kernels the same fragments as the row-strided reads: identical outputs,
+    and the images hold exactly the documented element order."""
+    rng = np.random.default_rng(d * 7 + R)
+    tdt = torch.bfloat16
+    rnd = lambda *s: torch.from_numpy((rng.standard_normal(s) * 0.2).astype(np.float32)).to('cuda', tdt)
+    dims = _dims(d)
+    W = [rnd(*dims[l if l < 6 else l - 3]) for l in range(9)]
+    bias = [torch.from_numpy(rng.standard_normal(w.shape[1]).astype(np.float32) * 0.1).cuda() for w in W]
+    widths = [d, 256, 128, 64, 128, 256, d]
+    x0, gD3 = rnd(R, d), rnd(R, d)
+    outs = {}
+    for packed in (False, True):
+        Wt = [torch.zeros(w.shape[1], w.shape[0], device='cuda', dtype=tdt) for w in W]
+        wpf = [torch.zeros(w.numel(), device='cuda', dtype=tdt) for w in W]
+        wpb = [torch.zeros(w.numel(), device='cuda', dtype=tdt) for w in W]
+        act = [x0.clone()] + [torch.zeros(R, w, device='cuda', dtype=tdt) for w in widths[1:]]
+        act6t = torch.zeros(d, R, device='cuda', dtype=tdt)
+        gact = [torch.zeros(R, w, device='cuda', dtype=tdt) for w in (256, 128, 64, 128, 256)]
+        gpre1 = torch.zeros(R, d, device='cuda')
+        gpre1t = torch.zeros(d, (R + 63) // 64 * 64, device='cuda', dtype=tdt)
+        slab = torch.zeros((R // 32) * int(L.lib().cc_tower_slab_elems(d)), device='cuda')
+        t = L.TowerArgs(dtype=L.CC_BF16, d=d, B=B, R=R)
+        t.slab = slab.data_ptr()
+        for l in range(9):
+            t.w[l], t.wt[l], t.b[l] = W[l].data_ptr(), Wt[l].data_ptr(), bias[l].data_ptr()
+            if packed:
+                t.wpf[l], t.wpb[l] = wpf[l].data_ptr(), wpb[l].data_ptr()
+        for a in range(7):
+            t.act[a] = act[a].data_ptr()
+        t.act6t, t.gD3, t.gpre1, t.gpre1t = act6t.data_ptr(), gD3.data_ptr(), gpre1.data_ptr(), gpre1t.data_ptr()
+        act6p, act6tp = torch.zeros(R * d, device='cuda', dtype=tdt), torch.zeros(R * d, device='cuda', dtype=tdt)
+        t.act6p, t.act6tp = act6p.data_ptr(), act6tp.data_ptr()
+        for a in range(5):
+            t.gact[a] = gact[a].data_ptr()
+        s = L.stream_ptr()
+        for fn in ('cc_tower_transpose', 'cc_tower_fwd', 'cc_tower_bwd_chain'):
+            L.call(fn, ctypes.byref(t), s)
+        torch.cuda.synchronize()
+        outs[packed] = [a.cpu() for a in act[1:]] + [act6t.cpu()] + [g.cpu() for g in gact] + [gpre1.cpu(), gpre1t.cpu()]
+        D3 = act[6].cpu()
+        assert torch.equal(act6p.cpu(), D3.view(R // 32, 32, d // 16, 2, 8).permute(0, 2, 3, 1, 4).reshape(-1))
+        assert torch.equal(act6tp.cpu(), D3.t().contiguous().view(d // 32, 32, R // 16, 2, 8)
+                           .permute(0, 2, 3, 1, 4).reshape(-1))
+        if packed:
+            for l in range(9 if R > B else 6):
+                w = W[l].cpu().view(torch.int16).numpy()
+                K, N = w.shape
+                f = wpf[l].cpu().view(torch.int16).numpy().reshape(N // 32, K // 16, 2, 32, 8)
+                assert np.array_equal(f, w.T.reshape(N // 32, 32, K // 16, 2, 8).transpose(0, 2, 3, 1, 4)), l
+                b = wpb[l].cpu().view(torch.int16).numpy().reshape(K // 32, N // 16, 2, 32, 8)
+                assert np.array_equal(b, w.reshape(K // 32, 32, N // 16, 2, 8).transpose(0, 2, 3, 1, 4)), l
+    for i, (a, b) in enumerate(zip(outs[False], outs[True])):
+        assert torch.equal(a, b), i

@@ -24,7 +24,7 @@ tick = torch.zeros(1, device='cuda', dtype=torch.int32)
 
 
 def run():
-    L.call('cc_dec_bce_dw', L.ptr(D3), L.ptr(D3t), B, L.ptr(WoT), L.ptr(bo), B, d, V, L.ptr(ybits),
+    L.call('cc_dec_bce_dw', L.ptr(D3), L.ptr(D3t), B, None, None, L.ptr(WoT), L.ptr(bo), B, d, V, L.ptr(ybits),
            L.ptr(dZ), L.ptr(gW), L.ptr(gb), L.ptr(part), L.ptr(loss), 1.0 / (B * V), L.ptr(tick),
            L.stream_ptr())
 
