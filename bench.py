@@ -244,7 +244,8 @@ def main():
     if world == 1:
         adam_ms = float(np.mean([a.elapsed_time(b) for a, b in adam_ev]))
         roof = roofline_for('cc_adam_dense', adam_ms, tr)
-        roof['measured'] = 'HIP events around the Adam kernel in every timed step (same stream)'
+        roof['measured'] = ('HIP events around the Adam kernel on its stream, every %d-th timed step '
+                            '(eager launch behind the forward/backward graph)' % ADAM_SAMPLE)
         roof['traffic'] = None
         if args.traffic_json and os.path.exists(args.traffic_json):
             # PMC bytes were collected on one configuration: attach them only to the same launch

@@ -14,6 +14,11 @@
 // and the last block (agent-scope ticket) reduces the partials in block order — deterministic.
 #include "common.hpp"
 
+// dev-only timing hook (tools/micro/dec_probe.hip defines it); compiled out of the library
+#ifndef DEC_PROBE
+#define DEC_PROBE(k)
+#endif
+
 namespace {
 
 constexpr int NB = 96;      // V columns per block: ceil(22000 / 96) = 230 blocks <= 256 CUs, one round
@@ -83,6 +88,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   const int V = p.V;
   const int VW = (V + 31) >> 5;
 
+  DEC_PROBE(0);
   // ---- resident operands: Wo^T slice (rows clamped at the edge: they feed masked columns only)
   // and the target bits; every load of the batch issued before the first LDS store
   {
@@ -142,6 +148,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   };
   load_a(af[0], 0);
   __syncthreads();
+  DEC_PROBE(1);
   const float scale = p.scale;
 #pragma unroll
   for (int ps = 0; ps < npass; ++ps) {
@@ -160,6 +167,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ps & 1][kk], b, acc[j], 0, 0, 0);
       }
     }
+    DEC_PROBE(2 + 2 * ps);
     const int rb = ps * 256 + w * 32;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -196,6 +204,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         *reinterpret_cast<uint2 *>(Zt + sw_off(col, rb + 8 * g + 4 * half, CHB)) =
             *reinterpret_cast<const uint2 *>(&tt[4 * g]);
     }
+    DEC_PROBE(3 + 2 * ps);
   }
 
   // bias gradient: column sums of the rounded dZ in a fixed order (lane halves, then waves)
@@ -210,6 +219,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   for (int off = 32; off > 0; off >>= 1) lossf += __shfl_xor(lossf, off);
   if (lane == 0) red_loss[w] = (double)lossf;
   __syncthreads();   // dZ^T image, red_cs, red_loss complete
+  DEC_PROBE(6);
   if (tid < NB && n0 + tid < V) {
     float g = 0.f;
     for (int i = 0; i < NTH / 64; ++i) g += red_cs[i][tid];
@@ -271,6 +281,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    DEC_PROBE(7);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int gc2 = n0 + j * 32 + (lane & 31);
@@ -282,6 +293,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     }
   }
 
+  DEC_PROBE(8);
   // ---- the last block reduces the loss partials in block order
   if (p.loss_out) {
     __syncthreads();

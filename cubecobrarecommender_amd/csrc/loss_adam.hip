@@ -391,7 +391,7 @@ extern "C" int cc_adam_dense(float *p, float *m, float *v, const float *g, uint1
              "cc_adam_dense: buffers must be 16-byte aligned");
   CC_REQUIRE(!shadow || (uintptr_t)shadow % 8 == 0, "cc_adam_dense: shadow must be 8-byte aligned");
   if (n <= 0) return CC_OK;
-  const int64_t blocks = std::min<int64_t>(cdiv(cdiv(n, 4), NT), 256 * 8);
+  const int64_t blocks = std::min<int64_t>(cdiv(cdiv(n, 4), NT), 1 << 30);  // one float4 per thread
   const cc_adam::Args a{p, m, v, g, (bf16_t *)shadow, n, lr, beta1, beta2, eps};
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(NT), 0, as_stream(stream), a, state);
   CC_LAUNCH_CHECK("adam_kernel");

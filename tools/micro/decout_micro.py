@@ -21,22 +21,27 @@ gb = torch.empty(V, device='cuda')
 part = torch.zeros(4096, device='cuda', dtype=torch.float64)
 loss = torch.zeros(1, device='cuda', dtype=torch.float64)
 tick = torch.zeros(1, device='cuda', dtype=torch.int32)
+D3p = D3.view(B // 32, 32, d // 16, 2, 8).permute(0, 2, 3, 1, 4).contiguous()
+D3tp = D3t.view(d // 32, 32, B // 16, 2, 8).permute(0, 2, 3, 1, 4).contiguous()
+PK = [None, None]
 
 
 def run():
-    L.call('cc_dec_bce_dw', L.ptr(D3), L.ptr(D3t), B, None, None, L.ptr(WoT), L.ptr(bo), B, d, V, L.ptr(ybits),
+    L.call('cc_dec_bce_dw', L.ptr(D3), L.ptr(D3t), B, PK[0], PK[1], L.ptr(WoT), L.ptr(bo), B, d, V, L.ptr(ybits),
            L.ptr(dZ), L.ptr(gW), L.ptr(gb), L.ptr(part), L.ptr(loss), 1.0 / (B * V), L.ptr(tick),
            L.stream_ptr())
 
 
-for _ in range(3):
-    run()
-torch.cuda.synchronize()
-e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-n = int(os.environ.get('N', '50'))
-e0.record()
-for _ in range(n):
-    run()
-e1.record()
-torch.cuda.synchronize()
-print(f'dec_bce_dw {e0.elapsed_time(e1) / n * 1000:.1f} us (dbg={os.environ.get("CCREC_DECOUT_DBG", "0")}, V={V})')
+for pk in (0, 1):
+    PK[:] = [L.ptr(D3p), L.ptr(D3tp)] if pk else [None, None]
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = int(os.environ.get('N', '50'))
+    e0.record()
+    for _ in range(n):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    print(f'dec_bce_dw packed={pk} {e0.elapsed_time(e1) / n * 1000:.1f} us (dbg={os.environ.get("CCREC_DECOUT_DBG", "0")}, V={V})')
