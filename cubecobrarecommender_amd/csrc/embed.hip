@@ -125,6 +125,84 @@ __global__ __launch_bounds__(256) void gather_kernel(const T *__restrict__ table
   }
 }
 
+// Forward, bf16 d = 256: each lane loads 16 B (8 columns) so one wave load instruction fetches TWO
+// table rows (half-wave h takes list entries of parity h) — twice the bytes in flight per
+// instruction; GWN waves per cube, U loads in flight per lane.  Partial sums: lane halves
+// (shuffle), then waves in order through LDS — deterministic.
+typedef __attribute__((ext_vector_type(4))) uint32_t g_u32x4;
+template <int GWN, int U>
+__global__ __launch_bounds__(64 * GWN) void gather2_kernel(const bf16_t *__restrict__ table,
+                                                          const float *__restrict__ bias, int R,
+                                                          const int32_t *__restrict__ x_cnt,
+                                                          const int32_t *__restrict__ x_idx, int x_cap,
+                                                          bf16_t *__restrict__ out) {
+  constexpr int D = 256;
+  __shared__ __attribute__((aligned(16))) float part[GWN][D];
+  __shared__ int32_t ls[GIDX];
+  const int row = blockIdx.x;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
+  const int c0 = (lane & 31) * 8;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  const int n = x_cnt[row];
+  const int q = ((n + GWN - 1) / GWN + 1) & ~1;  // even chunks: pairs never straddle waves
+  const int i0 = min(n, w * q), i1 = min(n, i0 + q);
+  const int32_t *__restrict__ glst = x_idx + (int64_t)row * x_cap;
+  const bool staged = n <= GIDX;
+  if (staged)
+    for (int t = threadIdx.x; t < n; t += 64 * GWN) ls[t] = glst[t];
+  __syncthreads();
+  const int32_t *lst = staged ? ls : glst;
+  int i = i0;
+  for (; i + 2 * U <= i1; i += 2 * U) {
+    int j[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) j[u] = lst[i + 2 * u + h];
+    g_u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const g_u32x4 *>(table + (int64_t)j[u] * D + c0);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[2 * e] += __uint_as_float(v[u][e] << 16);
+        acc[2 * e + 1] += __uint_as_float(v[u][e] & 0xFFFF0000u);
+      }
+  }
+  for (; i + h < i1; i += 2) {
+    const g_u32x4 v = *reinterpret_cast<const g_u32x4 *>(table + (int64_t)lst[i + h] * D + c0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc[2 * e] += __uint_as_float(v[e] << 16);
+      acc[2 * e + 1] += __uint_as_float(v[e] & 0xFFFF0000u);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] += __shfl_xor(acc[e], 32);
+  if (h == 0) {
+    *reinterpret_cast<float4 *>(&part[w][c0]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *reinterpret_cast<float4 *>(&part[w][c0 + 4]) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  }
+  __syncthreads();
+  if (threadIdx.x < D / 8) {
+    const int c = threadIdx.x * 8;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = part[0][c + e];
+#pragma unroll
+      for (int p = 1; p < GWN; ++p) v += part[p][c + e];
+      v += bias[c + e];
+      o[e] = v > 0.f ? v : 0.f;
+    }
+    g_u32x4 pk;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pk[e] = (uint32_t)f2bf(o[2 * e]) | ((uint32_t)f2bf(o[2 * e + 1]) << 16);
+    *reinterpret_cast<g_u32x4 *>(out + (int64_t)row * D + c) = pk;
+  }
+}
+
 // Backward: 4 waves per W1 row (row V = the bias when bias_grad is given); wave w walks the w-th
 // quarter of the row's bit words, collecting up to U set bits before issuing their dPre loads
 // together (heavy Zipf rows have a set bit for nearly every batch row).  Partials added in wave order.
@@ -318,6 +396,19 @@ extern "C" int cc_embed_gather_fwd(int32_t dtype, const void *table, const float
   const dim3 grid((unsigned)R), block(256);
   const int epl = d / 64;
   hipStream_t s = as_stream(stream);
+  static const int g2 = [] {  // A/B switch (dev): 16-B lanes, two rows per load; waves x loads
+    const char *e = getenv("CCREC_GATHER2");
+    return e ? atoi(e) : 48;
+  }();
+  if (dtype == CC_BF16 && d == 256 && g2 > 0) {
+#define G2(GWN, U) \
+  if (g2 == GWN * 10 + U) hipLaunchKernelGGL((gather2_kernel<GWN, U>), grid, dim3(64 * GWN), 0, s, \
+                                             (const bf16_t *)table, bias, R, x_cnt, x_idx, x_cap, (bf16_t *)out);
+    G2(4, 4) G2(4, 8) G2(8, 4) G2(8, 8) G2(4, 6) G2(8, 6)
+#undef G2
+    CC_LAUNCH_CHECK("gather2_kernel");
+    return CC_OK;
+  }
   static const int gu = [] {  // A/B switch: row loads in flight per lane (bf16, d = 256)
     const char *e = getenv("CCREC_GATHER_U");
     return e ? atoi(e) : 8;  // measured at cfg 2: 8 -> 328.5 us/step, 16 -> 337, 32 -> 341
