@@ -91,6 +91,8 @@ SIGNATURES = {
     'cc_infer_encode_ws_size': (_SZ, [_I32, _I32, _I32]),
     'cc_infer_encode_fp32': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _P]),
     'cc_infer_decode_fp32': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
+    'cc_similar_ws_size': (_SZ, [_I32]),
+    'cc_similar_cards': (C.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     'cc_tower_slab_elems': (_I64, [_I32]),
     'cc_tower_fwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_bwd': (C.c_int, [C.POINTER(TowerArgs), _P]),

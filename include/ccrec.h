@@ -339,6 +339,18 @@ int cc_infer_decode_fp32(const float *params, int32_t V, int32_t d, int32_t R,
                          const float *zlat, float *h3_ws, float *probs, void *stream);
 
 /* ----------------------------------------------------------------------------------
+ * Card similarity (src/scripts/similarity.py:19-31).  emb [V][K] fp32 = the
+ * encoder on the identity (cc_infer_encode_fp32 on one-card rows).  dist_j = Keras
+ * CosineSimilarity(emb[q], emb[j]) = -sum(l2_normalize(a) * l2_normalize(b)), fp32 in index
+ * order without contraction; out_idx/out_dist = the N smallest by numpy argsort(kind='stable')
+ * (ties -> lower index first).  dist_all (optional) receives all V distances.  N <= 4096.
+ * ws: cc_similar_ws_size(V) bytes, 8-B aligned.
+ * ---------------------------------------------------------------------------------- */
+size_t cc_similar_ws_size(int32_t V);
+int cc_similar_cards(const float *emb, int32_t V, int32_t K, int32_t q, int32_t N, int32_t *out_idx,
+                     float *out_dist, float *dist_all, void *ws, void *stream);
+
+/* ----------------------------------------------------------------------------------
  * Top-N (ml_recommend.py:87-108): rank all V probabilities descending, ties -> higher
  * index first (= numpy argsort(kind='stable')[::-1]); additions = first max(amount,1)
  * indices not in the cube; cut_vals[i] = probs[cube_idx[i]].  cube_idx: n DISTINCT card ids.

@@ -1,0 +1,87 @@
+"""N4 card similarity (src/scripts/similarity.py:19-31): the CPU oracle's own properties (no GPU)
+and the GPU path (cc_infer_encode_fp32 on the identity + cc_similar_cards) against it, bit-exact."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import infer_ref, similarity_ref
+
+
+def _rand_emb(rng, V, K=64, zero_rows=(), dup_rows=()):
+    e = np.maximum(rng.standard_normal((V, K)).astype(np.float32), 0)
+    for z in zero_rows:
+        e[z] = 0
+    for a, b in dup_rows:
+        e[b] = e[a]
+    return e
+
+
+def test_oracle_cosine_properties():
+    rng = np.random.default_rng(0)
+    e = _rand_emb(rng, 300, zero_rows=(5, 17), dup_rows=((3, 200), (3, 250)))
+    d = similarity_ref.cosine_dists(e, 3)
+    n = e.astype(np.float64) / np.maximum(np.linalg.norm(e.astype(np.float64), axis=1, keepdims=True), 1e-6)
+    want = -(n @ n[3])
+    assert np.max(np.abs(d - want)) < 1e-6
+    assert d[5] == 0 and d[17] == 0                     # all-zero embeddings: l2_normalize -> 0
+    order, dd, _ = similarity_ref.most_similar(e, 3, 5)
+    assert list(order[:3]) == [3, 200, 250]              # exact ties at -1: lower index first
+    assert np.all(np.diff(dd) >= 0)
+
+
+def test_oracle_batched_encoder_equals_per_row():
+    from oracle import model_ref
+    V, d = 120, 64
+    P = model_ref.init_params(V, d, seed=4, bias_std=0.05)
+    rows = [0, 7, 119, 50]
+    got = similarity_ref.encode32_rows(P, rows)
+    for r, g in zip(rows, got):
+        assert np.array_equal(g, infer_ref.encode32(P, [r]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('V,N', [(300, 1), (300, 300), (20884, 40), (5000, 4096)])
+def test_gpu_similar_cards_bit_exact(V, N):
+    import torch
+    from cubecobrarecommender_amd.similarity import similar
+    rng = np.random.default_rng(V + N)
+    e = _rand_emb(rng, V, zero_rows=(1, 2, V - 1), dup_rows=((10, 11), (10, V - 2), (3, 4)))
+    emb = torch.from_numpy(e).cuda()
+    for q in (10, 1, 3, V - 3):
+        idx, dist = similar(emb, q, N)
+        oi, od, _ = similarity_ref.most_similar(e, q, N)
+        assert np.array_equal(idx, oi), q
+        assert np.array_equal(dist.view(np.uint32) & 0x7FFFFFFF, od.view(np.uint32) & 0x7FFFFFFF), q
+
+
+@pytest.mark.gpu
+def test_gpu_card_embeddings_and_cli(tmp_path):
+    """model.encoder on the identity (reference architecture, V=20884, d=512) == the oracle, and
+    scripts/similarity.py prints the oracle's ranking."""
+    from cubecobrarecommender_amd.model import CC_Recommender, load_model
+    from cubecobrarecommender_amd.similarity import card_embeddings
+    V, d = 20884, 512
+    model = CC_Recommender(V, d=d, dtype='bf16', seed=3)
+    dest = str(tmp_path / 'ml_files' / 'high_req')
+    model.save(dest, save_format='tf')
+    m2 = load_model(dest)
+    P = m2.layout.unpack(m2._current_flat())
+    emb = card_embeddings(m2).cpu().numpy()
+    rows = np.r_[0:64, 10000:10064, V - 64:V]
+    assert np.array_equal(emb[rows], similarity_ref.encode32_rows(P, rows))
+    names = {i: f'card {i}' for i in range(V)}
+    names[77] = 'lightning bolt'
+    idmap = tmp_path / 'id_map.json'
+    idmap.write_text(json.dumps({str(k): v for k, v in names.items()}))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from scripts import similarity as cli
+    lines = []
+    rows_out = cli.main(['lightning_bolt', '12', '--model-dir', dest, '--id-map', str(idmap)],
+                        print_fn=lambda *a: lines.append(' '.join(str(x) for x in a)))
+    oi, od, _ = similarity_ref.most_similar(emb, 77, 12)
+    assert [r[1] for r in rows_out] == [names[int(i)] for i in oi]
+    assert lines[0].startswith('1: lightning bolt')
+    assert [r[2] for r in rows_out] == [float(x) for x in od]
