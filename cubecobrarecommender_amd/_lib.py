@@ -68,12 +68,14 @@ SIGNATURES = {
     'cc_crc32c': (C.c_uint32, [C.c_uint32, _P, _SZ]),
     'cc_noise_fwd': (C.c_int, [C.POINTER(NoiseArgs), _P]),
     'cc_embed_gather_fwd': (C.c_int, [_I32, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P]),
+    'cc_embed_gather_fwd_warm': (C.c_int, [_I32, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _I64, _P]),
     'cc_embed_scatter_bwd': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_embed_grad_mfma': (C.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_gemm': (C.c_int, [C.POINTER(GemmArgs), _P]),
     'cc_gemm_pair': (C.c_int, [C.POINTER(GemmArgs), C.POINTER(GemmArgs), _P]),
     'cc_gemm_grid': (C.c_int, [_I32, _I32, _P]),
     'cc_splitk_reduce': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
+    'cc_splitk_reduce_warm': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _I64, _P]),
     'cc_colsum': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P]),
     'cc_transpose': (C.c_int, [_I32, _P, _I32, _I32, _P, _P]),
     'cc_quant_mx8': (C.c_int, [_I32, _P, _I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P]),

@@ -96,3 +96,18 @@ __device__ __forceinline__ double u53_open0(uint32_t hi, uint32_t lo) {
 __device__ __forceinline__ uint32_t mulhi_bound(uint32_t x, uint32_t n) {
   return (uint32_t)(((uint64_t)x * (uint64_t)n) >> 32);
 }
+
+// L2 warm-up for the NEXT launch, called at the end of a kernel: workgroups are dispatched
+// round-robin over the 8 XCDs (block b -> XCD b % 8), so the blocks of one XCD together read one
+// dword per 128-B line of [p, p + bytes) and the next kernel finds those lines in every XCD's L2.
+__device__ __forceinline__ void l2_warm(const void *p, int64_t bytes, int block, int nblocks) {
+  if (!p || bytes <= 0 || nblocks < 8) return;
+  const int per = nblocks / 8;
+  if (block >= per * 8) return;
+  const int part = block / 8;
+  const int64_t lines = (bytes + 127) / 128, chunk = (lines + per - 1) / per;
+  const int64_t l0 = (int64_t)part * chunk, l1 = l0 + chunk < lines ? l0 + chunk : lines;
+  uint32_t acc = 0u;
+  for (int64_t l = l0 + threadIdx.x; l < l1; l += blockDim.x) acc += reinterpret_cast<const uint32_t *>(p)[l * 32];
+  asm volatile("" ::"v"(acc));
+}

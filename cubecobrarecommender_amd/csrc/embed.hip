@@ -135,7 +135,8 @@ __global__ __launch_bounds__(64 * GWN) void gather2_kernel(const bf16_t *__restr
                                                           const float *__restrict__ bias, int R,
                                                           const int32_t *__restrict__ x_cnt,
                                                           const int32_t *__restrict__ x_idx, int x_cap,
-                                                          bf16_t *__restrict__ out) {
+                                                          bf16_t *__restrict__ out, const void *warm,
+                                                          int64_t warm_bytes) {
   constexpr int D = 256;
   __shared__ __attribute__((aligned(16))) float part[GWN][D];
   __shared__ int32_t ls[GIDX];
@@ -201,6 +202,7 @@ __global__ __launch_bounds__(64 * GWN) void gather2_kernel(const bf16_t *__restr
     for (int e = 0; e < 4; ++e) pk[e] = (uint32_t)f2bf(o[2 * e]) | ((uint32_t)f2bf(o[2 * e + 1]) << 16);
     *reinterpret_cast<g_u32x4 *>(out + (int64_t)row * D + c) = pk;
   }
+  l2_warm(warm, warm_bytes, blockIdx.x, gridDim.x);  // the tower forward's packed weights
 }
 
 // Backward: 4 waves per W1 row (row V = the bias when bias_grad is given); wave w walks the w-th
@@ -386,9 +388,21 @@ __global__ __launch_bounds__(256, 2) void embed_grad_mfma_kernel(const bf16_t *_
 
 }  // namespace
 
+extern "C" int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const float *bias, int32_t V,
+                                        int32_t d, int32_t R, const int32_t *x_cnt,
+                                        const int32_t *x_idx, int32_t x_cap, void *out,
+                                        const void *warm, int64_t warm_bytes, void *stream);
+
 extern "C" int cc_embed_gather_fwd(int32_t dtype, const void *table, const float *bias, int32_t V,
                                    int32_t d, int32_t R, const int32_t *x_cnt,
                                    const int32_t *x_idx, int32_t x_cap, void *out, void *stream) {
+  return cc_embed_gather_fwd_warm(dtype, table, bias, V, d, R, x_cnt, x_idx, x_cap, out, nullptr, 0, stream);
+}
+
+extern "C" int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const float *bias, int32_t V,
+                                        int32_t d, int32_t R, const int32_t *x_cnt,
+                                        const int32_t *x_idx, int32_t x_cap, void *out,
+                                        const void *warm, int64_t warm_bytes, void *stream) {
   CC_REQUIRE(table && bias && x_cnt && x_idx && out, "cc_embed_gather_fwd: null pointer");
   CC_REQUIRE(d % 64 == 0 && d >= 64 && d <= 1024, "cc_embed_gather_fwd: d must be 64..1024, %64");
   CC_REQUIRE(V > 0 && R >= 0 && x_cap > 0, "cc_embed_gather_fwd: bad sizes");
@@ -403,7 +417,8 @@ extern "C" int cc_embed_gather_fwd(int32_t dtype, const void *table, const float
   if (dtype == CC_BF16 && d == 256 && g2 > 0) {
 #define G2(GWN, U) \
   if (g2 == GWN * 10 + U) hipLaunchKernelGGL((gather2_kernel<GWN, U>), grid, dim3(64 * GWN), 0, s, \
-                                             (const bf16_t *)table, bias, R, x_cnt, x_idx, x_cap, (bf16_t *)out);
+                                             (const bf16_t *)table, bias, R, x_cnt, x_idx, x_cap, (bf16_t *)out, \
+                                             warm, warm_bytes);
     G2(4, 4) G2(4, 8) G2(8, 4) G2(8, 8) G2(4, 6) G2(8, 6)
 #undef G2
     CC_LAUNCH_CHECK("gather2_kernel");

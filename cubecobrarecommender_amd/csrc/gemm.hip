@@ -794,9 +794,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restr
                                                             int splits, int M, int N,
                                                             const T *__restrict__ H, T *C,
                                                             float *Cf, const float *cs_part,
-                                                            float *cs_out) {
+                                                            float *cs_out, const void *warm, int64_t warm_bytes) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t MN = (int64_t)M * N;
+  l2_warm(warm, warm_bytes, blockIdx.x, gridDim.x);  // the next launch's operands (tower backward)
   if (cs_out && i < N) {
     float c = 0.f;
     for (int z = 0; z < splits; ++z) c += cs_part[(int64_t)z * N + i];
@@ -1010,19 +1011,34 @@ extern "C" int cc_gemm_pair(const cc_gemm_args *g0, const cc_gemm_args *g1, void
   return CC_OK;
 }
 
+extern "C" int cc_splitk_reduce_warm(int32_t dtype, const float *partials, int32_t splits, int32_t M,
+                                     int32_t N, const void *H, void *C, float *Cf,
+                                     const float *colsum_partials, float *colsum_out, const void *warm,
+                                     int64_t warm_bytes, void *stream);
+
 extern "C" int cc_splitk_reduce(int32_t dtype, const float *partials, int32_t splits, int32_t M,
                                 int32_t N, const void *H, void *C, float *Cf,
                                 const float *colsum_partials, float *colsum_out, void *stream) {
+  return cc_splitk_reduce_warm(dtype, partials, splits, M, N, H, C, Cf, colsum_partials, colsum_out,
+                               nullptr, 0, stream);
+}
+
+extern "C" int cc_splitk_reduce_warm(int32_t dtype, const float *partials, int32_t splits, int32_t M,
+                                     int32_t N, const void *H, void *C, float *Cf,
+                                     const float *colsum_partials, float *colsum_out, const void *warm,
+                                     int64_t warm_bytes, void *stream) {
   CC_REQUIRE(partials && splits >= 1, "cc_splitk_reduce: args");
   const int64_t MN = (int64_t)M * N;
   if (MN == 0) return CC_OK;
   const dim3 grid((unsigned)cdiv(MN, 256)), block(256);
   if (dtype == CC_BF16)
     hipLaunchKernelGGL(splitk_reduce_kernel<bf16_t>, grid, block, 0, as_stream(stream), partials,
-                       splits, M, N, (const bf16_t *)H, (bf16_t *)C, Cf, colsum_partials, colsum_out);
+                       splits, M, N, (const bf16_t *)H, (bf16_t *)C, Cf, colsum_partials, colsum_out,
+                       warm, warm_bytes);
   else
     hipLaunchKernelGGL(splitk_reduce_kernel<float>, grid, block, 0, as_stream(stream), partials,
-                       splits, M, N, (const float *)H, (float *)C, Cf, colsum_partials, colsum_out);
+                       splits, M, N, (const float *)H, (float *)C, Cf, colsum_partials, colsum_out,
+                       warm, warm_bytes);
   CC_LAUNCH_CHECK("splitk_reduce_kernel");
   return CC_OK;
 }

@@ -508,9 +508,11 @@ class Trainer:
             t()
         # ---- E (model.py:35-42) on R rows: gather + 3 Dense
         t = self._tick('cc_embed_gather_fwd')
-        L.call('cc_embed_gather_fwd', self.dtype, self.w('encoder/encoded_1/kernel'),
+        wf = self.wpack[0] if self.wpack is not None else None   # warm the tower forward's weights
+        L.call('cc_embed_gather_fwd_warm', self.dtype, self.w('encoder/encoded_1/kernel'),
                self.pf('encoder/encoded_1/bias'), V, d, R, L.ptr(self.x_cnt), L.ptr(self.x_idx),
-               self.x_cap, L.ptr(self.H1), s)
+               self.x_cap, L.ptr(self.H1), L.ptr(wf) if wf is not None else None,
+               2 * wf.numel() if wf is not None else 0, s)
         t()
         branches = [('decoder', (0, B))] + ([('decoder_for_reg', (B, 2 * B))] if self.use_reg else [])
         if self.fused_tower:
@@ -590,8 +592,10 @@ class Trainer:
                     t = self._tick('dec_dX')
                     L.call('cc_gemm', L.C.byref(gx), s)
                     t()
-                    L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), self.splits, B, d,
-                           L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
+                    wb = self.wpack[1] if self.wpack is not None else None   # warm the tower bwd's weights
+                    L.call('cc_splitk_reduce_warm', self.dtype, L.ptr(self.split_buf), self.splits, B, d,
+                           L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None,
+                           L.ptr(wb) if wb is not None else None, 2 * wb.numel() if wb is not None else 0, s)
                     continue
                 gw = self._gemm(d, V, B, **self._dec_dw(k, r0), ta=0, tb=1,
                                 Cf=self.gp(pre + '/reconstruct/kernel'),

@@ -117,6 +117,11 @@ int cc_adam_noise(float *p, float *m, float *v, const float *g, uint16_t *shadow
 int cc_embed_gather_fwd(int32_t dtype, const void *table, const float *bias, int32_t V,
                         int32_t d, int32_t R, const int32_t *x_cnt, const int32_t *x_idx,
                         int32_t x_cap, void *out, void *stream);
+/* cc_embed_gather_fwd + the L2 warm-up of cc_splitk_reduce_warm for the next launch (the tower
+ * forward's packed weights); bf16 d = 256 only does the warm-up, other shapes ignore it. */
+int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const float *bias, int32_t V, int32_t d,
+                             int32_t R, const int32_t *x_cnt, const int32_t *x_idx, int32_t x_cap,
+                             void *out, const void *warm, int64_t warm_bytes, void *stream);
 
 /* ----------------------------------------------------------------------------------
  * E1 backward: dW1[r] = sum_{b : r in x_b} dpre[b] (ascending b, deterministic), for every
@@ -188,6 +193,12 @@ int cc_gemm_grid(int32_t M, int32_t N, int32_t *tiles);
 int cc_splitk_reduce(int32_t dtype, const float *partials, int32_t splits, int32_t M, int32_t N,
                      const void *H, void *C, float *Cf, const float *colsum_partials,
                      float *colsum_out, void *stream);
+/* ... and, at the end of every workgroup, one dword per 128-B line of [warm, warm + warm_bytes)
+ * read by the workgroups of each XCD in turn: the next launch (the tower backward's packed
+ * weights) finds them in every XCD's L2.  Results identical to cc_splitk_reduce. */
+int cc_splitk_reduce_warm(int32_t dtype, const float *partials, int32_t splits, int32_t M, int32_t N,
+                          const void *H, void *C, float *Cf, const float *colsum_partials,
+                          float *colsum_out, const void *warm, int64_t warm_bytes, void *stream);
 
 /* MX-FP8 quantisation (oracle/mx8_ref.py, bit-exact): blocks of 32 along the GEMM K axis, E8M0
  * exponent e = min{e : amax <= 448 * 2^e}, codes = e4m3 RNE of x * 2^-e.  src is [rows][ld_src]
