@@ -14,6 +14,11 @@
 
 #include "common.hpp"
 
+// dev-only timing hook (tools/micro/eg_probe.hip defines it); compiled out of the library
+#ifndef EG_PROBE
+#define EG_PROBE(k)
+#endif
+
 namespace {
 
 // EPL consecutive elements of one table row -> fp32, with the widest aligned vector loads.
@@ -315,19 +320,29 @@ __global__ __launch_bounds__(256, 2) void embed_grad_mfma_kernel(const bf16_t *_
   const int wm = wave >> 1, wn = wave & 1;
   const int v0 = blockIdx.x * EG_ROWS;
   const int XW = (R + 31) >> 5, XWP = RP >> 5;
-  for (int i = tid; i < EG_ROWS * XWP; i += 256) {
-    const int r = i / XWP, w = i % XWP, v = v0 + r;
-    uint32_t m = 0u;
-    if (w < XW) {
-      if (v < V) {
-        uint32_t *src = xt + (int64_t)v * XW + w;
-        m = *src;
-        *src = 0u;  // consumed: the next step's F finds xt zeroed
-      } else if (v == V && bias_grad) {
-        m = (w == XW - 1 && (R & 31)) ? (1u << (R & 31)) - 1u : 0xFFFFFFFFu;
-      }
+  EG_PROBE(0);
+  // the block's bit words: every load issued before any store (one HBM round trip, not one per
+  // word — the zeroing stores would otherwise order each next load behind them)
+  constexpr int AS_Q = EG_ROWS * EG_XWMAX / 256;
+  uint32_t mv[AS_Q];
+#pragma unroll
+  for (int q = 0; q < AS_Q; ++q) {
+    const int i = tid + 256 * q, r = i / XWP, w = i % XWP, v = v0 + r;
+    mv[q] = 0u;
+    if (i < EG_ROWS * XWP && w < XW) {
+      if (v < V)
+        mv[q] = xt[(int64_t)v * XW + w];
+      else if (v == V && bias_grad)
+        mv[q] = (w == XW - 1 && (R & 31)) ? (1u << (R & 31)) - 1u : 0xFFFFFFFFu;
     }
-    As[r][w] = m;
+  }
+#pragma unroll
+  for (int q = 0; q < AS_Q; ++q) {
+    const int i = tid + 256 * q, r = i / XWP, w = i % XWP, v = v0 + r;
+    if (i < EG_ROWS * XWP) {
+      if (w < XW && v < V) xt[(int64_t)v * XW + w] = 0u;  // consumed: the next step's F finds xt zeroed
+      As[r][w] = mv[q];
+    }
   }
   const int nk = RP / EG_BK;
   const int arow = wm * 32 + (lane & 31);
@@ -352,6 +367,7 @@ __global__ __launch_bounds__(256, 2) void embed_grad_mfma_kernel(const bf16_t *_
     __syncthreads();  // As visible; previous chunk's readers of Bs are done
     EG_STORE(0)
     __syncthreads();
+    EG_PROBE(1);
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) { EG_LOAD(kt + 1) }
       const bf16_t *bs = Bs[kt & 1];
@@ -368,6 +384,7 @@ __global__ __launch_bounds__(256, 2) void embed_grad_mfma_kernel(const bf16_t *_
       }
       if (kt + 1 < nk) { EG_STORE((kt + 1) & 1) }
       __syncthreads();
+      EG_PROBE(2 + kt);
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -382,6 +399,7 @@ __global__ __launch_bounds__(256, 2) void embed_grad_mfma_kernel(const bf16_t *_
       }
     }
   }
+  EG_PROBE(15);
 #undef EG_LOAD
 #undef EG_STORE
 }
