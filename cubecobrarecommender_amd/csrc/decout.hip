@@ -40,7 +40,8 @@ struct DecOutP {
   const bf16_t *D3t;       // [d][ldt]
   const bf16_t *D3p;       // optional packed A images (cc_tower_args.act6p / act6tp; ldt rows)
   const bf16_t *D3tp;
-  const bf16_t *WoT;       // [V][d]
+  const bf16_t *WoT;       // [V][d], or null: the slice is transposed from Wo in LDS
+  const bf16_t *Wo;        // [d][V] (the bf16 shadow of the reconstruct kernel)
   const float *bo;         // [V]
   const uint32_t *y_bits;  // [B][ceil(V/32)]
   bf16_t *dZ;              // [B][V]
@@ -95,10 +96,30 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     constexpr int NW = NB * CHD / NTH, NY = (B * NJ + NTH - 1) / NTH;
     v4u wv[NW];
     uint32_t yv[NY];
+    // from Wo [d][V]: chunk c = (k, 8 consecutive columns); columns past V clamp to V - 1
+    constexpr int CN = NB / 8;  // 16-B column chunks per Wo row segment
+    const bool fromWo = p.WoT == nullptr;
+    const bool vec = fromWo && (V % 8 == 0) && n0 + NB <= V;
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
-      const int c = tid + NTH * q, n = c / CHD, ch = c % CHD;
-      wv[q] = *reinterpret_cast<const v4u *>(p.WoT + (int64_t)min(n0 + n, V - 1) * d + ch * 8);
+      const int c = tid + NTH * q;
+      if (!fromWo) {
+        const int n = c / CHD, ch = c % CHD;
+        wv[q] = *reinterpret_cast<const v4u *>(p.WoT + (int64_t)min(n0 + n, V - 1) * d + ch * 8);
+      } else if (vec) {
+        const int k = c / CN, nc = c % CN;
+        wv[q] = *reinterpret_cast<const v4u *>(p.Wo + (int64_t)k * V + n0 + nc * 8);
+      } else {  // ragged edge block: element loads
+        const int k = c / CN, nc = c % CN;
+        uint32_t w2[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t lo = p.Wo[(int64_t)k * V + min(n0 + nc * 8 + 2 * e, V - 1)];
+          const uint32_t hi = p.Wo[(int64_t)k * V + min(n0 + nc * 8 + 2 * e + 1, V - 1)];
+          w2[e] = lo | (hi << 16);
+        }
+        wv[q] = v4u{w2[0], w2[1], w2[2], w2[3]};
+      }
     }
 #pragma unroll
     for (int q = 0; q < NY; ++q) {
@@ -108,8 +129,16 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
-      const int c = tid + NTH * q, n = c / CHD, ch = c % CHD;
-      *reinterpret_cast<v4u *>(Wt + sw_off(n, ch * 8, CHD)) = wv[q];
+      const int c = tid + NTH * q;
+      if (!fromWo) {
+        const int n = c / CHD, ch = c % CHD;
+        *reinterpret_cast<v4u *>(Wt + sw_off(n, ch * 8, CHD)) = wv[q];
+      } else {  // transpose: element e of chunk (k, nc) -> Wt[nc * 8 + e][k]
+        const int k = c / CN, nc = c % CN;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          Wt[sw_off(nc * 8 + e, k, CHD)] = (bf16_t)(wv[q][e >> 1] >> (16 * (e & 1)));
+      }
     }
 #pragma unroll
     for (int q = 0; q < NY; ++q)
@@ -318,17 +347,18 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 }  // namespace
 
 extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const void *D3p,
-                             const void *D3tp, const void *WoT,
+                             const void *D3tp, const void *WoT, const void *Wo,
                              const float *bo, int32_t B, int32_t d, int32_t V, const uint32_t *y_bits,
                              void *dZ, float *gW, float *gb, double *loss_partials, double *loss_out,
                              double loss_scale, uint32_t *ticket, void *stream) {
-  CC_REQUIRE(D3 && D3t && WoT && bo && y_bits && dZ && gW && gb && loss_partials,
+  CC_REQUIRE(D3 && D3t && (WoT || Wo) && bo && y_bits && dZ && gW && gb && loss_partials,
              "cc_dec_bce_dw: null pointer");
   CC_REQUIRE(B == 128 || B == 256 || B == 512, "cc_dec_bce_dw: B must be 128, 256 or 512");
   CC_REQUIRE(d == 128 || d == 256, "cc_dec_bce_dw: d must be 128 or 256");
   CC_REQUIRE(V > 0 && ldt >= B && ldt % 8 == 0, "cc_dec_bce_dw: V > 0, ldt >= B, ldt % 8 == 0");
   CC_REQUIRE(!loss_out || ticket, "cc_dec_bce_dw: loss_out needs a ticket word");
-  CC_REQUIRE((((uintptr_t)D3 | (uintptr_t)D3t | (uintptr_t)WoT) & 15) == 0, "cc_dec_bce_dw: operands 16-B aligned");
+  CC_REQUIRE((((uintptr_t)D3 | (uintptr_t)D3t | (uintptr_t)WoT | (uintptr_t)Wo) & 15) == 0,
+             "cc_dec_bce_dw: operands 16-B aligned");
   DecOutP p;
   p.D3 = (const bf16_t *)D3;
   p.D3t = (const bf16_t *)D3t;
@@ -337,6 +367,7 @@ extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const
   CC_REQUIRE(!D3tp || ldt % 16 == 0, "cc_dec_bce_dw: packed D3^T needs ldt % 16 == 0");
   CC_REQUIRE((((uintptr_t)D3p | (uintptr_t)D3tp) & 15) == 0, "cc_dec_bce_dw: packed images 16-B aligned");
   p.WoT = (const bf16_t *)WoT;
+  p.Wo = (const bf16_t *)Wo;
   p.bo = bo;
   p.y_bits = y_bits;
   p.dZ = (bf16_t *)dZ;

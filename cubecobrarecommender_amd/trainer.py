@@ -388,6 +388,8 @@ class Trainer:
         (bf16), or with fp8 the MX-FP8 images Wo^T [V][d] (forward) and Wo [d][Vp] (dX)."""
         d, V = self.cfg.d, self.cfg.V
         for k, pre in enumerate(branches_of(self.use_reg)):
+            if k == 0 and self.fused_out and not getattr(self, "fused_adam", False):
+                continue    # cc_dec_bce_dw reads Wo itself: no Wo^T copy for the D1 branch
             if self.mx8:
                 L.call('cc_quant_mx8', L.CC_BF16, self.w(pre + '/reconstruct/kernel'), d, V, V, 1,
                        L.ptr(self.WoT8[k]), d, L.ptr(self.WoT8s[k]), None, s)
@@ -537,7 +539,8 @@ class Trainer:
         if self.fused_out:     # logits + BCE + dZ + dWo/dbo in one pass (csrc/decout.hip)
             L.call('cc_dec_bce_dw', L.ptr(self.D3), L.ptr(self.D3t), R,
                    L.ptr(self.D3p) if self.D3p is not None else None,
-                   L.ptr(self.D3tp) if self.D3p is not None else None, L.ptr(self.WoT[0]),
+                   L.ptr(self.D3tp) if self.D3p is not None else None, None,
+                   self.w('decoder/reconstruct/kernel'),   # Wo [d][V]: slices transposed in LDS
                    self.pf('decoder/reconstruct/bias'), B, d, V, L.ptr(self.y_bits), L.ptr(self.dZout),
                    self.gp('decoder/reconstruct/kernel'), self.gp('decoder/reconstruct/bias'),
                    L.ptr(self.bce_part), L.ptr(self.loss_dev), 1.0 / (B * V), L.ptr(self.tickets), s)

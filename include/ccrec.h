@@ -287,13 +287,15 @@ int cc_dec_bce_fused(int32_t dtype, const void *H3, const void *Wo, const float 
                      int32_t B, int32_t d, int32_t V, const uint32_t *y_bits, void *dZ,
                      double *loss_partials, int32_t *n_partials, void *stream);
 /* D1 output layer in one pass (bf16; B in {128, 256, 512}, d in {128, 256}): per 96-column
- * slice of V, logits z = D3 Wo + bo (Wo as Wo^T [V][d]), dZ = (sigmoid(z) - y)/(B*V) written
+ * slice of V, logits z = D3 Wo + bo (Wo as Wo^T [V][d]; with WoT NULL the [d][V] weights Wo
+ * themselves, each block transposing its slice in LDS — no Wo^T copy to refresh after Adam;
+ * D3p / D3tp: optional packed operand images, cc_tower_args.act6p / act6tp), dZ = (sigmoid(z) - y)/(B*V) written
  * row-major [B][V] (for the dX product), and dWo [d][V] = D3^T dZ (D3t = D3^T [d][ldt]) and
  * dbo = colsum dZ from the block's LDS copy of dZ^T — no dZ^T in HBM, no separate dW launch.
  * loss_partials: cc_dec_bce_dw_blocks(V) doubles; loss_out (optional, with ticket) =
  * sum(partials) * loss_scale reduced by the last block. */
 int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const void *D3p, const void *D3tp,
-                  const void *WoT, const float *bo,
+                  const void *WoT, const void *Wo, const float *bo,
                   int32_t B, int32_t d, int32_t V, const uint32_t *y_bits, void *dZ, float *gW,
                   float *gb, double *loss_partials, double *loss_out, double loss_scale,
                   uint32_t *ticket, void *stream);

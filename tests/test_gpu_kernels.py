@@ -405,18 +405,26 @@ def test_dec_bce_dw_matches_unfused(B, d, V):
     part = torch.zeros(nblk, device='cuda', dtype=torch.float64)
     loss = torch.zeros(1, device='cuda', dtype=torch.float64)
     tick = torch.zeros(1, device='cuda', dtype=torch.int32)
-    L.call('cc_dec_bce_dw', L.ptr(D3), L.ptr(D3t), B, None, None, L.ptr(WoT), L.ptr(bo), B, d, V, L.ptr(ybits),
+    L.call('cc_dec_bce_dw', L.ptr(D3), L.ptr(D3t), B, None, None, L.ptr(WoT), None, L.ptr(bo), B, d, V, L.ptr(ybits),
            L.ptr(dZ), L.ptr(gW), L.ptr(gb), L.ptr(part), L.ptr(loss), scale, L.ptr(tick), L.stream_ptr())
     # the fragment-packed operand images (cc_tower_args.act6p / act6tp) give identical results
     D3p = D3.view(B // 32, 32, d // 16, 2, 8).permute(0, 2, 3, 1, 4).contiguous()
     D3tp = D3t.view(d // 32, 32, B // 16, 2, 8).permute(0, 2, 3, 1, 4).contiguous()
     dZp, gWp, gbp = torch.zeros_like(dZ), torch.zeros_like(gW), torch.zeros_like(gb)
     lossp = torch.zeros_like(loss)
-    L.call('cc_dec_bce_dw', L.ptr(D3), L.ptr(D3t), B, L.ptr(D3p), L.ptr(D3tp), L.ptr(WoT), L.ptr(bo), B, d, V,
+    L.call('cc_dec_bce_dw', L.ptr(D3), L.ptr(D3t), B, L.ptr(D3p), L.ptr(D3tp), L.ptr(WoT), None, L.ptr(bo), B, d, V,
            L.ptr(ybits), L.ptr(dZp), L.ptr(gWp), L.ptr(gbp), L.ptr(part), L.ptr(lossp), scale, L.ptr(tick),
            L.stream_ptr())
     torch.cuda.synchronize()
     assert torch.equal(dZ, dZp) and torch.equal(gW, gWp) and torch.equal(gb, gbp) and torch.equal(loss, lossp)
+    # ... and so does reading Wo [d][V] itself (slice transposed in LDS) instead of the Wo^T copy
+    Wo = WoT.t().contiguous()
+    dZw, gWw, gbw, lossw = torch.zeros_like(dZ), torch.zeros_like(gW), torch.zeros_like(gb), torch.zeros_like(loss)
+    L.call('cc_dec_bce_dw', L.ptr(D3), L.ptr(D3t), B, L.ptr(D3p), L.ptr(D3tp), None, L.ptr(Wo), L.ptr(bo), B, d, V,
+           L.ptr(ybits), L.ptr(dZw), L.ptr(gWw), L.ptr(gbw), L.ptr(part), L.ptr(lossw), scale, L.ptr(tick),
+           L.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dZ, dZw) and torch.equal(gW, gWw) and torch.equal(gb, gbw) and torch.equal(loss, lossw)
     # unfused
     dZ2 = torch.zeros(B, V, **bf)
     dZt = torch.zeros(V, B, **bf)

@@ -29,11 +29,15 @@ def _setup(V, d, B, C, reg, dtype, seed=3, sizes=(20, 40, 80), fused_tower=True,
 @pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
 @pytest.mark.parametrize('reg', [0.0, 0.1])
 @pytest.mark.parametrize('V,d,B,fused', [(700, 64, 32, True), (2500, 128, 64, True), (2500, 256, 64, True),
-                                         (700, 64, 32, False), (2500, 128, 48, True)])
+                                         (700, 64, 32, False), (2500, 128, 48, True), (2500, 256, 128, True),
+                                         (2500, 128, 128, True)])
 def test_train_steps_match_oracle(dtype, reg, V, d, B, fused):
     C = 4 * B
     tr, lists, Mt, ns, P, perm = _setup(V, d, B, C, reg, dtype, fused_tower=fused)
     assert tr.fused_tower == (fused and B % 32 == 0)
+    if dtype == 'bf16' and B in (128, 256, 512) and d in (128, 256):
+        # the bench's path: fused D1 output kernel reading Wo, packed tower and D3 images
+        assert tr.fused_out and tr.wpack is not None and tr.D3p is not None
     cdf = noise_ref.cdf_of(ns)
     Mo = {k: np.zeros_like(v) for k, v in P.items()}
     Vo = {k: np.zeros_like(v) for k, v in P.items()}

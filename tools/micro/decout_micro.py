@@ -27,7 +27,7 @@ PK = [None, None]
 
 
 def run():
-    L.call('cc_dec_bce_dw', L.ptr(D3), L.ptr(D3t), B, PK[0], PK[1], L.ptr(WoT), L.ptr(bo), B, d, V, L.ptr(ybits),
+    L.call('cc_dec_bce_dw', L.ptr(D3), L.ptr(D3t), B, PK[0], PK[1], L.ptr(WoT), None, L.ptr(bo), B, d, V, L.ptr(ybits),
            L.ptr(dZ), L.ptr(gW), L.ptr(gb), L.ptr(part), L.ptr(loss), 1.0 / (B * V), L.ptr(tick),
            L.stream_ptr())
 
