@@ -58,6 +58,11 @@ class TowerArgs(C.Structure):
     ]
 
 
+class AdamPack(C.Structure):
+    _fields_ = [('n', C.c_int32), ('K', C.c_int32 * 9), ('N', C.c_int32 * 9), ('off', C.c_int64 * 9),
+                ('wpf', C.c_void_p * 9), ('wpb', C.c_void_p * 9)]
+
+
 _P, _I32, _I64, _F32, _F64, _SZ = C.c_void_p, C.c_int32, C.c_int64, C.c_float, C.c_double, C.c_size_t
 
 # name -> (restype, argtypes); every symbol include/ccrec.h declares
@@ -68,7 +73,8 @@ SIGNATURES = {
     'cc_crc32c': (C.c_uint32, [C.c_uint32, _P, _SZ]),
     'cc_noise_fwd': (C.c_int, [C.POINTER(NoiseArgs), _P]),
     'cc_embed_gather_fwd': (C.c_int, [_I32, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P]),
-    'cc_embed_gather_fwd_warm': (C.c_int, [_I32, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _I64, _P]),
+    'cc_embed_gather_fwd_warm': (C.c_int, [_I32, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _I64, _P, _I64,
+                                           _P]),
     'cc_embed_scatter_bwd': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_embed_grad_mfma': (C.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_gemm': (C.c_int, [C.POINTER(GemmArgs), _P]),
@@ -85,6 +91,8 @@ SIGNATURES = {
     'cc_dec_softmax_kl_fused': (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _F32, _P, _P, _P]),
     'cc_reduce_loss': (C.c_int, [_P, _I32, _F64, _P, _P]),
     'cc_adam_noise': (C.c_int, [_P, _P, _P, _P, _P, _I64, _F32, _F32, _F32, _F32, C.POINTER(NoiseArgs), _I64, _P]),
+    'cc_adam_noise_pack': (C.c_int, [_P, _P, _P, _P, _P, _I64, _F32, _F32, _F32, _F32, C.POINTER(NoiseArgs), _I64,
+                                     C.POINTER(AdamPack), _P]),
     'cc_adam_dense': (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _F32, _F32, _F32, _F32, _P]),
     'cc_adam_dense_t': (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _F32, _F32, _F32, _F32, _P, _I32,
                                   _I64, _P]),

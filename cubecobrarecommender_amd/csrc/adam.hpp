@@ -9,6 +9,7 @@ namespace cc_adam {
 
 __device__ __forceinline__ void elem(float &p, float &m, float &v, float g, float alpha,
                                      float omb1, float omb2, float eps) {
+#pragma clang fp contract(off)  // every kernel that inlines this rounds identically (no FMA choice)
   m += (g - m) * omb1;
   v += (g * g - v) * omb2;
   p -= (m * alpha) / (sqrtf(v) + eps);
@@ -22,8 +23,42 @@ struct Args {
   float lr, b1, b2, eps;
 };
 
+// Fragment-packed tower images (cc_adam_pack): the bf16 values of float4 group e..e+3 (one row
+// k, columns n..n+3 of layer l) go to the forward image (rows n, reduction k: 4 scattered 2-B
+// stores) and the backward image (rows k, reduction n: one 8-B store).  Same element order as
+// tower.hip's pack_off.
+struct Pack {
+  int n;
+  int K[9], N[9];
+  int64_t off[9];
+  bf16_t *wpf[9], *wpb[9];
+  int64_t lo, hi;  // [lo, hi) covers every packed layer
+};
+__device__ __forceinline__ int64_t frag_off(int t, int j, int lane, int red) {
+  return (((int64_t)t * (red / 16) + j) * 64 + lane) * 8;
+}
+__device__ __forceinline__ void pack4(const Pack &pk, int64_t e, const bf16_t (&b)[4]) {
+  if (e < pk.lo || e >= pk.hi) return;
+  for (int l = 0; l < pk.n; ++l) {
+    const int64_t o = e - pk.off[l];
+    const int K = pk.K[l], N = pk.N[l];
+    if (o < 0 || o >= (int64_t)K * N) continue;
+    const int k = (int)(o / N), n = (int)(o % N);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int nn = n + q;
+      pk.wpf[l][frag_off(nn >> 5, k >> 4, (nn & 31) + 32 * ((k >> 3) & 1), K) + (k & 7)] = b[q];
+    }
+    const int64_t ob = frag_off(k >> 5, n >> 4, (k & 31) + 32 * ((n >> 3) & 1), N) + (n & 7);
+    *reinterpret_cast<uint2 *>(pk.wpb[l] + ob) =
+        make_uint2((uint32_t)b[0] | ((uint32_t)b[1] << 16), (uint32_t)b[2] | ((uint32_t)b[3] << 16));
+    return;
+  }
+}
+
 // Blocks [0, nblocks) of whatever grid run this cover [0, n) grid-stride (float4 body + tail).
-__device__ __forceinline__ void range(const Args &a, int64_t step, int bid, int nblocks) {
+__device__ __forceinline__ void range(const Args &a, int64_t step, int bid, int nblocks,
+                                      const Pack *pk = nullptr) {
   const float t = (float)(step + 1);
   const float b1p = powf(a.b1, t), b2p = powf(a.b2, t);
   const float alpha = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
@@ -49,6 +84,10 @@ __device__ __forceinline__ void range(const Args &a, int64_t step, int bid, int 
       s.z = f2bf(pp.z);
       s.w = f2bf(pp.w);
       reinterpret_cast<ushort4 *>(a.shadow)[i] = s;
+      if (pk) {
+        const bf16_t b4[4] = {s.x, s.y, s.z, s.w};
+        pack4(*pk, i << 2, b4);
+      }
     }
   }
   for (int64_t i = (n4 << 2) + (int64_t)bid * blockDim.x + threadIdx.x; i < a.n; i += stride) {

@@ -141,7 +141,15 @@ __global__ __launch_bounds__(64 * GWN) void gather2_kernel(const bf16_t *__restr
                                                           const int32_t *__restrict__ x_cnt,
                                                           const int32_t *__restrict__ x_idx, int x_cap,
                                                           bf16_t *__restrict__ out, const void *warm,
-                                                          int64_t warm_bytes) {
+                                                          int64_t warm_bytes, int64_t *state, int64_t bpe) {
+  if (state && blockIdx.x == 0 && threadIdx.x == 0) {  // the previous step's counters
+    state[0] += 1;
+    state[1] += 1;
+    if (state[1] >= bpe) {
+      state[1] = 0;
+      state[2] += 1;
+    }
+  }
   constexpr int D = 256;
   __shared__ __attribute__((aligned(16))) float part[GWN][D];
   __shared__ int32_t ls[GIDX];
@@ -409,18 +417,30 @@ __global__ __launch_bounds__(256, 2) void embed_grad_mfma_kernel(const bf16_t *_
 extern "C" int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const float *bias, int32_t V,
                                         int32_t d, int32_t R, const int32_t *x_cnt,
                                         const int32_t *x_idx, int32_t x_cap, void *out,
-                                        const void *warm, int64_t warm_bytes, void *stream);
+                                        const void *warm, int64_t warm_bytes, int64_t *state,
+                                        int64_t bpe, void *stream);
 
 extern "C" int cc_embed_gather_fwd(int32_t dtype, const void *table, const float *bias, int32_t V,
                                    int32_t d, int32_t R, const int32_t *x_cnt,
                                    const int32_t *x_idx, int32_t x_cap, void *out, void *stream) {
-  return cc_embed_gather_fwd_warm(dtype, table, bias, V, d, R, x_cnt, x_idx, x_cap, out, nullptr, 0, stream);
+  return cc_embed_gather_fwd_warm(dtype, table, bias, V, d, R, x_cnt, x_idx, x_cap, out, nullptr, 0, nullptr, 1,
+                                  stream);
 }
 
 extern "C" int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const float *bias, int32_t V,
                                         int32_t d, int32_t R, const int32_t *x_cnt,
                                         const int32_t *x_idx, int32_t x_cap, void *out,
-                                        const void *warm, int64_t warm_bytes, void *stream) {
+                                        const void *warm, int64_t warm_bytes, int64_t *state,
+                                        int64_t bpe, void *stream) {
+  CC_REQUIRE(!state || bpe >= 1, "cc_embed_gather_fwd_warm: batches_per_epoch");
+  static const int g2 = [] {  // A/B switch (dev): 16-B lanes, two rows per load; waves x loads
+    const char *e = getenv("CCREC_GATHER2");
+    return e ? atoi(e) : 48;
+  }();
+  if (state && !(dtype == CC_BF16 && d == 256 && g2 > 0)) {  // other kernels: a separate launch
+    if (int rc = cc_state_advance(state, bpe, stream)) return rc;
+    state = nullptr;
+  }
   CC_REQUIRE(table && bias && x_cnt && x_idx && out, "cc_embed_gather_fwd: null pointer");
   CC_REQUIRE(d % 64 == 0 && d >= 64 && d <= 1024, "cc_embed_gather_fwd: d must be 64..1024, %64");
   CC_REQUIRE(V > 0 && R >= 0 && x_cap > 0, "cc_embed_gather_fwd: bad sizes");
@@ -428,15 +448,11 @@ extern "C" int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const 
   const dim3 grid((unsigned)R), block(256);
   const int epl = d / 64;
   hipStream_t s = as_stream(stream);
-  static const int g2 = [] {  // A/B switch (dev): 16-B lanes, two rows per load; waves x loads
-    const char *e = getenv("CCREC_GATHER2");
-    return e ? atoi(e) : 48;
-  }();
   if (dtype == CC_BF16 && d == 256 && g2 > 0) {
 #define G2(GWN, U) \
   if (g2 == GWN * 10 + U) hipLaunchKernelGGL((gather2_kernel<GWN, U>), grid, dim3(64 * GWN), 0, s, \
                                              (const bf16_t *)table, bias, R, x_cnt, x_idx, x_cap, (bf16_t *)out, \
-                                             warm, warm_bytes);
+                                             warm, warm_bytes, state, bpe);
     G2(4, 4) G2(4, 8) G2(8, 4) G2(8, 8) G2(4, 6) G2(8, 6)
 #undef G2
     CC_LAUNCH_CHECK("gather2_kernel");

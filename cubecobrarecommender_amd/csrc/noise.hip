@@ -234,23 +234,24 @@ __global__ __launch_bounds__(NT) void noise_kernel(cc_noise_args a) {
 // NEXT step (its {step, batch, epoch} = this step's advanced as cc_state_advance will): Adam is
 // HBM-bound, F latency-bound, and F touches only the batch buffers this step's backward has
 // released — one launch instead of F on the next step's critical path.
+template <bool PACK>
 __global__ __launch_bounds__(NT) void adam_noise_kernel(cc_adam::Args ad, cc_noise_args a,
-                                                        int nadam, int64_t bpe) {
+                                                        int nadam, int64_t bpe, cc_adam::Pack pk) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   __shared__ int s_k;
   // F's blocks come first: they are latency-bound chains that should start at once, the Adam
   // blocks stream around them
   const int64_t step = a.state[0];
   if ((int)blockIdx.x >= a.B) {
-    cc_adam::range(ad, step, (int)blockIdx.x - a.B, nadam);
-    return;
+    cc_adam::range(ad, step, (int)blockIdx.x - a.B, nadam, PACK ? &pk : nullptr);
+  } else {
+    int64_t batch = a.state[1] + 1, epoch = a.state[2];
+    if (batch >= bpe) {
+      batch = 0;
+      epoch += 1;
+    }
+    noise_block(a, smem, s_k, blockIdx.x, step + 1, batch, epoch);
   }
-  int64_t batch = a.state[1] + 1, epoch = a.state[2];
-  if (batch >= bpe) {
-    batch = 0;
-    epoch += 1;
-  }
-  noise_block(a, smem, s_k, blockIdx.x, step + 1, batch, epoch);
 }
 
 }  // namespace
@@ -291,8 +292,46 @@ extern "C" int cc_adam_noise(float *p, float *m, float *v, const float *g, uint1
   // around F's latency-bound blocks (measured in step: 61 us vs 66-72 with a 2048-block grid)
   const int nadam = n > 0 ? (int)cdiv(cdiv(n, 4), NT) : 0;
   const cc_adam::Args ad{p, m, v, g, (bf16_t *)shadow, n, lr, beta1, beta2, eps};
-  hipLaunchKernelGGL(adam_noise_kernel, dim3((unsigned)(nadam + next->B)), dim3(NT), lds,
-                     as_stream(stream), ad, *next, nadam, batches_per_epoch);
+  hipLaunchKernelGGL(adam_noise_kernel<false>, dim3((unsigned)(nadam + next->B)), dim3(NT), lds,
+                     as_stream(stream), ad, *next, nadam, batches_per_epoch, cc_adam::Pack{});
   CC_LAUNCH_CHECK("adam_noise_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_adam_noise_pack(float *p, float *m, float *v, const float *g, uint16_t *shadow,
+                                  int64_t n, float lr, float beta1, float beta2, float eps,
+                                  const cc_noise_args *next, int64_t batches_per_epoch,
+                                  const cc_adam_pack *pack, void *stream) {
+  CC_REQUIRE(p && m && v && g && shadow && pack, "cc_adam_noise_pack: null pointer");
+  CC_REQUIRE(((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g) % 16 == 0,
+             "cc_adam_noise_pack: buffers must be 16-byte aligned");
+  CC_REQUIRE((uintptr_t)shadow % 8 == 0, "cc_adam_noise_pack: shadow must be 8-byte aligned");
+  CC_REQUIRE(batches_per_epoch >= 1, "cc_adam_noise_pack: batches_per_epoch");
+  CC_REQUIRE(pack->n >= 1 && pack->n <= 9, "cc_adam_noise_pack: 1..9 layers");
+  cc_adam::Pack pk{};
+  pk.n = pack->n;
+  pk.lo = INT64_MAX;
+  pk.hi = 0;
+  for (int l = 0; l < pack->n; ++l) {
+    const int K = pack->K[l], N = pack->N[l];
+    CC_REQUIRE(K % 32 == 0 && N % 32 == 0 && pack->off[l] % 4 == 0 && pack->off[l] >= 0 &&
+                   pack->off[l] + (int64_t)K * N <= n && pack->wpf[l] && pack->wpb[l] &&
+                   (((uintptr_t)pack->wpb[l]) & 7) == 0,
+               "cc_adam_noise_pack: layer shape / offset / image");
+    pk.K[l] = K;
+    pk.N[l] = N;
+    pk.off[l] = pack->off[l];
+    pk.wpf[l] = (bf16_t *)pack->wpf[l];
+    pk.wpb[l] = (bf16_t *)pack->wpb[l];
+    pk.lo = std::min<int64_t>(pk.lo, pack->off[l]);
+    pk.hi = std::max<int64_t>(pk.hi, pack->off[l] + (int64_t)K * N);
+  }
+  size_t lds = 0;
+  if (int rc = noise_check(next, lds)) return rc;
+  const int nadam = n > 0 ? (int)cdiv(cdiv(n, 4), NT) : 0;
+  const cc_adam::Args ad{p, m, v, g, (bf16_t *)shadow, n, lr, beta1, beta2, eps};
+  hipLaunchKernelGGL(adam_noise_kernel<true>, dim3((unsigned)(nadam + next->B)), dim3(NT), lds,
+                     as_stream(stream), ad, *next, nadam, batches_per_epoch, pk);
+  CC_LAUNCH_CHECK("adam_noise_kernel (pack)");
   return CC_OK;
 }

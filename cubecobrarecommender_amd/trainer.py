@@ -281,6 +281,13 @@ class Trainer:
         # already hold the batch the next forward_backward consumes.
         self.prefetch = (cfg.prefetch_noise and cfg.world == 1 and not self.fused_adam
                          and os.environ.get('CCREC_PREFETCH_NOISE', '1') != '0')
+        # one process, packed tower images: the Adam + F launch also rewrites the tower kernels'
+        # packed images and advances the step counters (cc_adam_noise_pack) — the next step
+        # starts without a counters/transposes launch
+        self.adam_packs = (self.prefetch and self.wpack is not None
+                           and os.environ.get('CCREC_ADAM_PACK', '1') != '0')
+        self.adam_pack = self._adam_pack_desc() if self.adam_packs else None
+        self._adv_deferred = False   # the previous step's counter advance rides in the E1 gather
         self.noise_ready = False
         self.perms = None
         self.batches_per_epoch = max(1, data.C // (B * cfg.world))   # generator.py:36 (__len__)
@@ -363,6 +370,17 @@ class Trainer:
         t.gpre1t = self.gPre1T.data_ptr() if self.gPre1T is not None else None
         t.slab = self.slab.data_ptr()
         return t
+
+    def _adam_pack_desc(self):
+        layers = 9 if self.use_reg else 6
+        pk = L.AdamPack(n=layers)
+        for l, name in enumerate(self.tower_layers[:layers]):
+            K, N = self.layout.shape(name + '/kernel')
+            pk.K[l], pk.N[l] = K, N
+            pk.off[l] = self.layout.offset(name + '/kernel')
+            pk.wpf[l] = self.wpack[0, int(self.wt_off[l]):].data_ptr()
+            pk.wpb[l] = self.wpack[1, int(self.wt_off[l]):].data_ptr()
+        return pk
 
     def _adam_regions(self):
         """Row-major weights whose bf16 values the forward reads transposed: the six (nine)
@@ -487,7 +505,7 @@ class Trainer:
     # ------------------------------------------------------------------ the step
     def forward_backward(self, stream=None):
         """One step's gradients into self.grads (no optimizer): F, E, D1/D2 + losses, backward."""
-        self.flush(stream)
+        self.flush(stream, defer=self.noise_ready)   # (F drawn already: nothing reads the counters before E1)
         self.forward_backward_a(stream)
         self.forward_backward_b(stream)
 
@@ -514,7 +532,9 @@ class Trainer:
         L.call('cc_embed_gather_fwd_warm', self.dtype, self.w('encoder/encoded_1/kernel'),
                self.pf('encoder/encoded_1/bias'), V, d, R, L.ptr(self.x_cnt), L.ptr(self.x_idx),
                self.x_cap, L.ptr(self.H1), L.ptr(wf) if wf is not None else None,
-               2 * wf.numel() if wf is not None else 0, s)
+               2 * wf.numel() if wf is not None else 0,
+               L.ptr(self.state) if self._adv_deferred else None, self.batches_per_epoch, s)
+        self._adv_deferred = False
         t()
         branches = [('decoder', (0, B))] + ([('decoder_for_reg', (B, 2 * B))] if self.use_reg else [])
         if self.fused_tower:
@@ -693,9 +713,14 @@ class Trainer:
         t = self._tick('cc_adam_dense')
         if self.prefetch:     # + F for the next step in the same launch
             na = self._noise_args()
-            L.call('cc_adam_noise', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v),
-                   L.ptr(self.grads), L.ptr(self.shadow), n, cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,
-                   L.C.byref(na), self.batches_per_epoch, L.stream_ptr(stream))
+            if self.adam_packs:   # + packed tower images + step counters
+                L.call('cc_adam_noise_pack', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v),
+                       L.ptr(self.grads), L.ptr(self.shadow), n, cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,
+                       L.C.byref(na), self.batches_per_epoch, L.C.byref(self.adam_pack), L.stream_ptr(stream))
+            else:
+                L.call('cc_adam_noise', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v),
+                       L.ptr(self.grads), L.ptr(self.shadow), n, cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,
+                       L.C.byref(na), self.batches_per_epoch, L.stream_ptr(stream))
             self.noise_ready = True
         elif self.fused_adam:   # + transposed operand copies + step counters
             L.call('cc_adam_dense_t', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v),
@@ -708,11 +733,18 @@ class Trainer:
                    L.stream_ptr(stream))
         t()
 
-    def apply_rest(self, stream=None):
+    def apply_rest(self, stream=None, defer=False):
         """Advance the device step/epoch counters and refresh the transposed operand copies
         (the decoder's Wo^T on the side stream, concurrently).  With the fused Adam both are
         already done."""
         if self.fused_adam:
+            return
+        if self.adam_packs:   # packed tower images already written by the Adam launch
+            self.refresh_decoder_operands(L.stream_ptr(stream))
+            if defer:         # counters: in the next forward's E1 gather launch
+                self._adv_deferred = True
+            else:
+                L.call('cc_state_advance', L.ptr(self.state), self.batches_per_epoch, L.stream_ptr(stream))
             return
         if self.fused_tower and stream is None:
             ss = self._fork()
@@ -756,12 +788,13 @@ class Trainer:
             refresh_fn=lambda lo, hi: self.refresh_range(lo, hi),
             timing=timing)
 
-    def flush(self, stream=None):
+    def flush(self, stream=None, defer=False):
         """Run the previous step's deferred counters/transposes (before reading state or the
-        transposed operands from outside the step)."""
+        transposed operands from outside the step).  defer (forward_backward only): the counter
+        advance may ride in the forward's first launch."""
         if self.pending_rest:
             self.pending_rest = False
-            self.apply_rest(stream)
+            self.apply_rest(stream, defer=defer)
 
     def run_fb(self, stream=None):
         """Forward/backward of one step (graph replay or eager), preceded by the previous step's
@@ -843,11 +876,11 @@ class Trainer:
                 g_main, g_all = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
                 self.noise_ready = self.prefetch   # F already drawn by step k's Adam launch
                 with torch.cuda.graph(g_main):
-                    self.apply_rest()
+                    self.apply_rest(defer=True)
                     self.forward_backward()
                 self.noise_ready = self.prefetch
                 with torch.cuda.graph(g_all):
-                    self.apply_rest()
+                    self.apply_rest(defer=True)
                     self.forward_backward()
                     self.apply_adam()
         torch.cuda.synchronize()

@@ -108,6 +108,21 @@ int cc_noise_fwd(const cc_noise_args *a, void *stream);
 int cc_adam_noise(float *p, float *m, float *v, const float *g, uint16_t *shadow, int64_t n,
                   float lr, float beta1, float beta2, float eps, const cc_noise_args *next,
                   int64_t batches_per_epoch, void *stream);
+/* cc_adam_noise that also writes the updated bf16 values of the tower kernels into their
+ * fragment-packed images (cc_tower_args.wpf / wpb order), so no cc_tower_transpose launch is
+ * needed before the next forward (the step counters are then advanced by
+ * cc_embed_gather_fwd_warm's state argument).  pack->off[l] is the element offset of layer l's
+ * [K][N] kernel in the flat buffers. */
+typedef struct cc_adam_pack {
+  int32_t n;             /* layers (<= 9) */
+  int32_t K[9], N[9];
+  int64_t off[9];
+  void *wpf[9];
+  void *wpb[9];
+} cc_adam_pack;
+int cc_adam_noise_pack(float *p, float *m, float *v, const float *g, uint16_t *shadow, int64_t n,
+                       float lr, float beta1, float beta2, float eps, const cc_noise_args *next,
+                       int64_t batches_per_epoch, const cc_adam_pack *pack, void *stream);
 
 /* ----------------------------------------------------------------------------------
  * E1 forward: H[r] = ReLU(sum_{j in x_r} W1[j] + b1).  Replaces Dense(d)(x) on the 0/1
@@ -118,10 +133,13 @@ int cc_embed_gather_fwd(int32_t dtype, const void *table, const float *bias, int
                         int32_t d, int32_t R, const int32_t *x_cnt, const int32_t *x_idx,
                         int32_t x_cap, void *out, void *stream);
 /* cc_embed_gather_fwd + the L2 warm-up of cc_splitk_reduce_warm for the next launch (the tower
- * forward's packed weights); bf16 d = 256 only does the warm-up, other shapes ignore it. */
+ * forward's packed weights; bf16 d = 256 only, other shapes ignore it) and, with state non-NULL,
+ * the previous step's cc_state_advance(batches_per_epoch) (nothing in a step reads the counters
+ * before its Adam launch). */
 int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const float *bias, int32_t V, int32_t d,
                              int32_t R, const int32_t *x_cnt, const int32_t *x_idx, int32_t x_cap,
-                             void *out, const void *warm, int64_t warm_bytes, void *stream);
+                             void *out, const void *warm, int64_t warm_bytes, int64_t *state,
+                             int64_t batches_per_epoch, void *stream);
 
 /* ----------------------------------------------------------------------------------
  * E1 backward: dW1[r] = sum_{b : r in x_b} dpre[b] (ascending b, deterministic), for every

@@ -287,3 +287,24 @@ def test_wide_d1024_bf16_steps_match_oracle(reg):
     bad = {k: rel_err(gflat[k], grads[k]) for k in grads if (reg or not k.startswith('decoder_for_reg'))
            and not rel_err(gflat[k], grads[k]) < 2e-2}
     assert not bad, bad
+
+
+def test_adam_pack_images_and_counters():
+    """cc_adam_noise_pack (one-process step at the bench's shape class): after eager and graph
+    steps, the packed tower images written by the Adam launch equal a fresh repack of the bf16
+    shadow, and the counters advanced by the next E1 gather equal the step count."""
+    tr = _setup(2500, 256, 128, 1024, 0.0, 'bf16')[0]
+    assert tr.adam_packs and tr.fused_out
+    for _ in range(3):
+        tr.step()
+    tr.capture()
+    for _ in range(5):
+        tr.step()
+    torch.cuda.synchronize()
+    got = tr.wpack.clone()
+    tr.flush()
+    st = tr.state.cpu().numpy()
+    assert st[0] == 8 and st[1] == 8 % tr.batches_per_epoch and st[2] == 8 // tr.batches_per_epoch, st
+    tr.transpose_tower()
+    torch.cuda.synchronize()
+    assert torch.equal(got, tr.wpack)
