@@ -41,7 +41,7 @@ def parse():
                     help="collective backend for --gpus > 1 (nccl = RCCL; gloo only to rehearse the "
                          "data-parallel path with several ranks on one GPU)")
     ap.add_argument('--traffic-json', default=os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                                           'profiles', 'traffic_r01e.json'))
+                                                           'profiles', 'traffic_r01g.json'))
     return ap.parse_args()
 
 
@@ -265,7 +265,11 @@ def main():
                 'unit': 'GB/s', 'bytes_per_launch': byt, 'traffic': None,
                 'measured': 'HIP events around the sharded Adam kernels on the comm stream (sum per step)'}
     roof['frac'] = roof['achieved'] / roof['peak']
-    if world == 1 and getattr(tr, 'prefetch', False):
+    if world == 1 and getattr(tr, 'adam_packs', False):
+        roof['kernel'] = ('adam_noise_kernel<true> (cc_adam_noise_pack: TF Adam over all parameters + F '
+                          'of the next step + the tower kernels\' packed bf16 images in the same launch; '
+                          'bytes counted are Adam\'s only, F and the images add <2%)')
+    elif world == 1 and getattr(tr, 'prefetch', False):
         roof['kernel'] = ('adam_noise_kernel (cc_adam_noise: TF Adam over all parameters + F of the '
                           'next step in the same launch; bytes counted are Adam\'s only, F adds <2%)')
     elif world == 1 and getattr(tr, 'fused_adam', False):
