@@ -424,13 +424,13 @@ __device__ __forceinline__ float bce_dz(float z, uint32_t ybit, float scale, flo
 template <int EPI, int BM, typename T = bf16_t>
 __device__ __forceinline__ void nt_body(const GemmParams &p, int tiles_m, int bid, int nblk,
                                         int split, char *smem, uint32_t (*ys)[NBN / 32],
-                                        double *red, int &lastflag) {
+                                        double *red, int &lastflag, bool mapped = false) {
   using C = NtCfg<BM, T>;
   constexpr bool kBceRegs = BM <= 128;  // BCE math on the accumulators (no register pressure)
   constexpr int BK = C::BK, NTH = C::NTH;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
-  const int tile = xcd_tile(bid, nblk);
+  const int tile = mapped ? bid : xcd_tile(bid, nblk);
   // BCE: block-sum the loss and publish it as this tile's partial; with loss_out, an sc1 store
   // + agent ticket (MI355X guide hand-off: no L2 writeback fence) tells the last block to reduce.
   // Called before the epilogue's global stores, so the vmcnt wait has nothing else to drain.
@@ -678,13 +678,29 @@ __device__ __forceinline__ void nt_body(const GemmParams &p, int tiles_m, int bi
   }
 }
 
+// Split-K launches: the (split, tile) pairs are dealt to the XCDs in contiguous split-major runs,
+// so every tile of one K-split runs on one XCD and the split's A and B panels come from beyond
+// L2 once per XCD (tile-only remapping pinned each tile to one XCD across all splits, so the
+// panels shared by a split's tiles were fetched once per tile: 113 MB vs ~50 MB per dX product).
+__device__ __forceinline__ void split_pair(int lin, int nb, int splits, int &tile, int &split) {
+  const int q = xcd_tile(lin, nb * splits);
+  split = q / nb;
+  tile = q % nb;
+}
+
 template <int EPI, int BM>
 __global__ __launch_bounds__(NtCfg<BM>::NTH) void gemm_nt_bf16_kernel(GemmParams p, int tiles_m) {
   __shared__ __attribute__((aligned(16))) char smem[NtCfg<BM>::LDS];
   __shared__ uint32_t ys[EPI == CC_EPI_BCE ? BM : 1][NBN / 32];  // BCE targets of the tile
   __shared__ double red[NtCfg<BM>::NTH / 64];
   __shared__ int lastflag;
-  nt_body<EPI, BM>(p, tiles_m, blockIdx.x, gridDim.x, blockIdx.y, smem, ys, red, lastflag);
+  if constexpr (EPI == CC_EPI_SPLITK) {
+    int tile, split;
+    split_pair(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x, gridDim.y, tile, split);
+    nt_body<EPI, BM>(p, tiles_m, tile, gridDim.x, split, smem, ys, red, lastflag, true);
+  } else {
+    nt_body<EPI, BM>(p, tiles_m, blockIdx.x, gridDim.x, blockIdx.y, smem, ys, red, lastflag);
+  }
 }
 
 // The same tiles on MX-FP8 operands (128 x 128, K % 128 == 0).
@@ -694,7 +710,13 @@ __global__ __launch_bounds__(256) void gemm_nt_mx8_kernel(GemmParams p, int tile
   __shared__ uint32_t ys[EPI == CC_EPI_BCE ? 128 : 1][NBN / 32];
   __shared__ double red[NtCfg<128, uint8_t>::NTH / 64];
   __shared__ int lastflag;
-  nt_body<EPI, 128, uint8_t>(p, tiles_m, blockIdx.x, gridDim.x, blockIdx.y, smem, ys, red, lastflag);
+  if constexpr (EPI == CC_EPI_SPLITK) {
+    int tile, split;
+    split_pair(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x, gridDim.y, tile, split);
+    nt_body<EPI, 128, uint8_t>(p, tiles_m, tile, gridDim.x, split, smem, ys, red, lastflag, true);
+  } else {
+    nt_body<EPI, 128, uint8_t>(p, tiles_m, blockIdx.x, gridDim.x, blockIdx.y, smem, ys, red, lastflag);
+  }
 }
 
 // Two independent NT problems in one launch (grouped GEMM): blocks [0, nb0*s0) are problem 0's
@@ -711,7 +733,13 @@ __global__ __launch_bounds__(256) void gemm_nt_pair_kernel(GemmParams p0, int tm
   __shared__ int lastflag;
   const int b = blockIdx.x;
   if (b < nb0 * s0) {
-    nt_body<E0, 128, T>(p0, tm0, b % nb0, nb0, b / nb0, smem, ys, red, lastflag);
+    if constexpr (E0 == CC_EPI_SPLITK) {
+      int tile, split;
+      split_pair(b, nb0, s0, tile, split);
+      nt_body<E0, 128, T>(p0, tm0, tile, nb0, split, smem, ys, red, lastflag, true);
+    } else {
+      nt_body<E0, 128, T>(p0, tm0, b % nb0, nb0, b / nb0, smem, ys, red, lastflag);
+    }
   } else {
     const int c = b - nb0 * s0;
     nt_body<E1, 128, T>(p1, tm1, c % nb1, nb1, c / nb1, smem, ys, red, lastflag);
