@@ -55,6 +55,7 @@ class TowerArgs(C.Structure):
         ('gD3', C.c_void_p), ('gact', C.c_void_p * 5), ('gpre1', C.c_void_p), ('slab', C.c_void_p),
         ('gw', C.c_void_p * 9), ('gb', C.c_void_p * 9), ('gpre1t', C.c_void_p),
         ('wpf', C.c_void_p * 9), ('wpb', C.c_void_p * 9), ('act6p', C.c_void_p), ('act6tp', C.c_void_p),
+        ('hpt', C.c_void_p * 6), ('gpt', C.c_void_p * 6),
     ]
 
 

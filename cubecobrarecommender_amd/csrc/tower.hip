@@ -42,7 +42,8 @@ struct TowerP {
   const bf16_t *wpf[9];  // fragment-packed forward / backward weight images (cc_tower_args)
   const bf16_t *wpb[9];
   bf16_t *act6p, *act6tp;  // packed D3 operand images for cc_dec_bce_dw (fast forward only)
-  bool packed;
+  bf16_t *hpt[6], *gpt[6];  // packed transposed H_i / G_i images for the dW kernel (or null)
+  bool packed, dwpacked;
 };
 
 __host__ __device__ inline void chain_dims(int d, int i, int &K, int &N) {
@@ -410,6 +411,20 @@ __device__ __forceinline__ void cols_copy_out(const bf16_t *X, int ldx, bf16_t *
   }
 }
 
+// ... packed transposed (rows = the W features, reduction = batch rows): the block's rows are
+// reduction steps j = r0/16, r0/16 + 1 of fragment columns t = 0 .. W/32-1 (the MFMA operand
+// layout of the dW products, 1 KB per fragment)
+__device__ __forceinline__ void pt_copy_out(const bf16_t *X, int ldx, bf16_t *__restrict__ dst, int W, int R, int r0) {
+  for (int v = threadIdx.x; v < (W / 32) * 2 * 64; v += FNT) {
+    const int ln = v & 63, jj = (v >> 6) & 1, tt = v >> 7;
+    const bf16_t *src = X + (16 * jj + 8 * (ln >> 5)) * ldx + 32 * tt + (ln & 31);
+    uint32_t w4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w4[e] = (uint32_t)src[(2 * e) * ldx] | ((uint32_t)src[(2 * e + 1) * ldx] << 16);
+    *reinterpret_cast<u32v4 *>(dst + pack_off(tt, r0 / 16 + jj, ln, R)) = u32v4{w4[0], w4[1], w4[2], w4[3]};
+  }
+}
+
 constexpr int BIAS_MAX = 256 + 128 + 64 + 128 + 256 + 256;  // the six chain layers' widths, d <= 256
 // offset of chain layer i's bias in the block's LDS bias image (widths 256, 128, 64, 128, 256, d)
 __device__ __forceinline__ int bias_off(int i) {
@@ -461,6 +476,7 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
     if (c < nbias) bsm[c] = bv[q];
   }
   __syncthreads();
+  if (p.dwpacked) pt_copy_out(X0, ldx, p.hpt[0], p.d, p.R, r0);  // H_0 for dW
   TOWER_PROBE(1);
   bf16_t *xin = X0, *xout = X1;
 #pragma unroll
@@ -495,16 +511,8 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
             *reinterpret_cast<const u32v4 *>(xout + (ln & 31) * ldx + 16 * j + 8 * (ln >> 5));
       }
     }
-    if (i == 5 && p.act6tp) {  // D3^T as the dWo A operand: fragments (tt, r0/16 + jj), jj = 0, 1
-      for (int v = threadIdx.x; v < (N / 32) * 2 * 64; v += FNT) {
-        const int ln = v & 63, jj = (v >> 6) & 1, tt = v >> 7;
-        const bf16_t *src = xout + (16 * jj + 8 * (ln >> 5)) * ldx + 32 * tt + (ln & 31);
-        uint32_t w4[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w4[e] = (uint32_t)src[(2 * e) * ldx] | ((uint32_t)src[(2 * e + 1) * ldx] << 16);
-        *reinterpret_cast<u32v4 *>(p.act6tp + pack_off(tt, r0 / 16 + jj, ln, p.R)) = u32v4{w4[0], w4[1], w4[2], w4[3]};
-      }
-    }
+    if (i == 5 && p.act6tp) pt_copy_out(xout, ldx, p.act6tp, N, p.R, r0);  // D3^T: the dWo A operand
+    if (i < 5 && p.dwpacked) pt_copy_out(xout, ldx, p.hpt[i + 1], N, p.R, r0);  // H_{i+1} for dW
     bf16_t *tmp = xin;
     xin = xout;
     xout = tmp;
@@ -536,6 +544,7 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
   issue_layer(5, 1);
   rows_store(rg, p.d, Gr, ldx);
   __syncthreads();
+  if (p.dwpacked) pt_copy_out(Gr, ldx, p.gpt[5], p.d, p.R, r0);  // G_5 for dW
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
     int K, N;
@@ -564,8 +573,10 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
       }
     }
     __syncthreads();
-    if (i > 0)
+    if (i > 0) {
       rows_copy_out(Gr, ldx, reinterpret_cast<bf16_t *>(p.gact[i - 1]), K, r0);
+      if (p.dwpacked) pt_copy_out(Gr, ldx, p.gpt[i - 1], K, p.R, r0);  // G_{i-1} for dW
+    }
     else if (p.gpre1t)  // dPre1^T [d][ceil64(R)] (bf16) for cc_embed_grad_mfma
       cols_copy_out(Gr, ldx, reinterpret_cast<bf16_t *>(p.gpre1t), K, (p.R + 63) & ~63, r0);
   }
@@ -703,6 +714,60 @@ __global__ __launch_bounds__(DW_NT) void tower_dw_tiled_kernel(TowerP p, int rpw
                                 pcs[96 + threadIdx.x];
 }
 
+// dW from the packed transposed images: one wave per 32x32 tile of one layer, dW[k0.., n0..] =
+// sum over the layer's rows of H^T G as a chain of v_mfma_f32_32x32x16_bf16 whose A / B fragments
+// are whole 1 KB runs of hpt / gpt (no LDS staging, no cross-wave reduce); db from the same B
+// fragments on the k0 == 0 tiles.  Rows in order: deterministic.
+constexpr int DWP_U = 8;  // fragment pairs in flight per lane
+__global__ __launch_bounds__(64) void tower_dw_packed_kernel(TowerP p) {
+  int l, i, k0, n0, row0, nrows;
+  if (!dw_job(p, blockIdx.x, l, i, k0, n0, row0, nrows)) return;
+  int K, N;
+  chain_dims(p.d, i, K, N);
+  const int lane = threadIdx.x, half = lane >> 5;
+  const int R = p.R, j0 = row0 / 16, nj = nrows / 16;
+  const bf16_t *ha = p.hpt[i] + pack_off(k0 / 32, j0, lane, R);
+  const bf16_t *gb = p.gpt[i] + pack_off(n0 / 32, j0, lane, R);
+  f32x16_t acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float cs = 0.f;
+  const bool bias = k0 == 0;
+  int j = 0;
+  for (; j + DWP_U <= nj; j += DWP_U) {
+    bf16x8_t a[DWP_U], b[DWP_U];
+#pragma unroll
+    for (int u = 0; u < DWP_U; ++u) {
+      a[u] = *reinterpret_cast<const bf16x8_t *>(ha + (j + u) * 512);
+      b[u] = *reinterpret_cast<const bf16x8_t *>(gb + (j + u) * 512);
+    }
+#pragma unroll
+    for (int u = 0; u < DWP_U; ++u) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u], b[u], acc, 0, 0, 0);
+      if (bias) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cs += (float)b[u][e];
+      }
+    }
+  }
+  for (; j < nj; ++j) {
+    const bf16x8_t a = *reinterpret_cast<const bf16x8_t *>(ha + j * 512);
+    const bf16x8_t b = *reinterpret_cast<const bf16x8_t *>(gb + j * 512);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+    if (bias) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs += (float)b[e];
+    }
+  }
+  float *gw = p.gw[l] + (int64_t)(k0 + 4 * half) * N + n0 + (lane & 31);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) gw[(int64_t)((r & 3) + 8 * (r >> 2)) * N] = acc[r];
+  if (bias) {
+    cs += __shfl_xor(cs, 32);
+    if (half == 0) p.gb[l][n0 + lane] = cs;
+  }
+}
+
 __global__ __launch_bounds__(256) void tower_reduce_kernel(TowerP p) {
   const int nb = p.R / RB, nbB = p.B / RB;
   const int64_t E = p.slab_elems;
@@ -811,6 +876,13 @@ int make_params(const cc_tower_args *t, TowerP &p) {
   p.slab_elems = slab_off(t->d, 6);
   p.packed = t->dtype == CC_BF16 && t->d <= 256;
   const bool fast = p.packed;
+  p.dwpacked = fast;
+  for (int a = 0; a < 6; ++a) {
+    p.hpt[a] = static_cast<bf16_t *>(t->hpt[a]);
+    p.gpt[a] = static_cast<bf16_t *>(t->gpt[a]);
+    if (!t->hpt[a] || !t->gpt[a] || (((uintptr_t)t->hpt[a] | (uintptr_t)t->gpt[a]) & 15)) p.dwpacked = false;
+  }
+  if (t->B % 16 || t->R % 16) p.dwpacked = false;
   p.act6p = fast ? static_cast<bf16_t *>(t->act6p) : nullptr;
   p.act6tp = fast ? static_cast<bf16_t *>(t->act6tp) : nullptr;
   if (((uintptr_t)p.act6p | (uintptr_t)p.act6tp) & 15)
@@ -910,6 +982,11 @@ extern "C" int cc_tower_bwd_dw_direct(const cc_tower_args *t, void *stream) {
     int K, N;
     chain_dims(t->d, l < 6 ? l : l - 3, K, N);
     jobs += (K / 32) * (N / 32);
+  }
+  if (p.dwpacked) {  // the forward / backward chains wrote the packed transposed H_i / G_i
+    hipLaunchKernelGGL(tower_dw_packed_kernel, dim3(jobs), dim3(64), 0, as_stream(stream), p);
+    CC_LAUNCH_CHECK("tower_dw_packed_kernel");
+    return CC_OK;
   }
   hipLaunchKernelGGL(tower_dw_tiled_kernel, dim3(jobs), dim3(DW_NT), lds, as_stream(stream), p, rpw);
   CC_LAUNCH_CHECK("tower_dw_tiled_kernel");

@@ -226,7 +226,7 @@ class Trainer:
         self.gPre1T = torch.zeros(d, self.RP, **T) if self.embed_mfma else None
         if self.mx8 and not self.fused_tower:
             raise ValueError('fp8 needs the fused towers (fused_tower=True, B % 32 == 0)')
-        self.wpack = self.D3p = self.D3tp = None
+        self.wpack = self.D3p = self.D3tp = self.hpt = self.gpt = None
         if self.fused_tower:
             self.tower_layers = ('encoder/encoded_2', 'encoder/encoded_3', 'encoder/bottleneck',
                                  'decoder/decoded_1', 'decoder/decoded_2', 'decoder/decoded_3',
@@ -243,6 +243,10 @@ class Trainer:
             # ... and D3 as packed operand images of the fused D1 output kernel (cc_dec_bce_dw)
             self.D3p = torch.zeros(R * d, **T) if pack else None
             self.D3tp = torch.zeros(d * R, **T) if pack else None
+            # ... and every tower layer's input / output-gradient as packed transposed images
+            # (the dW kernel's MFMA operands): H widths d,256,128,64,128,256; G 256,128,64,128,256,d
+            self.hpt = [torch.zeros(R * w, **T) for w in (d, 256, 128, 64, 128, 256)] if pack else None
+            self.gpt = [torch.zeros(R * w, **T) for w in (256, 128, 64, 128, 256, d)] if pack else None
             slab = int(L.lib().cc_tower_slab_elems(d))
             self.slab = torch.zeros((R // 32) * slab, **f32)
             # decoder operands kept k-contiguous: D3^T (tower fwd), dZ^T (BCE epilogue), Wo^T shadow
@@ -363,6 +367,9 @@ class Trainer:
         t.act6t = self.D3t.data_ptr()
         if self.D3p is not None:
             t.act6p, t.act6tp = self.D3p.data_ptr(), self.D3tp.data_ptr()
+        if getattr(self, 'hpt', None) is not None and os.environ.get('CCREC_DW_PACKED', '1') != '0':
+            for a in range(6):
+                t.hpt[a], t.gpt[a] = self.hpt[a].data_ptr(), self.gpt[a].data_ptr()
         t.gD3 = self.gD3.data_ptr()
         for a, buf in enumerate((self.gH2, self.gH3, self.gZl, self.gD1, self.gD2)):
             t.gact[a] = buf.data_ptr()      # dPre of e2, e3, e4, d1, d2

@@ -278,6 +278,12 @@ typedef struct cc_tower_args {
    * reduction = batch rows ([d/32][R/16][64][8]).  Same fragment order as wpf. */
   void *act6p;
   void *act6tp;
+  /* optional (bf16, d <= 256, fast kernels; all twelve set): packed transposed images of every
+   * layer's input H_i [R][K_i] (written by cc_tower_fwd) and output gradient G_i [R][N_i]
+   * (cc_tower_bwd_chain), rows = features, reduction = batch rows, act6tp's layout; with them
+   * cc_tower_bwd_dw_direct runs one MFMA chain per 32x32 dW tile straight from these images. */
+  void *hpt[6];
+  void *gpt[6];
 } cc_tower_args;
 int64_t cc_tower_slab_elems(int32_t d);
 int cc_tower_fwd(const cc_tower_args *t, void *stream);

@@ -173,3 +173,61 @@ def test_packed_weight_images_bit_exact(d, B, R):
                 assert np.array_equal(b, w.reshape(K // 32, 32, N // 16, 2, 8).transpose(0, 2, 3, 1, 4)), l
     for i, (a, b) in enumerate(zip(outs[False], outs[True])):
         assert torch.equal(a, b), i
+
+
+@pytest.mark.parametrize('d,B,R', [(256, 64, 128), (256, 512, 512), (128, 32, 64)])
+def test_packed_dw_matches_tiled(d, B, R):
+    """cc_tower_bwd_dw_direct from the packed transposed H_i / G_i images (written by the fast
+    forward / backward chains) equals the LDS-staged tiled kernel up to fp32 summation order, and
+    the images hold the documented element order."""
+    rng = np.random.default_rng(d + 3 * R)
+    tdt = torch.bfloat16
+    rnd = lambda *s: torch.from_numpy((rng.standard_normal(s) * 0.2).astype(np.float32)).to('cuda', tdt)
+    dims = _dims(d)
+    W = [rnd(*dims[l if l < 6 else l - 3]) for l in range(9)]
+    bias = [torch.from_numpy(rng.standard_normal(w.shape[1]).astype(np.float32) * 0.1).cuda() for w in W]
+    widths = [d, 256, 128, 64, 128, 256, d]
+    x0, gD3 = rnd(R, d), rnd(R, d)
+    outs = {}
+    for packed in (False, True):
+        t = L.TowerArgs(dtype=L.CC_BF16, d=d, B=B, R=R)
+        keep = []
+        def buf(n, dt=tdt):
+            b = torch.zeros(n, device='cuda', dtype=dt)
+            keep.append(b)
+            return b
+        act = [x0.clone()] + [buf(R * w) for w in widths[1:]]
+        gact = [buf(R * w) for w in (256, 128, 64, 128, 256)]
+        gw = [buf(w.numel(), torch.float32) for w in W]
+        gb = [buf(w.shape[1], torch.float32) for w in W]
+        hpt = [buf(R * w) for w in (d, 256, 128, 64, 128, 256)]
+        gpt = [buf(R * w) for w in (256, 128, 64, 128, 256, d)]
+        for l in range(9):
+            t.w[l], t.wt[l], t.b[l] = W[l].data_ptr(), buf(W[l].numel()).data_ptr(), bias[l].data_ptr()
+            t.wpf[l], t.wpb[l] = buf(W[l].numel()).data_ptr(), buf(W[l].numel()).data_ptr()
+            t.gw[l], t.gb[l] = gw[l].data_ptr(), gb[l].data_ptr()
+        for a in range(7):
+            t.act[a] = act[a].data_ptr()
+        for a in range(5):
+            t.gact[a] = gact[a].data_ptr()
+        t.gD3, t.gpre1 = gD3.data_ptr(), buf(R * d, torch.float32).data_ptr()
+        t.gpre1t = buf(d * ((R + 63) // 64 * 64)).data_ptr()
+        t.slab = buf((R // 32) * int(L.lib().cc_tower_slab_elems(d)), torch.float32).data_ptr()
+        if packed:
+            for a in range(6):
+                t.hpt[a], t.gpt[a] = hpt[a].data_ptr(), gpt[a].data_ptr()
+        s = L.stream_ptr()
+        for fn in ('cc_tower_transpose', 'cc_tower_fwd', 'cc_tower_bwd_chain', 'cc_tower_bwd_dw_direct'):
+            L.call(fn, ctypes.byref(t), s)
+        torch.cuda.synchronize()
+        outs[packed] = ([g.cpu().numpy() for g in gw], [g.cpu().numpy() for g in gb])
+        if packed:
+            pt = lambda X, w: X.view(R // 16, 2, 8, w // 32, 32).permute(3, 0, 1, 4, 2).reshape(-1)
+            Hs = [x0.cpu()] + [act[a].cpu().view(R, widths[a]) for a in range(1, 6)]
+            Gs = [gact[a].cpu().view(R, w) for a, w in enumerate((256, 128, 64, 128, 256))] + [gD3.cpu()]
+            for a in range(6):
+                assert torch.equal(hpt[a].cpu(), pt(Hs[a], Hs[a].shape[1])), a
+                assert torch.equal(gpt[a].cpu(), pt(Gs[a], Gs[a].shape[1])), a
+    for l in range(9 if R > B else 6):
+        assert rel_err(outs[True][0][l], outs[False][0][l]) < 1e-5, l
+        assert rel_err(outs[True][1][l], outs[False][1][l]) < 1e-5, l
