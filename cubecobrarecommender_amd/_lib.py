@@ -55,7 +55,7 @@ class TowerArgs(C.Structure):
         ('gD3', C.c_void_p), ('gact', C.c_void_p * 5), ('gpre1', C.c_void_p), ('slab', C.c_void_p),
         ('gw', C.c_void_p * 9), ('gb', C.c_void_p * 9), ('gpre1t', C.c_void_p),
         ('wpf', C.c_void_p * 9), ('wpb', C.c_void_p * 9), ('act6p', C.c_void_p), ('act6tp', C.c_void_p),
-        ('hpt', C.c_void_p * 6), ('gpt', C.c_void_p * 6),
+        ('hpt', C.c_void_p * 6), ('gpt', C.c_void_p * 6), ('gpre1p', C.c_void_p),
     ]
 
 
@@ -104,6 +104,7 @@ SIGNATURES = {
     'cc_infer_decode_fp32': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_similar_ws_size': (_SZ, [_I32]),
     'cc_similar_cards': (C.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
+    'cc_embed_grad_packed': (C.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_tower_slab_elems': (_I64, [_I32]),
     'cc_tower_fwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_bwd': (C.c_int, [C.POINTER(TowerArgs), _P]),

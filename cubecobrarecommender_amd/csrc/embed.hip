@@ -412,6 +412,94 @@ __global__ __launch_bounds__(256, 2) void embed_grad_mfma_kernel(const bf16_t *_
 #undef EG_STORE
 }
 
+// cc_embed_grad_packed: the same product with B fragments streamed from the packed transposed
+// dPre1 image.  Wave w owns columns [64w, 64w + 64) for all EG_ROWS rows (2 x 2 accumulator
+// tiles), so each B fragment is loaded once per block; A = the row's bit bytes expanded in
+// registers (LDS bit words, as above).  EG_PU fragment pairs in flight per lane.
+constexpr int EG_PU = 8;
+__global__ __launch_bounds__(256, 2) void embed_grad_pk_kernel(const bf16_t *__restrict__ gP, int V, int R,
+                                                              int RP, uint32_t *xt, float *__restrict__ grad,
+                                                              float *__restrict__ bias_grad) {
+  constexpr int D = 256;
+  __shared__ uint32_t As[EG_ROWS][EG_XWMAX + 1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
+  const int v0 = blockIdx.x * EG_ROWS;
+  const int XW = (R + 31) >> 5, XWP = RP >> 5;
+  constexpr int AS_Q = EG_ROWS * EG_XWMAX / 256;
+  uint32_t mv[AS_Q];
+#pragma unroll
+  for (int q = 0; q < AS_Q; ++q) {
+    const int i = tid + 256 * q, r = i / XWP, wd = i % XWP, v = v0 + r;
+    mv[q] = 0u;
+    if (i < EG_ROWS * XWP && wd < XW) {
+      if (v < V)
+        mv[q] = xt[(int64_t)v * XW + wd];
+      else if (v == V && bias_grad)
+        mv[q] = (wd == XW - 1 && (R & 31)) ? (1u << (R & 31)) - 1u : 0xFFFFFFFFu;
+    }
+  }
+  // the first fragments fly while the bit words are staged
+  const bf16_t *b0 = gP + ((int64_t)(2 * w) * (RP / 16) * 64 + lane) * 8;
+  const bf16_t *b1 = gP + ((int64_t)(2 * w + 1) * (RP / 16) * 64 + lane) * 8;
+  const int nk = RP / 16;
+  bf16x8_t f0[EG_PU], f1[EG_PU];
+#pragma unroll
+  for (int u = 0; u < EG_PU; ++u)
+    if (u < nk) {
+      f0[u] = *reinterpret_cast<const bf16x8_t *>(b0 + u * 512);
+      f1[u] = *reinterpret_cast<const bf16x8_t *>(b1 + u * 512);
+    }
+#pragma unroll
+  for (int q = 0; q < AS_Q; ++q) {
+    const int i = tid + 256 * q, r = i / XWP, wd = i % XWP, v = v0 + r;
+    if (i < EG_ROWS * XWP) {
+      if (wd < XW && v < V) xt[(int64_t)v * XW + wd] = 0u;  // consumed: the next step's F finds xt zeroed
+      As[r][wd] = mv[q];
+    }
+  }
+  __syncthreads();
+  f32x16_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const int r0 = lane & 31, r1 = 32 + (lane & 31);
+  for (int j0 = 0; j0 < nk; j0 += EG_PU) {
+#pragma unroll
+    for (int u = 0; u < EG_PU; ++u) {
+      const int j = j0 + u;
+      if (j >= nk) break;
+      const int k = 16 * j + 8 * half;
+      const bf16x8_t a0 = expand_bits8((As[r0][k >> 5] >> (k & 31)) & 0xFFu);
+      const bf16x8_t a1 = expand_bits8((As[r1][k >> 5] >> (k & 31)) & 0xFFu);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, f0[u], acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, f1[u], acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, f0[u], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, f1[u], acc[1][1], 0, 0, 0);
+      if (j + EG_PU < nk) {  // refill the slot just consumed
+        f0[u] = *reinterpret_cast<const bf16x8_t *>(b0 + (j + EG_PU) * 512);
+        f1[u] = *reinterpret_cast<const bf16x8_t *>(b1 + (j + EG_PU) * 512);
+      }
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int col = 64 * w + 32 * b + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int v = v0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * half;
+        if (v < V)
+          grad[(int64_t)v * D + col] = acc[a][b][r];
+        else if (v == V && bias_grad)
+          bias_grad[col] = acc[a][b][r];
+      }
+    }
+}
+
 }  // namespace
 
 extern "C" int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const float *bias, int32_t V,
@@ -419,6 +507,20 @@ extern "C" int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const 
                                         const int32_t *x_idx, int32_t x_cap, void *out,
                                         const void *warm, int64_t warm_bytes, int64_t *state,
                                         int64_t bpe, void *stream);
+
+extern "C" int cc_embed_grad_packed(const void *dpre_p, int32_t V, int32_t d, int32_t R, int32_t ld_t,
+                                    uint32_t *xt_bits, float *grad, float *bias_grad, void *stream) {
+  CC_REQUIRE(dpre_p && xt_bits && grad, "cc_embed_grad_packed: null pointer");
+  CC_REQUIRE(d == 256, "cc_embed_grad_packed: d must be 256");
+  CC_REQUIRE(R > 0 && R <= 32 * EG_XWMAX, "cc_embed_grad_packed: R must be 1..1024");
+  CC_REQUIRE(ld_t % 64 == 0 && ld_t >= R && ((uintptr_t)dpre_p % 16) == 0,
+             "cc_embed_grad_packed: ld_t must be a multiple of 64 covering R, image 16-B aligned");
+  const int rows = bias_grad ? V + 1 : V;
+  hipLaunchKernelGGL(embed_grad_pk_kernel, dim3((unsigned)cdiv(rows, EG_ROWS)), dim3(256), 0, as_stream(stream),
+                     (const bf16_t *)dpre_p, V, R, ld_t, xt_bits, grad, bias_grad);
+  CC_LAUNCH_CHECK("embed_grad_pk_kernel");
+  return CC_OK;
+}
 
 extern "C" int cc_embed_gather_fwd(int32_t dtype, const void *table, const float *bias, int32_t V,
                                    int32_t d, int32_t R, const int32_t *x_cnt,

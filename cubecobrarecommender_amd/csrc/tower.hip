@@ -43,6 +43,7 @@ struct TowerP {
   const bf16_t *wpb[9];
   bf16_t *act6p, *act6tp;  // packed D3 operand images for cc_dec_bce_dw (fast forward only)
   bf16_t *hpt[6], *gpt[6];  // packed transposed H_i / G_i images for the dW kernel (or null)
+  bf16_t *gpre1p;           // packed transposed dPre1 for cc_embed_grad_packed (or null)
   bool packed, dwpacked;
 };
 
@@ -577,6 +578,8 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
       rows_copy_out(Gr, ldx, reinterpret_cast<bf16_t *>(p.gact[i - 1]), K, r0);
       if (p.dwpacked) pt_copy_out(Gr, ldx, p.gpt[i - 1], K, p.R, r0);  // G_{i-1} for dW
     }
+    else if (p.gpre1p)  // dPre1 as packed transposed fragments (reduction ceil64(R)) for cc_embed_grad_packed
+      pt_copy_out(Gr, ldx, p.gpre1p, K, (p.R + 63) & ~63, r0);
     else if (p.gpre1t)  // dPre1^T [d][ceil64(R)] (bf16) for cc_embed_grad_mfma
       cols_copy_out(Gr, ldx, reinterpret_cast<bf16_t *>(p.gpre1t), K, (p.R + 63) & ~63, r0);
   }
@@ -872,6 +875,8 @@ int make_params(const cc_tower_args *t, TowerP &p) {
   for (int a = 0; a < 5; ++a) p.gact[a] = t->gact[a];
   p.gpre1 = t->gpre1;
   p.gpre1t = t->dtype == CC_BF16 ? t->gpre1t : nullptr;
+  p.gpre1p = t->dtype == CC_BF16 && t->d <= 256 ? static_cast<bf16_t *>(t->gpre1p) : nullptr;
+  if ((uintptr_t)p.gpre1p & 15) return cc::fail(CC_ERR_ARG, "cc_tower: gpre1p must be 16-B aligned");
   p.slab = t->slab;
   p.slab_elems = slab_off(t->d, 6);
   p.packed = t->dtype == CC_BF16 && t->d <= 256;

@@ -226,7 +226,7 @@ class Trainer:
         self.gPre1T = torch.zeros(d, self.RP, **T) if self.embed_mfma else None
         if self.mx8 and not self.fused_tower:
             raise ValueError('fp8 needs the fused towers (fused_tower=True, B % 32 == 0)')
-        self.wpack = self.D3p = self.D3tp = self.hpt = self.gpt = None
+        self.wpack = self.D3p = self.D3tp = self.hpt = self.gpt = self.gpre1p = None
         if self.fused_tower:
             self.tower_layers = ('encoder/encoded_2', 'encoder/encoded_3', 'encoder/bottleneck',
                                  'decoder/decoded_1', 'decoder/decoded_2', 'decoder/decoded_3',
@@ -247,6 +247,9 @@ class Trainer:
             # (the dW kernel's MFMA operands): H widths d,256,128,64,128,256; G 256,128,64,128,256,d
             self.hpt = [torch.zeros(R * w, **T) for w in (d, 256, 128, 64, 128, 256)] if pack else None
             self.gpt = [torch.zeros(R * w, **T) for w in (256, 128, 64, 128, 256, d)] if pack else None
+            # dPre1 as packed transposed fragments (the W1 gradient's B operand; rows past R zero)
+            self.gpre1p = (torch.zeros(d * self.RP, **T) if pack and self.embed_mfma and d == 256
+                           and os.environ.get('CCREC_EG_PACKED', '1') != '0' else None)
             slab = int(L.lib().cc_tower_slab_elems(d))
             self.slab = torch.zeros((R // 32) * slab, **f32)
             # decoder operands kept k-contiguous: D3^T (tower fwd), dZ^T (BCE epilogue), Wo^T shadow
@@ -367,6 +370,8 @@ class Trainer:
         t.act6t = self.D3t.data_ptr()
         if self.D3p is not None:
             t.act6p, t.act6tp = self.D3p.data_ptr(), self.D3tp.data_ptr()
+        if self.gpre1p is not None:
+            t.gpre1p = self.gpre1p.data_ptr()
         if getattr(self, 'hpt', None) is not None and os.environ.get('CCREC_DW_PACKED', '1') != '0':
             for a in range(6):
                 t.hpt[a], t.gpt[a] = self.hpt[a].data_ptr(), self.gpt[a].data_ptr()
@@ -703,7 +708,10 @@ class Trainer:
             self._dense_bwd(self.H2, self.gH3, (0, R), 256, 128, 'encoder/encoded_3', gIn=self.gH2, mask=self.H2)
             self._dense_bwd(self.H1, self.gH2, (0, R), d, 256, 'encoder/encoded_2', gIn_f32=self.gPre1, mask=self.H1)
         t = self._tick('cc_embed_scatter_bwd')
-        if self.embed_mfma:
+        if self.gpre1p is not None:
+            L.call('cc_embed_grad_packed', L.ptr(self.gpre1p), V, d, R, self.RP, L.ptr(self.xt_bits),
+                   self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
+        elif self.embed_mfma:
             L.call('cc_embed_grad_mfma', L.ptr(self.gPre1T), V, d, R, self.RP, L.ptr(self.xt_bits),
                    self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
         else:

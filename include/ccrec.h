@@ -156,6 +156,11 @@ int cc_embed_scatter_bwd(const float *dpre, int32_t V, int32_t d, int32_t R,
  * Consumes (zeroes) xt_bits like cc_embed_scatter_bwd; deterministic. */
 int cc_embed_grad_mfma(const void *dpre_t, int32_t V, int32_t d, int32_t R, int32_t ld_t,
                        uint32_t *xt_bits, float *grad, float *bias_grad, void *stream);
+/* cc_embed_grad_mfma with B = dPre1 as packed transposed fragments (cc_tower_args.gpre1p,
+ * reduction length ld_t = ceil64(R)): each wave streams its 64 columns' fragments straight from
+ * L2 (1 KB per wave load), no LDS staging or per-K-tile barriers.  d == 256. */
+int cc_embed_grad_packed(const void *dpre_p, int32_t V, int32_t d, int32_t R, int32_t ld_t,
+                         uint32_t *xt_bits, float *grad, float *bias_grad, void *stream);
 
 /* ----------------------------------------------------------------------------------
  * Generic MFMA GEMM with fused epilogues — the Dense layers of the E/D towers and the
@@ -284,6 +289,10 @@ typedef struct cc_tower_args {
    * cc_tower_bwd_dw_direct runs one MFMA chain per 32x32 dW tile straight from these images. */
   void *hpt[6];
   void *gpt[6];
+  /* optional (bf16, d <= 256): dPre1 [R][d] as packed transposed fragments with reduction length
+   * ceil64(R) (rows past R stay zero: allocate zeroed) — cc_embed_grad_packed's B operand; when
+   * set, the fast backward chain writes it instead of gpre1t. */
+  void *gpre1p;
 } cc_tower_args;
 int64_t cc_tower_slab_elems(int32_t d);
 int cc_tower_fwd(const cc_tower_args *t, void *stream);

@@ -452,3 +452,33 @@ def test_dec_bce_dw_matches_unfused(B, d, V):
     want = (np.maximum(z, 0) - z * y + np.log1p(np.exp(-np.abs(z)))).mean()
     assert abs(loss.item() - want) < 1e-5 * abs(want)
     assert abs(part.sum().item() * scale - want) < 1e-5 * abs(want)
+
+
+@pytest.mark.parametrize('V,R', [(3000, 512), (777, 96), (22000, 1024)])
+def test_embed_grad_packed_bit_exact(V, R):
+    """cc_embed_grad_packed (B fragments streamed from the packed transposed dPre1) equals
+    cc_embed_grad_mfma (LDS-staged dPre1^T) bit for bit: same MFMA k order; both zero xt_bits."""
+    d = 256
+    RP = (R + 63) // 64 * 64
+    rng = np.random.default_rng(V + R)
+    X = rng.random((R, V)) < 0.02
+    xt = np.zeros((V, (R + 31) // 32), np.uint32)
+    rr, cc = np.nonzero(X)
+    np.bitwise_or.at(xt, (cc, rr // 32), (np.uint32(1) << (rr % 32).astype(np.uint32)))
+    g = (torch.randn(R, d, device='cuda') * 0.1).to(torch.bfloat16)
+    gpad = torch.zeros(RP, d, device='cuda', dtype=torch.bfloat16)
+    gpad[:R] = g
+    gT = gpad.t().contiguous()
+    gP = gpad.view(RP // 16, 2, 8, d // 32, 32).permute(3, 0, 1, 4, 2).contiguous()
+    outs = []
+    for fn, src in (('cc_embed_grad_mfma', gT), ('cc_embed_grad_packed', gP)):
+        xtd = torch.from_numpy(xt.view(np.int32)).cuda()
+        grad = torch.full((V, d), 7.0, device='cuda')
+        bg = torch.full((d,), 7.0, device='cuda')
+        L.call(fn, L.ptr(src), V, d, R, RP, L.ptr(xtd), L.ptr(grad), L.ptr(bg), L.stream_ptr())
+        torch.cuda.synchronize()
+        assert int(xtd.abs().sum().item()) == 0
+        outs.append((grad.cpu(), bg.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    want = X.T.astype(np.float64) @ g.double().cpu().numpy()
+    assert rel_err(outs[1][0].numpy(), want) < 1e-5
