@@ -183,11 +183,11 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   for (int ps = 0; ps < npass; ++ps) {
     if (ps + 1 < npass) load_a(af[(ps + 1) & 1], ps + 1);
     if (ps * 256 + w * 32 >= B) continue;          // wave-uniform: rows beyond B
-    f32x16_t acc[NJ];
+    f32x16_t acc[NJ];  // starts at the bias: z = bo + sum_k D3 Wo accumulates in the MFMA
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[j][r] = bias[j];
 #pragma unroll
     for (int kk = 0; kk < nkk; ++kk) {
 #pragma unroll
@@ -205,17 +205,20 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
       if (valid[j]) {
         // sigmoid_cross_entropy_with_logits (TF 2.5 Keras BCE on a sigmoid output):
         //   loss = max(z, 0) - z y + log1p(exp(-|z|)),  dz = (sigmoid(z) - y) / (B V)
-        // a = exp(-|z|) once; log1p and 1/(1+a) from it; log2 summed, scaled by ln 2 at the end
+        // a = exp(-|z|) once; log1p and 1/(1+a) from it.  The 16 factors 1 + a in (1, 2] of a
+        // lane's column are multiplied (<= 2^16) and one log2 per column taken: the log is a
+        // quarter-rate instruction; summed log2 scaled by ln 2 at the end
         bf16_t *dst = p.dZ + (int64_t)(rb + 4 * half) * V + n0 + col;
+        float lprod = 1.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = rb + acc_row(r, lane);
           const uint32_t yb = (ys[row * NJ + j] >> (lane & 31)) & 1u;
-          const float z = acc[j][r] + bias[j];
+          const float z = acc[j][r];
           const float a = __builtin_amdgcn_exp2f(-fabsf(z) * LOG2E);
           const float opa = 1.f + a;
           const float rp = __builtin_amdgcn_rcpf(opa);
-          lsum += __builtin_amdgcn_logf(opa);
+          lprod *= opa;
           rsum += fmaxf(yb ? -z : z, 0.f);
           const float sig = z >= 0.f ? rp : a * rp;
           const uint16_t zb = bf16_bits(fmaf(sig, scale, yb ? -scale : 0.f));
@@ -223,6 +226,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
           cs[j] += __uint_as_float((uint32_t)zb << 16);
           dst[(int64_t)((r & 3) + 8 * (r >> 2)) * V] = zb;
         }
+        lsum += __builtin_amdgcn_logf(lprod);
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) tt[r] = 0;
