@@ -477,7 +477,6 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
     if (c < nbias) bsm[c] = bv[q];
   }
   __syncthreads();
-  if (p.dwpacked) pt_copy_out(X0, ldx, p.hpt[0], p.d, p.R, r0);  // H_0 for dW
   TOWER_PROBE(1);
   bf16_t *xin = X0, *xout = X1;
 #pragma unroll
@@ -485,10 +484,14 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
     int K, N;
     chain_dims(p.d, i, K, N);
     if (i < 5) issue(i + 1, (i + 1) & 1);  // next layer's weights fly during this layer
+    f32x16_t acc;
+    if (t < N / 32) consume_frags_t(fr[i & 1], xin, ldx, K, acc);
+    TOWER_PROBE(2 + 3 * i);
+    // the previous layer's output (this layer's input, read-only now) to global while the MFMAs
+    // run: rows for the backward's ReLU masks, packed transposed for the dW kernel
+    if (i > 0) rows_copy_out(xin, ldx, reinterpret_cast<bf16_t *>(p.act[i]), K, r0);
+    if (p.dwpacked) pt_copy_out(xin, ldx, p.hpt[i], K, p.R, r0);
     if (t < N / 32) {
-      f32x16_t acc;
-      consume_frags_t(fr[i & 1], xin, ldx, K, acc);
-      TOWER_PROBE(2 + 3 * i);
       const int row = lane & 31, cb = 32 * t + 4 * half;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -501,23 +504,23 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
     }
     __syncthreads();
     TOWER_PROBE(4 + 3 * i);
-    // this layer's output rows to global (read by the backward and the dW kernel) while the next
-    // layer computes; D3^T [d][R] for the decoder's dW operand
-    rows_copy_out(xout, ldx, reinterpret_cast<bf16_t *>(p.act[i + 1]), N, r0);
-    if (i == 5 && p.act6t) cols_copy_out(xout, ldx, reinterpret_cast<bf16_t *>(p.act6t), N, p.R, r0);
-    if (i == 5 && p.act6p) {  // D3 as the logits' A operand: fragments (blockIdx.x, j)
-      for (int v = threadIdx.x; v < (N / 16) * 64; v += FNT) {
-        const int j = v >> 6, ln = v & 63;
-        *reinterpret_cast<u32v4 *>(p.act6p + pack_off(blockIdx.x, j, ln, N)) =
-            *reinterpret_cast<const u32v4 *>(xout + (ln & 31) * ldx + 16 * j + 8 * (ln >> 5));
-      }
-    }
-    if (i == 5 && p.act6tp) pt_copy_out(xout, ldx, p.act6tp, N, p.R, r0);  // D3^T: the dWo A operand
-    if (i < 5 && p.dwpacked) pt_copy_out(xout, ldx, p.hpt[i + 1], N, p.R, r0);  // H_{i+1} for dW
     bf16_t *tmp = xin;
     xin = xout;
     xout = tmp;
   }
+  // D3 (the last layer's output): rows, D3^T [d][R], and the packed operand images of the fused
+  // output-layer kernel
+  const int dd = p.d;
+  rows_copy_out(xin, ldx, reinterpret_cast<bf16_t *>(p.act[6]), dd, r0);
+  if (p.act6t) cols_copy_out(xin, ldx, reinterpret_cast<bf16_t *>(p.act6t), dd, p.R, r0);
+  if (p.act6p) {  // D3 as the logits' A operand: fragments (blockIdx.x, j)
+    for (int v = threadIdx.x; v < (dd / 16) * 64; v += FNT) {
+      const int j = v >> 6, ln = v & 63;
+      *reinterpret_cast<u32v4 *>(p.act6p + pack_off(blockIdx.x, j, ln, dd)) =
+          *reinterpret_cast<const u32v4 *>(xin + (ln & 31) * ldx + 16 * j + 8 * (ln >> 5));
+    }
+  }
+  if (p.act6tp) pt_copy_out(xin, ldx, p.act6tp, dd, p.R, r0);  // D3^T: the dWo A operand
 }
 
 __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
@@ -545,7 +548,6 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
   issue_layer(5, 1);
   rows_store(rg, p.d, Gr, ldx);
   __syncthreads();
-  if (p.dwpacked) pt_copy_out(Gr, ldx, p.gpt[5], p.d, p.R, r0);  // G_5 for dW
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
     int K, N;
@@ -560,6 +562,10 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
     }
     f32x16_t acc;
     if (t < K / 32) consume_frags_t(fr[i & 1], Gr, ldx, N, acc);
+    // this layer's incoming gradient G_i (Gr, read-only until the barrier) to global while the
+    // MFMAs run: rows (the dW fallback) and packed transposed for the dW kernel
+    if (i < 5) rows_copy_out(Gr, ldx, reinterpret_cast<bf16_t *>(p.gact[i]), N, r0);
+    if (p.dwpacked) pt_copy_out(Gr, ldx, p.gpt[i], N, p.R, r0);
     __syncthreads();  // every wave has finished reading Gr
     if (t < K / 32) {
 #pragma unroll
@@ -574,13 +580,10 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
       }
     }
     __syncthreads();
-    if (i > 0) {
-      rows_copy_out(Gr, ldx, reinterpret_cast<bf16_t *>(p.gact[i - 1]), K, r0);
-      if (p.dwpacked) pt_copy_out(Gr, ldx, p.gpt[i - 1], K, p.R, r0);  // G_{i-1} for dW
-    }
-    else if (p.gpre1p)  // dPre1 as packed transposed fragments (reduction ceil64(R)) for cc_embed_grad_packed
+    // (G_{i-1} for i > 0 is copied out during the next layer's MFMAs)
+    if (i == 0 && p.gpre1p)  // dPre1 as packed transposed fragments (reduction ceil64(R)): cc_embed_grad_packed
       pt_copy_out(Gr, ldx, p.gpre1p, K, (p.R + 63) & ~63, r0);
-    else if (p.gpre1t)  // dPre1^T [d][ceil64(R)] (bf16) for cc_embed_grad_mfma
+    else if (i == 0 && p.gpre1t)  // dPre1^T [d][ceil64(R)] (bf16) for cc_embed_grad_mfma
       cols_copy_out(Gr, ldx, reinterpret_cast<bf16_t *>(p.gpre1t), K, (p.R + 63) & ~63, r0);
   }
 }
