@@ -94,31 +94,41 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   // and the target bits; every load of the batch issued before the first LDS store
   {
     constexpr int NW = NB * CHD / NTH, NY = (B * NJ + NTH - 1) / NTH;
-    v4u wv[NW];
-    uint32_t yv[NY];
-    // from Wo [d][V]: chunk c = (k, 8 consecutive columns); columns past V clamp to V - 1
-    constexpr int CN = NB / 8;  // 16-B column chunks per Wo row segment
+    // from Wo [d][V]: task = (4 consecutive k, 8 consecutive columns) -> 4 row loads, then 8
+    // 8-byte LDS writes (the 4 k of one column are contiguous in the k-contiguous image);
+    // columns past V clamp to V - 1
+    constexpr int CN = NB / 8;                       // 16-B column chunks per Wo row segment
+    constexpr int NT4 = (d / 4 * CN + NTH - 1) / NTH;  // tasks per thread
     const bool fromWo = p.WoT == nullptr;
     const bool vec = fromWo && (V % 8 == 0) && n0 + NB <= V;
+    v4u wv[fromWo ? 1 : NW];
+    v4u w4[NT4][4];
+    uint32_t yv[NY];
+    if (!fromWo) {
 #pragma unroll
-    for (int q = 0; q < NW; ++q) {
-      const int c = tid + NTH * q;
-      if (!fromWo) {
-        const int n = c / CHD, ch = c % CHD;
+      for (int q = 0; q < NW; ++q) {
+        const int c = tid + NTH * q, n = c / CHD, ch = c % CHD;
         wv[q] = *reinterpret_cast<const v4u *>(p.WoT + (int64_t)min(n0 + n, V - 1) * d + ch * 8);
-      } else if (vec) {
-        const int k = c / CN, nc = c % CN;
-        wv[q] = *reinterpret_cast<const v4u *>(p.Wo + (int64_t)k * V + n0 + nc * 8);
-      } else {  // ragged edge block: element loads
-        const int k = c / CN, nc = c % CN;
-        uint32_t w2[4];
+      }
+    } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t lo = p.Wo[(int64_t)k * V + min(n0 + nc * 8 + 2 * e, V - 1)];
-          const uint32_t hi = p.Wo[(int64_t)k * V + min(n0 + nc * 8 + 2 * e + 1, V - 1)];
-          w2[e] = lo | (hi << 16);
+      for (int q = 0; q < NT4; ++q) {
+        const int tk = tid + NTH * q, kg = tk / CN, nc = tk % CN;
+        if (kg >= d / 4) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bf16_t *row = p.Wo + (int64_t)(4 * kg + r) * V;
+          if (vec) {
+            w4[q][r] = *reinterpret_cast<const v4u *>(row + n0 + nc * 8);
+          } else {  // ragged edge block: element loads
+            uint32_t w2[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              w2[e] = (uint32_t)row[min(n0 + nc * 8 + 2 * e, V - 1)] |
+                      ((uint32_t)row[min(n0 + nc * 8 + 2 * e + 1, V - 1)] << 16);
+            w4[q][r] = v4u{w2[0], w2[1], w2[2], w2[3]};
+          }
         }
-        wv[q] = v4u{w2[0], w2[1], w2[2], w2[3]};
       }
     }
 #pragma unroll
@@ -127,17 +137,24 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
       yv[q] = gw < VW ? p.y_bits[(int64_t)r * VW + gw] : 0u;
     }
     __builtin_amdgcn_sched_barrier(0);
+    if (!fromWo) {
 #pragma unroll
-    for (int q = 0; q < NW; ++q) {
-      const int c = tid + NTH * q;
-      if (!fromWo) {
-        const int n = c / CHD, ch = c % CHD;
+      for (int q = 0; q < NW; ++q) {
+        const int c = tid + NTH * q, n = c / CHD, ch = c % CHD;
         *reinterpret_cast<v4u *>(Wt + sw_off(n, ch * 8, CHD)) = wv[q];
-      } else {  // transpose: element e of chunk (k, nc) -> Wt[nc * 8 + e][k]
-        const int k = c / CN, nc = c % CN;
+      }
+    } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          Wt[sw_off(nc * 8 + e, k, CHD)] = (bf16_t)(wv[q][e >> 1] >> (16 * (e & 1)));
+      for (int q = 0; q < NT4; ++q) {
+        const int tk = tid + NTH * q, kg = tk / CN, nc = tk % CN;
+        if (kg >= d / 4) continue;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {  // column nc*8 + e, rows 4kg .. 4kg+3
+          const int sh = 16 * (e & 1);
+          const uint32_t x0 = (w4[q][0][e >> 1] >> sh) & 0xFFFFu, x1 = (w4[q][1][e >> 1] >> sh) & 0xFFFFu;
+          const uint32_t x2 = (w4[q][2][e >> 1] >> sh) & 0xFFFFu, x3 = (w4[q][3][e >> 1] >> sh) & 0xFFFFu;
+          *reinterpret_cast<uint2 *>(Wt + sw_off(nc * 8 + e, 4 * kg, CHD)) = make_uint2(x0 | (x1 << 16), x2 | (x3 << 16));
+        }
       }
     }
 #pragma unroll

@@ -24,16 +24,19 @@ tick = torch.zeros(1, device='cuda', dtype=torch.int32)
 D3p = D3.view(B // 32, 32, d // 16, 2, 8).permute(0, 2, 3, 1, 4).contiguous()
 D3tp = D3t.view(d // 32, 32, B // 16, 2, 8).permute(0, 2, 3, 1, 4).contiguous()
 PK = [None, None]
+WoD = [None]
+Wo = WoT.t().contiguous()
 
 
 def run():
-    L.call('cc_dec_bce_dw', L.ptr(D3), L.ptr(D3t), B, PK[0], PK[1], L.ptr(WoT), None, L.ptr(bo), B, d, V, L.ptr(ybits),
+    L.call('cc_dec_bce_dw', L.ptr(D3), L.ptr(D3t), B, PK[0], PK[1], None if WoD[0] else L.ptr(WoT), WoD[0], L.ptr(bo), B, d, V, L.ptr(ybits),
            L.ptr(dZ), L.ptr(gW), L.ptr(gb), L.ptr(part), L.ptr(loss), 1.0 / (B * V), L.ptr(tick),
            L.stream_ptr())
 
 
-for pk in (0, 1):
+for pk in (0, 1, 2):
     PK[:] = [L.ptr(D3p), L.ptr(D3tp)] if pk else [None, None]
+    WoD[0] = L.ptr(Wo) if pk == 2 else None
     for _ in range(3):
         run()
     torch.cuda.synchronize()
