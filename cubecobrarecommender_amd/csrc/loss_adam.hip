@@ -127,12 +127,15 @@ __global__ __launch_bounds__(NTR) void softmax_kl_rows_kernel(const float *__res
   for (int i = 0; i < NV; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      z[i][e] = expf(z[i][e] - mx);  // padding: exp(-inf) = 0
+      z[i][e] = __expf(z[i][e] - mx);  // padding: exp(-inf) = 0 (hardware exp2: ~2 ulp)
       se += z[i][e];
     }
   se = rows_reduce<float, NTR / 64>(se, redf, false);
   const float inv = 1.f / se;
-  double kl = 0.0, S = 0.0;
+  // per-thread partials in fp32 (<= 4 NV terms each; fp64 across threads), log of the ratio as
+  // a difference of hardware logs: the f64 adds and the IEEE divide + log per element made this
+  // kernel VALU-bound at twice its HBM time
+  float klf = 0.f, Sf32 = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     if ((int)threadIdx.x + i * NTR >= V4) break;
@@ -141,14 +144,14 @@ __global__ __launch_bounds__(NTR) void softmax_kl_rows_kernel(const float *__res
       const float p = z[i][e] * inv;
       const float tc = fminf(fmaxf(t[i][e], 1e-7f), 1.f);
       const float q = fminf(fmaxf(p, 1e-7f), 1.f);
-      kl += (double)(tc * logf(tc / q));
-      if (p >= 1e-7f) S += (double)tc;
+      klf += tc * (__logf(tc) - __logf(q));
+      if (p >= 1e-7f) Sf32 += tc;
       z[i][e] = p;
       t[i][e] = p >= 1e-7f ? -tc : 0.f;
     }
   }
-  kl = rows_reduce<double, NTR / 64>(kl, redd, false);
-  S = rows_reduce<double, NTR / 64>(S, redd, false);
+  double kl = rows_reduce<double, NTR / 64>((double)klf, redd, false);
+  double S = rows_reduce<double, NTR / 64>((double)Sf32, redd, false);
   const float Sf = (float)S;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
