@@ -284,7 +284,8 @@ def main():
         'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype,
         'data': 'synthetic cubes (SURVEY §8(d): Zipf popularity, sizes 180-720, C=65536), random-init weights',
         'config': {'workload': 'DAE training step (F noise + E + D1/BCE' + (' + D2/KL' if args.reg > 0 else '')
-                               + ' + backward + Adam), BASELINE configs[1]',
+                               + ' + backward + Adam), BASELINE configs[%d]'
+                               % (4 if args.dtype == 'fp8' else 3 if world > 1 else 2 if args.reg > 0 else 1),
                    'V': V, 'd': d, 'batch_per_gpu': B, 'global_batch': B * world, 'reg': args.reg,
                    'cubes': args.cubes, 'parallelism': f'dp{world}'},
         'roofline': roof,
