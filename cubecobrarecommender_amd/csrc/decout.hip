@@ -83,7 +83,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   __shared__ int lastflag;
   bf16_t *Wt = reinterpret_cast<bf16_t *>(smem);                 // [NB][d]
   bf16_t *Zt = reinterpret_cast<bf16_t *>(smem + ZT_OFF);        // [NB][B]
-  uint32_t *ys = reinterpret_cast<uint32_t *>(smem + YS_OFF);    // [B][NJ]
+  uint32_t *ys = reinterpret_cast<uint32_t *>(smem + YS_OFF);    // [NJ][B]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
   const int n0 = blockIdx.x * NB;
   const int V = p.V;
@@ -159,7 +159,10 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     }
 #pragma unroll
     for (int q = 0; q < NY; ++q)
-      if (tid + NTH * q < B * NJ) ys[tid + NTH * q] = yv[q];
+      if (tid + NTH * q < B * NJ) {  // target words column-tile-major: ys[j][row]
+        const int i = tid + NTH * q;
+        ys[(i % NJ) * B + i / NJ] = yv[q];
+      }
   }
 
   // ---- phase 1: logits, BCE, dZ (global + LDS dZ^T), bias-gradient partial, loss.  Wave w owns
@@ -227,10 +230,14 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         // quarter-rate instruction; summed log2 scaled by ln 2 at the end
         bf16_t *dst = p.dZ + (int64_t)(rb + 4 * half) * V + n0 + col;
         float lprod = 1.f;
+        // the 16 rows' target words: 4 runs of 4 consecutive rows -> 4 LDS reads of 16 B
+        uint4 yw[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) yw[g] = *reinterpret_cast<const uint4 *>(ys + j * B + rb + 8 * g + 4 * half);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = rb + acc_row(r, lane);
-          const uint32_t yb = (ys[row * NJ + j] >> (lane & 31)) & 1u;
+          const uint32_t ywr = (r & 3) == 0 ? yw[r >> 2].x : (r & 3) == 1 ? yw[r >> 2].y : (r & 3) == 2 ? yw[r >> 2].z : yw[r >> 2].w;
+          const uint32_t yb = (ywr >> (lane & 31)) & 1u;
           const float z = acc[j][r];
           const float a = __builtin_amdgcn_exp2f(-fabsf(z) * LOG2E);
           const float opa = 1.f + a;
