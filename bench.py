@@ -33,7 +33,11 @@ def parse():
     ap.add_argument('--dtype', default='bf16')
     ap.add_argument('--reg-shard', type=int, default=1,
                     help='with --reg > 0 on N > 1 ranks: M~ row-sharded at equal neg_sampler mass, '
-                         'owner computes (SURVEY 8(e)); 0 = every rank holds all of M~')
+                         'owner computes over the global reg draws (SURVEY 8(e)); 0 = every rank '
+                         'holds all of M~ and draws its own B reg rows')
+    ap.add_argument('--reg-mode', default='sampled', choices=('sampled', 'full'),
+                    help="sampled: B reg rows per step drawn from neg_sampler (generator.py:47-51); "
+                         "full: all |V| identity rows every step (README.md:27, the |V|x|V| MFMA path)")
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-steps', type=int, default=16)
     ap.add_argument('--no-recommend', action='store_true')
@@ -45,14 +49,37 @@ def parse():
     return ap.parse_args()
 
 
+def launch_ranks(args):
+    """--gpus N > 1 without a torch.distributed.run environment: start one rank per GPU as CHILD
+    processes (torch.distributed.run, rendezvous on 127.0.0.1) and exit with their status.  This
+    parent never touches the GPU (no HIP call before the children start, no exec)."""
+    if args.gpus <= 1 or 'WORLD_SIZE' in os.environ:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
+           '--master-addr', '127.0.0.1', f'--master-port={port}', os.path.abspath(__file__), *sys.argv[1:]]
+    sys.exit(subprocess.run(cmd, env=env).returncode)
+
+
 def setup_dist(args):
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
         import torch.distributed as dist
-        local = local % torch.cuda.device_count()
+        ndev = torch.cuda.device_count()
+        local = local % ndev
         torch.cuda.set_device(local)
+        if args.backend == 'nccl' and ndev < world:   # RCCL needs one GPU per rank
+            print(f'bench.py: {world} ranks on {ndev} GPU(s): gloo collectives instead of RCCL',
+                  file=sys.stderr)
+            args.backend = 'gloo'
         if args.backend == 'nccl':
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
         else:
@@ -91,6 +118,81 @@ def roofline_for(name, ms, tr):
         return {'bound': 'hbm', 'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s', 'bytes_per_launch': byt}
     return None
+
+
+def workload_label(args, world):
+    """Which BASELINE.json config this line measures (configs[0] is the CPU recommend case)."""
+    what = 'DAE training step (F noise + E + D1/BCE' + (
+        (' + D2/KL over all |V| identity rows' if args.reg_mode == 'full' else ' + D2/KL') if args.reg > 0 else '') + \
+        ' + backward + Adam)'
+    if args.dtype == 'fp8':
+        idx = 4
+    elif world > 1:
+        idx = 3
+    else:
+        idx = 2 if args.reg > 0 else 1
+    note = '' if (idx != 4 or world == 8) else f' on {world} of its 8 GPUs'
+    if idx == 3 and args.reg == 0:
+        note = ' with reg=0 (BCE only, configs[1] per GPU)'
+    return f'{what}, BASELINE configs[{idx}]{note}'
+
+
+def kernel_profile(tr, step, samples=8):
+    """Steady-state per-kernel durations (us) for the step-level report: HIP events around each
+    kernel of an eager step launched while the GPU is still busy with three queued whole-step graph
+    replays, so every interval is the kernel's own duration (not launch latency or first-launch
+    module loads).  Run after the timed region; it does not touch the headline number."""
+    tr.events = {}
+    for i in range(samples + 1):
+        for _ in range(3):
+            step(True)
+        tr.timing = True
+        step(False)
+        tr.timing = False
+        if i == 0:                 # first eager step after graph replays: discard
+            torch.cuda.synchronize()
+            tr.events = {}
+    return {k: 1e3 * v for k, v in tr.kernel_times_ms().items()}
+
+
+def step_roofline(tr, ms_per_step, kt):
+    """Whole-step HBM roofline: algorithmic bytes per step =
+    B*n*d*e (E1 gather) + 34*P (fp32 grad write+read, Adam p/m/v read+write, low-precision shadow)
+    + 2*e*d*V*n_dec (decoder output weights, forward + dX) + B*(4n + V/8) (x CSR + y bits)
+    [+ 4*B*V with reg (M~ rows)], n = mean noised cube size of the step's batch; plus the decoder
+    output layer's MFMA rate."""
+    cfg = tr.cfg
+    V, d, B = cfg.V, cfg.d, cfg.batch_size
+    e = 1 if tr.mx8 else 2 if tr.dtype == 1 else 4
+    n = float(tr.x_cnt[:B].float().mean().item())
+    P = tr.layout.total if tr.use_reg else tr.layout.main_total
+    ndec = 2 if tr.use_reg else 1
+    byt = B * n * d * e + 34 * P + 2 * e * d * V * ndec + B * (4 * n + V / 8) + (4 * tr.Breg * V if tr.use_reg else 0)
+    out = {'bound': 'hbm', 'bytes_per_step': byt, 'achieved': byt / (ms_per_step * 1e-3) / 1e9,
+           'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'mean_cube_n': n}
+    out['frac'] = out['achieved'] / out['peak']
+    if tr.full_reg:   # the |V| x |V| regulariser product dominates: MFMA-bound (SURVEY 8(d))
+        T = 512 * d + 81920
+        fl = 6.0 * (d * V + T) * (B + tr.Breg) + 4.0 * n * d * B   # SURVEY 8(d) FLOP/row
+        out.update({'bound': 'mfma', 'flops_per_step': fl, 'achieved_tflops': fl / (ms_per_step * 1e-3) / 1e12,
+                    'peak_tflops': BF16_PEAK_TFLOPS, 'frac_mfma': fl / (ms_per_step * 1e-3) / 1e12 / BF16_PEAK_TFLOPS})
+    if kt and 'dec_bce_fwd' in kt and getattr(tr, 'fused_out', False):
+        fl = 2 * 2.0 * B * d * V            # logits + dWo (dX runs in its own GEMM)
+        us = kt['dec_bce_fwd']
+        out['decoder_mfma'] = {'kernel': 'dec_bce_dw_kernel (fused D1: logits + sigmoid/BCE + dZ + dWo/dbo)',
+                               'flops_per_launch': fl, 'avg_us': us, 'achieved': fl / (us * 1e-6) / 1e12,
+                               'peak': BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                               'frac': fl / (us * 1e-6) / 1e12 / BF16_PEAK_TFLOPS}
+    if kt and 'dec_dX' in kt:
+        out['decoder_dx_mfma'] = {'flops_per_launch': 2.0 * B * d * V, 'avg_us': kt['dec_dX'],
+                                  'achieved': 2.0 * B * d * V / (kt['dec_dX'] * 1e-6) / 1e12,
+                                  'peak': BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s'}
+    if kt and 'cc_embed_gather_fwd' in kt:
+        gb = tr.R * n * d * e
+        out['gather'] = {'bytes_per_launch': gb, 'avg_us': kt['cc_embed_gather_fwd'],
+                         'achieved_GBs': gb / (kt['cc_embed_gather_fwd'] * 1e-6) / 1e9,
+                         'note': 'row bytes gathered (mostly L2/MALL hits: W1 is 11 MB)'}
+    return out
 
 
 def cpu_baseline(args, seconds_cap=30.0):
@@ -151,6 +253,7 @@ def recommend_latency(n_req=1000):
 
 def main():
     args = parse()
+    launch_ranks(args)
     world, rank, local = setup_dist(args)
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
@@ -166,16 +269,16 @@ def main():
     if args.reg > 0:
         from cubecobrarecommender_amd.adjacency import adjacency_normalised_gpu
         y_mtx = adjacency_normalised_gpu(indptr, indices, V, device=dev)
-        if reg_shard:    # keep only this rank's rows of M~
+        if world > 1 and (reg_shard or args.reg_mode == 'full'):    # keep only this rank's rows of M~
             from cubecobrarecommender_amd.trainer import reg_rows_for
-            reg_rows = reg_rows_for(ns, world, rank)
+            reg_rows = reg_rows_for(ns, world, rank, args.reg_mode)
             y_mtx = y_mtx[reg_rows[0]:reg_rows[1]].clone()
             torch.cuda.empty_cache()
     data = DeviceDataset(csr=(indptr, indices), num_cards=V, neg_sampler=ns, y_mtx=y_mtx, device=dev,
                          reg_rows=reg_rows)
     del y_mtx
     cfg = TrainConfig(V=V, d=d, batch_size=B, reg=args.reg, dtype=args.dtype, seed=1234,
-                      rank=rank, world=world, reg_shard=reg_shard)
+                      rank=rank, world=world, reg_shard=reg_shard, reg_mode=args.reg_mode)
     tr = Trainer(cfg, data, params_flat=glorot_flat(V, d, seed=42), device=dev)
     rng = np.random.default_rng(99)      # same permutations on every rank
     tr.set_epoch_permutations(np.stack([rng.permutation(args.cubes) for _ in range(4)]))
@@ -210,12 +313,8 @@ def main():
             tr.step()
             tr.graphs = saved
 
-    # per-kernel durations (HIP events, eager launches of the same step) for the roofline
-    tr.timing = True
-    for _ in range(10):
+    for _ in range(3):          # eager steps: module loads, lazy allocations
         step(False)
-    ktimes = tr.kernel_times_ms()
-    tr.timing = False
     tr.capture()
 
     for _ in range(args.warmup):
@@ -234,7 +333,9 @@ def main():
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    tr.check_status()
     losses = tr.losses()
+    ktimes = kernel_profile(tr, step) if world == 1 else None
     if rank != 0:
         if world > 1:
             import torch.distributed as dist
@@ -283,13 +384,14 @@ def main():
         'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype,
         'data': 'synthetic cubes (SURVEY §8(d): Zipf popularity, sizes 180-720, C=65536), random-init weights',
-        'config': {'workload': 'DAE training step (F noise + E + D1/BCE' + (' + D2/KL' if args.reg > 0 else '')
-                               + ' + backward + Adam), BASELINE configs[%d]'
-                               % (4 if args.dtype == 'fp8' else 3 if world > 1 else 2 if args.reg > 0 else 1),
+        'config': {'workload': workload_label(args, world),
                    'V': V, 'd': d, 'batch_per_gpu': B, 'global_batch': B * world, 'reg': args.reg,
+                   'reg_mode': args.reg_mode, 'reg_rows_per_gpu': tr.Breg,
+                   'reg_shard': 'owner computes' if tr.owner else ('full rows' if tr.full_reg and world > 1 else 'replicated'),
                    'cubes': args.cubes, 'parallelism': f'dp{world}'},
         'roofline': roof,
-        'kernel_ms_eager': ktimes,
+        'step_roofline': step_roofline(tr, dt / args.steps * 1e3, ktimes),
+        'kernel_us': ktimes,
         'final_loss': losses,
         'setup_s': setup_s,
     }

@@ -26,7 +26,8 @@ class NoiseArgs(C.Structure):
         ('guide_log2', C.c_int32), ('state', C.c_void_p),
         ('x_cnt', C.c_void_p), ('x_idx', C.c_void_p), ('y_bits', C.c_void_p),
         ('xt_bits', C.c_void_p), ('reg_idx', C.c_void_p), ('status', C.c_void_p),
-        ('reg_lo', C.c_int32), ('reg_hi', C.c_int32),
+        ('xt_rows', C.c_int32), ('reg_slots', C.c_int32), ('reg_lo', C.c_int32),
+        ('reg_hi', C.c_int32), ('reg_cap', C.c_int32),
     ]
 
 
@@ -56,6 +57,17 @@ class TowerArgs(C.Structure):
         ('gw', C.c_void_p * 9), ('gb', C.c_void_p * 9), ('gpre1t', C.c_void_p),
         ('wpf', C.c_void_p * 9), ('wpb', C.c_void_p * 9), ('act6p', C.c_void_p), ('act6tp', C.c_void_p),
         ('hpt', C.c_void_p * 6), ('gpt', C.c_void_p * 6), ('gpre1p', C.c_void_p),
+    ]
+
+
+class DecKlArgs(C.Structure):
+    _fields_ = [
+        ('d', C.c_int32), ('V', C.c_int32), ('rows', C.c_int32), ('ldt', C.c_int32), ('row0', C.c_int32),
+        ('D3p', C.c_void_p), ('D3tp', C.c_void_p), ('Wo', C.c_void_p),
+        ('bo', C.c_void_p), ('Mt', C.c_void_p), ('tsum', C.c_void_p), ('reg_idx', C.c_void_p),
+        ('scale', C.c_float), ('dZ', C.c_void_p), ('gW', C.c_void_p), ('gb', C.c_void_p),
+        ('loss_partials', C.c_void_p), ('loss_out', C.c_void_p), ('loss_scale', C.c_double),
+        ('ticket', C.c_void_p), ('ws', C.c_void_p),
     ]
 
 
@@ -91,6 +103,10 @@ SIGNATURES = {
     'cc_dec_bce_dw_blocks': (_I32, [_I32]),
     'cc_dec_softmax_kl_fused': (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _F32, _P, _P, _P]),
     'cc_reduce_loss': (C.c_int, [_P, _I32, _F64, _P, _P]),
+    'cc_dec_kl_ws_size': (_SZ, [_I32, _I32]),
+    'cc_dec_kl_blocks': (_I32, [_I32]),
+    'cc_dec_softmax_kl_dw': (C.c_int, [C.POINTER(DecKlArgs), _P]),
+    'cc_kl_tsum': (C.c_int, [_P, _I32, _I32, _P, _P]),
     'cc_adam_noise': (C.c_int, [_P, _P, _P, _P, _P, _I64, _F32, _F32, _F32, _F32, C.POINTER(NoiseArgs), _I64, _P]),
     'cc_adam_noise_pack': (C.c_int, [_P, _P, _P, _P, _P, _I64, _F32, _F32, _F32, _F32, C.POINTER(NoiseArgs), _I64,
                                      C.POINTER(AdamPack), _P]),
@@ -105,6 +121,9 @@ SIGNATURES = {
     'cc_similar_ws_size': (_SZ, [_I32]),
     'cc_similar_cards': (C.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     'cc_embed_grad_packed': (C.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _P]),
+    'cc_embed_identity_ws': (_SZ, [_I32, _I32]),
+    'cc_embed_identity_add': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
+    'cc_reg_rows': (C.c_int, [C.POINTER(NoiseArgs), _P]),
     'cc_tower_slab_elems': (_I64, [_I32]),
     'cc_tower_fwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_bwd': (C.c_int, [C.POINTER(TowerArgs), _P]),

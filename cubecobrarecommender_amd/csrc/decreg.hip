@@ -1,0 +1,568 @@
+// D2 output layer, fused: logits -> softmax -> KL against M~ rows -> dZ -> dWo, dbo, with no fp32
+// logits in HBM (model.py:64 Dense(V) + :98 softmax of the decoder_for_reg branch; train.py:85
+// kullback_leibler_divergence under TF 2.5's clip semantics).  The regulariser
+// counterpart of decout.hip's D1 kernel; the softmax's row normaliser needs every column, so the
+// logits are produced twice:
+//
+//   stats  (slice, 256-row group) blocks: z = D3 Wo + bo on MFMA over a 96-column slice, per-row
+//          max and sum exp(z - max) of the slice -> partials [rows][slices]
+//   merge  one wave per row: m = max_i m_i, s = sum_i s_i exp(m_i - m) -> {m, 1/s, ln s, S}, where
+//          S = sum_j clip(M~[row], 1e-7, 1) is the clipped row mass (cc_kl_tsum, once per M~)
+//   main   slice blocks over every row tile: z again, p = exp(z - m)/s, t = clip(M~ row, 1e-7, 1),
+//          KL += t (ln t - ln clip(p, 1e-7, 1)), dz = scale (p S - [p >= 1e-7] t) written row-major
+//          for the dX product and kept as dZ^T in LDS -> dWo[d][96] = D3^T dZ, dbo = colsum
+//   fix    TF's gradient passes through clip only where p >= 1e-7, so the exact S is
+//          S - delta, delta = sum_{p < 1e-7} t.  The main kernel raises a flag when any element of
+//          the step has p < 1e-7; two fix kernels (delta partials, then dz -= scale p delta with the
+//          matching dWo / dbo corrections) run only then — otherwise they exit at once.
+//
+// Padding rows (reg_idx < 0, owner-computes capacity / full-mode round-up) contribute nothing.
+// bf16 MFMA v_mfma_f32_32x32x16_bf16 with fp32 accumulation; A operands from the packed D3 images
+// the tower forward writes (cc_tower_args.act6p / act6tp), Wo read in place ([d][V], the slice
+// transposed into LDS).  Deterministic: every sum has a fixed order.
+#include "common.hpp"
+
+namespace {
+
+constexpr int NB = 96;       // V columns per block (230 slices at |V| = 22,000)
+constexpr int NJ = NB / 32;  // 32-column accumulator tiles per wave
+constexpr int NTH = 512;     // 8 waves
+constexpr int TR = 512;      // rows per tile of the main kernel (2 passes of 8 x 32)
+constexpr int SR = 256;      // rows per stats / fix-delta block
+constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+constexpr float PMIN = 1e-7f;
+constexpr float LN_PMIN = -16.11809565095832f;  // ln(1e-7)
+
+typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
+
+struct KlP {
+  int d, V, rows, ldt, row0, nsl;
+  const bf16_t *D3p, *D3tp, *Wo;
+  const float *bo, *Mt, *tsum;
+  const int32_t *reg_idx;
+  float scale;
+  bf16_t *dZ;
+  float *gW, *gb;
+  double *loss_partials, *loss_out;
+  double loss_scale;
+  uint32_t *ticket;
+  float *part_m, *part_s, *part_d;  // [rows][nsl]
+  float4 *rowstat;                  // [rows] {m, 1/s, ln s, S}
+  uint32_t *flag;                   // [1] an element with p < 1e-7 was seen this step
+};
+
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+__device__ __forceinline__ int sw_off(int row, int k, int chunks) {
+  return row * chunks * 8 + ((((k >> 3) ^ (row & 15)) << 3) | (k & 7));
+}
+__device__ __forceinline__ bf16x8_t frag(const bf16_t *S, int off) {
+  return *reinterpret_cast<const bf16x8_t *>(S + off);
+}
+__device__ __forceinline__ uint16_t bf16_bits(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+
+// Wo [d][V] slice [n0, n0 + NB) -> LDS k-contiguous image Wt[NB][d] (swizzled); columns past V clamp
+template <int D>
+__device__ __forceinline__ void load_wo_slice(const bf16_t *__restrict__ Wo, int V, int n0, bf16_t *Wt) {
+  constexpr int CHD = D / 8, CN = NB / 8, NT4 = (D / 4 * CN + NTH - 1) / NTH;
+  const int tid = threadIdx.x;
+  const bool vec = (V % 8 == 0) && n0 + NB <= V;
+  v4u w4[NT4][4];
+#pragma unroll
+  for (int q = 0; q < NT4; ++q) {
+    const int tk = tid + NTH * q, kg = tk / CN, nc = tk % CN;
+    if (kg >= D / 4) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bf16_t *row = Wo + (int64_t)(4 * kg + r) * V;
+      if (vec) {
+        w4[q][r] = *reinterpret_cast<const v4u *>(row + n0 + nc * 8);
+      } else {
+        uint32_t w2[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          w2[e] = (uint32_t)row[min(n0 + nc * 8 + 2 * e, V - 1)] |
+                  ((uint32_t)row[min(n0 + nc * 8 + 2 * e + 1, V - 1)] << 16);
+        w4[q][r] = v4u{w2[0], w2[1], w2[2], w2[3]};
+      }
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < NT4; ++q) {
+    const int tk = tid + NTH * q, kg = tk / CN, nc = tk % CN;
+    if (kg >= D / 4) continue;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int sh = 16 * (e & 1);
+      const uint32_t x0 = (w4[q][0][e >> 1] >> sh) & 0xFFFFu, x1 = (w4[q][1][e >> 1] >> sh) & 0xFFFFu;
+      const uint32_t x2 = (w4[q][2][e >> 1] >> sh) & 0xFFFFu, x3 = (w4[q][3][e >> 1] >> sh) & 0xFFFFu;
+      *reinterpret_cast<uint2 *>(Wt + sw_off(nc * 8 + e, 4 * kg, CHD)) = make_uint2(x0 | (x1 << 16), x2 | (x3 << 16));
+    }
+  }
+}
+
+// z[32 rows][NB] = bo + D3[rows] Wo_slice for the wave's 32-row block rb (packed D3 image)
+template <int D>
+__device__ __forceinline__ void logits_block(const KlP &p, const bf16_t *Wt, int rb, const float (&bias)[NJ],
+                                             f32x16_t (&acc)[NJ]) {
+  constexpr int nkk = D / 16, CHD = D / 8;
+  const int lane = threadIdx.x & 63, half = lane >> 5;
+  const bf16_t *src = p.D3p + ((int64_t)rb * nkk * 64 + lane) * 8;
+  constexpr int RING = nkk < 8 ? nkk : 8;  // A fragments in flight (a ring: the kernels that
+  bf16x8_t af[RING];                       // call this keep other accumulators live)
+#pragma unroll
+  for (int kk = 0; kk < RING; ++kk) af[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 512);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = bias[j];
+#pragma unroll
+  for (int kk = 0; kk < nkk; ++kk) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const bf16x8_t b = frag(Wt, sw_off(j * 32 + (lane & 31), kk * 16 + 8 * half, CHD));
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk % RING], b, acc[j], 0, 0, 0);
+    }
+    if (kk + RING < nkk) af[kk % RING] = *reinterpret_cast<const bf16x8_t *>(src + (kk + RING) * 512);
+  }
+}
+
+__device__ __forceinline__ float half_max(float v) {
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  return v;
+}
+__device__ __forceinline__ float half_sum(float v) {
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// ---------------------------------------------------------------- stats
+template <int D>
+__global__ __launch_bounds__(NTH) void kl_stats_kernel(KlP p) {
+  __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int sl = blockIdx.x, n0 = sl * NB;
+  const int r_blk = blockIdx.y * SR + w * 32;  // the wave's first row (regulariser-row index)
+  load_wo_slice<D>(p.Wo, p.V, n0, Wt);
+  __syncthreads();
+  if (r_blk >= p.rows) return;
+  float bias[NJ];
+  bool valid[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int gc = n0 + j * 32 + (lane & 31);
+    valid[j] = gc < p.V;
+    bias[j] = valid[j] ? p.bo[gc] : 0.f;
+  }
+  f32x16_t acc[NJ];
+  logits_block<D>(p, Wt, (p.row0 + r_blk) / 32, bias, acc);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) m = valid[j] ? fmaxf(m, acc[j][r]) : m;
+    m = half_max(m);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) s += valid[j] ? __builtin_amdgcn_exp2f((acc[j][r] - m) * LOG2E) : 0.f;
+    s = half_sum(s);
+    if ((lane & 31) == r) {
+      const int row = r_blk + acc_row(r, lane);
+      p.part_m[(int64_t)row * p.nsl + sl] = m;
+      p.part_s[(int64_t)row * p.nsl + sl] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- merge (one wave per row)
+__global__ __launch_bounds__(256) void kl_merge_kernel(KlP p) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *p.flag = 0u;  // this step's fix flag starts clear
+  if (row >= p.rows) return;
+  const float *pm = p.part_m + (int64_t)row * p.nsl, *ps = p.part_s + (int64_t)row * p.nsl;
+  float m = -INFINITY;
+  for (int i = lane; i < p.nsl; i += 64) m = fmaxf(m, pm[i]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  float s = 0.f;
+  for (int i = lane; i < p.nsl; i += 64) s += ps[i] * __builtin_amdgcn_exp2f((pm[i] - m) * LOG2E);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0) {
+    const int card = p.reg_idx[row];
+    p.rowstat[row] = make_float4(m, 1.f / s, __logf(s), card >= 0 ? p.tsum[card] : 0.f);
+  }
+}
+
+// ---------------------------------------------------------------- main
+constexpr int ZT_BYTES = NB * TR * 2;
+struct MainSmem {
+  bf16_t Zt[NB * TR];       // dZ^T tile [NB][TR] (swizzled)
+  float4 rs[TR];            // row stats of the tile
+  int32_t card[TR];         // reg_idx of the tile's rows
+  float red_cs[NTH / 64][NB];
+  double red_loss[NTH / 64];
+  int lastflag;
+};
+
+// FIX = false: the main pass.  FIX = true: the exact-clip correction (runs only when p.flag is set):
+// c = -scale p delta_row replaces dz; dZ, dWo, dbo are updated in place.
+template <int D, bool FIX>
+__global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
+  constexpr int CHB = TR / 8;
+  __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
+  __shared__ __attribute__((aligned(16))) MainSmem sm;
+  if constexpr (FIX) {
+    if (__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
+  const int n0 = blockIdx.x * NB;
+  const int V = p.V;
+  load_wo_slice<D>(p.Wo, V, n0, Wt);
+  float bias[NJ], cs[NJ];
+  bool valid[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int gc = n0 + j * 32 + (lane & 31);
+    valid[j] = gc < V;
+    bias[j] = valid[j] ? p.bo[gc] : 0.f;
+    cs[j] = 0.f;
+  }
+  float klsum = 0.f;
+  bool dead = false;
+  // M~ rows and dZ through buffer descriptors: a 32-bit byte offset per access instead of a 64-bit
+  // address (M~ < 4 GB at |V| <= 32k; dZ rows x V x 2 B < 4 GB)
+  const __amdgpu_buffer_rsrc_t mt_rs = __builtin_amdgcn_make_buffer_rsrc((void *)p.Mt, (short)0, 0xFFFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dz_rs = __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, 0xFFFFFFFF, 0x00020000);
+  const float scale = p.scale;
+
+  for (int t0 = 0; t0 < p.rows; t0 += TR) {
+    const int nt = min(TR, p.rows - t0);
+    __syncthreads();  // previous tile's phase 2 done with Zt / rs
+    for (int i = tid; i < nt; i += NTH) {
+      float4 st = p.rowstat[t0 + i];
+      if constexpr (FIX) {  // .w <- delta of the row: the sum of its slices' partials, in order
+        float dl = 0.f;
+        const float *pd = p.part_d + (int64_t)(t0 + i) * p.nsl;
+        for (int s = 0; s < p.nsl; ++s) dl += pd[s];
+        st.w = dl;
+      }
+      sm.rs[i] = st;
+      sm.card[i] = p.reg_idx[t0 + i];
+    }
+    __syncthreads();
+    // ---- phase 1: two passes of 8 waves x 32 rows
+#pragma unroll 1
+    for (int ps = 0; ps < 2; ++ps) {
+      const int rb = ps * 256 + w * 32;  // tile-local first row of the wave
+      if (rb >= nt) continue;            // wave-uniform
+      f32x16_t acc[NJ];
+      logits_block<D>(p, Wt, (p.row0 + t0 + rb) / 32, bias, acc);
+      // the M~ values of the wave's elements: column tile j's 16 per lane are loaded while tile
+      // j - 1's epilogue runs (issued behind the MFMAs: the A fragments are dead by then)
+      int cards[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) cards[r] = sm.card[rb + acc_row(r, lane)];
+      uint32_t zrow = (uint32_t)((t0 + rb + 4 * half) * V + n0 + (lane & 31));
+      asm volatile("" : "+v"(zrow));  // per-pass base of the dZ stores (no hoisted 64-bit addresses)
+      float tv[2][16];
+      auto load_t = [&](int j, float (&dst)[16]) {
+        const uint32_t gc = (uint32_t)(n0 + j * 32 + (lane & 31));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float v = __builtin_amdgcn_raw_buffer_load_b32(mt_rs, 4u * ((uint32_t)max(cards[r], 0) * (uint32_t)V + gc), 0, 0);
+          dst[r] = (cards[r] >= 0 && valid[j]) ? v : 0.f;
+        }
+      };
+      if constexpr (!FIX) load_t(0, tv[0]);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int col = j * 32 + (lane & 31);
+        if constexpr (!FIX) {
+          if (j + 1 < NJ) load_t(j + 1, tv[(j + 1) & 1]);
+        }
+        uint16_t tt[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int lr = rb + acc_row(r, lane);
+          const float4 st = sm.rs[lr];
+          const bool live_row = cards[r] >= 0 && valid[j];
+          const float zm = acc[j][r] - st.x;
+          const float pr = __builtin_amdgcn_exp2f(zm * LOG2E) * st.y;
+          const bool live = pr >= PMIN;
+          float dz;
+          if constexpr (!FIX) {
+            const float tc = __builtin_amdgcn_fmed3f(tv[j & 1][r], PMIN, 1.f);
+            const float lq = live ? fminf(zm - st.z, 0.f) : LN_PMIN;
+            const float term = tc * fmaf(__builtin_amdgcn_logf(tc), LN2, -lq);
+            klsum += live_row ? term : 0.f;
+            dead |= live_row && !live;
+            dz = live_row ? scale * (pr * st.w - (live ? tc : 0.f)) : 0.f;
+          } else {
+            dz = live_row ? -scale * pr * st.w : 0.f;  // st.w = delta
+          }
+          const uint32_t zoff = 2u * (zrow + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V + j * 32));
+          uint16_t zb;
+          if constexpr (FIX) {
+            const float old = valid[j] ? bf2f(p.dZ[zoff / 2]) : 0.f;
+            zb = bf16_bits(old + dz);
+            dz = __uint_as_float((uint32_t)zb << 16) - old;  // the change actually applied
+            tt[r] = bf16_bits(dz);
+          } else {
+            zb = bf16_bits(dz);
+            tt[r] = zb;
+          }
+          cs[j] += __uint_as_float((uint32_t)tt[r] << 16);
+          if (valid[j]) __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, 0);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<uint2 *>(sm.Zt + sw_off(col, rb + 8 * g + 4 * half, CHB)) =
+              *reinterpret_cast<const uint2 *>(&tt[4 * g]);
+      }
+    }
+    __syncthreads();
+    // ---- phase 2: dWo[d][NB] (+)= D3^T[d][tile rows] dZ[tile rows][NB] (wave w: d rows 32w..).
+    // A fresh accumulator per tile, added into gW (the block's slice stays L2-resident between
+    // tiles): nothing of phase 2 is live across phase 1's epilogue.
+    if (w * 32 < D) {
+      f32x16_t acc2[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
+      // K = the tile's rows (a multiple of 32) in chunks of 32 (two 16-row fragments), a ring of
+      // two chunks in flight
+      const int nc = nt / 32;
+      const int j0 = (p.row0 + t0) / 16;
+      const bf16_t *arow = p.D3tp + ((int64_t)w * (p.ldt / 16) * 64 + lane) * 8 + (int64_t)j0 * 512;
+      bf16x8_t ring[2][2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) ring[q][h] = *reinterpret_cast<const bf16x8_t *>(arow + (2 * min(q, nc - 1) + h) * 512);
+      for (int c0 = 0; c0 < nc; c0 += 2) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int c = c0 + q;
+          if (c < nc) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int j = 0; j < NJ; ++j) {
+                const bf16x8_t b = frag(sm.Zt, sw_off(j * 32 + (lane & 31), c * 32 + h * 16 + 8 * half, CHB));
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[q][h], b, acc2[j], 0, 0, 0);
+              }
+            const int cn = min(c + 2, nc - 1);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) ring[q][h] = *reinterpret_cast<const bf16x8_t *>(arow + (2 * cn + h) * 512);
+          }
+        }
+      }
+      const bool first = !FIX && t0 == 0;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int gc = n0 + j * 32 + (lane & 31);
+        if (gc < V) {
+          uint32_t g0 = (uint32_t)((w * 32 + 4 * half) * V + gc);
+          asm volatile("" : "+v"(g0));  // opaque per tile: keeps 48 row addresses from being hoisted
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float *gp = p.gW + (g0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V));
+            *gp = first ? acc2[j][r] : *gp + acc2[j][r];
+          }
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: dbo, loss partial, the fix flag
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const float c2 = cs[j] + __shfl_xor(cs[j], 32);
+    if (half == 0) sm.red_cs[w][j * 32 + (lane & 31)] = c2;
+  }
+  if constexpr (!FIX) {
+    if (__ballot(dead) != 0ull && lane == 0)
+      __hip_atomic_fetch_or(p.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) klsum += __shfl_xor(klsum, off);
+    if (lane == 0) sm.red_loss[w] = (double)klsum;
+  }
+  __syncthreads();
+  if (tid < NB && n0 + tid < V) {
+    float g = 0.f;
+    for (int i = 0; i < NTH / 64; ++i) g += sm.red_cs[i][tid];
+    if constexpr (FIX)
+      p.gb[n0 + tid] += g;
+    else
+      p.gb[n0 + tid] = g;
+  }
+  if constexpr (!FIX) {
+    if (tid == 0) {
+      double sum = 0.0;
+      for (int i = 0; i < NTH / 64; ++i) sum += sm.red_loss[i];
+      sm.lastflag = 0;
+      if (!p.loss_out) {
+        p.loss_partials[blockIdx.x] = sum;
+      } else {
+        __hip_atomic_store(&p.loss_partials[blockIdx.x], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t tk = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sm.lastflag = tk == gridDim.x - 1;
+      }
+    }
+    if (p.loss_out) {
+      __syncthreads();
+      if (sm.lastflag) {
+        double s2d = 0.0;
+        for (int i = tid; i < (int)gridDim.x; i += NTH)
+          s2d += __hip_atomic_load(&p.loss_partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s2d += __shfl_xor(s2d, off);
+        if (lane == 0) sm.red_loss[w] = s2d;
+        __syncthreads();
+        if (tid == 0) {
+          double tot = 0.0;
+          for (int i = 0; i < NTH / 64; ++i) tot += sm.red_loss[i];
+          p.loss_out[0] = tot * p.loss_scale;
+          __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- fix: delta partials
+template <int D>
+__global__ __launch_bounds__(NTH) void kl_delta_kernel(KlP p) {
+  __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
+  if (__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int sl = blockIdx.x, n0 = sl * NB;
+  const int r_blk = blockIdx.y * SR + w * 32;
+  load_wo_slice<D>(p.Wo, p.V, n0, Wt);
+  __syncthreads();
+  if (r_blk >= p.rows) return;
+  float bias[NJ];
+  bool valid[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int gc = n0 + j * 32 + (lane & 31);
+    valid[j] = gc < p.V;
+    bias[j] = valid[j] ? p.bo[gc] : 0.f;
+  }
+  f32x16_t acc[NJ];
+  logits_block<D>(p, Wt, (p.row0 + r_blk) / 32, bias, acc);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = r_blk + acc_row(r, lane);
+    const float4 st = p.rowstat[row];
+    const int card = p.reg_idx[row];
+    float dl = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const float pr = __builtin_amdgcn_exp2f((acc[j][r] - st.x) * LOG2E) * st.y;
+      if (card >= 0 && valid[j] && !(pr >= PMIN)) {
+        const float t = p.Mt[(int64_t)card * p.V + n0 + j * 32 + (lane & 31)];
+        dl += __builtin_amdgcn_fmed3f(t, PMIN, 1.f);
+      }
+    }
+    dl = half_sum(dl);
+    if ((lane & 31) == r) p.part_d[(int64_t)row * p.nsl + sl] = dl;
+  }
+}
+
+__global__ __launch_bounds__(256) void kl_tsum_kernel(const float *__restrict__ Mt, int V, float *__restrict__ tsum) {
+  __shared__ float red[4];
+  const float *row = Mt + (int64_t)blockIdx.x * V;
+  float s = 0.f;
+  for (int j = threadIdx.x; j < V; j += 256) s += __builtin_amdgcn_fmed3f(row[j], PMIN, 1.f);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) tsum[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+}  // namespace
+
+extern "C" size_t cc_dec_kl_ws_size(int32_t rows, int32_t V) {
+  const int64_t nsl = cdiv(V, NB);
+  return (size_t)(3 * rows * nsl * sizeof(float) + rows * sizeof(float4) + 256);
+}
+
+extern "C" int32_t cc_dec_kl_blocks(int32_t V) { return (int32_t)cdiv(V, NB); }
+
+extern "C" int cc_kl_tsum(const float *Mt, int32_t n, int32_t V, float *tsum, void *stream) {
+  CC_REQUIRE(Mt && tsum && n >= 0 && V > 0, "cc_kl_tsum: args");
+  if (n == 0) return CC_OK;
+  hipLaunchKernelGGL(kl_tsum_kernel, dim3((unsigned)n), dim3(256), 0, as_stream(stream), Mt, V, tsum);
+  CC_LAUNCH_CHECK("kl_tsum_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
+  CC_REQUIRE(a && a->D3p && a->D3tp && a->Wo && a->bo && a->Mt && a->tsum && a->reg_idx && a->dZ && a->gW &&
+                 a->gb && a->loss_partials && a->ws,
+             "cc_dec_softmax_kl_dw: null pointer");
+  CC_REQUIRE(a->d == 128 || a->d == 256, "cc_dec_softmax_kl_dw: d must be 128 or 256");
+  CC_REQUIRE(a->rows > 0 && a->rows % 32 == 0, "cc_dec_softmax_kl_dw: rows must be a positive multiple of 32");
+  CC_REQUIRE(a->row0 % 32 == 0 && a->ldt % 16 == 0 && a->ldt >= a->row0 + a->rows,
+             "cc_dec_softmax_kl_dw: row0 % 32, ldt % 16, ldt >= row0 + rows");
+  CC_REQUIRE(a->V > 0 && (!a->loss_out || a->ticket), "cc_dec_softmax_kl_dw: V / ticket");
+  CC_REQUIRE((((uintptr_t)a->D3p | (uintptr_t)a->D3tp | (uintptr_t)a->ws) & 15) == 0,
+             "cc_dec_softmax_kl_dw: packed images and ws 16-B aligned");
+  KlP p;
+  p.d = a->d;
+  p.V = a->V;
+  p.rows = a->rows;
+  p.ldt = a->ldt;
+  p.row0 = a->row0;
+  p.nsl = (int)cdiv(a->V, NB);
+  p.D3p = (const bf16_t *)a->D3p;
+  p.D3tp = (const bf16_t *)a->D3tp;
+  p.Wo = (const bf16_t *)a->Wo;
+  p.bo = a->bo;
+  p.Mt = a->Mt;
+  p.tsum = a->tsum;
+  p.reg_idx = a->reg_idx;
+  p.scale = a->scale;
+  p.dZ = (bf16_t *)a->dZ;
+  p.gW = a->gW;
+  p.gb = a->gb;
+  p.loss_partials = a->loss_partials;
+  p.loss_out = a->loss_out;
+  p.loss_scale = a->loss_scale;
+  p.ticket = a->ticket;
+  char *ws = (char *)a->ws;
+  const int64_t pn = (int64_t)a->rows * p.nsl;
+  p.rowstat = (float4 *)ws;
+  p.part_m = (float *)(ws + a->rows * sizeof(float4));
+  p.part_s = p.part_m + pn;
+  p.part_d = p.part_s + pn;
+  p.flag = (uint32_t *)(p.part_d + pn);
+  hipStream_t s = as_stream(stream);
+  const dim3 gs((unsigned)p.nsl, (unsigned)cdiv(a->rows, SR)), gm((unsigned)p.nsl);
+#define KL_LAUNCH(DD)                                                                                          \
+  if (a->d == DD) {                                                                                          \
+    hipLaunchKernelGGL((kl_stats_kernel<DD>), gs, dim3(NTH), 0, s, p);                                      \
+    CC_LAUNCH_CHECK("kl_stats_kernel");                                                                      \
+    hipLaunchKernelGGL(kl_merge_kernel, dim3((unsigned)cdiv(a->rows, 4)), dim3(256), 0, s, p);              \
+    CC_LAUNCH_CHECK("kl_merge_kernel");                                                                      \
+    hipLaunchKernelGGL((kl_main_kernel<DD, false>), gm, dim3(NTH), 0, s, p);                                \
+    CC_LAUNCH_CHECK("kl_main_kernel");                                                                       \
+    hipLaunchKernelGGL((kl_delta_kernel<DD>), gs, dim3(NTH), 0, s, p);                                      \
+    CC_LAUNCH_CHECK("kl_delta_kernel");                                                                      \
+    hipLaunchKernelGGL((kl_main_kernel<DD, true>), gm, dim3(NTH), 0, s, p);                                 \
+    CC_LAUNCH_CHECK("kl_fix_kernel");                                                                        \
+  }
+  KL_LAUNCH(256)
+  KL_LAUNCH(128)
+#undef KL_LAUNCH
+  return CC_OK;
+}

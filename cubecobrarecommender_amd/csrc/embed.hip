@@ -303,7 +303,8 @@ __global__ __launch_bounds__(64 * SGW) void scatter_bwd_kernel(const float *__re
 // by the tower backward chain).  Every row costs the same (no Zipf-heavy row latency chain, no
 // per-row dispatch); row V (with bias_grad) is the all-ones row: db1 = colsum dPre1.  A block owns
 // EG_ROWS rows of W1 and all d columns, so it also clears the bit words it consumed.
-constexpr int EG_ROWS = 64, EG_BK = 64, EG_XWMAX = 32;  // R <= 1024
+constexpr int EG_ROWS = 64, EG_BK = 64;
+constexpr int EG_XWMAX = 64;  // R <= 2048 (bit words per row staged in LDS: template XWM <= EG_XWMAX)
 
 typedef __attribute__((ext_vector_type(4))) uint32_t eg_u32x4;  // ext vectors stay in VGPRs
 __device__ __forceinline__ bf16x8_t expand_bits8(uint32_t b) {
@@ -314,7 +315,7 @@ __device__ __forceinline__ bf16x8_t expand_bits8(uint32_t b) {
   return __builtin_bit_cast(bf16x8_t, w);
 }
 
-template <int NC>
+template <int NC, int XWM>
 __global__ __launch_bounds__(256, 2) void embed_grad_mfma_kernel(const bf16_t *__restrict__ gT, int V,
                                                                 int d, int R, int RP, uint32_t *xt,
                                                                 float *__restrict__ grad,
@@ -323,15 +324,18 @@ __global__ __launch_bounds__(256, 2) void embed_grad_mfma_kernel(const bf16_t *_
   constexpr int NCH = NC * CH / 256;            // chunks staged per thread
   constexpr int NJ = NC / 64;                   // 32-col accumulators per wave (2 x 2 waves)
   __shared__ __attribute__((aligned(16))) bf16_t Bs[2][NC * EG_BK];
-  __shared__ uint32_t As[EG_ROWS][EG_XWMAX + 1];
+  __shared__ uint32_t As[EG_ROWS][XWM + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, half = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
   const int v0 = blockIdx.x * EG_ROWS;
-  const int XW = (R + 31) >> 5, XWP = RP >> 5;
+  // R rows enter the product; RP is the B image's row stride (>= ceil64(R): the full-mode
+  // regulariser's identity rows sit past R in the same image and are added separately)
+  const int RPE = (R + 63) & ~63;
+  const int XW = (R + 31) >> 5, XWP = RPE >> 5;
   EG_PROBE(0);
   // the block's bit words: every load issued before any store (one HBM round trip, not one per
   // word — the zeroing stores would otherwise order each next load behind them)
-  constexpr int AS_Q = EG_ROWS * EG_XWMAX / 256;
+  constexpr int AS_Q = EG_ROWS * XWM / 256;
   uint32_t mv[AS_Q];
 #pragma unroll
   for (int q = 0; q < AS_Q; ++q) {
@@ -352,7 +356,7 @@ __global__ __launch_bounds__(256, 2) void embed_grad_mfma_kernel(const bf16_t *_
       As[r][w] = mv[q];
     }
   }
-  const int nk = RP / EG_BK;
+  const int nk = RPE / EG_BK;
   const int arow = wm * 32 + (lane & 31);
   for (int nc0 = 0; nc0 < d; nc0 += NC) {
     f32x16_t acc[NJ];
@@ -417,15 +421,17 @@ __global__ __launch_bounds__(256, 2) void embed_grad_mfma_kernel(const bf16_t *_
 // tiles), so each B fragment is loaded once per block; A = the row's bit bytes expanded in
 // registers (LDS bit words, as above).  EG_PU fragment pairs in flight per lane.
 constexpr int EG_PU = 8;
+template <int XWM>
 __global__ __launch_bounds__(256, 2) void embed_grad_pk_kernel(const bf16_t *__restrict__ gP, int V, int R,
                                                               int RP, uint32_t *xt, float *__restrict__ grad,
                                                               float *__restrict__ bias_grad) {
   constexpr int D = 256;
-  __shared__ uint32_t As[EG_ROWS][EG_XWMAX + 1];
+  __shared__ uint32_t As[EG_ROWS][XWM + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
   const int v0 = blockIdx.x * EG_ROWS;
-  const int XW = (R + 31) >> 5, XWP = RP >> 5;
-  constexpr int AS_Q = EG_ROWS * EG_XWMAX / 256;
+  const int RPE = (R + 63) & ~63;  // rows in the product; RP: the packed image's reduction stride
+  const int XW = (R + 31) >> 5, XWP = RPE >> 5;
+  constexpr int AS_Q = EG_ROWS * XWM / 256;
   uint32_t mv[AS_Q];
 #pragma unroll
   for (int q = 0; q < AS_Q; ++q) {
@@ -441,7 +447,7 @@ __global__ __launch_bounds__(256, 2) void embed_grad_pk_kernel(const bf16_t *__r
   // the first fragments fly while the bit words are staged
   const bf16_t *b0 = gP + ((int64_t)(2 * w) * (RP / 16) * 64 + lane) * 8;
   const bf16_t *b1 = gP + ((int64_t)(2 * w + 1) * (RP / 16) * 64 + lane) * 8;
-  const int nk = RP / 16;
+  const int nk = RPE / 16;
   bf16x8_t f0[EG_PU], f1[EG_PU];
 #pragma unroll
   for (int u = 0; u < EG_PU; ++u)
@@ -512,13 +518,73 @@ extern "C" int cc_embed_grad_packed(const void *dpre_p, int32_t V, int32_t d, in
                                     uint32_t *xt_bits, float *grad, float *bias_grad, void *stream) {
   CC_REQUIRE(dpre_p && xt_bits && grad, "cc_embed_grad_packed: null pointer");
   CC_REQUIRE(d == 256, "cc_embed_grad_packed: d must be 256");
-  CC_REQUIRE(R > 0 && R <= 32 * EG_XWMAX, "cc_embed_grad_packed: R must be 1..1024");
+  CC_REQUIRE(R > 0 && R <= 32 * EG_XWMAX, "cc_embed_grad_packed: R must be 1..2048");
   CC_REQUIRE(ld_t % 64 == 0 && ld_t >= R && ((uintptr_t)dpre_p % 16) == 0,
              "cc_embed_grad_packed: ld_t must be a multiple of 64 covering R, image 16-B aligned");
   const int rows = bias_grad ? V + 1 : V;
-  hipLaunchKernelGGL(embed_grad_pk_kernel, dim3((unsigned)cdiv(rows, EG_ROWS)), dim3(256), 0, as_stream(stream),
-                     (const bf16_t *)dpre_p, V, R, ld_t, xt_bits, grad, bias_grad);
+  const dim3 grid((unsigned)cdiv(rows, EG_ROWS));
+  if (R <= 1024)
+    hipLaunchKernelGGL((embed_grad_pk_kernel<32>), grid, dim3(256), 0, as_stream(stream),
+                       (const bf16_t *)dpre_p, V, R, ld_t, xt_bits, grad, bias_grad);
+  else
+    hipLaunchKernelGGL((embed_grad_pk_kernel<64>), grid, dim3(256), 0, as_stream(stream),
+                       (const bf16_t *)dpre_p, V, R, ld_t, xt_bits, grad, bias_grad);
   CC_LAUNCH_CHECK("embed_grad_pk_kernel");
+  return CC_OK;
+}
+
+namespace {
+// Full-mode regulariser rows are one-hot identity rows: their W1 gradient is dPre1 itself, row by
+// row (rows of W1 touched once each: plain read-modify-write, no atomics).  Block b handles rows
+// [64b, 64b+64) for all d columns and writes its column sums to partial[b][d]; the bias gradient
+// adds them in block order (deterministic).
+constexpr int ID_ROWS = 64;
+__global__ __launch_bounds__(256) void embed_identity_add_kernel(const float *__restrict__ dpre, int n, int d,
+                                                                 int lo, int round_bf16,
+                                                                 float *__restrict__ grad,
+                                                                 float *__restrict__ partial) {
+  const int r0 = blockIdx.x * ID_ROWS, r1 = min(n, r0 + ID_ROWS);
+  for (int c = threadIdx.x; c < d; c += 256) {
+    float cs = 0.f;
+    for (int r = r0; r < r1; ++r) {
+      float v = dpre[(int64_t)r * d + c];
+      if (round_bf16) v = bf2f(f2bf(v));
+      grad[(int64_t)(lo + r) * d + c] += v;
+      cs += v;
+    }
+    partial[(int64_t)blockIdx.x * d + c] = cs;
+  }
+}
+
+__global__ __launch_bounds__(256) void embed_identity_bias_kernel(const float *__restrict__ partial, int nb,
+                                                                  int d, float *__restrict__ bias_grad) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += partial[(int64_t)b * d + c];
+  bias_grad[c] += s;
+}
+}  // namespace
+
+extern "C" size_t cc_embed_identity_ws(int32_t n, int32_t d) {
+  return (size_t)cdiv(n, ID_ROWS) * (size_t)d * sizeof(float);
+}
+
+extern "C" int cc_embed_identity_add(int32_t dtype, const float *dpre, int32_t n, int32_t d, int32_t lo,
+                                     float *grad, float *bias_grad, float *partial, void *stream) {
+  CC_REQUIRE(dpre && grad && partial, "cc_embed_identity_add: null pointer");
+  CC_REQUIRE(n >= 0 && d > 0 && lo >= 0, "cc_embed_identity_add: bad n/d/lo");
+  if (n == 0) return CC_OK;
+  const int nb = (int)cdiv(n, ID_ROWS);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(embed_identity_add_kernel, dim3(nb), dim3(256), 0, s, dpre, n, d, lo,
+                     dtype == CC_BF16 ? 1 : 0, grad, partial);
+  CC_LAUNCH_CHECK("embed_identity_add_kernel");
+  if (bias_grad) {
+    hipLaunchKernelGGL(embed_identity_bias_kernel, dim3((unsigned)cdiv(d, 256)), dim3(256), 0, s, partial, nb, d,
+                       bias_grad);
+    CC_LAUNCH_CHECK("embed_identity_bias_kernel");
+  }
   return CC_OK;
 }
 
@@ -629,18 +695,21 @@ extern "C" int cc_embed_grad_mfma(const void *dpre_t, int32_t V, int32_t d, int3
                                   uint32_t *xt_bits, float *grad, float *bias_grad, void *stream) {
   CC_REQUIRE(dpre_t && xt_bits && grad, "cc_embed_grad_mfma: null pointer");
   CC_REQUIRE(d % 128 == 0 && d >= 128 && d <= 1024, "cc_embed_grad_mfma: d must be 128..1024, %128");
-  CC_REQUIRE(R > 0 && R <= 32 * EG_XWMAX, "cc_embed_grad_mfma: R must be 1..1024");
+  CC_REQUIRE(R > 0 && R <= 32 * EG_XWMAX, "cc_embed_grad_mfma: R must be 1..2048");
   CC_REQUIRE(ld_t % EG_BK == 0 && ld_t >= R && ((uintptr_t)dpre_t % 16) == 0,
              "cc_embed_grad_mfma: ld_t must be a multiple of 64 covering R (zero padded), 16-B aligned");
   const int rows = bias_grad ? V + 1 : V;
   const dim3 grid((unsigned)cdiv(rows, EG_ROWS)), block(256);
   hipStream_t s = as_stream(stream);
-  if (d % 256 == 0)
-    hipLaunchKernelGGL((embed_grad_mfma_kernel<256>), grid, block, 0, s, (const bf16_t *)dpre_t, V, d, R,
-                       ld_t, xt_bits, grad, bias_grad);
-  else
-    hipLaunchKernelGGL((embed_grad_mfma_kernel<128>), grid, block, 0, s, (const bf16_t *)dpre_t, V, d, R,
-                       ld_t, xt_bits, grad, bias_grad);
+#define EGM(NCC, XWMM)                                                                                 \
+  hipLaunchKernelGGL((embed_grad_mfma_kernel<NCC, XWMM>), grid, block, 0, s, (const bf16_t *)dpre_t, V, d, R, \
+                     ld_t, xt_bits, grad, bias_grad)
+  if (d % 256 == 0) {
+    if (R <= 1024) EGM(256, 32); else EGM(256, 64);
+  } else {
+    if (R <= 1024) EGM(128, 32); else EGM(128, 64);
+  }
+#undef EGM
   CC_LAUNCH_CHECK("embed_grad_mfma_kernel");
   return CC_OK;
 }

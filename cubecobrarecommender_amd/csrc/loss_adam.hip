@@ -35,7 +35,8 @@ __device__ __forceinline__ double block_reduce_d(double v, double *red) {
 // One workgroup per regulariser row b.  p = softmax(z2[b]); t = clip(M~[reg_idx[b]], 1e-7, 1);
 // q = clip(p, 1e-7, 1); KL_b = sum t log(t/q).  Gradient (TF clip_by_value = Minimum/Maximum
 // grads: passes where p >= 1e-7): g_j = -t_j/p_j [p_j >= 1e-7]; <p,g> = -S, S = sum_{p>=1e-7} t;
-// dz_j = reg/B * (p_j g_j + p_j S) = reg/B * ([p_j>=1e-7] (-t_j) + p_j S).
+// dz_j = scale * (p_j g_j + p_j S) = scale * ([p_j>=1e-7] (-t_j) + p_j S), scale = reg * the
+// row's weight (1/B for B sampled rows).
 template <typename T>
 __global__ __launch_bounds__(NT) void softmax_kl_kernel(const float *__restrict__ Z2, int V,
                                                         const float *__restrict__ Mt,
@@ -46,6 +47,11 @@ __global__ __launch_bounds__(NT) void softmax_kl_kernel(const float *__restrict_
   __shared__ double redd[NT / 64];
   const int b = blockIdx.x;
   const float *z = Z2 + (int64_t)b * V;
+  if (reg_idx[b] < 0) {  // padding row (owner-computes capacity): no KL term, zero gradient
+    for (int j = threadIdx.x; j < V; j += NT) DT<T>::st(dZ + (int64_t)b * V + j, 0.f);
+    if (threadIdx.x == 0) kl_part[b] = 0.0;
+    return;
+  }
   const float *trow = Mt + (int64_t)reg_idx[b] * V;
   float mx = -INFINITY;
   for (int j = threadIdx.x; j < V; j += NT) mx = fmaxf(mx, z[j]);
@@ -105,6 +111,11 @@ __global__ __launch_bounds__(NTR) void softmax_kl_rows_kernel(const float *__res
   __shared__ float redf[NTR / 64];
   __shared__ double redd[NTR / 64];
   const int b = blockIdx.x, V4 = V >> 2;
+  if (reg_idx[b] < 0) {  // padding row (owner-computes capacity): no KL term, zero gradient
+    for (int j = threadIdx.x; j < V; j += NTR) DT<T>::st(dZ + (int64_t)b * V + j, 0.f);
+    if (threadIdx.x == 0) kl_part[b] = 0.0;
+    return;
+  }
   const float4 *z4 = reinterpret_cast<const float4 *>(Z2 + (int64_t)b * V);
   const float4 *t4 = reinterpret_cast<const float4 *>(Mt + (int64_t)reg_idx[b] * V);
   float z[NV][4], t[NV][4];
@@ -348,11 +359,10 @@ __global__ __launch_bounds__(NT) void to_bf16_kernel(const float *__restrict__ x
 }  // namespace
 
 extern "C" int cc_dec_softmax_kl_fused(int32_t dtype, const float *Z2, int32_t B, int32_t V,
-                                       const float *y_reg, const int32_t *reg_idx, float reg,
+                                       const float *y_reg, const int32_t *reg_idx, float scale,
                                        void *dZ, double *kl_partials, void *stream) {
   CC_REQUIRE(Z2 && y_reg && reg_idx && dZ && kl_partials, "cc_dec_softmax_kl_fused: null pointer");
   if (B == 0) return CC_OK;
-  const float scale = reg / (float)B;
   const bool aligned = (V % 4 == 0) && ((uintptr_t)Z2 % 16 == 0) && ((uintptr_t)y_reg % 16 == 0) &&
                        ((uintptr_t)dZ % 16 == 0);
   const int nv = (int)cdiv(V, 4 * NTR);

@@ -13,7 +13,9 @@
 //   add   : k draws, rejection against the global CDF of neg_sampler until the card is not
 //           in the cube (== the renormalised law of :93-94), exact fallback after 256 tries
 //   x = (cube \ cut) U add  (sorted CSR row),  y = cube \ ycut  (bitmask)     :96-101
-// The B reg rows (generator.py:47-51) are drawn by thread 0 of each block into rows B..2B-1.
+// The B reg rows (generator.py:47-51) are drawn by thread 0 of each block into rows B..2B-1
+// (with_reg = 1), or — data parallel with M~ row-sharded — all ranks draw the global slots and
+// each keeps the rows it owns (cc_reg_rows, owner computes).
 #include <algorithm>
 
 #include "adam.hpp"
@@ -52,15 +54,6 @@ __device__ __forceinline__ int search_right(const double *__restrict__ cdf, int 
       hi = mid;
   }
   return lo < V ? lo : V - 1;
-}
-
-// u in [0,1) -> [cdf[lo-1], cdf[hi-1]) (cdf[-1] = 0): the inverse-CDF draw restricted to cards
-// [lo, hi).  A product that rounds onto the upper edge is folded back to the lower one.
-__device__ __forceinline__ double shard_u(const double *__restrict__ cdf, int lo, int hi, double u) {
-#pragma clang fp contract(off)
-  const double ulo = lo > 0 ? cdf[lo - 1] : 0.0, uhi = cdf[hi - 1];
-  const double v = ulo + u * (uhi - ulo);
-  return v < uhi ? v : ulo;
 }
 
 __device__ __forceinline__ double noise_level(double mean, double std, double z) {
@@ -108,8 +101,7 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
   const int tid = threadIdx.x;
   const uint32_t slot = a.slot_base + (uint32_t)b;
   const uint32_t step = (uint32_t)step64;
-  const int R = a.with_reg ? 2 * a.B : a.B;
-  const int XW = (R + 31) >> 5;
+  const int XW = (a.xt_rows + 31) >> 5;
 
   const int32_t *perm = a.perm + (epoch % a.num_perms) * (int64_t)a.num_cubes;
   const int32_t cube = perm[batch * (int64_t)a.batch_stride + a.batch_offset + b];
@@ -209,18 +201,66 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
   // regulariser row for this slot (generator.py:47-51): one draw ∝ neg_sampler
   if (a.with_reg && tid == 0) {
     const u32x4 o = rng(a.seed, step, slot, KIND_REG, 0, 0);
-    int j;
-    if (a.reg_hi > 0) {  // row-sharded M~: the draw conditioned on the rank's shard of cards
-      j = search_right(a.cdf, a.V, shard_u(a.cdf, a.reg_lo, a.reg_hi, u53(o.x, o.y)), a.guide, a.guide_log2);
-      j = j < a.reg_lo ? a.reg_lo : (j >= a.reg_hi ? a.reg_hi - 1 : j);
-    } else {
-      j = search_right(a.cdf, a.V, u53(o.x, o.y), a.guide, a.guide_log2);
-    }
+    const int j = search_right(a.cdf, a.V, u53(o.x, o.y), a.guide, a.guide_log2);
     a.reg_idx[b] = j;
     const int r = a.B + b;
     a.x_idx[(int64_t)r * a.x_cap] = j;
     a.x_cnt[r] = 1;
     if (a.xt_bits) atomicOr(&a.xt_bits[(int64_t)j * XW + (r >> 5)], 1u << (r & 31));
+  }
+}
+
+// Owner-computes reg rows: thread t draws global slots t, t + NTO, ... (the one-process draw of
+// slot s), ownership bits are ballot-counted per wave, a block scan orders them by slot, and the
+// owned cards land as rows B + pos of x.  Slot s is handled by thread s % NTO in round s / NTO, so
+// the order "round-major, then thread" is slot order.
+constexpr int NTO = 1024;
+__global__ __launch_bounds__(NTO) void reg_rows_kernel(cc_noise_args a) {
+  __shared__ int wsum[NTO / 64];
+  __shared__ int base_s;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t step = (uint32_t)a.state[0];
+  const int XW = (a.xt_rows + 31) >> 5;
+  if (tid == 0) base_s = 0;
+  __syncthreads();
+  for (int s0 = 0; s0 < a.reg_slots; s0 += NTO) {
+    const int s = s0 + tid;
+    int j = -1;
+    if (s < a.reg_slots) {
+      const u32x4 o = rng(a.seed, step, (uint32_t)s, KIND_REG, 0, 0);
+      j = search_right(a.cdf, a.V, u53(o.x, o.y), a.guide, a.guide_log2);
+    }
+    const bool own = j >= a.reg_lo && j < a.reg_hi;
+    const uint64_t m = __ballot(own);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wv] = __popcll(m);
+    __syncthreads();
+    int off = base_s;
+    for (int w = 0; w < wv; ++w) off += wsum[w];
+    const int pos = off + before;
+    if (own) {
+      if (pos < a.reg_cap) {
+        const int r = a.B + pos;
+        a.reg_idx[pos] = j;
+        a.x_idx[(int64_t)r * a.x_cap] = j;
+        a.x_cnt[r] = 1;
+        if (a.xt_bits) atomicOr(&a.xt_bits[(int64_t)j * XW + (r >> 5)], 1u << (r & 31));
+      } else {
+        atomicOr(a.status, 2);
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int tot = 0;
+      for (int w = 0; w < NTO / 64; ++w) tot += wsum[w];
+      base_s += tot;
+    }
+    __syncthreads();
+  }
+  // padding rows: masked (no KL term, zero gradient)
+  for (int pos = base_s + tid; pos < a.reg_cap; pos += NTO) {
+    a.reg_idx[pos] = -1;
+    a.x_cnt[a.B + pos] = 0;
   }
 }
 
@@ -257,6 +297,8 @@ __global__ __launch_bounds__(NT) void adam_noise_kernel(cc_adam::Args ad, cc_noi
 }  // namespace
 
 static int noise_check(const cc_noise_args *a, size_t &lds) {
+  CC_REQUIRE(a != nullptr && a->xt_rows >= a->B + (a->with_reg ? a->B : 0),
+             "cc_noise_fwd: xt_rows must cover the rows that set xt bits");
   CC_REQUIRE(a != nullptr, "cc_noise_fwd: null args");
   CC_REQUIRE(a->V > 0 && a->B > 0 && a->x_cap > 0, "cc_noise_fwd: bad V/B/x_cap");
   CC_REQUIRE(a->cube_ptr && a->cube_idx && a->perm && a->cdf && a->neg_sampler && a->state,
@@ -275,6 +317,19 @@ extern "C" int cc_noise_fwd(const cc_noise_args *a, void *stream) {
   if (int rc = noise_check(a, lds)) return rc;
   hipLaunchKernelGGL(noise_kernel, dim3(a->B), dim3(NT), lds, as_stream(stream), *a);
   CC_LAUNCH_CHECK("noise_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_reg_rows(const cc_noise_args *a, void *stream) {
+  CC_REQUIRE(a != nullptr, "cc_reg_rows: null args");
+  CC_REQUIRE(a->V > 0 && a->B > 0 && a->x_cap > 0 && a->reg_slots > 0 && a->reg_cap > 0,
+             "cc_reg_rows: bad V/B/x_cap/reg_slots/reg_cap");
+  CC_REQUIRE(a->reg_lo >= 0 && a->reg_lo < a->reg_hi && a->reg_hi <= a->V, "cc_reg_rows: shard [lo, hi)");
+  CC_REQUIRE(a->cdf && a->state && a->x_cnt && a->x_idx && a->reg_idx && a->status,
+             "cc_reg_rows: null pointer");
+  CC_REQUIRE(!a->xt_bits || a->xt_rows >= a->B + a->reg_cap, "cc_reg_rows: xt_rows must cover B + reg_cap");
+  hipLaunchKernelGGL(reg_rows_kernel, dim3(1), dim3(NTO), 0, as_stream(stream), *a);
+  CC_LAUNCH_CHECK("reg_rows_kernel");
   return CC_OK;
 }
 

@@ -651,7 +651,7 @@ __device__ __forceinline__ bool dw_job(const TowerP &p, int bid, int &l, int &i,
       k0 = 32 * (bid / tn);
       n0 = 32 * (bid % tn);
       row0 = l < 6 ? 0 : p.B;
-      nrows = l < 3 ? p.R : p.B;
+      nrows = l < 3 ? p.R : (l < 6 ? p.B : p.R - p.B);   // reg branch: rows [B, R)
       return true;
     }
     bid -= nt;
@@ -984,7 +984,6 @@ extern "C" int cc_tower_bwd_dw_direct(const cc_tower_args *t, void *stream) {
   const int rmax = t->R > t->B ? t->R : t->B;
   const int rpw = ((rmax + 3) / 4 + 15) / 16 * 16;
   const size_t lds = std::max((size_t)4 * 2 * 32 * (rpw + 8) * 2, (size_t)(4 * 32 * 33 + 4 * 32) * 4);
-  CC_REQUIRE(lds <= 160 * 1024, "cc_tower_bwd_dw_direct: too many rows for one LDS stage");
   int jobs = 0;
   for (int l = 0; l < (t->R > t->B ? 9 : 6); ++l) {
     int K, N;
@@ -996,6 +995,7 @@ extern "C" int cc_tower_bwd_dw_direct(const cc_tower_args *t, void *stream) {
     CC_LAUNCH_CHECK("tower_dw_packed_kernel");
     return CC_OK;
   }
+  CC_REQUIRE(lds <= 160 * 1024, "cc_tower_bwd_dw_direct: too many rows for one LDS stage (use cc_tower_bwd_dw)");
   hipLaunchKernelGGL(tower_dw_tiled_kernel, dim3(jobs), dim3(DW_NT), lds, as_stream(stream), p, rpw);
   CC_LAUNCH_CHECK("tower_dw_tiled_kernel");
   return CC_OK;

@@ -2,12 +2,16 @@
 torch.distributed with backend "nccl" (= RCCL over xGMI on ROCm), gloo for CPU tests.
 
 Each rank takes its own B cubes of every global batch (disjoint slices of the shared epoch
-permutation: cubes perm[g*B*W + r*B : g*B*W + (r+1)*B]) and draws F and its B regulariser rows with
-Philox slots r*B..r*B+B-1, so the W ranks together process exactly the batch a single process with
-batch W*B would (tests/test_gpu_train.py::test_data_parallel_equivalence).  The only exchange is the
-all-reduce (average) of the fp32 gradient buffer before Adam; every rank then applies the same
-update, so weights stay replicated.  M~ is replicated (1.9 GB at |V|=22k fits every GPU); the
-row-sharded KL of §8(e) is a later-round optimisation."""
+permutation: cubes perm[g*B*W + r*B : g*B*W + (r+1)*B]) and draws F with Philox slots r*B..r*B+B-1,
+so the W ranks together process exactly the batch a single process with batch W*B would
+(tests/test_gpu_train.py::test_data_parallel_equivalence, tests/test_gpu_dp.py).  The exchange is
+the gradient reduction (zero.py: bucketed reduce-scatter, Adam on the rank's shard, all-gather of the
+parameters); every rank ends the step with the same weights.  With reg > 0 the regulariser is
+row-sharded over M~ (owner computes; trainer.reg_row_shards and DESIGN.md §5): each
+rank holds only its rows of M~ and computes the KL terms of the regulariser rows it owns.
+
+Backend: "nccl" (= RCCL over xGMI) with one GPU per rank; gloo on CPU, or when several ranks share
+one GPU (tests), or when CCREC_DIST_BACKEND says so."""
 import os
 
 import numpy as np
@@ -21,11 +25,13 @@ def init(backend=None):
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     cuda = torch.cuda.is_available()
-    dev = torch.device('cuda', local) if cuda else torch.device('cpu')
+    dev = torch.device('cuda', local % torch.cuda.device_count()) if cuda else torch.device('cpu')
     if cuda:
         torch.cuda.set_device(dev)
     if world > 1 and not torch.distributed.is_initialized():
-        backend = backend or ('nccl' if cuda else 'gloo')
+        backend = backend or os.environ.get('CCREC_DIST_BACKEND')
+        if backend is None:
+            backend = 'nccl' if cuda and torch.cuda.device_count() >= world else 'gloo'
         kw = {'device_id': dev} if backend == 'nccl' else {}
         torch.distributed.init_process_group(backend, **kw)
     return world, rank, dev

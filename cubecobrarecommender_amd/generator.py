@@ -3,7 +3,9 @@
 Same constructor and Sequence protocol (generator.py:6-15, 32-72):
     DataGenerator(adj_mtx, cubes, batch_size=64, shuffle=True, to_fit=True, noise=0.2, noise_std=0.1)
     len(gen) == C // batch_size           (generator.py:36, remainder dropped)
-    gen[i]                                -> the noised batch i of the current epoch
+    gen[i]                                -> [x_cubes, x_reg], [y_cubes, y_reg] (to_fit) or
+                                             [x_cubes, x_reg], dense float64 [B, V] like :58-61
+    gen.device_batch(i)                   -> the same batch kept in HBM (NoisedBatch)
     gen.on_epoch_end()                    -> reshuffle (generator.py:68-72)
 ``adj_mtx`` is M~ (train.py:69-71 applied), ``cubes`` a dense 0/1 [C, V] matrix (the reference's
 build_cubes output, utils.py:57-73), a list of card-index lists, or a CSR (indptr, indices).
@@ -67,7 +69,8 @@ class DataGenerator:
         self.seed = seed
         indptr, idx = _to_csr(cubes)
         self.N_cubes = len(indptr) - 1
-        self.N_cards = int(adj_mtx.shape[1]) if adj_mtx is not None else int(idx.max()) + 1
+        self.N_cards = (int(adj_mtx.shape[1]) if adj_mtx is not None else
+                        len(neg_sampler) if neg_sampler is not None else int(idx.max()) + 1)
         self.data = DeviceDataset(csr=(indptr, idx), num_cards=self.N_cards, y_mtx=adj_mtx,
                                   neg_sampler=neg_sampler, device=device)
         self.neg_sampler = self.data.neg_sampler_host          # generator.py:30
@@ -89,14 +92,33 @@ class DataGenerator:
         self.reset_indices()
 
     def epoch_permutations(self, epochs):
-        """The next `epochs` epoch orders (for a whole-fit, graph-replayable upload)."""
-        perms = [self.indices.copy()]
-        for _ in range(epochs - 1):
-            self.on_epoch_end()
+        """The next `epochs` epoch orders (for a whole-fit, graph-replayable upload).  Keras calls
+        on_epoch_end after every epoch, the last included, so a later fit() starts on a fresh order."""
+        perms = []
+        for _ in range(epochs):
             perms.append(self.indices.copy())
+            self.on_epoch_end()
         return np.stack(perms)
 
     def __getitem__(self, batch_number):
+        """generator.py:38-61: ``[x_cubes, x_reg], [y_cubes, y_reg]`` when to_fit, else
+        ``[x_cubes, x_reg]`` — dense float64 [B, V] numpy arrays (x_reg = one-hot rows of the reg
+        cards, y_reg = their M~ rows).  F runs on the GPU (cc_noise_fwd); use device_batch() to keep
+        the batch in HBM."""
+        nb = self.device_batch(batch_number)
+        B, V = len(nb.y_bits), self.N_cards
+        x_cubes = nb.x_dense()
+        reg = nb.reg_idx.cpu().numpy() if self.data.y_reg is not None else None
+        x_reg = np.zeros((B, V))
+        if reg is not None:
+            x_reg[np.arange(B), reg] = 1.0
+        if not self.to_fit:
+            return [x_cubes, x_reg]
+        y_reg = (nb.y_reg.cpu().numpy().astype(np.float64) if nb.y_reg is not None
+                 else np.zeros((B, V)))
+        return [x_cubes, x_reg], [nb.y_dense(), y_reg]
+
+    def device_batch(self, batch_number):
         """Run F (cc_noise_fwd) for batch `batch_number` of the current epoch; device-resident."""
         from .trainer import TrainConfig, Trainer
         if self._trainer is None:

@@ -75,7 +75,10 @@ class _Decoder:
 
 
 class CC_Recommender:
-    def __init__(self, num_cards, d=512, dtype='bf16', seed=0, params_flat=None):
+    def __init__(self, num_cards, d=512, dtype='fp32', seed=0, params_flat=None):
+        """dtype: GEMM operand precision of fit().  'fp32' (default) is the reference's precision
+        (TF float32, model.py); 'bf16' (bf16 MFMA operands, fp32 master weights / Adam / losses) and
+        'fp8' (+ MX-FP8 decoder output GEMMs) are opt-in."""
         self.N = int(num_cards)
         self.d = int(d)
         self.dtype = dtype
@@ -105,6 +108,10 @@ class CC_Recommender:
         self.lr = float(learning_rate)
 
     def fit(self, generator, epochs=1, verbose=1, rank=0, world=1, graphs=True, log=print):
+        """Keras ``fit(generator, epochs)`` (train.py:99-102).  The optimizer state persists across
+        calls like Keras' (optimizer.iterations and the m/v slots): a second fit() resumes Adam's
+        step count and moments, and the device step counter keeps the Philox noise draws fresh.
+        The logged loss is the epoch mean over its batches, as Keras' progress bar reports it."""
         from .trainer import TrainConfig, Trainer
         cfg = TrainConfig(V=self.N, d=self.d, batch_size=generator.batch_size, reg=self.reg,
                           noise=generator.noise, noise_std=generator.noise_std, lr=self.lr,
@@ -118,13 +125,21 @@ class CC_Recommender:
         steps = tr.batches_per_epoch
         if graphs:
             tr.capture()
+        loss_sum = torch.zeros(2, dtype=torch.float64, device=tr.loss_dev.device)
         for ep in range(epochs):
             t0 = time.perf_counter()
-            acc = 0.0
+            loss_sum.zero_()
             for _ in range(steps):
                 tr.step()          # data-parallel: bucketed reduce-scatter + sharded Adam (zero.py)
+                loss_sum += tr.loss_dev
             torch.cuda.synchronize()
-            l = tr.losses()
+            tr.check_status()
+            l = tr.losses(loss_sum / steps)
+            if world > 1:         # mean over ranks (each rank's loss is the mean over its cubes)
+                t = torch.tensor([l['bce'], l['kl']], dtype=torch.float64, device=tr.loss_dev.device)
+                torch.distributed.all_reduce(t)
+                l = {'bce': float(t[0]) / world, 'kl': float(t[1]) / world}
+                l['loss'] = l['bce'] + self.reg * l['kl']
             self.history.append(l)
             if verbose and rank == 0:
                 dt = time.perf_counter() - t0
@@ -132,20 +147,21 @@ class CC_Recommender:
                     f'- bce: {l["bce"]:.6f} - kl: {l["kl"]:.6f} - {steps * cfg.batch_size * world / dt:.0f} cubes/s')
 
         tr.flush()
+        if getattr(tr, 'sharded', None) is not None:   # data parallel: m, v are sharded — gather
+            tr.sharded.gather_state()                   # them here, on every rank (collective)
+        self._m = tr.standard(tr.m)
+        self._v = tr.standard(tr.v)
         self.trainer = tr
         self._recommender = None
         self._step = int(tr.state[0].item())
         return self
 
     def save(self, dest, save_format='tf'):
+        """model.save(dest, save_format='tf') (train.py:112-115).  No collectives: fit() already
+        gathered the optimizer state, so a data-parallel run may save from rank 0 alone."""
         lay = self.layout
         P = lay.unpack(self._current_flat())
-        if self.trainer is not None:
-            if getattr(self.trainer, 'sharded', None) is not None:   # data parallel: m, v sharded
-                self.trainer.sharded.gather_state()
-            m = lay.unpack(self.trainer.standard(self.trainer.m))
-            v = lay.unpack(self.trainer.standard(self.trainer.v))
-        elif self._m is not None:
+        if self._m is not None:
             m, v = lay.unpack(self._m), lay.unpack(self._v)
         else:
             m = v = None
@@ -167,7 +183,7 @@ class CC_Recommender:
         return self._rec()
 
 
-def load_model(path, dtype='bf16'):
+def load_model(path, dtype='fp32'):
     """keras.models.load_model('ml_files/<name>') (ml_recommend.py:54, ml_recommend_web.py:37)."""
     V, d, params, m, v, step = checkpoint.load_variables(path)
     lay = Layout(V, d)

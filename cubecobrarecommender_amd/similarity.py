@@ -19,17 +19,31 @@ def card_embeddings(model):
     return emb
 
 
+SIM_NMAX = 4096   # cc_similar_cards' in-LDS selection limit (csrc/similarity.hip)
+
+
 def similar(emb, idx, N):
     """(indices [N] int64, dists [N] float32) of the N cards closest to card idx (idx itself first
-    unless another card ties at -1)."""
+    unless another card ties at -1).  N <= 0 gives empty arrays (the reference's loop prints
+    nothing); N is capped at V.  Up to SIM_NMAX the selection runs in cc_similar_cards' one-workgroup
+    radix select; beyond it the same kernel's distance vector is fully sorted on the device
+    (stable, ties -> lower index, as numpy's argsort(kind='stable'))."""
     emb = emb.contiguous()
     V, K = emb.shape
+    N = min(int(N), V)
+    if N <= 0:
+        return np.zeros(0, np.int64), np.zeros(0, np.float32)
     dev = emb.device
     ws = torch.empty(int(L.lib().cc_similar_ws_size(V)) // 8 + 1, device=dev, dtype=torch.int64)
-    out_idx = torch.empty(N, device=dev, dtype=torch.int32)
-    out_d = torch.empty(N, device=dev, dtype=torch.float32)
-    L.call('cc_similar_cards', L.ptr(emb), V, K, int(idx), int(N), L.ptr(out_idx), L.ptr(out_d), None,
-           L.ptr(ws), L.stream_ptr())
+    n_sel = min(N, SIM_NMAX)
+    out_idx = torch.empty(n_sel, device=dev, dtype=torch.int32)
+    out_d = torch.empty(n_sel, device=dev, dtype=torch.float32)
+    dist_all = torch.empty(V, device=dev, dtype=torch.float32)
+    L.call('cc_similar_cards', L.ptr(emb), V, K, int(idx), n_sel, L.ptr(out_idx), L.ptr(out_d),
+           L.ptr(dist_all), L.ptr(ws), L.stream_ptr())
+    if N > SIM_NMAX:
+        order = torch.sort(dist_all, stable=True).indices[:N]
+        out_idx, out_d = order, dist_all[order]
     torch.cuda.current_stream().synchronize()
     return out_idx.cpu().numpy().astype(np.int64), out_d.cpu().numpy()
 

@@ -39,15 +39,19 @@ class TrainConfig:
     fused_tower: bool = True       # tower.hip row-block kernels (else per-layer cc_gemm launches)
     prefetch_noise: bool = True    # one process: F of step k+1 rides in step k's Adam launch
     reg_shard: bool = False        # data parallel + reg: M~ row-sharded, owner computes
+    reg_mode: str = 'sampled'      # 'sampled': B reg rows per step drawn ∝ neg_sampler (generator.py:47-51);
+    #                                'full': all |V| identity rows every step, KL(M~, D2(E(I))) as the
+    #                                reference README states the objective (README.md:27)
 
 
 def reg_row_shards(cdf, world):
-    """Row shards of M~ for the regulariser (owner computes): boundaries b[0..world]
-    at equal cumulative neg_sampler mass — shard r = cards whose CDF value lies in
+    """Row shards of M~ for the sampled regulariser (owner computes): boundaries
+    b[0..world] at equal cumulative neg_sampler mass — shard r = cards whose CDF value lies in
     (r/world, (r+1)/world] — and each shard's mass m_r = cdf[b_{r+1}-1] - cdf[b_r-1].  Rank r holds
-    rows [b_r, b_{r+1}) of M~ only and draws its B reg rows from neg_sampler conditioned on them
-    (csrc/noise.hip shard_u); weighting its KL by world * m_r makes the averaged gradient the
-    stratified estimate of the same expectation the one-process step samples."""
+    rows [b_r, b_{r+1}) of M~ only; every rank draws the step's world*B global reg rows (the same
+    draws one process of batch world*B makes) and computes the KL terms of the rows it owns
+    (cc_reg_rows), so the summed gradient is exactly the one-process gradient; equal mass balances
+    the expected rows per rank."""
     cdf = np.asarray(cdf, np.float64)
     V = len(cdf)
     b = np.searchsorted(cdf, np.arange(world + 1) / float(world), side='right')
@@ -62,13 +66,31 @@ def reg_row_shards(cdf, world):
     return b.astype(np.int64), mass
 
 
+def owner_capacity(mass, B, world, align=32, sigmas=6.0):
+    """Reg rows each rank reserves under owner computes: the world*B global draws land in shard r
+    Binomial(world*B, m_r) times; capacity = max over ranks of mean + 6 sigma (+1), rounded up to
+    `align` (an overflow sets the device status bit 2 and Trainer.check_status raises)."""
+    n = world * B
+    m = np.asarray(mass, np.float64)
+    need = np.max(n * m + sigmas * np.sqrt(n * m * (1.0 - m)) + 1.0)
+    return int(min(n, int(np.ceil(need / align)) * align))
+
+
+def full_rows(V, world, rank):
+    """Full mode: rank r owns identity rows [r*ceil(V/W), (r+1)*ceil(V/W)) ∩ [0, V)."""
+    per = -(-V // world)
+    return min(V, rank * per), min(V, (rank + 1) * per)
+
+
 def _cdf(neg_sampler):
     cdf = np.cumsum(np.asarray(neg_sampler, np.float64))
     return cdf / cdf[-1]
 
 
-def reg_rows_for(neg_sampler, world, rank):
-    """Rank's M~ row shard [lo, hi) (reg_row_shards on the dataset's CDF)."""
+def reg_rows_for(neg_sampler, world, rank, reg_mode='sampled'):
+    """Rank's M~ row shard [lo, hi): equal neg_sampler mass (sampled) or equal rows (full)."""
+    if reg_mode == 'full':
+        return full_rows(len(neg_sampler), world, rank)
     b, _ = reg_row_shards(_cdf(neg_sampler), world)
     return int(b[rank]), int(b[rank + 1])
 
@@ -148,13 +170,33 @@ class Trainer:
         self.use_reg = cfg.reg > 0
         if self.use_reg and data.y_reg is None:
             raise ValueError('reg > 0 needs the M~ matrix on the device')
-        self.R = 2 * B if self.use_reg else B
-        # regulariser rows: all of M~, or (data parallel, reg_shard) this rank's row shard
-        self.reg_rows, self.reg_weight = (0, V), 1.0
-        if self.use_reg and cfg.reg_shard and cfg.world > 1:
-            bnd, mass = reg_row_shards(data.cdf_host, cfg.world)
+        if cfg.reg_mode not in ('sampled', 'full'):
+            raise ValueError(f"reg_mode {cfg.reg_mode!r}: 'sampled' or 'full'")
+        W = cfg.world
+        self.full_reg = self.use_reg and cfg.reg_mode == 'full'
+        self.owner = self.use_reg and not self.full_reg and cfg.reg_shard and W > 1
+        ralign = 128 if cfg.dtype == 'fp8' else 32
+        # regulariser rows of this rank: rows [B, B + Breg) of every row-indexed buffer.
+        #   sampled: B draws per step (slot b of cube b), dz weight reg/B;
+        #   owner (data parallel, M~ row-sharded): the world*B global draws that fall in this
+        #     rank's shard, padded to a static capacity, masked rows reg_idx = -1; weight reg/B
+        #     (the zero.py average over ranks makes it reg/(world*B) per global row);
+        #   full: identity rows [lo, hi) (all of V on one GPU), weight reg*world/V.
+        self.reg_rows = (0, V)
+        self.Breg = B if self.use_reg else 0
+        self.kl_row_scale, self.kl_loss_scale = cfg.reg / B, 1.0 / B
+        if self.full_reg:
+            self.reg_rows = full_rows(V, W, cfg.rank)
+            n = self.reg_rows[1] - self.reg_rows[0]
+            self.Breg = -(-n // ralign) * ralign
+            self.kl_row_scale, self.kl_loss_scale = cfg.reg * W / V, W / V
+        elif self.owner:
+            bnd, mass = reg_row_shards(data.cdf_host, W)
             self.reg_rows = (int(bnd[cfg.rank]), int(bnd[cfg.rank + 1]))
-            self.reg_weight = float(cfg.world * mass[cfg.rank])
+            self.Breg = owner_capacity(mass, B, W, align=ralign)
+        self.R = B + self.Breg
+        self.xt_rows = B if self.full_reg else self.R      # rows of the MFMA W1-gradient product
+        self.reg_weight = 1.0
         if self.use_reg and data.reg_rows != self.reg_rows:
             if data.reg_rows != (0, V):
                 raise ValueError(f'dataset holds M~ rows {data.reg_rows}, rank needs {self.reg_rows}')
@@ -180,13 +222,13 @@ class Trainer:
         self.state = torch.zeros(4, device=self.dev, dtype=torch.int64)   # {step, batch, epoch, ticket}
         self.tickets = torch.zeros(4, device=self.dev, dtype=torch.int32)  # last-block hand-offs
         self.x_cap = max(1, data.max_n + int(data.max_n * 0.8) + 1)
-        R, VW, XW = self.R, (V + 31) // 32, (self.R + 31) // 32
+        R, VW, XW = self.R, (V + 31) // 32, (self.xt_rows + 31) // 32
         i32 = dict(device=self.dev, dtype=torch.int32)
         self.x_cnt = torch.zeros(R, **i32)
         self.x_idx = torch.zeros(R, self.x_cap, **i32)
         self.y_bits = torch.zeros(B, VW, **i32)
         self.xt_bits = torch.zeros(V, XW, **i32)
-        self.reg_idx = torch.zeros(B, **i32)
+        self.reg_idx = torch.zeros(max(self.Breg, 1), **i32)
         self.status = torch.zeros(1, **i32)
         T = dict(device=self.dev, dtype=self.tdt)
         self.H1 = torch.zeros(R, d, **T)
@@ -204,20 +246,26 @@ class Trainer:
         self.gH3 = torch.zeros(R, 128, **T)
         self.gH2 = torch.zeros(R, 256, **T)
         self.gPre1 = torch.zeros(R, d, **f32)
-        self.Z2 = torch.zeros(B, V, **f32) if self.use_reg else None
+        self.Z2 = torch.zeros(self.Breg, V, **f32) if self.use_reg else None
         self.splits = max(1, min(32, V // 512))            # decoder dX: K = V (32: 22.4 us vs 29.5 at 16)
+        # the regulariser branch's dX: M = Breg rows; with thousands of rows (full mode) the output
+        # tiles alone fill the chip — no split-K
+        self.splits_reg = self.splits if self.Breg <= 1024 else 1
         self.tsplits = max(1, min(8, B // 128))             # tower dW: K = rows (B or 2B)
-        self.split_buf = torch.zeros(max(self.splits * B * d, 2 * self.tsplits * max(d, 256) * 256), **f32)
+        self.split_buf = torch.zeros(max(self.splits * B * d, self.splits_reg * self.Breg * d,
+                                         2 * self.tsplits * max(d, 256) * 256), **f32)
         self.cs_buf = torch.zeros(2 * self.tsplits * max(d, 256), **f32)
         tiles = ((B + 63) // 64) * ((V + 63) // 64)
         self.bce_part = torch.zeros(tiles, device=self.dev, dtype=torch.float64)
-        self.kl_part = torch.zeros(B, device=self.dev, dtype=torch.float64)
+        self.kl_part = torch.zeros(max(self.Breg, 1), device=self.dev, dtype=torch.float64)
+        self.id_ws = (torch.zeros(int(L.lib().cc_embed_identity_ws(self.Breg, d)) // 4 + 1, **f32)
+                      if self.full_reg else None)
         self.loss_dev = torch.zeros(2, device=self.dev, dtype=torch.float64)
         # fused 32-row-block towers (tower.hip) when the widths fit; generic GEMMs otherwise
         self.fused_tower = cfg.fused_tower and (B % 32 == 0) and d <= (1024 if self.dtype == L.CC_BF16 else 256)
         # bf16 path: the W1 gradient on MFMA (cc_embed_grad_mfma) from dPre1^T bf16 [d][RP]
         # written by the tower backward chain (columns R..RP-1 stay zero)
-        self.embed_mfma = (self.dtype == L.CC_BF16 and self.fused_tower and d % 128 == 0 and R <= 1024
+        self.embed_mfma = (self.dtype == L.CC_BF16 and self.fused_tower and d % 128 == 0 and self.xt_rows <= 2048
                            and os.environ.get('CCREC_EMBED_MFMA', '1') != '0')
         self.RP = (R + 63) // 64 * 64
         # D1 output layer fused (logits + BCE + dZ + dWo, csrc/decout.hip) where its shape fits
@@ -254,7 +302,7 @@ class Trainer:
             self.slab = torch.zeros((R // 32) * slab, **f32)
             # decoder operands kept k-contiguous: D3^T (tower fwd), dZ^T (BCE epilogue), Wo^T shadow
             self.D3t = torch.zeros(d, R, **T)
-            self.dZt = torch.zeros(len(branches_of(self.use_reg)), V, B, **T)   # [branch][V][B]
+            self.dZt = [torch.zeros(V, n, **T) for n in self.branch_rows()]   # [branch][V][rows]
             self.WoT = torch.zeros(len(branches_of(self.use_reg)), V, d, **T)
             if self.mx8:   # MX-FP8 operand images of the decoder output layers (csrc/mx8.hip)
                 nbr, u8 = len(branches_of(self.use_reg)), dict(device=self.dev, dtype=torch.uint8)
@@ -269,12 +317,14 @@ class Trainer:
                 self.D3tqs = torch.zeros(d, R // 32, **u8)
                 self.dZq = torch.zeros(R, self.Vp, **u8)                  # dX A operand
                 self.dZqs = torch.zeros(R, self.Vp // 32, **u8)
-                self.dZtq = torch.zeros(nbr, V, B, **u8)                  # dW B operand (K = rows)
-                self.dZtqs = torch.zeros(nbr, V, B // 32, **u8)
+                self.dZtq = [torch.zeros(V, n, **u8) for n in self.branch_rows()]   # dW B operand (K = rows)
+                self.dZtqs = [torch.zeros(V, n // 32, **u8) for n in self.branch_rows()]
             self.targs = self._tower_args()
             self.transpose_tower()
         else:
             self.targs = None
+        if self.full_reg:
+            self._init_full_rows()
         # one process: Adam also writes the transposed operand copies and advances the step
         # counters (cc_adam_dense_t), so a step is two launches of graphs: fwd/bwd | Adam
         # (measured: in the step the fused kernel ran 77 us against 56 + 8 + 4 + 5 for Adam,
@@ -305,6 +355,39 @@ class Trainer:
         self.overlap = os.environ.get('CCREC_OVERLAP', '0') == '1'   # measured slower (graph branches), off
         self.timing = False          # bench.py: HIP events around the main kernels
         self.events = {}
+
+    def branch_rows(self):
+        """Rows of each decoder branch: B cubes, then Breg regulariser rows."""
+        return (self.cfg.batch_size, self.Breg) if self.use_reg else (self.cfg.batch_size,)
+
+    def branches(self):
+        """[(layer prefix, (r0, r1))] of the decoder branches in row order."""
+        B = self.cfg.batch_size
+        out = [('decoder', (0, B))]
+        if self.use_reg:
+            out.append(('decoder_for_reg', (B, B + self.Breg)))
+        return out
+
+    def _init_full_rows(self):
+        """Full mode: the regulariser rows are the static identity rows lo..hi-1 (x row = {card},
+        reg_idx = card); padding rows reg_idx -1, x_cnt 0.  Nothing redraws them per step."""
+        B, (lo, hi) = self.cfg.batch_size, self.reg_rows
+        n = hi - lo
+        ids = torch.full((self.Breg,), -1, dtype=torch.int32)
+        ids[:n] = torch.arange(lo, hi, dtype=torch.int32)
+        self.reg_idx.copy_(ids)
+        cnt = torch.zeros(self.Breg, dtype=torch.int32)
+        cnt[:n] = 1
+        self.x_cnt[B:].copy_(cnt)
+        self.x_idx[B:, 0].copy_(ids.clamp(min=0))
+
+    def check_status(self):
+        """Raise on device-side error flags (bit 1: a noised cube overflowed x_cap; bit 2: more
+        owned regulariser draws than the owner-computes capacity)."""
+        st = int(self.status.item())
+        if st:
+            raise RuntimeError(f'device status {st}: ' + ('x_cap overflow ' if st & 1 else '') +
+                               ('owner-computes reg capacity overflow' if st & 2 else ''))
 
     def _tick(self, name, stream=None):
         """Record a HIP event on the launching stream (bench timing); returns a closer."""
@@ -461,7 +544,8 @@ class Trainer:
 
     def _noise_args(self):
         cfg, V, B = self.cfg, self.cfg.V, self.cfg.batch_size
-        return L.NoiseArgs(V=V, B=B, x_cap=self.x_cap, with_reg=int(self.use_reg), seed=cfg.seed,
+        return L.NoiseArgs(V=V, B=B, x_cap=self.x_cap, with_reg=int(self.use_reg and not (self.owner or self.full_reg)),
+                           seed=cfg.seed,
                            slot_base=cfg.rank * B, batch_stride=B * cfg.world, batch_offset=cfg.rank * B,
                            noise_mean=cfg.noise, noise_std=cfg.noise_std,
                            cube_ptr=self.data.cube_ptr.data_ptr(), cube_idx=self.data.cube_idx.data_ptr(),
@@ -472,8 +556,8 @@ class Trainer:
                            x_cnt=self.x_cnt.data_ptr(), x_idx=self.x_idx.data_ptr(),
                            y_bits=self.y_bits.data_ptr(), xt_bits=self.xt_bits.data_ptr(),
                            reg_idx=self.reg_idx.data_ptr(), status=self.status.data_ptr(),
-                           reg_lo=self.reg_rows[0],
-                           reg_hi=self.reg_rows[1] if self.reg_rows != (0, V) else 0)
+                           xt_rows=self.xt_rows, reg_slots=B * cfg.world, reg_lo=self.reg_rows[0],
+                           reg_hi=self.reg_rows[1], reg_cap=self.Breg)
 
     def _gemm(self, M, N, K, A, lda, B, ldb, ta=0, tb=0, epi=L.CC_EPI_STORE, ldc=None, bias=None,
               relu=0, C=None, Cf=None, H=None, y_bits=None, scale=0.0, partials=None, splits=1,
@@ -538,6 +622,8 @@ class Trainer:
             t = self._tick('cc_noise_fwd')
             L.call('cc_noise_fwd', L.C.byref(na), s)
             t()
+        if self.owner:             # the rank's owned rows of the step's global reg draws
+            L.call('cc_reg_rows', L.C.byref(self._noise_args()), s)
         # ---- E (model.py:35-42) on R rows: gather + 3 Dense
         t = self._tick('cc_embed_gather_fwd')
         wf = self.wpack[0] if self.wpack is not None else None   # warm the tower forward's weights
@@ -548,7 +634,8 @@ class Trainer:
                L.ptr(self.state) if self._adv_deferred else None, self.batches_per_epoch, s)
         self._adv_deferred = False
         t()
-        branches = [('decoder', (0, B))] + ([('decoder_for_reg', (B, 2 * B))] if self.use_reg else [])
+        branches = self.branches()
+        Br = self.Breg
         if self.fused_tower:
             t = self._tick('cc_tower_fwd')
             L.call('cc_tower_fwd', L.C.byref(self.targs), s)
@@ -593,46 +680,48 @@ class Trainer:
         # ---- D2 output + softmax + KL vs M~ rows (model.py:98; train.py:85)
         if self.use_reg:
             if self.fused_tower:
-                self._gemm(B, V, d, **self._dec_fwd(1, B), tb=1,
+                self._gemm(Br, V, d, **self._dec_fwd(1, B), tb=1,
                            bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2))
             else:
-                self._gemm(B, V, d, L.ptr(self.D3[B:]), d, self.w('decoder_for_reg/reconstruct/kernel'), V,
+                self._gemm(Br, V, d, L.ptr(self.D3[B:]), d, self.w('decoder_for_reg/reconstruct/kernel'), V,
                            bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2))
             t = self._tick('dec_softmax_kl')
             # M~ row shard [lo, hi): the kernel indexes y_reg[reg_idx * V], so pass the base of
-            # row 0 (reg_idx lies in [lo, hi) by construction of the draw)
+            # row 0 (reg_idx lies in [lo, hi) or is -1 for a masked padding row)
             y_base = L.C.c_void_p(self.data.y_reg.data_ptr() - self.reg_rows[0] * V * 4)
-            L.call('cc_dec_softmax_kl_fused', self.dtype, L.ptr(self.Z2), B, V, y_base,
-                   L.ptr(self.reg_idx), float(cfg.reg * self.reg_weight), L.ptr(self.dZout[B:]),
+            L.call('cc_dec_softmax_kl_fused', self.dtype, L.ptr(self.Z2), Br, V, y_base,
+                   L.ptr(self.reg_idx), float(self.kl_row_scale), L.ptr(self.dZout[B:]),
                    L.ptr(self.kl_part), s)
             t()
-            if self.fused_tower:   # dZ2^T [V][B]: the k-contiguous operand of the reg branch's dW
-                L.call('cc_transpose', self.dtype, L.ptr(self.dZout[B:]), B, V, L.ptr(self.dZt[1]), s)
+            if self.fused_tower:   # dZ2^T [V][Breg]: the k-contiguous operand of the reg branch's dW
+                L.call('cc_transpose', self.dtype, L.ptr(self.dZout[B:]), Br, V, L.ptr(self.dZt[1]), s)
             ss = self._fork()
-            L.call('cc_reduce_loss', L.ptr(self.kl_part), B, self.reg_weight / B, L.ptr(self.loss_dev[1:]), ss)
+            L.call('cc_reduce_loss', L.ptr(self.kl_part), Br, self.kl_loss_scale, L.ptr(self.loss_dev[1:]), ss)
         # ---- backward through the output layers and decoder towers.  The output layers' dW
         # (side stream) and dX -> towers (this stream) only share read-only inputs.
         for k, (pre, (r0, r1)) in enumerate(branches):
             dz = self.dZout[r0:]
+            nr = r1 - r0
+            splits = self.splits if k == 0 else self.splits_reg
             if self.fused_tower:
                 if self.mx8:   # MX-FP8 dZ (dX A, K = V) and dZ^T (dW B, K = rows) + the bias grad
-                    L.call('cc_quant_mx8', L.CC_BF16, L.ptr(dz), B, V, V, 0, L.ptr(self.dZq[r0:]), self.Vp,
+                    L.call('cc_quant_mx8', L.CC_BF16, L.ptr(dz), nr, V, V, 0, L.ptr(self.dZq[r0:]), self.Vp,
                            L.ptr(self.dZqs[r0:]), None, s)
-                    L.call('cc_quant_mx8', L.CC_BF16, L.ptr(self.dZt[k]), V, B, B, 0, L.ptr(self.dZtq[k]), B,
+                    L.call('cc_quant_mx8', L.CC_BF16, L.ptr(self.dZt[k]), V, nr, nr, 0, L.ptr(self.dZtq[k]), nr,
                            L.ptr(self.dZtqs[k]), self.gp(pre + '/reconstruct/bias'), s)
-                gx = self._gemm(B, d, self.Vp if self.mx8 else V, **self._dec_dx(k, r0, pre), ta=0, tb=1,
-                                epi=L.CC_EPI_SPLITK, Cf=L.ptr(self.split_buf), splits=self.splits,
+                gx = self._gemm(nr, d, self.Vp if self.mx8 else V, **self._dec_dx(k, r0, pre), ta=0, tb=1,
+                                epi=L.CC_EPI_SPLITK, Cf=L.ptr(self.split_buf), splits=splits,
                                 launch=False)
                 if k == 0 and self.fused_out:   # dWo/dbo came out of cc_dec_bce_dw: dX only
                     t = self._tick('dec_dX')
                     L.call('cc_gemm', L.C.byref(gx), s)
                     t()
                     wb = self.wpack[1] if self.wpack is not None else None   # warm the tower bwd's weights
-                    L.call('cc_splitk_reduce_warm', self.dtype, L.ptr(self.split_buf), self.splits, B, d,
+                    L.call('cc_splitk_reduce_warm', self.dtype, L.ptr(self.split_buf), splits, nr, d,
                            L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None,
                            L.ptr(wb) if wb is not None else None, 2 * wb.numel() if wb is not None else 0, s)
                     continue
-                gw = self._gemm(d, V, B, **self._dec_dw(k, r0), ta=0, tb=1,
+                gw = self._gemm(d, V, nr, **self._dec_dw(k, r0), ta=0, tb=1,
                                 Cf=self.gp(pre + '/reconstruct/kernel'),
                                 colsum=None if self.mx8 else self.gp(pre + '/reconstruct/bias'), launch=False)
                 if not self.timing and not self.overlap:   # dX (split-K) and dW in one grouped launch
@@ -644,19 +733,19 @@ class Trainer:
                     t = self._tick('dec_dX')
                     L.call('cc_gemm', L.C.byref(gx), s)
                     t()
-                L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), self.splits, B, d,
+                L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), splits, nr, d,
                        L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
                 continue
             t = self._tick('dec_dW', self.side if self.overlap else None)
-            self._gemm(d, V, B, L.ptr(self.D3[r0:]), d, L.ptr(dz), V, ta=1, tb=0,
+            self._gemm(d, V, nr, L.ptr(self.D3[r0:]), d, L.ptr(dz), V, ta=1, tb=0,
                        Cf=self.gp(pre + '/reconstruct/kernel'), colsum=self.gp(pre + '/reconstruct/bias'),
                        stream=ss)
             t()
             t = self._tick('dec_dX')
-            self._gemm(B, d, V, L.ptr(dz), V, self.w(pre + '/reconstruct/kernel'), V, ta=0, tb=1,
-                       epi=L.CC_EPI_SPLITK, Cf=L.ptr(self.split_buf), splits=self.splits)
+            self._gemm(nr, d, V, L.ptr(dz), V, self.w(pre + '/reconstruct/kernel'), V, ta=0, tb=1,
+                       epi=L.CC_EPI_SPLITK, Cf=L.ptr(self.split_buf), splits=splits)
             t()
-            L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), self.splits, B, d,
+            L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), splits, nr, d,
                    L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
             rows = (r0, r1)
             self._dense_bwd(self.D2, self.gD3, rows, 256, d, pre + '/decoded_3', gIn=self.gD2, mask=self.D2)
@@ -681,11 +770,11 @@ class Trainer:
         return dict(A=L.ptr(self.dZout[r0:]), lda=V, B=self.w(pre + '/reconstruct/kernel'), ldb=V)
 
     def _dec_dw(self, k, r0):
-        R, B = self.R, self.cfg.batch_size
+        R, nr = self.R, self.branch_rows()[k]
         if self.mx8:
-            return dict(A=L.ptr(self.D3tq[:, r0:]), lda=R, B=L.ptr(self.dZtq[k]), ldb=B, dtype=L.CC_MX8,
+            return dict(A=L.ptr(self.D3tq[:, r0:]), lda=R, B=L.ptr(self.dZtq[k]), ldb=nr, dtype=L.CC_MX8,
                         a_scale=L.ptr(self.D3tqs[:, r0 // 32:]), b_scale=L.ptr(self.dZtqs[k]))
-        return dict(A=L.ptr(self.D3t[:, r0:]), lda=R, B=L.ptr(self.dZt[k]), ldb=B)
+        return dict(A=L.ptr(self.D3t[:, r0:]), lda=R, B=L.ptr(self.dZt[k]), ldb=nr)
 
     def forward_backward_b(self, stream=None):
         """Towers backward (both branches' rows together through the shared encoder) and the E1
@@ -698,7 +787,9 @@ class Trainer:
             L.call('cc_tower_bwd_chain', L.C.byref(self.targs), s)
             t()
             ss = self._fork()      # per-block dW slabs + their reduce overlap the E1 scatter
-            if self.dtype == L.CC_BF16 and os.environ.get('CCREC_TOWER_DW_DIRECT', '1') != '0':
+            # direct dW: from the packed images (any row count) or LDS-staged (rows <= ~1184)
+            direct = self.hpt is not None or max(R, cfg.batch_size) <= 1184
+            if self.dtype == L.CC_BF16 and direct and os.environ.get('CCREC_TOWER_DW_DIRECT', '1') != '0':
                 L.call('cc_tower_bwd_dw_direct', L.C.byref(self.targs), ss)
             else:
                 L.call('cc_tower_bwd_dw', L.C.byref(self.targs), ss)
@@ -708,15 +799,21 @@ class Trainer:
             self._dense_bwd(self.H2, self.gH3, (0, R), 256, 128, 'encoder/encoded_3', gIn=self.gH2, mask=self.H2)
             self._dense_bwd(self.H1, self.gH2, (0, R), d, 256, 'encoder/encoded_2', gIn_f32=self.gPre1, mask=self.H1)
         t = self._tick('cc_embed_scatter_bwd')
+        XR = self.xt_rows          # rows in the bitmask product (full mode: the cubes only)
         if self.gpre1p is not None:
-            L.call('cc_embed_grad_packed', L.ptr(self.gpre1p), V, d, R, self.RP, L.ptr(self.xt_bits),
+            L.call('cc_embed_grad_packed', L.ptr(self.gpre1p), V, d, XR, self.RP, L.ptr(self.xt_bits),
                    self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
         elif self.embed_mfma:
-            L.call('cc_embed_grad_mfma', L.ptr(self.gPre1T), V, d, R, self.RP, L.ptr(self.xt_bits),
+            L.call('cc_embed_grad_mfma', L.ptr(self.gPre1T), V, d, XR, self.RP, L.ptr(self.xt_bits),
                    self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
         else:
-            L.call('cc_embed_scatter_bwd', L.ptr(self.gPre1), V, d, R, L.ptr(self.xt_bits),
+            L.call('cc_embed_scatter_bwd', L.ptr(self.gPre1), V, d, XR, L.ptr(self.xt_bits),
                    self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
+        if self.full_reg:          # identity rows: dW1[lo + r] += dPre1[B + r]
+            B = cfg.batch_size
+            L.call('cc_embed_identity_add', self.dtype, L.ptr(self.gPre1[B:]),
+                   self.reg_rows[1] - self.reg_rows[0], d, self.reg_rows[0],
+                   self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), L.ptr(self.id_ws), s)
         t()
         if self.fused_tower:
             self._join()
@@ -905,8 +1002,9 @@ class Trainer:
         self.timing = timing
 
     # ------------------------------------------------------------------ inspection (tests)
-    def losses(self):
-        l = self.loss_dev.cpu().numpy()
+    def losses(self, loss_dev=None):
+        """{'bce', 'kl', 'loss'} of the last step (or of a given [2] device vector)."""
+        l = (self.loss_dev if loss_dev is None else loss_dev).cpu().numpy()
         bce, kl = float(l[0]), float(l[1]) if self.use_reg else 0.0
         return {'bce': bce, 'kl': kl, 'loss': bce + self.cfg.reg * kl}
 

@@ -72,7 +72,9 @@ typedef struct cc_noise_args {
   int32_t V;             /* cards */
   int32_t B;             /* cubes in this rank's batch */
   int32_t x_cap;         /* per-row capacity of x_idx (>= max cube size * 1.8) */
-  int32_t with_reg;      /* also draw B reg rows (rows B..2B-1 of x) */
+  int32_t with_reg;      /* 1: also draw one reg row per cube slot (rows B..2B-1 of x); 0: none
+                            here — cc_reg_rows (owner computes) or the static full-mode identity
+                            rows fill rows B.. of x */
   uint64_t seed;
   uint32_t slot_base;    /* rank * B: decorrelates ranks */
   int32_t batch_stride;  /* cubes consumed per global batch (B * world) */
@@ -89,18 +91,28 @@ typedef struct cc_noise_args {
                                                 searchsorted_right(cdf, g / 2^guide_log2) */
   int32_t guide_log2;                        /* 0 = no guide table (full binary search) */
   const int64_t *state;                      /* device {step, batch_in_epoch, epoch, 0} */
-  int32_t *x_cnt;                            /* [R] R = B (+B with reg) */
+  int32_t *x_cnt;                            /* [R] R = B (+ reg rows) */
   int32_t *x_idx;                            /* [R, x_cap] sorted card ids of x */
   uint32_t *y_bits;                          /* [B, ceil(V/32)] target bitmask */
   uint32_t *xt_bits;                         /* [V, ceil(R/32)] transposed x bits (zeroed) or NULL */
-  int32_t *reg_idx;                          /* [B] or NULL */
+  int32_t *reg_idx;                          /* [B] (with_reg), [reg_cap] (cc_reg_rows) or NULL */
   int32_t *status;                           /* [1] device error flags (0 = ok) */
-  int32_t reg_lo, reg_hi;                    /* M~ row shard [reg_lo, reg_hi) of this rank (SURVEY
-                                                8(e) owner computes): reg rows are drawn from
-                                                neg_sampler restricted to the shard (u mapped into
-                                                [cdf[lo-1], cdf[hi-1]) ); reg_hi == 0: all cards */
+  int32_t xt_rows;                           /* rows of the E1 gradient product: xt_bits is
+                                                [V, ceil(xt_rows/32)] (B, 2B, or B + reg_cap) */
+  /* cc_reg_rows only (data parallel, M~ row-sharded, owner computes — SURVEY 8(e)): */
+  int32_t reg_slots;                         /* global reg draws per step (B * world), slots 0.. */
+  int32_t reg_lo, reg_hi;                    /* this rank's M~ rows [reg_lo, reg_hi) */
+  int32_t reg_cap;                           /* reg rows of this rank: rows B..B+reg_cap-1 of x */
 } cc_noise_args;
 int cc_noise_fwd(const cc_noise_args *a, void *stream);
+/* Owner-computes regulariser rows: draws the reg_slots global reg rows of the step
+ * (slot s: the same Philox draw a one-process run of batch reg_slots makes for its slot s,
+ * generator.py:47-51), keeps those whose card lies in [reg_lo, reg_hi) in slot order as rows
+ * B, B+1, .. of x (x_cnt 1, reg_idx = card, xt bit set) and pads the rest of the reg_cap rows with
+ * x_cnt 0 and reg_idx -1 (masked: no KL term, no gradient).  More than reg_cap owned draws set
+ * status bit 2 (the surplus rows are dropped; reg_cap is sized ~6 sigma above the mean).
+ * One 1024-thread workgroup; reads the step from state like cc_noise_fwd. */
+int cc_reg_rows(const cc_noise_args *a, void *stream);
 /* cc_adam_dense(p, m, v, g, shadow, n, next->state, ...) and, in the same launch, cc_noise_fwd
  * for the step AFTER next->state (step + 1, batch advanced with epoch roll-over as
  * cc_state_advance(batches_per_epoch) would) — the batch buffers must be free (this step's
@@ -152,15 +164,24 @@ int cc_embed_scatter_bwd(const float *dpre, int32_t V, int32_t d, int32_t R,
                          const uint32_t *xt_bits, float *grad, float *bias_grad, void *stream);
 /* The same gradient on bf16 MFMA (the bf16/fp8 training path): dW1 = X^T dPre1 with the x^T
  * bitmask expanded to 0/1 bf16 A fragments in registers and dpre_t = dPre1^T bf16 [d][ld_t]
- * (ld_t % 64 == 0, columns R..ld_t-1 zero; cc_tower_args.gpre1t).  d % 128 == 0, R <= 1024.
+ * (ld_t % 64 == 0 is the row stride; rows 0..R-1 enter the product, columns R..ceil64(R)-1 zero;
+ * cc_tower_args.gpre1t).  d % 128 == 0, R <= 2048.
  * Consumes (zeroes) xt_bits like cc_embed_scatter_bwd; deterministic. */
 int cc_embed_grad_mfma(const void *dpre_t, int32_t V, int32_t d, int32_t R, int32_t ld_t,
                        uint32_t *xt_bits, float *grad, float *bias_grad, void *stream);
 /* cc_embed_grad_mfma with B = dPre1 as packed transposed fragments (cc_tower_args.gpre1p,
- * reduction length ld_t = ceil64(R)): each wave streams its 64 columns' fragments straight from
+ * reduction stride ld_t >= ceil64(R); the first R rows enter the product): each wave streams its 64 columns' fragments straight from
  * L2 (1 KB per wave load), no LDS staging or per-K-tile barriers.  d == 256. */
 int cc_embed_grad_packed(const void *dpre_p, int32_t V, int32_t d, int32_t R, int32_t ld_t,
                          uint32_t *xt_bits, float *grad, float *bias_grad, void *stream);
+/* Full-mode regulariser (all |V| one-hot identity rows, README.md:27 KL(M, D2(E(I)))): the rows'
+ * W1 gradient is dPre1 itself — grad[lo + r] += round(dpre[r]) for r < n and, with bias_grad,
+ * bias_grad += sum_r round(dpre[r]) in a fixed order; round = bf16 RNE for dtype CC_BF16 (the
+ * operand rounding of the MFMA path), none for CC_F32.  Run after the cube rows' E1 gradient.
+ * partial: cc_embed_identity_ws(n, d) bytes of scratch. */
+size_t cc_embed_identity_ws(int32_t n, int32_t d);
+int cc_embed_identity_add(int32_t dtype, const float *dpre, int32_t n, int32_t d, int32_t lo,
+                          float *grad, float *bias_grad, float *partial, void *stream);
 
 /* ----------------------------------------------------------------------------------
  * Generic MFMA GEMM with fused epilogues — the Dense layers of the E/D towers and the
@@ -333,9 +354,40 @@ int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const void *D3p,
                   float *gb, double *loss_partials, double *loss_out, double loss_scale,
                   uint32_t *ticket, void *stream);
 int32_t cc_dec_bce_dw_blocks(int32_t V);
+/* D2 softmax + KL on materialised fp32 logits Z2 [B][V] (model.py:98, train.py:85, TF 2.5 clip
+ * semantics): row b uses the M~ row y_reg + reg_idx[b] * V; dZ[b] = scale * ([p >= 1e-7](-t) +
+ * p * sum_{p>=1e-7} t) with scale = reg * (the row's weight in the objective, e.g. 1/B);
+ * kl_partials[b] = KL of row b.  reg_idx[b] < 0 marks a padding row: dZ[b] = 0, partial 0. */
 int cc_dec_softmax_kl_fused(int32_t dtype, const float *Z2, int32_t B, int32_t V,
-                            const float *y_reg, const int32_t *reg_idx, float reg, void *dZ,
+                            const float *y_reg, const int32_t *reg_idx, float scale, void *dZ,
                             double *kl_partials, void *stream);
+/* D2 output layer fused (decreg.hip): logits -> softmax -> KL vs M~ rows -> dZ -> dWo/dbo with
+ * no fp32 logits in HBM (model.py:64/98, train.py:85; TF 2.5 clip semantics).  Row r of the
+ * regulariser rows is row row0 + r of the packed D3 images D3p ([R/32][d/16][64][8], act6p) and
+ * D3tp ([d/32][ldt/16][64][8], act6tp); Wo [d][V] bf16 is read in place; Mt + card * V is the
+ * M~ row of card reg_idx[r] (-1: padding row, contributes nothing); tsum[card] =
+ * sum_j clip(M~[card, j], 1e-7, 1) (cc_kl_tsum), indexed like Mt.  Outputs: dZ [rows][V] bf16
+ * (= scale * ([p >= 1e-7](-t) + p * sum_{p>=1e-7} t), for the dX product), gW [d][V], gb [V],
+ * loss_partials (cc_dec_kl_blocks(V) doubles) and, with ticket, loss_out = sum * loss_scale.
+ * d in {128, 256}, rows % 32 == 0.  ws: cc_dec_kl_ws_size(rows, V) bytes, 16-B aligned. */
+typedef struct cc_dec_kl_args {
+  int32_t d, V, rows, ldt, row0;
+  const void *D3p, *D3tp, *Wo;
+  const float *bo, *Mt, *tsum;
+  const int32_t *reg_idx;
+  float scale;
+  void *dZ;
+  float *gW, *gb;
+  double *loss_partials, *loss_out;
+  double loss_scale;
+  uint32_t *ticket;
+  void *ws;
+} cc_dec_kl_args;
+size_t cc_dec_kl_ws_size(int32_t rows, int32_t V);
+int32_t cc_dec_kl_blocks(int32_t V);
+int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream);
+/* tsum[i] = sum_j clip(Mt[i * V + j], 1e-7, 1) for the n rows of Mt (once per M~) */
+int cc_kl_tsum(const float *Mt, int32_t n, int32_t V, float *tsum, void *stream);
 /* loss_out[0] = sum(partials[0:n]) * scale (fixed order, fp64) */
 int cc_reduce_loss(const double *partials, int32_t n, double scale, double *loss_out, void *stream);
 

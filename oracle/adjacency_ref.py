@@ -38,3 +38,30 @@ def normalise(adj_mtx):
     y = np.array(adj_mtx, dtype=np.float64, copy=True)
     np.fill_diagonal(y, 1)
     return y / y.sum(1)[:, None]
+
+
+def normalised_rows_from_lists(cube_lists, num_cards, rows):
+    """Rows ``rows`` of M~ (utils.py:75-91 then train.py:69-71) without forming the V x V matrix:
+    for each requested card i, counts[i, :] over the cubes containing i, M[i] = counts[i] / d_i
+    (all-zero when d_i = 0), diagonal := 1, divided by the row sum — the same float64 operations
+    as ``normalise(adjacency_from_lists(...))`` restricted to those rows."""
+    V = int(num_cards)
+    rows = np.asarray(rows, np.int64)
+    holders = {}
+    for c, lst in enumerate(cube_lists):
+        for j in np.unique(np.asarray(lst, np.int64)):
+            holders.setdefault(int(j), []).append(c)
+    out = np.zeros((len(rows), V))
+    cache = {}
+    for r, i in enumerate(rows):
+        i = int(i)
+        if i not in cache:
+            counts = np.zeros(V)
+            for c in holders.get(i, ()):
+                counts[np.unique(np.asarray(cube_lists[c], np.int64))] += 1.0
+            d = counts[i]
+            m = counts / d if d != 0 else counts
+            m[i] = 1.0
+            cache[i] = m / m.sum()
+        out[r] = cache[i]
+    return out

@@ -78,7 +78,9 @@ def train_forward_backward(P, x_lists, y_lists, V, d, reg=0.0, reg_idx=None, y_r
     """One Keras train_step's forward + backward (train.py:99-102 via model.py:117-125).
 
     x_lists / y_lists: per-cube sorted card lists of the noised input x and the target y.
-    reg_idx [B] and y_reg [B, V] (rows of M~) are used when reg > 0.
+    reg_idx [n] and y_reg [n, V] (rows of M~) are used when reg > 0: the regulariser rows, n = B
+    sampled rows (generator.py:47-51) or all |V| identity rows (full mode, README.md:27); the KL
+    is the mean over the n rows (Keras' batch mean), so its gradient carries reg / n.
     Returns (losses dict, grads dict keyed like P).
     """
     rq = _rq(mode)
@@ -86,7 +88,7 @@ def train_forward_backward(P, x_lists, y_lists, V, d, reg=0.0, reg_idx=None, y_r
     bdt = np.float32 if mode == 'fp32' else np.float64
     W = {k: (rq(v) if k.endswith('/kernel') else np.asarray(v, bdt)) for k, v in P.items()}
     use_reg = reg > 0
-    R = 2 * B if use_reg else B
+    nreg = len(reg_idx) if use_reg else 0
     Xs = _csr(list(x_lists) + ([[int(i)] for i in reg_idx] if use_reg else []), V).astype(bdt)
     # E1: sparse gather-sum of the (bf16 shadow) rows + bias, ReLU
     pre1 = Xs @ W['encoder/encoded_1/kernel'] + W['encoder/encoded_1/bias']
@@ -142,9 +144,9 @@ def train_forward_backward(P, x_lists, y_lists, V, d, reg=0.0, reg_idx=None, y_r
             loss = (T * np.log(T / q)).sum(axis=1).mean()
             g = np.where(p >= 1e-7, -T / q, 0.0)
             dz = p * (g - (p * g).sum(axis=1, keepdims=True))
-            return loss, dz * (reg / B)
+            return loss, dz * (reg / nreg)
 
-        losses['kl'] = decoder_branch('decoder_for_reg', np.arange(B, 2 * B), kl)
+        losses['kl'] = decoder_branch('decoder_for_reg', np.arange(B, B + nreg), kl)
     else:
         losses['kl'] = 0.0
     losses['loss'] = losses['bce'] + reg * losses['kl']

@@ -181,34 +181,37 @@ def philox_cube(includes, cdf, neg_sampler, seed, step, slot, mean=0.2, std=0.1)
     return np.nonzero(x)[0], np.nonzero(y)[0], k
 
 
-def philox_reg_indices(cdf, seed, step, slot_base, count, shard=None):
-    """generator.py:47-51 (B reg rows iid ∝ neg_sampler) on Philox.  ``shard=(lo, hi)``: the
-    row-sharded M~ of SURVEY §8(e) — the draw conditioned on cards [lo, hi): u is mapped into
-    [cdf[lo-1], cdf[hi-1]) (an upper-edge rounding folds back to the lower edge), as
-    csrc/noise.hip ``shard_u``."""
+def philox_reg_indices(cdf, seed, step, slot_base, count):
+    """generator.py:47-51 (B reg rows iid ∝ neg_sampler) on Philox: slot s draws
+    searchsorted_right(cdf, u53(Philox(seed; 0, REG<<24, s, step)))."""
     slots = np.uint32(slot_base) + np.arange(count, dtype=np.uint32)
     k0 = np.uint32(seed & 0xFFFFFFFF)
     k1 = np.uint32((seed >> 32) & 0xFFFFFFFF)
     o0, o1, _, _ = philox4x32(np.uint32(0), np.uint32(KIND_REG << 24), slots,
                               np.uint32(step & 0xFFFFFFFF), k0, k1)
     u = u53(o0, o1)
-    if shard is None:
-        return _searchsorted_right(cdf, u).astype(np.int64)
-    lo, hi = shard
-    ulo = float(cdf[lo - 1]) if lo > 0 else 0.0
-    uhi = float(cdf[hi - 1])
-    v = ulo + u * (uhi - ulo)
-    v = np.where(v < uhi, v, ulo)
-    return np.clip(_searchsorted_right(cdf, v), lo, hi - 1).astype(np.int64)
+    return _searchsorted_right(cdf, u).astype(np.int64)
+
+
+def owner_reg_rows(cdf, seed, step, slots, lo, hi, cap):
+    """SURVEY §8(e) owner computes (csrc/noise.hip cc_reg_rows): the step's `slots` global reg draws
+    (slot s exactly as a one-process run of batch `slots` draws it), the cards in [lo, hi) kept in
+    slot order, padded with -1 to `cap`.  Returns (reg_idx [cap], owned count, overflow flag)."""
+    j = philox_reg_indices(cdf, seed, step, 0, slots)
+    own = j[(j >= lo) & (j < hi)]
+    out = np.full(cap, -1, np.int64)
+    n = min(len(own), cap)
+    out[:n] = own[:n]
+    return out, len(own), len(own) > cap
 
 
 def philox_noise_batch(cube_lists, cdf, neg_sampler, seed, step, slot_base=0,
-                       mean=0.2, std=0.1, with_reg=True, shard=None):
+                       mean=0.2, std=0.1, with_reg=True):
     xs, ys, ks = [], [], []
     for b, inc in enumerate(cube_lists):
         x, y, k = philox_cube(inc, cdf, neg_sampler, seed, step, slot_base + b, mean, std)
         xs.append(x)
         ys.append(y)
         ks.append(k)
-    reg = philox_reg_indices(cdf, seed, step, slot_base, len(cube_lists), shard) if with_reg else None
+    reg = philox_reg_indices(cdf, seed, step, slot_base, len(cube_lists)) if with_reg else None
     return xs, ys, reg, np.array(ks)

@@ -27,6 +27,8 @@ def main(argv=None, print_fn=print):
     rows = similar_cards(model, name, a.N, int_to_card, card_to_int)
     for rank, card, dist in rows:
         print_fn(str(rank) + ':', card, dist)
+    if a.N > len(int_to_card):   # the reference's ranked[i] runs past the end (similarity.py:32-34)
+        raise IndexError(f'index {len(int_to_card)} is out of bounds for axis 0 with size {len(int_to_card)}')
     return rows
 
 

@@ -4,7 +4,7 @@
 Loads data/maps/nameToId.json + data/cube/*.json (train.py:40-51) and output/full_adj_mtx.npy
 (:55; computed on the GPU when absent), builds M~ (:69-71), trains CC_Recommender with Adam on
 BCE + reg*KL (:82-102) on the GPU and saves ml_files/<name>/ (:112-115).  Optional flags:
---d (E/D width, reference 512), --dtype bf16|fp32, --synthetic C V (no data/ needed),
+--d (E/D width, reference 512), --dtype fp32|bf16|fp8 (fp32 = the reference's precision), --synthetic C V (no data/ needed),
 data-parallel over all GPUs when launched with torch.distributed.run."""
 import argparse
 import os
@@ -25,7 +25,7 @@ def main(argv=None):
     ap.add_argument('noise', type=float)
     ap.add_argument('seed', nargs='?', type=int, default=0)
     ap.add_argument('--d', type=int, default=512)
-    ap.add_argument('--dtype', default='bf16')
+    ap.add_argument('--dtype', default='fp32')
     ap.add_argument('--synthetic', nargs=2, type=int, metavar=('C', 'V'))
     ap.add_argument('--data-dir', default='./data')
     ap.add_argument('--adj', default='./output/full_adj_mtx.npy')
@@ -44,17 +44,23 @@ def main(argv=None):
         V, name_lookup, card_to_int, _ = D.get_card_maps(os.path.join(a.data_dir, 'maps', 'nameToId.json'))
         indptr, idx = D.lists_to_csr(D.build_cube_lists(os.path.join(a.data_dir, 'cube'), name_lookup, card_to_int))
     print('Creating Graph for Regularization . . . \n')
+    from cubecobrarecommender_amd.synthetic import neg_sampler_from_csr
     if os.path.exists(a.adj) and not a.synthetic:
-        M = torch.from_numpy(np.load(a.adj)).to(dev, torch.float32)
+        M = torch.from_numpy(np.load(a.adj)).to(dev, torch.float64)
         M.fill_diagonal_(1.0)
-        y_mtx = M / M.sum(1, keepdim=True)                                  # train.py:69-71
+        M /= M.sum(1, keepdim=True)                  # train.py:69-71, in float64 like the reference
+        neg_sampler = (M.sum(0) / M.sum()).cpu().numpy()                    # generator.py:30
+        y_mtx = M.to(torch.float32)
+        del M
     else:
         y_mtx = adjacency.adjacency_normalised_gpu(indptr, idx, V, device=dev)
+        neg_sampler = neg_sampler_from_csr(indptr, idx, V)   # the float64 closed form of :30
     print('Setting Up Model . . . \n')
     model = CC_Recommender(V, d=a.d, dtype=a.dtype, seed=a.seed)
     model.compile(optimizer='adam', loss=['binary_crossentropy', 'kullback_leibler_divergence'],
                   loss_weights=[1.0, a.reg], metrics=['accuracy'])
-    gen = DataGenerator(y_mtx, (indptr, idx), batch_size=a.batch_size, noise=a.noise, seed=a.seed, device=dev)
+    gen = DataGenerator(y_mtx, (indptr, idx), batch_size=a.batch_size, noise=a.noise, seed=a.seed, device=dev,
+                        neg_sampler=neg_sampler)
     model.fit(gen, epochs=a.epochs, rank=rank, world=world)
     if rank == 0:
         model.save(os.path.join(a.out_dir, a.name), save_format='tf')

@@ -24,13 +24,56 @@ def test_datagenerator_batches_match_oracle():
     assert np.allclose(gen.neg_sampler, noise_ref.neg_sampler_of(Mt.astype(np.float32)), rtol=1e-6)
     cdf = noise_ref.cdf_of(gen.neg_sampler)
     for i in (0, 3):
-        batch = gen[i]
+        batch = gen.device_batch(i)
         cubes = [lists[c] for c in gen.indices[i * B:(i + 1) * B]]
         oxs, oys, oreg, _ = noise_ref.philox_noise_batch(cubes, cdf, gen.neg_sampler, 5, i)
         xl = batch.x_lists()
         assert all(np.array_equal(xl[b], oxs[b]) for b in range(B))
         assert np.array_equal(batch.reg_idx.cpu().numpy(), oreg)
         assert np.array_equal(batch.y_reg.cpu().numpy(), Mt.astype(np.float32)[oreg])
+
+
+def test_datagenerator_getitem_reference_format():
+    """gen[i] returns what generator.py:58-61 returns: [x_cubes, x_reg], [y_cubes, y_reg], dense
+    float64 [B, V]; to_fit=False gives [x_cubes, x_reg] only."""
+    V, C, B = 500, 64, 8
+    lists, Mt, ns = problem(9, C, V, (10, 30, 60))
+    gen = DataGenerator(Mt.astype(np.float32), lists, batch_size=B, noise=0.2, seed=3)
+    (x0, x1), (y0, y1) = gen[1]
+    nb = gen.device_batch(1)
+    for a in (x0, x1, y0, y1):
+        assert a.shape == (B, V) and a.dtype == np.float64
+    xl = nb.x_lists()
+    reg = nb.reg_idx.cpu().numpy()
+    for b in range(B):
+        assert np.array_equal(np.nonzero(x0[b])[0], xl[b])
+        assert np.array_equal(np.nonzero(x1[b])[0], [reg[b]])
+        assert np.array_equal(y1[b], Mt.astype(np.float32)[reg[b]].astype(np.float64))
+    assert set(np.unique(x0)) <= {0.0, 1.0} and set(np.unique(y0)) <= {0.0, 1.0}
+    gen.to_fit = False
+    X = gen[1]
+    assert len(X) == 2 and np.array_equal(X[0], x0)
+
+
+def test_fit_twice_resumes_optimizer():
+    """Two fit(epochs=1) calls == one fit(epochs=2): Adam's step count and moments and the noise
+    counters carry over (Keras keeps optimizer.iterations and the slots across fit calls)."""
+    V, d, C = 600, 64, 128
+    lists, Mt, ns = problem(13, C, V, (15, 40, 90))
+    runs = []
+    for split in (False, True):
+        gen = DataGenerator(Mt.astype(np.float32), lists, batch_size=32, noise=0.2, seed=4)
+        model = CC_Recommender(V, d=d, seed=2)
+        model.compile(loss_weights=[1.0, 0.1])
+        if split:
+            model.fit(gen, epochs=1, verbose=0)
+            model.fit(gen, epochs=1, verbose=0)
+        else:
+            model.fit(gen, epochs=2, verbose=0)
+        runs.append((model._current_flat(), model._m, model._step))
+    assert runs[0][2] == runs[1][2] == 2 * (C // 32)
+    np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(runs[1][1], runs[0][1], rtol=0, atol=1e-7)
 
 
 def test_fit_save_load_recommend(tmp_path):

@@ -1,0 +1,175 @@
+"""GPU parity at the shipped configurations ("check the shipped configuration"):
+
+* the bench's exact Trainer — |V| = 22,000, d = 256, B = 512, bf16, capture() and the steady-state
+  one-launch-per-step graph (Adam + next step's F + packed tower images), fused D1 output kernel
+  reading Wo — against oracle/model_ref.py (mode='bf16') for several steps, reg 0 and 0.1;
+* the reference architecture (|V| = 20,884 as the reference checkpoint, d = 512, fp32;
+  src/ml/model.py:27-33, 58-64) at the 1e-4 fp32 bar;
+* the GPU noise law F at |V| = 22,000 against the reference's own MT19937 law (oracle MTNoise,
+  pinned to generator.py's batches) — SURVEY §4's statistical tier.
+"""
+import numpy as np
+import pytest
+import torch
+
+from cubecobrarecommender_amd.layout import Layout, glorot_flat
+from cubecobrarecommender_amd.synthetic import neg_sampler_from_csr, synthetic_cubes
+from cubecobrarecommender_amd.trainer import DeviceDataset, TrainConfig, Trainer
+from oracle import adjacency_ref, model_ref, noise_ref
+from tests.gpu_helpers import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _csr_lists(indptr, indices):
+    return [indices[indptr[c]:indptr[c + 1]] for c in range(len(indptr) - 1)]
+
+
+def _check_step(tr, P, lists, perm, ns, step, reg, mode, loss_tol, gtol, y_rows):
+    V, d, B = tr.cfg.V, tr.cfg.d, tr.cfg.batch_size
+    cdf = noise_ref.cdf_of(ns)
+    cubes = [lists[c] for c in perm[step * B:(step + 1) * B]]
+    oxs, oys, oreg, _ = noise_ref.philox_noise_batch(cubes, cdf, ns, tr.cfg.seed, step)
+    y_reg = y_rows(oreg) if reg > 0 else None
+    losses, grads = model_ref.train_forward_backward(P, oxs, oys, V, d, reg=reg, reg_idx=oreg,
+                                                     y_reg=y_reg, mode=mode)
+    got = tr.losses()
+    assert abs(got['bce'] - losses['bce']) / losses['bce'] < loss_tol, (step, got, losses)
+    if reg > 0:
+        assert abs(got['kl'] - losses['kl']) / losses['kl'] < loss_tol, (step, got, losses)
+    g = tr.layout.unpack(tr.standard(tr.grads))
+    errs = {k: rel_err(g[k], grads[k]) for k in grads if reg or not k.startswith('decoder_for_reg')}
+    bad = {k: v for k, v in errs.items() if not v < gtol}
+    assert not bad, (step, bad)
+    return errs
+
+
+@pytest.mark.parametrize('reg', [0.0, 0.1])
+def test_bench_configuration_matches_oracle(reg):
+    """bench.py's Trainer, exactly: V=22000, d=256, B=512, bf16, glorot_flat(seed=42), seed 1234,
+    graphs captured; steps 0 (eager-queued graphs) and 1-2 (the one-graph steady state)."""
+    from cubecobrarecommender_amd.adjacency import adjacency_normalised_gpu
+    V, d, B, C = 22000, 256, 512, 8192
+    indptr_t, indices_t = synthetic_cubes(C, V, seed=20250301, device='cuda')
+    indptr, indices = np.asarray(indptr_t), np.asarray(indices_t)
+    ns = neg_sampler_from_csr(indptr, indices, V)
+    lists = _csr_lists(indptr, indices)
+    y_mtx = adjacency_normalised_gpu(indptr, indices, V, device='cuda') if reg > 0 else None
+    data = DeviceDataset(csr=(indptr, indices), num_cards=V, neg_sampler=ns, y_mtx=y_mtx, device='cuda')
+    cfg = TrainConfig(V=V, d=d, batch_size=B, reg=reg, dtype='bf16', seed=1234)
+    flat = glorot_flat(V, d, seed=42)
+    tr = Trainer(cfg, data, params_flat=flat)
+    assert tr.fused_out and tr.adam_packs and tr.prefetch and tr.wpack is not None
+    perm = np.random.default_rng(99).permutation(C).astype(np.int32)
+    tr.set_epoch_permutations(perm[None, :])
+    tr.capture()
+
+    def y_rows(idx):   # M~ rows: the device fp32 matrix (pinned bit-exact in test_gpu_adjacency),
+        got = y_mtx[torch.as_tensor(idx, device='cuda').long()].cpu().numpy()   # checked here
+        want = adjacency_ref.normalised_rows_from_lists(lists, V, idx)
+        assert np.max(np.abs(got - want) / np.maximum(want, 1e-30)) < 2e-7
+        return got
+    for step in range(3):
+        P = Layout(V, d).unpack(tr.standard(tr.params))
+        tr.step()
+        torch.cuda.synchronize()
+        _check_step(tr, P, lists, perm, ns, step, reg, 'bf16', 2e-4, 2e-2, y_rows)
+    assert tr.graphs is not None and tr.graphs[4] is not None
+
+
+@pytest.mark.parametrize('reg', [0.0, 0.1])
+def test_reference_architecture_fp32(reg):
+    """The reference model (d = 512, fp32 everywhere; model.py:27-33, 58-64) at the reference
+    checkpoint's |V| = 20,884: loss within 1e-4 relative and every gradient within 1e-4 L2 of the
+    float64 oracle, over two steps with Adam between them."""
+    from cubecobrarecommender_amd.adjacency import adjacency_normalised_gpu
+    V, d, B, C = 20884, 512, 64, 512
+    indptr_t, indices_t = synthetic_cubes(C, V, seed=5, device='cuda', sizes=(45, 90, 180),
+                                          probs=(0.3, 0.4, 0.3))
+    indptr, indices = np.asarray(indptr_t), np.asarray(indices_t)
+    ns = neg_sampler_from_csr(indptr, indices, V)
+    lists = _csr_lists(indptr, indices)
+    y_mtx = adjacency_normalised_gpu(indptr, indices, V, device='cuda') if reg > 0 else None
+    data = DeviceDataset(csr=(indptr, indices), num_cards=V, neg_sampler=ns, y_mtx=y_mtx, device='cuda')
+    P = model_ref.init_params(V, d, seed=8, bias_std=0.01)
+    lay = Layout(V, d)
+    tr = Trainer(TrainConfig(V=V, d=d, batch_size=B, reg=reg, dtype='fp32', seed=17), data,
+                 params_flat=lay.pack(P))
+    perm = np.random.default_rng(2).permutation(C).astype(np.int32)
+    tr.set_epoch_permutation(perm)
+    Mo = {k: np.zeros_like(v) for k, v in P.items()}
+    Vo = {k: np.zeros_like(v) for k, v in P.items()}
+
+    def y_rows(idx):
+        return adjacency_ref.normalised_rows_from_lists(lists, V, idx)
+    for step in range(2):
+        tr.forward_backward()
+        torch.cuda.synchronize()
+        _check_step(tr, P, lists, perm, ns, step, reg, 'fp64', 1e-4, 1e-4, y_rows)
+        # advance both on the GPU's gradients with TF Adam; the GPU update must equal the formula
+        G = lay.unpack(tr.standard(tr.grads))
+        tr.apply()
+        torch.cuda.synchronize()
+        P, Mo, Vo = model_ref.adam_tf(P, Mo, Vo, G, t=step + 1)
+        got = lay.unpack(tr.standard(tr.params))
+        n = lay.total if reg else lay.main_total
+        assert np.max(np.abs(lay.pack(got)[:n] - lay.pack(P)[:n])) < 1e-6
+
+
+def test_noise_law_matches_reference_at_22k():
+    """F on the GPU (Philox law) vs the reference's MT19937 law (oracle MTNoise, bit-exact with
+    generator.py) at |V| = 22,000 on the same 1,024 synthetic cubes: distinct cut / add / ycut counts
+    per cube (two-sample KS), the ycut <= k//4 and add-outside-cube structure, and the added-card
+    frequencies of the 30 most likely cards (chi-square), all at alpha = 1e-4."""
+    from scipy import stats
+    from cubecobrarecommender_amd.generator import DataGenerator
+    V, C, B = 22000, 1024, 512
+    indptr_t, indices_t = synthetic_cubes(C, V, seed=20250301, device='cuda')
+    indptr, indices = np.asarray(indptr_t), np.asarray(indices_t)
+    ns = neg_sampler_from_csr(indptr, indices, V)
+    lists = _csr_lists(indptr, indices)
+    gen = DataGenerator(None, (indptr, indices), batch_size=B, shuffle=False, seed=7, neg_sampler=ns)
+    assert gen.N_cards == V or gen.data.V == V
+    gpu = []
+    for rep in range(2):          # two epochs over the same cubes: fresh draws (step counter)
+        gen.epoch = rep
+        for bi in range(C // B):
+            nb = gen.device_batch(bi)
+            xs = nb.x_lists()
+            yb = nb.y_dense()
+            for b in range(B):
+                gpu.append((lists[bi * B + b], xs[b], np.nonzero(yb[b])[0]))
+    mt = noise_ref.MTNoise(np.random.RandomState(11), ns, V)
+    ref = []
+    for rep in range(2):
+        for c in range(C):
+            x, y = mt.cube(lists[c])
+            ref.append((lists[c], x, y))
+
+    def observables(rows):
+        cut, add, ycut, adds = [], [], [], {}
+        for inc, x, y in rows:
+            s_inc, s_x, s_y = set(inc.tolist()), set(x.tolist()), set(y.tolist())
+            assert s_y <= s_inc
+            cut.append(len(s_inc - s_x) / len(inc))
+            a = s_x - s_inc
+            add.append(len(a) / len(inc))
+            ycut.append(len(s_inc - s_y) / len(inc))
+            for j in a:
+                adds[j] = adds.get(j, 0) + 1
+        return np.array(cut), np.array(add), np.array(ycut), adds
+    g, r = observables(gpu), observables(ref)
+    for a, b, what in zip(g[:3], r[:3], ('cut', 'add', 'ycut')):
+        p = stats.ks_2samp(a, b).pvalue
+        assert p > 1e-4, (what, p, a.mean(), b.mean())
+    # the 30 most-added cards over both samples (the popular cards sit in almost every cube and are
+    # rarely added); a selection symmetric in the two samples keeps the homogeneity test valid
+    both = {j: g[3].get(j, 0) + r[3].get(j, 0) for j in set(g[3]) | set(r[3])}
+    top = sorted(both, key=lambda j: -both[j])[:30]
+    cg = np.array([g[3].get(int(j), 0) for j in top], float)
+    cr = np.array([r[3].get(int(j), 0) for j in top], float)
+    tot = np.array([[cg.sum(), sum(g[3].values()) - cg.sum()], [cr.sum(), sum(r[3].values()) - cr.sum()]])
+    table = np.vstack([cg, cr])
+    p = stats.chi2_contingency(table).pvalue
+    assert p > 1e-4, (p, cg[:5], cr[:5])
+    assert stats.chi2_contingency(tot).pvalue > 1e-4

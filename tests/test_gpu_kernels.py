@@ -48,7 +48,7 @@ def _run_noise(lists, V, B, ns, seed, step, with_reg=True, slot_rank=0, guide_lo
                     cdf=cdf_d.data_ptr(), neg_sampler=ns_d.data_ptr(), state=state.data_ptr(),
                     guide=guide.data_ptr() if guide is not None else None, guide_log2=guide_log2,
                     x_cnt=x_cnt.data_ptr(), x_idx=x_idx.data_ptr(), y_bits=y_bits.data_ptr(),
-                    xt_bits=xt.data_ptr(), reg_idx=reg.data_ptr(), status=status.data_ptr())
+                    xt_bits=xt.data_ptr(), reg_idx=reg.data_ptr(), status=status.data_ptr(), xt_rows=R)
     L.call('cc_noise_fwd', ctypes.byref(a), L.stream_ptr())
     torch.cuda.synchronize()
     assert int(status.item()) == 0
@@ -312,6 +312,7 @@ def test_softmax_kl_rows(V, dtype):
     Mt /= Mt.sum(1, keepdims=True)
     Mt[:, ::7] = 0.0
     ridx = rng.integers(0, B + 3, B).astype(np.int32)
+    ridx[7] = -1                                # a masked padding row (owner-computes capacity)
     dt = L.CC_BF16 if dtype == 'bf16' else L.CC_F32
     tdt = torch.bfloat16 if dtype == 'bf16' else torch.float32
     Zd = torch.from_numpy(Z).cuda()
@@ -319,10 +320,11 @@ def test_softmax_kl_rows(V, dtype):
     rd = torch.from_numpy(ridx).cuda()
     dZ = torch.zeros(B, V, device='cuda', dtype=tdt)
     part = torch.zeros(B, device='cuda', dtype=torch.float64)
-    L.call('cc_dec_softmax_kl_fused', dt, L.ptr(Zd), B, V, L.ptr(Md), L.ptr(rd), reg, L.ptr(dZ),
+    L.call('cc_dec_softmax_kl_fused', dt, L.ptr(Zd), B, V, L.ptr(Md), L.ptr(rd), reg / B, L.ptr(dZ),
            L.ptr(part), L.stream_ptr())
     torch.cuda.synchronize()
-    kl, dz = _softmax_kl_ref(Z, Mt[ridx], reg, B)
+    kl, dz = _softmax_kl_ref(Z, Mt[np.maximum(ridx, 0)], reg, B)
+    kl[7], dz[7] = 0.0, 0.0
     np.testing.assert_allclose(part.cpu().numpy(), kl, rtol=1e-4)
     assert rel_err(dZ.float().cpu().numpy(), dz) < (1e-5 if dtype == 'fp32' else 4e-3)
 

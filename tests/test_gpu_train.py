@@ -308,3 +308,38 @@ def test_adam_pack_images_and_counters():
     tr.transpose_tower()
     torch.cuda.synchronize()
     assert torch.equal(got, tr.wpack)
+
+
+@pytest.mark.parametrize('dtype,V,d,B', [('fp32', 700, 64, 32), ('bf16', 1500, 256, 128)])
+def test_full_mode_regulariser_matches_oracle(dtype, V, d, B):
+    """reg_mode='full' (README.md:27: KL(M~, D2(E(I))) over ALL |V| identity rows every step):
+    the rows are static (x row = {card}, reg_idx = card, padded rows masked), their W1 gradient is
+    added row by row (cc_embed_identity_add), the KL is the mean over V rows — against the oracle
+    with reg_idx = arange(V), y_reg = M~, for two steps with Adam between them."""
+    C = 4 * B
+    lists, Mt, ns = problem(5, C, V, (20, 40, 80))
+    P = model_ref.init_params(V, d, seed=5, bias_std=0.01)
+    lay = Layout(V, d)
+    cfg = TrainConfig(V=V, d=d, batch_size=B, reg=0.3, dtype=dtype, seed=5, reg_mode='full')
+    tr = Trainer(cfg, DeviceDataset(lists, V, y_mtx=Mt.astype(np.float32), neg_sampler=ns), params_flat=lay.pack(P))
+    assert tr.full_reg and tr.Breg >= V and tr.Breg % 32 == 0 and tr.R == B + tr.Breg
+    perm = np.random.default_rng(5).permutation(C).astype(np.int32)
+    tr.set_epoch_permutation(perm)
+    tr.capture()
+    cdf = noise_ref.cdf_of(ns)
+    mode, ltol, gtol = ('fp64', 1e-4, 1e-4) if dtype == 'fp32' else ('bf16', 2e-4, 2e-2)
+    for step in range(2):
+        Pk = lay.unpack(tr.standard(tr.params))
+        tr.step()
+        torch.cuda.synchronize()
+        cubes = [lists[c] for c in perm[step * B:(step + 1) * B]]
+        oxs, oys, _, _ = noise_ref.philox_noise_batch(cubes, cdf, ns, 5, step, with_reg=False)
+        losses, grads = model_ref.train_forward_backward(Pk, oxs, oys, V, d, reg=0.3, reg_idx=np.arange(V),
+                                                         y_reg=Mt, mode=mode)
+        got = tr.losses()
+        assert abs(got['bce'] - losses['bce']) / losses['bce'] < ltol, (step, got, losses)
+        assert abs(got['kl'] - losses['kl']) / losses['kl'] < ltol, (step, got, losses)
+        g = lay.unpack(tr.standard(tr.grads))
+        bad = {k: rel_err(g[k], grads[k]) for k in grads if not rel_err(g[k], grads[k]) < gtol}
+        assert not bad, (step, bad)
+    tr.check_status()

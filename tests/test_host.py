@@ -19,10 +19,11 @@ def test_neg_sampler_closed_form_matches_dense_definition():
 
 
 def test_reg_row_shards_equal_mass_and_owner_draws():
-    """M~ row shards at equal cumulative neg_sampler mass; a rank's reg draws (Philox
-    oracle, shard-conditioned) stay in its rows and follow neg_sampler restricted to them."""
+    """SURVEY §8(e) owner computes: M~ row shards at equal cumulative neg_sampler mass; the ranks'
+    owned rows of the global draws partition exactly the one-process draws (slot order kept), and
+    the static capacity covers the Binomial(world*B, m_r) owned count at 6 sigma."""
     import pytest
-    from cubecobrarecommender_amd.trainer import reg_row_shards
+    from cubecobrarecommender_amd.trainer import full_rows, owner_capacity, reg_row_shards
     rng = np.random.default_rng(5)
     V = 3000
     ns = 1.0 / (1.0 + rng.permutation(V))
@@ -34,18 +35,32 @@ def test_reg_row_shards_equal_mass_and_owner_draws():
         assert b[0] == 0 and b[-1] == V and np.all(np.diff(b) > 0)
         assert abs(m.sum() - 1.0) < 1e-12
         assert np.all(np.abs(m - 1.0 / W) < ns.max() + 1e-12)   # off by at most one card's mass
-    b, m = reg_row_shards(cdf, 4)
-    for r in range(4):
-        lo, hi = int(b[r]), int(b[r + 1])
-        draws = noise_ref.philox_reg_indices(cdf, 11, 0, 0, 40000, (lo, hi))
-        assert draws.min() >= lo and draws.max() < hi
-        freq = np.bincount(draws - lo, minlength=hi - lo) / len(draws)
-        want = ns[lo:hi] / ns[lo:hi].sum()
-        top = np.argsort(-want)[:20]
-        assert np.all(np.abs(freq[top] - want[top]) < 5 * np.sqrt(want[top] / len(draws)) + 1e-3)
-    # unsharded oracle path unchanged by the new argument
-    np.testing.assert_array_equal(noise_ref.philox_reg_indices(cdf, 11, 3, 7, 500),
-                                  noise_ref.philox_reg_indices(cdf, 11, 3, 7, 500, None))
+    B, W = 512, 8
+    b, m = reg_row_shards(cdf, W)
+    cap = owner_capacity(m, B, W)
+    assert cap % 32 == 0 and W * B * m.max() < cap <= W * B
+    flat = np.full(8, 1 / 8)        # the bench's shards sit within 0.1 % of equal mass
+    assert owner_capacity(flat, 512, 8) == 640 and owner_capacity(flat[:2] * 4, 512, 2) == 640
+    worst = 0
+    for step in range(40):
+        one = noise_ref.philox_reg_indices(cdf, 11, step, 0, W * B)      # one process, batch W*B
+        parts = []
+        for r in range(W):
+            rows, n, over = noise_ref.owner_reg_rows(cdf, 11, step, W * B, int(b[r]), int(b[r + 1]), cap)
+            assert not over and np.all(rows[n:] == -1)
+            assert np.all((rows[:n] >= b[r]) & (rows[:n] < b[r + 1]))
+            parts.append(rows[:n])
+            worst = max(worst, n)
+        # every draw is owned by exactly one rank, in slot order within the rank
+        merged = np.concatenate(parts)
+        assert np.array_equal(np.sort(merged), np.sort(one))
+        for r in range(W):
+            sel = one[(one >= b[r]) & (one < b[r + 1])]
+            assert np.array_equal(parts[r], sel)
+    assert worst <= cap
+    lo_hi = [full_rows(22000, 8, r) for r in range(8)]
+    assert lo_hi[0][0] == 0 and lo_hi[-1][1] == 22000
+    assert all(lo_hi[i][1] == lo_hi[i + 1][0] for i in range(7))
     heavy = np.full(10, 0.01)
     heavy[0] = 0.91
     with pytest.raises(ValueError):

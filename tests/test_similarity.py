@@ -43,7 +43,7 @@ def test_oracle_batched_encoder_equals_per_row():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('V,N', [(300, 1), (300, 300), (20884, 40), (5000, 4096)])
+@pytest.mark.parametrize('V,N', [(300, 1), (300, 300), (20884, 40), (5000, 4096), (9000, 6000)])
 def test_gpu_similar_cards_bit_exact(V, N):
     import torch
     from cubecobrarecommender_amd.similarity import similar
@@ -55,6 +55,7 @@ def test_gpu_similar_cards_bit_exact(V, N):
         oi, od, _ = similarity_ref.most_similar(e, q, N)
         assert np.array_equal(idx, oi), q
         assert np.array_equal(dist.view(np.uint32) & 0x7FFFFFFF, od.view(np.uint32) & 0x7FFFFFFF), q
+    assert len(similar(emb, 0, 0)[0]) == 0 and len(similar(emb, 0, V + 5)[0]) == V
 
 
 @pytest.mark.gpu
