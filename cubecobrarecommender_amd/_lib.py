@@ -64,7 +64,8 @@ class DecKlArgs(C.Structure):
     _fields_ = [
         ('d', C.c_int32), ('V', C.c_int32), ('rows', C.c_int32), ('ldt', C.c_int32), ('row0', C.c_int32),
         ('D3p', C.c_void_p), ('D3tp', C.c_void_p), ('Wo', C.c_void_p),
-        ('bo', C.c_void_p), ('Mt', C.c_void_p), ('tsum', C.c_void_p), ('reg_idx', C.c_void_p),
+        ('bo', C.c_void_p), ('Mt', C.c_void_p), ('tsum', C.c_void_p), ('mt_bytes', C.c_int64), ('mt_lo', C.c_int32),
+        ('reg_idx', C.c_void_p),
         ('scale', C.c_float), ('dZ', C.c_void_p), ('gW', C.c_void_p), ('gb', C.c_void_p),
         ('loss_partials', C.c_void_p), ('loss_out', C.c_void_p), ('loss_scale', C.c_double),
         ('ticket', C.c_void_p), ('ws', C.c_void_p),

@@ -46,8 +46,10 @@ struct KlP {
   double *loss_partials, *loss_out;
   double loss_scale;
   uint32_t *ticket;
+  uint32_t mt_bytes;               // extent of Mt from its base (buffer range check)
+  int mt_lo;                        // first card whose M~ row is resident
   float *part_m, *part_s, *part_d;  // [rows][nsl]
-  float4 *rowstat;                  // [rows] {m, 1/s, ln s, S}
+  float4 *rowstat;                  // [rows] {m, ln s, S, -}
   uint32_t *flag;                   // [1] an element with p < 1e-7 was seen this step
 };
 
@@ -114,9 +116,12 @@ __device__ __forceinline__ void logits_block(const KlP &p, const bf16_t *Wt, int
   for (int kk = 0; kk < RING; ++kk) af[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 512);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int j = 0; j < NJ; ++j)
+  for (int j = 0; j < NJ; ++j) {
+    float b = bias[j];
+    asm volatile("" : "+v"(b));  // per call: the 48-register bias broadcast is not hoisted (and spilled)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = bias[j];
+    for (int r = 0; r < 16; ++r) acc[j][r] = b;
+  }
 #pragma unroll
   for (int kk = 0; kk < nkk; ++kk) {
 #pragma unroll
@@ -126,6 +131,36 @@ __device__ __forceinline__ void logits_block(const KlP &p, const bf16_t *Wt, int
     }
     if (kk + RING < nkk) af[kk % RING] = *reinterpret_cast<const bf16x8_t *>(src + (kk + RING) * 512);
   }
+}
+
+// Reduce-scatter of 16 per-row values over the 32 lanes of a half-wave (lanes with the same
+// lane >> 5 hold the same 16 rows of an MFMA accumulator, one column each): 8 + 4 + 2 + 1 + 1
+// shuffles instead of 16 x 5.  Returns, in every lane, the reduction of row (lane >> 1) & 15.
+template <bool MAX>
+__device__ __forceinline__ float rs16(const float (&v)[16]) {
+  const int lane = threadIdx.x & 63;
+  float a[8];
+  {
+    const bool b = lane & 16;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float send = b ? v[i] : v[i + 8], keep = b ? v[i + 8] : v[i];
+      const float got = __shfl_xor(send, 16);
+      a[i] = MAX ? fmaxf(keep, got) : keep + got;
+    }
+  }
+#pragma unroll
+  for (int h = 4, m = 8; h >= 1; h >>= 1, m >>= 1) {  // xor 8, 4, 2 on 4, 2, 1 values
+    const bool b = lane & m;
+#pragma unroll
+    for (int i = 0; i < h; ++i) {
+      const float send = b ? a[i] : a[i + h], keep = b ? a[i + h] : a[i];
+      const float got = __shfl_xor(send, m);
+      a[i] = MAX ? fmaxf(keep, got) : keep + got;
+    }
+  }
+  const float got = __shfl_xor(a[0], 1);
+  return MAX ? fmaxf(a[0], got) : a[0] + got;
 }
 
 __device__ __forceinline__ float half_max(float v) {
@@ -159,21 +194,30 @@ __global__ __launch_bounds__(NTH) void kl_stats_kernel(KlP p) {
   }
   f32x16_t acc[NJ];
   logits_block<D>(p, Wt, (p.row0 + r_blk) / 32, bias, acc);
+  // per-row max over the slice: lane-local over the NJ columns, then across the half-wave
+  float v[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     float m = -INFINITY;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) m = valid[j] ? fmaxf(m, acc[j][r]) : m;
-    m = half_max(m);
-    float s = 0.f;
+    v[r] = m;
+  }
+  const float mr = rs16<true>(v);  // max of row (lane >> 1) & 15
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) s += valid[j] ? __builtin_amdgcn_exp2f((acc[j][r] - m) * LOG2E) : 0.f;
-    s = half_sum(s);
-    if ((lane & 31) == r) {
-      const int row = r_blk + acc_row(r, lane);
-      p.part_m[(int64_t)row * p.nsl + sl] = m;
-      p.part_s[(int64_t)row * p.nsl + sl] = s;
-    }
+  for (int r = 0; r < 16; ++r) {   // broadcast each row's max back from lane 2r of the half
+    const float m = __shfl(mr, (lane & 32) + 2 * r);
+    float e = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) e += valid[j] ? __builtin_amdgcn_exp2f((acc[j][r] - m) * LOG2E) : 0.f;
+    v[r] = e;
+  }
+  const float sr = rs16<false>(v);
+  if ((lane & 1) == 0) {
+    const int rr = (lane >> 1) & 15;
+    const int row = r_blk + acc_row(rr, lane);
+    p.part_m[(int64_t)row * p.nsl + sl] = mr;
+    p.part_s[(int64_t)row * p.nsl + sl] = sr;
   }
 }
 
@@ -194,7 +238,7 @@ __global__ __launch_bounds__(256) void kl_merge_kernel(KlP p) {
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
   if (lane == 0) {
     const int card = p.reg_idx[row];
-    p.rowstat[row] = make_float4(m, 1.f / s, __logf(s), card >= 0 ? p.tsum[card] : 0.f);
+    p.rowstat[row] = make_float4(m, __logf(s), card >= 0 ? p.tsum[card] : 0.f, 0.f);
   }
 }
 
@@ -203,7 +247,7 @@ constexpr int ZT_BYTES = NB * TR * 2;
 struct MainSmem {
   bf16_t Zt[NB * TR];       // dZ^T tile [NB][TR] (swizzled)
   float4 rs[TR];            // row stats of the tile
-  int32_t card[TR];         // reg_idx of the tile's rows
+  int32_t card[TR];         // M~ row byte offset of the tile's rows (0x80000000: padding row)
   float red_cs[NTH / 64][NB];
   double red_loss[NTH / 64];
   int lastflag;
@@ -212,15 +256,10 @@ struct MainSmem {
 // FIX = false: the main pass.  FIX = true: the exact-clip correction (runs only when p.flag is set):
 // c = -scale p delta_row replaces dz; dZ, dWo, dbo are updated in place.
 template <int D, bool FIX>
-__global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
+__device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt, MainSmem &sm) {
   constexpr int CHB = TR / 8;
-  __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
-  __shared__ __attribute__((aligned(16))) MainSmem sm;
-  if constexpr (FIX) {
-    if (__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
-  }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
-  const int n0 = blockIdx.x * NB;
+  const int n0 = sl * NB;
   const int V = p.V;
   load_wo_slice<D>(p.Wo, V, n0, Wt);
   float bias[NJ], cs[NJ];
@@ -236,8 +275,10 @@ __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
   bool dead = false;
   // M~ rows and dZ through buffer descriptors: a 32-bit byte offset per access instead of a 64-bit
   // address (M~ < 4 GB at |V| <= 32k; dZ rows x V x 2 B < 4 GB)
-  const __amdgpu_buffer_rsrc_t mt_rs = __builtin_amdgcn_make_buffer_rsrc((void *)p.Mt, (short)0, 0xFFFFFFFF, 0x00020000);
-  const __amdgpu_buffer_rsrc_t dz_rs = __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, 0xFFFFFFFF, 0x00020000);
+  // (out-of-range offsets — padding rows, columns past V — read 0 / drop the store: no branches)
+  const __amdgpu_buffer_rsrc_t mt_rs = __builtin_amdgcn_make_buffer_rsrc((void *)p.Mt, (short)0, p.mt_bytes, 0x00020000);  // < 2^31
+  const __amdgpu_buffer_rsrc_t dz_rs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)p.rows * (uint32_t)V * 2u, 0x00020000);
   const float scale = p.scale;
 
   for (int t0 = 0; t0 < p.rows; t0 += TR) {
@@ -245,14 +286,15 @@ __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
     __syncthreads();  // previous tile's phase 2 done with Zt / rs
     for (int i = tid; i < nt; i += NTH) {
       float4 st = p.rowstat[t0 + i];
-      if constexpr (FIX) {  // .w <- delta of the row: the sum of its slices' partials, in order
+      if constexpr (FIX) {  // .z <- delta of the row: the sum of its slices' partials, in order
         float dl = 0.f;
         const float *pd = p.part_d + (int64_t)(t0 + i) * p.nsl;
         for (int s = 0; s < p.nsl; ++s) dl += pd[s];
-        st.w = dl;
+        st.z = dl;
       }
       sm.rs[i] = st;
-      sm.card[i] = p.reg_idx[t0 + i];
+      const int card = p.reg_idx[t0 + i];
+      sm.card[i] = card >= 0 ? (int32_t)((uint32_t)card * (uint32_t)V * 4u) : (int32_t)0x80000000u;
     }
     __syncthreads();
     // ---- phase 1: two passes of 8 waves x 32 rows
@@ -264,21 +306,23 @@ __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
       logits_block<D>(p, Wt, (p.row0 + t0 + rb) / 32, bias, acc);
       // the M~ values of the wave's elements: column tile j's 16 per lane are loaded while tile
       // j - 1's epilogue runs (issued behind the MFMAs: the A fragments are dead by then)
-      int cards[16];
+      // row byte offsets into M~ (card * V * 4), or a sentinel past the buffer's range for
+      // padding rows: their loads return 0 without touching memory.  Loads are unconditional
+      // (a conditional load becomes a branch with a wait per load).
+      uint32_t roff[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) cards[r] = sm.card[rb + acc_row(r, lane)];
+      for (int r = 0; r < 16; ++r) roff[r] = (uint32_t)sm.card[rb + acc_row(r, lane)];
       uint32_t zrow = (uint32_t)((t0 + rb + 4 * half) * V + n0 + (lane & 31));
       asm volatile("" : "+v"(zrow));  // per-pass base of the dZ stores (no hoisted 64-bit addresses)
       float tv[2][16];
       auto load_t = [&](int j, float (&dst)[16]) {
-        const uint32_t gc = (uint32_t)(n0 + j * 32 + (lane & 31));
+        const uint32_t gc4 = 4u * (uint32_t)(n0 + j * 32 + (lane & 31));
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float v = __builtin_amdgcn_raw_buffer_load_b32(mt_rs, 4u * ((uint32_t)max(cards[r], 0) * (uint32_t)V + gc), 0, 0);
-          dst[r] = (cards[r] >= 0 && valid[j]) ? v : 0.f;
-        }
+        for (int r = 0; r < 16; ++r)
+          dst[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mt_rs, roff[r] + gc4, 0, 0));
       };
       if constexpr (!FIX) load_t(0, tv[0]);
+      bool deadp = false;   // an element of this pass has p < 1e-7
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int col = j * 32 + (lane & 31);
@@ -290,20 +334,20 @@ __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
         for (int r = 0; r < 16; ++r) {
           const int lr = rb + acc_row(r, lane);
           const float4 st = sm.rs[lr];
-          const bool live_row = cards[r] >= 0 && valid[j];
-          const float zm = acc[j][r] - st.x;
-          const float pr = __builtin_amdgcn_exp2f(zm * LOG2E) * st.y;
+          const bool live_row = roff[r] < 0x80000000u && valid[j];
+          const float lp = acc[j][r] - st.x - st.y;  // ln p = z - m - ln s
+          const float pr = __builtin_amdgcn_exp2f(lp * LOG2E);
           const bool live = pr >= PMIN;
           float dz;
           if constexpr (!FIX) {
             const float tc = __builtin_amdgcn_fmed3f(tv[j & 1][r], PMIN, 1.f);
-            const float lq = live ? fminf(zm - st.z, 0.f) : LN_PMIN;
+            const float lq = live ? fminf(lp, 0.f) : LN_PMIN;  // ln clip(p, 1e-7, 1)
             const float term = tc * fmaf(__builtin_amdgcn_logf(tc), LN2, -lq);
             klsum += live_row ? term : 0.f;
-            dead |= live_row && !live;
-            dz = live_row ? scale * (pr * st.w - (live ? tc : 0.f)) : 0.f;
+            deadp |= live_row && !live;
+            dz = live_row ? scale * (pr * st.z - (live ? tc : 0.f)) : 0.f;
           } else {
-            dz = live_row ? -scale * pr * st.w : 0.f;  // st.w = delta
+            dz = live_row ? -scale * pr * st.z : 0.f;  // st.z = delta
           }
           const uint32_t zoff = 2u * (zrow + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V + j * 32));
           uint16_t zb;
@@ -324,6 +368,7 @@ __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
           *reinterpret_cast<uint2 *>(sm.Zt + sw_off(col, rb + 8 * g + 4 * half, CHB)) =
               *reinterpret_cast<const uint2 *>(&tt[4 * g]);
       }
+      if constexpr (!FIX) dead |= deadp;
     }
     __syncthreads();
     // ---- phase 2: dWo[d][NB] (+)= D3^T[d][tile rows] dZ[tile rows][NB] (wave w: d rows 32w..).
@@ -408,9 +453,9 @@ __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
       for (int i = 0; i < NTH / 64; ++i) sum += sm.red_loss[i];
       sm.lastflag = 0;
       if (!p.loss_out) {
-        p.loss_partials[blockIdx.x] = sum;
+        p.loss_partials[sl] = sum;
       } else {
-        __hip_atomic_store(&p.loss_partials[blockIdx.x], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&p.loss_partials[sl], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint32_t tk = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sm.lastflag = tk == gridDim.x - 1;
@@ -437,43 +482,68 @@ __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
   }
 }
 
+template <int D>
+__global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
+  __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
+  __shared__ __attribute__((aligned(16))) MainSmem sm;
+  kl_slice<D, false>(p, blockIdx.x, Wt, sm);
+}
+
+// The exact-clip correction: a small persistent grid (FIXG blocks) that leaves at once when the
+// step saw no p < 1e-7, and otherwise walks the slices.
+constexpr int FIXG = 64;
+template <int D>
+__global__ __launch_bounds__(NTH) void kl_fix_kernel(KlP p) {
+  __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
+  __shared__ __attribute__((aligned(16))) MainSmem sm;
+  if (__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+  for (int sl = blockIdx.x; sl < p.nsl; sl += gridDim.x) {
+    kl_slice<D, true>(p, sl, Wt, sm);
+    __syncthreads();  // LDS reuse by the next slice
+  }
+}
+
 // ---------------------------------------------------------------- fix: delta partials
 template <int D>
 __global__ __launch_bounds__(NTH) void kl_delta_kernel(KlP p) {
   __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
   if (__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int sl = blockIdx.x, n0 = sl * NB;
-  const int r_blk = blockIdx.y * SR + w * 32;
-  load_wo_slice<D>(p.Wo, p.V, n0, Wt);
-  __syncthreads();
-  if (r_blk >= p.rows) return;
-  float bias[NJ];
-  bool valid[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int gc = n0 + j * 32 + (lane & 31);
-    valid[j] = gc < p.V;
-    bias[j] = valid[j] ? p.bo[gc] : 0.f;
-  }
-  f32x16_t acc[NJ];
-  logits_block<D>(p, Wt, (p.row0 + r_blk) / 32, bias, acc);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = r_blk + acc_row(r, lane);
-    const float4 st = p.rowstat[row];
-    const int card = p.reg_idx[row];
-    float dl = 0.f;
+  const int ngroups = (int)cdiv(p.rows, SR);
+  for (int wi = blockIdx.x; wi < p.nsl * ngroups; wi += gridDim.x) {
+    const int sl = wi % p.nsl, n0 = sl * NB;
+    const int r_blk = (wi / p.nsl) * SR + w * 32;
+    __syncthreads();  // the previous item's readers of Wt are done
+    load_wo_slice<D>(p.Wo, p.V, n0, Wt);
+    __syncthreads();
+    if (r_blk >= p.rows) continue;  // wave-uniform; no barrier below
+    float bias[NJ];
+    bool valid[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const float pr = __builtin_amdgcn_exp2f((acc[j][r] - st.x) * LOG2E) * st.y;
-      if (card >= 0 && valid[j] && !(pr >= PMIN)) {
-        const float t = p.Mt[(int64_t)card * p.V + n0 + j * 32 + (lane & 31)];
-        dl += __builtin_amdgcn_fmed3f(t, PMIN, 1.f);
-      }
+      const int gc = n0 + j * 32 + (lane & 31);
+      valid[j] = gc < p.V;
+      bias[j] = valid[j] ? p.bo[gc] : 0.f;
     }
-    dl = half_sum(dl);
-    if ((lane & 31) == r) p.part_d[(int64_t)row * p.nsl + sl] = dl;
+    f32x16_t acc[NJ];
+    logits_block<D>(p, Wt, (p.row0 + r_blk) / 32, bias, acc);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = r_blk + acc_row(r, lane);
+      const float4 st = p.rowstat[row];
+      const int card = p.reg_idx[row];
+      float dl = 0.f;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float pr = __builtin_amdgcn_exp2f((acc[j][r] - st.x - st.y) * LOG2E);
+        if (card >= 0 && valid[j] && !(pr >= PMIN)) {
+          const float t = p.Mt[(int64_t)card * p.V + n0 + j * 32 + (lane & 31)];
+          dl += __builtin_amdgcn_fmed3f(t, PMIN, 1.f);
+        }
+      }
+      dl = half_sum(dl);
+      if ((lane & 31) == r) p.part_d[(int64_t)row * p.nsl + sl] = dl;
+    }
   }
 }
 
@@ -529,6 +599,11 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
   p.Wo = (const bf16_t *)a->Wo;
   p.bo = a->bo;
   p.Mt = a->Mt;
+  CC_REQUIRE(a->mt_bytes > 0 && a->mt_bytes <= 0x7FFFFFFFll && (int64_t)a->rows * a->V * 2 <= 0xFFFFFFFFll,
+             "cc_dec_softmax_kl_dw: M~ extent below 2 GB and dZ below 4 GB (32-bit buffer offsets)");
+  p.mt_bytes = (uint32_t)a->mt_bytes;
+  CC_REQUIRE(a->mt_lo >= 0 && (int64_t)(a->mt_lo + 1) * a->V * 4 <= a->mt_bytes, "cc_dec_softmax_kl_dw: mt_lo");
+  p.mt_lo = a->mt_lo;
   p.tsum = a->tsum;
   p.reg_idx = a->reg_idx;
   p.scale = a->scale;
@@ -554,11 +629,11 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
     CC_LAUNCH_CHECK("kl_stats_kernel");                                                                      \
     hipLaunchKernelGGL(kl_merge_kernel, dim3((unsigned)cdiv(a->rows, 4)), dim3(256), 0, s, p);              \
     CC_LAUNCH_CHECK("kl_merge_kernel");                                                                      \
-    hipLaunchKernelGGL((kl_main_kernel<DD, false>), gm, dim3(NTH), 0, s, p);                                \
+    hipLaunchKernelGGL((kl_main_kernel<DD>), gm, dim3(NTH), 0, s, p);                                       \
     CC_LAUNCH_CHECK("kl_main_kernel");                                                                       \
-    hipLaunchKernelGGL((kl_delta_kernel<DD>), gs, dim3(NTH), 0, s, p);                                      \
+    hipLaunchKernelGGL((kl_delta_kernel<DD>), dim3(FIXG), dim3(NTH), 0, s, p);                              \
     CC_LAUNCH_CHECK("kl_delta_kernel");                                                                      \
-    hipLaunchKernelGGL((kl_main_kernel<DD, true>), gm, dim3(NTH), 0, s, p);                                 \
+    hipLaunchKernelGGL((kl_fix_kernel<DD>), dim3(FIXG), dim3(NTH), 0, s, p);                                \
     CC_LAUNCH_CHECK("kl_fix_kernel");                                                                        \
   }
   KL_LAUNCH(256)

@@ -246,7 +246,7 @@ class Trainer:
         self.gH3 = torch.zeros(R, 128, **T)
         self.gH2 = torch.zeros(R, 256, **T)
         self.gPre1 = torch.zeros(R, d, **f32)
-        self.Z2 = torch.zeros(self.Breg, V, **f32) if self.use_reg else None
+        self.Z2 = None             # materialised fp32 D2 logits (the unfused regulariser path only)
         self.splits = max(1, min(32, V // 512))            # decoder dX: K = V (32: 22.4 us vs 29.5 at 16)
         # the regulariser branch's dX: M = Breg rows; with thousands of rows (full mode) the output
         # tiles alone fill the chip — no split-K
@@ -300,9 +300,14 @@ class Trainer:
                            and os.environ.get('CCREC_EG_PACKED', '1') != '0' else None)
             slab = int(L.lib().cc_tower_slab_elems(d))
             self.slab = torch.zeros((R // 32) * slab, **f32)
+            # D2 output layer fused (logits twice -> softmax -> KL -> dZ -> dWo, csrc/decreg.hip): bf16,
+            # d in {128, 256} with the packed D3 images (the same shape class as the fused D1 kernel)
+            self.fused_reg = (self.use_reg and self.D3p is not None and not self.mx8 and d in (128, 256)
+                              and self.Breg % 32 == 0 and os.environ.get('CCREC_REG_FUSED', '1') != '0')
             # decoder operands kept k-contiguous: D3^T (tower fwd), dZ^T (BCE epilogue), Wo^T shadow
             self.D3t = torch.zeros(d, R, **T)
-            self.dZt = [torch.zeros(V, n, **T) for n in self.branch_rows()]   # [branch][V][rows]
+            self.dZt = [torch.zeros(V, n, **T) if not (k == 1 and self.fused_reg) else None
+                        for k, n in enumerate(self.branch_rows())]   # [branch][V][rows]
             self.WoT = torch.zeros(len(branches_of(self.use_reg)), V, d, **T)
             if self.mx8:   # MX-FP8 operand images of the decoder output layers (csrc/mx8.hip)
                 nbr, u8 = len(branches_of(self.use_reg)), dict(device=self.dev, dtype=torch.uint8)
@@ -323,6 +328,17 @@ class Trainer:
             self.transpose_tower()
         else:
             self.targs = None
+        if not self.fused_tower:
+            self.fused_reg = False
+        if self.use_reg and not self.fused_reg:
+            self.Z2 = torch.zeros(self.Breg, V, **f32)
+        if self.fused_reg:
+            lo, hi = self.reg_rows
+            self.tsum = torch.zeros(hi - lo, **f32)       # clipped M~ row sums, once (static M~)
+            L.call('cc_kl_tsum', L.ptr(data.y_reg), hi - lo, V, L.ptr(self.tsum), L.stream_ptr())
+            self.kl_ws = torch.zeros(int(L.lib().cc_dec_kl_ws_size(self.Breg, V)) // 4 + 4, **f32)
+            self.kl_part = torch.zeros(max(int(L.lib().cc_dec_kl_blocks(V)), 1), device=self.dev,
+                                       dtype=torch.float64)
         if self.full_reg:
             self._init_full_rows()
         # one process: Adam also writes the transposed operand copies and advances the step
@@ -503,6 +519,8 @@ class Trainer:
         for k, pre in enumerate(branches_of(self.use_reg)):
             if k == 0 and self.fused_out and not getattr(self, "fused_adam", False):
                 continue    # cc_dec_bce_dw reads Wo itself: no Wo^T copy for the D1 branch
+            if k == 1 and self.fused_reg and not getattr(self, "fused_adam", False):
+                continue    # cc_dec_softmax_kl_dw reads Wo itself
             if self.mx8:
                 L.call('cc_quant_mx8', L.CC_BF16, self.w(pre + '/reconstruct/kernel'), d, V, V, 1,
                        L.ptr(self.WoT8[k]), d, L.ptr(self.WoT8s[k]), None, s)
@@ -678,7 +696,22 @@ class Trainer:
         t()
         ss = self._fork()          # off the critical path: loss reductions, output-layer dW
         # ---- D2 output + softmax + KL vs M~ rows (model.py:98; train.py:85)
-        if self.use_reg:
+        if self.use_reg and self.fused_reg:   # logits -> softmax -> KL -> dZ, dWo, dbo (decreg.hip)
+            lo, hi = self.reg_rows
+            t = self._tick("dec_softmax_kl")
+            ka = L.DecKlArgs(d=d, V=V, rows=Br, ldt=R, row0=B, D3p=L.ptr(self.D3p), D3tp=L.ptr(self.D3tp),
+                             Wo=self.w('decoder_for_reg/reconstruct/kernel'),
+                             bo=self.pf('decoder_for_reg/reconstruct/bias'),
+                             Mt=self.data.y_reg.data_ptr() - lo * V * 4, tsum=self.tsum.data_ptr() - lo * 4,
+                             mt_bytes=hi * V * 4, mt_lo=lo, reg_idx=L.ptr(self.reg_idx),
+                             scale=float(self.kl_row_scale), dZ=L.ptr(self.dZout[B:]),
+                             gW=self.gp('decoder_for_reg/reconstruct/kernel'),
+                             gb=self.gp('decoder_for_reg/reconstruct/bias'), loss_partials=L.ptr(self.kl_part),
+                             loss_out=L.ptr(self.loss_dev[1:]), loss_scale=float(self.kl_loss_scale),
+                             ticket=L.ptr(self.tickets[1:]), ws=L.ptr(self.kl_ws))
+            L.call('cc_dec_softmax_kl_dw', L.C.byref(ka), s)
+            t()
+        elif self.use_reg:
             if self.fused_tower:
                 self._gemm(Br, V, d, **self._dec_fwd(1, B), tb=1,
                            bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2))
@@ -712,6 +745,11 @@ class Trainer:
                 gx = self._gemm(nr, d, self.Vp if self.mx8 else V, **self._dec_dx(k, r0, pre), ta=0, tb=1,
                                 epi=L.CC_EPI_SPLITK, Cf=L.ptr(self.split_buf), splits=splits,
                                 launch=False)
+                if k == 1 and self.fused_reg:   # dWo/dbo came out of cc_dec_softmax_kl_dw: dX only
+                    L.call('cc_gemm', L.C.byref(gx), s)
+                    L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), splits, nr, d,
+                           L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
+                    continue
                 if k == 0 and self.fused_out:   # dWo/dbo came out of cc_dec_bce_dw: dX only
                     t = self._tick('dec_dX')
                     L.call('cc_gemm', L.C.byref(gx), s)

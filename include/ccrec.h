@@ -374,6 +374,8 @@ typedef struct cc_dec_kl_args {
   int32_t d, V, rows, ldt, row0;
   const void *D3p, *D3tp, *Wo;
   const float *bo, *Mt, *tsum;
+  int64_t mt_bytes;          /* bytes of Mt addressable from its base (rows of the shard end at it) */
+  int32_t mt_lo;             /* first card whose M~ row is resident (the shard's lo; 0 unsharded) */
   const int32_t *reg_idx;
   float scale;
   void *dZ;

@@ -343,3 +343,31 @@ def test_full_mode_regulariser_matches_oracle(dtype, V, d, B):
         bad = {k: rel_err(g[k], grads[k]) for k in grads if not rel_err(g[k], grads[k]) < gtol}
         assert not bad, (step, bad)
     tr.check_status()
+
+
+@pytest.mark.parametrize('V,B', [(2500, 128), (3001, 256)])
+def test_fused_regulariser_clip_fix_path(V, B):
+    """The fused D2 kernels' exact-clip path (csrc/decreg.hip): a decoder_for_reg bias spread
+    pushes part of every softmax row below 1e-7, so TF's clip gradient mask matters (S shrinks by
+    the excluded target mass) — the main kernel flags it and the fix kernels correct dZ, dWo, dbo.
+    Against the bf16-emulating oracle; a V not a multiple of the 96-column slices included."""
+    d = 256
+    tr, lists, Mt, ns, P, perm = _setup(V, d, B, 4 * B, 0.5, 'bf16')
+    assert tr.fused_reg
+    rng = np.random.default_rng(V)
+    P['decoder_for_reg/reconstruct/bias'] = np.linspace(-40, 6, V)[rng.permutation(V)].astype(np.float32)
+    tr.params.copy_(torch.from_numpy(tr.layout.pack(P)))
+    tr.refresh_shadow()
+    cdf = noise_ref.cdf_of(ns)
+    tr.forward_backward()
+    torch.cuda.synchronize()
+    cubes = [lists[c] for c in perm[:B]]
+    oxs, oys, oreg, _ = noise_ref.philox_noise_batch(cubes, cdf, ns, tr.cfg.seed, 0)
+    losses, grads = model_ref.train_forward_backward(P, oxs, oys, V, d, reg=0.5, reg_idx=oreg, y_reg=Mt[oreg],
+                                                     mode='bf16')
+    got = tr.losses()
+    assert abs(got['kl'] - losses['kl']) / losses['kl'] < 2e-4, (got, losses)
+    g = tr.layout.unpack(tr.grads.cpu().numpy())
+    for k in ('decoder_for_reg/reconstruct/kernel', 'decoder_for_reg/reconstruct/bias',
+              'decoder_for_reg/decoded_3/kernel', 'encoder/encoded_1/kernel'):
+        assert rel_err(g[k], grads[k]) < 2e-2, (k, rel_err(g[k], grads[k]))
