@@ -22,6 +22,11 @@
 // transposed into LDS).  Deterministic: every sum has a fixed order.
 #include "common.hpp"
 
+// dev-only timing hook (tools/micro/kl_probe.hip defines it); compiled out of the library
+#ifndef KL_PROBE
+#define KL_PROBE(k)
+#endif
+
 namespace {
 
 constexpr int NB = 96;       // V columns per block (230 slices at |V| = 22,000)
@@ -103,18 +108,27 @@ __device__ __forceinline__ void load_wo_slice(const bf16_t *__restrict__ Wo, int
   }
 }
 
-// z[32 rows][NB] = bo + D3[rows] Wo_slice for the wave's 32-row block rb (packed D3 image)
+// z[32 rows][NB] = bo + D3[rows] Wo_slice for the wave's 32-row block rb (packed D3 image): the
+// A-fragment loads (logits_load, a ring of LRING) and the MFMAs (logits_mfma) are separate so a
+// caller can put other loads behind the fragments' in the memory queue
 template <int D>
-__device__ __forceinline__ void logits_block(const KlP &p, const bf16_t *Wt, int rb, const float (&bias)[NJ],
-                                             f32x16_t (&acc)[NJ]) {
-  constexpr int nkk = D / 16, CHD = D / 8;
-  const int lane = threadIdx.x & 63, half = lane >> 5;
-  const bf16_t *src = p.D3p + ((int64_t)rb * nkk * 64 + lane) * 8;
-  constexpr int RING = nkk < 8 ? nkk : 8;  // A fragments in flight (a ring: the kernels that
-  bf16x8_t af[RING];                       // call this keep other accumulators live)
+struct LFrag {
+  static constexpr int nkk = D / 16, RING = nkk < 8 ? nkk : 8;
+  bf16x8_t af[RING];
+  const bf16_t *src;
+};
+template <int D>
+__device__ __forceinline__ void logits_load(const KlP &p, int rb, LFrag<D> &f) {
+  const int lane = threadIdx.x & 63;
+  f.src = p.D3p + ((int64_t)rb * LFrag<D>::nkk * 64 + lane) * 8;
 #pragma unroll
-  for (int kk = 0; kk < RING; ++kk) af[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 512);
-  __builtin_amdgcn_sched_barrier(0);
+  for (int kk = 0; kk < LFrag<D>::RING; ++kk) f.af[kk] = *reinterpret_cast<const bf16x8_t *>(f.src + kk * 512);
+}
+template <int D>
+__device__ __forceinline__ void logits_mfma(const bf16_t *Wt, LFrag<D> &f, const float (&bias)[NJ],
+                                            f32x16_t (&acc)[NJ]) {
+  constexpr int nkk = LFrag<D>::nkk, RING = LFrag<D>::RING, CHD = D / 8;
+  const int lane = threadIdx.x & 63, half = lane >> 5;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     float b = bias[j];
@@ -127,10 +141,18 @@ __device__ __forceinline__ void logits_block(const KlP &p, const bf16_t *Wt, int
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const bf16x8_t b = frag(Wt, sw_off(j * 32 + (lane & 31), kk * 16 + 8 * half, CHD));
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk % RING], b, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.af[kk % RING], b, acc[j], 0, 0, 0);
     }
-    if (kk + RING < nkk) af[kk % RING] = *reinterpret_cast<const bf16x8_t *>(src + (kk + RING) * 512);
+    if (kk + RING < nkk) f.af[kk % RING] = *reinterpret_cast<const bf16x8_t *>(f.src + (kk + RING) * 512);
   }
+}
+template <int D>
+__device__ __forceinline__ void logits_block(const KlP &p, const bf16_t *Wt, int rb, const float (&bias)[NJ],
+                                             f32x16_t (&acc)[NJ]) {
+  LFrag<D> f;
+  logits_load<D>(p, rb, f);
+  __builtin_amdgcn_sched_barrier(0);
+  logits_mfma<D>(Wt, f, bias, acc);
 }
 
 // Reduce-scatter of 16 per-row values over the 32 lanes of a half-wave (lanes with the same
@@ -181,8 +203,10 @@ __global__ __launch_bounds__(NTH) void kl_stats_kernel(KlP p) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int sl = blockIdx.x, n0 = sl * NB;
   const int r_blk = blockIdx.y * SR + w * 32;  // the wave's first row (regulariser-row index)
+  if (blockIdx.y == 0) KL_PROBE(8);
   load_wo_slice<D>(p.Wo, p.V, n0, Wt);
   __syncthreads();
+  if (blockIdx.y == 0) KL_PROBE(9);
   if (r_blk >= p.rows) return;
   float bias[NJ];
   bool valid[NJ];
@@ -203,6 +227,7 @@ __global__ __launch_bounds__(NTH) void kl_stats_kernel(KlP p) {
     for (int j = 0; j < NJ; ++j) m = valid[j] ? fmaxf(m, acc[j][r]) : m;
     v[r] = m;
   }
+  if (blockIdx.y == 0) KL_PROBE(10);
   const float mr = rs16<true>(v);  // max of row (lane >> 1) & 15
 #pragma unroll
   for (int r = 0; r < 16; ++r) {   // broadcast each row's max back from lane 2r of the half
@@ -213,6 +238,7 @@ __global__ __launch_bounds__(NTH) void kl_stats_kernel(KlP p) {
     v[r] = e;
   }
   const float sr = rs16<false>(v);
+  if (blockIdx.y == 0) KL_PROBE(11);
   if ((lane & 1) == 0) {
     const int rr = (lane >> 1) & 15;
     const int row = r_blk + acc_row(rr, lane);
@@ -261,6 +287,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
   const int n0 = sl * NB;
   const int V = p.V;
+  KL_PROBE(0);
   load_wo_slice<D>(p.Wo, V, n0, Wt);
   float bias[NJ], cs[NJ];
   bool valid[NJ];
@@ -297,80 +324,113 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       sm.card[i] = card >= 0 ? (int32_t)((uint32_t)card * (uint32_t)V * 4u) : (int32_t)0x80000000u;
     }
     __syncthreads();
+    KL_PROBE(1);
     // ---- phase 1: two passes of 8 waves x 32 rows
 #pragma unroll 1
     for (int ps = 0; ps < 2; ++ps) {
       const int rb = ps * 256 + w * 32;  // tile-local first row of the wave
       if (rb >= nt) continue;            // wave-uniform
-      f32x16_t acc[NJ];
-      logits_block<D>(p, Wt, (p.row0 + t0 + rb) / 32, bias, acc);
-      // the M~ values of the wave's elements: column tile j's 16 per lane are loaded while tile
-      // j - 1's epilogue runs (issued behind the MFMAs: the A fragments are dead by then)
       // row byte offsets into M~ (card * V * 4), or a sentinel past the buffer's range for
       // padding rows: their loads return 0 without touching memory.  Loads are unconditional
-      // (a conditional load becomes a branch with a wait per load).
+      // (a conditional load becomes a branch with a wait per load) and all of the pass's are
+      // issued before its logits, so their HBM latency runs under the MFMAs.
       uint32_t roff[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) roff[r] = (uint32_t)sm.card[rb + acc_row(r, lane)];
       uint32_t zrow = (uint32_t)((t0 + rb + 4 * half) * V + n0 + (lane & 31));
       asm volatile("" : "+v"(zrow));  // per-pass base of the dZ stores (no hoisted 64-bit addresses)
-      float tv[2][16];
-      auto load_t = [&](int j, float (&dst)[16]) {
-        const uint32_t gc4 = 4u * (uint32_t)(n0 + j * 32 + (lane & 31));
+      LFrag<D> lf;                      // A fragments first in the memory queue, then M~
+      logits_load<D>(p, (p.row0 + t0 + rb) / 32, lf);
+      float tv[NJ][16];
+      if constexpr (!FIX) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          dst[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mt_rs, roff[r] + gc4, 0, 0));
-      };
-      if constexpr (!FIX) load_t(0, tv[0]);
+        for (int j = 0; j < NJ; ++j) {
+          const uint32_t gc4 = 4u * (uint32_t)(n0 + j * 32 + (lane & 31));
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            tv[j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mt_rs, roff[r] + gc4, 0, 0));
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16_t acc[NJ];
+      logits_mfma<D>(Wt, lf, bias, acc);
+      KL_PROBE(2 + 2 * ps);
       bool deadp = false;   // an element of this pass has p < 1e-7
+      float mn = 1.f;       // (fast path) the smallest p of the lane's elements
+      // wave-uniform: every row of the wave is a real regulariser row (no padding)
+      bool rows_ok = true;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) rows_ok &= roff[r] < 0x80000000u;
+      rows_ok = __ballot(!rows_ok) == 0ull;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int col = j * 32 + (lane & 31);
-        if constexpr (!FIX) {
-          if (j + 1 < NJ) load_t(j + 1, tv[(j + 1) & 1]);
-        }
         uint16_t tt[16];
+        // the common case — all rows real, all 32 columns inside V: no per-element masks, the
+        // clip of q folded into one med3 (ln clip(p, 1e-7, 1) = med3(ln p, ln 1e-7, 0)), the
+        // dead-element test as a running min of p
+        const bool fast = !FIX && rows_ok && __ballot(!valid[j]) == 0ull;
+        if (fast) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int lr = rb + acc_row(r, lane);
-          const float4 st = sm.rs[lr];
-          const bool live_row = roff[r] < 0x80000000u && valid[j];
-          const float lp = acc[j][r] - st.x - st.y;  // ln p = z - m - ln s
-          const float pr = __builtin_amdgcn_exp2f(lp * LOG2E);
-          const bool live = pr >= PMIN;
-          float dz;
-          if constexpr (!FIX) {
-            const float tc = __builtin_amdgcn_fmed3f(tv[j & 1][r], PMIN, 1.f);
-            const float lq = live ? fminf(lp, 0.f) : LN_PMIN;  // ln clip(p, 1e-7, 1)
-            const float term = tc * fmaf(__builtin_amdgcn_logf(tc), LN2, -lq);
-            klsum += live_row ? term : 0.f;
-            deadp |= live_row && !live;
-            dz = live_row ? scale * (pr * st.z - (live ? tc : 0.f)) : 0.f;
-          } else {
-            dz = live_row ? -scale * pr * st.z : 0.f;  // st.z = delta
-          }
-          const uint32_t zoff = 2u * (zrow + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V + j * 32));
-          uint16_t zb;
-          if constexpr (FIX) {
-            const float old = valid[j] ? bf2f(p.dZ[zoff / 2]) : 0.f;
-            zb = bf16_bits(old + dz);
-            dz = __uint_as_float((uint32_t)zb << 16) - old;  // the change actually applied
-            tt[r] = bf16_bits(dz);
-          } else {
-            zb = bf16_bits(dz);
+          for (int r = 0; r < 16; ++r) {
+            const float4 st = sm.rs[rb + acc_row(r, lane)];
+            const float lp = acc[j][r] - st.x - st.y;  // ln p = z - m - ln s
+            const float pr = __builtin_amdgcn_exp2f(lp * LOG2E);
+            const float tc = __builtin_amdgcn_fmed3f(tv[j][r], PMIN, 1.f);
+            klsum = fmaf(tc, fmaf(__builtin_amdgcn_logf(tc), LN2, -__builtin_amdgcn_fmed3f(lp, LN_PMIN, 0.f)), klsum);
+            mn = fminf(mn, pr);
+            const uint16_t zb = bf16_bits(scale * fmaf(pr, st.z, pr >= PMIN ? -tc : 0.f));
             tt[r] = zb;
+            cs[j] += __uint_as_float((uint32_t)zb << 16);
+            const uint32_t zoff = 2u * (zrow + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V + j * 32));
+            __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, 0);
           }
-          cs[j] += __uint_as_float((uint32_t)tt[r] << 16);
-          if (valid[j]) __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, 0);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int lr = rb + acc_row(r, lane);
+            const float4 st = sm.rs[lr];
+            const bool live_row = roff[r] < 0x80000000u && valid[j];
+            const float lp = acc[j][r] - st.x - st.y;  // ln p = z - m - ln s
+            const float pr = __builtin_amdgcn_exp2f(lp * LOG2E);
+            const bool live = pr >= PMIN;
+            float dz;
+            if constexpr (!FIX) {
+              const float tc = __builtin_amdgcn_fmed3f(tv[j][r], PMIN, 1.f);
+              const float lq = live ? fminf(lp, 0.f) : LN_PMIN;  // ln clip(p, 1e-7, 1)
+              const float term = tc * fmaf(__builtin_amdgcn_logf(tc), LN2, -lq);
+              klsum += live_row ? term : 0.f;
+              deadp |= live_row && !live;
+              dz = live_row ? scale * (pr * st.z - (live ? tc : 0.f)) : 0.f;
+            } else {
+              dz = live_row ? -scale * pr * st.z : 0.f;  // st.z = delta
+            }
+            const uint32_t zoff = 2u * (zrow + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V + j * 32));
+            uint16_t zb;
+            if constexpr (FIX) {
+              const float old = valid[j] ? bf2f(p.dZ[zoff / 2]) : 0.f;
+              zb = bf16_bits(old + dz);
+              dz = __uint_as_float((uint32_t)zb << 16) - old;  // the change actually applied
+              tt[r] = bf16_bits(dz);
+            } else {
+              zb = bf16_bits(dz);
+              tt[r] = zb;
+            }
+            cs[j] += __uint_as_float((uint32_t)tt[r] << 16);
+            if (valid[j]) __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, 0);
+          }
         }
 #pragma unroll
         for (int g = 0; g < 4; ++g)
           *reinterpret_cast<uint2 *>(sm.Zt + sw_off(col, rb + 8 * g + 4 * half, CHB)) =
               *reinterpret_cast<const uint2 *>(&tt[4 * g]);
       }
+      deadp |= mn < PMIN;
+      KL_PROBE(3 + 2 * ps);
       if constexpr (!FIX) dead |= deadp;
     }
     __syncthreads();
+    KL_PROBE(6);
     // ---- phase 2: dWo[d][NB] (+)= D3^T[d][tile rows] dZ[tile rows][NB] (wave w: d rows 32w..).
     // A fresh accumulator per tile, added into gW (the block's slice stays L2-resident between
     // tiles): nothing of phase 2 is live across phase 1's epilogue.
@@ -381,18 +441,19 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
       // K = the tile's rows (a multiple of 32) in chunks of 32 (two 16-row fragments), a ring of
-      // two chunks in flight
+      // P2 chunks in flight (the loads come from L2: one chunk's 6 MFMAs cannot cover one latency)
+      constexpr int P2 = 6;
       const int nc = nt / 32;
       const int j0 = (p.row0 + t0) / 16;
       const bf16_t *arow = p.D3tp + ((int64_t)w * (p.ldt / 16) * 64 + lane) * 8 + (int64_t)j0 * 512;
-      bf16x8_t ring[2][2];
+      bf16x8_t ring[P2][2];
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+      for (int q = 0; q < P2; ++q)
 #pragma unroll
         for (int h = 0; h < 2; ++h) ring[q][h] = *reinterpret_cast<const bf16x8_t *>(arow + (2 * min(q, nc - 1) + h) * 512);
-      for (int c0 = 0; c0 < nc; c0 += 2) {
+      for (int c0 = 0; c0 < nc; c0 += P2) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < P2; ++q) {
           const int c = c0 + q;
           if (c < nc) {
 #pragma unroll
@@ -402,7 +463,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
                 const bf16x8_t b = frag(sm.Zt, sw_off(j * 32 + (lane & 31), c * 32 + h * 16 + 8 * half, CHB));
                 acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[q][h], b, acc2[j], 0, 0, 0);
               }
-            const int cn = min(c + 2, nc - 1);
+            const int cn = min(c + P2, nc - 1);
 #pragma unroll
             for (int h = 0; h < 2; ++h) ring[q][h] = *reinterpret_cast<const bf16x8_t *>(arow + (2 * cn + h) * 512);
           }
@@ -425,6 +486,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
     }
   }
 
+  KL_PROBE(7);
   // ---- epilogue: dbo, loss partial, the fix flag
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
