@@ -1,0 +1,168 @@
+// Decoder dX product, split-K with an LDS-DMA pipeline: P[s][M][N] = A[M][k in split s] . B[N][..]^T,
+// A = dZ [M][lda] bf16 (the output-layer gradient, K = |V|), B = Wo [N][ldb] bf16 (the reconstruct
+// kernel as stored, [d][V]: k-contiguous) — the Dense(V) input gradient of model.py:64 inside fit.
+//
+// The shape (M = 512 rows, N = d = 256, K = 22,000) gives 8 output tiles of 128 x 128, so the chip
+// is filled by splitting K (32 splits: 256 workgroups, ~11 K-tiles each).  With so few K-tiles per
+// workgroup the register-staged NT kernel (gemm.hip) never reaches a steady state: its 2-3 tiles
+// in flight do not cover one L2/MALL round trip.  Here every K-tile (A 128 x 64 + B 128 x 64 bf16,
+// 32 KB) is copied global -> LDS by buffer_load_dwordx4 ... lds (no VGPR staging), four LDS stages
+// deep (three tiles in flight while the fourth is multiplied), counted vmcnt waits and raw
+// s_barrier (a __syncthreads would drain the DMA queue).  The LDS images are lane-linear per wave
+// instruction (8 rows x 128 B); the 16-B chunk XOR swizzle (chunk ^ row & 7) is applied on the
+// global source address.  k >= kend chunks point past the buffer's range: the DMA writes zeros.
+// (tile, split) pairs are dealt split-major over the 8 XCDs so a split's A and B panels are
+// fetched into one XCD's L2 once.  The split partials are summed by cc_splitk_reduce.
+#include "common.hpp"
+
+namespace {
+
+constexpr int XBM = 128, XBN = 128, XBK = 64, XST = 4, XNT = 256;
+constexpr int XTILE_BYTES = (XBM + XBN) * XBK * 2;  // one stage: A then B, 32 KB
+constexpr int XLDS = XST * XTILE_BYTES;             // 128 KB
+
+__device__ __forceinline__ int xcd_remap(int b, int nb) {  // bijective blocks -> XCD-contiguous ids
+  const int q = nb / 8, r = nb % 8, x = b % 8, slot = b / 8;
+  return x < r ? x * (q + 1) + slot : r * (q + 1) + (x - r) * q + slot;
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+struct DxP {
+  const bf16_t *A, *B;
+  float *P;
+  int M, N, K, lda, ldb, splits, kchunk, tiles_m;
+  uint32_t a_bytes, b_bytes;
+};
+
+// issue the DMA of K-tile (k0) into stage buffer st: wave w moves A rows [32w, 32w+32) and B rows
+// [32w, 32w+32) as 4 + 4 instructions of 8 rows x 128 B
+__device__ __forceinline__ void dma_tile(const DxP &p, const __amdgpu_buffer_rsrc_t &ra,
+                                         const __amdgpu_buffer_rsrc_t &rb, char *smem, int st, int bm,
+                                         int bn, int k0, int kend) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int rl = lane >> 3, slot = lane & 7;
+  char *sa = smem + st * XTILE_BYTES, *sb = sa + XBM * XBK * 2;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = w * 4 + u;       // instruction index: rows 8i .. 8i + 7
+    const int row = 8 * i + rl;
+    const int c = slot ^ (row & 7);
+    const int k = k0 + 8 * c;
+    const uint32_t oa = k < kend ? (uint32_t)(((bm + row) * p.lda + k) * 2) : 0x80000000u;
+    const uint32_t ob = k < kend ? (uint32_t)(((bn + row) * p.ldb + k) * 2) : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void *)(sa + i * 1024), 16, oa, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void *)(sb + i * 1024), 16, ob, 0, 0, 0);
+  }
+}
+
+template <int N_OUT>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N_OUT == 16)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if constexpr (N_OUT == 8)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ bf16x8_t frag(const char *s, int row, int c) {  // 16 B: row, k-chunk c
+  return *reinterpret_cast<const bf16x8_t *>(s + row * 128 + ((c ^ (row & 7)) << 4));
+}
+
+__global__ __launch_bounds__(XNT) void dx_splitk_kernel(DxP p) {
+  __shared__ __attribute__((aligned(1024))) char smem[XLDS];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5;
+  const int wm = w >> 1, wn = w & 1;
+  const int ntiles = p.tiles_m * (p.N / XBN);
+  const int q = xcd_remap(blockIdx.x, ntiles * p.splits);
+  const int split = q / ntiles, tile = q % ntiles;
+  const int bm = (tile % p.tiles_m) * XBM, bn = (tile / p.tiles_m) * XBN;
+  const int kbeg = split * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
+  const int nk = kbeg < kend ? (kend - kbeg + XBK - 1) / XBK : 0;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void *)p.A, (short)0, p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void *)p.B, (short)0, p.b_bytes, 0x00020000);
+  f32x16_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // prologue: XST - 1 tiles in flight
+#pragma unroll
+  for (int s = 0; s < XST - 1; ++s)
+    if (s < nk) dma_tile(p, ra, rb, smem, s, bm, bn, kbeg + s * XBK, kend);
+  const int ar = wm * 64 + (lane & 31), br = wn * 64 + (lane & 31);
+  for (int t = 0; t < nk; ++t) {
+    // tile t landed in every wave (own DMAs counted, then the barrier); 8 DMA instructions per
+    // wave per tile, min(2, nk - 1 - t) tiles issued after t may stay in flight
+    const int after = min(XST - 2, nk - 1 - t);
+    if (after >= 2)
+      wait_vm<16>();
+    else if (after == 1)
+      wait_vm<8>();
+    else
+      wait_vm<0>();
+    __builtin_amdgcn_s_barrier();   // raw barrier: a __syncthreads fence would drain the DMA queue
+    asm volatile("" ::: "memory");  // no LDS read or DMA issue moves across it
+    // every wave finished reading buffer (t - 1) % XST in iteration t - 1: refill it with t + 3
+    if (t + XST - 1 < nk) dma_tile(p, ra, rb, smem, (t + XST - 1) % XST, bm, bn, kbeg + (t + XST - 1) * XBK, kend);
+    const char *sa = smem + (t % XST) * XTILE_BYTES, *sb = sa + XBM * XBK * 2;
+#pragma unroll
+    for (int kk = 0; kk < XBK / 16; ++kk) {
+      const int c = 2 * kk + half;
+      const bf16x8_t a0 = frag(sa, ar, c), a1 = frag(sa, ar + 32, c);
+      const bf16x8_t b0 = frag(sb, br, c), b1 = frag(sb, br + 32, c);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+    }
+  }
+  // partial tile -> P[split][M][N] (lanes 0..31 of a half: 32 consecutive columns of one row)
+  float *out = p.P + (int64_t)split * p.M * p.N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = bn + wn * 64 + j * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = bm + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        out[(int64_t)row * p.N + col] = acc[i][j][r];
+      }
+    }
+}
+
+}  // namespace
+
+extern "C" int cc_gemm_dx_splitk(const void *A, int32_t lda, const void *B, int32_t ldb, int32_t M, int32_t N,
+                                 int32_t K, int32_t splits, float *partials, void *stream) {
+  CC_REQUIRE(A && B && partials, "cc_gemm_dx_splitk: null pointer");
+  CC_REQUIRE(M > 0 && N > 0 && M % XBM == 0 && N % XBN == 0, "cc_gemm_dx_splitk: M, N multiples of 128");
+  CC_REQUIRE(K > 0 && K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K,
+             "cc_gemm_dx_splitk: K, lda, ldb multiples of 8, lda/ldb >= K");
+  CC_REQUIRE(splits >= 1 && splits <= 1024, "cc_gemm_dx_splitk: splits 1..1024");
+  CC_REQUIRE((int64_t)M * lda * 2 < 0x80000000ll && (int64_t)N * ldb * 2 < 0x80000000ll,
+             "cc_gemm_dx_splitk: operands must stay below 2 GB (32-bit buffer offsets)");
+  CC_REQUIRE((((uintptr_t)A | (uintptr_t)B) & 15) == 0, "cc_gemm_dx_splitk: operands 16-B aligned");
+  DxP p;
+  p.A = (const bf16_t *)A;
+  p.B = (const bf16_t *)B;
+  p.P = partials;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = lda;
+  p.ldb = ldb;
+  p.splits = splits;
+  p.kchunk = (int)cdiv(cdiv(K, splits), XBK) * XBK;
+  p.tiles_m = M / XBM;
+  p.a_bytes = (uint32_t)((int64_t)M * lda * 2);
+  p.b_bytes = (uint32_t)((int64_t)N * ldb * 2);
+  const int nb = (M / XBM) * (N / XBN) * splits;
+  hipLaunchKernelGGL(dx_splitk_kernel, dim3((unsigned)nb), dim3(XNT), 0, as_stream(stream), p);
+  CC_LAUNCH_CHECK("dx_splitk_kernel");
+  return CC_OK;
+}

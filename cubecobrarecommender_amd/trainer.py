@@ -247,7 +247,7 @@ class Trainer:
         self.gH2 = torch.zeros(R, 256, **T)
         self.gPre1 = torch.zeros(R, d, **f32)
         self.Z2 = None             # materialised fp32 D2 logits (the unfused regulariser path only)
-        self.splits = max(1, min(32, V // 512))            # decoder dX: K = V (32: 22.4 us vs 29.5 at 16)
+        self.splits = max(1, min(int(os.environ.get('CCREC_DX_SPLITS', '32')), V // 512))   # decoder dX: K = V
         # the regulariser branch's dX: M = Breg rows; with thousands of rows (full mode) the output
         # tiles alone fill the chip — no split-K
         self.splits_reg = self.splits if self.Breg <= 1024 else 1
@@ -268,6 +268,8 @@ class Trainer:
         self.embed_mfma = (self.dtype == L.CC_BF16 and self.fused_tower and d % 128 == 0 and self.xt_rows <= 2048
                            and os.environ.get('CCREC_EMBED_MFMA', '1') != '0')
         self.RP = (R + 63) // 64 * 64
+        # decoder dX on the LDS-DMA pipelined split-K kernel (dxgemm.hip; CCREC_DX_GLDS=0: gemm.hip's)
+        self.dx_glds = self.dtype == L.CC_BF16 and os.environ.get('CCREC_DX_GLDS', '1') != '0'
         # D1 output layer fused (logits + BCE + dZ + dWo, csrc/decout.hip) where its shape fits
         self.fused_out = (self.dtype == L.CC_BF16 and self.fused_tower and not self.mx8 and d in (128, 256)
                           and B in (128, 256, 512) and os.environ.get('CCREC_DEC_FUSED', '1') != '0')
@@ -746,13 +748,13 @@ class Trainer:
                                 epi=L.CC_EPI_SPLITK, Cf=L.ptr(self.split_buf), splits=splits,
                                 launch=False)
                 if k == 1 and self.fused_reg:   # dWo/dbo came out of cc_dec_softmax_kl_dw: dX only
-                    L.call('cc_gemm', L.C.byref(gx), s)
+                    self._dx(gx, r0, nr, splits, pre, s)
                     L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), splits, nr, d,
                            L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
                     continue
                 if k == 0 and self.fused_out:   # dWo/dbo came out of cc_dec_bce_dw: dX only
                     t = self._tick('dec_dX')
-                    L.call('cc_gemm', L.C.byref(gx), s)
+                    self._dx(gx, r0, nr, splits, pre, s)
                     t()
                     wb = self.wpack[1] if self.wpack is not None else None   # warm the tower bwd's weights
                     L.call('cc_splitk_reduce_warm', self.dtype, L.ptr(self.split_buf), splits, nr, d,
@@ -790,6 +792,16 @@ class Trainer:
             self._dense_bwd(self.D1, self.gD2, rows, 128, 256, pre + '/decoded_2', gIn=self.gD1, mask=self.D1)
             self._dense_bwd(self.Zl, self.gD1, rows, 64, 128, pre + '/decoded_1', gIn=self.gZl, mask=self.Zl)
         self._join()
+
+    def _dx(self, gx, r0, nr, splits, pre, s):
+        """Decoder dX split-K partials into split_buf: the LDS-DMA pipelined kernel (dxgemm.hip)
+        on the bf16 shapes it takes, else cc_gemm's register-staged NT path (same partials)."""
+        d, V = self.cfg.d, self.cfg.V
+        if (self.dx_glds and not self.mx8 and nr % 128 == 0 and d % 128 == 0 and V % 8 == 0):
+            L.call('cc_gemm_dx_splitk', L.ptr(self.dZout[r0:]), V, self.w(pre + '/reconstruct/kernel'), V,
+                   nr, d, V, splits, L.ptr(self.split_buf), s)
+        else:
+            L.call('cc_gemm', L.C.byref(gx), s)
 
     # operands of the decoder output-layer products (branch k, rows [r0, r0 + B)): bf16 NT images
     # (D3, Wo^T, dZ, Wo, D3^T, dZ^T) or their MX-FP8 codes + E8M0 scales

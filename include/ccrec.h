@@ -390,6 +390,12 @@ int32_t cc_dec_kl_blocks(int32_t V);
 int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream);
 /* tsum[i] = sum_j clip(Mt[i * V + j], 1e-7, 1) for the n rows of Mt (once per M~) */
 int cc_kl_tsum(const float *Mt, int32_t n, int32_t V, float *tsum, void *stream);
+/* Decoder dX split-K on bf16 MFMA with an LDS-DMA pipeline (dxgemm.hip): partials[s][M][N] =
+ * A[M][k in split s] . B[N][k in split s]^T, A [M][lda] (dZ), B [N][ldb] (Wo as [d][V]), splits of
+ * ceil64(ceil(K / splits)) — the same partials (and split boundaries) as cc_gemm's EPI_SPLITK NT
+ * path; reduce with cc_splitk_reduce.  M, N multiples of 128, K % 8 == 0, operands < 2 GB. */
+int cc_gemm_dx_splitk(const void *A, int32_t lda, const void *B, int32_t ldb, int32_t M, int32_t N,
+                      int32_t K, int32_t splits, float *partials, void *stream);
 /* loss_out[0] = sum(partials[0:n]) * scale (fixed order, fp64) */
 int cc_reduce_loss(const double *partials, int32_t n, double scale, double *loss_out, void *stream);
 

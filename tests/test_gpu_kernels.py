@@ -484,3 +484,24 @@ def test_embed_grad_packed_bit_exact(V, R):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     want = X.T.astype(np.float64) @ g.double().cpu().numpy()
     assert rel_err(outs[1][0].numpy(), want) < 1e-5
+
+
+@pytest.mark.parametrize('M,N,K,splits', [(512, 256, 22000, 32), (640, 128, 1000, 7), (128, 256, 64, 1),
+                                          (256, 256, 5008, 3)])
+def test_dx_splitk_glds_matches_nt_gemm(M, N, K, splits):
+    """cc_gemm_dx_splitk (LDS-DMA pipeline, dxgemm.hip) == cc_gemm's register-staged NT split-K path:
+    the same split boundaries and the same MFMA chain order, so the fp32 partials agree bit for bit;
+    ragged K (a K-tile past the end is zero-filled by the buffer range check) included."""
+    rng = np.random.default_rng(M + K)
+    A = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32)).to(torch.bfloat16).cuda()
+    Bm = torch.from_numpy(rng.standard_normal((N, K)).astype(np.float32)).to(torch.bfloat16).cuda()
+    p1 = torch.full((splits, M, N), 7.0, device='cuda')
+    p0 = torch.zeros(splits, M, N, device='cuda')
+    g = L.GemmArgs(dtype=L.CC_BF16, ta=0, tb=1, epilogue=L.CC_EPI_SPLITK, M=M, N=N, K=K, lda=K, ldb=K, ldc=N,
+                   splits=splits, A=L.ptr(A), B=L.ptr(Bm), Cf=L.ptr(p0))
+    L.call('cc_gemm', ctypes.byref(g), L.stream_ptr())
+    L.call('cc_gemm_dx_splitk', L.ptr(A), K, L.ptr(Bm), K, M, N, K, splits, L.ptr(p1), L.stream_ptr())
+    torch.cuda.synchronize()
+    want = (A.float() @ Bm.float().t()).cpu().numpy()
+    assert rel_err(p1.sum(0).cpu().numpy(), want) < 1e-5
+    np.testing.assert_array_equal(p1.cpu().numpy(), p0.cpu().numpy())

@@ -1,3 +1,5 @@
 cd $GRAFT_REPO_ROOT
-timeout -k 10 600 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_fullsize.py tests/test_gpu_dp.py -x -q --timeout 200 --timeout-method thread -k "fused_regulariser or full_mode or bench_config or match_oracle or sharded" > gpurun_out/t.log 2>&1; rc=$?; tail -3 gpurun_out/t.log; [ $rc -ne 0 ] && exit $rc
-bash tools/prof_micro.sh r02n tools/micro/kl_micro.py | head -6
+for sp in 16 24 32 48; do
+  CCREC_DX_SPLITS=$sp timeout -k 10 200 python bench.py --steps 100 --no-cpu-baseline --no-recommend > gpurun_out/sp$sp.log 2>&1 || exit 1
+  tail -1 gpurun_out/sp$sp.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print($sp, round(d['ms_per_step']*1e3,1), d['kernel_us']['dec_dX'])"
+done
