@@ -90,6 +90,25 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   const int VW = (V + 31) >> 5;
 
   DEC_PROBE(0);
+  // pass 0's A fragments first: their L2 round trip overlaps the resident staging below
+  bf16x8_t af[2][nkk];
+  auto load_a = [&](bf16x8_t (&dst)[nkk], int pass) {
+    if (p.D3p) {  // fragment (row block, kk) = 1 KB contiguous: whole cache lines per wave load
+      const int rb = min(pass * 8 + w, B / 32 - 1);
+      const bf16_t *src = p.D3p + ((int64_t)rb * nkk * 64 + lane) * 8;
+#pragma unroll
+      for (int kk = 0; kk < nkk; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 512);
+    } else {
+      const int row = min(pass * 256 + w * 32 + (lane & 31), B - 1);
+      const bf16_t *src = p.D3 + (int64_t)row * d + 8 * half;
+#pragma unroll
+      for (int kk = 0; kk < nkk; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 16);
+    }
+    // keep the whole batch in flight: without this fence the scheduler sinks each load to its
+    // MFMA and the pass becomes a chain of dependent L2 round trips
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  load_a(af[0], 0);
   // ---- resident operands: Wo^T slice (rows clamped at the edge: they feed masked columns only)
   // and the target bits; every load of the batch issued before the first LDS store
   {
@@ -178,27 +197,14 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     bias[j] = valid[j] ? p.bo[gc] : 0.f;
     cs[j] = 0.f;
   }
-  bf16x8_t af[2][nkk];
-  auto load_a = [&](bf16x8_t (&dst)[nkk], int pass) {
-    if (p.D3p) {  // fragment (row block, kk) = 1 KB contiguous: whole cache lines per wave load
-      const int rb = min(pass * 8 + w, B / 32 - 1);
-      const bf16_t *src = p.D3p + ((int64_t)rb * nkk * 64 + lane) * 8;
-#pragma unroll
-      for (int kk = 0; kk < nkk; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 512);
-    } else {
-      const int row = min(pass * 256 + w * 32 + (lane & 31), B - 1);
-      const bf16_t *src = p.D3 + (int64_t)row * d + 8 * half;
-#pragma unroll
-      for (int kk = 0; kk < nkk; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 16);
-    }
-    // keep the whole batch in flight: without this fence the scheduler sinks each load to its
-    // MFMA and the pass becomes a chain of dependent L2 round trips
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  load_a(af[0], 0);
-  __syncthreads();
+  // LDS-only barrier: __syncthreads would also wait for pass 0's A fragments (vmcnt counts loads)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   DEC_PROBE(1);
   const float scale = p.scale;
+  // dZ and gW through buffer descriptors: a 32-bit byte offset per store instead of a 64-bit
+  // address (dZ = B x V x 2 B and gW = d x V x 4 B stay below 4 GB: checked on the host)
+  const __amdgpu_buffer_rsrc_t dz_rs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)B * (uint32_t)V * 2u, 0x00020000);
 #pragma unroll
   for (int ps = 0; ps < npass; ++ps) {
     if (ps + 1 < npass) load_a(af[(ps + 1) & 1], ps + 1);
@@ -228,7 +234,8 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         // a = exp(-|z|) once; log1p and 1/(1+a) from it.  The 16 factors 1 + a in (1, 2] of a
         // lane's column are multiplied (<= 2^16) and one log2 per column taken: the log is a
         // quarter-rate instruction; summed log2 scaled by ln 2 at the end
-        bf16_t *dst = p.dZ + (int64_t)(rb + 4 * half) * V + n0 + col;
+        uint32_t zrow = (uint32_t)((rb + 4 * half) * V + n0 + col);
+        asm volatile("" : "+v"(zrow));  // per column tile: no hoisted per-row store addresses
         float lprod = 1.f;
         // the 16 rows' target words: 4 runs of 4 consecutive rows -> 4 LDS reads of 16 B
         uint4 yw[4];
@@ -248,7 +255,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
           const uint16_t zb = bf16_bits(fmaf(sig, scale, yb ? -scale : 0.f));
           tt[r] = zb;
           cs[j] += __uint_as_float((uint32_t)zb << 16);
-          dst[(int64_t)((r & 3) + 8 * (r >> 2)) * V] = zb;
+          __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, 2u * (zrow + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V)), 0, 0);
         }
         lsum += __builtin_amdgcn_logf(lprod);
       } else {
@@ -270,52 +277,40 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     const float c2 = cs[j] + __shfl_xor(cs[j], 32);
     if (half == 0) red_cs[w][j * 32 + (lane & 31)] = c2;
   }
-  // loss: block partial, published before phase 2's stores
   float lossf = rsum + lsum * LN2;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) lossf += __shfl_xor(lossf, off);
   if (lane == 0) red_loss[w] = (double)lossf;
-  __syncthreads();   // dZ^T image, red_cs, red_loss complete
+  // phase 2's first A fragments in flight before the barrier.  The barrier waits for LDS only:
+  // __syncthreads' release fence would also drain every wave's dZ stores (vmcnt(0), ~4 us), and
+  // nothing below reads them.
+  constexpr int P2D = 4;
+  constexpr int nk2 = B / BK;
+  // A fragment (kc, kk): row-strided from D3^T, or 1 KB contiguous from the packed image
+  const bool pk = p.D3tp != nullptr;
+  const bf16_t *arow = pk ? p.D3tp + ((int64_t)min(w, d / 32 - 1) * (p.ldt / 16) * 64 + lane) * 8
+                          : p.D3t + (int64_t)(min(w, d / 32 - 1) * 32 + (lane & 31)) * p.ldt + 8 * half;
+  auto afrag = [&](int kc, int kk) {
+    return *reinterpret_cast<const bf16x8_t *>(arow + (pk ? (kc * 4 + kk) * 512 : kc * BK + kk * 16));
+  };
+  bf16x8_t ring[P2D][4];
+#pragma unroll
+  for (int q = 0; q < P2D; ++q)
+    if (q < nk2)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) ring[q][kk] = afrag(q, kk);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // dZ^T image, red_cs, red_loss
   DEC_PROBE(6);
   if (tid < NB && n0 + tid < V) {
     float g = 0.f;
     for (int i = 0; i < NTH / 64; ++i) g += red_cs[i][tid];
     p.gb[n0 + tid] = g;
   }
-  if (tid == 0) {
-    double sum = 0.0;
-    for (int i = 0; i < NTH / 64; ++i) sum += red_loss[i];
-    lastflag = 0;
-    if (!p.loss_out) {
-      p.loss_partials[blockIdx.x] = sum;
-    } else {
-      __hip_atomic_store(&p.loss_partials[blockIdx.x], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint32_t tk = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      lastflag = tk == gridDim.x - 1;
-    }
-  }
 
   // ---- phase 2: dWo[d][NB] = D3^T[d][B] . dZ[B][NB].  Wave w owns rows 32w .. +32 of d (waves
   // beyond d idle) and all NB columns; A fragments from global through a ring P2D chunks of 64 k
   // deep, B fragments from the dZ^T image.
   if (w * 32 < d) {
-    constexpr int P2D = 4;
-    constexpr int nk2 = B / BK;
-    // A fragment (kc, kk): row-strided from D3^T, or 1 KB contiguous from the packed image
-    const bool pk = p.D3tp != nullptr;
-    const bf16_t *arow = pk ? p.D3tp + ((int64_t)w * (p.ldt / 16) * 64 + lane) * 8
-                            : p.D3t + (int64_t)(w * 32 + (lane & 31)) * p.ldt + 8 * half;
-    auto afrag = [&](int kc, int kk) {
-      return *reinterpret_cast<const bf16x8_t *>(arow + (pk ? (kc * 4 + kk) * 512 : kc * BK + kk * 16));
-    };
-    bf16x8_t ring[P2D][4];
-#pragma unroll
-    for (int q = 0; q < P2D; ++q)
-      if (q < nk2)
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) ring[q][kk] = afrag(q, kk);
-    __builtin_amdgcn_sched_barrier(0);
     f32x16_t acc2[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -339,17 +334,36 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
       }
     }
     DEC_PROBE(7);
+    const __amdgpu_buffer_rsrc_t gw_rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)p.gW, (short)0, (uint32_t)d * (uint32_t)V * 4u, 0x00020000);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int gc2 = n0 + j * 32 + (lane & 31);
       if (gc2 < V) {
-        float *g = p.gW + (int64_t)(w * 32 + 4 * half) * V + gc2;
+        uint32_t g0 = (uint32_t)((w * 32 + 4 * half) * V + gc2);
+        asm volatile("" : "+v"(g0));
 #pragma unroll
-        for (int r = 0; r < 16; ++r) g[(int64_t)((r & 3) + 8 * (r >> 2)) * V] = acc2[j][r];
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc2[j][r]), gw_rs,
+                                                4u * (g0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V)), 0, 0);
       }
     }
   }
 
+  // loss: the block partial, published after phase 2's stores (the ticket's vmcnt(0) drains them)
+  if (tid == 0) {
+    double sum = 0.0;
+    for (int i = 0; i < NTH / 64; ++i) sum += red_loss[i];
+    lastflag = 0;
+    if (!p.loss_out) {
+      p.loss_partials[blockIdx.x] = sum;
+    } else {
+      __hip_atomic_store(&p.loss_partials[blockIdx.x], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t tk = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lastflag = tk == gridDim.x - 1;
+    }
+  }
   DEC_PROBE(8);
   // ---- the last block reduces the loss partials in block order
   if (p.loss_out) {
@@ -384,6 +398,7 @@ extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const
   CC_REQUIRE(B == 128 || B == 256 || B == 512, "cc_dec_bce_dw: B must be 128, 256 or 512");
   CC_REQUIRE(d == 128 || d == 256, "cc_dec_bce_dw: d must be 128 or 256");
   CC_REQUIRE(V > 0 && ldt >= B && ldt % 8 == 0, "cc_dec_bce_dw: V > 0, ldt >= B, ldt % 8 == 0");
+  CC_REQUIRE((int64_t)d * V * 4 <= 0xFFFFFFFFll, "cc_dec_bce_dw: dWo below 4 GB (32-bit buffer offsets)");
   CC_REQUIRE(!loss_out || ticket, "cc_dec_bce_dw: loss_out needs a ticket word");
   CC_REQUIRE((((uintptr_t)D3 | (uintptr_t)D3t | (uintptr_t)WoT | (uintptr_t)Wo) & 15) == 0,
              "cc_dec_bce_dw: operands 16-B aligned");

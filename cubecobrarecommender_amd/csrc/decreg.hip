@@ -12,9 +12,10 @@
 //          KL += t (ln t - ln clip(p, 1e-7, 1)), dz = scale (p S - [p >= 1e-7] t) written row-major
 //          for the dX product and kept as dZ^T in LDS -> dWo[d][96] = D3^T dZ, dbo = colsum
 //   fix    TF's gradient passes through clip only where p >= 1e-7, so the exact S is
-//          S - delta, delta = sum_{p < 1e-7} t.  The main kernel raises a flag when any element of
-//          the step has p < 1e-7; two fix kernels (delta partials, then dz -= scale p delta with the
-//          matching dWo / dbo corrections) run only then — otherwise they exit at once.
+//          S - delta, delta = sum_{p < 1e-7} t.  The main kernel writes each (row, slice)'s delta
+//          partial (zero unless a wave saw such an element) and raises a flag; the fix kernel
+//          (dz -= scale p delta with the matching dWo / dbo corrections) runs only then —
+//          otherwise it exits at once.
 //
 // Padding rows (reg_idx < 0, owner-computes capacity / full-mode round-up) contribute nothing.
 // bf16 MFMA v_mfma_f32_32x32x16_bf16 with fp32 accumulation; A operands from the packed D3 images
@@ -33,7 +34,6 @@ constexpr int NB = 96;       // V columns per block (230 slices at |V| = 22,000)
 constexpr int NJ = NB / 32;  // 32-column accumulator tiles per wave
 constexpr int NTH = 512;     // 8 waves
 constexpr int TR = 512;      // rows per tile of the main kernel (2 passes of 8 x 32)
-constexpr int SR = 256;      // rows per stats / fix-delta block
 constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
 constexpr float PMIN = 1e-7f;
 constexpr float LN_PMIN = -16.11809565095832f;  // ln(1e-7)
@@ -57,6 +57,11 @@ struct KlP {
   float4 *rowstat;                  // [rows] {m, ln s, S, -}
   uint32_t *flag;                   // [1] an element with p < 1e-7 was seen this step
 };
+
+// Workgroup barrier over LDS only.  __syncthreads' release fence also waits for every outstanding
+// global access of the wave (vmcnt(0): the dZ / dWo stores and in-flight loads) — not needed where
+// only LDS is handed between the waves.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 __device__ __forceinline__ int sw_off(int row, int k, int chunks) {
@@ -111,23 +116,23 @@ __device__ __forceinline__ void load_wo_slice(const bf16_t *__restrict__ Wo, int
 // z[32 rows][NB] = bo + D3[rows] Wo_slice for the wave's 32-row block rb (packed D3 image): the
 // A-fragment loads (logits_load, a ring of LRING) and the MFMAs (logits_mfma) are separate so a
 // caller can put other loads behind the fragments' in the memory queue
-template <int D>
+template <int D, int RG = (D / 16 < 8 ? D / 16 : 8)>
 struct LFrag {
-  static constexpr int nkk = D / 16, RING = nkk < 8 ? nkk : 8;
+  static constexpr int nkk = D / 16, RING = RG;
   bf16x8_t af[RING];
   const bf16_t *src;
 };
-template <int D>
-__device__ __forceinline__ void logits_load(const KlP &p, int rb, LFrag<D> &f) {
+template <int D, int RG>
+__device__ __forceinline__ void logits_load(const KlP &p, int rb, LFrag<D, RG> &f) {
   const int lane = threadIdx.x & 63;
-  f.src = p.D3p + ((int64_t)rb * LFrag<D>::nkk * 64 + lane) * 8;
+  f.src = p.D3p + ((int64_t)rb * LFrag<D, RG>::nkk * 64 + lane) * 8;
 #pragma unroll
-  for (int kk = 0; kk < LFrag<D>::RING; ++kk) f.af[kk] = *reinterpret_cast<const bf16x8_t *>(f.src + kk * 512);
+  for (int kk = 0; kk < RG; ++kk) f.af[kk] = *reinterpret_cast<const bf16x8_t *>(f.src + kk * 512);
 }
-template <int D>
-__device__ __forceinline__ void logits_mfma(const bf16_t *Wt, LFrag<D> &f, const float (&bias)[NJ],
+template <int D, int RG>
+__device__ __forceinline__ void logits_mfma(const bf16_t *Wt, LFrag<D, RG> &f, const float (&bias)[NJ],
                                             f32x16_t (&acc)[NJ]) {
-  constexpr int nkk = LFrag<D>::nkk, RING = LFrag<D>::RING, CHD = D / 8;
+  constexpr int nkk = LFrag<D, RG>::nkk, RING = RG, CHD = D / 8;
   const int lane = threadIdx.x & 63, half = lane >> 5;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -197,69 +202,108 @@ __device__ __forceinline__ float half_sum(float v) {
 }
 
 // ---------------------------------------------------------------- stats
+// z^T[96 cols][32 rows] per wave with the operands swapped (Wo slice = A, D3 rows = B): a lane holds
+// ONE row and 16 columns per 32-column tile, so the row's max / sum over the slice are lane-local
+// (+ one exchange between the lane halves).  Columns past V start at -inf (bias) and drop out of
+// both.  One block per slice stages its Wo slice once; its waves walk the 32-row blocks.
 template <int D>
-__global__ __launch_bounds__(NTH) void kl_stats_kernel(KlP p) {
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(1, 2))) void kl_stats_kernel(KlP p) {
   __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int CHD = D / 8;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5;
   const int sl = blockIdx.x, n0 = sl * NB;
-  const int r_blk = blockIdx.y * SR + w * 32;  // the wave's first row (regulariser-row index)
-  if (blockIdx.y == 0) KL_PROBE(8);
+  __shared__ __attribute__((aligned(16))) float bs[NB];   // the slice's bias, -inf past V
+  KL_PROBE(8);
+  if (sl == 0 && threadIdx.x == 0) *p.flag = 0u;  // this step's fix flag starts clear
+  if (threadIdx.x < NB) bs[threadIdx.x] = n0 + (int)threadIdx.x < p.V ? p.bo[n0 + threadIdx.x] : -INFINITY;
   load_wo_slice<D>(p.Wo, p.V, n0, Wt);
   __syncthreads();
-  if (blockIdx.y == 0) KL_PROBE(9);
-  if (r_blk >= p.rows) return;
-  float bias[NJ];
-  bool valid[NJ];
+  KL_PROBE(9);
+  // wave w walks the 32-row blocks w, w + 8, ...; the next block's fragments load during this one
+  const int nrb = p.rows / 32;
+  constexpr int nkk = D / 16;
+  bf16x8_t af[2][nkk];
+  auto load = [&](bf16x8_t (&dst)[nkk], int rb) {
+    const bf16_t *src = p.D3p + ((int64_t)((p.row0 + 32 * min(rb, nrb - 1)) / 32) * nkk * 64 + lane) * 8;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int gc = n0 + j * 32 + (lane & 31);
-    valid[j] = gc < p.V;
-    bias[j] = valid[j] ? p.bo[gc] : 0.f;
-  }
-  f32x16_t acc[NJ];
-  logits_block<D>(p, Wt, (p.row0 + r_blk) / 32, bias, acc);
-  // per-row max over the slice: lane-local over the NJ columns, then across the half-wave
-  float v[16];
+    for (int kk = 0; kk < nkk; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 512);
+  };
+  auto body = [&](const bf16x8_t (&cur)[nkk], int rb) {
+    f32x16_t acc[NJ];  // bias-initialised: registers 4g..4g+3 are columns 8g + 4 half .. +3
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 b = *reinterpret_cast<const float4 *>(bs + j * 32 + 8 * g + 4 * half);
+        acc[j][4 * g] = b.x;
+        acc[j][4 * g + 1] = b.y;
+        acc[j][4 * g + 2] = b.z;
+        acc[j][4 * g + 3] = b.w;
+      }
+#pragma unroll
+    for (int kk = 0; kk < nkk; ++kk)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const bf16x8_t a = frag(Wt, sw_off(j * 32 + (lane & 31), kk * 16 + 8 * half, CHD));
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, cur[kk], acc[j], 0, 0, 0);
+      }
+    if (rb == w) KL_PROBE(10);
     float m = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) m = valid[j] ? fmaxf(m, acc[j][r]) : m;
-    v[r] = m;
-  }
-  if (blockIdx.y == 0) KL_PROBE(10);
-  const float mr = rs16<true>(v);  // max of row (lane >> 1) & 15
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {   // broadcast each row's max back from lane 2r of the half
-    const float m = __shfl(mr, (lane & 32) + 2 * r);
+      for (int r = 0; r < 16; ++r) m = fmaxf(m, acc[j][r]);
+    m = fmaxf(m, __shfl_xor(m, 32));
     float e = 0.f;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) e += valid[j] ? __builtin_amdgcn_exp2f((acc[j][r] - m) * LOG2E) : 0.f;
-    v[r] = e;
-  }
-  const float sr = rs16<false>(v);
-  if (blockIdx.y == 0) KL_PROBE(11);
-  if ((lane & 1) == 0) {
-    const int rr = (lane >> 1) & 15;
-    const int row = r_blk + acc_row(rr, lane);
-    p.part_m[(int64_t)row * p.nsl + sl] = mr;
-    p.part_s[(int64_t)row * p.nsl + sl] = sr;
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) e += __builtin_amdgcn_exp2f((acc[j][r] - m) * LOG2E);
+    e += __shfl_xor(e, 32);
+    if (rb == w) KL_PROBE(11);
+    if (half == 0) {
+      const int row = 32 * rb + lane;
+      p.part_m[(int64_t)row * p.nsl + sl] = m;
+      p.part_s[(int64_t)row * p.nsl + sl] = e;
+    }
+  };
+  constexpr int W8 = NTH / 64;
+  load(af[0], w);
+  for (int rb = w; rb < nrb; rb += 2 * W8) {
+    if (rb + W8 < nrb) load(af[1], rb + W8);
+    __builtin_amdgcn_sched_barrier(0);
+    body(af[0], rb);
+    if (rb + W8 < nrb) {
+      if (rb + 2 * W8 < nrb) load(af[0], rb + 2 * W8);
+      __builtin_amdgcn_sched_barrier(0);
+      body(af[1], rb + W8);
+    }
   }
 }
 
 // ---------------------------------------------------------------- merge (one wave per row)
+// The row's slice partials are loaded once (MRG per lane in registers) — one memory round trip.
+constexpr int MRG = 8;  // nsl <= 512 (|V| <= 49,152): checked on the host
 __global__ __launch_bounds__(256) void kl_merge_kernel(KlP p) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *p.flag = 0u;  // this step's fix flag starts clear
   if (row >= p.rows) return;
   const float *pm = p.part_m + (int64_t)row * p.nsl, *ps = p.part_s + (int64_t)row * p.nsl;
+  float mv[MRG], sv[MRG];
+#pragma unroll
+  for (int q = 0; q < MRG; ++q) {
+    const int i = lane + 64 * q;
+    mv[q] = i < p.nsl ? pm[i] : -INFINITY;
+    sv[q] = i < p.nsl ? ps[i] : 0.f;
+  }
   float m = -INFINITY;
-  for (int i = lane; i < p.nsl; i += 64) m = fmaxf(m, pm[i]);
+#pragma unroll
+  for (int q = 0; q < MRG; ++q) m = fmaxf(m, mv[q]);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
   float s = 0.f;
-  for (int i = lane; i < p.nsl; i += 64) s += ps[i] * __builtin_amdgcn_exp2f((pm[i] - m) * LOG2E);
+#pragma unroll
+  for (int q = 0; q < MRG; ++q) s += sv[q] * __builtin_amdgcn_exp2f((mv[q] - m) * LOG2E);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
   if (lane == 0) {
@@ -310,7 +354,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
 
   for (int t0 = 0; t0 < p.rows; t0 += TR) {
     const int nt = min(TR, p.rows - t0);
-    __syncthreads();  // previous tile's phase 2 done with Zt / rs
+    lds_barrier();  // previous tile's phase 2 done with Zt / rs
     for (int i = tid; i < nt; i += NTH) {
       float4 st = p.rowstat[t0 + i];
       if constexpr (FIX) {  // .z <- delta of the row: the sum of its slices' partials, in order
@@ -323,7 +367,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       const int card = p.reg_idx[t0 + i];
       sm.card[i] = card >= 0 ? (int32_t)((uint32_t)card * (uint32_t)V * 4u) : (int32_t)0x80000000u;
     }
-    __syncthreads();
+    lds_barrier();
     KL_PROBE(1);
     // ---- phase 1: two passes of 8 waves x 32 rows
 #pragma unroll 1
@@ -339,7 +383,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       for (int r = 0; r < 16; ++r) roff[r] = (uint32_t)sm.card[rb + acc_row(r, lane)];
       uint32_t zrow = (uint32_t)((t0 + rb + 4 * half) * V + n0 + (lane & 31));
       asm volatile("" : "+v"(zrow));  // per-pass base of the dZ stores (no hoisted 64-bit addresses)
-      LFrag<D> lf;                      // A fragments first in the memory queue, then M~
+      LFrag<D, D / 16> lf;              // all A fragments first in the memory queue, then M~
       logits_load<D>(p, (p.row0 + t0 + rb) / 32, lf);
       float tv[NJ][16];
       if constexpr (!FIX) {
@@ -426,10 +470,33 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
               *reinterpret_cast<const uint2 *>(&tt[4 * g]);
       }
       deadp |= mn < PMIN;
+      if constexpr (!FIX) {
+        // the exact-clip delta partial of each row over this slice: sum of its targets where
+        // p < 1e-7 (rare: zero unless the wave saw such an element); read by the fix kernel
+        float red = 0.f;
+        if (__ballot(deadp) != 0ull) {
+          float dl[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float4 st = sm.rs[rb + acc_row(r, lane)];
+            float a = 0.f;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              const float pr = __builtin_amdgcn_exp2f((acc[j][r] - st.x - st.y) * LOG2E);
+              const bool live_row = roff[r] < 0x80000000u && valid[j];
+              a += live_row && !(pr >= PMIN) ? __builtin_amdgcn_fmed3f(tv[j][r], PMIN, 1.f) : 0.f;
+            }
+            dl[r] = a;
+          }
+          red = rs16<false>(dl);
+        }
+        if ((lane & 1) == 0)
+          p.part_d[(int64_t)(t0 + rb + acc_row((lane >> 1) & 15, lane)) * p.nsl + sl] = red;
+      }
       KL_PROBE(3 + 2 * ps);
       if constexpr (!FIX) dead |= deadp;
     }
-    __syncthreads();
+    lds_barrier();
     KL_PROBE(6);
     // ---- phase 2: dWo[d][NB] (+)= D3^T[d][tile rows] dZ[tile rows][NB] (wave w: d rows 32w..).
     // A fresh accumulator per tile, added into gW (the block's slice stays L2-resident between
@@ -500,7 +567,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
     for (int off = 32; off > 0; off >>= 1) klsum += __shfl_xor(klsum, off);
     if (lane == 0) sm.red_loss[w] = (double)klsum;
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < NB && n0 + tid < V) {
     float g = 0.f;
     for (int i = 0; i < NTH / 64; ++i) g += sm.red_cs[i][tid];
@@ -565,50 +632,6 @@ __global__ __launch_bounds__(NTH) void kl_fix_kernel(KlP p) {
   }
 }
 
-// ---------------------------------------------------------------- fix: delta partials
-template <int D>
-__global__ __launch_bounds__(NTH) void kl_delta_kernel(KlP p) {
-  __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
-  if (__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int ngroups = (int)cdiv(p.rows, SR);
-  for (int wi = blockIdx.x; wi < p.nsl * ngroups; wi += gridDim.x) {
-    const int sl = wi % p.nsl, n0 = sl * NB;
-    const int r_blk = (wi / p.nsl) * SR + w * 32;
-    __syncthreads();  // the previous item's readers of Wt are done
-    load_wo_slice<D>(p.Wo, p.V, n0, Wt);
-    __syncthreads();
-    if (r_blk >= p.rows) continue;  // wave-uniform; no barrier below
-    float bias[NJ];
-    bool valid[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int gc = n0 + j * 32 + (lane & 31);
-      valid[j] = gc < p.V;
-      bias[j] = valid[j] ? p.bo[gc] : 0.f;
-    }
-    f32x16_t acc[NJ];
-    logits_block<D>(p, Wt, (p.row0 + r_blk) / 32, bias, acc);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = r_blk + acc_row(r, lane);
-      const float4 st = p.rowstat[row];
-      const int card = p.reg_idx[row];
-      float dl = 0.f;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const float pr = __builtin_amdgcn_exp2f((acc[j][r] - st.x - st.y) * LOG2E);
-        if (card >= 0 && valid[j] && !(pr >= PMIN)) {
-          const float t = p.Mt[(int64_t)card * p.V + n0 + j * 32 + (lane & 31)];
-          dl += __builtin_amdgcn_fmed3f(t, PMIN, 1.f);
-        }
-      }
-      dl = half_sum(dl);
-      if ((lane & 31) == r) p.part_d[(int64_t)row * p.nsl + sl] = dl;
-    }
-  }
-}
-
 __global__ __launch_bounds__(256) void kl_tsum_kernel(const float *__restrict__ Mt, int V, float *__restrict__ tsum) {
   __shared__ float red[4];
   const float *row = Mt + (int64_t)blockIdx.x * V;
@@ -647,6 +670,7 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
   CC_REQUIRE(a->row0 % 32 == 0 && a->ldt % 16 == 0 && a->ldt >= a->row0 + a->rows,
              "cc_dec_softmax_kl_dw: row0 % 32, ldt % 16, ldt >= row0 + rows");
   CC_REQUIRE(a->V > 0 && (!a->loss_out || a->ticket), "cc_dec_softmax_kl_dw: V / ticket");
+  CC_REQUIRE(cdiv(a->V, NB) <= 64 * MRG, "cc_dec_softmax_kl_dw: V <= 49,152");
   CC_REQUIRE((((uintptr_t)a->D3p | (uintptr_t)a->D3tp | (uintptr_t)a->ws) & 15) == 0,
              "cc_dec_softmax_kl_dw: packed images and ws 16-B aligned");
   KlP p;
@@ -684,7 +708,7 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
   p.part_d = p.part_s + pn;
   p.flag = (uint32_t *)(p.part_d + pn);
   hipStream_t s = as_stream(stream);
-  const dim3 gs((unsigned)p.nsl, (unsigned)cdiv(a->rows, SR)), gm((unsigned)p.nsl);
+  const dim3 gs((unsigned)p.nsl), gm((unsigned)p.nsl);
 #define KL_LAUNCH(DD)                                                                                          \
   if (a->d == DD) {                                                                                          \
     hipLaunchKernelGGL((kl_stats_kernel<DD>), gs, dim3(NTH), 0, s, p);                                      \
@@ -693,8 +717,6 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
     CC_LAUNCH_CHECK("kl_merge_kernel");                                                                      \
     hipLaunchKernelGGL((kl_main_kernel<DD>), gm, dim3(NTH), 0, s, p);                                       \
     CC_LAUNCH_CHECK("kl_main_kernel");                                                                       \
-    hipLaunchKernelGGL((kl_delta_kernel<DD>), dim3(FIXG), dim3(NTH), 0, s, p);                              \
-    CC_LAUNCH_CHECK("kl_delta_kernel");                                                                      \
     hipLaunchKernelGGL((kl_fix_kernel<DD>), dim3(FIXG), dim3(NTH), 0, s, p);                                \
     CC_LAUNCH_CHECK("kl_fix_kernel");                                                                        \
   }

@@ -1,0 +1,91 @@
+// Per-block phase timestamps of dec_bce_dw_kernel at the bench shape (B = 512, d = 256, V = 22000, Wo read
+// in place, packed D3 images) on random operands (dev tool): HIP-event time of the call, start / end spread
+// over blocks and per-phase medians.
+// hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I cubecobrarecommender_amd/csrc tools/micro/dec_probe2.hip \
+//   cubecobrarecommender_amd/csrc/api.cpp cubecobrarecommender_amd/csrc/host_util.cpp -o tools/micro/bin/dec_probe2
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+__device__ unsigned long long g_blk[1024][16];
+#define DEC_PROBE(k)                                                          \
+  do {                                                                        \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_blk[blockIdx.x][(k)] = wall_clock64(); \
+  } while (0)
+#include "decout.hip"
+
+static uint16_t f2bf(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return (uint16_t)((u + 0x7FFF + ((u >> 16) & 1)) >> 16);
+}
+
+int main() {
+  const int B = 512, d = 256, V = 22000, VW = (V + 31) / 32;
+  std::mt19937 rng(1);
+  std::normal_distribution<float> nd(0.f, 1.f);
+  auto upload_bf = [&](size_t n, float sd) {
+    std::vector<uint16_t> h(n);
+    for (auto &x : h) x = f2bf(sd * nd(rng));
+    void *p;
+    (void)hipMalloc(&p, n * 2);
+    (void)hipMemcpy(p, h.data(), n * 2, hipMemcpyHostToDevice);
+    return p;
+  };
+  void *D3 = upload_bf((size_t)B * d, 0.5f), *D3t = upload_bf((size_t)B * d, 0.5f);
+  void *D3p = upload_bf((size_t)B * d, 0.5f), *D3tp = upload_bf((size_t)B * d, 0.5f);
+  void *Wo = upload_bf((size_t)V * d, 0.05f);
+  void *bo, *yb, *dZ, *gW, *gb, *part, *loss, *tick;
+  (void)hipMalloc(&bo, V * 4);
+  (void)hipMemset(bo, 0, V * 4);
+  (void)hipMalloc(&yb, (size_t)B * VW * 4);
+  {
+    std::vector<uint32_t> y((size_t)B * VW);
+    for (auto &x : y) x = (rng() & rng() & rng() & rng() & rng()) ;  // ~3 % ones
+    (void)hipMemcpy(yb, y.data(), y.size() * 4, hipMemcpyHostToDevice);
+  }
+  (void)hipMalloc(&dZ, (size_t)B * V * 2);
+  (void)hipMalloc(&gW, (size_t)d * V * 4);
+  (void)hipMalloc(&gb, V * 4);
+  (void)hipMalloc(&part, 4096 * 8);
+  (void)hipMalloc(&loss, 8);
+  (void)hipMalloc(&tick, 8);
+  (void)hipMemset(tick, 0, 8);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  const int nb = (V + 95) / 96;
+  for (int rep = 0; rep < 6; ++rep) {
+    (void)hipEventRecord(e0, nullptr);
+    int rc = cc_dec_bce_dw(D3, D3t, B, D3p, D3tp, nullptr, Wo, (const float *)bo, B, d, V, (const uint32_t *)yb, dZ,
+                           (float *)gW, (float *)gb, (double *)part, (double *)loss, 1.0 / (B * V), (uint32_t *)tick,
+                           nullptr);
+    (void)hipEventRecord(e1, nullptr);
+    (void)hipDeviceSynchronize();
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    static unsigned long long g[1024][16];
+    (void)hipMemcpyFromSymbol(g, HIP_SYMBOL(g_blk), sizeof(g));
+    unsigned long long t0 = ~0ull;
+    for (int b = 0; b < nb; ++b) t0 = std::min(t0, g[b][0]);
+    std::vector<double> st, en, ph[9];
+    for (int b = 0; b < nb; ++b) {
+      st.push_back((g[b][0] - t0) * 10.0);
+      en.push_back((g[b][8] - t0) * 10.0);
+      for (int k = 1; k < 9; ++k) ph[k].push_back((g[b][k] - g[b][k - 1]) * 10.0);
+    }
+    auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+    auto mx = [](const std::vector<double> &v) { return *std::max_element(v.begin(), v.end()); };
+    printf("rep %d rc %d call %.1f us | blocks %d start max %.0f ns, end med %.0f max %.0f ns\n", rep, rc, ms * 1e3,
+           nb, mx(st), med(en), mx(en));
+    printf("   medians (ns): resident %.0f, p0 mfma %.0f, p0 epi %.0f, p1 mfma %.0f, p1 epi %.0f, sync %.0f, "
+           "ph2 mfma %.0f, ph2 stores %.0f\n", med(ph[1]), med(ph[2]), med(ph[3]), med(ph[4]), med(ph[5]), med(ph[6]),
+           med(ph[7]), med(ph[8]));
+  }
+  return 0;
+}
