@@ -20,6 +20,11 @@ FLAGS = ['-O3', '-fPIC', '-std=c++17', f'--offload-arch={ARCH}', '-I', INC, '-I'
          '-Wall', '-Wno-unused-function', '-Wno-unused-variable']
 
 
+# per-file flags: the fused D1 kernel's inputs are finite logits; without NaN semantics its max()
+# needs no canonicalising v_max (one VALU op per logit in a VALU-bound epilogue)
+FILE_FLAGS = {'decout.hip': ['-fno-honor-nans']}
+
+
 def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(('.hip', '.cpp')))
 
@@ -34,7 +39,7 @@ def _compile(src, force):
     obj = os.path.join(OBJ, os.path.basename(src) + '.o')
     if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(src), _headers_mtime()):
         return obj
-    cmd = [HIPCC, *FLAGS, '-c', src, '-o', obj]
+    cmd = [HIPCC, *FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), '-c', src, '-o', obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f'hipcc failed for {src}:\n{r.stderr}')

@@ -234,8 +234,8 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         // a = exp(-|z|) once; log1p and 1/(1+a) from it.  The 16 factors 1 + a in (1, 2] of a
         // lane's column are multiplied (<= 2^16) and one log2 per column taken: the log is a
         // quarter-rate instruction; summed log2 scaled by ln 2 at the end
-        uint32_t zrow = (uint32_t)((rb + 4 * half) * V + n0 + col);
-        asm volatile("" : "+v"(zrow));  // per column tile: no hoisted per-row store addresses
+        // store offsets: the lane part in a VGPR, the row part (r) as the scalar soffset
+        const uint32_t zv = 2u * (uint32_t)((rb + 4 * half) * V + n0 + col);
         float lprod = 1.f;
         // the 16 rows' target words: 4 runs of 4 consecutive rows -> 4 LDS reads of 16 B
         uint4 yw[4];
@@ -252,10 +252,11 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
           lprod *= opa;
           rsum += fmaxf(yb ? -z : z, 0.f);
           const float sig = z >= 0.f ? rp : a * rp;
-          const uint16_t zb = bf16_bits(fmaf(sig, scale, yb ? -scale : 0.f));
+          const float dzf = fmaf(sig, scale, yb ? -scale : 0.f);
+          const uint16_t zb = bf16_bits(dzf);
           tt[r] = zb;
-          cs[j] += __uint_as_float((uint32_t)zb << 16);
-          __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, 2u * (zrow + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V)), 0, 0);
+          cs[j] += dzf;  // the bias gradient sums the fp32 dz (the reference's arithmetic)
+          __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zv, 2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), 0);
         }
         lsum += __builtin_amdgcn_logf(lprod);
       } else {
@@ -271,7 +272,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     DEC_PROBE(3 + 2 * ps);
   }
 
-  // bias gradient: column sums of the rounded dZ in a fixed order (lane halves, then waves)
+  // bias gradient: column sums of dz in a fixed order (lane halves, then waves)
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const float c2 = cs[j] + __shfl_xor(cs[j], 32);

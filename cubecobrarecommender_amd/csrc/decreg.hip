@@ -423,11 +423,13 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
             const float tc = __builtin_amdgcn_fmed3f(tv[j][r], PMIN, 1.f);
             klsum = fmaf(tc, fmaf(__builtin_amdgcn_logf(tc), LN2, -__builtin_amdgcn_fmed3f(lp, LN_PMIN, 0.f)), klsum);
             mn = fminf(mn, pr);
-            const uint16_t zb = bf16_bits(scale * fmaf(pr, st.z, pr >= PMIN ? -tc : 0.f));
+            const float dzf = scale * fmaf(pr, st.z, pr >= PMIN ? -tc : 0.f);
+            const uint16_t zb = bf16_bits(dzf);
             tt[r] = zb;
-            cs[j] += __uint_as_float((uint32_t)zb << 16);
-            const uint32_t zoff = 2u * (zrow + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V + j * 32));
-            __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, 0);
+            cs[j] += dzf;  // the bias gradient sums the fp32 dz
+            // the lane part of the offset in a VGPR, the row part (r) as the scalar soffset
+            __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, 2u * (zrow + (uint32_t)(j * 32)),
+                                                  2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), 0);
           }
         } else {
 #pragma unroll
@@ -456,11 +458,12 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
               zb = bf16_bits(old + dz);
               dz = __uint_as_float((uint32_t)zb << 16) - old;  // the change actually applied
               tt[r] = bf16_bits(dz);
+              cs[j] += __uint_as_float((uint32_t)tt[r] << 16);
             } else {
               zb = bf16_bits(dz);
               tt[r] = zb;
+              cs[j] += dz;
             }
-            cs[j] += __uint_as_float((uint32_t)tt[r] << 16);
             if (valid[j]) __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, 0);
           }
         }

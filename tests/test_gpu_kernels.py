@@ -388,8 +388,8 @@ def _nt_gemm(M, N, K, A, lda, Bm, ldb, epi, **kw):
 def test_dec_bce_dw_matches_unfused(B, d, V):
     """cc_dec_bce_dw (logits + BCE + dZ + dWo/dbo in one pass) vs the unfused NT-GEMM path (BCE
     epilogue writing dZ and dZ^T, then dW = D3^T dZ^T with the colsum bias gradient): dZ and dWo
-    bitwise (same MFMA k order), dbo and the loss within fp32 summation-order error; the fp64
-    oracle of the same bf16 operands bounds both."""
+    to a bf16 ulp, dbo (fused: the fp32 dz summed; unfused: the rounded dZ) to the same level; the
+    fp64 oracle of the same bf16 operands bounds both."""
     torch.manual_seed(B + d + V)
     bf = dict(device='cuda', dtype=torch.bfloat16)
     D3 = (torch.randn(B, d, device='cuda') * 0.5).to(torch.bfloat16)
@@ -450,7 +450,8 @@ def test_dec_bce_dw_matches_unfused(B, d, V):
     dzk = dZ.double().cpu().numpy()
     assert np.max(np.abs(dzk - dz_ref) / np.maximum(np.abs(dz_ref), 1e-30)) < 2 ** -8 + 1e-5
     assert rel_err(gW.cpu().numpy(), D3.double().cpu().numpy().T @ dzk) < 1e-5
-    assert rel_err(gb.cpu().numpy(), dzk.sum(0)) < 1e-5
+    # dbo sums the fp32 dz (before the bf16 rounding of the dZ operand): against the fp64 dz
+    assert rel_err(gb.cpu().numpy(), dz_ref.sum(0)) < 2e-5
     want = (np.maximum(z, 0) - z * y + np.log1p(np.exp(-np.abs(z)))).mean()
     assert abs(loss.item() - want) < 1e-5 * abs(want)
     assert abs(part.sum().item() * scale - want) < 1e-5 * abs(want)
