@@ -248,7 +248,37 @@ def recommend_latency(n_req=1000):
         out[f'amount_{amount}'] = {'p50_ms': float(np.percentile(lat, 50)),
                                    'p99_ms': float(np.percentile(lat, 99)), 'requests': len(lat)}
     out['config'] = 'V=20884 d=512 fp32 resident model, cube n=360, index list in -> top-N indices out'
+    out['cold_load'] = cold_load(flat, lay, V, d, rng)
     return out
+
+
+def cold_load(flat, lay, V, d, rng):
+    """BASELINE configs[0]'s cold path (ml_recommend.py:54-108: load_model on ml_files/<name>, then
+    one single-cube recommend): a checkpoint of the reference architecture is written in the
+    ml_files layout (TF tensor bundle, checkpoint.py), then load_model + the first recommend are
+    timed in this process (torch and the HIP library already loaded; the reference's own
+    interpreter start and TF import are not part of either side)."""
+    import shutil
+    import tempfile
+    from cubecobrarecommender_amd import checkpoint
+    from cubecobrarecommender_amd.model import load_model
+    tmp = tempfile.mkdtemp(prefix='ccrec_cold_')
+    try:
+        path = os.path.join(tmp, 'recommender')
+        checkpoint.save_model(path, V, d, lay.unpack(flat))
+        size = sum(os.path.getsize(os.path.join(dp, f)) for dp, _, fs in os.walk(path) for f in fs)
+        cube = rng.choice(V, 360, replace=False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        model = load_model(path)
+        t1 = time.perf_counter()
+        model.recommender().recommend(cube, 100)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        return {'load_model_s': t1 - t0, 'first_recommend_s': t2 - t1, 'total_s': t2 - t0,
+                'checkpoint_bytes': size}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def main():

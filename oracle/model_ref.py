@@ -17,7 +17,10 @@ TF 2.5.2 semantics restated (not vendored, not installed — "parity unpinned" v
 
 ``mode``: 'fp64' (exact reference), or 'bf16' which rounds exactly the operands the GPU's bf16
 MFMA path rounds (weights' bf16 shadow, activations and dZ/dPre fed to GEMMs) while accumulating
-in fp64 — the GPU's mixed-precision arithmetic up to summation order.
+in fp64 — the GPU's mixed-precision arithmetic up to summation order; 'mx8' is 'bf16' with the
+decoder output-layer / regulariser products (model.py:64,94,98) on MX-FP8 operands exactly as
+config 5 quantises them (oracle/mx8_ref.py: e4m3fn codes + one E8M0 scale per 32 K-elements, the
+bf16 values quantised along each product's K axis), dequantised and accumulated in fp64.
 """
 import numpy as np
 import scipy.sparse as sp
@@ -55,8 +58,16 @@ def bf16_round(a):
     return u.astype(np.uint32).view(np.float32)
 
 
+def _mx8_mm(A, B):
+    """A [M, K] . B [N, K]^T on MX-FP8 operands quantised along K (config 5's block-scaled MFMA)."""
+    from oracle import mx8_ref
+    qa, sa = mx8_ref.quantize_rows(A)
+    qb, sb = mx8_ref.quantize_rows(B)
+    return mx8_ref.dequantize_rows(qa, sa) @ mx8_ref.dequantize_rows(qb, sb).T
+
+
 def _rq(mode):
-    if mode == 'bf16':
+    if mode in ('bf16', 'mx8'):
         return lambda a: bf16_round(a).astype(np.float64)
     if mode == 'fp32':   # plain fp32 numpy (the CPU-baseline leg of bench.py)
         return lambda a: np.asarray(a, np.float32)
@@ -110,12 +121,20 @@ def train_forward_backward(P, x_lists, y_lists, V, d, reg=0.0, reg_idx=None, y_r
         for nm in ('decoded_1', 'decoded_2', 'decoded_3'):
             h = rq(_relu(h @ W[prefix + '/' + nm + '/kernel'] + W[prefix + '/' + nm + '/bias']))
             hh.append(h)
-        z = h @ W[prefix + '/reconstruct/kernel'] + W[prefix + '/reconstruct/bias']
+        Wo = W[prefix + '/reconstruct/kernel']
+        if mode == 'mx8':     # logits: D3 [rows][d] . Wo^T [V][d], both quantised along d
+            z = _mx8_mm(h, Wo.T) + W[prefix + '/reconstruct/bias']
+        else:
+            z = h @ Wo + W[prefix + '/reconstruct/bias']
         loss, dz = out_grad_fn(z)
         dzq = rq(dz)
-        grads[prefix + '/reconstruct/kernel'] += hh[3].T @ dzq
+        if mode == 'mx8':     # dW: D3^T . dZ along the rows; dX: dZ . Wo^T along V
+            grads[prefix + '/reconstruct/kernel'] += _mx8_mm(hh[3].T, dzq.T)
+            dh = _mx8_mm(dzq, Wo)
+        else:
+            grads[prefix + '/reconstruct/kernel'] += hh[3].T @ dzq
+            dh = dzq @ Wo.T
         grads[prefix + '/reconstruct/bias'] += dzq.sum(0)
-        dh = dzq @ W[prefix + '/reconstruct/kernel'].T
         for li, nm in ((3, 'decoded_3'), (2, 'decoded_2'), (1, 'decoded_1')):
             dpre = rq(dh * (hh[li] > 0))
             grads[prefix + '/' + nm + '/kernel'] += hh[li - 1].T @ dpre

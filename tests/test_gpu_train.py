@@ -237,8 +237,10 @@ def test_data_parallel_equivalence(reg):
 @pytest.mark.parametrize('V,d,B', [(1500, 128, 128), (2500, 1024, 128)])
 def test_fp8_decoder_steps_track_oracle(reg, V, d, B):
     """Config 5: MX-FP8 decoder output / regulariser GEMMs, everything else bf16.
-    Parity is claimed at fp32 only (§8(d)); here F is bit-exact, the losses track the bf16-emulating
-    oracle within the fp8 element precision (3 mantissa bits) and the gradients within 10 % L2."""
+    Against the MX-FP8-emulating oracle (model_ref mode='mx8': the same e4m3fn + E8M0 quantisation
+    of the same bf16 operands along each product's K axis): F bit-exact, losses within 1e-3 and
+    gradients within 3e-2 relative L2 (an operand that rounds one bf16 ulp differently can land in
+    the neighbouring fp8 code, 2^-3 apart)."""
     C = 4 * B
     tr, lists, Mt, ns, P, perm = _setup(V, d, B, C, reg, 'fp8')
     assert tr.mx8 and tr.fused_tower
@@ -252,14 +254,14 @@ def test_fp8_decoder_steps_track_oracle(reg, V, d, B):
         for b in range(B):
             assert np.array_equal(xs[b], oxs[b]) and np.array_equal(ys[b], oys[b])
         losses, grads = model_ref.train_forward_backward(
-            P, oxs, oys, V, d, reg=reg, reg_idx=oreg, y_reg=Mt[oreg] if reg > 0 else None, mode='bf16')
+            P, oxs, oys, V, d, reg=reg, reg_idx=oreg, y_reg=Mt[oreg] if reg > 0 else None, mode='mx8')
         got = tr.losses()
-        assert abs(got['bce'] - losses['bce']) / losses['bce'] < 1e-2, (step, got, losses)
+        assert abs(got['bce'] - losses['bce']) / losses['bce'] < 1e-3, (step, got, losses)
         if reg > 0:
-            assert abs(got['kl'] - losses['kl']) / losses['kl'] < 1e-2, (step, got, losses)
+            assert abs(got['kl'] - losses['kl']) / losses['kl'] < 1e-3, (step, got, losses)
         gflat = tr.layout.unpack(tr.grads.cpu().numpy())
         errs = {k: rel_err(gflat[k], grads[k]) for k in grads if reg or not k.startswith('decoder_for_reg')}
-        bad = {k: v for k, v in errs.items() if not v < 0.1}
+        bad = {k: v for k, v in errs.items() if not v < 3e-2}
         assert not bad, (step, bad)
         tr.apply()
         torch.cuda.synchronize()
