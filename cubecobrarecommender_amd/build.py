@@ -12,12 +12,15 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, 'csrc')
 INC = os.path.join(ROOT, 'include')
-OBJ = os.path.join(PKG, 'build_obj')
-LIB = os.path.join(PKG, 'libccrec_hip.so')
+# dev experiments: CCREC_BUILD_TAG=x builds libccrec_hip_x.so from build_obj_x with CCREC_EXTRA_FLAGS
+# (load it with CCREC_LIB=...); the product library is the untagged one
+_TAG = os.environ.get('CCREC_BUILD_TAG', '')
+OBJ = os.path.join(PKG, 'build_obj' + (f'_{_TAG}' if _TAG else ''))
+LIB = os.path.join(PKG, 'libccrec_hip' + (f'_{_TAG}' if _TAG else '') + '.so')
 ARCH = os.environ.get('CCREC_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['-O3', '-fPIC', '-std=c++17', f'--offload-arch={ARCH}', '-I', INC, '-I', CSRC,
-         '-Wall', '-Wno-unused-function', '-Wno-unused-variable']
+         '-Wall', '-Wno-unused-function', '-Wno-unused-variable'] + os.environ.get('CCREC_EXTRA_FLAGS', '').split()
 
 
 # per-file flags: the fused D1 kernel's inputs are finite logits; without NaN semantics its max()

@@ -7,6 +7,8 @@
 
 namespace cc_adam {
 
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
 __device__ __forceinline__ void elem(float &p, float &m, float &v, float g, float alpha,
                                      float omb1, float omb2, float eps) {
 #pragma clang fp contract(off)  // every kernel that inlines this rounds identically (no FMA choice)
@@ -66,17 +68,24 @@ __device__ __forceinline__ void range(const Args &a, int64_t step, int bid, int 
   const int64_t n4 = a.n >> 2;
   const int64_t stride = (int64_t)nblocks * blockDim.x;
   for (int64_t i = (int64_t)bid * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 pp = reinterpret_cast<float4 *>(a.p)[i];
-    float4 mm = reinterpret_cast<float4 *>(a.m)[i];
-    float4 vv = reinterpret_cast<float4 *>(a.v)[i];
-    const float4 gg = reinterpret_cast<const float4 *>(a.g)[i];
+    // p, m, v, g stream through once per step: non-temporal loads and stores (the bf16 shadow and
+    // the packed images, which the next step's kernels read, keep the default policy).  Measured
+    // in the step: 180-184 -> 178 us (Adam -1.5 us; the next W1-gradient kernel -2.5 us: Adam no
+    // longer evicts the lines it reads)
+    f32x4_t pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.p) + i);
+    f32x4_t mv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.m) + i);
+    f32x4_t vv4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.v) + i);
+    const f32x4_t gv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.g) + i);
+    float4 pp = make_float4(pv[0], pv[1], pv[2], pv[3]), mm = make_float4(mv[0], mv[1], mv[2], mv[3]);
+    float4 vv = make_float4(vv4[0], vv4[1], vv4[2], vv4[3]);
+    const float4 gg = make_float4(gv[0], gv[1], gv[2], gv[3]);
     float *pe = &pp.x, *me = &mm.x, *ve = &vv.x;
     const float *ge = &gg.x;
 #pragma unroll
     for (int e = 0; e < 4; ++e) elem(pe[e], me[e], ve[e], ge[e], alpha, omb1, omb2, a.eps);
-    reinterpret_cast<float4 *>(a.p)[i] = pp;
-    reinterpret_cast<float4 *>(a.m)[i] = mm;
-    reinterpret_cast<float4 *>(a.v)[i] = vv;
+    __builtin_nontemporal_store(f32x4_t{pp.x, pp.y, pp.z, pp.w}, reinterpret_cast<f32x4_t *>(a.p) + i);
+    __builtin_nontemporal_store(f32x4_t{mm.x, mm.y, mm.z, mm.w}, reinterpret_cast<f32x4_t *>(a.m) + i);
+    __builtin_nontemporal_store(f32x4_t{vv.x, vv.y, vv.z, vv.w}, reinterpret_cast<f32x4_t *>(a.v) + i);
     if (a.shadow) {
       ushort4 s;
       s.x = f2bf(pp.x);

@@ -70,6 +70,12 @@ __device__ __forceinline__ bf16x8_t frag(const bf16_t *S, int off) {
 __device__ __forceinline__ uint16_t bf16_bits(float f) {  // RNE (v_cvt_pk_bf16_f32), finite inputs
   return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+// two floats -> one packed bf16 pair (lo = a, hi = b), RNE: ONE v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t bf16_pack2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
+}
 
 template <int D, int BB>
 __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
@@ -81,6 +87,10 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   __shared__ float red_cs[NTH / 64][NB];
   __shared__ double red_loss[NTH / 64];
   __shared__ int lastflag;
+  // the slice's bias as MFMA B fragments: k = 0, 1, 2 carry the exact three-bf16 split of bo
+  // (hi + mid + lo == bo in fp32), so one MFMA against a ones A fragment starts the accumulators at
+  // the bias with no per-element moves (the epilogue is VALU-bound; the MFMA pipe has room)
+  __shared__ __attribute__((aligned(16))) bf16_t bfr[NJ * 64 * 8];
   bf16_t *Wt = reinterpret_cast<bf16_t *>(smem);                 // [NB][d]
   bf16_t *Zt = reinterpret_cast<bf16_t *>(smem + ZT_OFF);        // [NB][B]
   uint32_t *ys = reinterpret_cast<uint32_t *>(smem + YS_OFF);    // [NJ][B]
@@ -188,15 +198,26 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   // rows pass*256 + 32w .. +32 and all NB columns; its A fragments (16 B per lane per 16-k step)
   // come straight from global/L2 into registers, the next pass's in flight during this one.
   float rsum = 0.f, lsum = 0.f, cs[NJ];
-  float bias[NJ];
   bool valid[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int gc = n0 + j * 32 + (lane & 31);
     valid[j] = gc < V;
-    bias[j] = valid[j] ? p.bo[gc] : 0.f;
     cs[j] = 0.f;
   }
+  if (tid < NJ * 64) {
+    const int gc = n0 + (tid >> 6) * 32 + (tid & 31);
+    const float b = ((tid & 32) == 0 && gc < V) ? p.bo[gc] : 0.f;
+    const __bf16 hi = (__bf16)b;
+    const float r1 = b - (float)hi;
+    const __bf16 mid = (__bf16)r1;
+    const __bf16 lo = (__bf16)(r1 - (float)mid);
+    const __bf16 z0 = (__bf16)0.f;
+    *reinterpret_cast<bf16x8_t *>(bfr + tid * 8) = bf16x8_t{hi, mid, lo, z0, z0, z0, z0, z0};
+  }
+  bf16x8_t ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)(half == 0 && e < 3 ? 1.f : 0.f);
   // LDS-only barrier: __syncthreads would also wait for pass 0's A fragments (vmcnt counts loads)
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   DEC_PROBE(1);
@@ -209,11 +230,11 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   for (int ps = 0; ps < npass; ++ps) {
     if (ps + 1 < npass) load_a(af[(ps + 1) & 1], ps + 1);
     if (ps * 256 + w * 32 >= B) continue;          // wave-uniform: rows beyond B
-    f32x16_t acc[NJ];  // starts at the bias: z = bo + sum_k D3 Wo accumulates in the MFMA
+    f32x16_t acc[NJ];  // starts at the bias (exactly): z = bo + sum_k D3 Wo accumulates in the MFMA
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[j][r] = bias[j];
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, *reinterpret_cast<const bf16x8_t *>(bfr + (j * 64 + lane) * 8),
+                                                       f32x16_t{}, 0, 0, 0);
 #pragma unroll
     for (int kk = 0; kk < nkk; ++kk) {
 #pragma unroll
@@ -227,7 +248,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int col = j * 32 + (lane & 31);
-      uint16_t tt[16];
+      uint32_t tt[8];  // dz of rows (r, r+1) as one packed bf16 pair (one v_cvt_pk_bf16_f32)
       if (valid[j]) {
         // sigmoid_cross_entropy_with_logits (TF 2.5 Keras BCE on a sigmoid output):
         //   loss = max(z, 0) - z y + log1p(exp(-|z|)),  dz = (sigmoid(z) - y) / (B V)
@@ -236,38 +257,54 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         // quarter-rate instruction; summed log2 scaled by ln 2 at the end
         // store offsets: the lane part in a VGPR, the row part (r) as the scalar soffset
         const uint32_t zv = 2u * (uint32_t)((rb + 4 * half) * V + n0 + col);
-        float lprod = 1.f;
+        f32x2_t lprod = {1.f, 1.f}, rs2 = {0.f, 0.f}, cs2 = {0.f, 0.f};  // even / odd rows: packed math
         // the 16 rows' target words: 4 runs of 4 consecutive rows -> 4 LDS reads of 16 B
         uint4 yw[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) yw[g] = *reinterpret_cast<const uint4 *>(ys + j * B + rb + 8 * g + 4 * half);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const uint32_t ywr = (r & 3) == 0 ? yw[r >> 2].x : (r & 3) == 1 ? yw[r >> 2].y : (r & 3) == 2 ? yw[r >> 2].z : yw[r >> 2].w;
-          const uint32_t yb = (ywr >> (lane & 31)) & 1u;
-          const float z = acc[j][r];
-          const float a = __builtin_amdgcn_exp2f(-fabsf(z) * LOG2E);
-          const float opa = 1.f + a;
-          const float rp = __builtin_amdgcn_rcpf(opa);
-          lprod *= opa;
-          rsum += fmaxf(yb ? -z : z, 0.f);
-          const float sig = z >= 0.f ? rp : a * rp;
-          const float dzf = fmaf(sig, scale, yb ? -scale : 0.f);
-          const uint16_t zb = bf16_bits(dzf);
-          tt[r] = zb;
-          cs[j] += dzf;  // the bias gradient sums the fp32 dz (the reference's arithmetic)
-          __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zv, 2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), 0);
+        for (int r2 = 0; r2 < 16; r2 += 2) {
+          f32x2_t z2, a2, opa2, rp2, sel2, rl2, ys2;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int r = r2 + e;
+            const uint32_t ywr = (r & 3) == 0 ? yw[r >> 2].x : (r & 3) == 1 ? yw[r >> 2].y : (r & 3) == 2 ? yw[r >> 2].z : yw[r >> 2].w;
+            const bool yb = (ywr >> (lane & 31)) & 1u;
+            z2[e] = acc[j][r];
+            a2[e] = __builtin_amdgcn_exp2f(-fabsf(z2[e]) * LOG2E);
+            rl2[e] = fmaxf(yb ? -z2[e] : z2[e], 0.f);
+            ys2[e] = yb ? -scale : 0.f;
+          }
+          opa2 = 1.f + a2;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) rp2[e] = __builtin_amdgcn_rcpf(opa2[e]);
+          lprod *= opa2;
+          rs2 += rl2;
+          const f32x2_t arp2 = a2 * rp2;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) sel2[e] = z2[e] >= 0.f ? rp2[e] : arp2[e];
+          const f32x2_t dzp = sel2 * scale + ys2;   // fma: (sigmoid(z) - y) / (B V)
+          cs2 += dzp;   // the bias gradient sums the fp32 dz (the reference's arithmetic)
+          const uint32_t pk = bf16_pack2(dzp[0], dzp[1]);
+          tt[r2 >> 1] = pk;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int r = r2 + e;
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(e ? pk >> 16 : pk), dz_rs, zv,
+                                                  2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), 0);
+          }
         }
-        lsum += __builtin_amdgcn_logf(lprod);
+        lsum += __builtin_amdgcn_logf(lprod[0] * lprod[1]);
+        rsum += rs2[0] + rs2[1];
+        cs[j] += cs2[0] + cs2[1];
       } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) tt[r] = 0;
+        for (int r = 0; r < 8; ++r) tt[r] = 0;
       }
       // dZ^T image: registers 4g..4g+3 = 4 consecutive rows -> one 8-byte LDS store
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<uint2 *>(Zt + sw_off(col, rb + 8 * g + 4 * half, CHB)) =
-            *reinterpret_cast<const uint2 *>(&tt[4 * g]);
+        *reinterpret_cast<uint2 *>(Zt + sw_off(col, rb + 8 * g + 4 * half, CHB)) = make_uint2(tt[2 * g], tt[2 * g + 1]);
     }
     DEC_PROBE(3 + 2 * ps);
   }

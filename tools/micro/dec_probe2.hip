@@ -13,9 +13,11 @@
 #include <vector>
 
 __device__ unsigned long long g_blk[1024][16];
+__device__ unsigned long long g_wav[1024][8][16];
 #define DEC_PROBE(k)                                                          \
   do {                                                                        \
     if (threadIdx.x == 0 && blockIdx.x < 1024) g_blk[blockIdx.x][(k)] = wall_clock64(); \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) g_wav[blockIdx.x][threadIdx.x >> 6][(k)] = wall_clock64(); \
   } while (0)
 #include "decout.hip"
 
@@ -86,6 +88,18 @@ int main() {
     printf("   medians (ns): resident %.0f, p0 mfma %.0f, p0 epi %.0f, p1 mfma %.0f, p1 epi %.0f, sync %.0f, "
            "ph2 mfma %.0f, ph2 stores %.0f\n", med(ph[1]), med(ph[2]), med(ph[3]), med(ph[4]), med(ph[5]), med(ph[6]),
            med(ph[7]), med(ph[8]));
+    if (rep == 5) {
+      static unsigned long long gw[1024][8][16];
+      (void)hipMemcpyFromSymbol(gw, HIP_SYMBOL(g_wav), sizeof(gw));
+      for (int w = 0; w < 8; ++w) {
+        std::vector<double> pt[9];
+        for (int b = 0; b < nb; ++b)
+          for (int k = 1; k < 9; ++k) pt[k].push_back((gw[b][w][k] - gw[b][0][0]) * 10.0);
+        printf("   wave %d points (ns from block start, median): ", w);
+        for (int k = 1; k < 9; ++k) printf("%.0f ", med(pt[k]));
+        printf("\n");
+      }
+    }
   }
   return 0;
 }
