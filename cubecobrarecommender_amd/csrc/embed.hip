@@ -539,30 +539,74 @@ namespace {
 // [64b, 64b+64) for all d columns and writes its column sums to partial[b][d]; the bias gradient
 // adds them in block order (deterministic).
 constexpr int ID_ROWS = 64;
+// 256 threads: d/4 threads per row (float4 columns), 1024/d rows per pass; every load of the
+// block's rows is issued before the read-modify-writes (the per-row chain was latency-bound)
 __global__ __launch_bounds__(256) void embed_identity_add_kernel(const float *__restrict__ dpre, int n, int d,
                                                                  int lo, int round_bf16,
                                                                  float *__restrict__ grad,
                                                                  float *__restrict__ partial) {
+  __shared__ float4 red[256];
+  const int tpr = d >> 2, rpp = 256 / tpr;
+  const int q = threadIdx.x % tpr, rr = threadIdx.x / tpr;
   const int r0 = blockIdx.x * ID_ROWS, r1 = min(n, r0 + ID_ROWS);
-  for (int c = threadIdx.x; c < d; c += 256) {
-    float cs = 0.f;
-    for (int r = r0; r < r1; ++r) {
-      float v = dpre[(int64_t)r * d + c];
-      if (round_bf16) v = bf2f(f2bf(v));
-      grad[(int64_t)(lo + r) * d + c] += v;
-      cs += v;
+  float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int rb = r0 + rr; rb < r1; rb += 4 * rpp) {
+    float4 v[4], g[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = rb + u * rpp;
+      if (r < r1) {
+        v[u] = reinterpret_cast<const float4 *>(dpre + (int64_t)r * d)[q];
+        g[u] = reinterpret_cast<const float4 *>(grad + (int64_t)(lo + r) * d)[q];
+      }
     }
-    partial[(int64_t)blockIdx.x * d + c] = cs;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = rb + u * rpp;
+      if (r < r1) {
+        float4 x = v[u];
+        if (round_bf16) x = make_float4(bf2f(f2bf(x.x)), bf2f(f2bf(x.y)), bf2f(f2bf(x.z)), bf2f(f2bf(x.w)));
+        reinterpret_cast<float4 *>(grad + (int64_t)(lo + r) * d)[q] =
+            make_float4(g[u].x + x.x, g[u].y + x.y, g[u].z + x.z, g[u].w + x.w);
+        cs = make_float4(cs.x + x.x, cs.y + x.y, cs.z + x.z, cs.w + x.w);
+      }
+    }
+  }
+  red[threadIdx.x] = cs;
+  __syncthreads();
+  if (rr == 0) {  // column sums over the row groups in a fixed order
+    float4 t = red[q];
+    for (int k = 1; k < rpp; ++k) {
+      const float4 o = red[k * tpr + q];
+      t = make_float4(t.x + o.x, t.y + o.y, t.z + o.z, t.w + o.w);
+    }
+    reinterpret_cast<float4 *>(partial + (int64_t)blockIdx.x * d)[q] = t;
   }
 }
 
+// bias_grad[c] += sum_b partial[b][c]: 4 waves per 64 columns, wave w sums a contiguous quarter of
+// the partials (8 loads in flight), then the quarters are added in wave order
 __global__ __launch_bounds__(256) void embed_identity_bias_kernel(const float *__restrict__ partial, int nb,
                                                                   int d, float *__restrict__ bias_grad) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= d) return;
+  __shared__ float red[4][64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 64 + lane;
+  const int per = (nb + 3) / 4, b0 = min(nb, w * per), b1 = min(nb, b0 + per);
   float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += partial[(int64_t)b * d + c];
-  bias_grad[c] += s;
+  if (c < d) {
+    int b = b0;
+    for (; b + 8 <= b1; b += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = partial[(int64_t)(b + u) * d + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; b < b1; ++b) s += partial[(int64_t)b * d + c];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < d) bias_grad[c] += ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 }  // namespace
 
@@ -573,7 +617,7 @@ extern "C" size_t cc_embed_identity_ws(int32_t n, int32_t d) {
 extern "C" int cc_embed_identity_add(int32_t dtype, const float *dpre, int32_t n, int32_t d, int32_t lo,
                                      float *grad, float *bias_grad, float *partial, void *stream) {
   CC_REQUIRE(dpre && grad && partial, "cc_embed_identity_add: null pointer");
-  CC_REQUIRE(n >= 0 && d > 0 && lo >= 0, "cc_embed_identity_add: bad n/d/lo");
+  CC_REQUIRE(n >= 0 && d >= 64 && d <= 1024 && (d & (d - 1)) == 0 && lo >= 0, "cc_embed_identity_add: bad n/d/lo");
   if (n == 0) return CC_OK;
   const int nb = (int)cdiv(n, ID_ROWS);
   hipStream_t s = as_stream(stream);
@@ -581,7 +625,7 @@ extern "C" int cc_embed_identity_add(int32_t dtype, const float *dpre, int32_t n
                      dtype == CC_BF16 ? 1 : 0, grad, partial);
   CC_LAUNCH_CHECK("embed_identity_add_kernel");
   if (bias_grad) {
-    hipLaunchKernelGGL(embed_identity_bias_kernel, dim3((unsigned)cdiv(d, 256)), dim3(256), 0, s, partial, nb, d,
+    hipLaunchKernelGGL(embed_identity_bias_kernel, dim3((unsigned)cdiv(d, 64)), dim3(256), 0, s, partial, nb, d,
                        bias_grad);
     CC_LAUNCH_CHECK("embed_identity_bias_kernel");
   }

@@ -774,6 +774,91 @@ __global__ __launch_bounds__(64) void tower_dw_packed_kernel(TowerP p) {
   }
 }
 
+// Row-split form for tall layers (full-mode regulariser: ~22k rows per chain): job (tile, split s)
+// accumulates rows chunk s of the tile's chain into part[(job * S + s)] (the lane's 16 accumulators
+// + its bias partial); tower_dw_split_reduce adds the S partials of each tile in split order
+// (deterministic) — the one-wave-per-tile chain over 22k rows left most of the chip idle.
+constexpr int DWS_STRIDE = 64 * 16 + 64;  // floats per (job, split) partial
+__global__ __launch_bounds__(64) void tower_dw_packed_split_kernel(TowerP p, int S, float *__restrict__ part) {
+  int l, i, k0, n0, row0, nrows;
+  const int job = blockIdx.x, sp = blockIdx.y;
+  if (!dw_job(p, job, l, i, k0, n0, row0, nrows)) return;
+  const int lane = threadIdx.x;
+  const int R = p.R, nj = nrows / 16, chunk = (nj + S - 1) / S;
+  const int ja = min(nj, sp * chunk), jb = min(nj, ja + chunk);
+  const int j0 = row0 / 16;
+  const bf16_t *ha = p.hpt[i] + pack_off(k0 / 32, j0, lane, R);
+  const bf16_t *gb = p.gpt[i] + pack_off(n0 / 32, j0, lane, R);
+  f32x16_t acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float cs = 0.f;
+  const bool bias = k0 == 0;
+  int j = ja;
+  for (; j + DWP_U <= jb; j += DWP_U) {
+    bf16x8_t a[DWP_U], b[DWP_U];
+#pragma unroll
+    for (int u = 0; u < DWP_U; ++u) {
+      a[u] = *reinterpret_cast<const bf16x8_t *>(ha + (j + u) * 512);
+      b[u] = *reinterpret_cast<const bf16x8_t *>(gb + (j + u) * 512);
+    }
+#pragma unroll
+    for (int u = 0; u < DWP_U; ++u) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u], b[u], acc, 0, 0, 0);
+      if (bias) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cs += (float)b[u][e];
+      }
+    }
+  }
+  for (; j < jb; ++j) {
+    const bf16x8_t a = *reinterpret_cast<const bf16x8_t *>(ha + j * 512);
+    const bf16x8_t b = *reinterpret_cast<const bf16x8_t *>(gb + j * 512);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+    if (bias) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs += (float)b[e];
+    }
+  }
+  float *dst = part + ((int64_t)job * S + sp) * DWS_STRIDE;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    reinterpret_cast<float4 *>(dst + lane * 16)[q] = make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+  dst[1024 + lane] = cs;
+}
+
+__global__ __launch_bounds__(64) void tower_dw_split_reduce_kernel(TowerP p, int S, const float *__restrict__ part) {
+  int l, i, k0, n0, row0, nrows;
+  const int job = blockIdx.x;
+  if (!dw_job(p, job, l, i, k0, n0, row0, nrows)) return;
+  int K, N;
+  chain_dims(p.d, i, K, N);
+  const int lane = threadIdx.x, half = lane >> 5;
+  f32x16_t acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float cs = 0.f;
+  for (int sp = 0; sp < S; ++sp) {
+    const float *src = part + ((int64_t)job * S + sp) * DWS_STRIDE;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = reinterpret_cast<const float4 *>(src + lane * 16)[q];
+      acc[4 * q] += v.x;
+      acc[4 * q + 1] += v.y;
+      acc[4 * q + 2] += v.z;
+      acc[4 * q + 3] += v.w;
+    }
+    cs += src[1024 + lane];
+  }
+  float *gw = p.gw[l] + (int64_t)(k0 + 4 * half) * N + n0 + (lane & 31);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) gw[(int64_t)((r & 3) + 8 * (r >> 2)) * N] = acc[r];
+  if (k0 == 0) {
+    cs += __shfl_xor(cs, 32);
+    if (half == 0) p.gb[l][n0 + lane] = cs;
+  }
+}
+
 __global__ __launch_bounds__(256) void tower_reduce_kernel(TowerP p) {
   const int nb = p.R / RB, nbB = p.B / RB;
   const int64_t E = p.slab_elems;
@@ -991,6 +1076,15 @@ extern "C" int cc_tower_bwd_dw_direct(const cc_tower_args *t, void *stream) {
     jobs += (K / 32) * (N / 32);
   }
   if (p.dwpacked) {  // the forward / backward chains wrote the packed transposed H_i / G_i
+    // tall chains (full-mode regulariser rows): split the rows, S partials per tile in the slab
+    const int S = std::min(16, std::max(1, t->R / 1024));
+    if (S > 1 && p.slab && (int64_t)jobs * S * DWS_STRIDE <= (int64_t)(t->R / RB) * p.slab_elems) {
+      hipLaunchKernelGGL(tower_dw_packed_split_kernel, dim3(jobs, S), dim3(64), 0, as_stream(stream), p, S, p.slab);
+      CC_LAUNCH_CHECK("tower_dw_packed_split_kernel");
+      hipLaunchKernelGGL(tower_dw_split_reduce_kernel, dim3(jobs), dim3(64), 0, as_stream(stream), p, S, p.slab);
+      CC_LAUNCH_CHECK("tower_dw_split_reduce_kernel");
+      return CC_OK;
+    }
     hipLaunchKernelGGL(tower_dw_packed_kernel, dim3(jobs), dim3(64), 0, as_stream(stream), p);
     CC_LAUNCH_CHECK("tower_dw_packed_kernel");
     return CC_OK;
