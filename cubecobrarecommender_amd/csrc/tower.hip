@@ -588,6 +588,222 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
   }
 }
 
+// ------------------------------------------------------------------ bf16 wide path (256 < d <= 1024)
+// The d <= 256 kernels above give each wave ONE 32-column tile per layer with its whole reduction
+// (<= 256 = 16 fragments) in registers.  At d = 1024 (config 5) the first / last layers have 32
+// output tiles or a 1,024-long reduction, so a wave's work becomes a stream of items (layer, tile,
+// 256-long reduction chunk) in layer order: the next item's fragments (possibly of a later layer)
+// load while the current item's MFMAs run, and a wave crossing a layer boundary joins that
+// layer's barrier first — every wave passes every barrier once, in order, whatever its items.
+// Activations ping-pong between two LDS images (forward: layer in / out; backward: G in / dH out)
+// so a tile's epilogue never waits for the other waves' reads.
+constexpr int WBIAS_MAX = 832 + 1024;  // bias_off(5) + d
+
+struct WItem {
+  int i, t, c, nch, red;  // chain layer, 32-column tile, reduction chunk, chunks per tile, reduction
+};
+// the q-th item of wave w (forward: layers 0..5, tiles of N, reduction K; backward: layers 5..0,
+// tiles of K, reduction N)
+__device__ __forceinline__ bool witem(int d, bool fwd, int w, int q, WItem &it) {
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    const int i = fwd ? s : 5 - s;
+    int K, N;
+    chain_dims(d, i, K, N);
+    const int nt = (fwd ? N : K) >> 5, red = fwd ? K : N;
+    const int nch = (red + 255) >> 8;
+    const int mine = nt > w ? (nt - w + 7) >> 3 : 0;
+    const int cnt = mine * nch;
+    if (q < cnt) {
+      it.i = i;
+      it.t = w + 8 * (q / nch);
+      it.c = q % nch;
+      it.nch = nch;
+      it.red = red;
+      return true;
+    }
+    q -= cnt;
+  }
+  return false;
+}
+// fragments j = 16c .. 16c + 15 of tile t of a packed image with reduction `red`
+__device__ __forceinline__ void issue_chunk(Frags &F, const bf16_t *__restrict__ P, const WItem &it) {
+  const int lane = threadIdx.x & 63;
+  const bf16_t *base = P + (((int64_t)it.t * (it.red / 16) + 16 * it.c) * 64 + lane) * 8;
+  const int nf = min(FB, it.red / 16 - 16 * it.c);
+#pragma unroll
+  for (int j = 0; j < FB; ++j)
+    if (j < nf) F.f[j] = *reinterpret_cast<const bf16x8_t *>(base + j * 512);
+}
+// acc (+)= chunk c of the transposed product (packed weights = A, LDS rows = B; see consume_frags_t)
+__device__ __forceinline__ void consume_chunk_t(const Frags &F, const bf16_t *A, int lda, const WItem &it,
+                                                f32x16_t &acc) {
+  const int lane = threadIdx.x & 63;
+  const bf16_t *arow = A + (lane & 31) * lda + 8 * (lane >> 5) + 256 * it.c;
+  if (it.c == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  }
+  const int nf = min(FB, it.red / 16 - 16 * it.c);
+#pragma unroll
+  for (int j = 0; j < FB; ++j)
+    if (j < nf)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.f[j], *reinterpret_cast<const bf16x8_t *>(arow + 16 * j), acc,
+                                                    0, 0, 0);
+}
+
+__global__ __launch_bounds__(FNT) void tower_fwd_wide_kernel(TowerP p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ __attribute__((aligned(16))) float bsm[WBIAS_MAX];
+  const int ldx = p.maxw + 8;
+  bf16_t *xin = reinterpret_cast<bf16_t *>(smem);
+  bf16_t *xout = xin + RB * ldx;
+  const int r0 = blockIdx.x * RB;
+  const bool reg = r0 >= p.B;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5;
+  const int d = p.d, nbias = bias_off(5) + d;
+  auto wimg = [&](int i) {
+    const int l = i < 3 ? i : i + (reg ? 3 : 0);
+    return p.wpf[l];
+  };
+  Frags fr[2];
+  WItem a, b;
+  bool ha = witem(d, true, w, 0, a);
+  if (ha) issue_chunk(fr[0], wimg(a.i), a);
+  for (int c = threadIdx.x; c < nbias; c += FNT) {
+    const int i = c < 256 ? 0 : c < 384 ? 1 : c < 448 ? 2 : c < 576 ? 3 : c < 832 ? 4 : 5;
+    const int l = i < 3 ? i : i + (reg ? 3 : 0);
+    bsm[c] = p.b[l][c - bias_off(i)];
+  }
+  load_block_n<bf16_t, FNT>(reinterpret_cast<const bf16_t *>(p.act[0]), d, r0, xin, ldx);
+  __syncthreads();
+  int layer = 0;
+  auto layer_start = [&](int i) {  // the layer's input (read-only now) to global: rows + packed transposed
+    int K, N;
+    chain_dims(d, i, K, N);
+    if (i > 0) rows_copy_out(xin, ldx, reinterpret_cast<bf16_t *>(p.act[i]), K, r0);
+    if (p.dwpacked) pt_copy_out(xin, ldx, p.hpt[i], K, p.R, r0);
+  };
+  auto advance = [&]() {
+    __syncthreads();
+    bf16_t *tmp = xin;
+    xin = xout;
+    xout = tmp;
+    if (++layer < 6) layer_start(layer);
+  };
+  layer_start(0);
+  f32x16_t acc;
+  auto step = [&](const Frags &F, const WItem &it) {
+    while (layer < it.i) advance();
+    consume_chunk_t(F, xin, ldx, it, acc);
+    if (it.c == it.nch - 1) {
+      const int row = lane & 31, cb = 32 * it.t + 4 * half;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 b4 = *reinterpret_cast<const float4 *>(bsm + bias_off(it.i) + cb + 8 * g);
+        *reinterpret_cast<uint2 *>(xout + row * ldx + cb + 8 * g) =
+            pack4_bf16(fmaxf(acc[4 * g] + b4.x, 0.f), fmaxf(acc[4 * g + 1] + b4.y, 0.f),
+                       fmaxf(acc[4 * g + 2] + b4.z, 0.f), fmaxf(acc[4 * g + 3] + b4.w, 0.f));
+      }
+    }
+  };
+  int q = 0;
+  while (ha) {
+    const bool hb = witem(d, true, w, q + 1, b);
+    if (hb) issue_chunk(fr[1], wimg(b.i), b);
+    step(fr[0], a);
+    if (!hb) break;
+    ha = witem(d, true, w, q + 2, a);
+    if (ha) issue_chunk(fr[0], wimg(a.i), a);
+    step(fr[1], b);
+    q += 2;
+  }
+  while (layer < 6) advance();
+  // D3 = the last layer's output (now xin): rows and D3^T [d][R]
+  rows_copy_out(xin, ldx, reinterpret_cast<bf16_t *>(p.act[6]), d, r0);
+  if (p.act6t) cols_copy_out(xin, ldx, reinterpret_cast<bf16_t *>(p.act6t), d, p.R, r0);
+}
+
+__global__ __launch_bounds__(FNT) void tower_bwd_chain_wide_kernel(TowerP p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int ldx = p.maxw + 8;
+  bf16_t *gin = reinterpret_cast<bf16_t *>(smem);
+  bf16_t *gout = gin + RB * ldx;
+  const int r0 = blockIdx.x * RB;
+  const bool reg = r0 >= p.B;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5;
+  const int row = lane & 31;
+  const int d = p.d;
+  auto wimg = [&](int i) {
+    const int l = i < 3 ? i : i + (reg ? 3 : 0);
+    return p.wpb[l];
+  };
+  Frags fr[2];
+  WItem a, b;
+  bool ha = witem(d, false, w, 0, a);
+  if (ha) issue_chunk(fr[0], wimg(a.i), a);
+  load_block_n<bf16_t, FNT>(reinterpret_cast<const bf16_t *>(p.gD3), d, r0, gin, ldx);
+  __syncthreads();
+  int layer = 5;  // the layer whose incoming gradient gin holds
+  auto layer_start = [&](int i) {  // G_i (read-only now) to global: rows (the dW fallback) + packed
+    int K, N;
+    chain_dims(d, i, K, N);
+    if (i < 5) rows_copy_out(gin, ldx, reinterpret_cast<bf16_t *>(p.gact[i]), N, r0);
+    if (p.dwpacked) pt_copy_out(gin, ldx, p.gpt[i], N, p.R, r0);
+  };
+  auto advance = [&]() {
+    __syncthreads();
+    bf16_t *tmp = gin;
+    gin = gout;
+    gout = tmp;
+    if (--layer >= 0) layer_start(layer);
+  };
+  layer_start(5);
+  f32x16_t acc;
+  uint2 hm[4];
+  auto step = [&](const Frags &F, const WItem &it) {
+    while (layer > it.i) advance();
+    int K, N;
+    chain_dims(d, it.i, K, N);
+    const int cb = 32 * it.t + 4 * half;
+    if (it.c == 0) {  // the layer input's ReLU mask at this lane's accumulator positions
+      const bf16_t *H = reinterpret_cast<const bf16_t *>(p.act[it.i]) + (int64_t)(r0 + row) * K + cb;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) hm[g] = *reinterpret_cast<const uint2 *>(H + 8 * g);
+    }
+    consume_chunk_t(F, gin, ldx, it, acc);
+    if (it.c == it.nch - 1) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float v0 = __uint_as_float(hm[g].x << 16) > 0.f ? acc[4 * g] : 0.f;
+        const float v1 = __uint_as_float(hm[g].x & 0xFFFF0000u) > 0.f ? acc[4 * g + 1] : 0.f;
+        const float v2 = __uint_as_float(hm[g].y << 16) > 0.f ? acc[4 * g + 2] : 0.f;
+        const float v3 = __uint_as_float(hm[g].y & 0xFFFF0000u) > 0.f ? acc[4 * g + 3] : 0.f;
+        if (it.i == 0)
+          *reinterpret_cast<float4 *>(p.gpre1 + (int64_t)(r0 + row) * K + cb + 8 * g) = make_float4(v0, v1, v2, v3);
+        *reinterpret_cast<uint2 *>(gout + row * ldx + cb + 8 * g) = pack4_bf16(v0, v1, v2, v3);
+      }
+    }
+  };
+  int q = 0;
+  while (ha) {
+    const bool hb = witem(d, false, w, q + 1, b);
+    if (hb) issue_chunk(fr[1], wimg(b.i), b);
+    step(fr[0], a);
+    if (!hb) break;
+    ha = witem(d, false, w, q + 2, a);
+    if (ha) issue_chunk(fr[0], wimg(a.i), a);
+    step(fr[1], b);
+    q += 2;
+  }
+  while (layer >= 0) advance();
+  // dPre1 (now gin) for the W1 gradient: packed transposed fragments or dPre1^T [d][ceil64(R)]
+  if (p.gpre1p)
+    pt_copy_out(gin, ldx, p.gpre1p, d, (p.R + 63) & ~63, r0);
+  else if (p.gpre1t)
+    cols_copy_out(gin, ldx, reinterpret_cast<bf16_t *>(p.gpre1t), d, (p.R + 63) & ~63, r0);
+}
+
 // dW partials: one block per (chain layer i, 32-row block): slab[blk][i] = H^T G over the block's
 // rows (A = H^T, B = G from transposed LDS images, MFMA), db = colsum G.  Spreads the slab writes
 // over 6x more CUs than the chain.
@@ -967,8 +1183,16 @@ int make_params(const cc_tower_args *t, TowerP &p) {
   if ((uintptr_t)p.gpre1p & 15) return cc::fail(CC_ERR_ARG, "cc_tower: gpre1p must be 16-B aligned");
   p.slab = t->slab;
   p.slab_elems = slab_off(t->d, 6);
-  p.packed = t->dtype == CC_BF16 && t->d <= 256;
-  const bool fast = p.packed;
+  // packed weight images: d <= 256 (fast kernels, optional) and 256 < d <= 1024 (wide kernels,
+  // which need them; without them the generic 4-wave kernels run)
+  p.packed = t->dtype == CC_BF16;
+  for (int l = 0; l < 9; ++l) {
+    p.wpf[l] = static_cast<const bf16_t *>(t->wpf[l]);
+    p.wpb[l] = static_cast<const bf16_t *>(t->wpb[l]);
+    if (l < (t->R > t->B ? 9 : 6) && (!t->wpf[l] || !t->wpb[l])) p.packed = false;
+  }
+  const bool narrow = t->dtype == CC_BF16 && t->d <= 256;
+  const bool fast = narrow || p.packed;  // the fast (d <= 256) or wide chains run
   p.dwpacked = fast;
   for (int a = 0; a < 6; ++a) {
     p.hpt[a] = static_cast<bf16_t *>(t->hpt[a]);
@@ -976,15 +1200,10 @@ int make_params(const cc_tower_args *t, TowerP &p) {
     if (!t->hpt[a] || !t->gpt[a] || (((uintptr_t)t->hpt[a] | (uintptr_t)t->gpt[a]) & 15)) p.dwpacked = false;
   }
   if (t->B % 16 || t->R % 16) p.dwpacked = false;
-  p.act6p = fast ? static_cast<bf16_t *>(t->act6p) : nullptr;
-  p.act6tp = fast ? static_cast<bf16_t *>(t->act6tp) : nullptr;
+  p.act6p = narrow ? static_cast<bf16_t *>(t->act6p) : nullptr;  // fused D1 / D2 operands: d <= 256
+  p.act6tp = narrow ? static_cast<bf16_t *>(t->act6tp) : nullptr;
   if (((uintptr_t)p.act6p | (uintptr_t)p.act6tp) & 15)
     return cc::fail(CC_ERR_ARG, "cc_tower: packed D3 images must be 16-B aligned");
-  for (int l = 0; l < 9; ++l) {
-    p.wpf[l] = static_cast<const bf16_t *>(t->wpf[l]);
-    p.wpb[l] = static_cast<const bf16_t *>(t->wpb[l]);
-    if (l < (t->R > t->B ? 9 : 6) && (!t->wpf[l] || !t->wpb[l])) p.packed = false;
-  }
   if (p.packed)
     for (int l = 0; l < 9; ++l)
       if ((((uintptr_t)t->wpf[l] | (uintptr_t)t->wpb[l]) & 15) != 0)
@@ -1004,6 +1223,8 @@ extern "C" int cc_tower_fwd(const cc_tower_args *t, void *stream) {
   const size_t lds = (size_t)2 * RB * (p.maxw + 16 / es) * es;
   if (t->dtype == CC_BF16 && p.d <= 256)
     hipLaunchKernelGGL(tower_fwd_fast_kernel, dim3(p.R / RB), dim3(FNT), lds, as_stream(stream), p);
+  else if (t->dtype == CC_BF16 && p.packed)
+    hipLaunchKernelGGL(tower_fwd_wide_kernel, dim3(p.R / RB), dim3(FNT), lds, as_stream(stream), p);
   else if (t->dtype == CC_BF16)
     hipLaunchKernelGGL(tower_fwd_kernel<bf16_t>, dim3(p.R / RB), dim3(NT), lds, as_stream(stream), p);
   else
@@ -1026,6 +1247,8 @@ static int tower_bwd_launch(const cc_tower_args *t, void *stream, bool chain, bo
   if (t->dtype == CC_BF16) {
     if (chain && p.d <= 256)
       hipLaunchKernelGGL(tower_bwd_chain_fast_kernel, gc, dim3(FNT), lds_chain, s, p);
+    else if (chain && p.packed)
+      hipLaunchKernelGGL(tower_bwd_chain_wide_kernel, gc, dim3(FNT), lds_chain, s, p);
     else if (chain)
       hipLaunchKernelGGL(tower_bwd_chain_kernel<bf16_t>, gc, dim3(NT), lds_chain, s, p);
     if (dw) hipLaunchKernelGGL(tower_dw_kernel<bf16_t>, gd, dim3(NT), lds_dw, s, p);

@@ -285,9 +285,10 @@ class Trainer:
             sizes = [int(np.prod(self.layout.shape(n + '/kernel'))) for n in self.tower_layers]
             self.wt_off = np.concatenate([[0], np.cumsum([(n + 63) // 64 * 64 for n in sizes])])
             self.wt = torch.zeros(int(self.wt_off[-1]), **T)
-            # fragment-packed forward/backward weight images for the d <= 256 bf16 tower kernels
-            # (written with wt by cc_tower_transpose; the opt-in fused Adam writes only wt)
-            pack = (self.dtype == L.CC_BF16 and d <= 256 and os.environ.get('CCREC_FUSED_ADAM', '0') != '1'
+            # fragment-packed forward/backward weight images for the bf16 tower kernels (d <= 256:
+            # fast, 256 < d <= 1024: wide; written with wt by cc_tower_transpose and by the Adam
+            # launch; the opt-in fused Adam writes only wt)
+            pack = (self.dtype == L.CC_BF16 and d <= 1024 and os.environ.get('CCREC_FUSED_ADAM', '0') != '1'
                     and os.environ.get('CCREC_TOWER_PACK', '1') != '0')
             self.wpack = torch.zeros(2, int(self.wt_off[-1]), **T) if pack else None
             # ... and D3 as packed operand images of the fused D1 output kernel (cc_dec_bce_dw)
