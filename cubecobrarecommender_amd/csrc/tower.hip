@@ -599,6 +599,22 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
 // so a tile's epilogue never waits for the other waves' reads.
 constexpr int WBIAS_MAX = 832 + 1024;  // bias_off(5) + d
 
+// Workgroup barrier over LDS only: __syncthreads' release fence also drains every outstanding
+// global access of the wave (vmcnt(0)) — the prefetched fragments of the next item and the
+// copy-out stores — while only the LDS images are handed between the waves here.
+__device__ __forceinline__ void wide_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// a[k] of a kernel-argument pointer array with a runtime layer index, as a select chain over
+// constant-offset reads: indexing the array directly compiles to a global load whose vmcnt wait
+// (in-order counter) drained the in-flight fragments before every item
+template <typename T, int N>
+__device__ __forceinline__ T pick(const T (&a)[N], int k) {
+  T r = a[0];
+#pragma unroll
+  for (int j = 1; j < N; ++j) r = k == j ? a[j] : r;
+  return r;
+}
+
 struct WItem {
   int i, t, c, nch, red;  // chain layer, 32-column tile, reduction chunk, chunks per tile, reduction
 };
@@ -626,16 +642,26 @@ __device__ __forceinline__ bool witem(int d, bool fwd, int w, int q, WItem &it) 
   }
   return false;
 }
-// fragments j = 16c .. 16c + 15 of tile t of a packed image with reduction `red`
+// fragments j = 16c .. 16c + 15 of tile t of a packed image with reduction `red`.  Always 16
+// unconditional loads (a chunk shorter than 16 fragments re-reads its last one: same lines, L1
+// hits): a conditional load compiles to a branch, and the compiler then drains vmcnt to zero
+// before it — which serialises the item pipeline (the first d = 1024 forward ran 50 us that way)
 __device__ __forceinline__ void issue_chunk(Frags &F, const bf16_t *__restrict__ P, const WItem &it) {
   const int lane = threadIdx.x & 63;
   const bf16_t *base = P + (((int64_t)it.t * (it.red / 16) + 16 * it.c) * 64 + lane) * 8;
-  const int nf = min(FB, it.red / 16 - 16 * it.c);
+  const int last = min(FB, it.red / 16 - 16 * it.c) - 1;
 #pragma unroll
-  for (int j = 0; j < FB; ++j)
-    if (j < nf) F.f[j] = *reinterpret_cast<const bf16x8_t *>(base + j * 512);
+  for (int j = 0; j < FB; ++j) F.f[j] = *reinterpret_cast<const bf16x8_t *>(base + min(j, last) * 512);
 }
-// acc (+)= chunk c of the transposed product (packed weights = A, LDS rows = B; see consume_frags_t)
+template <int NF>
+__device__ __forceinline__ void mfma_chunk(const Frags &F, const bf16_t *arow, f32x16_t &acc) {
+#pragma unroll
+  for (int j = 0; j < NF; ++j)
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.f[j], *reinterpret_cast<const bf16x8_t *>(arow + 16 * j), acc,
+                                                  0, 0, 0);
+}
+// acc (+)= chunk c of the transposed product (packed weights = A, LDS rows = B; see consume_frags_t).
+// A chunk holds 16, 12, 8 or 4 fragments (reductions are multiples of 64): static MFMA counts.
 __device__ __forceinline__ void consume_chunk_t(const Frags &F, const bf16_t *A, int lda, const WItem &it,
                                                 f32x16_t &acc) {
   const int lane = threadIdx.x & 63;
@@ -645,11 +671,14 @@ __device__ __forceinline__ void consume_chunk_t(const Frags &F, const bf16_t *A,
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   }
   const int nf = min(FB, it.red / 16 - 16 * it.c);
-#pragma unroll
-  for (int j = 0; j < FB; ++j)
-    if (j < nf)
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.f[j], *reinterpret_cast<const bf16x8_t *>(arow + 16 * j), acc,
-                                                    0, 0, 0);
+  if (nf == 16)
+    mfma_chunk<16>(F, arow, acc);
+  else if (nf == 12)
+    mfma_chunk<12>(F, arow, acc);
+  else if (nf == 8)
+    mfma_chunk<8>(F, arow, acc);
+  else
+    mfma_chunk<4>(F, arow, acc);
 }
 
 __global__ __launch_bounds__(FNT) void tower_fwd_wide_kernel(TowerP p) {
@@ -660,12 +689,9 @@ __global__ __launch_bounds__(FNT) void tower_fwd_wide_kernel(TowerP p) {
   bf16_t *xout = xin + RB * ldx;
   const int r0 = blockIdx.x * RB;
   const bool reg = r0 >= p.B;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, half = lane >> 5;
   const int d = p.d, nbias = bias_off(5) + d;
-  auto wimg = [&](int i) {
-    const int l = i < 3 ? i : i + (reg ? 3 : 0);
-    return p.wpf[l];
-  };
+  auto wimg = [&](int i) { return pick(p.wpf, i < 3 ? i : i + (reg ? 3 : 0)); };
   Frags fr[2];
   WItem a, b;
   bool ha = witem(d, true, w, 0, a);
@@ -676,16 +702,16 @@ __global__ __launch_bounds__(FNT) void tower_fwd_wide_kernel(TowerP p) {
     bsm[c] = p.b[l][c - bias_off(i)];
   }
   load_block_n<bf16_t, FNT>(reinterpret_cast<const bf16_t *>(p.act[0]), d, r0, xin, ldx);
-  __syncthreads();
+  wide_barrier();
   int layer = 0;
   auto layer_start = [&](int i) {  // the layer's input (read-only now) to global: rows + packed transposed
     int K, N;
     chain_dims(d, i, K, N);
-    if (i > 0) rows_copy_out(xin, ldx, reinterpret_cast<bf16_t *>(p.act[i]), K, r0);
-    if (p.dwpacked) pt_copy_out(xin, ldx, p.hpt[i], K, p.R, r0);
+    if (i > 0) rows_copy_out(xin, ldx, reinterpret_cast<bf16_t *>(pick(p.act, i)), K, r0);
+    if (p.dwpacked) pt_copy_out(xin, ldx, pick(p.hpt, i), K, p.R, r0);
   };
   auto advance = [&]() {
-    __syncthreads();
+    wide_barrier();
     bf16_t *tmp = xin;
     xin = xout;
     xout = tmp;
@@ -731,28 +757,25 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_wide_kernel(TowerP p) {
   bf16_t *gout = gin + RB * ldx;
   const int r0 = blockIdx.x * RB;
   const bool reg = r0 >= p.B;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, half = lane >> 5;
   const int row = lane & 31;
   const int d = p.d;
-  auto wimg = [&](int i) {
-    const int l = i < 3 ? i : i + (reg ? 3 : 0);
-    return p.wpb[l];
-  };
+  auto wimg = [&](int i) { return pick(p.wpb, i < 3 ? i : i + (reg ? 3 : 0)); };
   Frags fr[2];
   WItem a, b;
   bool ha = witem(d, false, w, 0, a);
   if (ha) issue_chunk(fr[0], wimg(a.i), a);
   load_block_n<bf16_t, FNT>(reinterpret_cast<const bf16_t *>(p.gD3), d, r0, gin, ldx);
-  __syncthreads();
+  wide_barrier();
   int layer = 5;  // the layer whose incoming gradient gin holds
   auto layer_start = [&](int i) {  // G_i (read-only now) to global: rows (the dW fallback) + packed
     int K, N;
     chain_dims(d, i, K, N);
-    if (i < 5) rows_copy_out(gin, ldx, reinterpret_cast<bf16_t *>(p.gact[i]), N, r0);
-    if (p.dwpacked) pt_copy_out(gin, ldx, p.gpt[i], N, p.R, r0);
+    if (i < 5) rows_copy_out(gin, ldx, reinterpret_cast<bf16_t *>(pick(p.gact, i)), N, r0);
+    if (p.dwpacked) pt_copy_out(gin, ldx, pick(p.gpt, i), N, p.R, r0);
   };
   auto advance = [&]() {
-    __syncthreads();
+    wide_barrier();
     bf16_t *tmp = gin;
     gin = gout;
     gout = tmp;
@@ -761,16 +784,21 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_wide_kernel(TowerP p) {
   layer_start(5);
   f32x16_t acc;
   uint2 hm[4];
+  // the ReLU mask of item it's layer input at this lane's accumulator positions, loaded BEFORE
+  // the next item's fragments are issued (vmcnt retires in order: the epilogue's wait for the
+  // mask then leaves those fragments in flight); every chunk, no branch
+  auto mask_load = [&](const WItem &it) {
+    int K, N;
+    chain_dims(d, it.i, K, N);
+    const bf16_t *H = reinterpret_cast<const bf16_t *>(pick(p.act, it.i)) + (int64_t)(r0 + row) * K + 32 * it.t + 4 * half;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) hm[g] = *reinterpret_cast<const uint2 *>(H + 8 * g);
+  };
   auto step = [&](const Frags &F, const WItem &it) {
     while (layer > it.i) advance();
     int K, N;
     chain_dims(d, it.i, K, N);
     const int cb = 32 * it.t + 4 * half;
-    if (it.c == 0) {  // the layer input's ReLU mask at this lane's accumulator positions
-      const bf16_t *H = reinterpret_cast<const bf16_t *>(p.act[it.i]) + (int64_t)(r0 + row) * K + cb;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) hm[g] = *reinterpret_cast<const uint2 *>(H + 8 * g);
-    }
     consume_chunk_t(F, gin, ldx, it, acc);
     if (it.c == it.nch - 1) {
 #pragma unroll
@@ -787,10 +815,12 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_wide_kernel(TowerP p) {
   };
   int q = 0;
   while (ha) {
+    mask_load(a);
     const bool hb = witem(d, false, w, q + 1, b);
     if (hb) issue_chunk(fr[1], wimg(b.i), b);
     step(fr[0], a);
     if (!hb) break;
+    mask_load(b);
     ha = witem(d, false, w, q + 2, a);
     if (ha) issue_chunk(fr[0], wimg(a.i), a);
     step(fr[1], b);
