@@ -10,6 +10,7 @@
 //   the batch rows containing card r; their dPre rows (L2-resident, [R, d] fp32) are summed in
 //   ascending row order — deterministic, and dense over every row (rows absent from the batch
 //   get an exact zero gradient, as TF's dense MatMul gradient gives).
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -506,7 +507,247 @@ __global__ __launch_bounds__(256, 2) void embed_grad_pk_kernel(const bf16_t *__r
     }
 }
 
+// cc_embed_grad_cs: the same product by COLUMN SLICE.  The row-tile kernels above give every block
+// all d columns, so every block re-reads the whole dPre1 image (256 KB at R = 512) from L2 —
+// 88 MB for the step at ~70 GB/s per CU, and their 344 blocks leave the 2-block CUs on the
+// critical path.  Here block (row chunk rc, slice cs) owns 32 columns: it stages its slice of
+// dPre1 (nk = ceil64(R)/16 MFMA B fragments, 1 KB each) in LDS once, and each of its 8 waves
+// takes 32-row tiles of the chunk: the tile's bit words go straight into registers (a lane holds
+// its row's XWM words), A fragments come from a byte LUT in LDS (256 values x 16 lane copies,
+// 16 B each: one conflict-free ds_read_b128) instead of ~20 VALU bit tricks per fragment.  Same MFMA k
+// order per tile as the kernels above: the same fp32 results.  The chunk's xt words are cleared
+// by the last of its slice blocks to finish (a ticket per chunk, reset by that block: no spin, no
+// extra launch).
+constexpr int CS_NT = 512;                     // 8 waves, ~one block per CU
+constexpr int cs_tpw(int xwm) { return xwm <= 32 ? 3 : 1; }      // tiles per wave (registers)
+constexpr int cs_lut_copies(int xwm) { return xwm <= 32 ? 16 : 4; }  // 4 at R > 1024: LDS
+constexpr int cs_lut_bytes(int xwm) { return 256 * 16 * cs_lut_copies(xwm); }  // byte -> 8 bf16 (16 B)
+__device__ __forceinline__ uint4 byte_bf16(uint32_t e) {  // 8 bits -> 8 bf16 of 1.0 / 0.0
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (((e >> (2 * i)) & 1u) ? 0x3F80u : 0u) | (((e >> (2 * i + 1)) & 1u) ? 0x3F800000u : 0u);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+template <bool PK, int XWM, bool VEC>
+__global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *__restrict__ gsrc, int V, int d, int R,
+                                                            int RP, int tpc, uint32_t *xt,
+                                                            float *__restrict__ grad,
+                                                            float *__restrict__ bias_grad, uint32_t *tickets) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
+  const int nsl = d >> 5, cs = blockIdx.x % nsl, rc = blockIdx.x / nsl;
+  const int RPE = (R + 63) & ~63, nk = RPE >> 4;
+  const int XW = (R + 31) >> 5;  // words per xt row; the product runs over XWM words (zeros past XW)
+  const int rows_total = V + (bias_grad ? 1 : 0);
+  const int NTL = (rows_total + 31) >> 5;
+  const int t0 = rc * tpc, nt = min(NTL, t0 + tpc) - t0;
+  const int v0 = 32 * t0;
+  EG_PROBE(0);
+  constexpr int LC = cs_lut_copies(XWM);
+  bf16_t *Bs = reinterpret_cast<bf16_t *>(smem);                  // fragment j at (j * 64 + lane) * 8
+  unsigned char *lut = smem + (size_t)2 * XWM * 1024;             // [256 values][16 copies] x 16 B
+  // ---- every global read first: the bit words of all the wave's tiles (wave w takes tiles w,
+  // w + 8, ... of the chunk; a lane holds its row's XWM words per tile), then the B slice and LUT
+  // (every global load below is unconditional — clamped address, then a select — so the
+  // compiler's vmcnt waits stay counted: a load behind a branch made it drain to zero, which
+  // serialised the staging loads and the next tile's bit prefetch)
+  auto load_bits = [&](int t, uint32_t (&wd)[XWM]) {
+    const int v = v0 + 32 * t + (lane & 31);  // this lane's A row
+    const bool real = t < nt && v < V;
+    const uint32_t *src = xt + (int64_t)(real ? v : 0) * XW;
+    if constexpr (VEC) {  // XW % 4 == 0: 16-B loads
+#pragma unroll
+      for (int q = 0; q < XWM / 4; ++q) {
+        const uint4 x4 = *reinterpret_cast<const uint4 *>(src + 4 * min(q, XW / 4 - 1));
+        wd[4 * q] = x4.x;
+        wd[4 * q + 1] = x4.y;
+        wd[4 * q + 2] = x4.z;
+        wd[4 * q + 3] = x4.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < XWM; ++q) wd[q] = src[min(q, XW - 1)];
+    }
+    const bool brow = t < nt && v == V && bias_grad;  // the bias row: every batch row
+#pragma unroll
+    for (int q = 0; q < XWM; ++q) {
+      const uint32_t bm = (q == XW - 1 && (R & 31)) ? (1u << (R & 31)) - 1u : 0xFFFFFFFFu;
+      wd[q] = q >= XW ? 0u : real ? wd[q] : brow ? bm : 0u;
+    }
+  };
+  constexpr int NW = CS_NT / 64;
+  constexpr int TPW = cs_tpw(XWM);  // tiles per wave (the host sizes tpc <= NW * TPW)
+  uint32_t wds[TPW][XWM];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) load_bits(w + NW * i, wds[i]);
+  // the B slice: 2 XWM fragments (those past nk are zero), a compile-time count per thread
+  constexpr int NBT = 2 * XWM * 64 / CS_NT;
+  {
+    uint4 v[NBT];
+    const uint4 *bsrc = reinterpret_cast<const uint4 *>(gsrc + (int64_t)cs * (RP / 16) * 512);
+#pragma unroll
+    for (int u = 0; u < NBT; ++u) {
+      const int f = u * CS_NT + tid, fc = min(f, nk * 64 - 1);
+      if constexpr (PK) {  // packed transposed dPre1: the slice's fragments are one contiguous run
+        v[u] = bsrc[fc];
+      } else {  // dPre1^T [d][RP]: fragment (j, lane) = 8 consecutive rows of column 32 cs + (lane & 31)
+        const int j = fc >> 6, ln = fc & 63;
+        v[u] = *reinterpret_cast<const uint4 *>(gsrc + (int64_t)(32 * cs + (ln & 31)) * RP + 16 * j + 8 * (ln >> 5));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NBT; ++u) {
+      const int f = u * CS_NT + tid;
+      reinterpret_cast<uint4 *>(Bs)[f] = (f >> 6) < nk ? v[u] : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  for (int e = tid; e < 256 * LC; e += CS_NT) reinterpret_cast<uint4 *>(lut)[e] = byte_bf16((uint32_t)(e / LC));
+  EG_PROBE(1);
+  __syncthreads();  // (its release fence: every load of the block, bit words included, has returned)
+  EG_PROBE(2);
+  // the chunk's ticket now, before any store of this block: the last of the chunk's nsl slice
+  // blocks to get here clears the chunk's xt words at its end; the atomic's return is read there
+  // (it was issued before the stores, so that wait does not drain them)
+  uint32_t tk = 0u;
+  if (tid == 0) tk = __hip_atomic_fetch_add(&tickets[rc], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // ---- tiles
+  // the A fragment of a byte: one ds_read_b128 from this lane's copy (lane & 15: the 16 lanes a
+  // b128 read serves per cycle hit 16 distinct bank quads, whatever their bytes) — full rate even
+  // at one or two waves per SIMD, where 8-B LDS reads run at a fifth of it
+  const unsigned char *lutl = lut + (lane % LC) * 16;
+  const uint32_t sh = 8u * (uint32_t)half;
+  // XWM = 16 (R <= 512, the headline shape): the wave keeps the whole B slice in 128 VGPRs, read
+  // from LDS once — the tile loop then reads only its A fragments from LDS (at two 1-KB LDS reads
+  // per MFMA the LDS array, not the MFMA, set the pace)
+  constexpr bool BREG = XWM == 16;
+  bf16x8_t breg[BREG ? 2 * XWM : 1];
+  if constexpr (BREG) {
+#pragma unroll
+    for (int k = 0; k < 2 * XWM; ++k) breg[k] = *reinterpret_cast<const bf16x8_t *>(Bs + (k * 64 + lane) * 8);
+  }
+  auto tile = [&](int t, const uint32_t (&wd)[XWM]) {
+    f32x16_t acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    // A fragment of k-step k (word k/2, half-word k%2, this lane's byte): one LUT read; B: one
+    // ds_read_b128 of the staged slice.  Groups of CS_G k-steps: the next group's 2 CS_G reads are
+    // issued (sched_barrier) before this group's MFMAs, so the LDS latency runs under them.  The
+    // B address is made opaque per tile so the compiler does not hoist the whole slice into VGPRs.
+    constexpr int CS_G = 4, NG = 2 * XWM / CS_G;
+    uint32_t boff = (uint32_t)lane * 16u;  // byte offset of this lane's fragment slot in Bs
+    asm volatile("" : "+v"(boff));
+    auto fetch = [&](int g, bf16x8_t (&da)[CS_G], bf16x8_t (&db)[CS_G]) {
+#pragma unroll
+      for (int u = 0; u < CS_G; ++u) {
+        const int k = CS_G * g + u;
+        const uint32_t s = 16u * (uint32_t)(k & 1) + sh;
+        da[u] = *reinterpret_cast<const bf16x8_t *>(lutl + __builtin_amdgcn_ubfe(wd[k >> 1], s, 8) * (16 * LC));
+        if constexpr (BREG)
+          db[u] = breg[k];
+        else
+          db[u] = *reinterpret_cast<const bf16x8_t *>(reinterpret_cast<const unsigned char *>(Bs) + boff + k * 1024);
+      }
+    };
+    bf16x8_t af[2][CS_G], bf[2][CS_G];
+    fetch(0, af[0], bf[0]);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (g + 1 < NG) fetch(g + 1, af[(g + 1) & 1], bf[(g + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < CS_G; ++u)  // operands swapped: acc = (dW1 tile)^T, see below
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[g & 1][u], af[g & 1][u], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // With the dPre1 fragments as the MFMA's A operand and the bit fragments as its B operand (the
+    // same registers), lane l holds W1 row v0 + 32 t + (l & 31) and the slice's columns
+    // 8 g + 4 (l >> 5) .. +3, g = 0..3: four 16-B stores per lane instead of sixteen 4-B ones.
+    const int vr = v0 + 32 * t + (lane & 31);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c0 = 32 * cs + 8 * g + 4 * half;
+      const float4 q = make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
+      if (vr < V)
+        *reinterpret_cast<float4 *>(grad + (int64_t)vr * d + c0) = q;
+      else if (vr == V && bias_grad)
+        *reinterpret_cast<float4 *>(bias_grad + c0) = q;
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < TPW; ++i)
+    if (w + NW * i < nt) tile(w + NW * i, wds[i]);
+  EG_PROBE(3);
+  if (tid == 0) last = tk == (uint32_t)(nsl - 1);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only: no store drain
+  if (last) {
+    const int vend = min(V, v0 + 32 * nt);
+    for (int64_t i = (int64_t)v0 * XW + tid; i < (int64_t)vend * XW; i += CS_NT) xt[i] = 0u;
+    if (tid == 0) __hip_atomic_store(&tickets[rc], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  EG_PROBE(15);
+}
+
+// launch geometry of cc_embed_grad_cs: 32-row tiles per chunk and the LDS size
+void cs_plan(int V, int d, int R, bool bias, int &tpc, int &nrc, size_t &lds) {
+  const int RPE = (R + 63) & ~63;
+  const int NTL = (V + (bias ? 1 : 0) + 31) / 32;
+  const int xwm = RPE / 32 <= 16 ? 16 : RPE / 32 <= 32 ? 32 : 64;  // the kernel's XWM
+  const int nsl = d / 32;
+  // ~one block per CU (the slice is staged once per block), at most cs_tpw tiles per wave
+  nrc = std::max(std::max(1, std::min(NTL, 256 / nsl)), (int)cdiv(NTL, (CS_NT / 64) * cs_tpw(xwm)));
+  tpc = (int)cdiv(NTL, nrc);
+  nrc = (int)cdiv(NTL, tpc);
+  lds = (size_t)2 * xwm * 1024 + cs_lut_bytes(xwm);
+}
+
 }  // namespace
+
+extern "C" int32_t cc_embed_grad_cs_tickets(int32_t V, int32_t d, int32_t R) {
+  if (V <= 0 || d < 32 || R <= 0) return 0;
+  int tpc, nrc;
+  size_t lds;
+  cs_plan(V, d, R, true, tpc, nrc, lds);
+  return nrc;
+}
+
+extern "C" int cc_embed_grad_cs(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R, int32_t ld_t,
+                                uint32_t *xt_bits, float *grad, float *bias_grad, uint32_t *tickets, void *stream) {
+  CC_REQUIRE(dpre && xt_bits && grad && tickets, "cc_embed_grad_cs: null pointer");
+  CC_REQUIRE((((uintptr_t)grad | (uintptr_t)bias_grad) & 15) == 0, "cc_embed_grad_cs: grad / bias_grad 16-B aligned");
+  CC_REQUIRE(d % 32 == 0 && d >= 32 && d <= 4096, "cc_embed_grad_cs: d must be a multiple of 32");
+  CC_REQUIRE(V > 0 && R > 0 && R <= 2048, "cc_embed_grad_cs: V > 0, R in 1..2048");
+  CC_REQUIRE(ld_t % 64 == 0 && ld_t >= R && ((uintptr_t)dpre % 16) == 0,
+             "cc_embed_grad_cs: ld_t must be a multiple of 64 covering R, dPre1 image 16-B aligned");
+  int tpc, nrc;
+  size_t lds;
+  cs_plan(V, d, R, bias_grad != nullptr, tpc, nrc, lds);
+  CC_REQUIRE(lds <= 160 * 1024 - 64, "cc_embed_grad_cs: R too large for the LDS stage");
+  const dim3 grid((unsigned)(nrc * (d / 32)));
+  const int xw = ((R + 63) & ~63) / 32;  // bit words per row in the product
+  hipStream_t s = as_stream(stream);
+  const bool vec = ((R + 31) / 32) % 4 == 0;  // xt rows 16-B aligned
+#define CS_LAUNCH(PKV, XWMV, VECV)                                                                          \
+  hipLaunchKernelGGL((embed_grad_cs_kernel<PKV, XWMV, VECV>), grid, dim3(CS_NT), lds, s, (const bf16_t *)dpre, \
+                     V, d, R, ld_t, tpc, xt_bits, grad, bias_grad, tickets)
+#define CS_LAUNCH2(XWMV)                                     \
+  if (packed) {                                              \
+    if (vec) CS_LAUNCH(true, XWMV, true); else CS_LAUNCH(true, XWMV, false);   \
+  } else {                                                   \
+    if (vec) CS_LAUNCH(false, XWMV, true); else CS_LAUNCH(false, XWMV, false); \
+  }
+  if (xw <= 16) {
+    CS_LAUNCH2(16)
+  } else if (xw <= 32) {
+    CS_LAUNCH2(32)
+  } else {
+    CS_LAUNCH2(64)
+  }
+#undef CS_LAUNCH2
+#undef CS_LAUNCH
+  CC_LAUNCH_CHECK("embed_grad_cs_kernel");
+  return CC_OK;
+}
 
 extern "C" int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const float *bias, int32_t V,
                                         int32_t d, int32_t R, const int32_t *x_cnt,

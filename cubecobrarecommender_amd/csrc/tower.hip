@@ -301,6 +301,8 @@ __global__ __launch_bounds__(NT) void tower_bwd_chain_kernel(TowerP p) {
 }
 
 // ------------------------------------------------------------------ bf16 fast path (d <= 256)
+// (templated on d: every layer's widths are compile-time constants, so no fragment load or MFMA
+// sits behind a branch — a conditional load makes the compiler drain vmcnt before it)
 // Same math as the kernels above, shaped for latency: 8 waves, one 32-column output tile per
 // wave per layer, and the NEXT layer's weight fragments are loaded into registers while the
 // current layer's MFMAs run — weights do not depend on the activations, so every layer after
@@ -432,6 +434,12 @@ __device__ __forceinline__ int bias_off(int i) {
   return i <= 0 ? 0 : i == 1 ? 256 : i == 2 ? 384 : i == 3 ? 448 : i == 4 ? 576 : 832;
 }
 
+// Workgroup barrier over LDS only: the chains hand only LDS images between their waves, and
+// __syncthreads' release fence would also drain every outstanding global access (the next
+// layer's prefetched weight fragments, the copy-out stores) at each layer boundary.
+__device__ __forceinline__ void fast_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int D>
 __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ __attribute__((aligned(16))) float bsm[BIAS_MAX];
@@ -441,12 +449,12 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
   const int r0 = blockIdx.x * RB;
   const bool reg = r0 >= p.B;
   const int t = threadIdx.x >> 6, lane = threadIdx.x & 63, half = lane >> 5;
-  const int nbias = bias_off(5) + p.d;
+  const int nbias = bias_off(5) + D;
   Frags fr[2];
   TOWER_PROBE(0);
   // the block's input rows first (they gate the first MFMA), then the biases, then the weights
   RowRegs rg;
-  rows_issue(rg, reinterpret_cast<const bf16_t *>(p.act[0]), p.d, r0);
+  rows_issue(rg, reinterpret_cast<const bf16_t *>(p.act[0]), D, r0);
   float bv[3];
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
@@ -461,7 +469,7 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
   auto issue = [&](int i, int slot) {
     const int l = i < 3 ? i : i + (reg ? 3 : 0);
     int K, N;
-    chain_dims(p.d, i, K, N);
+    chain_dims(D, i, K, N);
     if (t < N / 32) {
       if (p.packed)
         issue_frags_packed(fr[slot], p.wpf[l], K, t);
@@ -470,19 +478,19 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
     }
   };
   issue(0, 0);
-  rows_store(rg, p.d, X0, ldx);
+  rows_store(rg, D, X0, ldx);
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
     const int c = (int)threadIdx.x + q * FNT;
     if (c < nbias) bsm[c] = bv[q];
   }
-  __syncthreads();
+  fast_barrier();
   TOWER_PROBE(1);
   bf16_t *xin = X0, *xout = X1;
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     int K, N;
-    chain_dims(p.d, i, K, N);
+    chain_dims(D, i, K, N);
     if (i < 5) issue(i + 1, (i + 1) & 1);  // next layer's weights fly during this layer
     f32x16_t acc;
     if (t < N / 32) consume_frags_t(fr[i & 1], xin, ldx, K, acc);
@@ -502,7 +510,7 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
       }
       TOWER_PROBE(3 + 3 * i);
     }
-    __syncthreads();
+    fast_barrier();
     TOWER_PROBE(4 + 3 * i);
     bf16_t *tmp = xin;
     xin = xout;
@@ -510,7 +518,7 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
   }
   // D3 (the last layer's output): rows, D3^T [d][R], and the packed operand images of the fused
   // output-layer kernel
-  const int dd = p.d;
+  const int dd = D;
   rows_copy_out(xin, ldx, reinterpret_cast<bf16_t *>(p.act[6]), dd, r0);
   if (p.act6t) cols_copy_out(xin, ldx, reinterpret_cast<bf16_t *>(p.act6t), dd, p.R, r0);
   if (p.act6p) {  // D3 as the logits' A operand: fragments (blockIdx.x, j)
@@ -523,6 +531,7 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
   if (p.act6tp) pt_copy_out(xin, ldx, p.act6tp, dd, p.R, r0);  // D3^T: the dWo A operand
 }
 
+template <int D>
 __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int ldx = p.maxw + 8;
@@ -535,7 +544,7 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
   auto issue_layer = [&](int i, int slot) {
     const int l = i < 3 ? i : i + (reg ? 3 : 0);
     int K, N;
-    chain_dims(p.d, i, K, N);
+    chain_dims(D, i, K, N);
     if (t < K / 32) {
       if (p.packed)
         issue_frags_packed(fr[slot], p.wpb[l], N, t);
@@ -544,14 +553,14 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
     }
   };
   RowRegs rg;
-  rows_issue(rg, reinterpret_cast<const bf16_t *>(p.gD3), p.d, r0);
+  rows_issue(rg, reinterpret_cast<const bf16_t *>(p.gD3), D, r0);
   issue_layer(5, 1);
-  rows_store(rg, p.d, Gr, ldx);
-  __syncthreads();
+  rows_store(rg, D, Gr, ldx);
+  fast_barrier();
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
     int K, N;
-    chain_dims(p.d, i, K, N);
+    chain_dims(D, i, K, N);
     if (i > 0) issue_layer(i - 1, (i - 1) & 1);
     // the layer input's ReLU mask at this lane's accumulator positions: lands during the MFMAs
     uint2 hm[4];
@@ -566,7 +575,7 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
     // MFMAs run: rows (the dW fallback) and packed transposed for the dW kernel
     if (i < 5) rows_copy_out(Gr, ldx, reinterpret_cast<bf16_t *>(p.gact[i]), N, r0);
     if (p.dwpacked) pt_copy_out(Gr, ldx, p.gpt[i], N, p.R, r0);
-    __syncthreads();  // every wave has finished reading Gr
+    fast_barrier();  // every wave has finished reading Gr
     if (t < K / 32) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -579,7 +588,7 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
         *reinterpret_cast<uint2 *>(Gr + row * ldx + cb + 8 * g) = pack4_bf16(v0, v1, v2, v3);
       }
     }
-    __syncthreads();
+    fast_barrier();
     // (G_{i-1} for i > 0 is copied out during the next layer's MFMAs)
     if (i == 0 && p.gpre1p)  // dPre1 as packed transposed fragments (reduction ceil64(R)): cc_embed_grad_packed
       pt_copy_out(Gr, ldx, p.gpre1p, K, (p.R + 63) & ~63, r0);
@@ -599,10 +608,6 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
 // so a tile's epilogue never waits for the other waves' reads.
 constexpr int WBIAS_MAX = 832 + 1024;  // bias_off(5) + d
 
-// Workgroup barrier over LDS only: __syncthreads' release fence also drains every outstanding
-// global access of the wave (vmcnt(0)) — the prefetched fragments of the next item and the
-// copy-out stores — while only the LDS images are handed between the waves here.
-__device__ __forceinline__ void wide_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // a[k] of a kernel-argument pointer array with a runtime layer index, as a select chain over
 // constant-offset reads: indexing the array directly compiles to a global load whose vmcnt wait
@@ -702,7 +707,7 @@ __global__ __launch_bounds__(FNT) void tower_fwd_wide_kernel(TowerP p) {
     bsm[c] = p.b[l][c - bias_off(i)];
   }
   load_block_n<bf16_t, FNT>(reinterpret_cast<const bf16_t *>(p.act[0]), d, r0, xin, ldx);
-  wide_barrier();
+  fast_barrier();
   int layer = 0;
   auto layer_start = [&](int i) {  // the layer's input (read-only now) to global: rows + packed transposed
     int K, N;
@@ -711,7 +716,7 @@ __global__ __launch_bounds__(FNT) void tower_fwd_wide_kernel(TowerP p) {
     if (p.dwpacked) pt_copy_out(xin, ldx, pick(p.hpt, i), K, p.R, r0);
   };
   auto advance = [&]() {
-    wide_barrier();
+    fast_barrier();
     bf16_t *tmp = xin;
     xin = xout;
     xout = tmp;
@@ -766,7 +771,7 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_wide_kernel(TowerP p) {
   bool ha = witem(d, false, w, 0, a);
   if (ha) issue_chunk(fr[0], wimg(a.i), a);
   load_block_n<bf16_t, FNT>(reinterpret_cast<const bf16_t *>(p.gD3), d, r0, gin, ldx);
-  wide_barrier();
+  fast_barrier();
   int layer = 5;  // the layer whose incoming gradient gin holds
   auto layer_start = [&](int i) {  // G_i (read-only now) to global: rows (the dW fallback) + packed
     int K, N;
@@ -775,7 +780,7 @@ __global__ __launch_bounds__(FNT) void tower_bwd_chain_wide_kernel(TowerP p) {
     if (p.dwpacked) pt_copy_out(gin, ldx, pick(p.gpt, i), N, p.R, r0);
   };
   auto advance = [&]() {
-    wide_barrier();
+    fast_barrier();
     bf16_t *tmp = gin;
     gin = gout;
     gout = tmp;
@@ -1251,8 +1256,16 @@ extern "C" int cc_tower_fwd(const cc_tower_args *t, void *stream) {
   if (rc) return rc;
   const int es = t->dtype == CC_BF16 ? 2 : 4;
   const size_t lds = (size_t)2 * RB * (p.maxw + 16 / es) * es;
-  if (t->dtype == CC_BF16 && p.d <= 256)
-    hipLaunchKernelGGL(tower_fwd_fast_kernel, dim3(p.R / RB), dim3(FNT), lds, as_stream(stream), p);
+  if (t->dtype == CC_BF16 && p.d <= 256) {
+    const dim3 g(p.R / RB), b(FNT);
+    hipStream_t s = as_stream(stream);
+    switch (p.d) {
+      case 64: hipLaunchKernelGGL(tower_fwd_fast_kernel<64>, g, b, lds, s, p); break;
+      case 128: hipLaunchKernelGGL(tower_fwd_fast_kernel<128>, g, b, lds, s, p); break;
+      case 192: hipLaunchKernelGGL(tower_fwd_fast_kernel<192>, g, b, lds, s, p); break;
+      default: hipLaunchKernelGGL(tower_fwd_fast_kernel<256>, g, b, lds, s, p); break;
+    }
+  }
   else if (t->dtype == CC_BF16 && p.packed)
     hipLaunchKernelGGL(tower_fwd_wide_kernel, dim3(p.R / RB), dim3(FNT), lds, as_stream(stream), p);
   else if (t->dtype == CC_BF16)
@@ -1275,8 +1288,14 @@ static int tower_bwd_launch(const cc_tower_args *t, void *stream, bool chain, bo
   const dim3 gc(p.R / RB), gd(6 * (p.R / RB));
   hipStream_t s = as_stream(stream);
   if (t->dtype == CC_BF16) {
-    if (chain && p.d <= 256)
-      hipLaunchKernelGGL(tower_bwd_chain_fast_kernel, gc, dim3(FNT), lds_chain, s, p);
+    if (chain && p.d <= 256) {
+      switch (p.d) {
+        case 64: hipLaunchKernelGGL(tower_bwd_chain_fast_kernel<64>, gc, dim3(FNT), lds_chain, s, p); break;
+        case 128: hipLaunchKernelGGL(tower_bwd_chain_fast_kernel<128>, gc, dim3(FNT), lds_chain, s, p); break;
+        case 192: hipLaunchKernelGGL(tower_bwd_chain_fast_kernel<192>, gc, dim3(FNT), lds_chain, s, p); break;
+        default: hipLaunchKernelGGL(tower_bwd_chain_fast_kernel<256>, gc, dim3(FNT), lds_chain, s, p); break;
+      }
+    }
     else if (chain && p.packed)
       hipLaunchKernelGGL(tower_bwd_chain_wide_kernel, gc, dim3(FNT), lds_chain, s, p);
     else if (chain)

@@ -276,7 +276,7 @@ class Trainer:
         self.gPre1T = torch.zeros(d, self.RP, **T) if self.embed_mfma else None
         if self.mx8 and not self.fused_tower:
             raise ValueError('fp8 needs the fused towers (fused_tower=True, B % 32 == 0)')
-        self.wpack = self.D3p = self.D3tp = self.hpt = self.gpt = self.gpre1p = None
+        self.wpack = self.D3p = self.D3tp = self.hpt = self.gpt = self.gpre1p = self.eg_tickets = None
         if self.fused_tower:
             self.tower_layers = ('encoder/encoded_2', 'encoder/encoded_3', 'encoder/bottleneck',
                                  'decoder/decoded_1', 'decoder/decoded_2', 'decoder/decoded_3',
@@ -301,6 +301,12 @@ class Trainer:
             # dPre1 as packed transposed fragments (the W1 gradient's B operand; rows past R zero)
             self.gpre1p = (torch.zeros(d * self.RP, **T) if pack and self.embed_mfma and d == 256
                            and os.environ.get('CCREC_EG_PACKED', '1') != '0' else None)
+            # the W1 gradient by column slices (cc_embed_grad_cs; CCREC_EG_CS=0: the row-tile kernels):
+            # one zeroed ticket per row chunk, left zero by every call
+            self.eg_tickets = (torch.zeros(max(1, int(L.lib().cc_embed_grad_cs_tickets(V, d, self.xt_rows))),
+                                           device=self.dev, dtype=torch.int32)
+                               if (self.gpre1p is not None or self.embed_mfma)
+                               and os.environ.get('CCREC_EG_CS', '1') != '0' else None)
             slab = int(L.lib().cc_tower_slab_elems(d))
             self.slab = torch.zeros((R // 32) * slab, **f32)
             # D2 output layer fused (logits twice -> softmax -> KL -> dZ -> dWo, csrc/decreg.hip): bf16,
@@ -851,7 +857,11 @@ class Trainer:
             self._dense_bwd(self.H1, self.gH2, (0, R), d, 256, 'encoder/encoded_2', gIn_f32=self.gPre1, mask=self.H1)
         t = self._tick('cc_embed_scatter_bwd')
         XR = self.xt_rows          # rows in the bitmask product (full mode: the cubes only)
-        if self.gpre1p is not None:
+        if self.eg_tickets is not None:   # column slices (cc_embed_grad_cs), from the packed image or dPre1^T
+            src, pk = (self.gpre1p, 1) if self.gpre1p is not None else (self.gPre1T, 0)
+            L.call('cc_embed_grad_cs', L.ptr(src), pk, V, d, XR, self.RP, L.ptr(self.xt_bits),
+                   self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), L.ptr(self.eg_tickets), s)
+        elif self.gpre1p is not None:
             L.call('cc_embed_grad_packed', L.ptr(self.gpre1p), V, d, XR, self.RP, L.ptr(self.xt_bits),
                    self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
         elif self.embed_mfma:

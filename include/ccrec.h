@@ -174,6 +174,16 @@ int cc_embed_grad_mfma(const void *dpre_t, int32_t V, int32_t d, int32_t R, int3
  * L2 (1 KB per wave load), no LDS staging or per-K-tile barriers.  d == 256. */
 int cc_embed_grad_packed(const void *dpre_p, int32_t V, int32_t d, int32_t R, int32_t ld_t,
                          uint32_t *xt_bits, float *grad, float *bias_grad, void *stream);
+/* The same gradient by column slice (the training path's default): one workgroup per (32-row
+ * chunk of W1 rows, 32 columns) stages its dPre1 slice and bit words in LDS once.  dpre is the
+ * packed transposed image (packed != 0, cc_tower_args.gpre1p) or dPre1^T [d][ld_t] (packed == 0,
+ * cc_tower_args.gpre1t); d % 32 == 0, R <= 2048.  tickets: cc_embed_grad_cs_tickets(V, d, R)
+ * uint32 words, zero before the first call and left zero by every call (the last workgroup of a
+ * chunk to stage its bit words clears them in xt_bits and resets its ticket).  Bit-identical to
+ * cc_embed_grad_mfma / cc_embed_grad_packed (same MFMA k order); consumes xt_bits likewise. */
+int cc_embed_grad_cs(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R, int32_t ld_t,
+                     uint32_t *xt_bits, float *grad, float *bias_grad, uint32_t *tickets, void *stream);
+int32_t cc_embed_grad_cs_tickets(int32_t V, int32_t d, int32_t R);
 /* Full-mode regulariser (all |V| one-hot identity rows, README.md:27 KL(M, D2(E(I)))): the rows'
  * W1 gradient is dPre1 itself — grad[lo + r] += round(dpre[r]) for r < n and, with bias_grad,
  * bias_grad += sum_r round(dpre[r]) in a fixed order; round = bf16 RNE for dtype CC_BF16 (the

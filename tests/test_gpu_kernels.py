@@ -487,6 +487,52 @@ def test_embed_grad_packed_bit_exact(V, R):
     assert rel_err(outs[1][0].numpy(), want) < 1e-5
 
 
+@pytest.mark.parametrize('V,R,d', [(22000, 512, 256), (3000, 512, 256), (777, 96, 256), (22000, 1024, 256),
+                                   (5000, 1024, 1024), (1500, 200, 128), (64, 32, 32)])
+def test_embed_grad_cs_bit_exact(V, R, d):
+    """cc_embed_grad_cs (column slices: the dPre1 slice and the chunk's bit words staged in LDS
+    once, A fragments from a nibble LUT) equals cc_embed_grad_mfma bit for bit (same MFMA k order),
+    from the packed image and from dPre1^T; it zeroes xt_bits and leaves its tickets zero, so a
+    second call (the next step) works the same."""
+    RP = (R + 63) // 64 * 64
+    rng = np.random.default_rng(V + R + d)
+    g = (torch.randn(R, d, device='cuda') * 0.1).to(torch.bfloat16)
+    gpad = torch.zeros(RP, d, device='cuda', dtype=torch.bfloat16)
+    gpad[:R] = g
+    gT = gpad.t().contiguous()
+    gP = gpad.view(RP // 16, 2, 8, d // 32, 32).permute(3, 0, 1, 4, 2).contiguous()
+    nt = int(L.lib().cc_embed_grad_cs_tickets(V, d, R))
+    assert nt >= 1
+    tickets = torch.zeros(nt, device='cuda', dtype=torch.int32)
+    for rep in range(2):
+        X = rng.random((R, V)) < (0.02 if rep == 0 else 0.3)
+        xt = np.zeros((V, (R + 31) // 32), np.uint32)
+        rr, cc = np.nonzero(X)
+        np.bitwise_or.at(xt, (cc, rr // 32), (np.uint32(1) << (rr % 32).astype(np.uint32)))
+        outs = []
+        runs = [('cs', 1, gP), ('cs', 0, gT)]
+        if d % 128 == 0:
+            runs.insert(0, ('mfma', None, gT))
+        for kind, pk, src in runs:
+            xtd = torch.from_numpy(xt.view(np.int32)).cuda()
+            grad = torch.full((V, d), 7.0, device='cuda')
+            bg = torch.full((d,), 7.0, device='cuda')
+            if kind == 'mfma':
+                L.call('cc_embed_grad_mfma', L.ptr(src), V, d, R, RP, L.ptr(xtd), L.ptr(grad), L.ptr(bg), L.stream_ptr())
+            else:
+                L.call('cc_embed_grad_cs', L.ptr(src), pk, V, d, R, RP, L.ptr(xtd), L.ptr(grad), L.ptr(bg),
+                       L.ptr(tickets), L.stream_ptr())
+            torch.cuda.synchronize()
+            assert int(xtd.abs().sum().item()) == 0, kind
+            assert int(tickets.abs().sum().item()) == 0, kind
+            outs.append((grad.cpu(), bg.cpu()))
+        for o in outs[1:]:
+            assert torch.equal(outs[0][0], o[0]) and torch.equal(outs[0][1], o[1])
+        want = X.T.astype(np.float64) @ g.double().cpu().numpy()
+        assert rel_err(outs[-1][0].numpy(), want) < 1e-5
+        assert rel_err(outs[-1][1].numpy(), g.double().cpu().numpy().sum(0)) < 1e-5
+
+
 @pytest.mark.parametrize('M,N,K,splits', [(512, 256, 22000, 32), (640, 128, 1000, 7), (128, 256, 64, 1),
                                           (256, 256, 5008, 3)])
 def test_dx_splitk_glds_matches_nt_gemm(M, N, K, splits):
