@@ -546,10 +546,20 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
         if (gc < V) {
           uint32_t g0 = (uint32_t)((w * 32 + 4 * half) * V + gc);
           asm volatile("" : "+v"(g0));  // opaque per tile: keeps 48 row addresses from being hoisted
+          // the tile's 16 partial sums of this column are added to gW with 8 loads in flight at
+          // a time (a load-add-store per element serialised 48 round trips per tile: the
+          // full-mode regulariser walks 43 tiles per slice)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float *gp = p.gW + (g0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V));
-            *gp = first ? acc2[j][r] : *gp + acc2[j][r];
+          for (int h8 = 0; h8 < 16; h8 += 8) {  // two groups of 8 loads in flight (registers)
+            float old[8];
+            if (!first) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) old[r] = p.gW[g0 + (uint32_t)((((h8 + r) & 3) + 8 * ((h8 + r) >> 2)) * V)];
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+              p.gW[g0 + (uint32_t)((((h8 + r) & 3) + 8 * ((h8 + r) >> 2)) * V)] =
+                  first ? acc2[j][h8 + r] : old[r] + acc2[j][h8 + r];
           }
         }
       }

@@ -250,7 +250,9 @@ class Trainer:
         self.splits = max(1, min(int(os.environ.get('CCREC_DX_SPLITS', '32')), V // 512))   # decoder dX: K = V
         # the regulariser branch's dX: M = Breg rows; with thousands of rows (full mode) the output
         # tiles alone fill the chip — no split-K
-        self.splits_reg = self.splits if self.Breg <= 1024 else int(os.environ.get('CCREC_DX_SPLITS_REG', '1'))
+        # full-mode regulariser (~|V| rows): 2 K-splits (tools/micro/dx_full_micro.py at |V| = 22,000:
+        # 1 split 643 us, 2 or 4 splits 515 us, the library GEMM 391-399 us)
+        self.splits_reg = self.splits if self.Breg <= 1024 else int(os.environ.get('CCREC_DX_SPLITS_REG', '2'))
         self.tsplits = max(1, min(8, B // 128))             # tower dW: K = rows (B or 2B)
         self.split_buf = torch.zeros(max(self.splits * B * d, self.splits_reg * self.Breg * d,
                                          2 * self.tsplits * max(d, 256) * 256), **f32)
