@@ -99,6 +99,8 @@ def roofline_for(name, ms, tr):
     V, d, B = cfg.V, cfg.d, cfg.batch_size
     if name == 'cc_adam_dense':
         n = tr.layout.total if tr.use_reg else tr.layout.main_total
+        if getattr(tr, 'fuse_w1', False):     # W1's Adam runs in its gradient kernel
+            n -= tr.w1_off
         byt = n * (16 + 12 + 2)                    # read p,m,v,g; write p,m,v; write bf16 shadow
         if getattr(tr, 'fused_adam', False):      # + the transposed bf16 operand copies
             byt += 2 * sum(int(r.rows) * int(r.cols) for r in tr.adam_regions)
@@ -168,6 +170,8 @@ def step_roofline(tr, ms_per_step, kt):
     P = tr.layout.total if tr.use_reg else tr.layout.main_total
     ndec = 2 if tr.use_reg else 1
     byt = B * n * d * e + 34 * P + 2 * e * d * V * ndec + B * (4 * n + V / 8) + (4 * tr.Breg * V if tr.use_reg else 0)
+    if getattr(tr, 'fuse_w1', False):   # W1's fp32 gradient is never written nor read back
+        byt -= 8 * tr.w1_off
     out = {'bound': 'hbm', 'bytes_per_step': byt, 'achieved': byt / (ms_per_step * 1e-3) / 1e9,
            'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'mean_cube_n': n}
     out['frac'] = out['achieved'] / out['peak']
@@ -308,7 +312,9 @@ def main():
                          reg_rows=reg_rows)
     del y_mtx
     cfg = TrainConfig(V=V, d=d, batch_size=B, reg=args.reg, dtype=args.dtype, seed=1234,
-                      rank=rank, world=world, reg_shard=reg_shard, reg_mode=args.reg_mode)
+                      rank=rank, world=world, reg_shard=reg_shard, reg_mode=args.reg_mode,
+                      fuse_w1_adam=True)   # one process: W1's Adam in its gradient kernel (parity:
+    #                                        tests/test_gpu_train.py::test_fused_w1_adam_matches_unfused)
     tr = Trainer(cfg, data, params_flat=glorot_flat(V, d, seed=42), device=dev)
     rng = np.random.default_rng(99)      # same permutations on every rank
     tr.set_epoch_permutations(np.stack([rng.permutation(args.cubes) for _ in range(4)]))
@@ -397,8 +403,10 @@ def main():
                 'measured': 'HIP events around the sharded Adam kernels on the comm stream (sum per step)'}
     roof['frac'] = roof['achieved'] / roof['peak']
     if world == 1 and getattr(tr, 'adam_packs', False):
-        roof['kernel'] = ('adam_noise_kernel<true> (cc_adam_noise_pack: TF Adam over all parameters + F '
-                          'of the next step + the tower kernels\' packed bf16 images in the same launch; '
+        roof['kernel'] = ('adam_noise_kernel<true> (cc_adam_noise_pack: TF Adam over all parameters '
+                          + ('after W1 (W1\'s Adam runs in the W1-gradient kernel, cc_embed_grad_cs_adam) '
+                             if getattr(tr, 'fuse_w1', False) else '')
+                          + '+ F of the next step + the tower kernels\' packed bf16 images in the same launch; '
                           'bytes counted are Adam\'s only, F and the images add <2%)')
     elif world == 1 and getattr(tr, 'prefetch', False):
         roof['kernel'] = ('adam_noise_kernel (cc_adam_noise: TF Adam over all parameters + F of the '

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "adam.hpp"
 #include "common.hpp"
 
 // dev-only timing hook (tools/micro/eg_probe.hip defines it); compiled out of the library
@@ -520,19 +521,32 @@ __global__ __launch_bounds__(256, 2) void embed_grad_pk_kernel(const bf16_t *__r
 // extra launch).
 constexpr int CS_NT = 512;                     // 8 waves, ~one block per CU
 constexpr int cs_tpw(int xwm) { return xwm <= 32 ? 3 : 1; }      // tiles per wave (registers)
-constexpr int cs_lut_copies(int xwm) { return xwm <= 32 ? 16 : 4; }  // 4 at R > 1024: LDS
-constexpr int cs_lut_bytes(int xwm) { return 256 * 16 * cs_lut_copies(xwm); }  // byte -> 8 bf16 (16 B)
+// byte -> 8 bf16 (16 B) LUT lane copies: fewer where the LDS is short (R > 512 with the Adam
+// epilogue's re-layout tiles, R > 1024): 2-way bank conflicts at 8 copies
+constexpr int cs_lut_copies(int xwm, bool adam) { return xwm <= 16 ? 16 : xwm <= 32 ? (adam ? 8 : 16) : 4; }
+constexpr int cs_lut_bytes(int xwm, bool adam) { return 256 * 16 * cs_lut_copies(xwm, adam); }
 __device__ __forceinline__ uint4 byte_bf16(uint32_t e) {  // 8 bits -> 8 bf16 of 1.0 / 0.0
   uint32_t w[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) w[i] = (((e >> (2 * i)) & 1u) ? 0x3F80u : 0u) | (((e >> (2 * i + 1)) & 1u) ? 0x3F800000u : 0u);
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
-template <bool PK, int XWM, bool VEC>
+// ADAM: TF Adam on W1 in the tile epilogue (one process: the gradient is final here) — p, m, v
+// stream through once, the bf16 shadow is rewritten, the W1 gradient is never stored; the bias
+// row's gradient still goes to bias_grad for the main Adam launch
+struct CsAdam {
+  float *p, *m, *v;      // W1 rows of the flat fp32 buffers ([V][d])
+  bf16_t *shadow;        // W1 rows of the bf16 shadow
+  const int64_t *state;  // device step counters: t = state[0] + 1 (cc_adam_dense's t)
+  float lr, b1, b2, eps;
+};
+
+template <bool PK, int XWM, bool VEC, bool ADAM>
 __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *__restrict__ gsrc, int V, int d, int R,
                                                             int RP, int tpc, uint32_t *xt,
                                                             float *__restrict__ grad,
-                                                            float *__restrict__ bias_grad, uint32_t *tickets) {
+                                                            float *__restrict__ bias_grad, uint32_t *tickets,
+                                                            CsAdam ad) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
@@ -544,9 +558,10 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
   const int t0 = rc * tpc, nt = min(NTL, t0 + tpc) - t0;
   const int v0 = 32 * t0;
   EG_PROBE(0);
-  constexpr int LC = cs_lut_copies(XWM);
+  constexpr int LC = cs_lut_copies(XWM, ADAM);
   bf16_t *Bs = reinterpret_cast<bf16_t *>(smem);                  // fragment j at (j * 64 + lane) * 8
   unsigned char *lut = smem + (size_t)2 * XWM * 1024;             // [256 values][16 copies] x 16 B
+  float *tx = reinterpret_cast<float *>(lut + cs_lut_bytes(XWM, ADAM));  // ADAM: per-wave 32 x 36 tiles
   // ---- every global read first: the bit words of all the wave's tiles (wave w takes tiles w,
   // w + 8, ... of the chunk; a lane holds its row's XWM words per tile), then the B slice and LUT
   // (every global load below is unconditional — clamped address, then a select — so the
@@ -620,13 +635,38 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
   // XWM = 16 (R <= 512, the headline shape): the wave keeps the whole B slice in 128 VGPRs, read
   // from LDS once — the tile loop then reads only its A fragments from LDS (at two 1-KB LDS reads
   // per MFMA the LDS array, not the MFMA, set the pace)
-  constexpr bool BREG = XWM == 16;
+  constexpr bool BREG = XWM == 16 && !ADAM;  // (the Adam epilogue needs those registers)
   bf16x8_t breg[BREG ? 2 * XWM : 1];
   if constexpr (BREG) {
 #pragma unroll
     for (int k = 0; k < 2 * XWM; ++k) breg[k] = *reinterpret_cast<const bf16x8_t *>(Bs + (k * 64 + lane) * 8);
   }
+  float alpha = 0.f, omb1 = 0.f, omb2 = 0.f;
+  if constexpr (ADAM) {  // cc_adam::range's constants, same expressions
+    const float tt = (float)(ad.state[0] + 1);
+    const float b1p = powf(ad.b1, tt), b2p = powf(ad.b2, tt);
+    alpha = ad.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+    omb1 = 1.f - ad.b1;
+    omb2 = 1.f - ad.b2;
+  }
   auto tile = [&](int t, const uint32_t (&wd)[XWM]) {
+    const int vr = v0 + 32 * t + (lane & 31);
+    // Adam operands of this lane's 16 elements, issued before the MFMAs (unconditional: a
+    // clamped row, stored only for real rows)
+    // (the Adam epilogue works on the tile re-laid through LDS: instruction g covers tile rows
+    // 8 g .. 8 g + 7, lane l row 8 g + (l >> 3), columns 4 (l & 7) .. +3 — eight whole 128-B lines
+    // per wave instruction instead of 32 partial ones)
+    cc_adam::f32x4_t ap[ADAM ? 4 : 1], am[ADAM ? 4 : 1], av[ADAM ? 4 : 1];
+    if constexpr (ADAM) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int vg = v0 + 32 * t + 8 * g + (lane >> 3);
+        const int64_t rb = (int64_t)(vg < V ? vg : V - 1) * d + 32 * cs + 4 * (lane & 7);
+        ap[g] = *reinterpret_cast<const cc_adam::f32x4_t *>(ad.p + rb);
+        am[g] = *reinterpret_cast<const cc_adam::f32x4_t *>(ad.m + rb);
+        av[g] = *reinterpret_cast<const cc_adam::f32x4_t *>(ad.v + rb);
+      }
+    }
     f32x16_t acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -663,15 +703,47 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
     // With the dPre1 fragments as the MFMA's A operand and the bit fragments as its B operand (the
     // same registers), lane l holds W1 row v0 + 32 t + (l & 31) and the slice's columns
     // 8 g + 4 (l >> 5) .. +3, g = 0..3: four 16-B stores per lane instead of sixteen 4-B ones.
-    const int vr = v0 + 32 * t + (lane & 31);
+    if constexpr (ADAM) {
+      float *T = tx + w * (32 * 36);  // this wave's 32 x 32 tile, row pitch 36 floats
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int c0 = 32 * cs + 8 * g + 4 * half;
-      const float4 q = make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
-      if (vr < V)
-        *reinterpret_cast<float4 *>(grad + (int64_t)vr * d + c0) = q;
-      else if (vr == V && bias_grad)
-        *reinterpret_cast<float4 *>(bias_grad + c0) = q;
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4 *>(T + (lane & 31) * 36 + 8 * g + 4 * half) =
+            make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int rr = 8 * g + (lane >> 3), c0 = 32 * cs + 4 * (lane & 7);
+        const int vg = v0 + 32 * t + rr;
+        const float4 q = *reinterpret_cast<const float4 *>(T + rr * 36 + 4 * (lane & 7));
+        if (vg < V) {
+          float pe[4] = {ap[g][0], ap[g][1], ap[g][2], ap[g][3]}, me[4] = {am[g][0], am[g][1], am[g][2], am[g][3]};
+          float ve[4] = {av[g][0], av[g][1], av[g][2], av[g][3]};
+          const float ge[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cc_adam::elem(pe[e], me[e], ve[e], ge[e], alpha, omb1, omb2, ad.eps);
+          const int64_t o = (int64_t)vg * d + c0;
+          *reinterpret_cast<cc_adam::f32x4_t *>(ad.p + o) = cc_adam::f32x4_t{pe[0], pe[1], pe[2], pe[3]};
+          *reinterpret_cast<cc_adam::f32x4_t *>(ad.m + o) = cc_adam::f32x4_t{me[0], me[1], me[2], me[3]};
+          *reinterpret_cast<cc_adam::f32x4_t *>(ad.v + o) = cc_adam::f32x4_t{ve[0], ve[1], ve[2], ve[3]};
+          ushort4 sh;
+          sh.x = f2bf(pe[0]);
+          sh.y = f2bf(pe[1]);
+          sh.z = f2bf(pe[2]);
+          sh.w = f2bf(pe[3]);
+          *reinterpret_cast<ushort4 *>(ad.shadow + o) = sh;
+        } else if (vg == V && bias_grad) {
+          *reinterpret_cast<float4 *>(bias_grad + c0) = q;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c0 = 32 * cs + 8 * g + 4 * half;
+        const float4 q = make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
+        if (vr < V)
+          *reinterpret_cast<float4 *>(grad + (int64_t)vr * d + c0) = q;
+        else if (vr == V && bias_grad)
+          *reinterpret_cast<float4 *>(bias_grad + c0) = q;
+      }
     }
   };
 #pragma unroll
@@ -689,7 +761,7 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
 }
 
 // launch geometry of cc_embed_grad_cs: 32-row tiles per chunk and the LDS size
-void cs_plan(int V, int d, int R, bool bias, int &tpc, int &nrc, size_t &lds) {
+void cs_plan(int V, int d, int R, bool bias, int &tpc, int &nrc, size_t &lds, bool adam = false) {
   const int RPE = (R + 63) & ~63;
   const int NTL = (V + (bias ? 1 : 0) + 31) / 32;
   const int xwm = RPE / 32 <= 16 ? 16 : RPE / 32 <= 32 ? 32 : 64;  // the kernel's XWM
@@ -698,7 +770,7 @@ void cs_plan(int V, int d, int R, bool bias, int &tpc, int &nrc, size_t &lds) {
   nrc = std::max(std::max(1, std::min(NTL, 256 / nsl)), (int)cdiv(NTL, (CS_NT / 64) * cs_tpw(xwm)));
   tpc = (int)cdiv(NTL, nrc);
   nrc = (int)cdiv(NTL, tpc);
-  lds = (size_t)2 * xwm * 1024 + cs_lut_bytes(xwm);
+  lds = (size_t)2 * xwm * 1024 + cs_lut_bytes(xwm, adam) + (adam ? (size_t)(CS_NT / 64) * 32 * 36 * 4 : 0);
 }
 
 }  // namespace
@@ -711,6 +783,38 @@ extern "C" int32_t cc_embed_grad_cs_tickets(int32_t V, int32_t d, int32_t R) {
   return nrc;
 }
 
+static int embed_grad_cs_launch(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R, int32_t ld_t,
+                                uint32_t *xt_bits, float *grad, float *bias_grad, uint32_t *tickets,
+                                const CsAdam *ad, void *stream) {
+  int tpc, nrc;
+  size_t lds;
+  cs_plan(V, d, R, bias_grad != nullptr, tpc, nrc, lds, ad != nullptr);
+  CC_REQUIRE(lds <= 160 * 1024 - 64, "cc_embed_grad_cs: R too large for the LDS stage");
+  const dim3 grid((unsigned)(nrc * (d / 32)));
+  const int xw = ((R + 63) & ~63) / 32;  // bit words per row in the product
+  const bool vec = ((R + 31) / 32) % 4 == 0;  // xt rows 16-B aligned
+  const CsAdam a = ad ? *ad : CsAdam{};
+  hipStream_t s = as_stream(stream);
+#define CS_LAUNCH(PKV, XWMV, VECV, ADV)                                                                          \
+  hipLaunchKernelGGL((embed_grad_cs_kernel<PKV, XWMV, VECV, ADV>), grid, dim3(CS_NT), lds, s, (const bf16_t *)dpre, \
+                     V, d, R, ld_t, tpc, xt_bits, grad, bias_grad, tickets, a)
+#define CS_LAUNCH2(XWMV, ADV)                                                                 \
+  if (packed) {                                                                               \
+    if (vec) CS_LAUNCH(true, XWMV, true, ADV); else CS_LAUNCH(true, XWMV, false, ADV);        \
+  } else {                                                                                    \
+    if (vec) CS_LAUNCH(false, XWMV, true, ADV); else CS_LAUNCH(false, XWMV, false, ADV);      \
+  }
+  if (ad) {
+    if (xw <= 16) { CS_LAUNCH2(16, true) } else if (xw <= 32) { CS_LAUNCH2(32, true) } else { CS_LAUNCH2(64, true) }
+  } else {
+    if (xw <= 16) { CS_LAUNCH2(16, false) } else if (xw <= 32) { CS_LAUNCH2(32, false) } else { CS_LAUNCH2(64, false) }
+  }
+#undef CS_LAUNCH2
+#undef CS_LAUNCH
+  CC_LAUNCH_CHECK("embed_grad_cs_kernel");
+  return CC_OK;
+}
+
 extern "C" int cc_embed_grad_cs(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R, int32_t ld_t,
                                 uint32_t *xt_bits, float *grad, float *bias_grad, uint32_t *tickets, void *stream) {
   CC_REQUIRE(dpre && xt_bits && grad && tickets, "cc_embed_grad_cs: null pointer");
@@ -719,34 +823,23 @@ extern "C" int cc_embed_grad_cs(const void *dpre, int32_t packed, int32_t V, int
   CC_REQUIRE(V > 0 && R > 0 && R <= 2048, "cc_embed_grad_cs: V > 0, R in 1..2048");
   CC_REQUIRE(ld_t % 64 == 0 && ld_t >= R && ((uintptr_t)dpre % 16) == 0,
              "cc_embed_grad_cs: ld_t must be a multiple of 64 covering R, dPre1 image 16-B aligned");
-  int tpc, nrc;
-  size_t lds;
-  cs_plan(V, d, R, bias_grad != nullptr, tpc, nrc, lds);
-  CC_REQUIRE(lds <= 160 * 1024 - 64, "cc_embed_grad_cs: R too large for the LDS stage");
-  const dim3 grid((unsigned)(nrc * (d / 32)));
-  const int xw = ((R + 63) & ~63) / 32;  // bit words per row in the product
-  hipStream_t s = as_stream(stream);
-  const bool vec = ((R + 31) / 32) % 4 == 0;  // xt rows 16-B aligned
-#define CS_LAUNCH(PKV, XWMV, VECV)                                                                          \
-  hipLaunchKernelGGL((embed_grad_cs_kernel<PKV, XWMV, VECV>), grid, dim3(CS_NT), lds, s, (const bf16_t *)dpre, \
-                     V, d, R, ld_t, tpc, xt_bits, grad, bias_grad, tickets)
-#define CS_LAUNCH2(XWMV)                                     \
-  if (packed) {                                              \
-    if (vec) CS_LAUNCH(true, XWMV, true); else CS_LAUNCH(true, XWMV, false);   \
-  } else {                                                   \
-    if (vec) CS_LAUNCH(false, XWMV, true); else CS_LAUNCH(false, XWMV, false); \
-  }
-  if (xw <= 16) {
-    CS_LAUNCH2(16)
-  } else if (xw <= 32) {
-    CS_LAUNCH2(32)
-  } else {
-    CS_LAUNCH2(64)
-  }
-#undef CS_LAUNCH2
-#undef CS_LAUNCH
-  CC_LAUNCH_CHECK("embed_grad_cs_kernel");
-  return CC_OK;
+  return embed_grad_cs_launch(dpre, packed, V, d, R, ld_t, xt_bits, grad, bias_grad, tickets, nullptr, stream);
+}
+
+extern "C" int cc_embed_grad_cs_adam(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R,
+                                     int32_t ld_t, uint32_t *xt_bits, float *bias_grad, uint32_t *tickets, float *p,
+                                     float *m, float *v, uint16_t *shadow, const int64_t *state, float lr,
+                                     float beta1, float beta2, float eps, void *stream) {
+  CC_REQUIRE(dpre && xt_bits && tickets && p && m && v && shadow && state, "cc_embed_grad_cs_adam: null pointer");
+  CC_REQUIRE((((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)bias_grad) & 15) == 0 &&
+                 ((uintptr_t)shadow & 7) == 0,
+             "cc_embed_grad_cs_adam: p, m, v, bias_grad 16-B aligned, shadow 8-B aligned");
+  CC_REQUIRE(d % 32 == 0 && d >= 32 && d <= 4096, "cc_embed_grad_cs_adam: d must be a multiple of 32");
+  CC_REQUIRE(V > 0 && R > 0 && R <= 2048, "cc_embed_grad_cs_adam: V > 0, R in 1..2048");
+  CC_REQUIRE(ld_t % 64 == 0 && ld_t >= R && ((uintptr_t)dpre % 16) == 0,
+             "cc_embed_grad_cs_adam: ld_t must be a multiple of 64 covering R, dPre1 image 16-B aligned");
+  const CsAdam ad{p, m, v, (bf16_t *)shadow, state, lr, beta1, beta2, eps};
+  return embed_grad_cs_launch(dpre, packed, V, d, R, ld_t, xt_bits, nullptr, bias_grad, tickets, &ad, stream);
 }
 
 extern "C" int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const float *bias, int32_t V,

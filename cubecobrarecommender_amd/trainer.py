@@ -39,6 +39,8 @@ class TrainConfig:
     fused_tower: bool = True       # tower.hip row-block kernels (else per-layer cc_gemm launches)
     prefetch_noise: bool = True    # one process: F of step k+1 rides in step k's Adam launch
     reg_shard: bool = False        # data parallel + reg: M~ row-sharded, owner computes
+    fuse_w1_adam: bool = False     # one process: TF Adam on W1 inside the W1-gradient kernel (its
+    #                                gradient is then never stored; bench.py turns it on)
     reg_mode: str = 'sampled'      # 'sampled': B reg rows per step drawn ∝ neg_sampler (generator.py:47-51);
     #                                'full': all |V| identity rows every step, KL(M~, D2(E(I))) as the
     #                                reference README states the objective (README.md:27)
@@ -370,6 +372,14 @@ class Trainer:
         # starts without a counters/transposes launch
         self.adam_packs = (self.prefetch and self.wpack is not None
                            and os.environ.get('CCREC_ADAM_PACK', '1') != '0')
+        # TF Adam on W1 in the W1-gradient kernel's epilogue (cc_embed_grad_cs_adam): the main Adam
+        # launch then starts after W1 (W1 is the first tensor of the layout).  One process only
+        # (DP reduces the gradient first), the column-slice kernel, not the full-mode regulariser
+        # (its identity rows add to the W1 gradient after that kernel).
+        self.w1_off = self.layout.offset('encoder/encoded_1/bias')   # = W1's padded size
+        self.fuse_w1 = (cfg.fuse_w1_adam and self.adam_packs and self.eg_tickets is not None and not self.full_reg
+                        and self.layout.offset('encoder/encoded_1/kernel') == 0
+                        and os.environ.get('CCREC_FUSE_W1_ADAM', '1') != '0')
         self.adam_pack = self._adam_pack_desc() if self.adam_packs else None
         self._adv_deferred = False   # the previous step's counter advance rides in the E1 gather
         self.noise_ready = False
@@ -499,7 +509,7 @@ class Trainer:
         for l, name in enumerate(self.tower_layers[:layers]):
             K, N = self.layout.shape(name + '/kernel')
             pk.K[l], pk.N[l] = K, N
-            pk.off[l] = self.layout.offset(name + '/kernel')
+            pk.off[l] = self.layout.offset(name + '/kernel') - (self.w1_off if self.fuse_w1 else 0)
             pk.wpf[l] = self.wpack[0, int(self.wt_off[l]):].data_ptr()
             pk.wpb[l] = self.wpack[1, int(self.wt_off[l]):].data_ptr()
         return pk
@@ -859,7 +869,14 @@ class Trainer:
             self._dense_bwd(self.H1, self.gH2, (0, R), d, 256, 'encoder/encoded_2', gIn_f32=self.gPre1, mask=self.H1)
         t = self._tick('cc_embed_scatter_bwd')
         XR = self.xt_rows          # rows in the bitmask product (full mode: the cubes only)
-        if self.eg_tickets is not None:   # column slices (cc_embed_grad_cs), from the packed image or dPre1^T
+        if self.eg_tickets is not None and self.fuse_w1:   # column slices + TF Adam on W1 in the epilogue
+            cfg_ = self.cfg
+            src, pk = (self.gpre1p, 1) if self.gpre1p is not None else (self.gPre1T, 0)
+            L.call('cc_embed_grad_cs_adam', L.ptr(src), pk, V, d, XR, self.RP, L.ptr(self.xt_bits),
+                   self.gp('encoder/encoded_1/bias'), L.ptr(self.eg_tickets), L.ptr(self.params), L.ptr(self.m),
+                   L.ptr(self.v), L.ptr(self.shadow), L.ptr(self.state), cfg_.lr, cfg_.beta1, cfg_.beta2,
+                   cfg_.eps, s)
+        elif self.eg_tickets is not None:   # column slices (cc_embed_grad_cs), from the packed image or dPre1^T
             src, pk = (self.gpre1p, 1) if self.gpre1p is not None else (self.gPre1T, 0)
             L.call('cc_embed_grad_cs', L.ptr(src), pk, V, d, XR, self.RP, L.ptr(self.xt_bits),
                    self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), L.ptr(self.eg_tickets), s)
@@ -889,8 +906,9 @@ class Trainer:
         if self.prefetch:     # + F for the next step in the same launch
             na = self._noise_args()
             if self.adam_packs:   # + packed tower images + step counters
-                L.call('cc_adam_noise_pack', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v),
-                       L.ptr(self.grads), L.ptr(self.shadow), n, cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,
+                o = self.w1_off if self.fuse_w1 else 0   # (W1 already updated by its gradient kernel)
+                L.call('cc_adam_noise_pack', L.ptr(self.params[o:]), L.ptr(self.m[o:]), L.ptr(self.v[o:]),
+                       L.ptr(self.grads[o:]), L.ptr(self.shadow[o:]), n - o, cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,
                        L.C.byref(na), self.batches_per_epoch, L.C.byref(self.adam_pack), L.stream_ptr(stream))
             else:
                 L.call('cc_adam_noise', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v),
@@ -1025,10 +1043,16 @@ class Trainer:
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream())
         saved = self.state.clone()
+        # the fused W1 Adam updates W1 inside forward_backward: undo the warm-up's update
+        w1 = ([b[:self.w1_off].clone() for b in (self.params, self.m, self.v, self.shadow)]
+              if self.fuse_w1 else None)
         with torch.cuda.stream(s):           # warm-up launch outside capture (lazy module loads)
             self.forward_backward()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        if w1 is not None:
+            for b, c in zip((self.params, self.m, self.v, self.shadow), w1):
+                b[:self.w1_off].copy_(c)
         g_fb, g_adam, g_rest = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         if self.cfg.world > 1:   # (forward_backward_a | forward_backward_b | counters): the
             with torch.cuda.graph(g_fb):       # sharded optimizer's collectives run between them

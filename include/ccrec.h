@@ -184,6 +184,15 @@ int cc_embed_grad_packed(const void *dpre_p, int32_t V, int32_t d, int32_t R, in
 int cc_embed_grad_cs(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R, int32_t ld_t,
                      uint32_t *xt_bits, float *grad, float *bias_grad, uint32_t *tickets, void *stream);
 int32_t cc_embed_grad_cs_tickets(int32_t V, int32_t d, int32_t R);
+/* cc_embed_grad_cs with TF Adam (cc_adam_dense's update, t = state[0] + 1) applied to W1 in the
+ * kernel's epilogue (one process: the gradient is final there): p, m, v are W1's rows [V][d] of
+ * the flat fp32 buffers, shadow its bf16 rows; the W1 gradient itself is never stored, the bias
+ * gradient goes to bias_grad for the main Adam launch (which then starts after W1).  Bit-identical
+ * parameters / moments to cc_embed_grad_cs followed by cc_adam_dense over W1. */
+int cc_embed_grad_cs_adam(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R, int32_t ld_t,
+                          uint32_t *xt_bits, float *bias_grad, uint32_t *tickets, float *p, float *m, float *v,
+                          uint16_t *shadow, const int64_t *state, float lr, float beta1, float beta2, float eps,
+                          void *stream);
 /* Full-mode regulariser (all |V| one-hot identity rows, README.md:27 KL(M, D2(E(I)))): the rows'
  * W1 gradient is dPre1 itself — grad[lo + r] += round(dpre[r]) for r < n and, with bias_grad,
  * bias_grad += sum_r round(dpre[r]) in a fixed order; round = bf16 RNE for dtype CC_BF16 (the

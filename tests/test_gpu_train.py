@@ -312,6 +312,38 @@ def test_adam_pack_images_and_counters():
     assert torch.equal(got, tr.wpack)
 
 
+@pytest.mark.parametrize('reg', [0.0, 0.1])
+def test_fused_w1_adam_matches_unfused(reg):
+    """TrainConfig(fuse_w1_adam=True) — bench.py's step: TF Adam on W1 in the column-slice W1-gradient
+    kernel's epilogue, the main Adam launch starting after W1 — gives bit-identical parameters,
+    bf16 shadow, Adam moments and losses to the unfused step (same cc_adam::elem update, same
+    gradient values), over eager steps and graph replays."""
+    out = {}
+    for fuse in (False, True):
+        lists, Mt, ns = problem(11, 1024, 2500, (20, 40, 80))
+        P = model_ref.init_params(2500, 256, seed=11, bias_std=0.01)
+        lay = Layout(2500, 256)
+        cfg = TrainConfig(V=2500, d=256, batch_size=256, reg=reg, dtype='bf16', seed=11, fuse_w1_adam=fuse)
+        tr = Trainer(cfg, DeviceDataset(lists, 2500, y_mtx=Mt.astype(np.float32) if reg > 0 else None,
+                                        neg_sampler=ns), params_flat=lay.pack(P))
+        tr.set_epoch_permutation(np.random.default_rng(11).permutation(1024).astype(np.int32))
+        assert tr.fuse_w1 == fuse and tr.adam_packs
+        losses = []
+        for _ in range(2):
+            tr.step()
+            losses.append(tr.losses())
+        tr.capture()
+        for _ in range(3):
+            tr.step()
+            losses.append(tr.losses())
+        tr.flush()
+        torch.cuda.synchronize()
+        out[fuse] = (tr.params.cpu(), tr.m.cpu(), tr.v.cpu(), tr.shadow.cpu(), losses)
+    for a, b in zip(out[False][:4], out[True][:4]):
+        assert torch.equal(a, b)
+    assert out[False][4] == out[True][4]
+
+
 @pytest.mark.parametrize('dtype,V,d,B', [('fp32', 700, 64, 32), ('bf16', 1500, 256, 128)])
 def test_full_mode_regulariser_matches_oracle(dtype, V, d, B):
     """reg_mode='full' (README.md:27: KL(M~, D2(E(I))) over ALL |V| identity rows every step):
