@@ -80,37 +80,72 @@ __global__ __launch_bounds__(64) void quant_rows_kernel(const T *__restrict__ sr
   }
 }
 
-// Transposed: dst[c][r] = q(src[r][c]); K axis = r.  grid (ceil(cols / 256), ld_dst / 32), block
-// 256: tile rows [32 by, 32 by + 32), cols [256 bx, +256); lane c emits dst row (256 bx + c)'s block by.
-constexpr int QT_C = 256;
+// Transposed: dst[c][r] = q(src[r][c]); K axis = r.  grid (ceil(cols / 64), ld_dst / 128), block
+// 256: tile rows [128 by, +128), cols [64 bx, +64) (a whole 128-B line of every bf16 source row);
+// thread (rb = tid / 64, c = tid % 64) emits dst row (64 bx + c)'s block 4 by + rb, so the four
+// waves of a block write one whole 128-B line of each of its 64 dst rows.
+constexpr int QT_C = 64, QT_R = 128;
 template <typename T>
-__global__ __launch_bounds__(QT_C) void quant_t_kernel(const T *__restrict__ src, int rows, int cols,
-                                                       int ld_src, uint8_t *__restrict__ dst, int ld_dst,
-                                                       uint8_t *__restrict__ scales) {
-  __shared__ float tile[32][QT_C + 1];
-  const int c0 = blockIdx.x * QT_C, r0 = blockIdx.y * 32;
-  for (int i = threadIdx.x; i < 32 * QT_C; i += QT_C) {
-    const int rr = i / QT_C, cc = i % QT_C;
-    const int gr = r0 + rr, gc = c0 + cc;
-    tile[rr][cc] = gr < rows && gc < cols ? ldf(src, (int64_t)gr * ld_src + gc) : 0.f;
+__global__ __launch_bounds__(256) void quant_t_kernel(const T *__restrict__ src, int rows, int cols,
+                                                      int ld_src, uint8_t *__restrict__ dst, int ld_dst,
+                                                      uint8_t *__restrict__ scales) {
+  __shared__ float tile[QT_R][QT_C + 1];
+  const int c0 = blockIdx.x * QT_C, r0 = blockIdx.y * QT_R;
+  if (sizeof(T) == 2 && c0 + QT_C <= cols && (ld_src % 8) == 0 && ((uintptr_t)src % 16) == 0) {
+    // full-width bf16 tile: 16-B loads, all of a thread's issued before any LDS store
+    constexpr int NV = QT_R * QT_C / 8 / 256;  // 16-B vectors per thread
+    uint4 u[NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int i = threadIdx.x + q * 256, rr = i / (QT_C / 8), cc = (i % (QT_C / 8)) * 8;
+      const int gr = min(r0 + rr, rows - 1);
+      u[q] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(src) + (int64_t)gr * ld_src + c0 + cc);
+    }
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int i = threadIdx.x + q * 256, rr = i / (QT_C / 8), cc = (i % (QT_C / 8)) * 8;
+      const bool ok = r0 + rr < rows;
+      const uint32_t uw[4] = {u[q].x, u[q].y, u[q].z, u[q].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        tile[rr][cc + 2 * e] = ok ? __uint_as_float(uw[e] << 16) : 0.f;
+        tile[rr][cc + 2 * e + 1] = ok ? __uint_as_float(uw[e] & 0xFFFF0000u) : 0.f;
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < QT_R * QT_C; i += 256) {
+      const int rr = i / QT_C, cc = i % QT_C;
+      const int gr = r0 + rr, gc = c0 + cc;
+      tile[rr][cc] = gr < rows && gc < cols ? ldf(src, (int64_t)gr * ld_src + gc) : 0.f;
+    }
   }
   __syncthreads();
-  const int c = c0 + threadIdx.x;
-  if (c >= cols) return;
+  const int cl = threadIdx.x % QT_C, rb = threadIdx.x / QT_C;
+  const int c = c0 + cl;
   float v[32];
   float amax = 0.f;
 #pragma unroll
   for (int e = 0; e < 32; ++e) {
-    v[e] = tile[e][threadIdx.x];
+    v[e] = tile[32 * rb + e][cl];
     amax = fmaxf(amax, fabsf(v[e]));
   }
   const int ex = block_exp(amax);
   uint32_t w[8];
   encode32(v, ex, w);
-  uint4 *d4 = reinterpret_cast<uint4 *>(dst + (int64_t)c * ld_dst + r0);
-  d4[0] = make_uint4(w[0], w[1], w[2], w[3]);
-  d4[1] = make_uint4(w[4], w[5], w[6], w[7]);
-  scales[(int64_t)c * (ld_dst / 32) + blockIdx.y] = (uint8_t)(ex + 127);
+  if (c < cols) scales[(int64_t)c * (ld_dst / 32) + 4 * blockIdx.y + rb] = (uint8_t)(ex + 127);
+  // re-lay the codes through LDS so each store instruction writes whole 128-B lines (8 lanes per dst
+  // row) instead of 64 scattered 16-B pieces; rows padded to 9 x 16 B against bank conflicts
+  __syncthreads();
+  uint4 *ot = reinterpret_cast<uint4 *>(&tile[0][0]);
+  ot[cl * 9 + 2 * rb] = make_uint4(w[0], w[1], w[2], w[3]);
+  ot[cl * 9 + 2 * rb + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int i = threadIdx.x + 256 * q, rr = i / 8, sg = i % 8;
+    if (c0 + rr < cols)
+      *reinterpret_cast<uint4 *>(dst + (int64_t)(c0 + rr) * ld_dst + r0 + 16 * sg) = ot[rr * 9 + sg];
+  }
 }
 
 }  // namespace
@@ -140,12 +175,12 @@ extern "C" int cc_quant_mx8(int32_t dtype, const void *src, int32_t rows, int32_
   }
   CC_REQUIRE(!rowsum, "cc_quant_mx8: rowsum only without transpose");
   CC_REQUIRE(ld_dst >= rows, "cc_quant_mx8: ld_dst < rows");
-  const dim3 grid((unsigned)cdiv(cols, QT_C), (unsigned)(ld_dst / 32));
+  const dim3 grid((unsigned)cdiv(cols, QT_C), (unsigned)(ld_dst / QT_R));
   if (dtype == CC_BF16)
-    hipLaunchKernelGGL(quant_t_kernel<bf16_t>, grid, dim3(QT_C), 0, s, (const bf16_t *)src, rows, cols, ld_src,
+    hipLaunchKernelGGL(quant_t_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t *)src, rows, cols, ld_src,
                        dst, ld_dst, scales);
   else
-    hipLaunchKernelGGL(quant_t_kernel<float>, grid, dim3(QT_C), 0, s, (const float *)src, rows, cols, ld_src,
+    hipLaunchKernelGGL(quant_t_kernel<float>, grid, dim3(256), 0, s, (const float *)src, rows, cols, ld_src,
                        dst, ld_dst, scales);
   CC_LAUNCH_CHECK("quant_t_kernel");
   return CC_OK;

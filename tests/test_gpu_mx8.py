@@ -59,11 +59,13 @@ def test_quant_rows_bit_exact(dtype, rows, cols, ld):
     assert np.array_equal(q, qr)
 
 
-@pytest.mark.parametrize('rows,cols,ld', [(64, 300, 128), (512, 1000, 512), (100, 257, 128)])
-def test_quant_transposed_bit_exact(rows, cols, ld):
+@pytest.mark.parametrize('dtype', ['bf16', 'fp32'])
+@pytest.mark.parametrize('rows,cols,ld', [(64, 300, 128), (512, 1000, 512), (100, 257, 128), (1000, 1024, 1024),
+                                          (130, 2112, 256)])
+def test_quant_transposed_bit_exact(dtype, rows, cols, ld):
     rng = np.random.default_rng(rows + cols)
     X = _data(rng, rows, cols)
-    Xv, q, s, _ = _quant_gpu(X, L.CC_BF16, ld, transpose=True)
+    Xv, q, s, _ = _quant_gpu(X, L.CC_BF16 if dtype == 'bf16' else L.CC_F32, ld, transpose=True)
     qr, sr = mx8_ref.quantize_rows(np.ascontiguousarray(Xv.T), ld)
     assert np.array_equal(s, sr)
     assert np.array_equal(q, qr)
