@@ -27,7 +27,7 @@ class NoiseArgs(C.Structure):
         ('x_cnt', C.c_void_p), ('x_idx', C.c_void_p), ('y_bits', C.c_void_p),
         ('xt_bits', C.c_void_p), ('reg_idx', C.c_void_p), ('status', C.c_void_p),
         ('xt_rows', C.c_int32), ('reg_slots', C.c_int32), ('reg_lo', C.c_int32),
-        ('reg_hi', C.c_int32), ('reg_cap', C.c_int32),
+        ('reg_hi', C.c_int32), ('reg_cap', C.c_int32), ('x_bits', C.c_void_p),
     ]
 
 
@@ -89,6 +89,8 @@ SIGNATURES = {
     'cc_embed_gather_fwd': (C.c_int, [_I32, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P]),
     'cc_embed_gather_fwd_warm': (C.c_int, [_I32, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _I64, _P, _I64,
                                            _P]),
+    'cc_embed_gather_fwd_xt': (C.c_int, [_I32, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _I64, _P, _I64,
+                                         _P, _P, _I32, _P]),
     'cc_embed_scatter_bwd': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_embed_grad_mfma': (C.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_gemm': (C.c_int, [C.POINTER(GemmArgs), _P]),

@@ -132,6 +132,49 @@ __global__ __launch_bounds__(256) void gather_kernel(const T *__restrict__ table
   }
 }
 
+// xt = bit transpose of the x row bitmasks: xt[j][w] bit r = x_bits[32 w + r] bit j, rows < xt_rows.
+// One block per XT_TJ words of cards (32 XT_TJ cards); a wave transposes two 32 x 32 bit tiles per
+// pass (lanes 0-31 tile A, 32-63 tile B) by 32 ballots, every xt word written.  The row words of
+// XT_Q passes are loaded up front (unconditional clamped loads): one load latency per XT_Q passes.
+constexpr int XT_TJ = 2, XT_Q = 4;
+__device__ __forceinline__ void xt_transpose_block(const uint32_t *__restrict__ xb, int V,
+                                                   uint32_t *__restrict__ xt, int xt_rows, int tb) {
+  const int VW = (V + 31) >> 5, XW = (xt_rows + 31) >> 5;
+  const int lane = threadIdx.x & 63, c = lane & 31;
+  const int nw = (int)(blockDim.x >> 6), wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int npair = XW * XT_TJ;  // (row word w, card word jw) tiles of this block (even)
+  for (int p0 = 2 * wv; p0 < npair; p0 += 2 * nw * XT_Q) {
+    uint32_t word[XT_Q];
+#pragma unroll
+    for (int q = 0; q < XT_Q; ++q) {
+      const int p = p0 + 2 * nw * q + (lane >> 5);
+      const int w = p / XT_TJ, jw = tb * XT_TJ + p % XT_TJ, r = 32 * w + c;
+      const bool ok = p < npair && r < xt_rows && jw < VW;
+      const uint32_t u = xb[(int64_t)min(r, xt_rows - 1) * VW + min(jw, VW - 1)];
+      word[q] = ok ? u : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < XT_Q; ++q) {
+      const int p = p0 + 2 * nw * q + (lane >> 5);
+      const int w = p / XT_TJ, jw = tb * XT_TJ + p % XT_TJ;
+      uint32_t out = 0u;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        const uint64_t bal = __ballot((word[q] >> k) & 1u);
+        const uint32_t t = lane < 32 ? (uint32_t)bal : (uint32_t)(bal >> 32);
+        out = c == k ? t : out;
+      }
+      const int j = 32 * jw + c;
+      if (p < npair && jw < VW && j < V) xt[(int64_t)j * XW + w] = out;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void xt_transpose_kernel(const uint32_t *__restrict__ xb, int V,
+                                                           uint32_t *__restrict__ xt, int xt_rows) {
+  xt_transpose_block(xb, V, xt, xt_rows, blockIdx.x);
+}
+
 // Forward, bf16 d = 256: each lane loads 16 B (8 columns) so one wave load instruction fetches TWO
 // table rows (half-wave h takes list entries of parity h) — twice the bytes in flight per
 // instruction; GWN waves per cube, U loads in flight per lane.  Partial sums: lane halves
@@ -143,8 +186,15 @@ __global__ __launch_bounds__(64 * GWN) void gather2_kernel(const bf16_t *__restr
                                                           const int32_t *__restrict__ x_cnt,
                                                           const int32_t *__restrict__ x_idx, int x_cap,
                                                           bf16_t *__restrict__ out, const void *warm,
-                                                          int64_t warm_bytes, int64_t *state, int64_t bpe) {
-  if (state && blockIdx.x == 0 && threadIdx.x == 0) {  // the previous step's counters
+                                                          int64_t warm_bytes, int64_t *state, int64_t bpe,
+                                                          const uint32_t *__restrict__ xb, int V,
+                                                          uint32_t *__restrict__ xt, int xt_rows) {
+  const int nxt = xt ? (((V + 31) >> 5) + XT_TJ - 1) / XT_TJ : 0;
+  if ((int)blockIdx.x < nxt) {  // blocks 0..nxt-1: the xt transpose (short; dispatched first, they
+    xt_transpose_block(xb, V, xt, xt_rows, (int)blockIdx.x);  // run beside the latency-bound gather)
+    return;
+  }
+  if (state && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {  // the previous step's counters
     state[0] += 1;
     state[1] += 1;
     if (state[1] >= bpe) {
@@ -155,7 +205,7 @@ __global__ __launch_bounds__(64 * GWN) void gather2_kernel(const bf16_t *__restr
   constexpr int D = 256;
   __shared__ __attribute__((aligned(16))) float part[GWN][D];
   __shared__ int32_t ls[GIDX];
-  const int row = blockIdx.x;
+  const int row = (int)blockIdx.x - nxt;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
   const int c0 = (lane & 31) * 8;
   float acc[8];
@@ -217,7 +267,7 @@ __global__ __launch_bounds__(64 * GWN) void gather2_kernel(const bf16_t *__restr
     for (int e = 0; e < 4; ++e) pk[e] = (uint32_t)f2bf(o[2 * e]) | ((uint32_t)f2bf(o[2 * e + 1]) << 16);
     *reinterpret_cast<g_u32x4 *>(out + (int64_t)row * D + c) = pk;
   }
-  l2_warm(warm, warm_bytes, blockIdx.x, gridDim.x);  // the tower forward's packed weights
+  l2_warm(warm, warm_bytes, row, R);  // the tower forward's packed weights (gather blocks only)
 }
 
 // Backward: 4 waves per W1 row (row V = the bias when bias_grad is given); wave w walks the w-th
@@ -625,7 +675,7 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
   // blocks to get here clears the chunk's xt words at its end; the atomic's return is read there
   // (it was issued before the stores, so that wait does not drain them)
   uint32_t tk = 0u;
-  if (tid == 0) tk = __hip_atomic_fetch_add(&tickets[rc], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0 && tickets) tk = __hip_atomic_fetch_add(&tickets[rc], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // ---- tiles
   // the A fragment of a byte: one ds_read_b128 from this lane's copy (lane & 15: the 16 lanes a
   // b128 read serves per cycle hit 16 distinct bank quads, whatever their bytes) — full rate even
@@ -750,12 +800,14 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
   for (int i = 0; i < TPW; ++i)
     if (w + NW * i < nt) tile(w + NW * i, wds[i]);
   EG_PROBE(3);
-  if (tid == 0) last = tk == (uint32_t)(nsl - 1);
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only: no store drain
-  if (last) {
-    const int vend = min(V, v0 + 32 * nt);
-    for (int64_t i = (int64_t)v0 * XW + tid; i < (int64_t)vend * XW; i += CS_NT) xt[i] = 0u;
-    if (tid == 0) __hip_atomic_store(&tickets[rc], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tickets) {  // (no tickets: the caller rewrites every xt word before the next use)
+    if (tid == 0) last = tk == (uint32_t)(nsl - 1);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS only: no store drain
+    if (last) {
+      const int vend = min(V, v0 + 32 * nt);
+      for (int64_t i = (int64_t)v0 * XW + tid; i < (int64_t)vend * XW; i += CS_NT) xt[i] = 0u;
+      if (tid == 0) __hip_atomic_store(&tickets[rc], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   EG_PROBE(15);
 }
@@ -817,7 +869,7 @@ static int embed_grad_cs_launch(const void *dpre, int32_t packed, int32_t V, int
 
 extern "C" int cc_embed_grad_cs(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R, int32_t ld_t,
                                 uint32_t *xt_bits, float *grad, float *bias_grad, uint32_t *tickets, void *stream) {
-  CC_REQUIRE(dpre && xt_bits && grad && tickets, "cc_embed_grad_cs: null pointer");
+  CC_REQUIRE(dpre && xt_bits && grad, "cc_embed_grad_cs: null pointer");
   CC_REQUIRE((((uintptr_t)grad | (uintptr_t)bias_grad) & 15) == 0, "cc_embed_grad_cs: grad / bias_grad 16-B aligned");
   CC_REQUIRE(d % 32 == 0 && d >= 32 && d <= 4096, "cc_embed_grad_cs: d must be a multiple of 32");
   CC_REQUIRE(V > 0 && R > 0 && R <= 2048, "cc_embed_grad_cs: V > 0, R in 1..2048");
@@ -830,7 +882,7 @@ extern "C" int cc_embed_grad_cs_adam(const void *dpre, int32_t packed, int32_t V
                                      int32_t ld_t, uint32_t *xt_bits, float *bias_grad, uint32_t *tickets, float *p,
                                      float *m, float *v, uint16_t *shadow, const int64_t *state, float lr,
                                      float beta1, float beta2, float eps, void *stream) {
-  CC_REQUIRE(dpre && xt_bits && tickets && p && m && v && shadow && state, "cc_embed_grad_cs_adam: null pointer");
+  CC_REQUIRE(dpre && xt_bits && p && m && v && shadow && state, "cc_embed_grad_cs_adam: null pointer");
   CC_REQUIRE((((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)bias_grad) & 15) == 0 &&
                  ((uintptr_t)shadow & 7) == 0,
              "cc_embed_grad_cs_adam: p, m, v, bias_grad 16-B aligned, shadow 8-B aligned");
@@ -978,7 +1030,19 @@ extern "C" int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const 
                                         const int32_t *x_idx, int32_t x_cap, void *out,
                                         const void *warm, int64_t warm_bytes, int64_t *state,
                                         int64_t bpe, void *stream) {
+  return cc_embed_gather_fwd_xt(dtype, table, bias, V, d, R, x_cnt, x_idx, x_cap, out, warm, warm_bytes, state,
+                                bpe, nullptr, nullptr, 0, stream);
+}
+
+extern "C" int cc_embed_gather_fwd_xt(int32_t dtype, const void *table, const float *bias, int32_t V,
+                                      int32_t d, int32_t R, const int32_t *x_cnt,
+                                      const int32_t *x_idx, int32_t x_cap, void *out,
+                                      const void *warm, int64_t warm_bytes, int64_t *state,
+                                      int64_t bpe, const uint32_t *x_bits, uint32_t *xt_bits, int32_t xt_rows,
+                                      void *stream) {
   CC_REQUIRE(!state || bpe >= 1, "cc_embed_gather_fwd_warm: batches_per_epoch");
+  CC_REQUIRE(!xt_bits || (x_bits && xt_rows >= 1 && xt_rows <= R),
+             "cc_embed_gather_fwd_xt: xt_bits needs x_bits and 1 <= xt_rows <= R");
   static const int g2 = [] {  // A/B switch (dev): 16-B lanes, two rows per load; waves x loads
     const char *e = getenv("CCREC_GATHER2");
     return e ? atoi(e) : 48;
@@ -992,17 +1056,22 @@ extern "C" int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const 
   CC_REQUIRE(V > 0 && R >= 0 && x_cap > 0, "cc_embed_gather_fwd: bad sizes");
   if (R == 0) return CC_OK;
   const dim3 grid((unsigned)R), block(256);
+  const int nxt = xt_bits ? (int)cdiv((V + 31) / 32, XT_TJ) : 0;  // xt transpose blocks
   const int epl = d / 64;
   hipStream_t s = as_stream(stream);
   if (dtype == CC_BF16 && d == 256 && g2 > 0) {
 #define G2(GWN, U) \
-  if (g2 == GWN * 10 + U) hipLaunchKernelGGL((gather2_kernel<GWN, U>), grid, dim3(64 * GWN), 0, s, \
+  if (g2 == GWN * 10 + U) hipLaunchKernelGGL((gather2_kernel<GWN, U>), dim3((unsigned)(R + nxt)), dim3(64 * GWN), 0, s, \
                                              (const bf16_t *)table, bias, R, x_cnt, x_idx, x_cap, (bf16_t *)out, \
-                                             warm, warm_bytes, state, bpe);
+                                             warm, warm_bytes, state, bpe, x_bits, V, xt_bits, xt_rows);
     G2(4, 4) G2(4, 8) G2(8, 4) G2(8, 8) G2(4, 6) G2(8, 6)
 #undef G2
     CC_LAUNCH_CHECK("gather2_kernel");
     return CC_OK;
+  }
+  if (xt_bits) {
+    hipLaunchKernelGGL(xt_transpose_kernel, dim3((unsigned)nxt), dim3(256), 0, s, x_bits, V, xt_bits, xt_rows);
+    CC_LAUNCH_CHECK("xt_transpose_kernel");
   }
   static const int gu = [] {  // A/B switch: row loads in flight per lane (bf16, d = 256)
     const char *e = getenv("CCREC_GATHER_U");

@@ -161,9 +161,12 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
     if (pick >= 0) atomicOr(&add_bits[pick >> 5], 1u << (pick & 31));
   }
   __syncthreads();
-  // y bitmask: cube \ ycut
+  // y bitmask: cube \ ycut (and x as a bitmask, for cc_embed_gather_fwd_xt's transpose)
   uint32_t *yrow = a.y_bits + (int64_t)b * VW;
   for (int w = tid; w < VW; w += NT) yrow[w] = cube_bits[w] & ~ycut_bits[w];
+  if (a.x_bits)
+    for (int w = tid; w < VW; w += NT)
+      a.x_bits[(int64_t)b * VW + w] = (cube_bits[w] & ~cut_bits[w]) | add_bits[w];
   // x: sorted compaction of (cube \ cut) | add  — chunked block scan over the VW words
   const int per = (VW + NT - 1) / NT;
   const int w0 = tid * per, w1 = min(VW, w0 + per);
@@ -207,6 +210,13 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
     a.x_idx[(int64_t)r * a.x_cap] = j;
     a.x_cnt[r] = 1;
     if (a.xt_bits) atomicOr(&a.xt_bits[(int64_t)j * XW + (r >> 5)], 1u << (r & 31));
+    s_k = j;
+  }
+  if (a.with_reg && a.x_bits) {  // the reg row {j} as a bitmask
+    __syncthreads();
+    const int j = s_k;
+    uint32_t *xr = a.x_bits + (int64_t)(a.B + b) * VW;
+    for (int w = tid; w < VW; w += NT) xr[w] = w == (j >> 5) ? 1u << (j & 31) : 0u;
   }
 }
 

@@ -367,6 +367,15 @@ class Trainer:
         # already hold the batch the next forward_backward consumes.
         self.prefetch = (cfg.prefetch_noise and cfg.world == 1 and not self.fused_adam
                          and os.environ.get('CCREC_PREFETCH_NOISE', '1') != '0')
+        # one process: F (in the Adam launch) writes its x rows as bitmasks and the next E1 gather
+        # launch bit-transposes them into the W1-gradient bitmask (cc_embed_gather_fwd_xt) — F's
+        # scattered xt atomics queued behind the Adam streams (measured: the Adam + F launch
+        # 40.5 -> 36.9 us without them; the same atomics in the gather cost it 13 us)
+        self.xt_in_gather = (self.prefetch and self.dtype == L.CC_BF16
+                             and os.environ.get('CCREC_XT_IN_GATHER', '1') != '0')
+        # (F's x rows as bitmasks [R][ceil(V/32)]; rows F does not draw stay zero)
+        self.x_bits = (torch.zeros(self.R, (cfg.V + 31) // 32, device=self.dev, dtype=torch.int32)
+                       if self.xt_in_gather else None)
         # one process, packed tower images: the Adam + F launch also rewrites the tower kernels'
         # packed images and advances the step counters (cc_adam_noise_pack) — the next step
         # starts without a counters/transposes launch
@@ -593,10 +602,12 @@ class Trainer:
                            neg_sampler=self.data.neg_sampler.data_ptr(), guide=self.data.guide.data_ptr(),
                            guide_log2=self.data.guide_log2, state=self.state.data_ptr(),
                            x_cnt=self.x_cnt.data_ptr(), x_idx=self.x_idx.data_ptr(),
-                           y_bits=self.y_bits.data_ptr(), xt_bits=self.xt_bits.data_ptr(),
+                           y_bits=self.y_bits.data_ptr(),
+                           xt_bits=0 if getattr(self, 'xt_in_gather', False) else self.xt_bits.data_ptr(),
                            reg_idx=self.reg_idx.data_ptr(), status=self.status.data_ptr(),
                            xt_rows=self.xt_rows, reg_slots=B * cfg.world, reg_lo=self.reg_rows[0],
-                           reg_hi=self.reg_rows[1], reg_cap=self.Breg)
+                           reg_hi=self.reg_rows[1], reg_cap=self.Breg,
+                           x_bits=self.x_bits.data_ptr() if getattr(self, 'xt_in_gather', False) else 0)
 
     def _gemm(self, M, N, K, A, lda, B, ldb, ta=0, tb=0, epi=L.CC_EPI_STORE, ldc=None, bias=None,
               relu=0, C=None, Cf=None, H=None, y_bits=None, scale=0.0, partials=None, splits=1,
@@ -666,11 +677,13 @@ class Trainer:
         # ---- E (model.py:35-42) on R rows: gather + 3 Dense
         t = self._tick('cc_embed_gather_fwd')
         wf = self.wpack[0] if self.wpack is not None else None   # warm the tower forward's weights
-        L.call('cc_embed_gather_fwd_warm', self.dtype, self.w('encoder/encoded_1/kernel'),
+        L.call('cc_embed_gather_fwd_xt', self.dtype, self.w('encoder/encoded_1/kernel'),
                self.pf('encoder/encoded_1/bias'), V, d, R, L.ptr(self.x_cnt), L.ptr(self.x_idx),
                self.x_cap, L.ptr(self.H1), L.ptr(wf) if wf is not None else None,
                2 * wf.numel() if wf is not None else 0,
-               L.ptr(self.state) if self._adv_deferred else None, self.batches_per_epoch, s)
+               L.ptr(self.state) if self._adv_deferred else None, self.batches_per_epoch,
+               L.ptr(self.x_bits) if self.xt_in_gather else None,
+               L.ptr(self.xt_bits) if self.xt_in_gather else None, self.xt_rows, s)
         self._adv_deferred = False
         t()
         branches = self.branches()
@@ -873,13 +886,13 @@ class Trainer:
             cfg_ = self.cfg
             src, pk = (self.gpre1p, 1) if self.gpre1p is not None else (self.gPre1T, 0)
             L.call('cc_embed_grad_cs_adam', L.ptr(src), pk, V, d, XR, self.RP, L.ptr(self.xt_bits),
-                   self.gp('encoder/encoded_1/bias'), L.ptr(self.eg_tickets), L.ptr(self.params), L.ptr(self.m),
+                   self.gp('encoder/encoded_1/bias'), self._eg_tk(), L.ptr(self.params), L.ptr(self.m),
                    L.ptr(self.v), L.ptr(self.shadow), L.ptr(self.state), cfg_.lr, cfg_.beta1, cfg_.beta2,
                    cfg_.eps, s)
         elif self.eg_tickets is not None:   # column slices (cc_embed_grad_cs), from the packed image or dPre1^T
             src, pk = (self.gpre1p, 1) if self.gpre1p is not None else (self.gPre1T, 0)
             L.call('cc_embed_grad_cs', L.ptr(src), pk, V, d, XR, self.RP, L.ptr(self.xt_bits),
-                   self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), L.ptr(self.eg_tickets), s)
+                   self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), self._eg_tk(), s)
         elif self.gpre1p is not None:
             L.call('cc_embed_grad_packed', L.ptr(self.gpre1p), V, d, XR, self.RP, L.ptr(self.xt_bits),
                    self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
@@ -897,6 +910,11 @@ class Trainer:
         t()
         if self.fused_tower:
             self._join()
+
+    def _eg_tk(self):
+        """W1-gradient tickets (its last block per row chunk clears the chunk's xt words), or None
+        when the next E1 gather rewrites every xt word (xt_in_gather)."""
+        return None if self.xt_in_gather else L.ptr(self.eg_tickets)
 
     def apply_adam(self, stream=None):
         """TF Adam over every trained parameter (+ bf16 shadow refresh)."""

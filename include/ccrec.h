@@ -103,6 +103,8 @@ typedef struct cc_noise_args {
   int32_t reg_slots;                         /* global reg draws per step (B * world), slots 0.. */
   int32_t reg_lo, reg_hi;                    /* this rank's M~ rows [reg_lo, reg_hi) */
   int32_t reg_cap;                           /* reg rows of this rank: rows B..B+reg_cap-1 of x */
+  uint32_t *x_bits;                          /* [rows, ceil(V/32)] x rows as bitmasks (rows F
+                                                draws: B, or 2B with_reg), or NULL */
 } cc_noise_args;
 int cc_noise_fwd(const cc_noise_args *a, void *stream);
 /* Owner-computes regulariser rows: draws the reg_slots global reg rows of the step
@@ -152,6 +154,18 @@ int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const float *bias
                              int32_t R, const int32_t *x_cnt, const int32_t *x_idx, int32_t x_cap,
                              void *out, const void *warm, int64_t warm_bytes, int64_t *state,
                              int64_t batches_per_epoch, void *stream);
+/* cc_embed_gather_fwd_warm that, with xt_bits non-NULL, also writes the whole W1-gradient
+ * bitmask as the bit transpose of F's x row bitmasks (cc_noise_args.x_bits [R, ceil(V/32)]):
+ * xt_bits[card * ceil(xt_rows/32) + row/32] bit row%32 = x_bits[row] bit card, rows < xt_rows,
+ * every word written (no zeroed xt needed) — the bits cc_noise_fwd sets by atomics when its
+ * xt_bits is non-NULL.  One process gives F x_bits instead of xt_bits: F's next-step draw runs
+ * inside the HBM-bound Adam launch, where its scattered atomics queued behind the Adam streams;
+ * here (bf16 d = 256) the transpose rides as extra blocks of the latency-bound gather. */
+int cc_embed_gather_fwd_xt(int32_t dtype, const void *table, const float *bias, int32_t V, int32_t d,
+                           int32_t R, const int32_t *x_cnt, const int32_t *x_idx, int32_t x_cap,
+                           void *out, const void *warm, int64_t warm_bytes, int64_t *state,
+                           int64_t batches_per_epoch, const uint32_t *x_bits, uint32_t *xt_bits,
+                           int32_t xt_rows, void *stream);
 
 /* ----------------------------------------------------------------------------------
  * E1 backward: dW1[r] = sum_{b : r in x_b} dpre[b] (ascending b, deterministic), for every
@@ -179,7 +193,8 @@ int cc_embed_grad_packed(const void *dpre_p, int32_t V, int32_t d, int32_t R, in
  * packed transposed image (packed != 0, cc_tower_args.gpre1p) or dPre1^T [d][ld_t] (packed == 0,
  * cc_tower_args.gpre1t); d % 32 == 0, R <= 2048.  tickets: cc_embed_grad_cs_tickets(V, d, R)
  * uint32 words, zero before the first call and left zero by every call (the last workgroup of a
- * chunk to stage its bit words clears them in xt_bits and resets its ticket).  Bit-identical to
+ * chunk to stage its bit words clears them in xt_bits and resets its ticket); tickets NULL leaves
+ * xt_bits as it is (for callers that rewrite every word, cc_embed_gather_fwd_xt).  Bit-identical to
  * cc_embed_grad_mfma / cc_embed_grad_packed (same MFMA k order); consumes xt_bits likewise. */
 int cc_embed_grad_cs(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R, int32_t ld_t,
                      uint32_t *xt_bits, float *grad, float *bias_grad, uint32_t *tickets, void *stream);

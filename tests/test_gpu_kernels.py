@@ -18,7 +18,7 @@ def _gpu():
     L.lib()
 
 
-def _run_noise(lists, V, B, ns, seed, step, with_reg=True, slot_rank=0, guide_log2=0):
+def _run_noise(lists, V, B, ns, seed, step, with_reg=True, slot_rank=0, guide_log2=0, x_bits=None):
     dev = 'cuda'
     lens = np.array([len(c) for c in lists])
     indptr = np.zeros(len(lists) + 1, np.int64)
@@ -48,7 +48,8 @@ def _run_noise(lists, V, B, ns, seed, step, with_reg=True, slot_rank=0, guide_lo
                     cdf=cdf_d.data_ptr(), neg_sampler=ns_d.data_ptr(), state=state.data_ptr(),
                     guide=guide.data_ptr() if guide is not None else None, guide_log2=guide_log2,
                     x_cnt=x_cnt.data_ptr(), x_idx=x_idx.data_ptr(), y_bits=y_bits.data_ptr(),
-                    xt_bits=xt.data_ptr(), reg_idx=reg.data_ptr(), status=status.data_ptr(), xt_rows=R)
+                    xt_bits=xt.data_ptr() if x_bits is None else None, reg_idx=reg.data_ptr(),
+                    status=status.data_ptr(), xt_rows=R, x_bits=x_bits.data_ptr() if x_bits is not None else None)
     L.call('cc_noise_fwd', ctypes.byref(a), L.stream_ptr())
     torch.cuda.synchronize()
     assert int(status.item()) == 0
@@ -82,6 +83,51 @@ def test_noise_bit_exact_vs_oracle(V, B, sizes, seed, step, glog2):
     for r in range(0, R, max(1, R // 7)):
         col = (xt[:, r // 32] >> np.uint32(r % 32)) & 1
         assert np.array_equal(np.nonzero(col)[0], xs[r])
+
+
+@pytest.mark.parametrize('V,B,d,sizes,rows', [(22000, 64, 256, (180, 360, 720), 'R'), (1500, 64, 256, (40, 200, 400), 'R'),
+                                               (1500, 64, 64, (40, 200, 400), 'R'), (300, 48, 256, (5, 30, 60), 'B'),
+                                               (1000, 40, 128, (5, 30, 60), 'B')])
+def test_gather_xt_transpose(V, B, d, sizes, rows):
+    """F with x_bits (row bitmasks, no xt atomics) + cc_embed_gather_fwd_xt's bit transpose (fused
+    into the bf16 d = 256 gather, a separate kernel otherwise) == the xt bits F's atomics set, and
+    the gathered rows are unchanged."""
+    lists, Mt, ns = problem(11, B, V, sizes)
+    xs, ys, reg, xt_ref, cdf = _run_noise(lists, V, B, ns, 11, 3)
+    R, VW = 2 * B, (V + 31) // 32
+    xb = torch.zeros(R, VW, device='cuda', dtype=torch.int32)
+    xs2, ys2, _, xt_none, _ = _run_noise(lists, V, B, ns, 11, 3, x_bits=xb)
+    assert not xt_none.any()
+    for r in range(R):
+        assert np.array_equal(xs2[r], xs[r])
+        bits = np.nonzero(np.unpackbits(xb[r].cpu().numpy().view(np.uint8), bitorder='little')[:V])[0]
+        assert np.array_equal(bits, xs[r]), f'x_bits row {r}'
+    xt_rows = R if rows == 'R' else B
+    XW = (xt_rows + 31) // 32
+    exp = np.zeros((V, XW), np.uint32)
+    for r in range(xt_rows):
+        exp[xs[r], r // 32] |= np.uint32(1 << (r % 32))
+    if rows == 'R':
+        assert np.array_equal(exp, xt_ref)
+    cap = max(len(x) for x in xs) + 1
+    x_cnt = torch.tensor([len(x) for x in xs], dtype=torch.int32, device='cuda')
+    x_idx = torch.zeros(R, cap, dtype=torch.int32)
+    for r, x in enumerate(xs):
+        x_idx[r, :len(x)] = torch.from_numpy(x.astype(np.int32))
+    x_idx = x_idx.cuda()
+    table = (torch.randn(V, d, device='cuda') * 0.1).to(torch.bfloat16)
+    bias = torch.randn(d, device='cuda') * 0.1
+    outs = []
+    for xt_on in (False, True):
+        out = torch.zeros(R, d, device='cuda', dtype=torch.bfloat16)
+        xt = torch.full((V, XW), -1, device='cuda', dtype=torch.int32)   # every word is written
+        L.call('cc_embed_gather_fwd_xt', L.CC_BF16, L.ptr(table), L.ptr(bias), V, d, R, L.ptr(x_cnt), L.ptr(x_idx),
+               cap, L.ptr(out), None, 0, None, 1, L.ptr(xb) if xt_on else None, L.ptr(xt) if xt_on else None,
+               xt_rows, L.stream_ptr())
+        torch.cuda.synchronize()
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+    assert np.array_equal(xt.cpu().numpy().view(np.uint32), exp)
 
 
 def test_noise_edge_cases():
