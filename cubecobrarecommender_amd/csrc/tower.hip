@@ -13,6 +13,7 @@
 #include <algorithm>
 
 #include "common.hpp"
+#include "xt.hpp"
 
 // dev-only timing hook (tools/micro/tower_probe.hip defines it); compiled out of the library
 #ifndef TOWER_PROBE
@@ -44,6 +45,9 @@ struct TowerP {
   bf16_t *act6p, *act6tp;  // packed D3 operand images for cc_dec_bce_dw (fast forward only)
   bf16_t *hpt[6], *gpt[6];  // packed transposed H_i / G_i images for the dW kernel (or null)
   bf16_t *gpre1p;           // packed transposed dPre1 for cc_embed_grad_packed (or null)
+  const uint32_t *xb;       // x row bitmasks -> xt (fast forward's extra blocks; or null)
+  uint32_t *xt;
+  int xt_V, xt_rows;
   bool packed, dwpacked;
 };
 
@@ -441,6 +445,10 @@ __device__ __forceinline__ void fast_barrier() { asm volatile("s_waitcnt lgkmcnt
 
 template <int D>
 __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
+  if ((int)blockIdx.x >= p.R / RB) {  // blocks past the chains: the xt transpose on the idle CUs
+    xt_transpose_block(p.xb, p.xt_V, p.xt, p.xt_rows, (int)blockIdx.x - p.R / RB);
+    return;
+  }
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ __attribute__((aligned(16))) float bsm[BIAS_MAX];
   const int ldx = p.maxw + 8;
@@ -1215,6 +1223,10 @@ int make_params(const cc_tower_args *t, TowerP &p) {
   p.gpre1 = t->gpre1;
   p.gpre1t = t->dtype == CC_BF16 ? t->gpre1t : nullptr;
   p.gpre1p = t->dtype == CC_BF16 && t->d <= 256 ? static_cast<bf16_t *>(t->gpre1p) : nullptr;
+  p.xb = static_cast<const uint32_t *>(t->x_bits);
+  p.xt = static_cast<uint32_t *>(t->xt_bits);
+  p.xt_V = t->xt_V;
+  p.xt_rows = t->xt_rows;
   if ((uintptr_t)p.gpre1p & 15) return cc::fail(CC_ERR_ARG, "cc_tower: gpre1p must be 16-B aligned");
   p.slab = t->slab;
   p.slab_elems = slab_off(t->d, 6);
@@ -1256,8 +1268,12 @@ extern "C" int cc_tower_fwd(const cc_tower_args *t, void *stream) {
   if (rc) return rc;
   const int es = t->dtype == CC_BF16 ? 2 : 4;
   const size_t lds = (size_t)2 * RB * (p.maxw + 16 / es) * es;
+  CC_REQUIRE(!p.xt || (p.xb && t->dtype == CC_BF16 && p.d <= 256 && p.xt_V > 0 && p.xt_rows >= 1 &&
+                       p.xt_rows <= p.R),
+             "cc_tower_fwd: xt_bits needs x_bits, bf16, d <= 256 and 1 <= xt_rows <= R");
   if (t->dtype == CC_BF16 && p.d <= 256) {
-    const dim3 g(p.R / RB), b(FNT);
+    const int nxt = p.xt ? (int)cdiv((p.xt_V + 31) / 32, XT_TJ) : 0;
+    const dim3 g((unsigned)(p.R / RB + nxt)), b(FNT);
     hipStream_t s = as_stream(stream);
     switch (p.d) {
       case 64: hipLaunchKernelGGL(tower_fwd_fast_kernel<64>, g, b, lds, s, p); break;

@@ -376,6 +376,14 @@ class Trainer:
         # (F's x rows as bitmasks [R][ceil(V/32)]; rows F does not draw stay zero)
         self.x_bits = (torch.zeros(self.R, (cfg.V + 31) // 32, device=self.dev, dtype=torch.int32)
                        if self.xt_in_gather else None)
+        # ... in the tower forward launch instead when its fast kernel runs (d <= 256): its 16-32
+        # chain blocks leave the other CUs idle (measured: in the gather launch the transpose
+        # blocks cost it 2-3 us)
+        self.xt_in_tower = (self.xt_in_gather and self.targs is not None and cfg.d <= 256
+                            and os.environ.get('CCREC_XT_IN_TOWER', '1') != '0')
+        if self.xt_in_tower:
+            self.targs.x_bits, self.targs.xt_bits = self.x_bits.data_ptr(), self.xt_bits.data_ptr()
+            self.targs.xt_V, self.targs.xt_rows = cfg.V, self.xt_rows
         # one process, packed tower images: the Adam + F launch also rewrites the tower kernels'
         # packed images and advances the step counters (cc_adam_noise_pack) — the next step
         # starts without a counters/transposes launch
@@ -682,8 +690,8 @@ class Trainer:
                self.x_cap, L.ptr(self.H1), L.ptr(wf) if wf is not None else None,
                2 * wf.numel() if wf is not None else 0,
                L.ptr(self.state) if self._adv_deferred else None, self.batches_per_epoch,
-               L.ptr(self.x_bits) if self.xt_in_gather else None,
-               L.ptr(self.xt_bits) if self.xt_in_gather else None, self.xt_rows, s)
+               L.ptr(self.x_bits) if self.xt_in_gather and not self.xt_in_tower else None,
+               L.ptr(self.xt_bits) if self.xt_in_gather and not self.xt_in_tower else None, self.xt_rows, s)
         self._adv_deferred = False
         t()
         branches = self.branches()

@@ -348,6 +348,12 @@ typedef struct cc_tower_args {
    * ceil64(R) (rows past R stay zero: allocate zeroed) — cc_embed_grad_packed's B operand; when
    * set, the fast backward chain writes it instead of gpre1t. */
   void *gpre1p;
+  /* optional (bf16, d <= 256): cc_tower_fwd also writes the W1-gradient bitmask xt_bits
+   * [xt_V][ceil(xt_rows/32)] as the bit transpose of x_bits [>= xt_rows][ceil(xt_V/32)] (as
+   * cc_embed_gather_fwd_xt does), in extra blocks beside the 32-row tower chains (NULL: no). */
+  const void *x_bits;
+  void *xt_bits;
+  int32_t xt_V, xt_rows;
 } cc_tower_args;
 int64_t cc_tower_slab_elems(int32_t d);
 int cc_tower_fwd(const cc_tower_args *t, void *stream);
