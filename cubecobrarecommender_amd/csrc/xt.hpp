@@ -11,7 +11,10 @@ namespace {
 // One block per XT_TJ words of cards (32 XT_TJ cards); a wave transposes two 32 x 32 bit tiles per
 // pass (lanes 0-31 tile A, 32-63 tile B) by 32 ballots, every xt word written.  The row words of
 // XT_Q passes are loaded up front (unconditional clamped loads): one load latency per XT_Q passes.
-constexpr int XT_TJ = 2, XT_Q = 4;
+#ifndef CC_XT_TJ
+#define CC_XT_TJ 2
+#endif
+constexpr int XT_TJ = CC_XT_TJ, XT_Q = 4;
 __device__ __forceinline__ void xt_transpose_block(const uint32_t *__restrict__ xb, int V,
                                                    uint32_t *__restrict__ xt, int xt_rows, int tb) {
   const int VW = (V + 31) >> 5, XW = (xt_rows + 31) >> 5;
