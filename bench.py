@@ -76,8 +76,9 @@ def setup_dist(args):
         ndev = torch.cuda.device_count()
         local = local % ndev
         torch.cuda.set_device(local)
-        if args.backend == 'nccl' and ndev < world:   # RCCL needs one GPU per rank
-            print(f'bench.py: {world} ranks on {ndev} GPU(s): gloo collectives instead of RCCL',
+        per_node = int(os.environ.get('LOCAL_WORLD_SIZE', str(world)))
+        if args.backend == 'nccl' and ndev < per_node:   # RCCL needs one GPU per rank
+            print(f'bench.py: {per_node} ranks on {ndev} GPU(s): gloo collectives instead of RCCL',
                   file=sys.stderr)
             args.backend = 'gloo'
         if args.backend == 'nccl':

@@ -84,6 +84,7 @@ _P, _I32, _I64, _F32, _F64, _SZ = C.c_void_p, C.c_int32, C.c_int64, C.c_float, C
 SIGNATURES = {
     'cc_abi_version': (C.c_int, []),
     'cc_last_error_string': (C.c_char_p, []),
+    'cc_build_id': (C.c_char_p, []),
     'cc_param_layout': (C.c_int, [_I32, _I32, _P, _P, _P, _P]),
     'cc_crc32c': (C.c_uint32, [C.c_uint32, _P, _SZ]),
     'cc_noise_fwd': (C.c_int, [C.POINTER(NoiseArgs), _P]),
@@ -176,6 +177,18 @@ def lib():
             raise CCError('libccrec_hip ABI version mismatch')
         _lib = L
     return _lib
+
+
+def check_build_id():
+    """Raise unless the loaded library was compiled from the sources in this tree (buildid.py):
+    tests/conftest.py and __graft_entry__.smoke() call it so no result rests on a stale binary."""
+    from .buildid import tree_build_id
+    got = lib().cc_build_id().decode()
+    want = tree_build_id()
+    if got != want:
+        raise CCError(f'{LIB_PATH} was built from other sources (build id {got}, tree {want}): '
+                      f'rebuild with `python -m cubecobrarecommender_amd.build`')
+    return got
 
 
 def check(rc, what=''):

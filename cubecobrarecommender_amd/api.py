@@ -52,10 +52,12 @@ def get_model(path):
         return _models[path]
 
 
-def recommend(model, cube_indices, amount, int_to_card, non_json=False, print_fn=print):
+def recommend(model, cube_indices, amount, int_to_card, non_json=False, print_fn=print, print_cuts=True):
     """ml_recommend.py:78-116 / ml_recommend_web.py:39-67 on the GPU.  Returns
     {"additions": {name: p}, "cuts": {name: p}} (additions empty in non_json mode, as the reference
-    prints instead of storing them)."""
+    prints instead of storing them).  print_cuts: in non_json mode also print the lowest-scoring
+    cuts — the CLI does (ml_recommend.py:110-116), the web function does not
+    (ml_recommend_web.py:50-67 prints only the additions)."""
     out = model.recommender().recommend(cube_indices, amount)
     output = {'additions': {}, 'cuts': {}}
     for idx, p in zip(out['additions'].tolist(), out['add_vals'].tolist()):
@@ -66,7 +68,7 @@ def recommend(model, cube_indices, amount, int_to_card, non_json=False, print_fn
             output['additions'][card] = p
     for idx, p in zip(list(cube_indices), out['cut_vals'].tolist()):
         output['cuts'][int_to_card[idx]] = p
-    if non_json:   # ml_recommend.py:110-116: lowest-scoring cuts
+    if non_json and print_cuts:   # ml_recommend.py:110-116: lowest-scoring cuts
         cards = list(output['cuts'].keys())
         vals = list(output['cuts'].values())
         rank_cuts = np.argsort(np.array(vals), kind='stable')

@@ -38,22 +38,33 @@ def _headers_mtime():
     return max(os.path.getmtime(h) for h in hs)
 
 
-def _compile(src, force):
+def _compile(src, force, build_id):
     obj = os.path.join(OBJ, os.path.basename(src) + '.o')
+    extra = []
+    if os.path.basename(src) == 'api.cpp':   # the source identity (buildid.py) lives in api.cpp
+        extra = [f'-DCC_BUILD_ID="{build_id}"']
+        stamp = os.path.join(OBJ, 'build_id.txt')
+        if not os.path.exists(stamp) or open(stamp).read() != build_id:
+            force = True
     if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(src), _headers_mtime()):
         return obj
-    cmd = [HIPCC, *FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), '-c', src, '-o', obj]
+    cmd = [HIPCC, *FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *extra, '-c', src, '-o', obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f'hipcc failed for {src}:\n{r.stderr}')
+    if extra:
+        with open(os.path.join(OBJ, 'build_id.txt'), 'w') as fh:
+            fh.write(build_id)
     return obj
 
 
 def build(force=False, jobs=8):
+    from .buildid import tree_build_id
     os.makedirs(OBJ, exist_ok=True)
+    bid = tree_build_id()
     try:
         with cf.ThreadPoolExecutor(jobs) as ex:
-            objs = list(ex.map(lambda s: _compile(s, force), sources()))
+            objs = list(ex.map(lambda s: _compile(s, force, bid), sources()))
     except RuntimeError:
         if os.path.exists(LIB):
             os.remove(LIB)        # never leave a stale library behind a failed build

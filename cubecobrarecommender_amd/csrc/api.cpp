@@ -40,6 +40,13 @@ int param_offsets(int V, int d, int64_t *off, int64_t *size, int64_t *total, int
 
 extern "C" int cc_abi_version(void) { return CC_ABI_VERSION; }
 
+// SHA-256 prefix of the sources this library was compiled from (build.py -> buildid.py); the
+// Python side refuses a library whose id differs from the tree's sources.
+#ifndef CC_BUILD_ID
+#define CC_BUILD_ID "unknown"
+#endif
+extern "C" const char *cc_build_id(void) { return CC_BUILD_ID; }
+
 extern "C" const char *cc_last_error_string(void) { return cc::g_last_error.c_str(); }
 
 extern "C" int cc_param_layout(int32_t V, int32_t d, int64_t *offsets, int64_t *sizes,

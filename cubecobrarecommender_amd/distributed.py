@@ -31,7 +31,15 @@ def init(backend=None):
     if world > 1 and not torch.distributed.is_initialized():
         backend = backend or os.environ.get('CCREC_DIST_BACKEND')
         if backend is None:
-            backend = 'nccl' if cuda and torch.cuda.device_count() >= world else 'gloo'
+            # one GPU per rank OF THIS NODE (LOCAL_WORLD_SIZE; a multi-node launch has world >
+            # GPUs per node and still one GPU per rank)
+            per_node = int(os.environ.get('LOCAL_WORLD_SIZE', str(world)))
+            backend = 'nccl' if cuda and torch.cuda.device_count() >= per_node else 'gloo'
+            if backend == 'gloo':
+                import sys
+                print(f'cubecobrarecommender_amd.distributed: {per_node} ranks per node on '
+                      f'{torch.cuda.device_count() if cuda else 0} GPU(s): gloo collectives instead of RCCL',
+                      file=sys.stderr)
         kw = {'device_id': dev} if backend == 'nccl' else {}
         torch.distributed.init_process_group(backend, **kw)
     return world, rank, dev

@@ -22,6 +22,7 @@ from .layout import Layout, glorot_flat
 from .recommender import Recommender
 
 _LOSSES = ('binary_crossentropy', 'kullback_leibler_divergence')
+STATUS_EVERY = 16   # fit(): device status flags are read (one host sync) every this many steps
 
 
 class Tensor:
@@ -115,7 +116,12 @@ class CC_Recommender:
         from .trainer import TrainConfig, Trainer
         cfg = TrainConfig(V=self.N, d=self.d, batch_size=generator.batch_size, reg=self.reg,
                           noise=generator.noise, noise_std=generator.noise_std, lr=self.lr,
-                          dtype=self.dtype, seed=self.seed, rank=rank, world=world)
+                          dtype=self.dtype, seed=self.seed, rank=rank, world=world,
+                          # one process: W1's Adam inside its gradient kernel where the trainer's
+                          # bf16 path supports it (bit-identical to the unfused step,
+                          # tests/test_gpu_train.py::test_fused_w1_adam_matches_unfused) — the
+                          # configuration bench.py measures
+                          fuse_w1_adam=(world == 1))
         tr = Trainer(cfg, generator.data, params_flat=self._current_flat())
         if self._m is not None:
             tr.load_standard(tr.m, self._m)
@@ -129,9 +135,11 @@ class CC_Recommender:
         for ep in range(epochs):
             t0 = time.perf_counter()
             loss_sum.zero_()
-            for _ in range(steps):
+            for i in range(steps):
                 tr.step()          # data-parallel: bucketed reduce-scatter + sharded Adam (zero.py)
                 loss_sum += tr.loss_dev
+                if (i + 1) % STATUS_EVERY == 0:   # an x_cap / owner-capacity overflow stops the
+                    tr.check_status()             # run within STATUS_EVERY steps, not at epoch end
             torch.cuda.synchronize()
             tr.check_status()
             l = tr.losses(loss_sum / steps)

@@ -84,6 +84,17 @@ def full_rows(V, world, rank):
     return min(V, rank * per), min(V, (rank + 1) * per)
 
 
+def fused_reg_fits(hi, V, Breg):
+    """cc_dec_softmax_kl_dw's 32-bit buffer extents (decreg.hip: mt_bytes < 2^31 for M~ rows up to
+    `hi`, the Breg x V bf16 dZ < 2^32 bytes)."""
+    return hi * V * 4 <= 0x7FFFFFFF and Breg * V * 2 <= 0xFFFFFFFF
+
+
+def dx_splitk_fits(M, V, d):
+    """cc_gemm_dx_splitk's operand extents (dxgemm.hip: M*V and d*V bf16 elements < 2 GB)."""
+    return M * V * 2 < (1 << 31) and d * V * 2 < (1 << 31)
+
+
 def _cdf(neg_sampler):
     cdf = np.cumsum(np.asarray(neg_sampler, np.float64))
     return cdf / cdf[-1]
@@ -315,8 +326,11 @@ class Trainer:
             self.slab = torch.zeros((R // 32) * slab, **f32)
             # D2 output layer fused (logits twice -> softmax -> KL -> dZ -> dWo, csrc/decreg.hip): bf16,
             # d in {128, 256} with the packed D3 images (the same shape class as the fused D1 kernel)
+            # (its buffer descriptors address M~ up to row hi and the Breg x V bf16 dZ with 32-bit
+            # extents: larger card pools fall back to the Z2 path instead of failing)
             self.fused_reg = (self.use_reg and self.D3p is not None and not self.mx8 and d in (128, 256)
-                              and self.Breg % 32 == 0 and os.environ.get('CCREC_REG_FUSED', '1') != '0')
+                              and self.Breg % 32 == 0 and fused_reg_fits(self.reg_rows[1], V, self.Breg)
+                              and os.environ.get('CCREC_REG_FUSED', '1') != '0')
             # decoder operands kept k-contiguous: D3^T (tower fwd), dZ^T (BCE epilogue), Wo^T shadow
             self.D3t = torch.zeros(d, R, **T)
             self.dZt = [torch.zeros(V, n, **T) if not (k == 1 and self.fused_reg) else None
@@ -837,7 +851,8 @@ class Trainer:
         """Decoder dX split-K partials into split_buf: the LDS-DMA pipelined kernel (dxgemm.hip)
         on the bf16 shapes it takes, else cc_gemm's register-staged NT path (same partials)."""
         d, V = self.cfg.d, self.cfg.V
-        if (self.dx_glds and not self.mx8 and nr % 128 == 0 and d % 128 == 0 and V % 8 == 0):
+        if (self.dx_glds and not self.mx8 and nr % 128 == 0 and d % 128 == 0 and V % 8 == 0
+                and dx_splitk_fits(nr, V, d)):
             L.call('cc_gemm_dx_splitk', L.ptr(self.dZout[r0:]), V, self.w(pre + '/reconstruct/kernel'), V,
                    nr, d, V, splits, L.ptr(self.split_buf), s)
         else:

@@ -15,8 +15,10 @@ HBM traffic world times over.  Here (ZeRO-1):
     updated fp32 parameters in place; the bf16 operand shadow is refreshed locally.
 
 Every rank ends the step with identical parameters; m and v are only kept current on the owning
-rank's shard (the checkpoint writer gathers them, model.py).  With the gloo backend (CPU tests)
-reduce-scatter is emulated by all-reduce + slice.
+rank's shard (the checkpoint writer gathers them, model.py).  Every backend runs the same two
+collectives RCCL runs (reduce_scatter_tensor, in-place all_gather_into_tensor): gloo takes them on
+CPU tensors, so with gloo and device buffers (several ranks rehearsed on one GPU) each bucket is
+staged through a host copy around the identical call.
 """
 import torch
 import torch.distributed as dist
@@ -29,6 +31,8 @@ class ShardedStep:
         self.world = trainer.cfg.world
         self.rank = trainer.cfg.rank
         self.nccl = dist.get_backend(group) == 'nccl'
+        # gloo + device buffers: host staging around the same collective calls
+        self.stage = (not self.nccl) and trainer.params.is_cuda
         self.buckets = []
         for name, lo, hi in trainer.layout.buckets(trainer.use_reg):
             size = hi - lo
@@ -46,24 +50,23 @@ class ShardedStep:
     # ------------------------------------------------------------------ collectives
     def reduce_scatter(self, b, grads):
         src = grads[b['lo']:b['hi']]
-        if self.nccl:
-            dist.reduce_scatter_tensor(b['gshard'], src, op=dist.ReduceOp.SUM, group=self.group)
+        if self.stage:
+            out = torch.empty(b['chunk'], dtype=torch.float32)
+            dist.reduce_scatter_tensor(out, src.cpu(), op=dist.ReduceOp.SUM, group=self.group)
+            b['gshard'].copy_(out)
         else:
-            tmp = src.clone()
-            dist.all_reduce(tmp, op=dist.ReduceOp.SUM, group=self.group)
-            off = b['s0'] - b['lo']
-            b['gshard'].copy_(tmp[off:off + b['chunk']])
+            dist.reduce_scatter_tensor(b['gshard'], src, op=dist.ReduceOp.SUM, group=self.group)
         b['gshard'].mul_(1.0 / self.world)
 
     def all_gather(self, b, buf):
         full = buf[b['lo']:b['hi']]
-        mine = buf[b['s0']:b['s0'] + b['chunk']]
-        if self.nccl:   # in place: my shard already sits at rank * chunk inside the output
-            dist.all_gather_into_tensor(full, mine, group=self.group)
-        else:
-            parts = [torch.empty_like(mine) for _ in range(self.world)]
-            dist.all_gather(parts, mine.clone(), group=self.group)
-            full.copy_(torch.cat(parts))
+        off = b['s0'] - b['lo']
+        if self.stage:
+            host = full.cpu()
+            dist.all_gather_into_tensor(host, host[off:off + b['chunk']], group=self.group)
+            full.copy_(host)
+        else:           # in place: my shard already sits at rank * chunk inside the output
+            dist.all_gather_into_tensor(full, full[off:off + b['chunk']], group=self.group)
 
     def update(self, b, adam_fn, timing=False):
         """Reduce-scatter bucket b, Adam on this rank's shard, all-gather the parameters."""

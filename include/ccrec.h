@@ -47,6 +47,9 @@ enum cc_dtype { CC_F32 = 0, CC_BF16 = 1, CC_MX8 = 2 };
 
 int cc_abi_version(void);
 const char *cc_last_error_string(void);
+/* Source identity: the first 32 hex digits of a SHA-256 over csrc/ + include/ (buildid.py),
+ * compiled in by build.py.  Callers compare it with their tree to refuse a stale binary. */
+const char *cc_build_id(void);
 
 /* Host utility: CRC32C (Castagnoli) of [data, data+n) continuing from crc (0 to start) — the
  * checksum of TF tensor-bundle checkpoints (ml_files/<name>/variables). */

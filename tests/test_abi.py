@@ -49,3 +49,10 @@ def test_error_reporting_without_gpu():
     rc = lib.cc_param_layout(0, 0, None, None, None, None)
     assert rc == -1
     assert b'null' in lib.cc_last_error_string() or b'positive' in lib.cc_last_error_string()
+
+
+def test_library_build_id_is_this_trees():
+    """cc_build_id() carries the SHA-256 prefix of csrc/ + include/ the library was built from."""
+    from cubecobrarecommender_amd.buildid import tree_build_id
+    assert L.lib().cc_build_id().decode() == tree_build_id()
+    assert len(tree_build_id()) == 32

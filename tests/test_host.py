@@ -65,3 +65,15 @@ def test_reg_row_shards_equal_mass_and_owner_draws():
     heavy[0] = 0.91
     with pytest.raises(ValueError):
         reg_row_shards(np.cumsum(heavy) / heavy.sum(), 4)
+
+
+def test_fused_kernel_extent_gates():
+    """The fused D2 kernel and the split-K dX take 32-bit buffer extents: above them the trainer
+    must pick the unfused paths instead of failing at the first step."""
+    from cubecobrarecommender_amd.trainer import dx_splitk_fits, fused_reg_fits
+    assert fused_reg_fits(22000, 22000, 512)
+    assert fused_reg_fits(23170, 23170, 512)
+    assert not fused_reg_fits(23171, 23171, 512)       # hi * V * 4 > 2^31 - 1
+    assert fused_reg_fits(23171 // 2, 23171, 512)       # a row shard ending below the limit
+    assert dx_splitk_fits(512, 22000, 256)
+    assert not dx_splitk_fits(33000, 33000, 256)       # full-mode dZ (Breg ~ V) past 2 GB

@@ -18,6 +18,7 @@ def get_ml_recommend(cube_name, amount, root=ROOT, non_json=False,
     int_to_card, card_to_int = api.load_id_map(id_map)                  # :21-23
     cube_indices = api.cube_indices_of(card_names, card_to_int)         # :27-32
     model = api.get_model(model_dir)                                    # :37 (resident here)
-    output = api.recommend(model, cube_indices, amount, int_to_card, non_json=non_json)
+    output = api.recommend(model, cube_indices, amount, int_to_card, non_json=non_json,
+                           print_cuts=False)                           # :50-64 (additions only)
     if not non_json:
         return output
