@@ -13,11 +13,14 @@ The variables are a TF *tensor bundle*:
 Object paths follow the attribute names of model.py (``encoder/encoded_1/kernel`` ...), Adam slots
 ``<var>/.OPTIMIZER_SLOT/optimizer/{m,v}/...`` and ``optimizer/iter`` etc.
 
-The writer produces a bundle any tensor-bundle reader (tf.train.load_checkpoint) can parse; the
-reader parses such files (multi-block, prefix-compressed, multi-shard).  ``saved_model.pb`` (the
-TF graph, which TF is needed to produce) is written as an empty SavedModel message, and
-``ccrec_config.json`` records (V, d).  No real checkpoint exists in this pipeline (all ml_files
-are Git-LFS pointers), so compatibility with files written by TF itself is unpinned.
+The writer produces a bundle any tensor-bundle reader (tf.train.load_checkpoint) can parse, with
+the TF2 `_CHECKPOINTABLE_OBJECT_GRAPH` string (a TrackableObjectGraph proto naming every saved
+variable, its Keras layer name and Adam slots); the reader parses such files (multi-block,
+prefix-compressed, multi-shard, string tensors).  The reference's Git-LFS pointers pin the data
+sizes (12 * P + 40 B of variables at |V| = 20,884, d = 512; tests/test_checkpoint.py checks the
+writer against them); the byte contents of files written by TF itself stay unpinned (no real
+checkpoint exists in this pipeline).  ``saved_model.pb`` (the TF graph, which TF is needed to
+produce) is written as an empty SavedModel message, and ``ccrec_config.json`` records (V, d).
 """
 import json
 import os
@@ -29,9 +32,27 @@ from . import _lib as L
 from .layout import NAMES, Layout
 
 MAGIC = 0xdb4775248b80fb57
-DT_FLOAT, DT_INT64 = 1, 9
+DT_FLOAT, DT_STRING, DT_INT64 = 1, 7, 9
 _NP = {DT_FLOAT: np.float32, DT_INT64: np.int64}
 VAR_SUFFIX = '/.ATTRIBUTES/VARIABLE_VALUE'
+OBJECT_GRAPH_KEY = '_CHECKPOINTABLE_OBJECT_GRAPH'
+
+# Keras layer names of model.py (Dense(..., name=...)): the variables' TF names (full_name in the
+# object graph), e.g. encoder/encoded_1 -> 'encoder_e1' (model.py:27), decoder/reconstruct ->
+# 'main_reconstruction' (model.py:64, Decoder("main", ...) at :94)
+_LAYER_NAMES = {'encoder/encoded_1': 'encoder_e1', 'encoder/encoded_2': 'encoder_e2',
+                'encoder/encoded_3': 'encoder_e3', 'encoder/bottleneck': 'encoder_bottleneck'}
+for _pre, _tag in (('decoder', 'main'), ('decoder_for_reg', 'reg')):
+    _LAYER_NAMES.update({f'{_pre}/decoded_1': f'{_tag}_d1', f'{_pre}/decoded_2': f'{_tag}_d2',
+                         f'{_pre}/decoded_3': f'{_tag}_d3', f'{_pre}/reconstruct': f'{_tag}_reconstruction'})
+# Adam's scalar variables (Keras OptimizerV2: `iter` int64 + the float hyper-parameters) and the
+# compiled metrics' accumulators (keras_api/metrics/<i>/{total,count}).  The reference's own
+# checkpoints pin their total: the GPU shard of every 2-shard save is 391,661,320 B = 12 * P + 40
+# at |V| = 20,884, d = 512 (P = 32,638,440: weights + Adam m + v), i.e. 40 B of scalars beside the
+# object graph (shard 0, 18,317 B) — 8 (iter) + 4 * 4 (learning_rate, beta_1, beta_2, decay) + 2 *
+# 2 * 4 (two Mean accumulators: 'loss' and the first output's loss, model.metrics order).
+OPT_HYPERS = ('learning_rate', 'beta_1', 'beta_2', 'decay')
+METRICS = ('loss', 'output_1_loss')
 
 
 def crc32c(data, crc=0):
@@ -199,24 +220,46 @@ def _read_table(path):
 
 
 # ---------------------------------------------------------------------------- bundle
-def write_bundle(prefix, tensors):
-    """tensors: dict key -> numpy array (float32 / int64).  Writes <prefix>.index + .data-00000-of-00001."""
+def _string_scalar_bytes(b):
+    """A scalar DT_STRING tensor in a bundle data file (TF tensor_bundle's string layout): varint64
+    element length, the masked crc32c of the length bytes (uint32 LE), then the bytes."""
+    n = _varint(len(b))
+    return n + struct.pack('<I', _mask(crc32c(n))) + b
+
+
+def write_bundle(prefix, tensors, shard_of=None):
+    """tensors: dict key -> numpy array (float32 / int64) or bytes (a scalar DT_STRING).  Writes
+    <prefix>.index + <prefix>.data-0000K-of-0000N; shard_of(key) -> shard id (default: one shard).
+    TF's multi-device saver writes one shard per device (the object graph on the CPU shard, the
+    variables on the GPU shard), which the reference's 2-shard checkpoints show."""
     os.makedirs(os.path.dirname(prefix), exist_ok=True)
-    entries = [(b'', _header_proto(1))]
-    off = 0
-    with open(prefix + '.data-00000-of-00001', 'wb') as fh:
+    shard_of = shard_of or (lambda key: 0)
+    nshards = 1 + max((shard_of(k) for k in tensors), default=0)
+    entries = [(b'', _header_proto(nshards))]
+    files = [open(f'{prefix}.data-{s:05d}-of-{nshards:05d}', 'wb') for s in range(nshards)]
+    offs = [0] * nshards
+    try:
         for key in sorted(tensors):
-            a = np.array(tensors[key], order="C", copy=True)   # keeps 0-d scalars 0-d
-            dt = DT_FLOAT if a.dtype == np.float32 else DT_INT64
-            a = a.astype(_NP[dt], copy=False)
-            raw = a.tobytes()
-            fh.write(raw)
-            entries.append((key.encode(), _entry_proto(dt, a.shape, 0, off, len(raw), _mask(crc32c(raw)))))
-            off += len(raw)
+            sh = shard_of(key)
+            val = tensors[key]
+            if isinstance(val, (bytes, bytearray)):
+                dt, shape, raw = DT_STRING, (), _string_scalar_bytes(bytes(val))
+            else:
+                a = np.array(val, order="C", copy=True)   # keeps 0-d scalars 0-d
+                dt = DT_FLOAT if a.dtype == np.float32 else DT_INT64
+                a = a.astype(_NP[dt], copy=False)
+                shape, raw = a.shape, a.tobytes()
+            files[sh].write(raw)
+            entries.append((key.encode(), _entry_proto(dt, shape, sh, offs[sh], len(raw), _mask(crc32c(raw)))))
+            offs[sh] += len(raw)
+    finally:
+        for fh in files:
+            fh.close()
     _write_table(prefix + '.index', entries)
 
 
 def read_bundle(prefix, verify=True):
+    """-> {key: numpy array (float32 / int64) or bytes (scalar DT_STRING)}."""
     ents = _read_table(prefix + '.index')
     header = _parse(dict(ents)[b''])
     nshards = header.get(1, [1])[0]
@@ -227,20 +270,117 @@ def read_bundle(prefix, verify=True):
             continue
         e = _parse(v)
         dt = e.get(1, [0])[0]
-        if dt not in _NP:
+        if dt not in _NP and dt != DT_STRING:
             continue
         shape = [(_parse(dim).get(1, [0])[0]) for dim in _parse(e[2][0]).get(2, [])] if 2 in e else []
         shard, off, size = e.get(3, [0])[0], e.get(4, [0])[0], e.get(5, [0])[0]
         raw = np.asarray(shards[shard][off:off + size])
         if verify and 6 in e and _unmask(e[6][0]) != crc32c(raw):
             raise ValueError(f'crc mismatch for {k!r}')
+        if dt == DT_STRING:
+            if shape:
+                raise ValueError(f'{k!r}: only scalar strings are supported')
+            b = raw.tobytes()
+            n, i = _read_varint(b, 0)
+            if verify and _unmask(struct.unpack_from('<I', b, i)[0]) != crc32c(b[:i]):
+                raise ValueError(f'length crc mismatch for {k!r}')
+            out[k.decode()] = b[i + 4:i + 4 + n]
+            continue
         out[k.decode()] = raw.view(_NP[dt]).reshape(shape).copy()
     return out
 
 
+# ---------------------------------------------------------------------------- object graph
+def object_graph(keys, metrics=METRICS):
+    """TrackableObjectGraph proto (tensorflow/core/protobuf/trackable_object_graph.proto) of the
+    model's checkpoint — the `_CHECKPOINTABLE_OBJECT_GRAPH` string a TF2 checkpoint carries:
+    root (CC_Recommender, model.py:82-98) -> encoder / decoder / decoder_for_reg -> Dense layers
+    -> kernel / bias; optimizer -> iter + hypers, with slot_variables (m, v) per model variable;
+    keras_api -> metrics -> <i> -> total / count.  `keys`: the checkpoint keys written (so the
+    graph names exactly the saved tensors).
+      TrackableObject: children=1 {node_id=1, local_name=2}, attributes=2 {name=1, full_name=2,
+      checkpoint_key=3}, slot_variables=3 {original_variable_node_id=1, slot_name=2,
+      slot_variable_node_id=3}."""
+    keys = set(keys)
+    nodes = [{'children': [], 'attrs': [], 'slots': []}]
+
+    def new(parent, local):
+        nodes.append({'children': [], 'attrs': [], 'slots': []})
+        nodes[parent]['children'].append((len(nodes) - 1, local))
+        return len(nodes) - 1
+
+    def var(node, path, full):
+        nodes[node]['attrs'].append(('VARIABLE_VALUE', full, path + VAR_SUFFIX))
+
+    var_node = {}
+    subs = {}
+    for n in NAMES:
+        if n + VAR_SUFFIX not in keys:
+            continue
+        sub, layer, w = n.split('/')
+        if sub not in subs:
+            subs[sub] = (new(0, sub), {})
+        sid, layers = subs[sub]
+        if layer not in layers:
+            layers[layer] = new(sid, layer)
+        vid = new(layers[layer], w)
+        var(vid, n, f'cc__recommender/{sub}/{_LAYER_NAMES[sub + "/" + layer]}/{w}')
+        var_node[n] = vid
+    if f'optimizer/iter{VAR_SUFFIX}' in keys:
+        opt = new(0, 'optimizer')
+        for h in ('iter',) + OPT_HYPERS:
+            if f'optimizer/{h}{VAR_SUFFIX}' in keys:
+                var(new(opt, h), f'optimizer/{h}', f'Adam/{h}')
+        for n, vid in var_node.items():
+            for slot in ('m', 'v'):
+                path = f'{n}/.OPTIMIZER_SLOT/optimizer/{slot}'
+                if path + VAR_SUFFIX in keys:
+                    nodes.append({'children': [], 'attrs': [], 'slots': []})
+                    sv = len(nodes) - 1
+                    var(sv, path, f'Adam/cc__recommender/{n}/{slot}')
+                    nodes[opt]['slots'].append((vid, slot, sv))
+    if any(k.startswith('keras_api/metrics/') for k in keys):
+        api = new(0, 'keras_api')
+        ml = new(api, 'metrics')
+        for i, name in enumerate(metrics):
+            if f'keras_api/metrics/{i}/total{VAR_SUFFIX}' not in keys:
+                continue
+            mi = new(ml, str(i))
+            for w in ('total', 'count'):
+                var(new(mi, w), f'keras_api/metrics/{i}/{w}', f'{name}/{w}')
+    out = b''
+    for nd in nodes:
+        body = b''.join(_field(1, 2, _field(1, 0, c) + _field(2, 2, l.encode())) for c, l in nd['children'])
+        body += b''.join(_field(2, 2, _field(1, 2, a.encode()) + _field(2, 2, f.encode()) + _field(3, 2, k.encode()))
+                         for a, f, k in nd['attrs'])
+        body += b''.join(_field(3, 2, _field(1, 0, o) + _field(2, 2, sn.encode()) + _field(3, 0, sv))
+                         for o, sn, sv in nd['slots'])
+        out += _field(1, 2, body)
+    return out
+
+
+def parse_object_graph(b):
+    """-> list of nodes {'children': [(node_id, local_name)], 'attrs': [(name, full_name, key)],
+    'slots': [(orig_node, slot_name, slot_node)]} (the inverse of object_graph)."""
+    nodes = []
+    for body in _parse(b).get(1, []):
+        f = _parse(body)
+        ch = [(_parse(c).get(1, [0])[0], _parse(c).get(2, [b''])[0].decode()) for c in f.get(1, [])]
+        at = [tuple(_parse(a).get(i, [b''])[0].decode() for i in (1, 2, 3)) for a in f.get(2, [])]
+        sl = [(_parse(x).get(1, [0])[0], _parse(x).get(2, [b''])[0].decode(), _parse(x).get(3, [0])[0])
+              for x in f.get(3, [])]
+        nodes.append({'children': ch, 'attrs': at, 'slots': sl})
+    return nodes
+
+
 # ---------------------------------------------------------------------------- model files
-def save_model(dest, V, d, params, m=None, v=None, step=0, lr=1e-3, beta1=0.9, beta2=0.999):
-    """ml_files/<name>/ as train.py:112-115 lays it out.  params/m/v: dict name -> array."""
+def save_model(dest, V, d, params, m=None, v=None, step=0, lr=1e-3, beta1=0.9, beta2=0.999,
+               metrics=None, shards=1):
+    """ml_files/<name>/ as train.py:112-115 lays it out.  params/m/v: dict name -> array.
+    metrics: {'loss': (total, count), 'output_1_loss': (total, count)} — the compiled metrics'
+    accumulators after fit (zeros when absent; written with the optimizer state).  shards=2: the
+    object graph in shard 0 and every variable in shard 1, as the reference's GPU-trained
+    checkpoints are laid out (ml_files/cc_rec_1000_regularization/variables/)."""
     os.makedirs(os.path.join(dest, 'variables'), exist_ok=True)
     t = {}
     for n in NAMES:
@@ -250,11 +390,15 @@ def save_model(dest, V, d, params, m=None, v=None, step=0, lr=1e-3, beta1=0.9, b
             t[n + '/.OPTIMIZER_SLOT/optimizer/v' + VAR_SUFFIX] = np.asarray(v[n], np.float32)
     if m is not None:
         t['optimizer/iter' + VAR_SUFFIX] = np.array(step, np.int64)
-        t['optimizer/learning_rate' + VAR_SUFFIX] = np.array(lr, np.float32)
-        t['optimizer/beta_1' + VAR_SUFFIX] = np.array(beta1, np.float32)
-        t['optimizer/beta_2' + VAR_SUFFIX] = np.array(beta2, np.float32)
-        t['optimizer/decay' + VAR_SUFFIX] = np.array(0.0, np.float32)
-    write_bundle(os.path.join(dest, 'variables', 'variables'), t)
+        for h, val in zip(OPT_HYPERS, (lr, beta1, beta2, 0.0)):
+            t[f'optimizer/{h}' + VAR_SUFFIX] = np.array(val, np.float32)
+        for i, name in enumerate(METRICS):
+            tot, cnt = (metrics or {}).get(name, (0.0, 0.0))
+            t[f'keras_api/metrics/{i}/total' + VAR_SUFFIX] = np.array(tot, np.float32)
+            t[f'keras_api/metrics/{i}/count' + VAR_SUFFIX] = np.array(cnt, np.float32)
+    t[OBJECT_GRAPH_KEY] = object_graph(t.keys())
+    write_bundle(os.path.join(dest, 'variables', 'variables'), t,
+                 shard_of=(lambda k: 0 if k == OBJECT_GRAPH_KEY else 1) if shards == 2 else None)
     open(os.path.join(dest, 'saved_model.pb'), 'wb').close()          # empty SavedModel message
     json.dump({'num_cards': int(V), 'd': int(d), 'format': 'ccrec-mi355x/1'},
               open(os.path.join(dest, 'ccrec_config.json'), 'w'))
@@ -263,6 +407,11 @@ def save_model(dest, V, d, params, m=None, v=None, step=0, lr=1e-3, beta1=0.9, b
 def load_variables(path):
     """Read ml_files/<name>/ -> (V, d, params dict, m dict|None, v dict|None, step)."""
     t = read_bundle(os.path.join(path, 'variables', 'variables'))
+    if OBJECT_GRAPH_KEY in t:   # TF2 checkpoint: every variable the object graph names must be there
+        for nd in parse_object_graph(t[OBJECT_GRAPH_KEY]):
+            for _, _, key in nd['attrs']:
+                if key not in t:
+                    raise ValueError(f'{path}: object graph names {key!r}, absent from the bundle')
     params = {n: t[n + VAR_SUFFIX] for n in NAMES if n + VAR_SUFFIX in t}
     if 'encoder/encoded_1/kernel' not in params:
         raise ValueError(f'{path}: no encoder/encoded_1/kernel variable')

@@ -88,6 +88,7 @@ class CC_Recommender:
         self._flat = params_flat if params_flat is not None else glorot_flat(self.N, self.d, seed)
         self._m = self._v = None
         self._step = 0
+        self._metrics = None
         self.reg = 0.0
         self.lr = 1e-3
         self.trainer = None
@@ -149,6 +150,11 @@ class CC_Recommender:
                 l = {'bce': float(t[0]) / world, 'kl': float(t[1]) / world}
                 l['loss'] = l['bce'] + self.reg * l['kl']
             self.history.append(l)
+            # the compiled metrics' Mean accumulators as Keras leaves them after the epoch
+            # (reset per epoch; update_state(value, sample_weight=batch)): 'loss' and the first
+            # output's loss — written into the checkpoint with the optimizer state
+            n = float(steps * cfg.batch_size * world)
+            self._metrics = {'loss': (l['loss'] * n, n), 'output_1_loss': (l['bce'] * n, n)}
             if verbose and rank == 0:
                 dt = time.perf_counter() - t0
                 log(f'Epoch {ep + 1}/{epochs} - {steps} steps - {dt:.3f}s - loss: {l["loss"]:.6f} '
@@ -173,7 +179,7 @@ class CC_Recommender:
             m, v = lay.unpack(self._m), lay.unpack(self._v)
         else:
             m = v = None
-        checkpoint.save_model(dest, self.N, self.d, P, m, v, step=self._step, lr=self.lr)
+        checkpoint.save_model(dest, self.N, self.d, P, m, v, step=self._step, lr=self.lr, metrics=self._metrics)
 
     # --------------------------------------------------------------- internals
     def _current_flat(self):

@@ -28,3 +28,16 @@ def rel_err(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def record_errors(test, step, errs):
+    """Append observed parity errors as a JSON line to $CCREC_PARITY_LOG (if set): the tolerances
+    in the tests are set from these observations (about 3x the largest one seen)."""
+    import json
+    import os
+    path = os.environ.get('CCREC_PARITY_LOG')
+    if path:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, 'a') as fh:
+            fh.write(json.dumps({'test': test, 'step': step,
+                                 'errs': {k: float(v) for k, v in errs.items()}}) + '\n')

@@ -16,17 +16,33 @@ from cubecobrarecommender_amd.layout import Layout, glorot_flat
 from cubecobrarecommender_amd.synthetic import neg_sampler_from_csr, synthetic_cubes
 from cubecobrarecommender_amd.trainer import DeviceDataset, TrainConfig, Trainer
 from oracle import adjacency_ref, model_ref, noise_ref
-from tests.gpu_helpers import rel_err
+from tests.gpu_helpers import record_errors, rel_err
 
 pytestmark = pytest.mark.gpu
+
+# bars against the oracle emulating the same operand roundings (the remaining difference is
+# summation order): ~3x the largest error observed on MI355X (r03p CCREC_PARITY_LOG run,
+# tools/gpu_parity.sh).  Observed: bench config loss 5.4e-7 / grad 1.3e-3;
+# config 5 3.7e-8 / 8.5e-4; fp32 reference architecture 2.4e-7 / 6.6e-7.
+LOSS_TOL_BF16 = 2e-6
+GTOL_BF16 = 4e-3
+LOSS_TOL_MX8 = 1.5e-7
+GTOL_MX8 = 3e-3
+LOSS_TOL_FP32 = 1e-6       # (the north_star bar is 1e-4)
+GTOL_FP32 = 3e-6
 
 
 def _csr_lists(indptr, indices):
     return [indices[indptr[c]:indptr[c + 1]] for c in range(len(indptr) - 1)]
 
 
-def _check_step(tr, P, lists, perm, ns, step, reg, mode, loss_tol, gtol, y_rows):
+def _check_step(tr, P, lists, perm, ns, step, reg, mode, loss_tol, gtol, y_rows, g_override=None,
+                name='', rows_per_step=None):
+    """Compare the step's losses and gradients with the oracle on the same Philox batch.  gtol: one
+    bound for every tensor, or {tensor: bound} (missing tensors: the 'default' entry).
+    g_override: gradients the trainer does not store (the fused W1 Adam's, recovered from m)."""
     V, d, B = tr.cfg.V, tr.cfg.d, tr.cfg.batch_size
+    B = rows_per_step or B
     cdf = noise_ref.cdf_of(ns)
     cubes = [lists[c] for c in perm[step * B:(step + 1) * B]]
     oxs, oys, oreg, _ = noise_ref.philox_noise_batch(cubes, cdf, ns, tr.cfg.seed, step)
@@ -34,16 +50,24 @@ def _check_step(tr, P, lists, perm, ns, step, reg, mode, loss_tol, gtol, y_rows)
     losses, grads = model_ref.train_forward_backward(P, oxs, oys, V, d, reg=reg, reg_idx=oreg,
                                                      y_reg=y_reg, mode=mode)
     got = tr.losses()
-    assert abs(got['bce'] - losses['bce']) / losses['bce'] < loss_tol, (step, got, losses)
+    errs = {'loss/bce': abs(got['bce'] - losses['bce']) / losses['bce']}
     if reg > 0:
-        assert abs(got['kl'] - losses['kl']) / losses['kl'] < loss_tol, (step, got, losses)
+        errs['loss/kl'] = abs(got['kl'] - losses['kl']) / losses['kl']
     g = tr.layout.unpack(tr.standard(tr.grads))
-    errs = {k: rel_err(g[k], grads[k]) for k in grads if reg or not k.startswith('decoder_for_reg')}
-    bad = {k: v for k, v in errs.items() if not v < gtol}
+    g.update(g_override or {})
+    errs.update({k: rel_err(g[k], grads[k]) for k in grads if reg or not k.startswith('decoder_for_reg')})
+    record_errors(name, step, errs)
+    assert errs['loss/bce'] < loss_tol, (step, got, losses)
+    if reg > 0:
+        assert errs['loss/kl'] < loss_tol, (step, got, losses)
+    tol = gtol if isinstance(gtol, dict) else {'default': gtol}
+    bad = {k: v for k, v in errs.items() if not k.startswith('loss/')
+           and not v < tol.get(k, tol['default'])}
     assert not bad, (step, bad)
     return errs
 
 
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize('reg', [0.0, 0.1])
 def test_bench_configuration_matches_oracle(reg):
     """bench.py's Trainer, exactly: V=22000, d=256, B=512, bf16, glorot_flat(seed=42), seed 1234,
@@ -56,10 +80,11 @@ def test_bench_configuration_matches_oracle(reg):
     lists = _csr_lists(indptr, indices)
     y_mtx = adjacency_normalised_gpu(indptr, indices, V, device='cuda') if reg > 0 else None
     data = DeviceDataset(csr=(indptr, indices), num_cards=V, neg_sampler=ns, y_mtx=y_mtx, device='cuda')
-    cfg = TrainConfig(V=V, d=d, batch_size=B, reg=reg, dtype='bf16', seed=1234)
+    cfg = TrainConfig(V=V, d=d, batch_size=B, reg=reg, dtype='bf16', seed=1234,
+                      fuse_w1_adam=True)    # exactly bench.py's TrainConfig
     flat = glorot_flat(V, d, seed=42)
     tr = Trainer(cfg, data, params_flat=flat)
-    assert tr.fused_out and tr.adam_packs and tr.prefetch and tr.wpack is not None
+    assert tr.fused_out and tr.adam_packs and tr.prefetch and tr.wpack is not None and tr.fuse_w1
     perm = np.random.default_rng(99).permutation(C).astype(np.int32)
     tr.set_epoch_permutations(perm[None, :])
     tr.capture()
@@ -69,11 +94,27 @@ def test_bench_configuration_matches_oracle(reg):
         want = adjacency_ref.normalised_rows_from_lists(lists, V, idx)
         assert np.max(np.abs(got - want) / np.maximum(want, 1e-30)) < 2e-7
         return got
+    lay = Layout(V, d)
+    n1 = V * d
     for step in range(3):
-        P = Layout(V, d).unpack(tr.standard(tr.params))
+        P = lay.unpack(tr.standard(tr.params))
+        m0 = tr.m[:n1].double().cpu().numpy()
+        v0 = tr.v[:n1].double().cpu().numpy()
         tr.step()
         torch.cuda.synchronize()
-        _check_step(tr, P, lists, perm, ns, step, reg, 'bf16', 2e-4, 2e-2, y_rows)
+        # the fused W1 Adam never stores W1's gradient: recover it from the first moment
+        # (m1 = b1 m0 + (1 - b1) g), and check W1's update against TF Adam on that gradient
+        m1 = tr.m[:n1].double().cpu().numpy()
+        g1 = (m1 - 0.9 * m0) / (1.0 - 0.9)
+        w1 = {'encoder/encoded_1/kernel': g1.reshape(V, d)}
+        _check_step(tr, P, lists, perm, ns, step, reg, 'bf16', LOSS_TOL_BF16, GTOL_BF16, y_rows,
+                    g_override=w1, name=f'bench_cfg_reg{reg}')
+        t = step + 1
+        v1 = 0.999 * v0 + 0.001 * g1 * g1
+        lr_t = 1e-3 * np.sqrt(1 - 0.999 ** t) / (1 - 0.9 ** t)
+        want = P['encoder/encoded_1/kernel'].ravel().astype(np.float64) - lr_t * m1 / (np.sqrt(v1) + 1e-7)
+        got = tr.params[:n1].double().cpu().numpy()
+        assert np.max(np.abs(got - want)) < 1e-6
     assert tr.graphs is not None and tr.graphs[4] is not None
 
 
@@ -105,7 +146,8 @@ def test_reference_architecture_fp32(reg):
     for step in range(2):
         tr.forward_backward()
         torch.cuda.synchronize()
-        _check_step(tr, P, lists, perm, ns, step, reg, 'fp64', 1e-4, 1e-4, y_rows)
+        _check_step(tr, P, lists, perm, ns, step, reg, 'fp64', LOSS_TOL_FP32, GTOL_FP32, y_rows,
+                    name=f'refarch_fp32_{reg}')
         # advance both on the GPU's gradients with TF Adam; the GPU update must equal the formula
         G = lay.unpack(tr.standard(tr.grads))
         tr.apply()
@@ -116,14 +158,16 @@ def test_reference_architecture_fp32(reg):
         assert np.max(np.abs(lay.pack(got)[:n] - lay.pack(P)[:n])) < 1e-6
 
 
+@pytest.mark.timeout(300)
 def test_noise_law_matches_reference_at_22k():
     """F on the GPU (Philox law) vs the reference's MT19937 law (oracle MTNoise, bit-exact with
     generator.py) at |V| = 22,000 on the same 1,024 synthetic cubes: distinct cut / add / ycut counts
     per cube (two-sample KS), the ycut <= k//4 and add-outside-cube structure, and the added-card
-    frequencies of the 30 most likely cards (chi-square), all at alpha = 1e-4."""
+    frequencies of the 30 most likely cards (chi-square), all at alpha = 1e-4.  8,192 noised cubes
+    per side (the 2,048-cube version had little power against small biases)."""
     from scipy import stats
     from cubecobrarecommender_amd.generator import DataGenerator
-    V, C, B = 22000, 1024, 512
+    V, C, B = 22000, 4096, 512
     indptr_t, indices_t = synthetic_cubes(C, V, seed=20250301, device='cuda')
     indptr, indices = np.asarray(indptr_t), np.asarray(indices_t)
     ns = neg_sampler_from_csr(indptr, indices, V)
@@ -173,3 +217,41 @@ def test_noise_law_matches_reference_at_22k():
     p = stats.chi2_contingency(table).pvalue
     assert p > 1e-4, (p, cg[:5], cr[:5])
     assert stats.chi2_contingency(tot).pvalue > 1e-4
+
+
+@pytest.mark.timeout(300)
+def test_config5_full_size_matches_mx8_oracle():
+    """BASELINE configs[4]'s per-GPU step at full size: |V| = 22,000, d = 1024,
+    B = 512, MX-FP8 decoder output / regulariser GEMMs (everything else bf16), reg 0.1 — the
+    shipped `bench.py --d 1024 --dtype fp8 --reg 0.1` Trainer — against model_ref(mode='mx8'), which
+    quantises the same bf16 operands to e4m3fn + E8M0 along each product's K axis.  Two steps, graphs
+    captured; the oracle follows the GPU's parameters (fp8 code boundaries make trajectories drift)."""
+    from cubecobrarecommender_amd.adjacency import adjacency_normalised_gpu
+    V, d, B, C, reg = 22000, 1024, 512, 2048, 0.1
+    indptr_t, indices_t = synthetic_cubes(C, V, seed=20250301, device='cuda')
+    indptr, indices = np.asarray(indptr_t), np.asarray(indices_t)
+    ns = neg_sampler_from_csr(indptr, indices, V)
+    lists = _csr_lists(indptr, indices)
+    y_mtx = adjacency_normalised_gpu(indptr, indices, V, device='cuda')
+    data = DeviceDataset(csr=(indptr, indices), num_cards=V, neg_sampler=ns, y_mtx=y_mtx, device='cuda')
+    cfg = TrainConfig(V=V, d=d, batch_size=B, reg=reg, dtype='fp8', seed=1234, fuse_w1_adam=True)
+    tr = Trainer(cfg, data, params_flat=glorot_flat(V, d, seed=42))
+    assert tr.mx8 and tr.fused_tower
+    perm = np.random.default_rng(99).permutation(C).astype(np.int32)
+    tr.set_epoch_permutations(perm[None, :])
+
+    def y_rows(idx):
+        return y_mtx[torch.as_tensor(idx, device='cuda').long()].cpu().numpy()
+    lay = Layout(V, d)
+    for step in range(2):
+        P = lay.unpack(tr.standard(tr.params))
+        m0 = tr.m[:V * d].double().cpu().numpy()
+        tr.forward_backward()
+        torch.cuda.synchronize()
+        over = None
+        if tr.fuse_w1:   # W1's gradient is not stored: recover it from the first moment
+            over = {'encoder/encoded_1/kernel': ((tr.m[:V * d].double().cpu().numpy() - 0.9 * m0) / 0.1).reshape(V, d)}
+        _check_step(tr, P, lists, perm, ns, step, reg, 'mx8', LOSS_TOL_MX8, GTOL_MX8, y_rows,
+                    g_override=over, name='config5_full')
+        tr.apply()
+        torch.cuda.synchronize()

@@ -8,9 +8,32 @@ from cubecobrarecommender_amd import _lib as L
 from cubecobrarecommender_amd.layout import Layout
 from cubecobrarecommender_amd.trainer import DeviceDataset, TrainConfig, Trainer
 from oracle import model_ref, noise_ref
-from tests.gpu_helpers import problem, rel_err
+from tests.gpu_helpers import problem, record_errors, rel_err
 
 pytestmark = pytest.mark.gpu
+
+# bf16 / MX-FP8 bars against the oracle that emulates the same operand roundings (what is left is
+# summation order): ~3x the largest error observed on MI355X over these tests (CCREC_PARITY_LOG
+# runs, tools/gpu_parity.sh).  fp32: the north_star's 1e-4.
+# observed maxima (r03q, 49 tests): fp32 loss 7.2e-8 / grad 7.2e-7; bf16 6.5e-7 / 2.5e-3 (full mode's
+# 1,500 identity rows into W1: 6.7e-3); MX-FP8 4.4e-8 / 2.0e-3
+TOL = {'fp32': (3e-7, 3e-6), 'bf16': (2e-6, 8e-3), 'bf16_full': (2e-6, 2e-2),
+       'mx8': (1.5e-7, 6e-3)}   # (loss, gradient) relative
+
+
+def _errs(name, step, got, losses, grads, gflat, reg):
+    e = {'loss/bce': abs(got['bce'] - losses['bce']) / losses['bce']}
+    if reg > 0:
+        e['loss/kl'] = abs(got['kl'] - losses['kl']) / losses['kl']
+    e.update({k: rel_err(gflat[k], grads[k]) for k in grads if reg or not k.startswith('decoder_for_reg')})
+    record_errors(name, step, e)
+    return e
+
+
+def _assert_within(e, tol, step):
+    lt, gt = tol
+    bad = {k: v for k, v in e.items() if not v < (lt if k.startswith('loss/') else gt)}
+    assert not bad, (step, bad)
 
 
 def _setup(V, d, B, C, reg, dtype, seed=3, sizes=(20, 40, 80), fused_tower=True, prefetch=True):
@@ -42,7 +65,6 @@ def test_train_steps_match_oracle(dtype, reg, V, d, B, fused):
     Mo = {k: np.zeros_like(v) for k, v in P.items()}
     Vo = {k: np.zeros_like(v) for k, v in P.items()}
     mode = 'bf16' if dtype == 'bf16' else 'fp64'
-    loss_tol = 1e-4 if dtype == 'fp32' else 2e-4
     for step in range(3):
         tr.forward_backward()
         torch.cuda.synchronize()
@@ -55,16 +77,9 @@ def test_train_steps_match_oracle(dtype, reg, V, d, B, fused):
             assert np.array_equal(reg_idx, oreg)
         losses, grads = model_ref.train_forward_backward(
             P, oxs, oys, V, d, reg=reg, reg_idx=oreg, y_reg=Mt[oreg] if reg > 0 else None, mode=mode)
-        got = tr.losses()
-        assert abs(got['bce'] - losses['bce']) / losses['bce'] < loss_tol, (step, got, losses)
-        if reg > 0:
-            assert abs(got['kl'] - losses['kl']) / losses['kl'] < loss_tol, (step, got, losses)
-        gflat = tr.layout.unpack(tr.grads.cpu().numpy())
-        gtol = 1e-4 if dtype == 'fp32' else 2e-2
-        errs = {k: rel_err(gflat[k], grads[k]) for k in grads
-                if reg or not k.startswith('decoder_for_reg')}
-        bad = {k: v for k, v in errs.items() if not v < gtol}
-        assert not bad, (step, bad)
+        e = _errs(f'train_{dtype}_{reg}_{V}_{d}_{B}_{fused}', step, tr.losses(), losses, grads,
+                  tr.layout.unpack(tr.grads.cpu().numpy()), reg)
+        _assert_within(e, TOL[dtype], step)
         tr.apply()
         # advance the oracle with the oracle's own gradients (TF Adam in fp32)
         G = {k: grads[k] for k in grads}
@@ -255,14 +270,9 @@ def test_fp8_decoder_steps_track_oracle(reg, V, d, B):
             assert np.array_equal(xs[b], oxs[b]) and np.array_equal(ys[b], oys[b])
         losses, grads = model_ref.train_forward_backward(
             P, oxs, oys, V, d, reg=reg, reg_idx=oreg, y_reg=Mt[oreg] if reg > 0 else None, mode='mx8')
-        got = tr.losses()
-        assert abs(got['bce'] - losses['bce']) / losses['bce'] < 1e-3, (step, got, losses)
-        if reg > 0:
-            assert abs(got['kl'] - losses['kl']) / losses['kl'] < 1e-3, (step, got, losses)
-        gflat = tr.layout.unpack(tr.grads.cpu().numpy())
-        errs = {k: rel_err(gflat[k], grads[k]) for k in grads if reg or not k.startswith('decoder_for_reg')}
-        bad = {k: v for k, v in errs.items() if not v < 3e-2}
-        assert not bad, (step, bad)
+        e = _errs(f'fp8_{reg}_{V}_{d}_{B}', step, tr.losses(), losses, grads,
+                  tr.layout.unpack(tr.grads.cpu().numpy()), reg)
+        _assert_within(e, TOL['mx8'], step)
         tr.apply()
         torch.cuda.synchronize()
         P = tr.layout.unpack(tr.params.cpu().numpy())   # follow the GPU trajectory
@@ -281,14 +291,8 @@ def test_wide_d1024_bf16_steps_match_oracle(reg):
     oxs, oys, oreg, _ = noise_ref.philox_noise_batch(cubes, cdf, ns, tr.cfg.seed, 0)
     losses, grads = model_ref.train_forward_backward(
         P, oxs, oys, V, d, reg=reg, reg_idx=oreg, y_reg=Mt[oreg] if reg > 0 else None, mode='bf16')
-    got = tr.losses()
-    assert abs(got['bce'] - losses['bce']) / losses['bce'] < 2e-4
-    if reg > 0:
-        assert abs(got['kl'] - losses['kl']) / losses['kl'] < 2e-4
-    gflat = tr.layout.unpack(tr.grads.cpu().numpy())
-    bad = {k: rel_err(gflat[k], grads[k]) for k in grads if (reg or not k.startswith('decoder_for_reg'))
-           and not rel_err(gflat[k], grads[k]) < 2e-2}
-    assert not bad, bad
+    e = _errs(f'wide1024_{reg}', 0, tr.losses(), losses, grads, tr.layout.unpack(tr.grads.cpu().numpy()), reg)
+    _assert_within(e, TOL['bf16'], 0)
 
 
 def test_adam_pack_images_and_counters():
@@ -361,7 +365,7 @@ def test_full_mode_regulariser_matches_oracle(dtype, V, d, B):
     tr.set_epoch_permutation(perm)
     tr.capture()
     cdf = noise_ref.cdf_of(ns)
-    mode, ltol, gtol = ('fp64', 1e-4, 1e-4) if dtype == 'fp32' else ('bf16', 2e-4, 2e-2)
+    mode = 'fp64' if dtype == 'fp32' else 'bf16'
     for step in range(2):
         Pk = lay.unpack(tr.standard(tr.params))
         tr.step()
@@ -370,12 +374,9 @@ def test_full_mode_regulariser_matches_oracle(dtype, V, d, B):
         oxs, oys, _, _ = noise_ref.philox_noise_batch(cubes, cdf, ns, 5, step, with_reg=False)
         losses, grads = model_ref.train_forward_backward(Pk, oxs, oys, V, d, reg=0.3, reg_idx=np.arange(V),
                                                          y_reg=Mt, mode=mode)
-        got = tr.losses()
-        assert abs(got['bce'] - losses['bce']) / losses['bce'] < ltol, (step, got, losses)
-        assert abs(got['kl'] - losses['kl']) / losses['kl'] < ltol, (step, got, losses)
-        g = lay.unpack(tr.standard(tr.grads))
-        bad = {k: rel_err(g[k], grads[k]) for k in grads if not rel_err(g[k], grads[k]) < gtol}
-        assert not bad, (step, bad)
+        e = _errs(f'full_{dtype}_{V}_{d}_{B}', step, tr.losses(), losses, grads,
+                  lay.unpack(tr.standard(tr.grads)), 0.3)
+        _assert_within(e, TOL['fp32' if dtype == 'fp32' else 'bf16_full'], step)
     tr.check_status()
 
 
@@ -399,9 +400,7 @@ def test_fused_regulariser_clip_fix_path(V, B):
     oxs, oys, oreg, _ = noise_ref.philox_noise_batch(cubes, cdf, ns, tr.cfg.seed, 0)
     losses, grads = model_ref.train_forward_backward(P, oxs, oys, V, d, reg=0.5, reg_idx=oreg, y_reg=Mt[oreg],
                                                      mode='bf16')
-    got = tr.losses()
-    assert abs(got['kl'] - losses['kl']) / losses['kl'] < 2e-4, (got, losses)
-    g = tr.layout.unpack(tr.grads.cpu().numpy())
-    for k in ('decoder_for_reg/reconstruct/kernel', 'decoder_for_reg/reconstruct/bias',
-              'decoder_for_reg/decoded_3/kernel', 'encoder/encoded_1/kernel'):
-        assert rel_err(g[k], grads[k]) < 2e-2, (k, rel_err(g[k], grads[k]))
+    e = _errs(f'clipfix_{V}_{B}', 0, tr.losses(), losses, grads, tr.layout.unpack(tr.grads.cpu().numpy()), 0.5)
+    _assert_within({k: e[k] for k in ('loss/kl', 'decoder_for_reg/reconstruct/kernel',
+                                      'decoder_for_reg/reconstruct/bias', 'decoder_for_reg/decoded_3/kernel',
+                                      'encoder/encoded_1/kernel')}, TOL['bf16'], 0)
