@@ -233,6 +233,108 @@ __global__ __launch_bounds__(64 * GWN) void gather2_kernel(const bf16_t *__restr
   l2_warm(warm, warm_bytes, row, R);  // the tower forward's packed weights (gather blocks only)
 }
 
+// Forward, bf16 d = 256, column slices dealt to XCDs.  gather2 gives every block all 256 columns
+// of its row, so each XCD's 4 MB L2 sees the whole 11 MB W1 table (48 MB fetched beyond L2 per
+// step for an 11 MB table).  Here block b runs on XCD b % 8 (round-robin dispatch) and owns the
+// 64-column slice (b % 8) & 3 of row 2 (b / 8) + (b % 8) / 4: an XCD only ever reads one 128-B
+// line of each W1 row (2.8 MB of the table, L2-resident).  A wave load fetches the slice of 8
+// cards (8 lanes x 16 B each); the 8 card groups are added lane-wise by xor shuffles, the waves
+// in order through LDS (deterministic).
+constexpr int GX_NS = 4, GX_COLS = 256 / GX_NS;  // slices per row, columns per slice
+template <int GWN, int U>
+__global__ __launch_bounds__(64 * GWN) void gather_xcd_kernel(const bf16_t *__restrict__ table,
+                                                             const float *__restrict__ bias, int R,
+                                                             const int32_t *__restrict__ x_cnt,
+                                                             const int32_t *__restrict__ x_idx, int x_cap,
+                                                             bf16_t *__restrict__ out, const void *warm,
+                                                             int64_t warm_bytes, int64_t *state, int64_t bpe) {
+  if (state && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {  // the previous step's counters
+    state[0] += 1;
+    state[1] += 1;
+    if (state[1] >= bpe) {
+      state[1] = 0;
+      state[2] += 1;
+    }
+  }
+  constexpr int D = 256;
+  __shared__ __attribute__((aligned(16))) float part[GWN][GX_COLS];
+  __shared__ int32_t ls[GIDX];
+  const int xcd = (int)blockIdx.x & 7;
+  const int row = 2 * ((int)blockIdx.x >> 3) + (xcd >> 2);
+  const int slice = xcd & (GX_NS - 1);
+  if (row < R) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 3;
+    const int c0 = slice * GX_COLS + (lane & 7) * 8;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    const int n = x_cnt[row];
+    const int q = ((n + GWN - 1) / GWN + 7) & ~7;  // chunks of whole 8-card groups
+    const int i0 = min(n, w * q), i1 = min(n, i0 + q);
+    const int32_t *__restrict__ glst = x_idx + (int64_t)row * x_cap;
+    const bool staged = n <= GIDX;
+    if (staged)
+      for (int t = threadIdx.x; t < n; t += 64 * GWN) ls[t] = glst[t];
+    __syncthreads();
+    const int32_t *lst = staged ? ls : glst;
+    int i = i0;
+    for (; i + 8 * U <= i1; i += 8 * U) {
+      int j[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) j[u] = lst[i + 8 * u + g];
+      g_u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const g_u32x4 *>(table + (int64_t)j[u] * D + c0);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[2 * e] += __uint_as_float(v[u][e] << 16);
+          acc[2 * e + 1] += __uint_as_float(v[u][e] & 0xFFFF0000u);
+        }
+    }
+    for (; i < i1; i += 8) {
+      if (i + g < i1) {
+        const g_u32x4 v = *reinterpret_cast<const g_u32x4 *>(table + (int64_t)lst[i + g] * D + c0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[2 * e] += __uint_as_float(v[e] << 16);
+          acc[2 * e + 1] += __uint_as_float(v[e] & 0xFFFF0000u);
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      acc[e] += __shfl_xor(acc[e], 8);
+      acc[e] += __shfl_xor(acc[e], 16);
+      acc[e] += __shfl_xor(acc[e], 32);
+    }
+    if (g == 0) {
+      const int c = (lane & 7) * 8;
+      *reinterpret_cast<float4 *>(&part[w][c]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      *reinterpret_cast<float4 *>(&part[w][c + 4]) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    }
+    __syncthreads();
+    if (threadIdx.x < GX_COLS / 8) {
+      const int c = threadIdx.x * 8;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v = part[0][c + e];
+#pragma unroll
+        for (int p = 1; p < GWN; ++p) v += part[p][c + e];
+        v += bias[slice * GX_COLS + c + e];
+        o[e] = v > 0.f ? v : 0.f;
+      }
+      g_u32x4 pk;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pk[e] = (uint32_t)f2bf(o[2 * e]) | ((uint32_t)f2bf(o[2 * e + 1]) << 16);
+      *reinterpret_cast<g_u32x4 *>(out + (int64_t)row * D + slice * GX_COLS + c) = pk;
+    }
+  }
+  l2_warm(warm, warm_bytes, (int)blockIdx.x, (int)gridDim.x);  // the tower forward's packed weights
+}
+
 // Backward: 4 waves per W1 row (row V = the bias when bias_grad is given); wave w walks the w-th
 // quarter of the row's bit words, collecting up to U set bits before issuing their dPre loads
 // together (heavy Zipf rows have a set bit for nearly every batch row).  Partials added in wave order.
@@ -1022,6 +1124,22 @@ extern "C" int cc_embed_gather_fwd_xt(int32_t dtype, const void *table, const fl
   const int nxt = xt_bits ? (int)cdiv((V + 31) / 32, XT_TJ) : 0;  // xt transpose blocks
   const int epl = d / 64;
   hipStream_t s = as_stream(stream);
+  static const int gx = [] {  // A/B switch (dev): XCD column-sliced gather (0 = gather2); waves x loads
+    const char *e = getenv("CCREC_GATHER_XCD");
+    return e ? atoi(e) : 44;
+  }();
+  if (dtype == CC_BF16 && d == 256 && g2 > 0 && gx > 0 && !xt_bits) {
+    const dim3 gxg((unsigned)(cdiv(R, 2) * 8));
+#define GX(GWN, U) \
+  if (gx == GWN * 10 + U) hipLaunchKernelGGL((gather_xcd_kernel<GWN, U>), gxg, dim3(64 * GWN), 0, s, \
+                                             (const bf16_t *)table, bias, R, x_cnt, x_idx, x_cap, (bf16_t *)out, \
+                                             warm, warm_bytes, state, bpe); else
+    GX(4, 4) GX(4, 8) GX(2, 4) GX(2, 8) GX(8, 4) GX(8, 2)
+      return cc::fail(CC_ERR_UNSUPPORTED, "CCREC_GATHER_XCD: unknown variant");
+#undef GX
+    CC_LAUNCH_CHECK("gather_xcd_kernel");
+    return CC_OK;
+  }
   if (dtype == CC_BF16 && d == 256 && g2 > 0) {
 #define G2(GWN, U) \
   if (g2 == GWN * 10 + U) hipLaunchKernelGGL((gather2_kernel<GWN, U>), dim3((unsigned)(R + nxt)), dim3(64 * GWN), 0, s, \

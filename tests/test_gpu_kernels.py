@@ -283,6 +283,37 @@ def test_gather_and_scatter(dtype, d):
     assert rel_err(grad.cpu().numpy(), gw) < 1e-6
 
 
+@pytest.mark.parametrize('R', [51, 64])
+def test_gather_xcd_slices_edge_rows(R):
+    """The bf16 d = 256 E1 gather (XCD column slices: 4 slices x 2 row parities per 8 blocks): odd R
+    (the last block pair half empty), empty rows, one card, a row longer than the LDS index stage
+    (2,100 > 2,048: read from global), list tails that are not whole 8-card groups; every output
+    element within bf16 rounding of the fp64 sum, the counters advanced once."""
+    rng = np.random.default_rng(R)
+    V, d, cap = 3000, 256, 2112
+    W = torch.from_numpy(rng.standard_normal((V, d)).astype(np.float32)).to('cuda', torch.bfloat16)
+    b = torch.from_numpy(rng.standard_normal(d).astype(np.float32)).cuda()
+    sizes = [0, 1, 2100, 7, 9, 63, 65] + [int(rng.integers(0, 800)) for _ in range(R - 7)]
+    lists = [np.sort(rng.choice(V, n, replace=False)) for n in sizes]
+    xi = np.zeros((R, cap), np.int32)
+    for r, l in enumerate(lists):
+        xi[r, :len(l)] = l
+    cnt = torch.from_numpy(np.array(sizes, np.int32)).cuda()
+    xid = torch.from_numpy(xi).cuda()
+    out = torch.full((R + 1, d), 3.0, device='cuda', dtype=torch.bfloat16)   # row R must stay untouched
+    state = torch.tensor([5, 2, 0], dtype=torch.int64, device='cuda')
+    L.call('cc_embed_gather_fwd_warm', L.CC_BF16, L.ptr(W), L.ptr(b), V, d, R, L.ptr(cnt), L.ptr(xid), cap,
+           L.ptr(out), None, 0, L.ptr(state), 3, L.stream_ptr())
+    torch.cuda.synchronize()
+    Wd = W.double().cpu().numpy()
+    want = np.stack([np.maximum(Wd[l].sum(0) + b.double().cpu().numpy(), 0) for l in lists])
+    got = out.double().cpu().numpy()
+    assert np.all(got[R] == 3.0)
+    err = np.abs(got[:R] - want) / np.maximum(np.abs(want), 1.0)
+    assert err.max() < 2 ** -7, err.max()
+    assert state.tolist() == [6, 0, 1]
+
+
 @pytest.mark.parametrize('rows,cols', [(256, 22000), (64, 700), (256, 20884), (13, 7), (24, 40)])
 def test_transpose_bf16_and_fp32(rows, cols):
     """cc_transpose (the Wo^T refresh): vector bf16 path (rows, cols % 8 == 0) and scalar paths."""
