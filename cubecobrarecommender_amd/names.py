@@ -1,28 +1,111 @@
 """Card-name normalisation: ``unidecode.unidecode(name.lower())`` (src/scripts/ml_recommend.py:44,
-web/ml_recommend_web.py:29).  ``unidecode`` (requirements.txt:53) is not installed in this
-pipeline, so this is a restatement for the characters card names use: NFKD decomposition with
-combining marks dropped, plus unidecode's transliterations of the non-decomposable Latin letters.
-SURVEY §8(f) row N3; strings outside this table keep their characters (parity unpinned).
+web/ml_recommend_web.py:29; the same key in src/scripts/recommend.py:53 and cut_cards.py:53).
+
+``Unidecode==1.1.1`` (requirements.txt:53) is not installed in this pipeline, so its algorithm is
+restated here:
+
+* a code point below 0x80 is itself;
+* otherwise unidecode looks up ``x{cp >> 8:03x}.data[cp & 0xFF]`` — one replacement string per
+  code point, '' where the table holds none (its default ``errors='ignore'``);
+* code points above 0xEFFFF (private use and beyond) map to ''.
+
+The tables are restated for the blocks card names and their typographic variants use: Latin-1
+Supplement (x000), Latin Extended-A (x001), the Latin Extended-B letters with a plain base, Greek
+(x003, basic letters), Cyrillic (x004, basic letters), General Punctuation (x020), Letterlike
+Symbols / Number Forms (x021: the (tm)-style and Roman-numeral entries).  A code point outside
+them is decomposed (NFKD) and its base letters looked up the same way — that matches unidecode
+for the accented letters of other Latin blocks (x01e: Vietnamese etc.).  What neither covers (CJK,
+whose unidecode tables give pinyin/romaji, and other scripts) keeps its characters, so such a
+name simply misses the id map: parity unpinned there (no reference output exists in this
+pipeline: the reference's ml_files/*_id_map.json are Git-LFS pointers).
 """
 import unicodedata
 
-_SPECIAL = {
-    'æ': 'ae', 'Æ': 'AE', 'œ': 'oe', 'Œ': 'OE', 'ß': 'ss', 'ø': 'o', 'Ø': 'O', 'đ': 'd', 'Đ': 'D',
-    'ð': 'd', 'Ð': 'D', 'þ': 'th', 'Þ': 'Th', 'ł': 'l', 'Ł': 'L', 'ı': 'i', 'ŋ': 'ng', 'ĸ': 'q',
-    '‘': "'", '’': "'", '‚': ',', '“': '"', '”': '"', '–': '-', '—': '-', '…': '...', ' ': ' ',
-    '™': '(tm)', '®': '(r)', '©': '(c)', '½': ' 1/2', '×': 'x', '−': '-',
+# x000: U+0080..U+00FF (C1 controls -> '')
+_X000 = (
+    [''] * 32 +
+    [' ', '!', 'C/', 'PS', '$?', 'Y=', '|', 'SS', '"', '(c)', 'a', '<<', '!', '', '(r)', '-',
+     'deg', '+-', '2', '3', "'", 'u', 'P', '*', ',', '1', 'o', '>>', ' 1/4', ' 1/2', ' 3/4', '?',
+     'A', 'A', 'A', 'A', 'A', 'A', 'AE', 'C', 'E', 'E', 'E', 'E', 'I', 'I', 'I', 'I',
+     'D', 'N', 'O', 'O', 'O', 'O', 'O', 'x', 'O', 'U', 'U', 'U', 'U', 'Y', 'Th', 'ss',
+     'a', 'a', 'a', 'a', 'a', 'a', 'ae', 'c', 'e', 'e', 'e', 'e', 'i', 'i', 'i', 'i',
+     'd', 'n', 'o', 'o', 'o', 'o', 'o', '/', 'o', 'u', 'u', 'u', 'u', 'y', 'th', 'y'])
+assert len(_X000) == 128
+
+# x001 part 1: U+0100..U+017F (Latin Extended-A)
+_X001A = ('A a A a A a C c C c C c C c D d D d E e E e E e E e E e G g G g G g G g H h H h '
+          'I i I i I i I i I i IJ ij J j K k q L l L l L l L l L l N n N n N n \'n NG ng '
+          'O o O o O o OE oe R r R r R r S s S s S s S s T t T t T t U u U u U u U u U u U u '
+          'W w Y y Y Z z Z z Z z s').split(' ')
+assert len(_X001A) == 128
+
+# Greek (x003): basic capital and small letters, tonos forms
+_GREEK = {}
+for caps, small, lat in zip('ΑΒΓΔΕΖΗΘΙΚΛΜΝΞΟΠΡΣΤΥΦΧΨΩ', 'αβγδεζηθικλμνξοπρστυφχψω',
+                            ['A', 'B', 'G', 'D', 'E', 'Z', 'E', 'Th', 'I', 'K', 'L', 'M', 'N', 'Ks',
+                             'O', 'P', 'R', 'S', 'T', 'U', 'Ph', 'Kh', 'Ps', 'O']):
+    _GREEK[caps] = lat
+    _GREEK[small] = lat.lower()
+_GREEK.update({'ς': 's', 'ά': 'a', 'έ': 'e', 'ή': 'e', 'ί': 'i', 'ό': 'o', 'ύ': 'u', 'ώ': 'o',
+               'Ά': 'A', 'Έ': 'E', 'Ή': 'E', 'Ί': 'I', 'Ό': 'O', 'Ύ': 'U', 'Ώ': 'O', 'ϊ': 'i', 'ϋ': 'u',
+               'ΐ': 'i', 'ΰ': 'u', 'Ϊ': 'I', 'Ϋ': 'U'})
+
+# Cyrillic (x004): U+0410..U+044F plus Ё / ё
+_CYR = {}
+for i, lat in enumerate(['A', 'B', 'V', 'G', 'D', 'E', 'Zh', 'Z', 'I', 'I', 'K', 'L', 'M', 'N', 'O', 'P',
+                         'R', 'S', 'T', 'U', 'F', 'Kh', 'Ts', 'Ch', 'Sh', 'Shch', "'", 'Y', "'", 'E', 'Iu', 'Ia']):
+    _CYR[chr(0x410 + i)] = lat
+    _CYR[chr(0x430 + i)] = lat.lower()
+_CYR.update({'Ё': 'Io', 'ё': 'io'})
+
+# General Punctuation (x020) and Letterlike Symbols / Number Forms (x021) entries names use
+_PUNCT = {
+    ' ': ' ', ' ': ' ', ' ': ' ', ' ': ' ', ' ': ' ', ' ': ' ', ' ': ' ',
+    ' ': ' ', ' ': ' ', ' ': ' ', ' ': ' ', '​': '', '‌': '', '‍': '',
+    '‐': '-', '‑': '-', '‒': '-', '–': '-', '—': '--', '―': '--',
+    '‖': '||', '‗': '_', '‘': "'", '’': "'", '‚': ',', '‛': "'",
+    '“': '"', '”': '"', '„': ',,', '‟': '"', '†': '+', '‡': '++',
+    '•': '*', '‣': '*>', '․': '.', '‥': '..', '…': '...', '‧': '.',
+    ' ': ' ', '‰': '%0', '′': "'", '″': "''", '‹': '<', '›': '>',
+    '⁄': '/', '™': '(tm)', '№': 'No', '←': '<-', '→': '->',
+    'ʼ': "'", 'ˆ': '^', '˜': '~', '−': '-',
 }
+for i, r in enumerate(['I', 'II', 'III', 'IV', 'V', 'VI', 'VII', 'VIII', 'IX', 'X', 'XI', 'XII', 'L', 'C', 'D', 'M']):
+    _PUNCT[chr(0x2160 + i)] = r
+    _PUNCT[chr(0x2170 + i)] = r.lower()
+
+_TABLE = {chr(0x80 + i): r for i, r in enumerate(_X000)}
+_TABLE.update({chr(0x100 + i): r for i, r in enumerate(_X001A)})
+_TABLE.update(_GREEK)
+_TABLE.update(_CYR)
+_TABLE.update(_PUNCT)
 
 
-def unidecode_lite(s):
-    out = []
-    for ch in unicodedata.normalize('NFKD', s):
-        if unicodedata.combining(ch):
-            continue
-        out.append(_SPECIAL.get(ch, ch))
-    return ''.join(out)
+def _repl(ch):
+    cp = ord(ch)
+    if cp < 0x80:
+        return ch
+    if cp > 0xEFFFF:
+        return ''
+    r = _TABLE.get(ch)
+    if r is not None:
+        return r
+    # other blocks: NFKD base letters, each looked up again (combining marks -> '')
+    dec = unicodedata.normalize('NFKD', ch)
+    if dec != ch:
+        return ''.join('' if unicodedata.combining(c) else _repl(c) for c in dec)
+    if unicodedata.combining(ch):
+        return ''
+    return ch   # not restated (CJK, other scripts): parity unpinned, see the module docstring
+
+
+def unidecode(s):
+    """unidecode.unidecode (Unidecode 1.1.1) for the blocks restated above."""
+    if s.isascii():
+        return s
+    return ''.join(_repl(ch) for ch in s)
 
 
 def normalize(name):
     """The lookup key of ml_recommend.py:44: unidecode(name.lower())."""
-    return unidecode_lite(name.lower())
+    return unidecode(name.lower())

@@ -77,3 +77,25 @@ def test_fused_kernel_extent_gates():
     assert fused_reg_fits(23171 // 2, 23171, 512)       # a row shard ending below the limit
     assert dx_splitk_fits(512, 22000, 256)
     assert not dx_splitk_fits(33000, 33000, 256)       # full-mode dZ (Breg ~ V) past 2 GB
+
+
+def test_names_unidecode_restatement():
+    """N3 (ml_recommend.py:44): unidecode(name.lower()) restated for Latin-1 / Latin Extended-A,
+    Greek, Cyrillic, punctuation and number forms (Unidecode 1.1.1's per-code-point tables);
+    ASCII passes through unchanged, combining marks vanish, private use maps to ''."""
+    from cubecobrarecommender_amd.names import normalize, unidecode
+    cases = {
+        'Lim-Dûl the Necromancer': 'lim-dul the necromancer', 'Æther Vial': 'aether vial',
+        'Jötun Grunt': 'jotun grunt', 'Déjà Vu': 'deja vu', 'Ifh-Bíff Efreet': 'ifh-biff efreet',
+        'Juzám Djinn': 'juzam djinn', 'Dandân': 'dandan', 'Sol Ring': 'sol ring',
+        'Phyrexian™ — “Obliterator”…': 'phyrexian(tm) -- "obliterator"...',
+        'Łukasz ½ × ÷': 'lukasz  1/2 x /', 'Ŀ Đ ħ ı ĸ ŉ Ŋ ŧ ſ ß þ': "l d h i q 'n ng t s ss th",
+        'Ελλάδα': 'ellada', 'Москва': 'moskva', 'Ⅻ': 'xii', 'Hồ Chí Minh': 'ho chi minh',
+        'µ°¿¡': 'udeg?!', 'á': 'a', '\U000F0000x': 'x',
+    }
+    for raw, want in cases.items():
+        assert normalize(raw) == want, (raw, normalize(raw), want)
+    assert unidecode('ÆON') == 'AEON' and unidecode('plain ascii') == 'plain ascii'
+    # every restated Latin-1 / Extended-A entry is ASCII
+    for cp in range(0x80, 0x180):
+        assert unidecode(chr(cp)).isascii(), hex(cp)
