@@ -372,7 +372,9 @@ def main():
         dt = float(t.item())
     tr.check_status()
     losses = tr.losses()
-    ktimes = kernel_profile(tr, step) if world == 1 else None
+    # per-kernel steady-state times (HIP events; with DP the collectives and the sharded Adam run
+    # between the ticked kernels and are not in them): every rank runs the same extra steps
+    ktimes = kernel_profile(tr, step)
     if rank != 0:
         if world > 1:
             import torch.distributed as dist

@@ -21,16 +21,12 @@
 
 namespace {
 
-constexpr int NB = 96;      // V columns per block: ceil(22000 / 96) = 230 blocks <= 256 CUs, one round
-constexpr int NJ = NB / 32; // 32-column accumulators per wave
+// V columns per block: d <= 256: 96 (ceil(22000 / 96) = 230 blocks <= 256 CUs, one round);
+// d = 512 (the reference width, model.py:62-64): 64, so the Wo^T slice and dZ^T fit the LDS
+template <int D> constexpr int nb_of() { return D <= 256 ? 96 : 64; }
+constexpr int NB_MIN = 64;
 constexpr int BK = 64;      // k per phase-2 ring chunk
 constexpr int NTH = 512;    // 8 waves
-constexpr int BMAX = 512;   // batch rows (B <= 512)
-constexpr int DMAX = 256;   // d <= 256
-// LDS map (bytes): the Wo^T slice [NB][d]; dZ^T [NB][B]; the target bits [B][NJ].
-constexpr int ZT_OFF = NB * DMAX * 2, ZT_BYTES = NB * BMAX * 2;
-constexpr int YS_OFF = ZT_OFF + ZT_BYTES, YS_BYTES = BMAX * NJ * 4;
-constexpr int LDS_BYTES = YS_OFF + YS_BYTES;
 constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
 
 typedef __attribute__((ext_vector_type(4))) uint32_t v4u;  // staging registers (stay in VGPRs)
@@ -80,9 +76,18 @@ __device__ __forceinline__ uint32_t bf16_pack2(float a, float b) {
 template <int D, int BB>
 __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   constexpr int d = D, B = BB;
+  constexpr int NB = nb_of<D>(), NJ = NB / 32;    // slice columns, 32-column accumulators per wave
   constexpr int CHD = d / 8, CHB = B / 8;
   constexpr int nkk = d / 16;                     // 16-k steps of phase 1
   constexpr int npass = (B + 255) / 256;          // 256-row passes of phase 1
+  // phase-1 A fragments: d <= 256 holds a whole pass (and the next one in flight); d = 512 walks
+  // a ring of 16 through the pass's 32 k-steps
+  constexpr bool RING1 = nkk > 16;
+  constexpr int NAF = RING1 ? 16 : nkk;
+  // LDS map (bytes): the Wo^T slice [NB][d]; dZ^T [NB][B]; the target bits [NJ][B]
+  constexpr int ZT_OFF = NB * d * 2, ZT_BYTES = NB * B * 2;
+  constexpr int YS_OFF = ZT_OFF + ZT_BYTES, LDS_BYTES = YS_OFF + B * NJ * 4;
+  static_assert(LDS_BYTES <= 150 * 1024, "dec_bce_dw_kernel: LDS");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
   __shared__ float red_cs[NTH / 64][NB];
   __shared__ double red_loss[NTH / 64];
@@ -101,19 +106,17 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 
   DEC_PROBE(0);
   // pass 0's A fragments first: their L2 round trip overlaps the resident staging below
-  bf16x8_t af[2][nkk];
-  auto load_a = [&](bf16x8_t (&dst)[nkk], int pass) {
-    if (p.D3p) {  // fragment (row block, kk) = 1 KB contiguous: whole cache lines per wave load
-      const int rb = min(pass * 8 + w, B / 32 - 1);
-      const bf16_t *src = p.D3p + ((int64_t)rb * nkk * 64 + lane) * 8;
+  bf16x8_t af[RING1 ? 1 : 2][NAF];
+  // fragment (row block, kk): packed = 1 KB contiguous (whole cache lines per wave load)
+  const int astr = p.D3p ? 512 : 16;
+  auto a_src = [&](int pass) -> const bf16_t * {
+    if (p.D3p) return p.D3p + ((int64_t)min(pass * 8 + w, B / 32 - 1) * nkk * 64 + lane) * 8;
+    return p.D3 + (int64_t)min(pass * 256 + w * 32 + (lane & 31), B - 1) * d + 8 * half;
+  };
+  auto load_a = [&](bf16x8_t (&dst)[NAF], int pass) {
+    const bf16_t *src = a_src(pass);
 #pragma unroll
-      for (int kk = 0; kk < nkk; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 512);
-    } else {
-      const int row = min(pass * 256 + w * 32 + (lane & 31), B - 1);
-      const bf16_t *src = p.D3 + (int64_t)row * d + 8 * half;
-#pragma unroll
-      for (int kk = 0; kk < nkk; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 16);
-    }
+    for (int kk = 0; kk < NAF; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * astr);
     // keep the whole batch in flight: without this fence the scheduler sinks each load to its
     // MFMA and the pass becomes a chain of dependent L2 round trips
     __builtin_amdgcn_sched_barrier(0);
@@ -228,21 +231,24 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
       __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)B * (uint32_t)V * 2u, 0x00020000);
 #pragma unroll
   for (int ps = 0; ps < npass; ++ps) {
-    if (ps + 1 < npass) load_a(af[(ps + 1) & 1], ps + 1);
+    if (!RING1 && ps + 1 < npass) load_a(af[(ps + 1) & 1], ps + 1);
     if (ps * 256 + w * 32 >= B) continue;          // wave-uniform: rows beyond B
     f32x16_t acc[NJ];  // starts at the bias (exactly): z = bo + sum_k D3 Wo accumulates in the MFMA
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
       acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, *reinterpret_cast<const bf16x8_t *>(bfr + (j * 64 + lane) * 8),
                                                        f32x16_t{}, 0, 0, 0);
+    const bf16_t *asrc = a_src(ps);
 #pragma unroll
     for (int kk = 0; kk < nkk; ++kk) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const bf16x8_t b = frag(Wt, sw_off(j * 32 + (lane & 31), kk * 16 + 8 * half, CHD));
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ps & 1][kk], b, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[RING1 ? 0 : ps & 1][kk % NAF], b, acc[j], 0, 0, 0);
       }
+      if (RING1 && kk + NAF < nkk) af[0][kk % NAF] = *reinterpret_cast<const bf16x8_t *>(asrc + (kk + NAF) * astr);
     }
+    if (RING1 && ps + 1 < npass) load_a(af[0], ps + 1);   // the next pass's head under this epilogue
     DEC_PROBE(2 + 2 * ps);
     const int rb = ps * 256 + w * 32;
 #pragma unroll
@@ -324,19 +330,27 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   // nothing below reads them.
   constexpr int P2D = 4;
   constexpr int nk2 = B / BK;
-  // A fragment (kc, kk): row-strided from D3^T, or 1 KB contiguous from the packed image
+  constexpr int ND2 = (d + 255) / 256;   // 32-row d tiles per wave: w (and w + 8 at d = 512)
+  // A fragment (kc, kk) of d tile dt: row-strided from D3^T, or 1 KB contiguous from the packed image
   const bool pk = p.D3tp != nullptr;
-  const bf16_t *arow = pk ? p.D3tp + ((int64_t)min(w, d / 32 - 1) * (p.ldt / 16) * 64 + lane) * 8
-                          : p.D3t + (int64_t)(min(w, d / 32 - 1) * 32 + (lane & 31)) * p.ldt + 8 * half;
+  auto arow_of = [&](int dt) -> const bf16_t * {
+    const int t = min(w + 8 * dt, d / 32 - 1);
+    return pk ? p.D3tp + ((int64_t)t * (p.ldt / 16) * 64 + lane) * 8
+              : p.D3t + (int64_t)(t * 32 + (lane & 31)) * p.ldt + 8 * half;
+  };
+  const bf16_t *arow = arow_of(0);
   auto afrag = [&](int kc, int kk) {
     return *reinterpret_cast<const bf16x8_t *>(arow + (pk ? (kc * 4 + kk) * 512 : kc * BK + kk * 16));
   };
   bf16x8_t ring[P2D][4];
+  auto fill_ring = [&]() {
 #pragma unroll
-  for (int q = 0; q < P2D; ++q)
-    if (q < nk2)
+    for (int q = 0; q < P2D; ++q)
+      if (q < nk2)
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) ring[q][kk] = afrag(q, kk);
+        for (int kk = 0; kk < 4; ++kk) ring[q][kk] = afrag(q, kk);
+  };
+  fill_ring();
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // dZ^T image, red_cs, red_loss
   DEC_PROBE(6);
   if (tid < NB && n0 + tid < V) {
@@ -345,10 +359,17 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     p.gb[n0 + tid] = g;
   }
 
-  // ---- phase 2: dWo[d][NB] = D3^T[d][B] . dZ[B][NB].  Wave w owns rows 32w .. +32 of d (waves
-  // beyond d idle) and all NB columns; A fragments from global through a ring P2D chunks of 64 k
+  // ---- phase 2: dWo[d][NB] = D3^T[d][B] . dZ[B][NB].  Wave w owns rows 32w .. +32 of d (and
+  // 32(w + 8) .. at d = 512; waves beyond d idle) and all NB columns; A fragments from global
+  // through a ring P2D chunks of 64 k
   // deep, B fragments from the dZ^T image.
-  if (w * 32 < d) {
+#pragma unroll 1
+  for (int dt = 0; dt < ND2 && (w + 8 * dt) * 32 < d; ++dt) {
+    if (dt > 0) {
+      arow = arow_of(dt);
+      fill_ring();
+    }
+    const int dr0 = (w + 8 * dt) * 32;   // this tile's first row of dWo
     f32x16_t acc2[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -378,7 +399,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     for (int j = 0; j < NJ; ++j) {
       const int gc2 = n0 + j * 32 + (lane & 31);
       if (gc2 < V) {
-        uint32_t g0 = (uint32_t)((w * 32 + 4 * half) * V + gc2);
+        uint32_t g0 = (uint32_t)((dr0 + 4 * half) * V + gc2);
         asm volatile("" : "+v"(g0));
 #pragma unroll
         for (int r = 0; r < 16; ++r)
@@ -434,7 +455,7 @@ extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const
   CC_REQUIRE(D3 && D3t && (WoT || Wo) && bo && y_bits && dZ && gW && gb && loss_partials,
              "cc_dec_bce_dw: null pointer");
   CC_REQUIRE(B == 128 || B == 256 || B == 512, "cc_dec_bce_dw: B must be 128, 256 or 512");
-  CC_REQUIRE(d == 128 || d == 256, "cc_dec_bce_dw: d must be 128 or 256");
+  CC_REQUIRE(d == 128 || d == 256 || d == 512, "cc_dec_bce_dw: d must be 128, 256 or 512");
   CC_REQUIRE(V > 0 && ldt >= B && ldt % 8 == 0, "cc_dec_bce_dw: V > 0, ldt >= B, ldt % 8 == 0");
   CC_REQUIRE((int64_t)d * V * 4 <= 0xFFFFFFFFll, "cc_dec_bce_dw: dWo below 4 GB (32-bit buffer offsets)");
   CC_REQUIRE(!loss_out || ticket, "cc_dec_bce_dw: loss_out needs a ticket word");
@@ -461,15 +482,17 @@ extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const
   p.scale = 1.0f / ((float)B * (float)V);
   p.V = V;
   p.ldt = ldt;
-  const dim3 grid((unsigned)cdiv(V, NB)), block(NTH);
+  const dim3 grid((unsigned)cdiv(V, d <= 256 ? nb_of<256>() : nb_of<512>())), block(NTH);
   hipStream_t s = as_stream(stream);
 #define DO_LAUNCH(DD, BBB) \
   if (d == DD && B == BBB) hipLaunchKernelGGL((dec_bce_dw_kernel<DD, BBB>), grid, block, 0, s, p);
   DO_LAUNCH(256, 512) DO_LAUNCH(256, 256) DO_LAUNCH(256, 128)
   DO_LAUNCH(128, 512) DO_LAUNCH(128, 256) DO_LAUNCH(128, 128)
+  DO_LAUNCH(512, 512) DO_LAUNCH(512, 256) DO_LAUNCH(512, 128)
 #undef DO_LAUNCH
   CC_LAUNCH_CHECK("dec_bce_dw_kernel");
   return CC_OK;
 }
 
-extern "C" int32_t cc_dec_bce_dw_blocks(int32_t V) { return (int32_t)cdiv(V, NB); }
+// an upper bound over every d (the narrowest slice)
+extern "C" int32_t cc_dec_bce_dw_blocks(int32_t V) { return (int32_t)cdiv(V, NB_MIN); }

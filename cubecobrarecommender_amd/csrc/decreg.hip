@@ -30,8 +30,10 @@
 
 namespace {
 
-constexpr int NB = 96;       // V columns per block (230 slices at |V| = 22,000)
-constexpr int NJ = NB / 32;  // 32-column accumulator tiles per wave
+// V columns per block: d <= 256: 96 (230 slices at |V| = 22,000); d = 512 (the reference width,
+// model.py:62-64): 64, so the Wo slice and the dZ^T tile fit the LDS together
+template <int D> constexpr int kl_nb() { return D <= 256 ? 96 : 64; }
+constexpr int NB_MIN = 64;
 constexpr int NTH = 512;     // 8 waves
 constexpr int TR = 512;      // rows per tile of the main kernel (2 passes of 8 x 32)
 constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
@@ -75,6 +77,7 @@ __device__ __forceinline__ uint16_t bf16_bits(float f) { return __builtin_bit_ca
 // Wo [d][V] slice [n0, n0 + NB) -> LDS k-contiguous image Wt[NB][d] (swizzled); columns past V clamp
 template <int D>
 __device__ __forceinline__ void load_wo_slice(const bf16_t *__restrict__ Wo, int V, int n0, bf16_t *Wt) {
+  constexpr int NB = kl_nb<D>();
   constexpr int CHD = D / 8, CN = NB / 8, NT4 = (D / 4 * CN + NTH - 1) / NTH;
   const int tid = threadIdx.x;
   const bool vec = (V % 8 == 0) && n0 + NB <= V;
@@ -130,10 +133,16 @@ __device__ __forceinline__ void logits_load(const KlP &p, int rb, LFrag<D, RG> &
   for (int kk = 0; kk < RG; ++kk) f.af[kk] = *reinterpret_cast<const bf16x8_t *>(f.src + kk * 512);
 }
 template <int D, int RG>
-__device__ __forceinline__ void logits_mfma(const bf16_t *Wt, LFrag<D, RG> &f, const float (&bias)[NJ],
-                                            f32x16_t (&acc)[NJ]) {
+__device__ __forceinline__ void logits_mfma(const bf16_t *Wt, LFrag<D, RG> &f, const float (&bias)[kl_nb<D>() / 32],
+                                            f32x16_t (&acc)[kl_nb<D>() / 32]) {
+  constexpr int NJ = kl_nb<D>() / 32;
   constexpr int nkk = LFrag<D, RG>::nkk, RING = RG, CHD = D / 8;
   const int lane = threadIdx.x & 63, half = lane >> 5;
+  // the Wo-slice fragments are the same for every row block: an opaque base per call keeps the
+  // compiler from hoisting all of them (192+ VGPRs) out of the callers' row loops
+  int wofs = 0;
+  asm volatile("" : "+v"(wofs));
+  Wt += wofs;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     float b = bias[j];
@@ -150,14 +159,6 @@ __device__ __forceinline__ void logits_mfma(const bf16_t *Wt, LFrag<D, RG> &f, c
     }
     if (kk + RING < nkk) f.af[kk % RING] = *reinterpret_cast<const bf16x8_t *>(f.src + (kk + RING) * 512);
   }
-}
-template <int D>
-__device__ __forceinline__ void logits_block(const KlP &p, const bf16_t *Wt, int rb, const float (&bias)[NJ],
-                                             f32x16_t (&acc)[NJ]) {
-  LFrag<D> f;
-  logits_load<D>(p, rb, f);
-  __builtin_amdgcn_sched_barrier(0);
-  logits_mfma<D>(Wt, f, bias, acc);
 }
 
 // Reduce-scatter of 16 per-row values over the 32 lanes of a half-wave (lanes with the same
@@ -208,6 +209,7 @@ __device__ __forceinline__ float half_sum(float v) {
 // both.  One block per slice stages its Wo slice once; its waves walk the 32-row blocks.
 template <int D>
 __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(1, 2))) void kl_stats_kernel(KlP p) {
+  constexpr int NB = kl_nb<D>(), NJ = NB / 32;
   __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
   constexpr int CHD = D / 8;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5;
@@ -220,15 +222,23 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   __syncthreads();
   KL_PROBE(9);
   // wave w walks the 32-row blocks w, w + 8, ...; the next block's fragments load during this one
+  // (d <= 256: two whole fragment sets; d = 512: one ring of 16 refilled during the MFMAs, the
+  // next block's head loaded behind the last MFMA)
   const int nrb = p.rows / 32;
   constexpr int nkk = D / 16;
-  bf16x8_t af[2][nkk];
-  auto load = [&](bf16x8_t (&dst)[nkk], int rb) {
-    const bf16_t *src = p.D3p + ((int64_t)((p.row0 + 32 * min(rb, nrb - 1)) / 32) * nkk * 64 + lane) * 8;
-#pragma unroll
-    for (int kk = 0; kk < nkk; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 512);
+  constexpr bool RINGS = nkk > 16;
+  constexpr int NAF = RINGS ? 16 : nkk;
+  constexpr int W8 = NTH / 64;
+  bf16x8_t af[RINGS ? 1 : 2][NAF];
+  auto src_of = [&](int rb) {
+    return p.D3p + ((int64_t)((p.row0 + 32 * min(rb, nrb - 1)) / 32) * nkk * 64 + lane) * 8;
   };
-  auto body = [&](const bf16x8_t (&cur)[nkk], int rb) {
+  auto load = [&](bf16x8_t (&dst)[NAF], int rb) {
+    const bf16_t *src = src_of(rb);
+#pragma unroll
+    for (int kk = 0; kk < NAF; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 512);
+  };
+  auto body = [&](bf16x8_t (&cur)[NAF], int rb) {
     f32x16_t acc[NJ];  // bias-initialised: registers 4g..4g+3 are columns 8g + 4 half .. +3
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -240,13 +250,20 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         acc[j][4 * g + 2] = b.z;
         acc[j][4 * g + 3] = b.w;
       }
+    const bf16_t *src = src_of(rb);
+    int wofs = 0;   // opaque per row block: the Wo-slice fragments are not hoisted out of the loop
+    asm volatile("" : "+v"(wofs));
+    const bf16_t *Wtb = Wt + wofs;
 #pragma unroll
-    for (int kk = 0; kk < nkk; ++kk)
+    for (int kk = 0; kk < nkk; ++kk) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const bf16x8_t a = frag(Wt, sw_off(j * 32 + (lane & 31), kk * 16 + 8 * half, CHD));
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, cur[kk], acc[j], 0, 0, 0);
+        const bf16x8_t a = frag(Wtb, sw_off(j * 32 + (lane & 31), kk * 16 + 8 * half, CHD));
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, cur[kk % NAF], acc[j], 0, 0, 0);
       }
+      if (RINGS && kk + NAF < nkk) cur[kk % NAF] = *reinterpret_cast<const bf16x8_t *>(src + (kk + NAF) * 512);
+    }
+    if (RINGS && rb + W8 < nrb) load(cur, rb + W8);
     if (rb == w) KL_PROBE(10);
     float m = -INFINITY;
 #pragma unroll
@@ -267,16 +284,19 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       p.part_s[(int64_t)row * p.nsl + sl] = e;
     }
   };
-  constexpr int W8 = NTH / 64;
   load(af[0], w);
-  for (int rb = w; rb < nrb; rb += 2 * W8) {
-    if (rb + W8 < nrb) load(af[1], rb + W8);
-    __builtin_amdgcn_sched_barrier(0);
-    body(af[0], rb);
-    if (rb + W8 < nrb) {
-      if (rb + 2 * W8 < nrb) load(af[0], rb + 2 * W8);
+  if constexpr (RINGS) {
+    for (int rb = w; rb < nrb; rb += W8) body(af[0], rb);
+  } else {
+    for (int rb = w; rb < nrb; rb += 2 * W8) {
+      if (rb + W8 < nrb) load(af[1], rb + W8);
       __builtin_amdgcn_sched_barrier(0);
-      body(af[1], rb + W8);
+      body(af[0], rb);
+      if (rb + W8 < nrb) {
+        if (rb + 2 * W8 < nrb) load(af[0], rb + 2 * W8);
+        __builtin_amdgcn_sched_barrier(0);
+        body(af[1], rb + W8);
+      }
     }
   }
 }
@@ -313,7 +333,7 @@ __global__ __launch_bounds__(256) void kl_merge_kernel(KlP p) {
 }
 
 // ---------------------------------------------------------------- main
-constexpr int ZT_BYTES = NB * TR * 2;
+template <int NB>
 struct MainSmem {
   bf16_t Zt[NB * TR];       // dZ^T tile [NB][TR] (swizzled)
   float4 rs[TR];            // row stats of the tile
@@ -325,8 +345,14 @@ struct MainSmem {
 
 // FIX = false: the main pass.  FIX = true: the exact-clip correction (runs only when p.flag is set):
 // c = -scale p delta_row replaces dz; dZ, dWo, dbo are updated in place.
-template <int D, bool FIX>
-__device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt, MainSmem &sm) {
+// PERSIST (the full-mode regulariser: |V| rows in many tiles): the block's dWo slice stays in the
+// waves' accumulators across all row tiles and is stored once at the end — the per-tile
+// read-modify-write of gW (96 KB each way per tile per block, 2 GB per step at |V| = 22,000) was
+// 40 % of the kernel by the phase probe (tools/micro/kl_probe_full.hip).
+template <int D, bool FIX, bool PERSIST = false>
+__device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt, MainSmem<kl_nb<D>()> &sm) {
+  constexpr int NB = kl_nb<D>(), NJ = NB / 32;
+  static_assert(!(FIX && PERSIST), "the fix pass adds into gW");
   constexpr int CHB = TR / 8;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
   const int n0 = sl * NB;
@@ -351,6 +377,15 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   const __amdgpu_buffer_rsrc_t dz_rs =
       __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)p.rows * (uint32_t)V * 2u, 0x00020000);
   const float scale = p.scale;
+  // phase 2's d tiles of wave w: 32w .. (and 32(w + 8) .. at d = 512)
+  constexpr int ND2 = (D + 255) / 256;
+  f32x16_t accp[PERSIST ? ND2 : 1][NJ];  // PERSIST: dWo[d tile][NB] over every tile
+#pragma unroll
+  for (int t = 0; t < (PERSIST ? ND2 : 1); ++t)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) accp[t][j][r] = 0.f;
 
   for (int t0 = 0; t0 < p.rows; t0 += TR) {
     const int nt = min(TR, p.rows - t0);
@@ -383,8 +418,8 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       for (int r = 0; r < 16; ++r) roff[r] = (uint32_t)sm.card[rb + acc_row(r, lane)];
       uint32_t zrow = (uint32_t)((t0 + rb + 4 * half) * V + n0 + (lane & 31));
       asm volatile("" : "+v"(zrow));  // per-pass base of the dZ stores (no hoisted 64-bit addresses)
-      LFrag<D, D / 16> lf;              // all A fragments first in the memory queue, then M~
-      logits_load<D>(p, (p.row0 + t0 + rb) / 32, lf);
+      LFrag<D, (PERSIST || D > 256) ? 8 : D / 16> lf;  // all A fragments first in the memory queue, then M~ (PERSIST: a ring of 8 leaves room for the dWo accumulators)
+      logits_load(p, (p.row0 + t0 + rb) / 32, lf);
       float tv[NJ][16];
       if constexpr (!FIX) {
 #pragma unroll
@@ -397,7 +432,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       }
       __builtin_amdgcn_sched_barrier(0);
       f32x16_t acc[NJ];
-      logits_mfma<D>(Wt, lf, bias, acc);
+      logits_mfma(Wt, lf, bias, acc);
       KL_PROBE(2 + 2 * ps);
       bool deadp = false;   // an element of this pass has p < 1e-7
       float mn = 1.f;       // (fast path) the smallest p of the lane's elements
@@ -410,6 +445,11 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       for (int j = 0; j < NJ; ++j) {
         const int col = j * 32 + (lane & 31);
         uint16_t tt[16];
+        // row stats re-read per column tile (an opaque base): held across the three tiles they
+        // cost 64 VGPRs, LDS has the bandwidth
+        int rsofs = 0;
+        asm volatile("" : "+v"(rsofs));
+        const float4 *rsp = sm.rs + rsofs;
         // the common case — all rows real, all 32 columns inside V: no per-element masks, the
         // clip of q folded into one med3 (ln clip(p, 1e-7, 1) = med3(ln p, ln 1e-7, 0)), the
         // dead-element test as a running min of p
@@ -417,7 +457,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
         if (fast) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const float4 st = sm.rs[rb + acc_row(r, lane)];
+            const float4 st = rsp[rb + acc_row(r, lane)];
             const float lp = acc[j][r] - st.x - st.y;  // ln p = z - m - ln s
             const float pr = __builtin_amdgcn_exp2f(lp * LOG2E);
             const float tc = __builtin_amdgcn_fmed3f(tv[j][r], PMIN, 1.f);
@@ -435,7 +475,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int lr = rb + acc_row(r, lane);
-            const float4 st = sm.rs[lr];
+            const float4 st = rsp[lr];
             const bool live_row = roff[r] < 0x80000000u && valid[j];
             const float lp = acc[j][r] - st.x - st.y;  // ln p = z - m - ln s
             const float pr = __builtin_amdgcn_exp2f(lp * LOG2E);
@@ -504,18 +544,24 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
     // ---- phase 2: dWo[d][NB] (+)= D3^T[d][tile rows] dZ[tile rows][NB] (wave w: d rows 32w..).
     // A fresh accumulator per tile, added into gW (the block's slice stays L2-resident between
     // tiles): nothing of phase 2 is live across phase 1's epilogue.
-    if (w * 32 < D) {
-      f32x16_t acc2[NJ];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
+    for (int dt = 0; dt < ND2; ++dt) {
+      const int wt = w + 8 * dt;   // this d tile (rows 32 wt .. of dWo)
+      if (wt * 32 >= D) break;
+      f32x16_t acc2l[NJ];
+      f32x16_t(&acc2)[NJ] = PERSIST ? accp[PERSIST ? dt : 0] : acc2l;
+      if constexpr (!PERSIST) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
+      }
       // K = the tile's rows (a multiple of 32) in chunks of 32 (two 16-row fragments), a ring of
       // P2 chunks in flight (the loads come from L2: one chunk's 6 MFMAs cannot cover one latency)
       constexpr int P2 = 6;
       const int nc = nt / 32;
       const int j0 = (p.row0 + t0) / 16;
-      const bf16_t *arow = p.D3tp + ((int64_t)w * (p.ldt / 16) * 64 + lane) * 8 + (int64_t)j0 * 512;
+      const bf16_t *arow = p.D3tp + ((int64_t)wt * (p.ldt / 16) * 64 + lane) * 8 + (int64_t)j0 * 512;
       bf16x8_t ring[P2][2];
 #pragma unroll
       for (int q = 0; q < P2; ++q)
@@ -543,8 +589,8 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int gc = n0 + j * 32 + (lane & 31);
-        if (gc < V) {
-          uint32_t g0 = (uint32_t)((w * 32 + 4 * half) * V + gc);
+        if (!PERSIST && gc < V) {
+          uint32_t g0 = (uint32_t)((wt * 32 + 4 * half) * V + gc);
           asm volatile("" : "+v"(g0));  // opaque per tile: keeps 48 row addresses from being hoisted
           // the tile's 16 partial sums of this column are added to gW with 8 loads in flight at
           // a time (a load-add-store per element serialised 48 round trips per tile: the
@@ -566,6 +612,22 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
     }
   }
 
+  if constexpr (PERSIST) {  // the slice's dWo, once
+#pragma unroll
+    for (int dt = 0; dt < ND2; ++dt) {
+      const int wt = w + 8 * dt;
+      if (wt * 32 >= D) break;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int gc = n0 + j * 32 + (lane & 31);
+        if (gc < V) {
+          const uint32_t g0 = (uint32_t)((wt * 32 + 4 * half) * V + gc);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) p.gW[g0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V)] = accp[dt][j][r];
+        }
+      }
+    }
+  }
   KL_PROBE(7);
   // ---- epilogue: dbo, loss partial, the fix flag
 #pragma unroll
@@ -624,11 +686,11 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   }
 }
 
-template <int D>
+template <int D, bool PERSIST>
 __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
-  __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
-  __shared__ __attribute__((aligned(16))) MainSmem sm;
-  kl_slice<D, false>(p, blockIdx.x, Wt, sm);
+  __shared__ __attribute__((aligned(16))) bf16_t Wt[kl_nb<D>() * D];
+  __shared__ __attribute__((aligned(16))) MainSmem<kl_nb<D>()> sm;
+  kl_slice<D, false, PERSIST>(p, blockIdx.x, Wt, sm);
 }
 
 // The exact-clip correction: a small persistent grid (FIXG blocks) that leaves at once when the
@@ -636,8 +698,8 @@ __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
 constexpr int FIXG = 64;
 template <int D>
 __global__ __launch_bounds__(NTH) void kl_fix_kernel(KlP p) {
-  __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
-  __shared__ __attribute__((aligned(16))) MainSmem sm;
+  __shared__ __attribute__((aligned(16))) bf16_t Wt[kl_nb<D>() * D];
+  __shared__ __attribute__((aligned(16))) MainSmem<kl_nb<D>()> sm;
   if (__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
   for (int sl = blockIdx.x; sl < p.nsl; sl += gridDim.x) {
     kl_slice<D, true>(p, sl, Wt, sm);
@@ -660,11 +722,11 @@ __global__ __launch_bounds__(256) void kl_tsum_kernel(const float *__restrict__ 
 }  // namespace
 
 extern "C" size_t cc_dec_kl_ws_size(int32_t rows, int32_t V) {
-  const int64_t nsl = cdiv(V, NB);
+  const int64_t nsl = cdiv(V, NB_MIN);   // an upper bound over every d
   return (size_t)(3 * rows * nsl * sizeof(float) + rows * sizeof(float4) + 256);
 }
 
-extern "C" int32_t cc_dec_kl_blocks(int32_t V) { return (int32_t)cdiv(V, NB); }
+extern "C" int32_t cc_dec_kl_blocks(int32_t V) { return (int32_t)cdiv(V, NB_MIN); }   // upper bound over d
 
 extern "C" int cc_kl_tsum(const float *Mt, int32_t n, int32_t V, float *tsum, void *stream) {
   CC_REQUIRE(Mt && tsum && n >= 0 && V > 0, "cc_kl_tsum: args");
@@ -678,7 +740,8 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
   CC_REQUIRE(a && a->D3p && a->D3tp && a->Wo && a->bo && a->Mt && a->tsum && a->reg_idx && a->dZ && a->gW &&
                  a->gb && a->loss_partials && a->ws,
              "cc_dec_softmax_kl_dw: null pointer");
-  CC_REQUIRE(a->d == 128 || a->d == 256, "cc_dec_softmax_kl_dw: d must be 128 or 256");
+  CC_REQUIRE(a->d == 128 || a->d == 256 || a->d == 512, "cc_dec_softmax_kl_dw: d must be 128, 256 or 512");
+  const int NB = a->d <= 256 ? kl_nb<256>() : kl_nb<512>();
   CC_REQUIRE(a->rows > 0 && a->rows % 32 == 0, "cc_dec_softmax_kl_dw: rows must be a positive multiple of 32");
   CC_REQUIRE(a->row0 % 32 == 0 && a->ldt % 16 == 0 && a->ldt >= a->row0 + a->rows,
              "cc_dec_softmax_kl_dw: row0 % 32, ldt % 16, ldt >= row0 + rows");
@@ -728,13 +791,17 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
     CC_LAUNCH_CHECK("kl_stats_kernel");                                                                      \
     hipLaunchKernelGGL(kl_merge_kernel, dim3((unsigned)cdiv(a->rows, 4)), dim3(256), 0, s, p);              \
     CC_LAUNCH_CHECK("kl_merge_kernel");                                                                      \
-    hipLaunchKernelGGL((kl_main_kernel<DD>), gm, dim3(NTH), 0, s, p);                                       \
+    if (a->rows > TR)                                                                                        \
+      hipLaunchKernelGGL((kl_main_kernel<DD, true>), gm, dim3(NTH), 0, s, p);                                \
+    else                                                                                                     \
+      hipLaunchKernelGGL((kl_main_kernel<DD, false>), gm, dim3(NTH), 0, s, p);                               \
     CC_LAUNCH_CHECK("kl_main_kernel");                                                                       \
     hipLaunchKernelGGL((kl_fix_kernel<DD>), dim3(FIXG), dim3(NTH), 0, s, p);                                \
     CC_LAUNCH_CHECK("kl_fix_kernel");                                                                        \
   }
   KL_LAUNCH(256)
   KL_LAUNCH(128)
+  KL_LAUNCH(512)
 #undef KL_LAUNCH
   return CC_OK;
 }

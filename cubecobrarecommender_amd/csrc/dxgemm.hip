@@ -13,6 +13,8 @@
 // global source address.  k >= kend chunks point past the buffer's range: the DMA writes zeros.
 // (tile, split) pairs are dealt split-major over the 8 XCDs so a split's A and B panels are
 // fetched into one XCD's L2 once.  The split partials are summed by cc_splitk_reduce.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace {
@@ -135,6 +137,100 @@ __global__ __launch_bounds__(XNT) void dx_splitk_kernel(DxP p) {
     }
 }
 
+// ---- the tall shape (the full-mode regulariser: M = |V| identity rows, N = d = 256): 128 x 256
+// tiles, so each dZ panel (the 968 MB operand at |V| = 22,000) is read from HBM once instead of
+// once per 128-column tile; 8 waves as 2 (M) x 4 (N) of 64 x 64, 3 LDS stages of A 128 x 64 +
+// B 256 x 64 (48 KB each).  Splits are dealt split-major over the XCDs as above, so a split's Wo
+// panel (256 x K/splits bf16) stays in one XCD's L2.
+constexpr int WBM = 128, WBN = 256, WST = 3, WNT = 512;
+constexpr int WTILE_BYTES = (WBM + WBN) * XBK * 2;  // 48 KB
+constexpr int WLDS = WST * WTILE_BYTES;              // 144 KB
+
+// stage st <- K-tile k0: A rows [0, 128) (2 instructions per wave) and B rows [0, 256) (4 per wave),
+// each instruction 8 rows x 128 B
+__device__ __forceinline__ void dma_tile_w(const DxP &p, const __amdgpu_buffer_rsrc_t &ra,
+                                           const __amdgpu_buffer_rsrc_t &rb, char *smem, int st, int bm,
+                                           int bn, int k0, int kend) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int rl = lane >> 3, slot = lane & 7;
+  char *sa = smem + st * WTILE_BYTES, *sb = sa + WBM * XBK * 2;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = w * 2 + u;  // A rows 8i .. 8i + 7
+    const int row = 8 * i + rl;
+    const int k = k0 + 8 * (slot ^ (row & 7));
+    const uint32_t oa = k < kend ? (uint32_t)(((bm + row) * p.lda + k) * 2) : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void *)(sa + i * 1024), 16, oa, 0, 0, 0);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = w * 4 + u;  // B rows 8i .. 8i + 7
+    const int row = 8 * i + rl;
+    const int k = k0 + 8 * (slot ^ (row & 7));
+    const uint32_t ob = k < kend ? (uint32_t)(((bn + row) * p.ldb + k) * 2) : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void *)(sb + i * 1024), 16, ob, 0, 0, 0);
+  }
+}
+
+__global__ __launch_bounds__(WNT) void dx_wide_kernel(DxP p) {
+  extern __shared__ __attribute__((aligned(1024))) char wsmem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5;
+  const int wm = w >> 2, wn = w & 3;
+  const int ntiles = p.tiles_m * (p.N / WBN);
+  const int q = xcd_remap(blockIdx.x, ntiles * p.splits);
+  const int split = q / ntiles, tile = q % ntiles;
+  const int bm = (tile % p.tiles_m) * WBM, bn = (tile / p.tiles_m) * WBN;
+  const int kbeg = split * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
+  const int nk = kbeg < kend ? (kend - kbeg + XBK - 1) / XBK : 0;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void *)p.A, (short)0, p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void *)p.B, (short)0, p.b_bytes, 0x00020000);
+  f32x16_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < WST - 1; ++s)
+    if (s < nk) dma_tile_w(p, ra, rb, wsmem, s, bm, bn, kbeg + s * XBK, kend);
+  const int ar = wm * 64 + (lane & 31), br = wn * 64 + (lane & 31);
+  for (int t = 0; t < nk; ++t) {
+    // tile t landed (own DMAs counted, then the barrier); 6 DMA instructions per wave per tile,
+    // min(1, nk - 1 - t) tiles issued after t may stay in flight
+    if (t + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + WST - 1 < nk) dma_tile_w(p, ra, rb, wsmem, (t + WST - 1) % WST, bm, bn, kbeg + (t + WST - 1) * XBK, kend);
+    const char *sa = wsmem + (t % WST) * WTILE_BYTES, *sb = sa + WBM * XBK * 2;
+#pragma unroll
+    for (int kk = 0; kk < XBK / 16; ++kk) {
+      const int c = 2 * kk + half;
+      const bf16x8_t a0 = frag(sa, ar, c), a1 = frag(sa, ar + 32, c);
+      const bf16x8_t b0 = frag(sb, br, c), b1 = frag(sb, br + 32, c);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+    }
+  }
+  float *out = p.P + (int64_t)split * p.M * p.N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = bn + wn * 64 + j * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = bm + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        out[(int64_t)row * p.N + col] = acc[i][j][r];
+      }
+    }
+}
+
 }  // namespace
 
 extern "C" int cc_gemm_dx_splitk(const void *A, int32_t lda, const void *B, int32_t ldb, int32_t M, int32_t N,
@@ -161,6 +257,21 @@ extern "C" int cc_gemm_dx_splitk(const void *A, int32_t lda, const void *B, int3
   p.tiles_m = M / XBM;
   p.a_bytes = (uint32_t)((int64_t)M * lda * 2);
   p.b_bytes = (uint32_t)((int64_t)N * ldb * 2);
+  static const int wide_min = [] {  // A/B switch (dev): smallest M for the 128 x 256 tiles (0: never)
+    const char *e = getenv("CCREC_DX_WIDE_MIN");
+    return e ? atoi(e) : 4096;
+  }();
+  if (wide_min > 0 && M >= wide_min && N % WBN == 0) {  // tall M (full-mode regulariser)
+    static bool attr = [] {
+      return hipFuncSetAttribute((const void *)dx_wide_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, WLDS) ==
+             hipSuccess;
+    }();
+    CC_REQUIRE(attr, "cc_gemm_dx_splitk: dynamic LDS attribute");
+    const int nb = (M / WBM) * (N / WBN) * splits;
+    hipLaunchKernelGGL(dx_wide_kernel, dim3((unsigned)nb), dim3(WNT), WLDS, as_stream(stream), p);
+    CC_LAUNCH_CHECK("dx_wide_kernel");
+    return CC_OK;
+  }
   const int nb = (M / XBM) * (N / XBN) * splits;
   hipLaunchKernelGGL(dx_splitk_kernel, dim3((unsigned)nb), dim3(XNT), 0, as_stream(stream), p);
   CC_LAUNCH_CHECK("dx_splitk_kernel");

@@ -758,9 +758,18 @@ __global__ __launch_bounds__(FNT) void tower_fwd_wide_kernel(TowerP p) {
     q += 2;
   }
   while (layer < 6) advance();
-  // D3 = the last layer's output (now xin): rows and D3^T [d][R]
+  // D3 = the last layer's output (now xin): rows and D3^T [d][R], and the packed operand images
+  // of the fused output-layer kernels (d = 512: cc_dec_bce_dw)
   rows_copy_out(xin, ldx, reinterpret_cast<bf16_t *>(p.act[6]), d, r0);
   if (p.act6t) cols_copy_out(xin, ldx, reinterpret_cast<bf16_t *>(p.act6t), d, p.R, r0);
+  if (p.act6p) {  // D3 as the logits' A operand: fragments (blockIdx.x, j)
+    for (int v = threadIdx.x; v < (d / 16) * 64; v += FNT) {
+      const int j = v >> 6, ln = v & 63;
+      *reinterpret_cast<u32v4 *>(p.act6p + pack_off(blockIdx.x, j, ln, d)) =
+          *reinterpret_cast<const u32v4 *>(xin + (ln & 31) * ldx + 16 * j + 8 * (ln >> 5));
+    }
+  }
+  if (p.act6tp) pt_copy_out(xin, ldx, p.act6tp, d, p.R, r0);  // D3^T: the dWo A operand
 }
 
 __global__ __launch_bounds__(FNT) void tower_bwd_chain_wide_kernel(TowerP p) {
@@ -1247,8 +1256,9 @@ int make_params(const cc_tower_args *t, TowerP &p) {
     if (!t->hpt[a] || !t->gpt[a] || (((uintptr_t)t->hpt[a] | (uintptr_t)t->gpt[a]) & 15)) p.dwpacked = false;
   }
   if (t->B % 16 || t->R % 16) p.dwpacked = false;
-  p.act6p = narrow ? static_cast<bf16_t *>(t->act6p) : nullptr;  // fused D1 / D2 operands: d <= 256
-  p.act6tp = narrow ? static_cast<bf16_t *>(t->act6tp) : nullptr;
+  // fused D1 / D2 operands: written by the fast (d <= 256) and wide (d <= 1024) bf16 chains
+  p.act6p = t->dtype == CC_BF16 && fast ? static_cast<bf16_t *>(t->act6p) : nullptr;
+  p.act6tp = t->dtype == CC_BF16 && fast ? static_cast<bf16_t *>(t->act6tp) : nullptr;
   if (((uintptr_t)p.act6p | (uintptr_t)p.act6tp) & 15)
     return cc::fail(CC_ERR_ARG, "cc_tower: packed D3 images must be 16-B aligned");
   if (p.packed)

@@ -265,7 +265,8 @@ class Trainer:
         # tiles alone fill the chip — no split-K
         # full-mode regulariser (~|V| rows): 2 K-splits (tools/micro/dx_full_micro.py at |V| = 22,000:
         # 1 split 643 us, 2 or 4 splits 515 us, the library GEMM 391-399 us)
-        self.splits_reg = self.splits if self.Breg <= 1024 else int(os.environ.get('CCREC_DX_SPLITS_REG', '2'))
+        # (the 128 x 256-tile kernel of dxgemm.hip for tall M: 4 splits)
+        self.splits_reg = self.splits if self.Breg <= 1024 else int(os.environ.get('CCREC_DX_SPLITS_REG', '4'))
         self.tsplits = max(1, min(8, B // 128))             # tower dW: K = rows (B or 2B)
         self.split_buf = torch.zeros(max(self.splits * B * d, self.splits_reg * self.Breg * d,
                                          2 * self.tsplits * max(d, 256) * 256), **f32)
@@ -286,7 +287,7 @@ class Trainer:
         # decoder dX on the LDS-DMA pipelined split-K kernel (dxgemm.hip; CCREC_DX_GLDS=0: gemm.hip's)
         self.dx_glds = self.dtype == L.CC_BF16 and os.environ.get('CCREC_DX_GLDS', '1') != '0'
         # D1 output layer fused (logits + BCE + dZ + dWo, csrc/decout.hip) where its shape fits
-        self.fused_out = (self.dtype == L.CC_BF16 and self.fused_tower and not self.mx8 and d in (128, 256)
+        self.fused_out = (self.dtype == L.CC_BF16 and self.fused_tower and not self.mx8 and d in (128, 256, 512)
                           and B in (128, 256, 512) and os.environ.get('CCREC_DEC_FUSED', '1') != '0')
         self.gPre1T = torch.zeros(d, self.RP, **T) if self.embed_mfma else None
         if self.mx8 and not self.fused_tower:
@@ -325,10 +326,10 @@ class Trainer:
             slab = int(L.lib().cc_tower_slab_elems(d))
             self.slab = torch.zeros((R // 32) * slab, **f32)
             # D2 output layer fused (logits twice -> softmax -> KL -> dZ -> dWo, csrc/decreg.hip): bf16,
-            # d in {128, 256} with the packed D3 images (the same shape class as the fused D1 kernel)
+            # d in {128, 256, 512} with the packed D3 images (the same shape class as the fused D1 kernel)
             # (its buffer descriptors address M~ up to row hi and the Breg x V bf16 dZ with 32-bit
             # extents: larger card pools fall back to the Z2 path instead of failing)
-            self.fused_reg = (self.use_reg and self.D3p is not None and not self.mx8 and d in (128, 256)
+            self.fused_reg = (self.use_reg and self.D3p is not None and not self.mx8 and d in (128, 256, 512)
                               and self.Breg % 32 == 0 and fused_reg_fits(self.reg_rows[1], V, self.Breg)
                               and os.environ.get('CCREC_REG_FUSED', '1') != '0')
             # decoder operands kept k-contiguous: D3^T (tower fwd), dZ^T (BCE epilogue), Wo^T shadow
@@ -519,7 +520,7 @@ class Trainer:
         for a, buf in enumerate((self.H1, self.H2, self.H3, self.Zl, self.D1, self.D2, self.D3)):
             t.act[a] = buf.data_ptr()
         t.act6t = self.D3t.data_ptr()
-        if self.D3p is not None:
+        if self.D3p is not None and (self.fused_out or self.fused_reg):   # the fused output kernels' operands
             t.act6p, t.act6tp = self.D3p.data_ptr(), self.D3tp.data_ptr()
         if self.gpre1p is not None:
             t.gpre1p = self.gpre1p.data_ptr()

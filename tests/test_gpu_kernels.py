@@ -126,7 +126,12 @@ def test_gather_xt_transpose(V, B, d, sizes, rows):
                xt_rows, L.stream_ptr())
         torch.cuda.synchronize()
         outs.append(out)
-    assert torch.equal(outs[0], outs[1])
+    # bf16 d = 256: without xt the XCD column-sliced gather runs (another fp32 summation order than
+    # the transposing gather2): equal to one bf16 ulp
+    o0, o1 = outs[0].float(), outs[1].float()
+    assert torch.all((o0 - o1).abs() <= o1.abs() * 2 ** -7 + 1e-30)
+    if d != 256:
+        assert torch.equal(outs[0], outs[1])
     assert np.array_equal(xt.cpu().numpy().view(np.uint32), exp)
 
 
@@ -461,7 +466,8 @@ def _nt_gemm(M, N, K, A, lda, Bm, ldb, epi, **kw):
     L.call('cc_gemm', ctypes.byref(g), L.stream_ptr())
 
 
-@pytest.mark.parametrize('B,d,V', [(512, 256, 2500), (128, 128, 700), (256, 256, 64)])
+@pytest.mark.parametrize('B,d,V', [(512, 256, 2500), (128, 128, 700), (256, 256, 64), (512, 512, 2500),
+                                   (128, 512, 700)])
 def test_dec_bce_dw_matches_unfused(B, d, V):
     """cc_dec_bce_dw (logits + BCE + dZ + dWo/dbo in one pass) vs the unfused NT-GEMM path (BCE
     epilogue writing dZ and dZ^T, then dW = D3^T dZ^T with the colsum bias gradient): dZ and dWo
@@ -611,11 +617,12 @@ def test_embed_grad_cs_bit_exact(V, R, d):
 
 
 @pytest.mark.parametrize('M,N,K,splits', [(512, 256, 22000, 32), (640, 128, 1000, 7), (128, 256, 64, 1),
-                                          (256, 256, 5008, 3)])
+                                          (256, 256, 5008, 3), (4096, 256, 3000, 4), (4224, 512, 2008, 3)])
 def test_dx_splitk_glds_matches_nt_gemm(M, N, K, splits):
     """cc_gemm_dx_splitk (LDS-DMA pipeline, dxgemm.hip) == cc_gemm's register-staged NT split-K path:
     the same split boundaries and the same MFMA chain order, so the fp32 partials agree bit for bit;
-    ragged K (a K-tile past the end is zero-filled by the buffer range check) included."""
+    ragged K (a K-tile past the end is zero-filled by the buffer range check) included; M >= 4096
+    with N % 256 == 0 runs the 128 x 256-tile kernel (the full-mode regulariser's dX)."""
     rng = np.random.default_rng(M + K)
     A = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32)).to(torch.bfloat16).cuda()
     Bm = torch.from_numpy(rng.standard_normal((N, K)).astype(np.float32)).to(torch.bfloat16).cuda()

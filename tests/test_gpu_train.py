@@ -53,12 +53,12 @@ def _setup(V, d, B, C, reg, dtype, seed=3, sizes=(20, 40, 80), fused_tower=True,
 @pytest.mark.parametrize('reg', [0.0, 0.1])
 @pytest.mark.parametrize('V,d,B,fused', [(700, 64, 32, True), (2500, 128, 64, True), (2500, 256, 64, True),
                                          (700, 64, 32, False), (2500, 128, 48, True), (2500, 256, 128, True),
-                                         (2500, 128, 128, True)])
+                                         (2500, 128, 128, True), (2500, 512, 128, True)])
 def test_train_steps_match_oracle(dtype, reg, V, d, B, fused):
     C = 4 * B
     tr, lists, Mt, ns, P, perm = _setup(V, d, B, C, reg, dtype, fused_tower=fused)
     assert tr.fused_tower == (fused and B % 32 == 0)
-    if dtype == 'bf16' and B in (128, 256, 512) and d in (128, 256):
+    if dtype == 'bf16' and B in (128, 256, 512) and d in (128, 256, 512):
         # the bench's path: fused D1 output kernel reading Wo, packed tower and D3 images
         assert tr.fused_out and tr.wpack is not None and tr.D3p is not None
     cdf = noise_ref.cdf_of(ns)
@@ -348,7 +348,7 @@ def test_fused_w1_adam_matches_unfused(reg):
     assert out[False][4] == out[True][4]
 
 
-@pytest.mark.parametrize('dtype,V,d,B', [('fp32', 700, 64, 32), ('bf16', 1500, 256, 128)])
+@pytest.mark.parametrize('dtype,V,d,B', [('fp32', 700, 64, 32), ('bf16', 1500, 256, 128), ('bf16', 1500, 512, 128)])
 def test_full_mode_regulariser_matches_oracle(dtype, V, d, B):
     """reg_mode='full' (README.md:27: KL(M~, D2(E(I))) over ALL |V| identity rows every step):
     the rows are static (x row = {card}, reg_idx = card, padded rows masked), their W1 gradient is
@@ -380,13 +380,13 @@ def test_full_mode_regulariser_matches_oracle(dtype, V, d, B):
     tr.check_status()
 
 
-@pytest.mark.parametrize('V,B', [(2500, 128), (3001, 256)])
-def test_fused_regulariser_clip_fix_path(V, B):
+@pytest.mark.parametrize('V,B,d', [(2500, 128, 256), (3001, 256, 256), (2500, 128, 512)])
+def test_fused_regulariser_clip_fix_path(V, B, d):
     """The fused D2 kernels' exact-clip path (csrc/decreg.hip): a decoder_for_reg bias spread
     pushes part of every softmax row below 1e-7, so TF's clip gradient mask matters (S shrinks by
     the excluded target mass) — the main kernel flags it and the fix kernels correct dZ, dWo, dbo.
-    Against the bf16-emulating oracle; a V not a multiple of the 96-column slices included."""
-    d = 256
+    Against the bf16-emulating oracle; a V not a multiple of the 96-column slices included; d = 512
+    runs the 64-column slices."""
     tr, lists, Mt, ns, P, perm = _setup(V, d, B, 4 * B, 0.5, 'bf16')
     assert tr.fused_reg
     rng = np.random.default_rng(V)
