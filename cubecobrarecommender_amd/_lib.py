@@ -58,6 +58,7 @@ class TowerArgs(C.Structure):
         ('wpf', C.c_void_p * 9), ('wpb', C.c_void_p * 9), ('act6p', C.c_void_p), ('act6tp', C.c_void_p),
         ('hpt', C.c_void_p * 6), ('gpt', C.c_void_p * 6), ('gpre1p', C.c_void_p),
         ('x_bits', C.c_void_p), ('xt_bits', C.c_void_p), ('xt_V', C.c_int32), ('xt_rows', C.c_int32),
+        ('d3q', C.c_void_p), ('d3qs', C.c_void_p), ('d3tq', C.c_void_p), ('d3tqs', C.c_void_p),
     ]
 
 

@@ -21,6 +21,8 @@
 // bf16 MFMA v_mfma_f32_32x32x16_bf16 with fp32 accumulation; A operands from the packed D3 images
 // the tower forward writes (cc_tower_args.act6p / act6tp), Wo read in place ([d][V], the slice
 // transposed into LDS).  Deterministic: every sum has a fixed order.
+#include <cstdlib>
+
 #include "common.hpp"
 
 // dev-only timing hook (tools/micro/kl_probe.hip defines it); compiled out of the library
@@ -39,6 +41,7 @@ constexpr int TR = 512;      // rows per tile of the main kernel (2 passes of 8 
 constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
 constexpr float PMIN = 1e-7f;
 constexpr float LN_PMIN = -16.11809565095832f;  // ln(1e-7)
+
 
 typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
 
@@ -345,14 +348,13 @@ struct MainSmem {
 
 // FIX = false: the main pass.  FIX = true: the exact-clip correction (runs only when p.flag is set):
 // c = -scale p delta_row replaces dz; dZ, dWo, dbo are updated in place.
-// PERSIST (the full-mode regulariser: |V| rows in many tiles): the block's dWo slice stays in the
-// waves' accumulators across all row tiles and is stored once at the end — the per-tile
-// read-modify-write of gW (96 KB each way per tile per block, 2 GB per step at |V| = 22,000) was
-// 40 % of the kernel by the phase probe (tools/micro/kl_probe_full.hip).
-template <int D, bool FIX, bool PERSIST = false>
+// (Measured and dropped for the full-mode regulariser: keeping the block's dWo slice in the
+// waves' accumulators across all row tiles instead of the per-tile gW read-modify-write — the
+// 48 extra registers pushed the logits' fragment ring from 16 to 8 and spilled, and the logits
+// phases then waited on L2 twice as long: 1,620 -> 2,015 us per block, tools/micro/kl_probe_full.hip.)
+template <int D, bool FIX>
 __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt, MainSmem<kl_nb<D>()> &sm) {
   constexpr int NB = kl_nb<D>(), NJ = NB / 32;
-  static_assert(!(FIX && PERSIST), "the fix pass adds into gW");
   constexpr int CHB = TR / 8;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
   const int n0 = sl * NB;
@@ -377,15 +379,9 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   const __amdgpu_buffer_rsrc_t dz_rs =
       __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)p.rows * (uint32_t)V * 2u, 0x00020000);
   const float scale = p.scale;
-  // phase 2's d tiles of wave w: 32w .. (and 32(w + 8) .. at d = 512)
-  constexpr int ND2 = (D + 255) / 256;
-  f32x16_t accp[PERSIST ? ND2 : 1][NJ];  // PERSIST: dWo[d tile][NB] over every tile
-#pragma unroll
-  for (int t = 0; t < (PERSIST ? ND2 : 1); ++t)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) accp[t][j][r] = 0.f;
+  const __amdgpu_buffer_rsrc_t gw_rs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)p.gW, (short)0, (uint32_t)D * (uint32_t)V * 4u, 0x00020000);
+  constexpr int ND2 = (D + 255) / 256;   // phase 2's d tiles of wave w: 32w .. (and 32(w + 8) .. at d = 512)
 
   for (int t0 = 0; t0 < p.rows; t0 += TR) {
     const int nt = min(TR, p.rows - t0);
@@ -418,7 +414,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       for (int r = 0; r < 16; ++r) roff[r] = (uint32_t)sm.card[rb + acc_row(r, lane)];
       uint32_t zrow = (uint32_t)((t0 + rb + 4 * half) * V + n0 + (lane & 31));
       asm volatile("" : "+v"(zrow));  // per-pass base of the dZ stores (no hoisted 64-bit addresses)
-      LFrag<D, (PERSIST || D > 256) ? 8 : D / 16> lf;  // all A fragments first in the memory queue, then M~ (PERSIST: a ring of 8 leaves room for the dWo accumulators)
+      LFrag<D, (D / 16 < 16 ? D / 16 : 16)> lf;  // all A fragments first in the memory queue, then M~ (d = 512: a ring of 16)
       logits_load(p, (p.row0 + t0 + rb) / 32, lf);
       float tv[NJ][16];
       if constexpr (!FIX) {
@@ -513,6 +509,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
               *reinterpret_cast<const uint2 *>(&tt[4 * g]);
       }
       deadp |= mn < PMIN;
+
       if constexpr (!FIX) {
         // the exact-clip delta partial of each row over this slice: sum of its targets where
         // p < 1e-7 (rare: zero unless the wave saw such an element); read by the fix kernel
@@ -548,13 +545,31 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
     for (int dt = 0; dt < ND2; ++dt) {
       const int wt = w + 8 * dt;   // this d tile (rows 32 wt .. of dWo)
       if (wt * 32 >= D) break;
-      f32x16_t acc2l[NJ];
-      f32x16_t(&acc2)[NJ] = PERSIST ? accp[PERSIST ? dt : 0] : acc2l;
-      if constexpr (!PERSIST) {
+      f32x16_t acc2[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
+      // the slice's running dWo (all tiles but the first): every load issued before the MFMA
+      // chain, so its MALL/HBM latency runs under it (loaded after the chain in groups of 8, the
+      // read-modify-write was ~10 us of each 38-us row tile in full mode).  Through a buffer
+      // descriptor: columns past V get an offset past the range (load 0, store dropped).
+      const bool first = !FIX && t0 == 0;
+      uint32_t gvo[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int gc = n0 + j * 32 + (lane & 31);
+        gvo[j] = gc < V ? 4u * (uint32_t)((wt * 32 + 4 * half) * V + gc) : 0x80000000u;
+        asm volatile("" : "+v"(gvo[j]));  // opaque per tile: the 48 addresses are not hoisted
+      }
+      float old[NJ][16];
+      if (!first) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
+          for (int r = 0; r < 16; ++r)
+            old[j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                      gw_rs, gvo[j], 4u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), 0));
       }
       // K = the tile's rows (a multiple of 32) in chunks of 32 (two 16-row fragments), a ring of
       // P2 chunks in flight (the loads come from L2: one chunk's 6 MFMAs cannot cover one latency)
@@ -585,49 +600,15 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
           }
         }
       }
-      const bool first = !FIX && t0 == 0;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int gc = n0 + j * 32 + (lane & 31);
-        if (!PERSIST && gc < V) {
-          uint32_t g0 = (uint32_t)((wt * 32 + 4 * half) * V + gc);
-          asm volatile("" : "+v"(g0));  // opaque per tile: keeps 48 row addresses from being hoisted
-          // the tile's 16 partial sums of this column are added to gW with 8 loads in flight at
-          // a time (a load-add-store per element serialised 48 round trips per tile: the
-          // full-mode regulariser walks 43 tiles per slice)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
-          for (int h8 = 0; h8 < 16; h8 += 8) {  // two groups of 8 loads in flight (registers)
-            float old[8];
-            if (!first) {
-#pragma unroll
-              for (int r = 0; r < 8; ++r) old[r] = p.gW[g0 + (uint32_t)((((h8 + r) & 3) + 8 * ((h8 + r) >> 2)) * V)];
-            }
-#pragma unroll
-            for (int r = 0; r < 8; ++r)
-              p.gW[g0 + (uint32_t)((((h8 + r) & 3) + 8 * ((h8 + r) >> 2)) * V)] =
-                  first ? acc2[j][h8 + r] : old[r] + acc2[j][h8 + r];
-          }
-        }
-      }
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(first ? acc2[j][r] : old[j][r] + acc2[j][r]), gw_rs,
+                                                gvo[j], 4u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), 0);
     }
   }
 
-  if constexpr (PERSIST) {  // the slice's dWo, once
-#pragma unroll
-    for (int dt = 0; dt < ND2; ++dt) {
-      const int wt = w + 8 * dt;
-      if (wt * 32 >= D) break;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int gc = n0 + j * 32 + (lane & 31);
-        if (gc < V) {
-          const uint32_t g0 = (uint32_t)((wt * 32 + 4 * half) * V + gc);
-#pragma unroll
-          for (int r = 0; r < 16; ++r) p.gW[g0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V)] = accp[dt][j][r];
-        }
-      }
-    }
-  }
   KL_PROBE(7);
   // ---- epilogue: dbo, loss partial, the fix flag
 #pragma unroll
@@ -686,11 +667,11 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   }
 }
 
-template <int D, bool PERSIST>
+template <int D>
 __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
   __shared__ __attribute__((aligned(16))) bf16_t Wt[kl_nb<D>() * D];
   __shared__ __attribute__((aligned(16))) MainSmem<kl_nb<D>()> sm;
-  kl_slice<D, false, PERSIST>(p, blockIdx.x, Wt, sm);
+  kl_slice<D, false>(p, blockIdx.x, Wt, sm);
 }
 
 // The exact-clip correction: a small persistent grid (FIXG blocks) that leaves at once when the
@@ -791,10 +772,7 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
     CC_LAUNCH_CHECK("kl_stats_kernel");                                                                      \
     hipLaunchKernelGGL(kl_merge_kernel, dim3((unsigned)cdiv(a->rows, 4)), dim3(256), 0, s, p);              \
     CC_LAUNCH_CHECK("kl_merge_kernel");                                                                      \
-    if (a->rows > TR)                                                                                        \
-      hipLaunchKernelGGL((kl_main_kernel<DD, true>), gm, dim3(NTH), 0, s, p);                                \
-    else                                                                                                     \
-      hipLaunchKernelGGL((kl_main_kernel<DD, false>), gm, dim3(NTH), 0, s, p);                               \
+    hipLaunchKernelGGL((kl_main_kernel<DD>), gm, dim3(NTH), 0, s, p);                                       \
     CC_LAUNCH_CHECK("kl_main_kernel");                                                                       \
     hipLaunchKernelGGL((kl_fix_kernel<DD>), dim3(FIXG), dim3(NTH), 0, s, p);                                \
     CC_LAUNCH_CHECK("kl_fix_kernel");                                                                        \

@@ -1128,7 +1128,9 @@ extern "C" int cc_embed_gather_fwd_xt(int32_t dtype, const void *table, const fl
     const char *e = getenv("CCREC_GATHER_XCD");
     return e ? atoi(e) : 44;
   }();
-  if (dtype == CC_BF16 && d == 256 && g2 > 0 && gx > 0 && !xt_bits) {
+  // (tall R — the full-mode regulariser's |V| one-card identity rows — stays on gather2: a block
+  // per 64-column slice of a one-card row is mostly overhead; measured 48 -> 121 us at R = 22,528)
+  if (dtype == CC_BF16 && d == 256 && g2 > 0 && gx > 0 && !xt_bits && R <= 4096) {
     const dim3 gxg((unsigned)(cdiv(R, 2) * 8));
 #define GX(GWN, U) \
   if (gx == GWN * 10 + U) hipLaunchKernelGGL((gather_xcd_kernel<GWN, U>), gxg, dim3(64 * GWN), 0, s, \

@@ -6,30 +6,15 @@
 // Row blocks: one lane per 32-element block (two 16-B stores per lane).  Transposed blocks: a
 // workgroup stages a [32 rows][256 cols] tile in LDS and each lane emits one output row's block.
 #include "common.hpp"
+#include "mx8.hpp"
 
 namespace {
 
 template <typename T>
 __device__ __forceinline__ float ldf(const T *p, int64_t i) { return DT<T>::ld(p + i); }
 
-__device__ __forceinline__ int block_exp(float amax) {
-  if (!(amax > 0.f)) return 0;
-  int x;
-  const float m = frexpf(amax, &x);
-  int e = x - 9 + (m > 0.875f ? 1 : 0);
-  return e < -127 ? -127 : (e > 127 ? 127 : e);
-}
-
-// 32 values -> 32 e4m3 codes (little-endian bytes in w[8]) at scale 2^-e
-__device__ __forceinline__ void encode32(const float *v, int e, uint32_t *w) {
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    int word = 0;
-    word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4 * q], -e), ldexpf(v[4 * q + 1], -e), word, false);
-    word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4 * q + 2], -e), ldexpf(v[4 * q + 3], -e), word, true);
-    w[q] = (uint32_t)word;
-  }
-}
+using cc_mx8::block_exp;
+using cc_mx8::encode32;
 
 // grid (ceil(nb / 64), rows), block 64: lane -> block j of row r; with rowsum (gridDim.x == 1) the
 // wave also sums the row (per-lane ascending partials, then a fixed xor tree: deterministic).

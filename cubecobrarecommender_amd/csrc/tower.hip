@@ -13,6 +13,7 @@
 #include <algorithm>
 
 #include "common.hpp"
+#include "mx8.hpp"
 #include "xt.hpp"
 
 // dev-only timing hook (tools/micro/tower_probe.hip defines it); compiled out of the library
@@ -48,6 +49,7 @@ struct TowerP {
   const uint32_t *xb;       // x row bitmasks -> xt (fast forward's extra blocks; or null)
   uint32_t *xt;
   int xt_V, xt_rows;
+  uint8_t *d3q, *d3qs, *d3tq, *d3tqs;  // D3's MX-FP8 operand images (config 5; wide forward only, or null)
   bool packed, dwpacked;
 };
 
@@ -770,6 +772,48 @@ __global__ __launch_bounds__(FNT) void tower_fwd_wide_kernel(TowerP p) {
     }
   }
   if (p.act6tp) pt_copy_out(xin, ldx, p.act6tp, d, p.R, r0);  // D3^T: the dWo A operand
+  if (p.d3q) {  // config 5: D3's MX-FP8 images (cc_quant_mx8's layout and rule, from the LDS copy)
+    const int nbr = d / 32;
+    for (int t = threadIdx.x; t < RB * nbr; t += FNT) {  // rows image: K = d, block b of row r
+      const int r = t / nbr, b = t % nbr;
+      float v[32];
+      float amax = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const u32v4 u = *reinterpret_cast<const u32v4 *>(xin + r * ldx + 32 * b + 8 * q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[8 * q + 2 * e] = __uint_as_float(u[e] << 16);
+          v[8 * q + 2 * e + 1] = __uint_as_float(u[e] & 0xFFFF0000u);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 32; ++e) amax = fmaxf(amax, fabsf(v[e]));
+      const int ex = cc_mx8::block_exp(amax);
+      uint32_t w[8];
+      cc_mx8::encode32(v, ex, w);
+      uint4 *dst = reinterpret_cast<uint4 *>(p.d3q + (int64_t)(r0 + r) * d + 32 * b);
+      dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+      dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+      p.d3qs[(int64_t)(r0 + r) * nbr + b] = (uint8_t)(ex + 127);
+    }
+    for (int c = threadIdx.x; c < d; c += FNT) {  // transposed image: K = rows, the block's 32 rows
+      float v[32];
+      float amax = 0.f;
+#pragma unroll
+      for (int r = 0; r < 32; ++r) {
+        v[r] = __uint_as_float((uint32_t)reinterpret_cast<const uint16_t *>(xin)[r * ldx + c] << 16);
+        amax = fmaxf(amax, fabsf(v[r]));
+      }
+      const int ex = cc_mx8::block_exp(amax);
+      uint32_t w[8];
+      cc_mx8::encode32(v, ex, w);
+      uint4 *dst = reinterpret_cast<uint4 *>(p.d3tq + (int64_t)c * p.R + r0);
+      dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+      dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+      p.d3tqs[(int64_t)c * (p.R / 32) + r0 / 32] = (uint8_t)(ex + 127);
+    }
+  }
 }
 
 __global__ __launch_bounds__(FNT) void tower_bwd_chain_wide_kernel(TowerP p) {
@@ -1236,6 +1280,14 @@ int make_params(const cc_tower_args *t, TowerP &p) {
   p.xt = static_cast<uint32_t *>(t->xt_bits);
   p.xt_V = t->xt_V;
   p.xt_rows = t->xt_rows;
+  // D3's MX-FP8 images: the wide bf16 chains only (all four pointers, 16-B aligned, R % 32 == 0)
+  p.d3q = static_cast<uint8_t *>(t->d3q);
+  p.d3qs = static_cast<uint8_t *>(t->d3qs);
+  p.d3tq = static_cast<uint8_t *>(t->d3tq);
+  p.d3tqs = static_cast<uint8_t *>(t->d3tqs);
+  if (p.d3q && !(p.d3qs && p.d3tq && p.d3tqs && t->dtype == CC_BF16 && t->d > 256 && t->d % 32 == 0 &&
+                 t->R % 32 == 0 && (((uintptr_t)p.d3q | (uintptr_t)p.d3tq) & 15) == 0))
+    return cc::fail(CC_ERR_ARG, "cc_tower: d3q/d3qs/d3tq/d3tqs need bf16, 256 < d (d % 32 == 0), R % 32 == 0, 16-B aligned codes");
   if ((uintptr_t)p.gpre1p & 15) return cc::fail(CC_ERR_ARG, "cc_tower: gpre1p must be 16-B aligned");
   p.slab = t->slab;
   p.slab_elems = slab_off(t->d, 6);

@@ -353,9 +353,18 @@ class Trainer:
                 self.dZtq = [torch.zeros(V, n, **u8) for n in self.branch_rows()]   # dW B operand (K = rows)
                 self.dZtqs = [torch.zeros(V, n // 32, **u8) for n in self.branch_rows()]
             self.targs = self._tower_args()
+            # config 5 on the wide chains: the tower forward writes D3's MX-FP8 images itself (two
+            # quantiser launches less per step)
+            self.d3q_in_tower = (self.mx8 and d > 256 and self.wpack is not None and R % 32 == 0
+                                 and os.environ.get('CCREC_D3Q_IN_TOWER', '1') != '0')
+            if self.d3q_in_tower:
+                t = self.targs
+                t.d3q, t.d3qs = self.D3q.data_ptr(), self.D3qs.data_ptr()
+                t.d3tq, t.d3tqs = self.D3tq.data_ptr(), self.D3tqs.data_ptr()
             self.transpose_tower()
         else:
             self.targs = None
+            self.d3q_in_tower = False
         if not self.fused_tower:
             self.fused_reg = False
         if self.use_reg and not self.fused_reg:
@@ -724,7 +733,7 @@ class Trainer:
                 self._dense_fwd(self.D1, rows, 128, 256, pre + '/decoded_2', self.D2)
                 self._dense_fwd(self.D2, rows, 256, d, pre + '/decoded_3', self.D3)
         # ---- D1 output + sigmoid + BCE -> dZ (model.py:64,94; train.py:85)
-        if self.mx8:   # MX-FP8 images of D3: rows (forward A) and transposed (dW A, K = rows)
+        if self.mx8 and not self.d3q_in_tower:   # MX-FP8 images of D3: rows (forward A) and transposed (dW A, K = rows)
             L.call('cc_quant_mx8', L.CC_BF16, L.ptr(self.D3), R, d, d, 0, L.ptr(self.D3q), d,
                    L.ptr(self.D3qs), None, s)
             L.call('cc_quant_mx8', L.CC_BF16, L.ptr(self.D3), R, d, d, 1, L.ptr(self.D3tq), R,

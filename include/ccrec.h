@@ -336,8 +336,8 @@ typedef struct cc_tower_args {
    * Used by the fast tower kernels when all of them are set. */
   void *wpf[9];
   void *wpb[9];
-  /* optional (bf16, d <= 256, fast kernels): D3 as fragment-packed MFMA operand images for
-   * cc_dec_bce_dw — act6p: rows = batch rows, reduction d ([R/32][d/16][64][8]); act6tp: rows = d,
+  /* optional (bf16, the fast d <= 256 and wide d <= 1024 kernels): D3 as fragment-packed MFMA
+   * operand images for cc_dec_bce_dw / cc_dec_softmax_kl_dw — act6p: rows = batch rows, reduction d ([R/32][d/16][64][8]); act6tp: rows = d,
    * reduction = batch rows ([d/32][R/16][64][8]).  Same fragment order as wpf. */
   void *act6p;
   void *act6tp;
@@ -357,6 +357,11 @@ typedef struct cc_tower_args {
   const void *x_bits;
   void *xt_bits;
   int32_t xt_V, xt_rows;
+  /* optional (config 5: bf16 towers with MX-FP8 decoder GEMMs, 256 < d, the wide chains): cc_tower_fwd
+   * also writes D3's MX-FP8 operand images exactly as cc_quant_mx8 would from D3 — d3q [R][d] codes
+   * with d3qs [R][d/32] E8M0 scales (K = d), d3tq [d][R] with d3tqs [d][R/32] (K = batch rows) —
+   * from the LDS copy it already holds (all four set, or none). */
+  void *d3q, *d3qs, *d3tq, *d3tqs;
 } cc_tower_args;
 int64_t cc_tower_slab_elems(int32_t d);
 int cc_tower_fwd(const cc_tower_args *t, void *stream);

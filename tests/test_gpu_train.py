@@ -57,7 +57,7 @@ def _setup(V, d, B, C, reg, dtype, seed=3, sizes=(20, 40, 80), fused_tower=True,
 def test_train_steps_match_oracle(dtype, reg, V, d, B, fused):
     C = 4 * B
     tr, lists, Mt, ns, P, perm = _setup(V, d, B, C, reg, dtype, fused_tower=fused)
-    assert tr.fused_tower == (fused and B % 32 == 0)
+    assert tr.fused_tower == (fused and B % 32 == 0 and (dtype == 'bf16' or d <= 256))
     if dtype == 'bf16' and B in (128, 256, 512) and d in (128, 256, 512):
         # the bench's path: fused D1 output kernel reading Wo, packed tower and D3 images
         assert tr.fused_out and tr.wpack is not None and tr.D3p is not None
@@ -258,11 +258,20 @@ def test_fp8_decoder_steps_track_oracle(reg, V, d, B):
     the neighbouring fp8 code, 2^-3 apart)."""
     C = 4 * B
     tr, lists, Mt, ns, P, perm = _setup(V, d, B, C, reg, 'fp8')
-    assert tr.mx8 and tr.fused_tower
+    assert tr.mx8 and tr.fused_tower and tr.d3q_in_tower == (d > 256)
     cdf = noise_ref.cdf_of(ns)
     for step in range(2):
         tr.forward_backward()
         torch.cuda.synchronize()
+        if tr.d3q_in_tower:   # the wide tower forward's D3 MX-FP8 images == cc_quant_mx8 of D3, bit for bit
+            R = tr.R
+            q, qs = torch.empty_like(tr.D3q), torch.empty_like(tr.D3qs)
+            qt, qts = torch.empty_like(tr.D3tq), torch.empty_like(tr.D3tqs)
+            L.call('cc_quant_mx8', L.CC_BF16, L.ptr(tr.D3), R, d, d, 0, L.ptr(q), d, L.ptr(qs), None, L.stream_ptr())
+            L.call('cc_quant_mx8', L.CC_BF16, L.ptr(tr.D3), R, d, d, 1, L.ptr(qt), R, L.ptr(qts), None, L.stream_ptr())
+            torch.cuda.synchronize()
+            assert torch.equal(q, tr.D3q) and torch.equal(qs, tr.D3qs)
+            assert torch.equal(qt, tr.D3tq) and torch.equal(qts, tr.D3tqs)
         xs, ys, reg_idx = tr.batch_lists()
         cubes = [lists[c] for c in perm[step * B:(step + 1) * B]]
         oxs, oys, oreg, _ = noise_ref.philox_noise_batch(cubes, cdf, ns, tr.cfg.seed, step)
