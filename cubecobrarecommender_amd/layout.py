@@ -29,25 +29,51 @@ class Layout:
     align > 1 (data-parallel training, align = world * 64) additionally starts the decoder output
     layer and the decoder_for_reg block on multiples of `align` and pads every block to one, so the
     three gradient buckets (towers + E1 | decoder output layer | decoder_for_reg) split into equal
-    per-rank shards (zero.py).  align == 1 is exactly cc_param_layout."""
+    per-rank shards (zero.py).  align == 1 is exactly cc_param_layout.
 
-    def __init__(self, V, d, align=1):
+    group_biases (data parallel with a bf16 shadow): the kernels keep that order and bucket
+    alignment, and every bias moves into one trailing 'biases' block.  zero.py then all-gathers
+    the kernels' bf16 shadow (half the bytes of the fp32 parameters) and keeps the fp32 biases —
+    which the kernels read in fp32 — exact on every rank by all-reducing their gradients and
+    running their Adam on every rank."""
+
+    def __init__(self, V, d, align=1, group_biases=False):
         self.V, self.d, self.align = int(V), int(d), int(align)
+        self.group_biases = bool(group_biases)
         self.entries = {}
         o = 0
-        for li, (fi, fo) in enumerate(layer_shapes(V, d)):
+        shapes = layer_shapes(V, d)
+        for li, (fi, fo) in enumerate(shapes):
             if li in (7, 8):
                 o = _round_up(o, self.align)
-            for name, shape in ((LAYERS[li] + '/kernel', (fi, fo)), (LAYERS[li] + '/bias', (fo,))):
+            parts = ((LAYERS[li] + '/kernel', (fi, fo)),) if self.group_biases else \
+                ((LAYERS[li] + '/kernel', (fi, fo)), (LAYERS[li] + '/bias', (fo,)))
+            for name, shape in parts:
                 self.entries[name] = (o, shape)
                 o += (int(np.prod(shape)) + 63) // 64 * 64
             if li == 7:
                 o = _round_up(o, self.align)
                 self.main_total = o
+        if self.group_biases:
+            o = _round_up(o, self.align)
+            self.bias_lo = o
+            for li, (fi, fo) in enumerate(shapes):
+                self.entries[LAYERS[li] + '/bias'] = (o, (fo,))
+                o += (fo + 63) // 64 * 64
+            self.main_total = _round_up(o, self.align)   # (the main model is no longer a prefix)
         self.total = _round_up(o, self.align)
 
     def buckets(self, with_reg):
         """Gradient buckets in the order backward produces them: (name, lo, hi)."""
+        if self.group_biases:
+            reg_lo = self.offset('decoder_for_reg/decoded_1/kernel')
+            reg_lo = reg_lo - reg_lo % self.align if reg_lo % self.align else reg_lo
+            out = [('decoder_output', self.offset('decoder/reconstruct/kernel'), reg_lo),
+                   ('towers_e1', 0, self.offset('decoder/reconstruct/kernel'))]
+            if with_reg:
+                out.append(('decoder_for_reg', reg_lo, self.bias_lo))
+            out.append(('biases', self.bias_lo, self.total))
+            return out
         out = [('decoder_output', self.offset('decoder/reconstruct/kernel'), self.main_total),
                ('towers_e1', 0, self.offset('decoder/reconstruct/kernel'))]
         if with_reg:

@@ -179,7 +179,9 @@ class Trainer:
         self.dev = torch.device(device)
         # data-parallel: gradient buckets aligned to world*64 so every rank owns an equal shard
         self.std_layout = Layout(V, d)
-        self.layout = Layout(V, d, align=cfg.world * 64) if cfg.world > 1 else self.std_layout
+        # (with a bf16 shadow the biases are grouped so zero.py all-gathers the kernels' bf16 shadow)
+        self.layout = (Layout(V, d, align=cfg.world * 64, group_biases=cfg.dtype in ('bf16', 'fp8'))
+                       if cfg.world > 1 else self.std_layout)
         self.use_reg = cfg.reg > 0
         if self.use_reg and data.y_reg is None:
             raise ValueError('reg > 0 needs the M~ matrix on the device')

@@ -14,8 +14,15 @@ HBM traffic world times over.  Here (ZeRO-1):
   * every rank runs TF Adam (cc_adam_dense) on its 1/world shard only and all-gathers the
     updated fp32 parameters in place; the bf16 operand shadow is refreshed locally.
 
-Every rank ends the step with identical parameters; m and v are only kept current on the owning
-rank's shard (the checkpoint writer gathers them, model.py).  Every backend runs the same two
+With a bf16 operand shadow (the bf16 / fp8 paths) and the grouped-bias layout (Layout(group_biases=
+True)), the kernels' parameters are all-gathered as the bf16 shadow the Adam launch wrote for the
+shard — half the bytes of the fp32 values, and exactly what every kernel reads — while the fp32
+biases (read in fp32 by the kernels) stay exact everywhere: their one small bucket is all-reduced
+and every rank runs its Adam.  The fp32 master values of the other ranks' kernel shards are then
+only brought in by gather_state() (checkpoints, tests).
+
+Every rank ends the step with identical operands (shadow and biases); m and v are only kept current
+on the owning rank's shard (the checkpoint writer gathers them, model.py).  Every backend runs the same two
 collectives RCCL runs (reduce_scatter_tensor, in-place all_gather_into_tensor): gloo takes them on
 CPU tensors, so with gloo and device buffers (several ranks rehearsed on one GPU) each bucket is
 staged through a host copy around the identical call.
@@ -41,6 +48,12 @@ class ShardedStep:
             self.buckets.append({
                 'name': name, 'lo': lo, 'hi': hi, 'chunk': chunk, 's0': lo + self.rank * chunk,
                 'gshard': torch.zeros(chunk, device=trainer.params.device, dtype=torch.float32)})
+        # bf16 shadow + grouped biases: gather the shadow, all-reduce the biases (module docstring)
+        self.shadow_gather = (getattr(trainer, 'shadow', None) is not None
+                              and getattr(trainer.layout, 'group_biases', False))
+        if self.shadow_gather:
+            bb = self.bucket('biases')
+            bb['gfull'] = torch.zeros(bb['hi'] - bb['lo'], device=trainer.params.device, dtype=torch.float32)
         self.comm = torch.cuda.Stream(device=trainer.params.device) if trainer.params.is_cuda else None
         self.adam_events = []          # (e0, e1, n) around each shard's Adam when timing
 
@@ -63,40 +76,70 @@ class ShardedStep:
         off = b['s0'] - b['lo']
         if self.stage:
             host = full.cpu()
+            if host.dtype == torch.bfloat16:   # gloo reduces/gathers no bf16: move the bits as int16
+                host = host.view(torch.int16)
             dist.all_gather_into_tensor(host, host[off:off + b['chunk']], group=self.group)
-            full.copy_(host)
+            full.copy_(host.view(full.dtype))
         else:           # in place: my shard already sits at rank * chunk inside the output
             dist.all_gather_into_tensor(full, full[off:off + b['chunk']], group=self.group)
 
+    def all_reduce_mean(self, b, grads):
+        """The biases bucket: the full mean gradient on every rank (b['gfull'])."""
+        src = grads[b['lo']:b['hi']]
+        if self.stage:
+            host = src.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group)
+            b['gfull'].copy_(host)
+        else:
+            b['gfull'].copy_(src)
+            dist.all_reduce(b['gfull'], op=dist.ReduceOp.SUM, group=self.group)
+        b['gfull'].mul_(1.0 / self.world)
+
     def update(self, b, adam_fn, timing=False):
-        """Reduce-scatter bucket b, Adam on this rank's shard, all-gather the parameters."""
-        self.reduce_scatter(b, self.tr.grads)
+        """Reduce-scatter bucket b, Adam on this rank's shard, all-gather the parameters (the
+        bf16 shadow in shadow_gather mode); the biases bucket: all-reduce, Adam on every rank."""
+        full = self.shadow_gather and b['name'] == 'biases'
+        if full:
+            self.all_reduce_mean(b, self.tr.grads)
+        else:
+            self.reduce_scatter(b, self.tr.grads)
         if timing:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        adam_fn(b['s0'], b['chunk'], b['gshard'])
+        if full:
+            adam_fn(b['lo'], b['hi'] - b['lo'], b['gfull'])
+        else:
+            adam_fn(b['s0'], b['chunk'], b['gshard'])
         if timing:
             e1.record()
-            self.adam_events.append((e0, e1, b['chunk']))
-        self.all_gather(b, self.tr.params)
+            self.adam_events.append((e0, e1, b['hi'] - b['lo'] if full else b['chunk']))
+        if full:
+            return
+        self.all_gather(b, self.tr.shadow if self.shadow_gather else self.tr.params)
 
     def gather_state(self):
-        """Make m and v complete on every rank (checkpointing): all-gather each bucket's shards."""
+        """Make m and v (and, in shadow_gather mode, the fp32 kernel parameters) complete on every
+        rank (checkpointing): all-gather each sharded bucket."""
         for b in self.buckets:
+            if self.shadow_gather and b['name'] == 'biases':
+                continue      # replicated
             self.all_gather(b, self.tr.m)
             self.all_gather(b, self.tr.v)
+            if self.shadow_gather:
+                self.all_gather(b, self.tr.params)
 
     # ------------------------------------------------------------------ one training step
     def step(self, phase_a, phase_b, rest, adam_fn, refresh_fn, timing=False):
         """phase_a / phase_b: the two halves of forward_backward (graph replays or eager);
         rest: counters + transposed operand copies; adam_fn(lo, n, g) / refresh_fn(lo, hi)."""
         first, later = self.buckets[0], self.buckets[1:]
+        refresh = (lambda lo, hi: None) if self.shadow_gather else refresh_fn   # (shadow gathered)
         if self.comm is None:          # CPU (gloo tests): no streams
             phase_a()
             phase_b()
             for b in self.buckets:
                 self.update(b, adam_fn)
-                refresh_fn(b['lo'], b['hi'])
+                refresh(b['lo'], b['hi'])
             rest()
             return
         main = torch.cuda.current_stream()
@@ -106,7 +149,7 @@ class ShardedStep:
         with torch.cuda.stream(self.comm):
             self.comm.wait_event(ev)
             self.update(first, adam_fn, timing)
-            refresh_fn(first['lo'], first['hi'])
+            refresh(first['lo'], first['hi'])
         phase_b()
         ev2 = torch.cuda.Event()
         ev2.record(main)
@@ -114,6 +157,6 @@ class ShardedStep:
             self.comm.wait_event(ev2)
             for b in later:
                 self.update(b, adam_fn, timing)
-                refresh_fn(b['lo'], b['hi'])
+                refresh(b['lo'], b['hi'])
         main.wait_stream(self.comm)
         rest()

@@ -51,11 +51,11 @@ def _adam(p, m, v, g, t, lr=1e-3, b1=0.9, b2=0.999, eps=1e-7):
 
 
 class _FakeTrainer:
-    def __init__(self, world, rank, with_reg):
+    def __init__(self, world, rank, with_reg, shadow=False):
         from types import SimpleNamespace
         from cubecobrarecommender_amd.layout import Layout
         self.cfg = SimpleNamespace(world=world, rank=rank)
-        self.layout = Layout(300, 64, align=world * 64)
+        self.layout = Layout(300, 64, align=world * 64, group_biases=shadow)
         self.use_reg = with_reg
         n = self.layout.total
         gen = torch.Generator().manual_seed(7)
@@ -63,44 +63,58 @@ class _FakeTrainer:
         self.m = torch.zeros(n)
         self.v = torch.zeros(n)
         self.grads = torch.randn(n, generator=torch.Generator().manual_seed(100 + rank))
+        self.shadow = self.params.to(torch.bfloat16) if shadow else None
 
 
-def _zero_worker(rank, world, port, q):
+def _zero_worker(rank, world, port, q, shadow=False):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from cubecobrarecommender_amd import distributed as D
     from cubecobrarecommender_amd.zero import ShardedStep
     D.init(backend='gloo')
-    tr = _FakeTrainer(world, rank, with_reg=True)
+    tr = _FakeTrainer(world, rank, with_reg=True, shadow=shadow)
     zs = ShardedStep(tr)
+    assert zs.shadow_gather == shadow
     for t in (1, 2):
         def adam_fn(lo, n, g, t=t):
             _adam(tr.params[lo:lo + n], tr.m[lo:lo + n], tr.v[lo:lo + n], g, t)
+            if tr.shadow is not None:     # cc_adam_dense writes the bf16 shadow of its range
+                tr.shadow[lo:lo + n] = tr.params[lo:lo + n].to(torch.bfloat16)
         zs.step(lambda: None, lambda: None, lambda: None, adam_fn, lambda lo, hi: None)
+    sh = tr.shadow.float().numpy().copy() if shadow else None
+    bias = tr.params[tr.layout.bias_lo:].numpy().copy() if shadow else None
     zs.gather_state()
-    q.put((rank, tr.params.numpy().copy(), tr.m.numpy().copy(), tr.v.numpy().copy()))
+    q.put((rank, tr.params.numpy().copy(), tr.m.numpy().copy(), tr.v.numpy().copy(), sh, bias))
     D.finish()
 
 
-def test_gloo_world2_sharded_adam_equals_allreduce_adam():
+@pytest.mark.parametrize('shadow', [False, True])
+def test_gloo_world2_sharded_adam_equals_allreduce_adam(shadow):
     """ZeRO-1 step (bucketed reduce-scatter, Adam on the rank's shard, all-gather; zero.py)
-    leaves every rank with exactly the parameters of a full Adam on the averaged gradient."""
+    leaves every rank with exactly the parameters of a full Adam on the averaged gradient.
+    shadow: the bf16 path's grouped-bias layout — the kernels' bf16 shadow is all-gathered and the
+    biases bucket all-reduced (Adam on every rank): after the steps every rank holds the exact
+    shadow and fp32 biases, and gather_state() completes the fp32 kernels, m and v."""
     world = 2
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    port = 29500 + (os.getpid() + 7) % 1000
-    ps = [ctx.Process(target=_zero_worker, args=(r, world, port, q)) for r in range(world)]
+    port = 29500 + (os.getpid() + 7 + 11 * shadow) % 1000
+    ps = [ctx.Process(target=_zero_worker, args=(r, world, port, q, shadow)) for r in range(world)]
     for p in ps:
         p.start()
-    res = {r: (pp, mm, vv) for r, pp, mm, vv in [q.get(timeout=120) for _ in ps]}
+    res = {r: rest for r, *rest in [q.get(timeout=120) for _ in ps]}
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
-    ref = _FakeTrainer(world, 0, with_reg=True)
-    g = sum(_FakeTrainer(world, r, True).grads for r in range(world)) * (1.0 / world)
+    ref = _FakeTrainer(world, 0, with_reg=True, shadow=shadow)
+    g = sum(_FakeTrainer(world, r, True, shadow=shadow).grads for r in range(world)) * (1.0 / world)
     for t in (1, 2):
         _adam(ref.params, ref.m, ref.v, g, t)
     for r in range(world):
-        np.testing.assert_array_equal(res[r][0], ref.params.numpy())
-        np.testing.assert_array_equal(res[r][1], ref.m.numpy())
-        np.testing.assert_array_equal(res[r][2], ref.v.numpy())
+        pp, mm, vv, sh, bias = res[r]
+        np.testing.assert_array_equal(pp, ref.params.numpy())
+        np.testing.assert_array_equal(mm, ref.m.numpy())
+        np.testing.assert_array_equal(vv, ref.v.numpy())
+        if shadow:
+            np.testing.assert_array_equal(sh, ref.params.to(torch.bfloat16).float().numpy())
+            np.testing.assert_array_equal(bias, ref.params[ref.layout.bias_lo:].numpy())
