@@ -103,8 +103,6 @@ def roofline_for(name, ms, tr):
         if getattr(tr, 'fuse_w1', False):     # W1's Adam runs in its gradient kernel
             n -= tr.w1_off
         byt = n * (16 + 12 + 2)                    # read p,m,v,g; write p,m,v; write bf16 shadow
-        if getattr(tr, 'fused_adam', False):      # + the transposed bf16 operand copies
-            byt += 2 * sum(int(r.rows) * int(r.cols) for r in tr.adam_regions)
         return {'bound': 'hbm', 'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s', 'bytes_per_launch': byt}
     if name in ('dec_bce_fwd', 'dec_dW', 'dec_dX'):
@@ -415,8 +413,6 @@ def main():
     elif world == 1 and getattr(tr, 'prefetch', False):
         roof['kernel'] = ('adam_noise_kernel (cc_adam_noise: TF Adam over all parameters + F of the '
                           'next step in the same launch; bytes counted are Adam\'s only, F adds <2%)')
-    elif world == 1 and getattr(tr, 'fused_adam', False):
-        roof['kernel'] = 'adam_fused_kernel (cc_adam_dense_t)'
     else:
         roof['kernel'] = 'adam_kernel (cc_adam_dense)'
     roof['avg_ms'] = adam_ms

@@ -283,14 +283,13 @@ class Trainer:
         self.fused_tower = cfg.fused_tower and (B % 32 == 0) and d <= (1024 if self.dtype == L.CC_BF16 else 256)
         # bf16 path: the W1 gradient on MFMA (cc_embed_grad_mfma) from dPre1^T bf16 [d][RP]
         # written by the tower backward chain (columns R..RP-1 stay zero)
-        self.embed_mfma = (self.dtype == L.CC_BF16 and self.fused_tower and d % 128 == 0 and self.xt_rows <= 2048
-                           and os.environ.get('CCREC_EMBED_MFMA', '1') != '0')
+        self.embed_mfma = self.dtype == L.CC_BF16 and self.fused_tower and d % 128 == 0 and self.xt_rows <= 2048
         self.RP = (R + 63) // 64 * 64
-        # decoder dX on the LDS-DMA pipelined split-K kernel (dxgemm.hip; CCREC_DX_GLDS=0: gemm.hip's)
-        self.dx_glds = self.dtype == L.CC_BF16 and os.environ.get('CCREC_DX_GLDS', '1') != '0'
+        # decoder dX on the LDS-DMA pipelined split-K kernel (dxgemm.hip; other dtypes: gemm.hip's)
+        self.dx_glds = self.dtype == L.CC_BF16
         # D1 output layer fused (logits + BCE + dZ + dWo, csrc/decout.hip) where its shape fits
         self.fused_out = (self.dtype == L.CC_BF16 and self.fused_tower and not self.mx8 and d in (128, 256, 512)
-                          and B in (128, 256, 512) and os.environ.get('CCREC_DEC_FUSED', '1') != '0')
+                          and B in (128, 256, 512))
         self.gPre1T = torch.zeros(d, self.RP, **T) if self.embed_mfma else None
         if self.mx8 and not self.fused_tower:
             raise ValueError('fp8 needs the fused towers (fused_tower=True, B % 32 == 0)')
@@ -306,8 +305,7 @@ class Trainer:
             # fragment-packed forward/backward weight images for the bf16 tower kernels (d <= 256:
             # fast, 256 < d <= 1024: wide; written with wt by cc_tower_transpose and by the Adam
             # launch; the opt-in fused Adam writes only wt)
-            pack = (self.dtype == L.CC_BF16 and d <= 1024 and os.environ.get('CCREC_FUSED_ADAM', '0') != '1'
-                    and os.environ.get('CCREC_TOWER_PACK', '1') != '0')
+            pack = self.dtype == L.CC_BF16 and d <= 1024
             self.wpack = torch.zeros(2, int(self.wt_off[-1]), **T) if pack else None
             # ... and D3 as packed operand images of the fused D1 output kernel (cc_dec_bce_dw)
             self.D3p = torch.zeros(R * d, **T) if pack else None
@@ -318,13 +316,13 @@ class Trainer:
             self.gpt = [torch.zeros(R * w, **T) for w in (256, 128, 64, 128, 256, d)] if pack else None
             # dPre1 as packed transposed fragments (the W1 gradient's B operand; rows past R zero)
             self.gpre1p = (torch.zeros(d * self.RP, **T) if pack and self.embed_mfma and d == 256
-                           and os.environ.get('CCREC_EG_PACKED', '1') != '0' else None)
-            # the W1 gradient by column slices (cc_embed_grad_cs; CCREC_EG_CS=0: the row-tile kernels):
+                           else None)
+            # the W1 gradient by column slices (cc_embed_grad_cs; without the MFMA operands: the row kernels):
             # one zeroed ticket per row chunk, left zero by every call
             self.eg_tickets = (torch.zeros(max(1, int(L.lib().cc_embed_grad_cs_tickets(V, d, self.xt_rows))),
                                            device=self.dev, dtype=torch.int32)
                                if (self.gpre1p is not None or self.embed_mfma)
-                               and os.environ.get('CCREC_EG_CS', '1') != '0' else None)
+                               else None)
             slab = int(L.lib().cc_tower_slab_elems(d))
             self.slab = torch.zeros((R // 32) * slab, **f32)
             # D2 output layer fused (logits twice -> softmax -> KL -> dZ -> dWo, csrc/decreg.hip): bf16,
@@ -332,8 +330,7 @@ class Trainer:
             # (its buffer descriptors address M~ up to row hi and the Breg x V bf16 dZ with 32-bit
             # extents: larger card pools fall back to the Z2 path instead of failing)
             self.fused_reg = (self.use_reg and self.D3p is not None and not self.mx8 and d in (128, 256, 512)
-                              and self.Breg % 32 == 0 and fused_reg_fits(self.reg_rows[1], V, self.Breg)
-                              and os.environ.get('CCREC_REG_FUSED', '1') != '0')
+                              and self.Breg % 32 == 0 and fused_reg_fits(self.reg_rows[1], V, self.Breg))
             # decoder operands kept k-contiguous: D3^T (tower fwd), dZ^T (BCE epilogue), Wo^T shadow
             self.D3t = torch.zeros(d, R, **T)
             self.dZt = [torch.zeros(V, n, **T) if not (k == 1 and self.fused_reg) else None
@@ -357,8 +354,7 @@ class Trainer:
             self.targs = self._tower_args()
             # config 5 on the wide chains: the tower forward writes D3's MX-FP8 images itself (two
             # quantiser launches less per step)
-            self.d3q_in_tower = (self.mx8 and d > 256 and self.wpack is not None and R % 32 == 0
-                                 and os.environ.get('CCREC_D3Q_IN_TOWER', '1') != '0')
+            self.d3q_in_tower = self.mx8 and d > 256 and self.wpack is not None and R % 32 == 0
             if self.d3q_in_tower:
                 t = self.targs
                 t.d3q, t.d3qs = self.D3q.data_ptr(), self.D3qs.data_ptr()
@@ -380,49 +376,36 @@ class Trainer:
                                        dtype=torch.float64)
         if self.full_reg:
             self._init_full_rows()
-        # one process: Adam also writes the transposed operand copies and advances the step
-        # counters (cc_adam_dense_t), so a step is two launches of graphs: fwd/bwd | Adam
-        # (measured: in the step the fused kernel ran 77 us against 56 + 8 + 4 + 5 for Adam,
-        # Wo^T, tower W^T and the counters — its 64x64 tiles read Wo with poor DRAM locality —
-        # so it is opt-in: CCREC_FUSED_ADAM=1)
-        self.fused_adam = (self.fused_tower and cfg.world == 1 and self.dtype == L.CC_BF16 and not self.mx8
-                           and os.environ.get('CCREC_FUSED_ADAM', '0') == '1')
-        self.adam_regions = self._adam_regions() if self.fused_adam else None
         # F for the next step in the Adam launch (cc_adam_noise): Adam is HBM-bound, F latency-
         # bound; F then leaves the forward's critical path.  noise_ready: the batch buffers
         # already hold the batch the next forward_backward consumes.
-        self.prefetch = (cfg.prefetch_noise and cfg.world == 1 and not self.fused_adam
-                         and os.environ.get('CCREC_PREFETCH_NOISE', '1') != '0')
+        self.prefetch = cfg.prefetch_noise and cfg.world == 1
         # one process: F (in the Adam launch) writes its x rows as bitmasks and the next E1 gather
         # launch bit-transposes them into the W1-gradient bitmask (cc_embed_gather_fwd_xt) — F's
         # scattered xt atomics queued behind the Adam streams (measured: the Adam + F launch
         # 40.5 -> 36.9 us without them; the same atomics in the gather cost it 13 us)
-        self.xt_in_gather = (self.prefetch and self.dtype == L.CC_BF16
-                             and os.environ.get('CCREC_XT_IN_GATHER', '1') != '0')
+        self.xt_in_gather = self.prefetch and self.dtype == L.CC_BF16
         # (F's x rows as bitmasks [R][ceil(V/32)]; rows F does not draw stay zero)
         self.x_bits = (torch.zeros(self.R, (cfg.V + 31) // 32, device=self.dev, dtype=torch.int32)
                        if self.xt_in_gather else None)
         # ... in the tower forward launch instead when its fast kernel runs (d <= 256): its 16-32
         # chain blocks leave the other CUs idle (measured: in the gather launch the transpose
         # blocks cost it 2-3 us)
-        self.xt_in_tower = (self.xt_in_gather and self.targs is not None and cfg.d <= 256
-                            and os.environ.get('CCREC_XT_IN_TOWER', '1') != '0')
+        self.xt_in_tower = self.xt_in_gather and self.targs is not None and cfg.d <= 256
         if self.xt_in_tower:
             self.targs.x_bits, self.targs.xt_bits = self.x_bits.data_ptr(), self.xt_bits.data_ptr()
             self.targs.xt_V, self.targs.xt_rows = cfg.V, self.xt_rows
         # one process, packed tower images: the Adam + F launch also rewrites the tower kernels'
         # packed images and advances the step counters (cc_adam_noise_pack) — the next step
         # starts without a counters/transposes launch
-        self.adam_packs = (self.prefetch and self.wpack is not None
-                           and os.environ.get('CCREC_ADAM_PACK', '1') != '0')
+        self.adam_packs = self.prefetch and self.wpack is not None
         # TF Adam on W1 in the W1-gradient kernel's epilogue (cc_embed_grad_cs_adam): the main Adam
         # launch then starts after W1 (W1 is the first tensor of the layout).  One process only
         # (DP reduces the gradient first), the column-slice kernel, not the full-mode regulariser
         # (its identity rows add to the W1 gradient after that kernel).
         self.w1_off = self.layout.offset('encoder/encoded_1/bias')   # = W1's padded size
         self.fuse_w1 = (cfg.fuse_w1_adam and self.adam_packs and self.eg_tickets is not None and not self.full_reg
-                        and self.layout.offset('encoder/encoded_1/kernel') == 0
-                        and os.environ.get('CCREC_FUSE_W1_ADAM', '1') != '0')
+                        and self.layout.offset('encoder/encoded_1/kernel') == 0)
         self.adam_pack = self._adam_pack_desc() if self.adam_packs else None
         self._adv_deferred = False   # the previous step's counter advance rides in the E1 gather
         self.noise_ready = False
@@ -432,7 +415,9 @@ class Trainer:
         self.pending_rest = False    # one process: step k's counters/transposes run at the head
         #                              of step k+1's forward graph (one graph launch less per step)
         self.side = torch.cuda.Stream(device=self.dev)   # dW / slab reduce / losses / transposes
-        self.overlap = os.environ.get('CCREC_OVERLAP', '0') == '1'   # measured slower (graph branches), off
+        # the side-stream work (output-layer dW, slab reduces) as graph branches: measured slower than
+        # keeping it on the one stream, so _fork / _join only mark where it could branch
+        self.overlap = False
         self.timing = False          # bench.py: HIP events around the main kernels
         self.events = {}
 
@@ -535,7 +520,7 @@ class Trainer:
             t.act6p, t.act6tp = self.D3p.data_ptr(), self.D3tp.data_ptr()
         if self.gpre1p is not None:
             t.gpre1p = self.gpre1p.data_ptr()
-        if getattr(self, 'hpt', None) is not None and os.environ.get('CCREC_DW_PACKED', '1') != '0':
+        if getattr(self, 'hpt', None) is not None:
             for a in range(6):
                 t.hpt[a], t.gpt[a] = self.hpt[a].data_ptr(), self.gpt[a].data_ptr()
         t.gD3 = self.gD3.data_ptr()
@@ -557,33 +542,14 @@ class Trainer:
             pk.wpb[l] = self.wpack[1, int(self.wt_off[l]):].data_ptr()
         return pk
 
-    def _adam_regions(self):
-        """Row-major weights whose bf16 values the forward reads transposed: the six (nine)
-        tower kernels -> wt, the output layers' kernels -> Wo^T; sorted by flat offset."""
-        n = self.layout.total if self.use_reg else self.layout.main_total
-        regs = []
-        for l, name in enumerate(self.tower_layers):
-            off = self.layout.offset(name + '/kernel')
-            K, N = self.layout.shape(name + '/kernel')
-            if off + K * N <= n:
-                regs.append((off, K, N, self.wt[int(self.wt_off[l]):].data_ptr()))
-        for k, pre in enumerate(branches_of(self.use_reg)):
-            off = self.layout.offset(pre + '/reconstruct/kernel')
-            regs.append((off, self.cfg.d, self.cfg.V, self.WoT[k].data_ptr()))
-        regs.sort()
-        arr = (L.AdamTRegion * len(regs))()
-        for i, (off, r, c, dst) in enumerate(regs):
-            arr[i].off, arr[i].rows, arr[i].cols, arr[i].dst = off, r, c, dst
-        return arr
-
     def refresh_decoder_operands(self, s):
         """Decoder output-layer operands from the current (bf16 shadow) weights Wo [d][V]: Wo^T
         (bf16), or with fp8 the MX-FP8 images Wo^T [V][d] (forward) and Wo [d][Vp] (dX)."""
         d, V = self.cfg.d, self.cfg.V
         for k, pre in enumerate(branches_of(self.use_reg)):
-            if k == 0 and self.fused_out and not getattr(self, "fused_adam", False):
+            if k == 0 and self.fused_out:
                 continue    # cc_dec_bce_dw reads Wo itself: no Wo^T copy for the D1 branch
-            if k == 1 and self.fused_reg and not getattr(self, "fused_adam", False):
+            if k == 1 and self.fused_reg:
                 continue    # cc_dec_softmax_kl_dw reads Wo itself
             if self.mx8:
                 L.call('cc_quant_mx8', L.CC_BF16, self.w(pre + '/reconstruct/kernel'), d, V, V, 1,
@@ -906,7 +872,7 @@ class Trainer:
             ss = self._fork()      # per-block dW slabs + their reduce overlap the E1 scatter
             # direct dW: from the packed images (any row count) or LDS-staged (rows <= ~1184)
             direct = self.hpt is not None or max(R, cfg.batch_size) <= 1184
-            if self.dtype == L.CC_BF16 and direct and os.environ.get('CCREC_TOWER_DW_DIRECT', '1') != '0':
+            if self.dtype == L.CC_BF16 and direct:
                 L.call('cc_tower_bwd_dw_direct', L.C.byref(self.targs), ss)
             else:
                 L.call('cc_tower_bwd_dw', L.C.byref(self.targs), ss)
@@ -968,11 +934,6 @@ class Trainer:
                        L.ptr(self.grads), L.ptr(self.shadow), n, cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,
                        L.C.byref(na), self.batches_per_epoch, L.stream_ptr(stream))
             self.noise_ready = True
-        elif self.fused_adam:   # + transposed operand copies + step counters
-            L.call('cc_adam_dense_t', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v),
-                   L.ptr(self.grads), L.ptr(self.shadow), n, L.ptr(self.state), cfg.lr, cfg.beta1,
-                   cfg.beta2, cfg.eps, self.adam_regions, len(self.adam_regions),
-                   self.batches_per_epoch, L.stream_ptr(stream))
         else:
             L.call('cc_adam_dense', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v), L.ptr(self.grads),
                    L.ptr(self.shadow), n, L.ptr(self.state), cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,
@@ -981,10 +942,7 @@ class Trainer:
 
     def apply_rest(self, stream=None, defer=False):
         """Advance the device step/epoch counters and refresh the transposed operand copies
-        (the decoder's Wo^T on the side stream, concurrently).  With the fused Adam both are
-        already done."""
-        if self.fused_adam:
-            return
+        (the decoder's Wo^T on the side stream, concurrently)."""
         if self.adam_packs:   # packed tower images already written by the Adam launch
             self.refresh_decoder_operands(L.stream_ptr(stream))
             if defer:         # counters: in the next forward's E1 gather launch
@@ -1069,7 +1027,7 @@ class Trainer:
             self.graphs[1].replay()
         else:
             self.apply_adam(stream)
-        self.pending_rest = not self.fused_adam
+        self.pending_rest = True
 
     def step(self, stream=None):
         if self.cfg.world > 1:
@@ -1119,22 +1077,19 @@ class Trainer:
             with torch.cuda.graph(g_adam):     # (with prefetch: + the next step's F)
                 self.apply_adam()
         g_main = g_all = None
-        if self.fused_adam:
-            g_rest = None
-        else:
-            with torch.cuda.graph(g_rest):
-                self.apply_rest()
-            if self.cfg.world == 1:   # rest of step k + forward/backward of step k+1 (+ its Adam)
-                g_main, g_all = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                self.noise_ready = self.prefetch   # F already drawn by step k's Adam launch
-                with torch.cuda.graph(g_main):
-                    self.apply_rest(defer=True)
-                    self.forward_backward()
-                self.noise_ready = self.prefetch
-                with torch.cuda.graph(g_all):
-                    self.apply_rest(defer=True)
-                    self.forward_backward()
-                    self.apply_adam()
+        with torch.cuda.graph(g_rest):
+            self.apply_rest()
+        if self.cfg.world == 1:   # rest of step k + forward/backward of step k+1 (+ its Adam)
+            g_main, g_all = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            self.noise_ready = self.prefetch   # F already drawn by step k's Adam launch
+            with torch.cuda.graph(g_main):
+                self.apply_rest(defer=True)
+                self.forward_backward()
+            self.noise_ready = self.prefetch
+            with torch.cuda.graph(g_all):
+                self.apply_rest(defer=True)
+                self.forward_backward()
+                self.apply_adam()
         torch.cuda.synchronize()
         self.state.copy_(saved)
         self.noise_ready = False
