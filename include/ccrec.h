@@ -388,8 +388,8 @@ int cc_tower_transpose_advance(const cc_tower_args *t, int64_t *state, int64_t b
 int cc_dec_bce_fused(int32_t dtype, const void *H3, const void *Wo, const float *bo,
                      int32_t B, int32_t d, int32_t V, const uint32_t *y_bits, void *dZ,
                      double *loss_partials, int32_t *n_partials, void *stream);
-/* D1 output layer in one pass (bf16; B in {128, 256, 512}, d in {128, 256}): per 96-column
- * slice of V, logits z = D3 Wo + bo (Wo as Wo^T [V][d]; with WoT NULL the [d][V] weights Wo
+/* D1 output layer in one pass (bf16; B in {128, 256, 512}, d in {128, 256, 512}): per
+ * 96-column (d = 512: 64-column) slice of V, logits z = D3 Wo + bo (Wo as Wo^T [V][d]; with WoT NULL the [d][V] weights Wo
  * themselves, each block transposing its slice in LDS — no Wo^T copy to refresh after Adam;
  * D3p / D3tp: optional packed operand images, cc_tower_args.act6p / act6tp), dZ = (sigmoid(z) - y)/(B*V) written
  * row-major [B][V] (for the dX product), and dWo [d][V] = D3^T dZ (D3t = D3^T [d][ldt]) and
@@ -417,7 +417,8 @@ int cc_dec_softmax_kl_fused(int32_t dtype, const float *Z2, int32_t B, int32_t V
  * sum_j clip(M~[card, j], 1e-7, 1) (cc_kl_tsum), indexed like Mt.  Outputs: dZ [rows][V] bf16
  * (= scale * ([p >= 1e-7](-t) + p * sum_{p>=1e-7} t), for the dX product), gW [d][V], gb [V],
  * loss_partials (cc_dec_kl_blocks(V) doubles) and, with ticket, loss_out = sum * loss_scale.
- * d in {128, 256}, rows % 32 == 0.  ws: cc_dec_kl_ws_size(rows, V) bytes, 16-B aligned. */
+ * d in {128, 256, 512} (96-column slices, 64 at d = 512), rows % 32 == 0.  ws:
+ * cc_dec_kl_ws_size(rows, V) bytes, 16-B aligned. */
 typedef struct cc_dec_kl_args {
   int32_t d, V, rows, ldt, row0;
   const void *D3p, *D3tp, *Wo;
