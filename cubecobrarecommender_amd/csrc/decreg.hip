@@ -379,8 +379,6 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   const __amdgpu_buffer_rsrc_t dz_rs =
       __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)p.rows * (uint32_t)V * 2u, 0x00020000);
   const float scale = p.scale;
-  const __amdgpu_buffer_rsrc_t gw_rs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)p.gW, (short)0, (uint32_t)D * (uint32_t)V * 4u, 0x00020000);
   constexpr int ND2 = (D + 255) / 256;   // phase 2's d tiles of wave w: 32w .. (and 32(w + 8) .. at d = 512)
 
   for (int t0 = 0; t0 < p.rows; t0 += TR) {
@@ -550,27 +548,6 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
-      // the slice's running dWo (all tiles but the first): every load issued before the MFMA
-      // chain, so its MALL/HBM latency runs under it (loaded after the chain in groups of 8, the
-      // read-modify-write was ~10 us of each 38-us row tile in full mode).  Through a buffer
-      // descriptor: columns past V get an offset past the range (load 0, store dropped).
-      const bool first = !FIX && t0 == 0;
-      uint32_t gvo[NJ];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int gc = n0 + j * 32 + (lane & 31);
-        gvo[j] = gc < V ? 4u * (uint32_t)((wt * 32 + 4 * half) * V + gc) : 0x80000000u;
-        asm volatile("" : "+v"(gvo[j]));  // opaque per tile: the 48 addresses are not hoisted
-      }
-      float old[NJ][16];
-      if (!first) {
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            old[j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                      gw_rs, gvo[j], 4u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), 0));
-      }
       // K = the tile's rows (a multiple of 32) in chunks of 32 (two 16-row fragments), a ring of
       // P2 chunks in flight (the loads come from L2: one chunk's 6 MFMAs cannot cover one latency)
       constexpr int P2 = 6;
@@ -600,12 +577,32 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
           }
         }
       }
+      const bool first = !FIX && t0 == 0;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
+      for (int j = 0; j < NJ; ++j) {
+        const int gc = n0 + j * 32 + (lane & 31);
+        if (gc < V) {
+          uint32_t g0 = (uint32_t)((wt * 32 + 4 * half) * V + gc);
+          asm volatile("" : "+v"(g0));  // opaque per tile: keeps 48 row addresses from being hoisted
+          // the tile's 16 partial sums of this column are added to gW with 8 loads in flight at
+          // a time (a load-add-store per element serialised 48 round trips per tile: the
+          // full-mode regulariser walks 43 tiles per slice).  (Measured and dropped: all 48 loads
+          // issued before the MFMA chain — the extra live registers spilled, 1,590 -> 2,040 us
+          // per block in full mode.)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(first ? acc2[j][r] : old[j][r] + acc2[j][r]), gw_rs,
-                                                gvo[j], 4u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), 0);
+          for (int h8 = 0; h8 < 16; h8 += 8) {  // two groups of 8 loads in flight (registers)
+            float old[8];
+            if (!first) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) old[r] = p.gW[g0 + (uint32_t)((((h8 + r) & 3) + 8 * ((h8 + r) >> 2)) * V)];
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+              p.gW[g0 + (uint32_t)((((h8 + r) & 3) + 8 * ((h8 + r) >> 2)) * V)] =
+                  first ? acc2[j][h8 + r] : old[r] + acc2[j][h8 + r];
+          }
+        }
+      }
     }
   }
 

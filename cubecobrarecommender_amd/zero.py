@@ -76,10 +76,8 @@ class ShardedStep:
         off = b['s0'] - b['lo']
         if self.stage:
             host = full.cpu()
-            if host.dtype == torch.bfloat16:   # gloo reduces/gathers no bf16: move the bits as int16
-                host = host.view(torch.int16)
             dist.all_gather_into_tensor(host, host[off:off + b['chunk']], group=self.group)
-            full.copy_(host.view(full.dtype))
+            full.copy_(host)
         else:           # in place: my shard already sits at rank * chunk inside the output
             dist.all_gather_into_tensor(full, full[off:off + b['chunk']], group=self.group)
 

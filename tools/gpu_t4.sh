@@ -10,3 +10,5 @@ run() { n=$1; shift; timeout -k 10 300 python -u bench.py --no-cpu-baseline --no
 run reg --reg 0.1
 run full --reg 0.1 --reg-mode full --steps 20 --warmup 3
 run c5 --reg 0.1 --d 1024 --dtype fp8 --steps 50 --warmup 5
+timeout -k 10 600 python -u -m pytest tests/test_gpu_dp.py -q --timeout 300 --timeout-method thread > $O/dp.log 2>&1
+tail -3 $O/dp.log; grep -E "^FAILED|Error" $O/dp.log | head -5
