@@ -40,6 +40,12 @@ constexpr int NTH = 512;     // 8 waves
 constexpr int TR = 512;      // rows per tile of the main kernel (2 passes of 8 x 32)
 constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
 constexpr float PMIN = 1e-7f;
+// Cache policy of the streamed operands of the main pass (M~ rows read once, dZ written once).
+// Full mode (many row tiles per slice): non-temporal for both, so they do not evict the block's
+// dWo slice between its per-tile read-modify-writes — 1,620 -> 1,500 us per block
+// (tools/micro/kl_probe_full.hip; either alone gains ~1 %).  One tile (the sampled regulariser):
+// default — the non-temporal pair slowed its epilogues (p1 4.9 -> 6.8 us).
+constexpr int KL_CPOL_NT = 2;  // the SLC/NT bit of the buffer instructions' cache-policy operand
 constexpr float LN_PMIN = -16.11809565095832f;  // ln(1e-7)
 
 
@@ -352,7 +358,7 @@ struct MainSmem {
 // waves' accumulators across all row tiles instead of the per-tile gW read-modify-write — the
 // 48 extra registers pushed the logits' fragment ring from 16 to 8 and spilled, and the logits
 // phases then waited on L2 twice as long: 1,620 -> 2,015 us per block, tools/micro/kl_probe_full.hip.)
-template <int D, bool FIX>
+template <int D, bool FIX, int CPOL = 0>
 __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt, MainSmem<kl_nb<D>()> &sm) {
   constexpr int NB = kl_nb<D>(), NJ = NB / 32;
   constexpr int CHB = TR / 8;
@@ -421,7 +427,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
           const uint32_t gc4 = 4u * (uint32_t)(n0 + j * 32 + (lane & 31));
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            tv[j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mt_rs, roff[r] + gc4, 0, 0));
+            tv[j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mt_rs, roff[r] + gc4, 0, CPOL));
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -463,7 +469,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
             cs[j] += dzf;  // the bias gradient sums the fp32 dz
             // the lane part of the offset in a VGPR, the row part (r) as the scalar soffset
             __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, 2u * (zrow + (uint32_t)(j * 32)),
-                                                  2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), 0);
+                                                  2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), CPOL);
           }
         } else {
 #pragma unroll
@@ -498,7 +504,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
               tt[r] = zb;
               cs[j] += dz;
             }
-            if (valid[j]) __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, 0);
+            if (valid[j]) __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, CPOL);
           }
         }
 #pragma unroll
@@ -664,11 +670,11 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   }
 }
 
-template <int D>
+template <int D, int CPOL>
 __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
   __shared__ __attribute__((aligned(16))) bf16_t Wt[kl_nb<D>() * D];
   __shared__ __attribute__((aligned(16))) MainSmem<kl_nb<D>()> sm;
-  kl_slice<D, false>(p, blockIdx.x, Wt, sm);
+  kl_slice<D, false, CPOL>(p, blockIdx.x, Wt, sm);
 }
 
 // The exact-clip correction: a small persistent grid (FIXG blocks) that leaves at once when the
@@ -769,7 +775,10 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
     CC_LAUNCH_CHECK("kl_stats_kernel");                                                                      \
     hipLaunchKernelGGL(kl_merge_kernel, dim3((unsigned)cdiv(a->rows, 4)), dim3(256), 0, s, p);              \
     CC_LAUNCH_CHECK("kl_merge_kernel");                                                                      \
-    hipLaunchKernelGGL((kl_main_kernel<DD>), gm, dim3(NTH), 0, s, p);                                       \
+    if (a->rows > TR)                                                                                        \
+      hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT>), gm, dim3(NTH), 0, s, p);                          \
+    else                                                                                                     \
+      hipLaunchKernelGGL((kl_main_kernel<DD, 0>), gm, dim3(NTH), 0, s, p);                                   \
     CC_LAUNCH_CHECK("kl_main_kernel");                                                                       \
     hipLaunchKernelGGL((kl_fix_kernel<DD>), dim3(FIXG), dim3(NTH), 0, s, p);                                \
     CC_LAUNCH_CHECK("kl_fix_kernel");                                                                        \

@@ -160,7 +160,7 @@ __device__ __forceinline__ void dma_tile_w(const DxP &p, const __amdgpu_buffer_r
     const int row = 8 * i + rl;
     const int k = k0 + 8 * (slot ^ (row & 7));
     const uint32_t oa = k < kend ? (uint32_t)(((bm + row) * p.lda + k) * 2) : 0x80000000u;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void *)(sa + i * 1024), 16, oa, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void *)(sa + i * 1024), 16, oa, 0, 0, 2);  // dZ is read once: non-temporal
   }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {

@@ -10,5 +10,5 @@ done
 for v in orig new orig new; do
   echo "== $v"
   timeout -k 5 120 tools/micro/bin/kl_probe_full_$v | tail -1 || exit 1
-  timeout -k 5 60 tools/micro/bin/kl_probe2_$v | tail -3 | head -2 || exit 1
+  timeout -k 5 60 tools/micro/bin/kl_probe2_$v | tail -4 | head -2 || exit 1
 done
