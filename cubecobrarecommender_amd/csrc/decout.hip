@@ -28,6 +28,15 @@ constexpr int NB_MIN = 64;
 constexpr int BK = 64;      // k per phase-2 ring chunk
 constexpr int NTH = 512;    // 8 waves
 constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+// cache policy (buffer cache-policy operand; 2 = non-temporal) of the dZ and dWo stores.  Measured
+// (r03 A/B, BCE step): non-temporal dZ slows the next dX kernel, which reads dZ from L2 (16 -> 19
+// us); both default
+#ifndef DEC_DZ_CPOL
+#define DEC_DZ_CPOL 0
+#endif
+#ifndef DEC_GW_CPOL
+#define DEC_GW_CPOL 0
+#endif
 
 typedef __attribute__((ext_vector_type(4))) uint32_t v4u;  // staging registers (stay in VGPRs)
 
@@ -297,7 +306,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
           for (int e = 0; e < 2; ++e) {
             const int r = r2 + e;
             __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(e ? pk >> 16 : pk), dz_rs, zv,
-                                                  2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), 0);
+                                                  2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), DEC_DZ_CPOL);
           }
         }
         lsum += __builtin_amdgcn_logf(lprod[0] * lprod[1]);
@@ -404,7 +413,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc2[j][r]), gw_rs,
-                                                4u * (g0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V)), 0, 0);
+                                                4u * (g0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V)), 0, DEC_GW_CPOL);
       }
     }
   }

@@ -646,6 +646,19 @@ __device__ __forceinline__ uint4 byte_bf16(uint32_t e) {  // 8 bits -> 8 bf16 of
   for (int i = 0; i < 4; ++i) w[i] = (((e >> (2 * i)) & 1u) ? 0x3F80u : 0u) | (((e >> (2 * i + 1)) & 1u) ? 0x3F800000u : 0u);
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
+// the W1 Adam epilogue's p / m / v streams (read and written once per step): cache policy.
+// Non-temporal measured slower (W1 kernel 32 -> 41 us in the BCE step, r03 A/B): default.
+#ifndef EG_ADAM_NT
+#define EG_ADAM_NT 0
+#endif
+__device__ __forceinline__ cc_adam::f32x4_t eg_ld(const cc_adam::f32x4_t *q) {
+  if constexpr (EG_ADAM_NT) return __builtin_nontemporal_load(q);
+  else return *q;
+}
+__device__ __forceinline__ void eg_st(cc_adam::f32x4_t *q, cc_adam::f32x4_t v) {
+  if constexpr (EG_ADAM_NT) __builtin_nontemporal_store(v, q);
+  else *q = v;
+}
 // ADAM: TF Adam on W1 in the tile epilogue (one process: the gradient is final here) — p, m, v
 // stream through once, the bf16 shadow is rewritten, the W1 gradient is never stored; the bias
 // row's gradient still goes to bias_grad for the main Adam launch
@@ -777,9 +790,9 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
       for (int g = 0; g < 4; ++g) {
         const int vg = v0 + 32 * t + 8 * g + (lane >> 3);
         const int64_t rb = (int64_t)(vg < V ? vg : V - 1) * d + 32 * cs + 4 * (lane & 7);
-        ap[g] = *reinterpret_cast<const cc_adam::f32x4_t *>(ad.p + rb);
-        am[g] = *reinterpret_cast<const cc_adam::f32x4_t *>(ad.m + rb);
-        av[g] = *reinterpret_cast<const cc_adam::f32x4_t *>(ad.v + rb);
+        ap[g] = eg_ld(reinterpret_cast<const cc_adam::f32x4_t *>(ad.p + rb));
+        am[g] = eg_ld(reinterpret_cast<const cc_adam::f32x4_t *>(ad.m + rb));
+        av[g] = eg_ld(reinterpret_cast<const cc_adam::f32x4_t *>(ad.v + rb));
       }
     }
     f32x16_t acc;
@@ -836,9 +849,9 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
 #pragma unroll
           for (int e = 0; e < 4; ++e) cc_adam::elem(pe[e], me[e], ve[e], ge[e], alpha, omb1, omb2, ad.eps);
           const int64_t o = (int64_t)vg * d + c0;
-          *reinterpret_cast<cc_adam::f32x4_t *>(ad.p + o) = cc_adam::f32x4_t{pe[0], pe[1], pe[2], pe[3]};
-          *reinterpret_cast<cc_adam::f32x4_t *>(ad.m + o) = cc_adam::f32x4_t{me[0], me[1], me[2], me[3]};
-          *reinterpret_cast<cc_adam::f32x4_t *>(ad.v + o) = cc_adam::f32x4_t{ve[0], ve[1], ve[2], ve[3]};
+          eg_st(reinterpret_cast<cc_adam::f32x4_t *>(ad.p + o), cc_adam::f32x4_t{pe[0], pe[1], pe[2], pe[3]});
+          eg_st(reinterpret_cast<cc_adam::f32x4_t *>(ad.m + o), cc_adam::f32x4_t{me[0], me[1], me[2], me[3]});
+          eg_st(reinterpret_cast<cc_adam::f32x4_t *>(ad.v + o), cc_adam::f32x4_t{ve[0], ve[1], ve[2], ve[3]});
           ushort4 sh;
           sh.x = f2bf(pe[0]);
           sh.y = f2bf(pe[1]);
