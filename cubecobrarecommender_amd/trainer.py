@@ -416,7 +416,9 @@ class Trainer:
         #                              of step k+1's forward graph (one graph launch less per step)
         self.side = torch.cuda.Stream(device=self.dev)   # dW / slab reduce / losses / transposes
         # the side-stream work (output-layer dW, slab reduces) as graph branches: measured slower than
-        # keeping it on the one stream, so _fork / _join only mark where it could branch
+        # keeping it on the one stream (r03: the tower dW beside the W1 gradient, 166.5 -> 181.7 us
+        # per step — every kernel of the graph got slower), so _fork / _join only mark where it could
+        # branch
         self.overlap = False
         self.timing = False          # bench.py: HIP events around the main kernels
         self.events = {}
