@@ -102,6 +102,8 @@ def roofline_for(name, ms, tr):
         n = tr.layout.total if tr.use_reg else tr.layout.main_total
         if getattr(tr, 'fuse_w1', False):     # W1's Adam runs in its gradient kernel
             n -= tr.w1_off
+        if getattr(tr, 'wo_range', None):     # [Wo, bo]'s in the tower backward launch
+            n -= tr.wo_range[1] - tr.wo_range[0]
         byt = n * (16 + 12 + 2)                    # read p,m,v,g; write p,m,v; write bf16 shadow
         return {'bound': 'hbm', 'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s', 'bytes_per_launch': byt}
@@ -312,7 +314,8 @@ def main():
     del y_mtx
     cfg = TrainConfig(V=V, d=d, batch_size=B, reg=args.reg, dtype=args.dtype, seed=1234,
                       rank=rank, world=world, reg_shard=reg_shard, reg_mode=args.reg_mode,
-                      fuse_w1_adam=True)   # one process: W1's Adam in its gradient kernel (parity:
+                      fuse_w1_adam=True,   # one process: W1's Adam in its gradient kernel, and (BCE
+                      wo_adam_in_tower=True)   # only) Wo's in the tower backward launch (parity:
     #                                        tests/test_gpu_train.py::test_fused_w1_adam_matches_unfused)
     tr = Trainer(cfg, data, params_flat=glorot_flat(V, d, seed=42), device=dev)
     rng = np.random.default_rng(99)      # same permutations on every rank

@@ -139,6 +139,8 @@ SIGNATURES = {
     'cc_tower_fwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_bwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_bwd_chain': (C.c_int, [C.POINTER(TowerArgs), _P]),
+    'cc_tower_bwd_chain_adam': (C.c_int, [C.POINTER(TowerArgs), _P, _P, _P, _P, _P, _I64, _P, _F32, _F32,
+                                          _F32, _F32, _P]),
     'cc_tower_bwd_dw': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_reduce': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_transpose': (C.c_int, [C.POINTER(TowerArgs), _P]),

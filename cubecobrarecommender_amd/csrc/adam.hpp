@@ -109,4 +109,60 @@ __device__ __forceinline__ void range(const Args &a, int64_t step, int bid, int 
   }
 }
 
+// range() for a few persistent blocks that share a launch with latency-bound work (the tower
+// backward chains, tower.hip): U float4 groups per thread in flight before any is consumed, so a
+// CU holding one such block still keeps enough bytes outstanding to stream.  Same element
+// update and rounding as range(); no packed images.
+template <int U>
+__device__ __forceinline__ void range_u(const Args &a, int64_t step, int bid, int nblocks) {
+  const float t = (float)(step + 1);
+  const float b1p = powf(a.b1, t), b2p = powf(a.b2, t);
+  const float alpha = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  const float omb1 = 1.f - a.b1, omb2 = 1.f - a.b2;
+  const int64_t n4 = a.n >> 2;
+  const int64_t stride = (int64_t)nblocks * blockDim.x;
+  for (int64_t i0 = (int64_t)bid * blockDim.x + threadIdx.x; i0 < n4; i0 += U * stride) {
+    f32x4_t pv[U], mv[U], vv[U], gv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i < n4) {
+        pv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.p) + i);
+        mv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.m) + i);
+        vv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.v) + i);
+        gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.g) + i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= n4) break;
+      float pe[4] = {pv[u][0], pv[u][1], pv[u][2], pv[u][3]};
+      float me[4] = {mv[u][0], mv[u][1], mv[u][2], mv[u][3]};
+      float ve[4] = {vv[u][0], vv[u][1], vv[u][2], vv[u][3]};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) elem(pe[e], me[e], ve[e], gv[u][e], alpha, omb1, omb2, a.eps);
+      __builtin_nontemporal_store(f32x4_t{pe[0], pe[1], pe[2], pe[3]}, reinterpret_cast<f32x4_t *>(a.p) + i);
+      __builtin_nontemporal_store(f32x4_t{me[0], me[1], me[2], me[3]}, reinterpret_cast<f32x4_t *>(a.m) + i);
+      __builtin_nontemporal_store(f32x4_t{ve[0], ve[1], ve[2], ve[3]}, reinterpret_cast<f32x4_t *>(a.v) + i);
+      if (a.shadow) {
+        ushort4 s;
+        s.x = f2bf(pe[0]);
+        s.y = f2bf(pe[1]);
+        s.z = f2bf(pe[2]);
+        s.w = f2bf(pe[3]);
+        reinterpret_cast<ushort4 *>(a.shadow)[i] = s;
+      }
+    }
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)bid * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    float pp = a.p[i], mm = a.m[i], vv = a.v[i];
+    elem(pp, mm, vv, a.g[i], alpha, omb1, omb2, a.eps);
+    a.p[i] = pp;
+    a.m[i] = mm;
+    a.v[i] = vv;
+    if (a.shadow) a.shadow[i] = f2bf(pp);
+  }
+}
+
 }  // namespace cc_adam

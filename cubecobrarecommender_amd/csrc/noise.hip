@@ -22,6 +22,11 @@
 #include "common.hpp"
 #include "detmath.hpp"
 
+// dev-only phase timestamps (tools/micro/noise_probe.hip defines it); compiled out of the library
+#ifndef NOISE_PROBE
+#define NOISE_PROBE(b, k)
+#endif
+
 namespace {
 
 constexpr int NT = 256;
@@ -108,9 +113,11 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
   const int64_t beg = a.cube_ptr[cube];
   const int n = (int)(a.cube_ptr[cube + 1] - beg);
   const int32_t *__restrict__ inc = a.cube_idx + beg;
+  NOISE_PROBE(b, 0);
 
   for (int w = tid; w < 4 * VW; w += NT) cube_bits[w] = 0u;
   __syncthreads();
+  NOISE_PROBE(b, 1);
   for (int i = tid; i < n; i += NT) {
     const int j = inc[i];
     atomicOr(&cube_bits[j >> 5], 1u << (j & 31));
@@ -127,6 +134,7 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
     s_k = k;
   }
   __syncthreads();
+  NOISE_PROBE(b, 2);
   const int k = s_k;
   // cut draws (with replacement from the includes)
   for (int i = tid; i < k; i += NT) {
@@ -136,6 +144,7 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
     atomicOr(&cut_bits[card >> 5], 1u << (card & 31));
   }
   __syncthreads();
+  NOISE_PROBE(b, 3);
   // ycut draws from the cut multiset
   const int nq = k >> 2;
   for (int q = tid; q < nq; q += NT) {
@@ -161,6 +170,7 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
     if (pick >= 0) atomicOr(&add_bits[pick >> 5], 1u << (pick & 31));
   }
   __syncthreads();
+  NOISE_PROBE(b, 4);
   // y bitmask: cube \ ycut (and x as a bitmask, for cc_embed_gather_fwd_xt's transpose)
   uint32_t *yrow = a.y_bits + (int64_t)b * VW;
   for (int w = tid; w < VW; w += NT) yrow[w] = cube_bits[w] & ~ycut_bits[w];
@@ -182,6 +192,7 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
   }
   if (lane == 63) scan[wv] = inc_sum;
   __syncthreads();
+  NOISE_PROBE(b, 5);
   int wbase = 0;
 #pragma unroll
   for (int w = 0; w < NT / 64; ++w) wbase += w < wv ? scan[w] : 0;
@@ -201,6 +212,7 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
     }
   }
   if (tid == 0) a.x_cnt[b] = min(total, a.x_cap);
+  NOISE_PROBE(b, 6);
   // regulariser row for this slot (generator.py:47-51): one draw ∝ neg_sampler
   if (a.with_reg && tid == 0) {
     const u32x4 o = rng(a.seed, step, slot, KIND_REG, 0, 0);

@@ -12,6 +12,7 @@
 // cc_tower_reduce sums the slabs in block order: deterministic dW/db for all 9 layers.
 #include <algorithm>
 
+#include "adam.hpp"
 #include "common.hpp"
 #include "mx8.hpp"
 #include "xt.hpp"
@@ -541,8 +542,15 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
   if (p.act6tp) pt_copy_out(xin, ldx, p.act6tp, dd, p.R, r0);  // D3^T: the dWo A operand
 }
 
-template <int D>
-__global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p) {
+// ADAM: blocks past the chains run TF Adam over a flat range (cc_tower_bwd_chain_adam) on the CUs
+// the 16-32 latency-bound chain blocks leave idle; the chains launch first, so they start at once.
+template <int D, bool ADAM>
+__global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p, cc_adam::Args ad,
+                                                                   const int64_t *ad_state) {
+  if (ADAM && (int)blockIdx.x >= p.R / RB) {
+    cc_adam::range_u<4>(ad, ad_state[0], (int)blockIdx.x - p.R / RB, (int)gridDim.x - p.R / RB);
+    return;
+  }
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int ldx = p.maxw + 8;
   bf16_t *Gr = reinterpret_cast<bf16_t *>(smem);
@@ -1354,7 +1362,9 @@ extern "C" int cc_tower_fwd(const cc_tower_args *t, void *stream) {
   return CC_OK;
 }
 
-static int tower_bwd_launch(const cc_tower_args *t, void *stream, bool chain, bool dw) {
+static int tower_bwd_launch(const cc_tower_args *t, void *stream, bool chain, bool dw,
+                            const cc_adam::Args *ad = nullptr, const int64_t *ad_state = nullptr,
+                            int ad_blocks = 0) {
   TowerP p;
   int rc = make_params(t, p);
   if (rc) return rc;
@@ -1367,12 +1377,22 @@ static int tower_bwd_launch(const cc_tower_args *t, void *stream, bool chain, bo
   hipStream_t s = as_stream(stream);
   if (t->dtype == CC_BF16) {
     if (chain && p.d <= 256) {
+      const cc_adam::Args a0 = ad ? *ad : cc_adam::Args{};
+      const dim3 ga(gc.x + (ad ? ad_blocks : 0));
+#define CHAIN_FAST(DD)                                                                              \
+  if (ad)                                                                                           \
+    hipLaunchKernelGGL((tower_bwd_chain_fast_kernel<DD, true>), ga, dim3(FNT), lds_chain, s, p, a0, \
+                       ad_state);                                                                   \
+  else                                                                                              \
+    hipLaunchKernelGGL((tower_bwd_chain_fast_kernel<DD, false>), gc, dim3(FNT), lds_chain, s, p, a0, \
+                       ad_state);
       switch (p.d) {
-        case 64: hipLaunchKernelGGL(tower_bwd_chain_fast_kernel<64>, gc, dim3(FNT), lds_chain, s, p); break;
-        case 128: hipLaunchKernelGGL(tower_bwd_chain_fast_kernel<128>, gc, dim3(FNT), lds_chain, s, p); break;
-        case 192: hipLaunchKernelGGL(tower_bwd_chain_fast_kernel<192>, gc, dim3(FNT), lds_chain, s, p); break;
-        default: hipLaunchKernelGGL(tower_bwd_chain_fast_kernel<256>, gc, dim3(FNT), lds_chain, s, p); break;
+        case 64: CHAIN_FAST(64) break;
+        case 128: CHAIN_FAST(128) break;
+        case 192: CHAIN_FAST(192) break;
+        default: CHAIN_FAST(256) break;
       }
+#undef CHAIN_FAST
     }
     else if (chain && p.packed)
       hipLaunchKernelGGL(tower_bwd_chain_wide_kernel, gc, dim3(FNT), lds_chain, s, p);
@@ -1392,6 +1412,31 @@ extern "C" int cc_tower_bwd(const cc_tower_args *t, void *stream) {
 }
 extern "C" int cc_tower_bwd_chain(const cc_tower_args *t, void *stream) {
   return tower_bwd_launch(t, stream, true, false);
+}
+extern "C" int cc_tower_bwd_chain_adam(const cc_tower_args *t, float *p, float *m, float *v, const float *g,
+                                       uint16_t *shadow, int64_t n, const int64_t *state, float lr,
+                                       float beta1, float beta2, float eps, void *stream) {
+  CC_REQUIRE(t && t->dtype == CC_BF16 && t->d <= 256,
+             "cc_tower_bwd_chain_adam: the bf16 fast chains (d <= 256) only");
+  CC_REQUIRE(p && m && v && g && state, "cc_tower_bwd_chain_adam: null pointer");
+  CC_REQUIRE(((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g) % 16 == 0,
+             "cc_tower_bwd_chain_adam: buffers must be 16-byte aligned");
+  CC_REQUIRE(!shadow || (uintptr_t)shadow % 8 == 0, "cc_tower_bwd_chain_adam: shadow must be 8-byte aligned");
+  CC_REQUIRE(n >= 0, "cc_tower_bwd_chain_adam: n");
+  if (n == 0) return tower_bwd_launch(t, stream, true, false);
+  const cc_adam::Args a{p, m, v, g, (bf16_t *)shadow, n, lr, beta1, beta2, eps};
+  // one 512-thread block per CU beside the chains (their VGPR budget admits one per CU), capped
+  // so no block runs out of work
+  static int cus = 0;
+  if (cus <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const int64_t want = cdiv(cdiv(n, 4), (int64_t)FNT * 4);
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(cus - t->R / RB, 8)));
+  return tower_bwd_launch(t, stream, true, false, &a, state, blocks);
 }
 extern "C" int cc_tower_bwd_dw(const cc_tower_args *t, void *stream) {
   return tower_bwd_launch(t, stream, false, true);

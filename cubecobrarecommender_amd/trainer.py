@@ -41,6 +41,9 @@ class TrainConfig:
     reg_shard: bool = False        # data parallel + reg: M~ row-sharded, owner computes
     fuse_w1_adam: bool = False     # one process: TF Adam on W1 inside the W1-gradient kernel (its
     #                                gradient is then never stored; bench.py turns it on)
+    wo_adam_in_tower: bool = False  # with fuse_w1_adam, BCE only, bf16 d <= 256: TF Adam on the decoder
+    #                                output layer in the tower backward launch (bench.py turns it on)
+    wo_tower_frac: float = 0.6     # ... on this trailing fraction of it; the rest stays in the Adam + F launch
     reg_mode: str = 'sampled'      # 'sampled': B reg rows per step drawn ∝ neg_sampler (generator.py:47-51);
     #                                'full': all |V| identity rows every step, KL(M~, D2(E(I))) as the
     #                                reference README states the objective (README.md:27)
@@ -140,7 +143,10 @@ class DeviceDataset:
         self.cdf_host = cdf
         self.neg_sampler = torch.from_numpy(ns).to(device)
         self.cdf = torch.from_numpy(cdf).to(device)
-        self.guide_log2 = 12   # CDF search guide table: 4097 entries
+        # CDF search guide table (2^16 + 1 entries, 256 KB): with Zipf-like popularity the tail
+        # cards share buckets, and each extra entry per bucket is one more dependent fp64 load in
+        # F's add draws (measured at 2^12: the add phase 3.5 us mean, 7.9 us worst per cube)
+        self.guide_log2 = 16
         guide = np.searchsorted(cdf, np.arange((1 << self.guide_log2) + 1) / float(1 << self.guide_log2), side='right')
         self.guide = torch.from_numpy(guide.astype(np.int32)).to(device)
         self.y_reg = None
@@ -407,6 +413,20 @@ class Trainer:
         self.fuse_w1 = (cfg.fuse_w1_adam and self.adam_packs and self.eg_tickets is not None and not self.full_reg
                         and self.layout.offset('encoder/encoded_1/kernel') == 0)
         self.adam_pack = self._adam_pack_desc() if self.adam_packs else None
+        # TF Adam on the decoder output layer (Wo, bo: ~96% of the parameters after W1) in extra
+        # workgroups of the tower backward launch (cc_tower_bwd_chain_adam): its gradient is final
+        # after cc_dec_bce_dw and dX has read its bf16 shadow, and the 16-32 latency-bound chain
+        # blocks leave the other CUs idle.  Only its trailing wo_tower_frac: the main Adam launch
+        # (which also runs the next step's F, latency-bound too) keeps [W1 end, split) to stream
+        # beside F.
+        self.wo_range = None
+        if (cfg.wo_adam_in_tower and self.fuse_w1 and not self.use_reg and self.fused_out
+                and self.targs is not None and self.dtype == L.CC_BF16 and cfg.d <= 256):
+            lo, hi = self.layout.offset('decoder/reconstruct/kernel'), self.layout.main_total
+            frac = float(os.environ.get('CCREC_WO_TOWER_FRAC', cfg.wo_tower_frac))   # (dev A/B knob)
+            split = hi - int((hi - lo) * min(max(frac, 0.0), 1.0)) // 256 * 256
+            if split < hi:
+                self.wo_range = (split, hi)
         self._adv_deferred = False   # the previous step's counter advance rides in the E1 gather
         self.noise_ready = False
         self.perms = None
@@ -869,7 +889,14 @@ class Trainer:
         s = self._s
         if self.fused_tower:
             t = self._tick('cc_tower_bwd')
-            L.call('cc_tower_bwd_chain', L.C.byref(self.targs), s)
+            if self.wo_range is not None:   # + TF Adam on [Wo, bo] beside the chains
+                lo, hi = self.wo_range
+                L.call('cc_tower_bwd_chain_adam', L.C.byref(self.targs), L.ptr(self.params[lo:]),
+                       L.ptr(self.m[lo:]), L.ptr(self.v[lo:]), L.ptr(self.grads[lo:]),
+                       L.ptr(self.shadow[lo:]), hi - lo, L.ptr(self.state), cfg.lr, cfg.beta1,
+                       cfg.beta2, cfg.eps, s)
+            else:
+                L.call('cc_tower_bwd_chain', L.C.byref(self.targs), s)
             t()
             ss = self._fork()      # per-block dW slabs + their reduce overlap the E1 scatter
             # direct dW: from the packed images (any row count) or LDS-staged (rows <= ~1184)
@@ -923,6 +950,8 @@ class Trainer:
         """TF Adam over every trained parameter (+ bf16 shadow refresh)."""
         cfg = self.cfg
         n = self.layout.total if self.use_reg else self.layout.main_total
+        if self.wo_range is not None:   # [Wo, bo] updated in the tower backward launch
+            n = self.wo_range[0]
         t = self._tick('cc_adam_dense')
         if self.prefetch:     # + F for the next step in the same launch
             na = self._noise_args()
@@ -1056,16 +1085,16 @@ class Trainer:
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream())
         saved = self.state.clone()
-        # the fused W1 Adam updates W1 inside forward_backward: undo the warm-up's update
-        w1 = ([b[:self.w1_off].clone() for b in (self.params, self.m, self.v, self.shadow)]
-              if self.fuse_w1 else None)
+        # the fused W1 (and Wo) Adam updates them inside forward_backward: undo the warm-up's update
+        spans = ([(0, self.w1_off)] if self.fuse_w1 else []) + ([self.wo_range] if self.wo_range else [])
+        saved_spans = [[b[lo:hi].clone() for b in (self.params, self.m, self.v, self.shadow)] for lo, hi in spans]
         with torch.cuda.stream(s):           # warm-up launch outside capture (lazy module loads)
             self.forward_backward()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        if w1 is not None:
-            for b, c in zip((self.params, self.m, self.v, self.shadow), w1):
-                b[:self.w1_off].copy_(c)
+        for (lo, hi), cs in zip(spans, saved_spans):
+            for b, c in zip((self.params, self.m, self.v, self.shadow), cs):
+                b[lo:hi].copy_(c)
         g_fb, g_adam, g_rest = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         if self.cfg.world > 1:   # (forward_backward_a | forward_backward_b | counters): the
             with torch.cuda.graph(g_fb):       # sharded optimizer's collectives run between them

@@ -369,6 +369,14 @@ int cc_tower_bwd(const cc_tower_args *t, void *stream);
 /* cc_tower_bwd = cc_tower_bwd_chain (dX chain; writes gpre1 and every layer's dPre) followed by
  * cc_tower_bwd_dw (per-block dW/db slabs); split so the slabs can overlap the E1 scatter. */
 int cc_tower_bwd_chain(const cc_tower_args *t, void *stream);
+/* cc_tower_bwd_chain plus, in extra workgroups of the same launch (on the CUs the 32-row chains
+ * leave idle), exactly cc_adam_dense(p, m, v, g, shadow, n, state, lr, beta1, beta2, eps) — for a
+ * flat range the chains do not read (the trainer: the decoder output layer, whose gradient is
+ * final after cc_dec_bce_dw and whose bf16 shadow the dX product has already consumed).
+ * bf16 fast chains (d <= 256) only. */
+int cc_tower_bwd_chain_adam(const cc_tower_args *t, float *p, float *m, float *v, const float *g,
+                            uint16_t *shadow, int64_t n, const int64_t *state, float lr, float beta1,
+                            float beta2, float eps, void *stream);
 int cc_tower_bwd_dw(const cc_tower_args *t, void *stream);
 int cc_tower_reduce(const cc_tower_args *t, void *stream);
 /* bf16: every layer's dW/db written directly (no slabs, no reduce): cc_tower_bwd_dw +

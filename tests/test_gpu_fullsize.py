@@ -81,10 +81,11 @@ def test_bench_configuration_matches_oracle(reg):
     y_mtx = adjacency_normalised_gpu(indptr, indices, V, device='cuda') if reg > 0 else None
     data = DeviceDataset(csr=(indptr, indices), num_cards=V, neg_sampler=ns, y_mtx=y_mtx, device='cuda')
     cfg = TrainConfig(V=V, d=d, batch_size=B, reg=reg, dtype='bf16', seed=1234,
-                      fuse_w1_adam=True)    # exactly bench.py's TrainConfig
+                      fuse_w1_adam=True, wo_adam_in_tower=True)    # exactly bench.py's TrainConfig
     flat = glorot_flat(V, d, seed=42)
     tr = Trainer(cfg, data, params_flat=flat)
     assert tr.fused_out and tr.adam_packs and tr.prefetch and tr.wpack is not None and tr.fuse_w1
+    assert (tr.wo_range is not None) == (reg == 0)
     perm = np.random.default_rng(99).permutation(C).astype(np.int32)
     tr.set_epoch_permutations(perm[None, :])
     tr.capture()

@@ -68,6 +68,8 @@ def _run_noise(lists, V, B, ns, seed, step, with_reg=True, slot_rank=0, guide_lo
     (1500, 64, (40, 200, 400), 2, 7, 12),
     (22000, 64, (180, 360, 450, 540, 720), 20250301, 123456, 0),
     (22000, 64, (180, 360, 450, 540, 720), 20250301, 123456, 12),
+    (22000, 64, (180, 360, 450, 540, 720), 20250301, 123456, 16),
+    (300, 16, (5, 30, 60), 1, 0, 16),
 ])
 def test_noise_bit_exact_vs_oracle(V, B, sizes, seed, step, glog2):
     lists, Mt, ns = problem(seed, B, V, sizes)

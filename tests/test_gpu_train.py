@@ -330,17 +330,20 @@ def test_fused_w1_adam_matches_unfused(reg):
     """TrainConfig(fuse_w1_adam=True) — bench.py's step: TF Adam on W1 in the column-slice W1-gradient
     kernel's epilogue, the main Adam launch starting after W1 — gives bit-identical parameters,
     bf16 shadow, Adam moments and losses to the unfused step (same cc_adam::elem update, same
-    gradient values), over eager steps and graph replays."""
+    gradient values), over eager steps and graph replays.  With wo_adam_in_tower as well (BCE
+    only): the decoder output layer's Adam in the tower backward launch (cc_tower_bwd_chain_adam,
+    cc_adam::range_u) — the same bits again."""
     out = {}
-    for fuse in (False, True):
+    for fuse, wo in ((False, False), (True, False), (True, True)):
         lists, Mt, ns = problem(11, 1024, 2500, (20, 40, 80))
         P = model_ref.init_params(2500, 256, seed=11, bias_std=0.01)
         lay = Layout(2500, 256)
-        cfg = TrainConfig(V=2500, d=256, batch_size=256, reg=reg, dtype='bf16', seed=11, fuse_w1_adam=fuse)
+        cfg = TrainConfig(V=2500, d=256, batch_size=256, reg=reg, dtype='bf16', seed=11, fuse_w1_adam=fuse,
+                          wo_adam_in_tower=wo)
         tr = Trainer(cfg, DeviceDataset(lists, 2500, y_mtx=Mt.astype(np.float32) if reg > 0 else None,
                                         neg_sampler=ns), params_flat=lay.pack(P))
         tr.set_epoch_permutation(np.random.default_rng(11).permutation(1024).astype(np.int32))
-        assert tr.fuse_w1 == fuse and tr.adam_packs
+        assert tr.fuse_w1 == fuse and tr.adam_packs and (tr.wo_range is not None) == (wo and reg == 0)
         losses = []
         for _ in range(2):
             tr.step()
@@ -351,10 +354,11 @@ def test_fused_w1_adam_matches_unfused(reg):
             losses.append(tr.losses())
         tr.flush()
         torch.cuda.synchronize()
-        out[fuse] = (tr.params.cpu(), tr.m.cpu(), tr.v.cpu(), tr.shadow.cpu(), losses)
-    for a, b in zip(out[False][:4], out[True][:4]):
-        assert torch.equal(a, b)
-    assert out[False][4] == out[True][4]
+        out[fuse, wo] = (tr.params.cpu(), tr.m.cpu(), tr.v.cpu(), tr.shadow.cpu(), losses)
+    for key in ((True, False), (True, True)):
+        for a, b in zip(out[False, False][:4], out[key][:4]):
+            assert torch.equal(a, b)
+        assert out[False, False][4] == out[key][4]
 
 
 @pytest.mark.parametrize('dtype,V,d,B', [('fp32', 700, 64, 32), ('bf16', 1500, 256, 128), ('bf16', 1500, 512, 128)])
