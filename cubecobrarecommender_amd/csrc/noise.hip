@@ -40,16 +40,19 @@ __device__ __forceinline__ u32x4 rng(uint64_t seed, uint32_t step, uint32_t slot
                        (uint32_t)(seed >> 32));
 }
 
-// first index j with cdf[j] > u  (numpy searchsorted side='right').  With a guide table the search
-// is restricted to [guide[g], guide[g+1]], g = floor(u 2^G) — the same answer (cdf is monotone and
-// g/2^G <= u < (g+1)/2^G), in ~log2(V/2^G) instead of log2(V) dependent loads.
+// first index j with cdf[j] > u  (numpy searchsorted side='right').  With a guide table the answer
+// lies in [guide[g], guide[g+1]], g = floor(u 2^G) (cdf is monotone and g/2^G <= u < (g+1)/2^G),
+// and hi = min(guide[g+1], V-1) is itself a valid answer (cdf[guide[g+1]] > (g+1)/2^G > u, and
+// cdf[V-1] = 1 > u), so the search runs over [lo, hi) with hi as the default: a bucket without a
+// cdf boundary (guide[g] == guide[g+1], most of the 2^16) needs no cdf load at all, the others one
+// dependent load fewer than a search over [lo, hi + 1).
 __device__ __forceinline__ int search_right(const double *__restrict__ cdf, int V, double u,
                                             const int32_t *__restrict__ guide, int glog2) {
   int lo = 0, hi = V;
   if (guide) {
     const int g = (int)(u * (double)(1 << glog2));
     lo = guide[g];
-    hi = min(guide[g + 1], V - 1) + 1;
+    hi = min(guide[g + 1], V - 1);
   }
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
@@ -101,7 +104,6 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
   uint32_t *ycut_bits = cut_bits + VW;
   uint32_t *add_bits = ycut_bits + VW;
   int32_t *scan = (int32_t *)(add_bits + VW);  // [NT + 1]
-  int32_t *cut_card = scan + NT + 1;           // [x_cap]
 
   const int tid = threadIdx.x;
   const uint32_t slot = a.slot_base + (uint32_t)b;
@@ -140,19 +142,20 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
   for (int i = tid; i < k; i += NT) {
     const uint32_t pos = mulhi_bound(rng(a.seed, step, slot, KIND_CUT, (uint32_t)i, 0).x, (uint32_t)n);
     const int card = inc[pos];
-    cut_card[i] = card;
     atomicOr(&cut_bits[card >> 5], 1u << (card & 31));
   }
-  __syncthreads();
-  NOISE_PROBE(b, 3);
-  // ycut draws from the cut multiset
+  // ycut draws from the cut multiset: draw q picks cut draw qq, whose card is a pure function of
+  // (qq, the cube) — recomputed here instead of read back from an LDS list, so the ycut draws need
+  // no barrier after the cut draws
   const int nq = k >> 2;
   for (int q = tid; q < nq; q += NT) {
     const uint32_t qq = mulhi_bound(rng(a.seed, step, slot, KIND_YCUT, (uint32_t)q, 0).x, (uint32_t)k);
-    const int card = cut_card[qq];
+    const uint32_t pos = mulhi_bound(rng(a.seed, step, slot, KIND_CUT, qq, 0).x, (uint32_t)n);
+    const int card = inc[pos];
     atomicOr(&ycut_bits[card >> 5], 1u << (card & 31));
   }
-  // add draws (rejection against the global CDF)
+  // add draws (rejection against the global CDF): they need only cube_bits, so they run beside the
+  // cut and ycut draws
   for (int i = tid; i < k; i += NT) {
     int pick = -1;
     for (int t = 0; t < ADD_MAX_TRIES; ++t) {
@@ -170,6 +173,7 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
     if (pick >= 0) atomicOr(&add_bits[pick >> 5], 1u << (pick & 31));
   }
   __syncthreads();
+  NOISE_PROBE(b, 3);
   NOISE_PROBE(b, 4);
   // y bitmask: cube \ ycut (and x as a bitmask, for cc_embed_gather_fwd_xt's transpose)
   uint32_t *yrow = a.y_bits + (int64_t)b * VW;
@@ -329,7 +333,7 @@ static int noise_check(const cc_noise_args *a, size_t &lds) {
   CC_REQUIRE(!a->with_reg || a->reg_idx, "cc_noise_fwd: with_reg needs reg_idx");
   CC_REQUIRE(a->num_perms >= 1 && a->num_cubes >= a->batch_stride, "cc_noise_fwd: num_perms/num_cubes");
   const int VW = (a->V + 31) / 32;
-  lds = (size_t)(4 * VW + NT + 1 + a->x_cap) * 4;
+  lds = (size_t)(4 * VW + NT + 1) * 4;
   CC_REQUIRE(lds <= 150 * 1024, "cc_noise_fwd: V / x_cap too large for LDS");
   return CC_OK;
 }

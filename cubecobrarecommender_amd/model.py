@@ -118,11 +118,12 @@ class CC_Recommender:
         cfg = TrainConfig(V=self.N, d=self.d, batch_size=generator.batch_size, reg=self.reg,
                           noise=generator.noise, noise_std=generator.noise_std, lr=self.lr,
                           dtype=self.dtype, seed=self.seed, rank=rank, world=world,
-                          # one process: W1's Adam inside its gradient kernel where the trainer's
-                          # bf16 path supports it (bit-identical to the unfused step,
+                          # one process: W1's Adam inside its gradient kernel and (BCE only) part of
+                          # Wo's beside the tower backward chains, where the trainer's bf16 path
+                          # supports it (bit-identical to the unfused step,
                           # tests/test_gpu_train.py::test_fused_w1_adam_matches_unfused) — the
                           # configuration bench.py measures
-                          fuse_w1_adam=(world == 1))
+                          fuse_w1_adam=(world == 1), wo_adam_in_tower=(world == 1))
         tr = Trainer(cfg, generator.data, params_flat=self._current_flat())
         if self._m is not None:
             tr.load_standard(tr.m, self._m)

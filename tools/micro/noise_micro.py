@@ -19,7 +19,8 @@ def build_probe():
     so = os.path.join(ROOT, 'tools', 'micro', 'libnoise_probe.so')
     src = os.path.join(ROOT, 'tools', 'micro', 'noise_probe.hip')
     pkg = os.path.join(ROOT, 'cubecobrarecommender_amd')
-    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+    deps = (src, os.path.join(pkg, 'csrc', 'noise.hip'))
+    if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(f) for f in deps):
         subprocess.check_call(['/opt/rocm/bin/hipcc', '-O3', '-std=c++17', '--offload-arch=gfx950', '-fPIC', '-shared',
                                '-I', os.path.join(ROOT, 'include'), '-I', os.path.join(pkg, 'csrc'), src,
                                '-L', pkg, '-lccrec_hip', '-Wl,-rpath,' + pkg, '-Wl,-Bsymbolic', '-o', so])
