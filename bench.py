@@ -325,10 +325,9 @@ def main():
     n_grad = tr.layout.total if tr.use_reg else tr.layout.main_total
 
     adam_ev = []
-    ADAM_SAMPLE = 8
+    ADAM_SAMPLE = 25
 
     def step(graphed, timed=False):
-        step.count = getattr(step, 'count', -1) + 1 if timed else -1
         if world > 1:   # bucketed reduce-scatter + sharded Adam + all-gather (zero.py)
             if not graphed:
                 saved, tr.graphs = tr.graphs, None
@@ -337,11 +336,10 @@ def main():
             else:
                 tr.step_dp(timing=timed)
             return
-        if timed and graphed and (len(adam_ev) == 0 or step.count % ADAM_SAMPLE == 0):
-            # every ADAM_SAMPLE-th timed step: HIP events on the stream bracketing the Adam kernel,
-            # launched eagerly right behind the forward/backward graph (the host is far ahead of
-            # the GPU, so the kernel is queued when e0 fires: the interval is its own duration).
-            # The other steps replay the whole step as one graph.
+        if timed and graphed:
+            # a sampled step: HIP events on the stream bracketing the Adam kernel, launched eagerly
+            # right behind the forward/backward graph (the host is far ahead of the GPU, so the
+            # kernel is queued when e0 fires: the interval is its own duration)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             tr.run_fb()
             tr.run_adam(events=(e0, e1))
@@ -351,18 +349,34 @@ def main():
             tr.step()
             tr.graphs = saved
 
+    def steps(n, timed=False):
+        """n graphed steps.  One process: every ADAM_SAMPLE-th timed step is the sampled step above;
+        the others replay tr.step_many's multi-step graph (cfg.graph_steps whole steps per replay,
+        single-step graphs for the remainder).  Data parallel: step by step."""
+        if world > 1:
+            for _ in range(n):
+                step(True, timed)
+            return
+        i = 0
+        while i < n:
+            if timed and i % ADAM_SAMPLE == 0:
+                step(True, timed=True)
+                i += 1
+                continue
+            m = min(n - i, ADAM_SAMPLE - i % ADAM_SAMPLE) if timed else n - i
+            tr.step_many(m)
+            i += m
+
     for _ in range(3):          # eager steps: module loads, lazy allocations
         step(False)
     tr.capture()
 
-    for _ in range(args.warmup):
-        step(True)
+    steps(args.warmup)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True, timed=True)
+    steps(args.steps, timed=True)
     barrier(world)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -429,7 +443,8 @@ def main():
                    'V': V, 'd': d, 'batch_per_gpu': B, 'global_batch': B * world, 'reg': args.reg,
                    'reg_mode': args.reg_mode, 'reg_rows_per_gpu': tr.Breg,
                    'reg_shard': 'owner computes' if tr.owner else ('full rows' if tr.full_reg and world > 1 else 'replicated'),
-                   'cubes': args.cubes, 'parallelism': f'dp{world}'},
+                   'cubes': args.cubes, 'parallelism': f'dp{world}',
+                   'graph_steps': tr.multi_n if world == 1 else 1},
         'roofline': roof,
         'step_roofline': step_roofline(tr, dt / args.steps * 1e3, ktimes),
         'kernel_us': ktimes,

@@ -131,17 +131,22 @@ class CC_Recommender:
             tr.state[0] = self._step
         tr.set_epoch_permutations(generator.epoch_permutations(epochs))
         steps = tr.batches_per_epoch
-        if graphs:
-            tr.capture()
         loss_sum = torch.zeros(2, dtype=torch.float64, device=tr.loss_dev.device)
+        if graphs:
+            tr.capture(loss_acc=loss_sum)   # (one process: + the multi-step graph of step_many)
         for ep in range(epochs):
             t0 = time.perf_counter()
             loss_sum.zero_()
-            for i in range(steps):
-                tr.step()          # data-parallel: bucketed reduce-scatter + sharded Adam (zero.py)
-                loss_sum += tr.loss_dev
-                if (i + 1) % STATUS_EVERY == 0:   # an x_cap / owner-capacity overflow stops the
-                    tr.check_status()             # run within STATUS_EVERY steps, not at epoch end
+            i = 0
+            while i < steps:
+                # data-parallel: bucketed reduce-scatter + sharded Adam (zero.py) per step; one
+                # process: multi-step graph replays; an x_cap / owner-capacity overflow stops the
+                # run within STATUS_EVERY steps, not at epoch end
+                n = min(STATUS_EVERY - i % STATUS_EVERY, steps - i)
+                tr.step_many(n, loss_acc=loss_sum)
+                i += n
+                if i % STATUS_EVERY == 0:
+                    tr.check_status()
             torch.cuda.synchronize()
             tr.check_status()
             l = tr.losses(loss_sum / steps)

@@ -44,6 +44,7 @@ class TrainConfig:
     wo_adam_in_tower: bool = False  # with fuse_w1_adam, BCE only, bf16 d <= 256: TF Adam on the decoder
     #                                output layer in the tower backward launch (bench.py turns it on)
     wo_tower_frac: float = 0.6     # ... on this trailing fraction of it; the rest stays in the Adam + F launch
+    graph_steps: int = 8           # one process: consecutive steady-state steps per hipGraph replay (step_many)
     reg_mode: str = 'sampled'      # 'sampled': B reg rows per step drawn ∝ neg_sampler (generator.py:47-51);
     #                                'full': all |V| identity rows every step, KL(M~, D2(E(I))) as the
     #                                reference README states the objective (README.md:27)
@@ -432,6 +433,7 @@ class Trainer:
         self.perms = None
         self.batches_per_epoch = max(1, data.C // (B * cfg.world))   # generator.py:36 (__len__)
         self.graphs = None
+        self.g_multi, self.multi_n, self.multi_acc = None, 0, None   # capture(): step_many's graph
         self.pending_rest = False    # one process: step k's counters/transposes run at the head
         #                              of step k+1's forward graph (one graph launch less per step)
         self.side = torch.cuda.Stream(device=self.dev)   # dW / slab reduce / losses / transposes
@@ -1060,12 +1062,15 @@ class Trainer:
             self.apply_adam(stream)
         self.pending_rest = True
 
+    def _steady(self):
+        return (self.graphs is not None and self.graphs[4] is not None and self.pending_rest
+                and (self.noise_ready or not self.prefetch))
+
     def step(self, stream=None):
         if self.cfg.world > 1:
             self.step_dp()
             return
-        if (self.graphs is not None and self.graphs[4] is not None and self.pending_rest
-                and (self.noise_ready or not self.prefetch)):
+        if self._steady():
             self.graphs[4].replay()    # steady state: rest(k-1) + fwd/bwd(k) + Adam(k) in one graph
             self.pending_rest = True
             self.noise_ready = self.prefetch
@@ -1073,7 +1078,28 @@ class Trainer:
         self.run_fb(stream)
         self.run_adam(stream)
 
-    def capture(self):
+    def step_many(self, n, loss_acc=None):
+        """n steps.  In the one-process steady state, graph_steps of them at a time replay one
+        captured graph of graph_steps consecutive whole steps (every step's kernels exactly as
+        step() launches them; the device counters advance inside): the ~6-9 us boundary between
+        two graph replays is paid once per graph_steps steps.  loss_acc: a [2] fp64 device tensor
+        that accumulates every step's (bce, kl) — it must be the tensor capture() was given."""
+        gm = self.g_multi
+        while n > 0:
+            if (gm is not None and n >= self.multi_n and self._steady()
+                    and (loss_acc is None) == (self.multi_acc is None)
+                    and (loss_acc is None or loss_acc is self.multi_acc)):
+                gm.replay()
+                self.pending_rest = True
+                self.noise_ready = self.prefetch
+                n -= self.multi_n
+                continue
+            self.step()
+            if loss_acc is not None:
+                loss_acc += self.loss_dev
+            n -= 1
+
+    def capture(self, loss_acc=None):
         """Capture the step as three hipGraphs (torch.cuda.CUDAGraph over our own kernel launches):
         forward_backward | Adam | counters+transposes (data parallel: forward_backward_a |
         forward_backward_b | counters+transposes, with zero.py's collectives and sharded Adam
@@ -1121,8 +1147,22 @@ class Trainer:
                 self.apply_rest(defer=True)
                 self.forward_backward()
                 self.apply_adam()
+        self.g_multi, self.multi_n, self.multi_acc = None, 0, None
+        if self.cfg.world == 1 and self.cfg.graph_steps > 1:   # step_many: graph_steps whole steps
+            self.g_multi = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_multi):
+                for _ in range(self.cfg.graph_steps):
+                    self.noise_ready = self.prefetch
+                    self.apply_rest(defer=True)
+                    self.forward_backward()
+                    self.apply_adam()
+                    if loss_acc is not None:
+                        loss_acc += self.loss_dev
+            self.multi_n, self.multi_acc = self.cfg.graph_steps, loss_acc
         torch.cuda.synchronize()
         self.state.copy_(saved)
+        if loss_acc is not None:
+            loss_acc.zero_()
         self.noise_ready = False
         self.graphs = (g_fb, g_adam, g_rest, g_main, g_all)
         self.timing = timing

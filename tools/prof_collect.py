@@ -6,6 +6,8 @@ that gpurun_out/ stays well under the copy-back limit, then delete the raw datab
                        MinNs, MaxNs), sorted by total time
   pmc   DIR OUT.json   per-kernel average (over dispatches) of every collected counter, plus the
                        dispatch count and the kernels' average duration when the db holds it
+  timeline DIR OUT.csv the last 80 kernel dispatches in start order: name, start and duration (ns)
+                       and the idle gap before each (launch boundaries inside a graph replay)
 """
 import csv
 import glob
@@ -60,9 +62,29 @@ def pmc(d, out):
     json.dump(res, open(out, 'w'), indent=1, sort_keys=True)
 
 
+def timeline(d, out, last=80):
+    rows = []
+    for db in dbs_of(d):
+        c = sqlite3.connect(db)
+        cur = c.execute('select * from kernels limit 1')
+        cols = [x[0] for x in cur.description]
+        st = next(x for x in cols if x in ('start', 'start_ns', 'begin', 'start_timestamp'))
+        en = next(x for x in cols if x in ('end', 'end_ns', 'stop', 'end_timestamp'))
+        rows += c.execute(f'select name, {st}, {en} from kernels').fetchall()
+    rows.sort(key=lambda r: r[1])
+    rows = rows[-last:]
+    with open(out, 'w', newline='') as f:
+        w = csv.writer(f)
+        w.writerow(['Name', 'StartNs', 'DurationNs', 'GapBeforeNs'])
+        prev = None
+        for name, s0, e0 in rows:
+            w.writerow([name[:100], s0 - rows[0][1], e0 - s0, (s0 - prev) if prev is not None else 0])
+            prev = e0
+
+
 def main():
     mode, d, out = sys.argv[1:4]
-    (stats if mode == 'stats' else pmc)(d, out)
+    {'stats': stats, 'pmc': pmc, 'timeline': timeline}[mode](d, out)
     shutil.rmtree(d, ignore_errors=True)
 
 
