@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of one kernel from the reduced PMC passes (tools/prof_collect.py pmc
+outputs of separate FETCH_SIZE and WRITE_SIZE runs): bytes = 2 x FETCH_SIZE x 1024 (gfx950: FETCH_SIZE
+counts half the bytes of 16-B/lane streaming reads; KB) + WRITE_SIZE x 1024 (MI355X_MICROARCH.md §HBM).
+
+usage: traffic_from_pmc.py <fetch.json> <write.json> <kernel-substring> <key> <out.json>
+"""
+import json
+import sys
+
+
+def pick(d, sub):
+    ks = [k for k in d if sub in k]
+    if not ks:
+        raise SystemExit(f'no kernel matching {sub!r}')
+    return ks[0], d[ks[0]]
+
+
+def main():
+    fj, wj, sub, key, out = sys.argv[1:6]
+    kn, f = pick(json.load(open(fj)), sub)
+    _, w = pick(json.load(open(wj)), sub)
+    fetch = 2.0 * 1024.0 * float(f['FETCH_SIZE'])
+    write = 1024.0 * float(w['WRITE_SIZE'])
+    res = {key: {'bytes_per_launch': fetch + write, 'fetch_bytes': fetch, 'write_bytes': write,
+                 'kernel': kn, 'dispatches': f.get('dispatches'),
+                 'method': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes (tools/gpu_r03x.sh); '
+                           'FETCH_SIZE x2 (gfx950 16-B/lane read correction), x1024 (KB); per-dispatch averages'}}
+    json.dump(res, open(out, 'w'), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == '__main__':
+    main()
