@@ -45,7 +45,7 @@ def parse():
                     help="collective backend for --gpus > 1 (nccl = RCCL; gloo only to rehearse the "
                          "data-parallel path with several ranks on one GPU)")
     ap.add_argument('--traffic-json', default=os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                                           'profiles', 'traffic_r02f.json'))
+                                                           'profiles', 'traffic_r03x.json'))
     return ap.parse_args()
 
 
@@ -114,6 +114,13 @@ def roofline_for(name, ms, tr):
     if name == 'cc_embed_gather_fwd':
         xs = tr.x_cnt.float().mean().item()
         byt = tr.R * xs * d * 2 + tr.R * d * 2
+        return {'bound': 'hbm', 'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s', 'bytes_per_launch': byt}
+    if name == 'cc_embed_scatter_bwd' and getattr(tr, 'fuse_w1', False):
+        # W1 [V][d]: p, m, v read + written (24 B), bf16 shadow written (2 B); the row bit matrix
+        # (V x ceil(rows/32) words) and the packed dPre1 image (rows x d bf16) read; b1's gradient row
+        rows = getattr(tr, 'xt_rows', tr.R)
+        byt = V * d * 26 + V * ((rows + 31) // 32) * 4 + ((rows + 63) // 64 * 64) * d * 2 + d * 4
         return {'bound': 'hbm', 'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s', 'bytes_per_launch': byt}
     if name == 'cc_embed_scatter_bwd':
@@ -325,7 +332,7 @@ def main():
     n_grad = tr.layout.total if tr.use_reg else tr.layout.main_total
 
     adam_ev = []
-    ADAM_SAMPLE = 25
+    ADAM_SAMPLE = 50
 
     def step(graphed, timed=False):
         if world > 1:   # bucketed reduce-scatter + sharded Adam + all-gather (zero.py)
@@ -337,13 +344,17 @@ def main():
                 tr.step_dp(timing=timed)
             return
         if timed and graphed:
-            # a sampled step: HIP events on the stream bracketing the Adam kernel, launched eagerly
-            # right behind the forward/backward graph (the host is far ahead of the GPU, so the
-            # kernel is queued when e0 fires: the interval is its own duration)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            tr.run_fb()
-            tr.run_adam(events=(e0, e1))
-            adam_ev.append((e0, e1))
+            # a sampled step, launched eagerly with HIP events on the stream around each kernel
+            # (the host is far ahead of the GPU, so every kernel is queued when its start event
+            # fires: each interval is the kernel's own duration); the HBM-bound W1-gradient + W1
+            # Adam kernel and the Adam + F launch are the roofline candidates
+            saved, tr.graphs = tr.graphs, None
+            tr.events, tr.timing = {}, True
+            tr.step()
+            tr.timing, tr.graphs = False, saved
+            for k in ('cc_embed_scatter_bwd', 'cc_adam_dense'):
+                adam_ev.extend((k, e0, e1) for e0, e1 in tr.events.get(k, ()))
+            tr.events = {}
         else:
             saved, tr.graphs = tr.graphs, (tr.graphs if graphed else None)
             tr.step()
@@ -397,14 +408,22 @@ def main():
         return
     value = B * world * args.steps / dt
     if world == 1:
-        adam_ms = float(np.mean([a.elapsed_time(b) for a, b in adam_ev]))
-        roof = roofline_for('cc_adam_dense', adam_ms, tr)
-        roof['measured'] = ('HIP events around the Adam kernel on its stream, every %d-th timed step '
-                            '(eager launch behind the forward/backward graph)' % ADAM_SAMPLE)
+        ms = {k: float(np.mean([a.elapsed_time(b) for kk, a, b in adam_ev if kk == k]))
+              for k in ('cc_embed_scatter_bwd', 'cc_adam_dense') if any(kk == k for kk, _, _ in adam_ev)}
+        # the dominant HBM-bound kernel: the W1-gradient kernel when W1's Adam rides in it and it
+        # takes longer than the Adam launch (the BCE line), else the Adam launch
+        dom = ('cc_embed_scatter_bwd' if getattr(tr, 'fuse_w1', False) and 'cc_embed_scatter_bwd' in ms
+               and ms['cc_embed_scatter_bwd'] >= ms.get('cc_adam_dense', 0.0) else 'cc_adam_dense')
+        adam_ms = ms[dom]
+        roof = roofline_for(dom, adam_ms, tr)
+        roof['measured'] = ('HIP events around the kernel on its stream in every %d-th timed step (an '
+                            'eager step between the multi-step graph replays); other candidate: %s'
+                            % (ADAM_SAMPLE, {k: round(v * 1e3, 2) for k, v in ms.items()}))
         roof['traffic'] = None
         if args.traffic_json and os.path.exists(args.traffic_json):
             # PMC bytes were collected on one configuration: attach them only to the same launch
-            key = 'adam_noise_kernel' if getattr(tr, 'prefetch', False) else 'adam_kernel'
+            key = ('embed_grad_cs_kernel' if dom == 'cc_embed_scatter_bwd' else
+                   'adam_noise_kernel' if getattr(tr, 'prefetch', False) else 'adam_kernel')
             tj = json.load(open(args.traffic_json)).get(key) or {}
             tb = tj.get('bytes_per_launch')
             # (the launch also runs the next step's F: its ~12 MB of batch-buffer traffic rides along)
@@ -412,6 +431,7 @@ def main():
                 roof['traffic'] = tb
                 roof['traffic_detail'] = tj
     else:   # sharded Adam: this rank's 1/world shard of every bucket, per step
+        dom = None
         torch.cuda.synchronize()
         ev = tr.sharded.adam_events
         n_sh = sum(n for _, _, n in ev) / args.steps
@@ -421,7 +441,11 @@ def main():
                 'unit': 'GB/s', 'bytes_per_launch': byt, 'traffic': None,
                 'measured': 'HIP events around the sharded Adam kernels on the comm stream (sum per step)'}
     roof['frac'] = roof['achieved'] / roof['peak']
-    if world == 1 and getattr(tr, 'adam_packs', False):
+    if world == 1 and dom == 'cc_embed_scatter_bwd':
+        roof['kernel'] = ('embed_grad_cs_kernel<.., ADAM> (cc_embed_grad_cs_adam: the W1 gradient X^T dPre1 from '
+                          'the bit-transposed batch on MFMA, TF Adam on W1 in its epilogue; bytes: W1 p/m/v read + '
+                          'write, the bf16 shadow, the bit matrix and the dPre1 image)')
+    elif world == 1 and getattr(tr, 'adam_packs', False):
         roof['kernel'] = ('adam_noise_kernel<true> (cc_adam_noise_pack: TF Adam over all parameters '
                           + ('after W1 (W1\'s Adam runs in the W1-gradient kernel, cc_embed_grad_cs_adam) '
                              if getattr(tr, 'fuse_w1', False) else '')

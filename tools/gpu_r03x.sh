@@ -11,6 +11,19 @@ if [ "$WHAT" = tests ] || [ "$WHAT" = all ]; then
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
   tail -1 $O/smoke.log
 fi
+if [ "$WHAT" = pmc ]; then
+  export TMPDIR=/tmp
+  B="$R/bench.py"
+  pmc() { n=$1; c=$2; shift 2
+    (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $c -d "$O/pmc_$n" -o run -- python3 "$B" --no-cpu-baseline --no-recommend "$@" > "$O/pmc_$n.log" 2>&1) || { echo "pmc $n failed"; tail -5 "$O/pmc_$n.log"; exit 1; }
+    python3 "$R/tools/prof_collect.py" pmc "$O/pmc_$n" "$O/pmc_$n.json" || exit 1; echo "pmc $n ok"; }
+  pmc fetch FETCH_SIZE --steps 16 --warmup 4
+  pmc write WRITE_SIZE --steps 16 --warmup 4
+  python3 "$R/tools/traffic_from_pmc.py" "$O/pmc_fetch.json" "$O/pmc_write.json" "$O/traffic_r03x.json" \
+    adam_noise_kernel:adam_noise_kernel embed_grad_cs_kernel:embed_grad_cs_kernel || exit 1
+  timeout -k 10 400 python -u bench.py --traffic-json $O/traffic_r03x.json > $O/bench_base.log 2>&1 || { tail -5 $O/bench_base.log; exit 1; }
+  tail -1 $O/bench_base.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['ms_per_step']*1e3,1), 'us/step', json.dumps(d['roofline']))"
+fi
 if [ "$WHAT" = prof ] || [ "$WHAT" = all ]; then
   export TMPDIR=/tmp
   B="$R/bench.py"
@@ -28,7 +41,8 @@ if [ "$WHAT" = prof ] || [ "$WHAT" = all ]; then
   pmc fetch FETCH_SIZE --steps 16 --warmup 4
   pmc write WRITE_SIZE --steps 16 --warmup 4
   pmc mfma "SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE" --steps 16 --warmup 4
-  python3 "$R/tools/traffic_from_pmc.py" "$O/pmc_fetch.json" "$O/pmc_write.json" adam_noise_kernel adam_noise_kernel "$O/traffic_r03x.json" || exit 1
+  python3 "$R/tools/traffic_from_pmc.py" "$O/pmc_fetch.json" "$O/pmc_write.json" "$O/traffic_r03x.json" \
+    adam_noise_kernel:adam_noise_kernel embed_grad_cs_kernel:embed_grad_cs_kernel || exit 1
 fi
 if [ "$WHAT" = bench ] || [ "$WHAT" = all ]; then
   TJ=$O/traffic_r03x.json; [ -f $TJ ] || TJ=$R/profiles/traffic_r03x.json

@@ -3,7 +3,7 @@
 outputs of separate FETCH_SIZE and WRITE_SIZE runs): bytes = 2 x FETCH_SIZE x 1024 (gfx950: FETCH_SIZE
 counts half the bytes of 16-B/lane streaming reads; KB) + WRITE_SIZE x 1024 (MI355X_MICROARCH.md §HBM).
 
-usage: traffic_from_pmc.py <fetch.json> <write.json> <kernel-substring> <key> <out.json>
+usage: traffic_from_pmc.py <fetch.json> <write.json> <out.json> <kernel-substring>:<key> [...]
 """
 import json
 import sys
@@ -17,15 +17,20 @@ def pick(d, sub):
 
 
 def main():
-    fj, wj, sub, key, out = sys.argv[1:6]
-    kn, f = pick(json.load(open(fj)), sub)
-    _, w = pick(json.load(open(wj)), sub)
-    fetch = 2.0 * 1024.0 * float(f['FETCH_SIZE'])
-    write = 1024.0 * float(w['WRITE_SIZE'])
-    res = {key: {'bytes_per_launch': fetch + write, 'fetch_bytes': fetch, 'write_bytes': write,
-                 'kernel': kn, 'dispatches': f.get('dispatches'),
-                 'method': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes (tools/gpu_r03x.sh); '
-                           'FETCH_SIZE x2 (gfx950 16-B/lane read correction), x1024 (KB); per-dispatch averages'}}
+    fj, wj, out = sys.argv[1:4]
+    F, W = json.load(open(fj)), json.load(open(wj))
+    res = {}
+    for spec in sys.argv[4:]:
+        sub, key = spec.split(':')
+        kn, f = pick(F, sub)
+        _, w = pick(W, sub)
+        fetch = 2.0 * 1024.0 * float(f['FETCH_SIZE'])
+        write = 1024.0 * float(w['WRITE_SIZE'])
+        res[key] = {'bytes_per_launch': fetch + write, 'fetch_bytes': fetch, 'write_bytes': write,
+                    'kernel': kn, 'dispatches': f.get('dispatches'),
+                    'method': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes '
+                              '(tools/gpu_r03x.sh); FETCH_SIZE x2 (gfx950 16-B/lane read correction), '
+                              'x1024 (KB); per-dispatch averages'}
     json.dump(res, open(out, 'w'), indent=1)
     print(json.dumps(res))
 
