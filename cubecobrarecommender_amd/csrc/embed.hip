@@ -662,6 +662,9 @@ __device__ __forceinline__ void eg_st(cc_adam::f32x4_t *q, cc_adam::f32x4_t v) {
 // ADAM: TF Adam on W1 in the tile epilogue (one process: the gradient is final here) — p, m, v
 // stream through once, the bf16 shadow is rewritten, the W1 gradient is never stored; the bias
 // row's gradient still goes to bias_grad for the main Adam launch
+#ifndef EG_PREFETCH
+#define EG_PREFETCH 1
+#endif
 struct CsAdam {
   float *p, *m, *v;      // W1 rows of the flat fp32 buffers ([V][d])
   bf16_t *shadow;        // W1 rows of the bf16 shadow
@@ -777,24 +780,35 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
     omb1 = 1.f - ad.b1;
     omb2 = 1.f - ad.b2;
   }
-  auto tile = [&](int t, const uint32_t (&wd)[XWM]) {
-    const int vr = v0 + 32 * t + (lane & 31);
-    // Adam operands of this lane's 16 elements, issued before the MFMAs (unconditional: a
-    // clamped row, stored only for real rows)
-    // (the Adam epilogue works on the tile re-laid through LDS: instruction g covers tile rows
-    // 8 g .. 8 g + 7, lane l row 8 g + (l >> 3), columns 4 (l & 7) .. +3 — eight whole 128-B lines
-    // per wave instruction instead of 32 partial ones)
-    cc_adam::f32x4_t ap[ADAM ? 4 : 1], am[ADAM ? 4 : 1], av[ADAM ? 4 : 1];
-    if constexpr (ADAM) {
+  // Adam operands of a tile's 16 elements per lane (unconditional: a clamped row, stored only for
+  // real rows), double-buffered: tile i + 1's are issued before tile i's epilogue, so its load
+  // latency runs under that epilogue and tile i + 1's MFMAs (EG_PREFETCH, R <= 512: the taller
+  // instances have no registers left for the second buffer; else before the MFMAs)
+  // (the Adam epilogue works on the tile re-laid through LDS: instruction g covers tile rows
+  // 8 g .. 8 g + 7, lane l row 8 g + (l >> 3), columns 4 (l & 7) .. +3 — eight whole 128-B lines
+  // per wave instruction instead of 32 partial ones)
+  constexpr bool PF = ADAM && EG_PREFETCH && XWM <= 16;
+  constexpr int NBUF = PF ? 2 : 1;
+  cc_adam::f32x4_t AP[NBUF][ADAM ? 4 : 1], AM[NBUF][ADAM ? 4 : 1], AV[NBUF][ADAM ? 4 : 1];
+  auto issue_adam = [&](int t, int b) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int vg = v0 + 32 * t + 8 * g + (lane >> 3);
-        const int64_t rb = (int64_t)(vg < V ? vg : V - 1) * d + 32 * cs + 4 * (lane & 7);
-        ap[g] = eg_ld(reinterpret_cast<const cc_adam::f32x4_t *>(ad.p + rb));
-        am[g] = eg_ld(reinterpret_cast<const cc_adam::f32x4_t *>(ad.m + rb));
-        av[g] = eg_ld(reinterpret_cast<const cc_adam::f32x4_t *>(ad.v + rb));
-      }
+    for (int g = 0; g < 4; ++g) {
+      const int vg = v0 + 32 * t + 8 * g + (lane >> 3);
+      const int64_t rb = (int64_t)(vg < V ? vg : V - 1) * d + 32 * cs + 4 * (lane & 7);
+      AP[b][g] = eg_ld(reinterpret_cast<const cc_adam::f32x4_t *>(ad.p + rb));
+      AM[b][g] = eg_ld(reinterpret_cast<const cc_adam::f32x4_t *>(ad.m + rb));
+      AV[b][g] = eg_ld(reinterpret_cast<const cc_adam::f32x4_t *>(ad.v + rb));
     }
+  };
+  if constexpr (PF) {
+    if (w < nt) issue_adam(w, 0);
+  }
+  auto tile = [&](int t, const uint32_t (&wd)[XWM], int b, int tn) {
+    const int vr = v0 + 32 * t + (lane & 31);
+    if constexpr (ADAM && !PF) issue_adam(t, 0);
+    cc_adam::f32x4_t(&ap)[ADAM ? 4 : 1] = AP[NBUF == 2 ? b : 0];
+    cc_adam::f32x4_t(&am)[ADAM ? 4 : 1] = AM[NBUF == 2 ? b : 0];
+    cc_adam::f32x4_t(&av)[ADAM ? 4 : 1] = AV[NBUF == 2 ? b : 0];
     f32x16_t acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -831,6 +845,9 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
     // With the dPre1 fragments as the MFMA's A operand and the bit fragments as its B operand (the
     // same registers), lane l holds W1 row v0 + 32 t + (l & 31) and the slice's columns
     // 8 g + 4 (l >> 5) .. +3, g = 0..3: four 16-B stores per lane instead of sixteen 4-B ones.
+    if constexpr (PF) {
+      if (tn < nt) issue_adam(tn, b ^ 1);  // the next tile's operands fly during this epilogue
+    }
     if constexpr (ADAM) {
       float *T = tx + w * (32 * 36);  // this wave's 32 x 32 tile, row pitch 36 floats
 #pragma unroll
@@ -876,7 +893,7 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
   };
 #pragma unroll
   for (int i = 0; i < TPW; ++i)
-    if (w + NW * i < nt) tile(w + NW * i, wds[i]);
+    if (w + NW * i < nt) tile(w + NW * i, wds[i], i & 1, w + NW * (i + 1));
   EG_PROBE(3);
   if (tickets) {  // (no tickets: the caller rewrites every xt word before the next use)
     if (tid == 0) last = tk == (uint32_t)(nsl - 1);
