@@ -102,8 +102,8 @@ def roofline_for(name, ms, tr):
         n = tr.layout.total if tr.use_reg else tr.layout.main_total
         if getattr(tr, 'fuse_w1', False):     # W1's Adam runs in its gradient kernel
             n -= tr.w1_off
-        if getattr(tr, 'wo_range', None):     # [Wo, bo]'s in the tower backward launch
-            n -= tr.wo_range[1] - tr.wo_range[0]
+        for lo, hi in (getattr(tr, 'wo_ranges', None) or ()):   # (the output layers' tails: in the
+            n -= hi - lo                                          # tower backward launch)
         byt = n * (16 + 12 + 2)                    # read p,m,v,g; write p,m,v; write bf16 shadow
         return {'bound': 'hbm', 'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
                 'unit': 'GB/s', 'bytes_per_launch': byt}

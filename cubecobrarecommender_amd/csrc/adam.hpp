@@ -23,6 +23,7 @@ struct Args {
   bf16_t *shadow;
   int64_t n;
   float lr, b1, b2, eps;
+  int64_t eoff;  // element offset of p from the base the Pack's layer offsets count from
 };
 
 // Fragment-packed tower images (cc_adam_pack): the bf16 values of float4 group e..e+3 (one row
@@ -95,7 +96,7 @@ __device__ __forceinline__ void range(const Args &a, int64_t step, int bid, int 
       reinterpret_cast<ushort4 *>(a.shadow)[i] = s;
       if (pk) {
         const bf16_t b4[4] = {s.x, s.y, s.z, s.w};
-        pack4(*pk, i << 2, b4);
+        pack4(*pk, a.eoff + (i << 2), b4);
       }
     }
   }

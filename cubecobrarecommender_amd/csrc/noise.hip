@@ -302,13 +302,16 @@ __global__ __launch_bounds__(NT) void noise_kernel(cc_noise_args a) {
 // released — one launch instead of F on the next step's critical path.
 template <bool PACK>
 __global__ __launch_bounds__(NT) void adam_noise_kernel(cc_adam::Args ad, cc_noise_args a,
-                                                        int nadam, int64_t bpe, cc_adam::Pack pk) {
+                                                        int nadam, int64_t bpe, cc_adam::Pack pk,
+                                                        cc_adam::Args ad1, int nadam1) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   __shared__ int s_k;
   // F's blocks come first: they are latency-bound chains that should start at once, the Adam
-  // blocks stream around them
+  // blocks (of the first flat range, then of the second, if any) stream around them
   const int64_t step = a.state[0];
-  if ((int)blockIdx.x >= a.B) {
+  if ((int)blockIdx.x >= a.B + nadam) {
+    cc_adam::range(ad1, step, (int)blockIdx.x - a.B - nadam, nadam1, PACK ? &pk : nullptr);
+  } else if ((int)blockIdx.x >= a.B) {
     cc_adam::range(ad, step, (int)blockIdx.x - a.B, nadam, PACK ? &pk : nullptr);
   } else {
     int64_t batch = a.state[1] + 1, epoch = a.state[2];
@@ -374,18 +377,20 @@ extern "C" int cc_adam_noise(float *p, float *m, float *v, const float *g, uint1
   const int nadam = n > 0 ? (int)cdiv(cdiv(n, 4), NT) : 0;
   const cc_adam::Args ad{p, m, v, g, (bf16_t *)shadow, n, lr, beta1, beta2, eps};
   hipLaunchKernelGGL(adam_noise_kernel<false>, dim3((unsigned)(nadam + next->B)), dim3(NT), lds,
-                     as_stream(stream), ad, *next, nadam, batches_per_epoch, cc_adam::Pack{});
+                     as_stream(stream), ad, *next, nadam, batches_per_epoch, cc_adam::Pack{}, cc_adam::Args{}, 0);
   CC_LAUNCH_CHECK("adam_noise_kernel");
   return CC_OK;
 }
 
-extern "C" int cc_adam_noise_pack(float *p, float *m, float *v, const float *g, uint16_t *shadow,
-                                  int64_t n, float lr, float beta1, float beta2, float eps,
-                                  const cc_noise_args *next, int64_t batches_per_epoch,
-                                  const cc_adam_pack *pack, void *stream) {
+extern "C" int cc_adam_noise_pack2(float *p, float *m, float *v, const float *g, uint16_t *shadow,
+                                   int64_t lo0, int64_t n0, int64_t lo1, int64_t n1, float lr, float beta1,
+                                   float beta2, float eps, const cc_noise_args *next, int64_t batches_per_epoch,
+                                   const cc_adam_pack *pack, void *stream) {
   CC_REQUIRE(p && m && v && g && shadow && pack, "cc_adam_noise_pack: null pointer");
-  CC_REQUIRE(((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g) % 16 == 0,
-             "cc_adam_noise_pack: buffers must be 16-byte aligned");
+  CC_REQUIRE(((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g) % 16 == 0 && lo0 % 4 == 0 && lo1 % 4 == 0,
+             "cc_adam_noise_pack: buffers must be 16-byte aligned, range starts multiples of 4");
+  CC_REQUIRE(lo0 >= 0 && n0 >= 0 && n1 >= 0 && (n1 == 0 || lo1 >= lo0 + n0), "cc_adam_noise_pack2: ranges");
+  const int64_t n = n1 > 0 ? lo1 + n1 : lo0 + n0;  // the extent the pack's layers must lie in
   CC_REQUIRE((uintptr_t)shadow % 8 == 0, "cc_adam_noise_pack: shadow must be 8-byte aligned");
   CC_REQUIRE(batches_per_epoch >= 1, "cc_adam_noise_pack: batches_per_epoch");
   CC_REQUIRE(pack->n >= 1 && pack->n <= 9, "cc_adam_noise_pack: 1..9 layers");
@@ -409,10 +414,24 @@ extern "C" int cc_adam_noise_pack(float *p, float *m, float *v, const float *g, 
   }
   size_t lds = 0;
   if (int rc = noise_check(next, lds)) return rc;
-  const int nadam = n > 0 ? (int)cdiv(cdiv(n, 4), NT) : 0;
-  const cc_adam::Args ad{p, m, v, g, (bf16_t *)shadow, n, lr, beta1, beta2, eps};
-  hipLaunchKernelGGL(adam_noise_kernel<true>, dim3((unsigned)(nadam + next->B)), dim3(NT), lds,
-                     as_stream(stream), ad, *next, nadam, batches_per_epoch, pk);
+  for (int l = 0; l < pack->n; ++l)  // every packed layer inside one of the two ranges
+    CC_REQUIRE((pack->off[l] >= lo0 && pack->off[l] + (int64_t)pack->K[l] * pack->N[l] <= lo0 + n0) ||
+                   (pack->off[l] >= lo1 && pack->off[l] + (int64_t)pack->K[l] * pack->N[l] <= lo1 + n1),
+               "cc_adam_noise_pack2: a packed layer outside the Adam ranges");
+  const int nadam = n0 > 0 ? (int)cdiv(cdiv(n0, 4), NT) : 0;
+  const int nadam1 = n1 > 0 ? (int)cdiv(cdiv(n1, 4), NT) : 0;
+  const cc_adam::Args ad{p + lo0, m + lo0, v + lo0, g + lo0, (bf16_t *)shadow + lo0, n0, lr, beta1, beta2, eps, lo0};
+  const cc_adam::Args ad1{p + lo1, m + lo1, v + lo1, g + lo1, (bf16_t *)shadow + lo1, n1, lr, beta1, beta2, eps, lo1};
+  hipLaunchKernelGGL(adam_noise_kernel<true>, dim3((unsigned)(nadam + nadam1 + next->B)), dim3(NT), lds,
+                     as_stream(stream), ad, *next, nadam, batches_per_epoch, pk, ad1, nadam1);
   CC_LAUNCH_CHECK("adam_noise_kernel (pack)");
   return CC_OK;
+}
+
+extern "C" int cc_adam_noise_pack(float *p, float *m, float *v, const float *g, uint16_t *shadow,
+                                  int64_t n, float lr, float beta1, float beta2, float eps,
+                                  const cc_noise_args *next, int64_t batches_per_epoch,
+                                  const cc_adam_pack *pack, void *stream) {
+  return cc_adam_noise_pack2(p, m, v, g, shadow, 0, n, 0, 0, lr, beta1, beta2, eps, next, batches_per_epoch,
+                             pack, stream);
 }

@@ -546,9 +546,10 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
 // the 16-32 latency-bound chain blocks leave idle; the chains launch first, so they start at once.
 template <int D, bool ADAM>
 __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p, cc_adam::Args ad,
-                                                                   const int64_t *ad_state) {
-  if (ADAM && (int)blockIdx.x >= p.R / RB) {
+                                                                   cc_adam::Args ad1, const int64_t *ad_state) {
+  if (ADAM && (int)blockIdx.x >= p.R / RB) {  // (two flat ranges, one after the other)
     cc_adam::range_u<4>(ad, ad_state[0], (int)blockIdx.x - p.R / RB, (int)gridDim.x - p.R / RB);
+    if (ad1.n > 0) cc_adam::range_u<4>(ad1, ad_state[0], (int)blockIdx.x - p.R / RB, (int)gridDim.x - p.R / RB);
     return;
   }
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1364,7 +1365,7 @@ extern "C" int cc_tower_fwd(const cc_tower_args *t, void *stream) {
 
 static int tower_bwd_launch(const cc_tower_args *t, void *stream, bool chain, bool dw,
                             const cc_adam::Args *ad = nullptr, const int64_t *ad_state = nullptr,
-                            int ad_blocks = 0) {
+                            int ad_blocks = 0, const cc_adam::Args *ad1 = nullptr) {
   TowerP p;
   int rc = make_params(t, p);
   if (rc) return rc;
@@ -1377,15 +1378,15 @@ static int tower_bwd_launch(const cc_tower_args *t, void *stream, bool chain, bo
   hipStream_t s = as_stream(stream);
   if (t->dtype == CC_BF16) {
     if (chain && p.d <= 256) {
-      const cc_adam::Args a0 = ad ? *ad : cc_adam::Args{};
+      const cc_adam::Args a0 = ad ? *ad : cc_adam::Args{}, a1 = ad1 ? *ad1 : cc_adam::Args{};
       const dim3 ga(gc.x + (ad ? ad_blocks : 0));
 #define CHAIN_FAST(DD)                                                                              \
   if (ad)                                                                                           \
     hipLaunchKernelGGL((tower_bwd_chain_fast_kernel<DD, true>), ga, dim3(FNT), lds_chain, s, p, a0, \
-                       ad_state);                                                                   \
+                       a1, ad_state);                                                               \
   else                                                                                              \
     hipLaunchKernelGGL((tower_bwd_chain_fast_kernel<DD, false>), gc, dim3(FNT), lds_chain, s, p, a0, \
-                       ad_state);
+                       a1, ad_state);
       switch (p.d) {
         case 64: CHAIN_FAST(64) break;
         case 128: CHAIN_FAST(128) break;
@@ -1414,17 +1415,22 @@ extern "C" int cc_tower_bwd_chain(const cc_tower_args *t, void *stream) {
   return tower_bwd_launch(t, stream, true, false);
 }
 extern "C" int cc_tower_bwd_chain_adam(const cc_tower_args *t, float *p, float *m, float *v, const float *g,
-                                       uint16_t *shadow, int64_t n, const int64_t *state, float lr,
-                                       float beta1, float beta2, float eps, void *stream) {
+                                       uint16_t *shadow, int64_t lo0, int64_t n0, int64_t lo1, int64_t n1,
+                                       const int64_t *state, float lr, float beta1, float beta2, float eps,
+                                       void *stream) {
   CC_REQUIRE(t && t->dtype == CC_BF16 && t->d <= 256,
              "cc_tower_bwd_chain_adam: the bf16 fast chains (d <= 256) only");
   CC_REQUIRE(p && m && v && g && state, "cc_tower_bwd_chain_adam: null pointer");
-  CC_REQUIRE(((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g) % 16 == 0,
-             "cc_tower_bwd_chain_adam: buffers must be 16-byte aligned");
+  CC_REQUIRE(((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g) % 16 == 0 && lo0 % 4 == 0 && lo1 % 4 == 0,
+             "cc_tower_bwd_chain_adam: buffers must be 16-byte aligned, range starts multiples of 4");
   CC_REQUIRE(!shadow || (uintptr_t)shadow % 8 == 0, "cc_tower_bwd_chain_adam: shadow must be 8-byte aligned");
-  CC_REQUIRE(n >= 0, "cc_tower_bwd_chain_adam: n");
+  CC_REQUIRE(lo0 >= 0 && n0 >= 0 && n1 >= 0 && (n1 == 0 || lo1 >= lo0 + n0), "cc_tower_bwd_chain_adam: ranges");
+  const int64_t n = n0 + n1;
   if (n == 0) return tower_bwd_launch(t, stream, true, false);
-  const cc_adam::Args a{p, m, v, g, (bf16_t *)shadow, n, lr, beta1, beta2, eps};
+  const cc_adam::Args a{p + lo0, m + lo0, v + lo0, g + lo0, shadow ? (bf16_t *)shadow + lo0 : nullptr, n0,
+                        lr, beta1, beta2, eps, lo0};
+  const cc_adam::Args a1{p + lo1, m + lo1, v + lo1, g + lo1, shadow ? (bf16_t *)shadow + lo1 : nullptr, n1,
+                         lr, beta1, beta2, eps, lo1};
   // one 512-thread block per CU beside the chains (their VGPR budget admits one per CU), capped
   // so no block runs out of work
   static int cus = 0;
@@ -1436,7 +1442,7 @@ extern "C" int cc_tower_bwd_chain_adam(const cc_tower_args *t, float *p, float *
   }
   const int64_t want = cdiv(cdiv(n, 4), (int64_t)FNT * 4);
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(cus - t->R / RB, 8)));
-  return tower_bwd_launch(t, stream, true, false, &a, state, blocks);
+  return tower_bwd_launch(t, stream, true, false, &a, state, blocks, &a1);
 }
 extern "C" int cc_tower_bwd_dw(const cc_tower_args *t, void *stream) {
   return tower_bwd_launch(t, stream, false, true);

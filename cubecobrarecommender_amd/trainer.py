@@ -41,9 +41,11 @@ class TrainConfig:
     reg_shard: bool = False        # data parallel + reg: M~ row-sharded, owner computes
     fuse_w1_adam: bool = False     # one process: TF Adam on W1 inside the W1-gradient kernel (its
     #                                gradient is then never stored; bench.py turns it on)
-    wo_adam_in_tower: bool = False  # with fuse_w1_adam, BCE only, bf16 d <= 256: TF Adam on the decoder
-    #                                output layer in the tower backward launch (bench.py turns it on)
-    wo_tower_frac: float = 0.6     # ... on this trailing fraction of it; the rest stays in the Adam + F launch
+    wo_adam_in_tower: bool = False  # with fuse_w1_adam, bf16 d <= 256 (fused output layers): TF Adam on
+    #                                the decoder output layers' tails in the tower backward launch (bench.py)
+    wo_tower_frac: float = -1.0    # ... on this trailing fraction of each; the rest stays in the Adam + F
+    #                                launch (< 0: measured per mode — 0.6 BCE only, 0.45 with the
+    #                                sampled regulariser; tools/gpu_t8.sh, tools/gpu_t15.sh sweeps)
     graph_steps: int = 8           # one process: consecutive steady-state steps per hipGraph replay (step_many)
     reg_mode: str = 'sampled'      # 'sampled': B reg rows per step drawn ∝ neg_sampler (generator.py:47-51);
     #                                'full': all |V| identity rows every step, KL(M~, D2(E(I))) as the
@@ -414,20 +416,31 @@ class Trainer:
         self.fuse_w1 = (cfg.fuse_w1_adam and self.adam_packs and self.eg_tickets is not None and not self.full_reg
                         and self.layout.offset('encoder/encoded_1/kernel') == 0)
         self.adam_pack = self._adam_pack_desc() if self.adam_packs else None
-        # TF Adam on the decoder output layer (Wo, bo: ~96% of the parameters after W1) in extra
-        # workgroups of the tower backward launch (cc_tower_bwd_chain_adam): its gradient is final
-        # after cc_dec_bce_dw and dX has read its bf16 shadow, and the 16-32 latency-bound chain
-        # blocks leave the other CUs idle.  Only its trailing wo_tower_frac: the main Adam launch
-        # (which also runs the next step's F, latency-bound too) keeps [W1 end, split) to stream
-        # beside F.
-        self.wo_range = None
-        if (cfg.wo_adam_in_tower and self.fuse_w1 and not self.use_reg and self.fused_out
+        # TF Adam on the decoder output layers (Wo, bo, and with the sampled regulariser Wo_reg, bo_reg:
+        # ~96% of the parameters after W1) in extra workgroups of the tower backward launch
+        # (cc_tower_bwd_chain_adam): their gradients are final after the output-layer kernels, the dX
+        # products have read their bf16 shadows, and the 16-32 latency-bound chain blocks leave the
+        # other CUs idle.  Only their trailing wo_tower_frac: the main Adam launch (which also runs
+        # the next step's F, latency-bound too) keeps the rest to stream beside F.  wo_ranges: the
+        # tower launch's [lo, hi) flat ranges; rest_ranges: the Adam launch's (W1 end onwards).
+        self.wo_ranges, self.rest_ranges = None, None
+        if (cfg.wo_adam_in_tower and self.fuse_w1 and self.fused_out and (not self.use_reg or self.fused_reg)
                 and self.targs is not None and self.dtype == L.CC_BF16 and cfg.d <= 256):
-            lo, hi = self.layout.offset('decoder/reconstruct/kernel'), self.layout.main_total
-            frac = float(os.environ.get('CCREC_WO_TOWER_FRAC', cfg.wo_tower_frac))   # (dev A/B knob)
-            split = hi - int((hi - lo) * min(max(frac, 0.0), 1.0)) // 256 * 256
-            if split < hi:
-                self.wo_range = (split, hi)
+            frac = cfg.wo_tower_frac if cfg.wo_tower_frac >= 0 else (0.45 if self.use_reg else 0.6)
+            frac = min(max(float(os.environ.get('CCREC_WO_TOWER_FRAC', frac)), 0.0), 1.0)  # (dev A/B knob)
+            lay = self.layout
+            spans = [(lay.offset('decoder/reconstruct/kernel'), lay.main_total)]
+            if self.use_reg:
+                spans.append((lay.offset('decoder_for_reg/reconstruct/kernel'), lay.total))
+            wo = [(hi - int((hi - lo) * frac) // 256 * 256, hi) for lo, hi in spans]
+            if all(a < b for a, b in wo):
+                self.wo_ranges = wo
+                rest, lo = [], self.w1_off
+                for a, b in wo:        # the complement inside [W1 end, end of the Adam range)
+                    rest.append((lo, a))
+                    lo = b
+                self.rest_ranges = rest
+        self.wo_range = self.wo_ranges[0] if self.wo_ranges else None   # (tests: is the placement on)
         self._adv_deferred = False   # the previous step's counter advance rides in the E1 gather
         self.noise_ready = False
         self.perms = None
@@ -891,12 +904,11 @@ class Trainer:
         s = self._s
         if self.fused_tower:
             t = self._tick('cc_tower_bwd')
-            if self.wo_range is not None:   # + TF Adam on [Wo, bo] beside the chains
-                lo, hi = self.wo_range
-                L.call('cc_tower_bwd_chain_adam', L.C.byref(self.targs), L.ptr(self.params[lo:]),
-                       L.ptr(self.m[lo:]), L.ptr(self.v[lo:]), L.ptr(self.grads[lo:]),
-                       L.ptr(self.shadow[lo:]), hi - lo, L.ptr(self.state), cfg.lr, cfg.beta1,
-                       cfg.beta2, cfg.eps, s)
+            if self.wo_ranges is not None:   # + TF Adam on the output layers' tails beside the chains
+                (a0, b0), (a1, b1) = self.wo_ranges[0], (self.wo_ranges + [(0, 0)])[1]
+                L.call('cc_tower_bwd_chain_adam', L.C.byref(self.targs), L.ptr(self.params), L.ptr(self.m),
+                       L.ptr(self.v), L.ptr(self.grads), L.ptr(self.shadow), a0, b0 - a0, a1, b1 - a1,
+                       L.ptr(self.state), cfg.lr, cfg.beta1, cfg.beta2, cfg.eps, s)
             else:
                 L.call('cc_tower_bwd_chain', L.C.byref(self.targs), s)
             t()
@@ -952,12 +964,17 @@ class Trainer:
         """TF Adam over every trained parameter (+ bf16 shadow refresh)."""
         cfg = self.cfg
         n = self.layout.total if self.use_reg else self.layout.main_total
-        if self.wo_range is not None:   # [Wo, bo] updated in the tower backward launch
-            n = self.wo_range[0]
         t = self._tick('cc_adam_dense')
         if self.prefetch:     # + F for the next step in the same launch
             na = self._noise_args()
-            if self.adam_packs:   # + packed tower images + step counters
+            if self.adam_packs and self.rest_ranges is not None:   # the complement of the tower launch's
+                o = self.w1_off                                      # ranges (pack offsets count from o)
+                (a0, b0), (a1, b1) = self.rest_ranges[0], (self.rest_ranges + [(o, o)])[1]
+                L.call('cc_adam_noise_pack2', L.ptr(self.params[o:]), L.ptr(self.m[o:]), L.ptr(self.v[o:]),
+                       L.ptr(self.grads[o:]), L.ptr(self.shadow[o:]), a0 - o, b0 - a0, a1 - o, b1 - a1,
+                       cfg.lr, cfg.beta1, cfg.beta2, cfg.eps, L.C.byref(na), self.batches_per_epoch,
+                       L.C.byref(self.adam_pack), L.stream_ptr(stream))
+            elif self.adam_packs:   # + packed tower images + step counters
                 o = self.w1_off if self.fuse_w1 else 0   # (W1 already updated by its gradient kernel)
                 L.call('cc_adam_noise_pack', L.ptr(self.params[o:]), L.ptr(self.m[o:]), L.ptr(self.v[o:]),
                        L.ptr(self.grads[o:]), L.ptr(self.shadow[o:]), n - o, cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,
@@ -1112,7 +1129,7 @@ class Trainer:
         s.wait_stream(torch.cuda.current_stream())
         saved = self.state.clone()
         # the fused W1 (and Wo) Adam updates them inside forward_backward: undo the warm-up's update
-        spans = ([(0, self.w1_off)] if self.fuse_w1 else []) + ([self.wo_range] if self.wo_range else [])
+        spans = ([(0, self.w1_off)] if self.fuse_w1 else []) + (list(self.wo_ranges) if self.wo_ranges else [])
         saved_spans = [[b[lo:hi].clone() for b in (self.params, self.m, self.v, self.shadow)] for lo, hi in spans]
         with torch.cuda.stream(s):           # warm-up launch outside capture (lazy module loads)
             self.forward_backward()

@@ -140,6 +140,13 @@ typedef struct cc_adam_pack {
 int cc_adam_noise_pack(float *p, float *m, float *v, const float *g, uint16_t *shadow, int64_t n,
                        float lr, float beta1, float beta2, float eps, const cc_noise_args *next,
                        int64_t batches_per_epoch, const cc_adam_pack *pack, void *stream);
+/* cc_adam_noise_pack over the two flat ranges [lo0, lo0 + n0) and [lo1, lo1 + n1) of the buffers at
+ * p, m, v, g, shadow (lo1 >= lo0 + n0; n1 may be 0; range starts multiples of 4); pack->off[l]
+ * counts from p and every packed layer lies inside one of the ranges. */
+int cc_adam_noise_pack2(float *p, float *m, float *v, const float *g, uint16_t *shadow, int64_t lo0,
+                        int64_t n0, int64_t lo1, int64_t n1, float lr, float beta1, float beta2, float eps,
+                        const cc_noise_args *next, int64_t batches_per_epoch, const cc_adam_pack *pack,
+                        void *stream);
 
 /* ----------------------------------------------------------------------------------
  * E1 forward: H[r] = ReLU(sum_{j in x_r} W1[j] + b1).  Replaces Dense(d)(x) on the 0/1
@@ -370,13 +377,14 @@ int cc_tower_bwd(const cc_tower_args *t, void *stream);
  * cc_tower_bwd_dw (per-block dW/db slabs); split so the slabs can overlap the E1 scatter. */
 int cc_tower_bwd_chain(const cc_tower_args *t, void *stream);
 /* cc_tower_bwd_chain plus, in extra workgroups of the same launch (on the CUs the 32-row chains
- * leave idle), exactly cc_adam_dense(p, m, v, g, shadow, n, state, lr, beta1, beta2, eps) — for a
- * flat range the chains do not read (the trainer: the decoder output layer, whose gradient is
- * final after cc_dec_bce_dw and whose bf16 shadow the dX product has already consumed).
+ * leave idle), exactly cc_adam_dense over the flat ranges [lo0, lo0 + n0) and [lo1, lo1 + n1) of
+ * p, m, v, g, shadow (lo1 >= lo0 + n0, n1 may be 0, starts multiples of 4) — ranges the chains do
+ * not read (the trainer: trailing parts of the decoder output layers, whose gradients are final
+ * after the output-layer kernels and whose bf16 shadows the dX products have already consumed).
  * bf16 fast chains (d <= 256) only. */
 int cc_tower_bwd_chain_adam(const cc_tower_args *t, float *p, float *m, float *v, const float *g,
-                            uint16_t *shadow, int64_t n, const int64_t *state, float lr, float beta1,
-                            float beta2, float eps, void *stream);
+                            uint16_t *shadow, int64_t lo0, int64_t n0, int64_t lo1, int64_t n1,
+                            const int64_t *state, float lr, float beta1, float beta2, float eps, void *stream);
 int cc_tower_bwd_dw(const cc_tower_args *t, void *stream);
 int cc_tower_reduce(const cc_tower_args *t, void *stream);
 /* bf16: every layer's dW/db written directly (no slabs, no reduce): cc_tower_bwd_dw +

@@ -85,7 +85,7 @@ def test_bench_configuration_matches_oracle(reg):
     flat = glorot_flat(V, d, seed=42)
     tr = Trainer(cfg, data, params_flat=flat)
     assert tr.fused_out and tr.adam_packs and tr.prefetch and tr.wpack is not None and tr.fuse_w1
-    assert (tr.wo_range is not None) == (reg == 0)
+    assert tr.wo_ranges is not None and len(tr.wo_ranges) == (2 if reg > 0 else 1)
     perm = np.random.default_rng(99).permutation(C).astype(np.int32)
     tr.set_epoch_permutations(perm[None, :])
     tr.capture()

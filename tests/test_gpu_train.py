@@ -330,9 +330,10 @@ def test_fused_w1_adam_matches_unfused(reg):
     """TrainConfig(fuse_w1_adam=True) — bench.py's step: TF Adam on W1 in the column-slice W1-gradient
     kernel's epilogue, the main Adam launch starting after W1 — gives bit-identical parameters,
     bf16 shadow, Adam moments and losses to the unfused step (same cc_adam::elem update, same
-    gradient values), over eager steps and graph replays.  With wo_adam_in_tower as well (BCE
-    only): the decoder output layer's Adam in the tower backward launch (cc_tower_bwd_chain_adam,
-    cc_adam::range_u) — the same bits again."""
+    gradient values), over eager steps and graph replays.  With wo_adam_in_tower as well: the
+    output layers' trailing parts (Wo, and Wo_reg with the regulariser) updated in the tower
+    backward launch (cc_tower_bwd_chain_adam, cc_adam::range_u) and the rest in two ranges of the
+    Adam + F launch (cc_adam_noise_pack2) — the same bits again."""
     out = {}
     for fuse, wo in ((False, False), (True, False), (True, True)):
         lists, Mt, ns = problem(11, 1024, 2500, (20, 40, 80))
@@ -343,7 +344,7 @@ def test_fused_w1_adam_matches_unfused(reg):
         tr = Trainer(cfg, DeviceDataset(lists, 2500, y_mtx=Mt.astype(np.float32) if reg > 0 else None,
                                         neg_sampler=ns), params_flat=lay.pack(P))
         tr.set_epoch_permutation(np.random.default_rng(11).permutation(1024).astype(np.int32))
-        assert tr.fuse_w1 == fuse and tr.adam_packs and (tr.wo_range is not None) == (wo and reg == 0)
+        assert tr.fuse_w1 == fuse and tr.adam_packs and (tr.wo_range is not None) == wo
         losses = []
         for _ in range(2):
             tr.step()
