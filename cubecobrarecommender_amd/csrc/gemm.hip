@@ -976,11 +976,26 @@ static bool nt_path(const cc_gemm_args *g, const GemmParams &p) {
          g->epilogue != CC_EPI_MASK;
 }
 
+// MX-FP8 STORE / split-K / BCE products go to the 256 x 256 LDS-DMA kernel (mx8gemm.hip; bit-identical
+// results).  CCREC_MX8_GEMM=128 (dev A/B switch, read per call) keeps them on the 128 x 128 kernel.
+static bool mx8_wide_ok(const cc_gemm_args *g) {
+  const char *e = getenv("CCREC_MX8_GEMM");
+  if (e && atoi(e) == 128) return false;
+  const bool bce_ok = g->epilogue == CC_EPI_BCE && g->C && (int64_t)g->M * g->ldc * 2 < 0x100000000ll &&
+                      (!g->Ct || ((uintptr_t)g->Ct % 8 == 0 && g->ldct % 4 == 0 && g->M % 4 == 0 &&
+                                  (int64_t)g->N * g->ldct * 2 < 0x80000000ll));
+  return g->dtype == CC_MX8 && (g->epilogue == CC_EPI_STORE || g->epilogue == CC_EPI_SPLITK || bce_ok) &&
+         g->M > 0 && g->N > 0 && !g->relu && !g->colsum && (!g->Ct || bce_ok) &&
+         (int64_t)g->M * g->lda < 0x80000000ll && (int64_t)g->N * g->ldb < 0x80000000ll &&
+         (g->epilogue == CC_EPI_SPLITK || g->ldc >= g->N);
+}
+
 extern "C" int cc_gemm(const cc_gemm_args *g, void *stream) {
   GemmParams p;
   if (int rc = gemm_params(g, p)) return rc;
   if (g->M == 0 || g->N == 0) return CC_OK;
   hipStream_t s = as_stream(stream);
+  if (mx8_wide_ok(g)) return cc_gemm_mx8_wide(g, nullptr, stream);
   if (g->dtype == CC_MX8) {
     switch (g->epilogue) {
       case CC_EPI_STORE: return launch_nt_mx8<CC_EPI_STORE>(g, p, s);
@@ -1013,6 +1028,7 @@ extern "C" int cc_gemm_pair(const cc_gemm_args *g0, const cc_gemm_args *g1, void
     return (nt_path(g, p) || g->dtype == CC_MX8) && g->M > 0 && g->N > 0 &&
            (g->epilogue == CC_EPI_STORE || g->epilogue == CC_EPI_SPLITK);
   };
+  if (mx8_wide_ok(g0) && mx8_wide_ok(g1)) return cc_gemm_mx8_wide(g0, g1, stream);
   if (!pairable(g0, p0) || !pairable(g1, p1) || (g0->dtype == CC_MX8) != (g1->dtype == CC_MX8)) {
     if (int rc = cc_gemm(g0, stream)) return rc;
     return cc_gemm(g1, stream);

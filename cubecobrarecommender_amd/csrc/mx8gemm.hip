@@ -1,0 +1,435 @@
+// MX-FP8 NT GEMM on 256 x 256 tiles with an LDS-DMA stage pipeline — config 5's decoder output
+// layer products (model.py:64 Dense(V) at d = 1024 and its backward, the regulariser's logits
+// model.py:98): C[M][N] = A[M][K] . B[N][K]^T, both operands e4m3 codes K-contiguous with one E8M0
+// scale per 32 K (cc_quant_mx8), v_mfma_scale_f32_32x32x64_f8f6f4, fp32 accumulation.
+//
+// Why a second kernel next to gemm.hip's 128 x 128 register-staged NT kernel: at d = 1024 that
+// kernel reaches ~0.58 PFLOP/s (12 % of the MX-FP8 peak, tools/micro/mx8_bench.py) — a 128 x 128
+// tile with 2 x 2 accumulators per wave reads 2 KB of LDS per MFMA, its register staging leaves
+// few tiles in flight, and the decoder shapes have only 4-8 K-tiles per output tile.  Here:
+//   * 8 waves as 2 (M) x 4 (N); a wave owns 128 x 64 outputs = 4 x 2 accumulators of 32 x 32, so
+//     its 6 fragments per 64-k step feed 8 MFMAs (1.5 KB of LDS per MFMA);
+//   * a K-tile is 128 fp8 of every row: A 256 x 128 B + B 256 x 128 B + the 4 scale bytes of each
+//     row, copied global -> LDS by buffer_load ... lds (16-B chunks, 8 rows x 128 B per wave
+//     instruction; scale words 4 B per lane), two stages: tile t + 1's DMA runs under tile t's
+//     MFMAs.  The LDS images are lane-linear; the 16-B chunk swizzle (chunk ^ row & 7) is applied
+//     on the global source address, so fragment reads are the conflict-free pattern of gemm.hip's
+//     nt_frag8.  Rows past M / N read zeros (their outputs are not stored);
+//   * (tile, split) pairs are dealt to the XCDs in contiguous runs (tiles sharing a B panel, or a
+//     K split's panels, run on one XCD and fetch the panel into its L2 once).
+// The MFMA sequence of every output (k-tiles ascending, two 64-k steps each) is the one gemm.hip's
+// MX kernel runs, so the results are bit-identical to it (tests/test_gpu_kernels.py).
+// Epilogues: STORE (optional bias; fp32 Cf and/or bf16 C), SPLITK (fp32 partials [split][M][N]) and
+// BCE (logits + bias -> sigmoid / BCE: dZ rows and optionally dZ^T in bf16, per-tile loss partials
+// reduced in tile order by the last block when loss_out is set).
+#include <cstdlib>
+
+#include "common.hpp"
+
+namespace {
+
+constexpr int QM = 256, QN = 256, QKB = 128, QNT = 512;
+constexpr int QA_BYTES = QM * QKB, QB_BYTES = QN * QKB;  // 32 KB each
+constexpr int QSTAGE = QA_BYTES + QB_BYTES + (QM + QN) * 4;
+constexpr int QLDS = 2 * QSTAGE;  // 132 KB
+// the BCE epilogue's LDS: a 256 x 129 fp32 pass tile, the 256 x 8 target words, the loss reduction
+constexpr int QLDS_BCE = QM * 129 * 4 + QM * 8 * 4 + 8 * 8 + 16;
+constexpr int QLDS_MAX = QLDS > QLDS_BCE ? QLDS : QLDS_BCE;
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+typedef __attribute__((ext_vector_type(8))) int i32x8_t;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
+
+struct QP {
+  const uint8_t *A, *B, *sa, *sb;
+  const float *bias;
+  bf16_t *C;
+  float *Cf;
+  // BCE epilogue (model.py:94 sigmoid + train.py:85 binary_crossentropy on the logits)
+  const uint32_t *y_bits;  // [M][ceil(N/32)] targets
+  bf16_t *Ct;              // optional dZ^T [N][ldct]
+  double *loss_partials;   // [ntiles]
+  double *loss_out;        // optional: the last block reduces the partials in tile order
+  uint32_t *ticket;
+  double loss_scale;
+  float scale;
+  int ldct;
+  int M, N, K, lda, ldb, ldc, splits, kchunk, tiles_m, ntiles, epi;
+  uint32_t a_bytes, b_bytes, sa_bytes, sb_bytes;
+};
+
+// sigmoid_cross_entropy_with_logits (TF 2.5 Keras BCE on a sigmoid output):
+//   loss = max(z, 0) - z y + log1p(exp(-|z|)),  dz = (sigmoid(z) - y) * scale,
+// from a = exp(-|z|) by the hardware exp2 / rcp (decout.hip's forms).  The log1p terms of a lane's
+// 16 rows are taken as ONE log2 of the product of their 1 + a in (1, 2] (<= 2^16; decout.hip):
+// `lprod` collects the factors, `rsum` the max(+-z, 0) parts; dead elements contribute 1 and 0
+__device__ __forceinline__ float q_bce(float z, uint32_t ybit, float scale, float &lprod, float &rsum, bool live) {
+  constexpr float LOG2E = 1.4426950408889634f;
+  const float a = __builtin_amdgcn_exp2f(-fabsf(z) * LOG2E);
+  const float opa = 1.f + a;
+  const float rp = __builtin_amdgcn_rcpf(opa);
+  lprod *= live ? opa : 1.f;
+  rsum += live ? fmaxf(ybit ? -z : z, 0.f) : 0.f;
+  const float sig = z >= 0.f ? rp : a * rp;
+  return (sig - (float)ybit) * scale;
+}
+
+__device__ __forceinline__ int xcd_run(int b, int nb) {  // bijective: block -> XCD-contiguous id
+  const int q = nb / 8, r = nb % 8, x = b % 8, slot = b / 8;
+  return x < r ? x * (q + 1) + slot : r * (q + 1) + (x - r) * q + slot;
+}
+
+// stage st <- K-tile at k0: wave w moves A rows [32w, 32w + 32) and B rows [32w, 32w + 32) (4 + 4
+// instructions of 8 rows x 128 B), waves 0-3 the A scale words of rows [64w, 64w + 64), waves 4-7
+// the B scale words (one 4-B-per-lane instruction each): 9 DMA instructions per wave per tile
+__device__ __forceinline__ void q_dma(const QP &p, const __amdgpu_buffer_rsrc_t &ra, const __amdgpu_buffer_rsrc_t &rb,
+                                      const __amdgpu_buffer_rsrc_t &rsa, const __amdgpu_buffer_rsrc_t &rsb,
+                                      char *smem, int st, int bm, int bn, int k0) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int rl = lane >> 3, slot = lane & 7;
+  char *sA = smem + st * QSTAGE, *sB = sA + QA_BYTES, *sS = sB + QB_BYTES;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = w * 4 + u;  // rows 8i .. 8i + 7
+    const int row = 8 * i + rl;
+    const int c = slot ^ (row & 7);
+    const uint32_t oa = bm + row < p.M ? (uint32_t)(bm + row) * (uint32_t)p.lda + (uint32_t)(k0 + 16 * c) : 0x80000000u;
+    const uint32_t ob = bn + row < p.N ? (uint32_t)(bn + row) * (uint32_t)p.ldb + (uint32_t)(k0 + 16 * c) : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void *)(sA + i * 1024), 16, oa, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void *)(sB + i * 1024), 16, ob, 0, 0, 0);
+  }
+  const int row = (w & 3) * 64 + lane;
+  if (w < 4) {
+    const uint32_t os = bm + row < p.M ? (uint32_t)(bm + row) * (uint32_t)(p.lda / 32) + (uint32_t)(k0 / 32) : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_void *)(sS + (w & 3) * 256), 4, os, 0, 0, 0);
+  } else {
+    const uint32_t os = bn + row < p.N ? (uint32_t)(bn + row) * (uint32_t)(p.ldb / 32) + (uint32_t)(k0 / 32) : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_void *)(sS + QM * 4 + (w & 3) * 256), 4, os, 0, 0, 0);
+  }
+}
+
+// the 32 x 64 fp8 fragment of rows `row` (lane & 31) for 64-k step kk: lane half h holds k 16h ..
+// 16h + 15 (low 16 B) and 32 + 16h .. (high 16 B) — chunks 4kk + h and 4kk + 2 + h (gemm.hip nt_frag8)
+__device__ __forceinline__ i32x8_t q_frag(const char *S, int row, int c0) {
+  const i32x4_t lo = *reinterpret_cast<const i32x4_t *>(S + row * QKB + ((c0 ^ (row & 7)) << 4));
+  const i32x4_t hi = *reinterpret_cast<const i32x4_t *>(S + row * QKB + (((c0 + 2) ^ (row & 7)) << 4));
+  return i32x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <bool BCE>
+__device__ __forceinline__ void q_body(const QP &p, int q, char *smem) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5;
+  const int wm = w >> 2, wn = w & 3;
+  const int split = q / p.ntiles, tile = q % p.ntiles;
+  const int bm = (tile % p.tiles_m) * QM, bn = (tile / p.tiles_m) * QN;
+  const int kbeg = split * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
+  const int nk = kbeg < kend ? (kend - kbeg) / QKB : 0;  // K % 128 == 0 and kchunk % 128 == 0
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void *)p.A, (short)0, p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void *)p.B, (short)0, p.b_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void *)p.sa, (short)0, p.sa_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void *)p.sb, (short)0, p.sb_bytes, 0x00020000);
+  f32x16_t acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  if (nk > 0) q_dma(p, ra, rb, rsa, rsb, smem, 0, bm, bn, kbeg);
+  // BCE: the tile's target words (256 rows x 8 words), 4 per thread, in flight during the K loop
+  constexpr bool bce = BCE;
+  const int YW = (p.N + 31) >> 5;
+  uint32_t yv[4] = {0u, 0u, 0u, 0u};
+  if constexpr (bce) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = threadIdx.x + QNT * u, r = i >> 3, gw = (bn >> 5) + (i & 7);
+      yv[u] = bm + r < p.M && gw < YW ? p.y_bits[(int64_t)(bm + r) * YW + gw] : 0u;
+    }
+  }
+  const int ar = wm * 128 + (lane & 31), br = wn * 64 + (lane & 31);
+  for (int t = 0; t < nk; ++t) {
+    // tile t landed in every wave (own DMAs drained, then the barrier), and every wave finished
+    // reading the other buffer in iteration t - 1 (its LDS reads retired before the barrier)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 1 < nk) q_dma(p, ra, rb, rsa, rsb, smem, (t + 1) & 1, bm, bn, kbeg + (t + 1) * QKB);
+    const char *sA = smem + (t & 1) * QSTAGE, *sB = sA + QA_BYTES;
+    const uint32_t *sS = reinterpret_cast<const uint32_t *>(sB + QB_BYTES);
+    uint32_t wa[4], wb[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wa[i] = sS[ar + 32 * i];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) wb[j] = sS[QM + br + 32 * j];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c0 = 4 * kk + half, sh = 8 * (2 * kk + half);
+      i32x8_t b[2];
+      int sb[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        b[j] = q_frag(sB, br + 32 * j, c0);
+        sb[j] = (int)((wb[j] >> sh) & 0xFFu);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const i32x8_t a = q_frag(sA, ar + 32 * i, c0);
+        const int sa = (int)((wa[i] >> sh) & 0xFFu);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b[j], acc[i][j], 0, 0, 0, sa, 0, sb[j]);
+      }
+    }
+  }
+  // ---- epilogue straight from the accumulators: lanes 0..31 of a half = 32 consecutive columns
+  // of one row (128 B of fp32 per row per instruction)
+  if (p.epi == CC_EPI_SPLITK) {
+    float *out = p.Cf + (int64_t)split * p.M * p.N;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = bn + wn * 64 + j * 32 + (lane & 31);
+      if (col >= p.N) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = bm + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          if (row < p.M) out[(int64_t)row * p.N + col] = acc[i][j][r];
+        }
+    }
+    return;
+  }
+  if constexpr (bce) {
+    // The epilogue runs from LDS, in two passes of 128 columns (the waves' j = 0 accumulators,
+    // then j = 1): the fp32 logits of the pass S[256][QSP] (odd pitch: the column reads of the
+    // dZ^T loop spread over the banks) and the tile's target words ys[cb][row].  Transforming the
+    // 128 accumulators in registers instead spilled (the fully unrolled BCE math of 128 values).
+    constexpr int QSP = 129;
+    float *S = reinterpret_cast<float *>(smem);
+    uint32_t *ys = reinterpret_cast<uint32_t *>(smem + QM * QSP * 4);
+    double *red = reinterpret_cast<double *>(smem + QM * QSP * 4 + QM * 8 * 4);
+    int *lastflag = reinterpret_cast<int *>(smem + QM * QSP * 4 + QM * 8 * 4 + 8 * sizeof(double));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();   // every wave left the K loop: the stage buffers are free
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // column-block-major: ys[cb][row]
+      const int i = threadIdx.x + QNT * u;
+      ys[(i & 7) * QM + (i >> 3)] = yv[u];
+    }
+    float lossf = 0.f;
+    const float scale = p.scale;
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      // local column c in [0, 128) <-> global bn + (c / 32) * 64 + jp * 32 + c % 32
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          S[(wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * QSP + wn * 32 + (lane & 31)] = acc[i][jp][r];
+      __syncthreads();
+      // rows: thread -> (row, 4 consecutive columns of one 32-column group); dz replaces z in S
+      for (int idx = threadIdx.x; idx < QM * 32; idx += QNT) {
+        const int lr = idx >> 5, cq = idx & 31, c = cq * 4, grp = c >> 5;
+        const int gc = bn + grp * 64 + jp * 32 + (c & 31), row = bm + lr;
+        const uint32_t yw = ys[((gc - bn) >> 5) * QM + lr] >> (c & 31);
+        float lprod = 1.f, rsum = 0.f, dz[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool live = row < p.M && gc + e < p.N;
+          const float z = S[lr * QSP + c + e] + (gc + e < p.N ? p.bias[gc + e] : 0.f);
+          dz[e] = q_bce(z, (yw >> e) & 1u, scale, lprod, rsum, live);
+          S[lr * QSP + c + e] = dz[e];
+        }
+        lossf += rsum + __builtin_amdgcn_logf(lprod) * 0.6931471805599453f;
+        if (row < p.M) {
+          bf16_t *dst = p.C + (int64_t)row * p.ldc + gc;
+          if (gc + 3 < p.N && (p.ldc & 3) == 0) {
+            *reinterpret_cast<uint2 *>(dst) = make_uint2((uint32_t)f2bf(dz[0]) | ((uint32_t)f2bf(dz[1]) << 16),
+                                                         (uint32_t)f2bf(dz[2]) | ((uint32_t)f2bf(dz[3]) << 16));
+          } else {
+            for (int e = 0; e < 4 && gc + e < p.N; ++e) dst[e] = f2bf(dz[e]);
+          }
+        }
+      }
+      if (p.Ct) {   // columns: thread -> (column, 8 consecutive rows): 16-B stores of dZ^T rows
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < 128 * (QM / 8); idx += QNT) {
+          const int c = idx / (QM / 8), lr = (idx % (QM / 8)) * 8;
+          const int gc = bn + (c >> 5) * 64 + jp * 32 + (c & 31), row = bm + lr;
+          if (gc >= p.N || row >= p.M) continue;
+          uint32_t pk[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            pk[e] = (uint32_t)f2bf(S[(lr + 2 * e) * QSP + c]) | ((uint32_t)f2bf(S[(lr + 2 * e + 1) * QSP + c]) << 16);
+          bf16_t *dst = p.Ct + (int64_t)gc * p.ldct + row;
+          if (row + 7 < p.M && (p.ldct & 7) == 0) {
+            *reinterpret_cast<uint4 *>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+          } else {
+            for (int e = 0; e < 8 && row + e < p.M; ++e) dst[e] = (bf16_t)(pk[e >> 1] >> (16 * (e & 1)));
+          }
+        }
+      }
+      __syncthreads();   // S is rewritten by the next pass
+    }
+    // the tile's loss partial (waves in order), then the last tile block reduces them in tile order
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) lossf += __shfl_xor(lossf, off);
+    if (lane == 0) red[w] = (double)lossf;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double sum = 0.0;
+      for (int v = 0; v < QNT / 64; ++v) sum += red[v];
+      *lastflag = 0;
+      if (!p.loss_out) {
+        p.loss_partials[tile] = sum;
+      } else {
+        __hip_atomic_store(&p.loss_partials[tile], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t tk = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *lastflag = tk == (uint32_t)p.ntiles - 1;
+      }
+    }
+    if (!p.loss_out) return;
+    __syncthreads();
+    if (!*lastflag) return;
+    double s2 = 0.0;
+    for (int v = threadIdx.x; v < p.ntiles; v += QNT)
+      s2 += __hip_atomic_load(&p.loss_partials[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s2 += __shfl_xor(s2, off);
+    __syncthreads();
+    if (lane == 0) red[w] = s2;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double tot = 0.0;
+      for (int v = 0; v < QNT / 64; ++v) tot += red[v];
+      p.loss_out[0] = tot * p.loss_scale;
+      __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = bn + wn * 64 + j * 32 + (lane & 31);
+    if (col >= p.N) continue;
+    const float bias = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = bm + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        if (row >= p.M) continue;
+        const float v = acc[i][j][r] + bias;
+        if (p.Cf) p.Cf[(int64_t)row * p.ldc + col] = v;
+        if (p.C) p.C[(int64_t)row * p.ldc + col] = f2bf(v);
+      }
+  }
+}
+
+template <bool BCE>
+__global__ __launch_bounds__(QNT) void mx8_wide_kernel(QP p) {
+  extern __shared__ __attribute__((aligned(1024))) char qsmem[];
+  q_body<BCE>(p, xcd_run(blockIdx.x, p.ntiles * p.splits), qsmem);
+}
+
+// two independent problems in one launch (the decoder's dX split-K and dW products): blocks
+// [0, n0) are problem 0's, the rest problem 1's, each dealt to the XCDs in contiguous runs
+__global__ __launch_bounds__(QNT) void mx8_wide_pair_kernel(QP p0, QP p1) {
+  extern __shared__ __attribute__((aligned(1024))) char qsmem[];
+  const int n0 = p0.ntiles * p0.splits;
+  if ((int)blockIdx.x < n0)
+    q_body<false>(p0, xcd_run(blockIdx.x, n0), qsmem);
+  else
+    q_body<false>(p1, xcd_run(blockIdx.x - n0, p1.ntiles * p1.splits), qsmem);
+}
+
+int q_params(const cc_gemm_args *g, QP &p) {
+  CC_REQUIRE(g && g->dtype == CC_MX8 && !g->ta && g->tb, "cc_gemm_mx8_wide: MX8 NT only");
+  CC_REQUIRE(g->A && g->B && g->a_scale && g->b_scale, "cc_gemm_mx8_wide: null operand");
+  CC_REQUIRE(g->M > 0 && g->N > 0 && g->K > 0, "cc_gemm_mx8_wide: empty problem");
+  CC_REQUIRE(g->K % 128 == 0 && g->lda % 128 == 0 && g->ldb % 128 == 0 && g->lda >= g->K && g->ldb >= g->K,
+             "cc_gemm_mx8_wide: K, lda, ldb multiples of 128, lda / ldb >= K");
+  CC_REQUIRE(g->epilogue == CC_EPI_STORE || g->epilogue == CC_EPI_SPLITK || g->epilogue == CC_EPI_BCE,
+             "cc_gemm_mx8_wide: STORE, SPLITK or BCE");
+  CC_REQUIRE(g->epilogue != CC_EPI_BCE || (g->bias && g->y_bits && g->loss_partials && g->C && g->ldc >= g->N &&
+                                           (!g->Ct || g->ldct >= g->M) && (!g->loss_out || g->ticket)),
+             "cc_gemm_mx8_wide: BCE needs bias, y_bits, loss_partials, C (ldc >= N), ldct >= M, a ticket with loss_out");
+  CC_REQUIRE(!g->Ct || ((uintptr_t)g->Ct % 8 == 0 && g->ldct % 4 == 0 && g->M % 4 == 0 &&
+                         (int64_t)g->N * g->ldct * 2 < 0x80000000ll),
+             "cc_gemm_mx8_wide: Ct 8-B aligned rows, M % 4 == 0, below 2 GB");
+  CC_REQUIRE(g->epilogue != CC_EPI_SPLITK || (g->Cf && g->splits >= 1), "cc_gemm_mx8_wide: split-K needs Cf");
+  CC_REQUIRE(g->epilogue != CC_EPI_STORE || g->ldc >= g->N, "cc_gemm_mx8_wide: ldc >= N");
+  CC_REQUIRE(!g->relu && !g->colsum && !g->H, "cc_gemm_mx8_wide: no relu / colsum / mask");
+  CC_REQUIRE((int64_t)g->M * g->lda < 0x80000000ll && (int64_t)g->N * g->ldb < 0x80000000ll,
+             "cc_gemm_mx8_wide: operands below 2 GB (32-bit buffer offsets)");
+  CC_REQUIRE((((uintptr_t)g->A | (uintptr_t)g->B) & 15) == 0 && (((uintptr_t)g->a_scale | (uintptr_t)g->b_scale) & 3) == 0,
+             "cc_gemm_mx8_wide: operands 16-B, scales 4-B aligned");
+  p.A = (const uint8_t *)g->A;
+  p.B = (const uint8_t *)g->B;
+  p.sa = g->a_scale;
+  p.sb = g->b_scale;
+  p.bias = g->bias;
+  p.C = (bf16_t *)g->C;
+  p.Cf = g->Cf;
+  p.M = g->M;
+  p.N = g->N;
+  p.K = g->K;
+  p.lda = g->lda;
+  p.ldb = g->ldb;
+  p.ldc = g->ldc;
+  p.epi = g->epilogue;
+  p.y_bits = g->y_bits;
+  p.Ct = (bf16_t *)g->Ct;
+  p.ldct = g->ldct;
+  p.loss_partials = g->loss_partials;
+  p.loss_out = g->epilogue == CC_EPI_BCE ? g->loss_out : nullptr;
+  p.ticket = g->ticket;
+  p.loss_scale = g->loss_scale;
+  p.scale = g->scale;
+  p.splits = g->epilogue == CC_EPI_SPLITK ? g->splits : 1;
+  p.kchunk = (int)cdiv(cdiv(g->K, p.splits), QKB) * QKB;
+  p.tiles_m = (int)cdiv(g->M, QM);
+  p.ntiles = p.tiles_m * (int)cdiv(g->N, QN);
+  p.a_bytes = (uint32_t)((int64_t)g->M * g->lda);
+  p.b_bytes = (uint32_t)((int64_t)g->N * g->ldb);
+  p.sa_bytes = (uint32_t)((int64_t)g->M * (g->lda / 32));
+  p.sb_bytes = (uint32_t)((int64_t)g->N * (g->ldb / 32));
+  return CC_OK;
+}
+
+bool q_attr() {
+  static const bool ok = hipFuncSetAttribute((const void *)mx8_wide_kernel<false>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, QLDS) == hipSuccess &&
+                         hipFuncSetAttribute((const void *)mx8_wide_kernel<true>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, QLDS_MAX) == hipSuccess &&
+                         hipFuncSetAttribute((const void *)mx8_wide_pair_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, QLDS) == hipSuccess;
+  return ok;
+}
+
+}  // namespace
+
+extern "C" int cc_gemm_mx8_wide(const cc_gemm_args *g0, const cc_gemm_args *g1, void *stream) {
+  QP p0, p1;
+  if (int rc = q_params(g0, p0)) return rc;
+  if (g1)
+    if (int rc = q_params(g1, p1)) return rc;
+  CC_REQUIRE(!g1 || (p0.epi != CC_EPI_BCE && p1.epi != CC_EPI_BCE), "cc_gemm_mx8_wide: no BCE in a pair");
+  CC_REQUIRE(p0.epi != CC_EPI_BCE || (int64_t)p0.M * p0.ldc * 2 < 0x100000000ll, "cc_gemm_mx8_wide: dZ below 4 GB");
+  CC_REQUIRE(q_attr(), "cc_gemm_mx8_wide: dynamic LDS attribute");
+  hipStream_t s = as_stream(stream);
+  if (!g1) {
+    if (p0.epi == CC_EPI_BCE)
+      hipLaunchKernelGGL(mx8_wide_kernel<true>, dim3((unsigned)p0.ntiles), dim3(QNT), QLDS_MAX, s, p0);
+    else
+      hipLaunchKernelGGL(mx8_wide_kernel<false>, dim3((unsigned)(p0.ntiles * p0.splits)), dim3(QNT), QLDS, s, p0);
+    CC_LAUNCH_CHECK("mx8_wide_kernel");
+    return CC_OK;
+  }
+  hipLaunchKernelGGL(mx8_wide_pair_kernel, dim3((unsigned)(p0.ntiles * p0.splits + p1.ntiles * p1.splits)),
+                     dim3(QNT), QLDS, s, p0, p1);
+  CC_LAUNCH_CHECK("mx8_wide_pair_kernel");
+  return CC_OK;
+}

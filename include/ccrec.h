@@ -273,6 +273,11 @@ int cc_gemm(const cc_gemm_args *g, void *stream);
 /* Two independent products in one launch (grouped GEMM) when both take the bf16 NT path with
  * the STORE or SPLITK epilogue; otherwise cc_gemm(g0) then cc_gemm(g1).  Same results. */
 int cc_gemm_pair(const cc_gemm_args *g0, const cc_gemm_args *g1, void *stream);
+/* MX-FP8 NT product(s) on 256 x 256 tiles with an LDS-DMA pipeline (mx8gemm.hip): epilogue STORE
+ * (optional bias, fp32 Cf and/or bf16 C) or SPLITK; g1 optional (a second problem in the same
+ * launch).  cc_gemm / cc_gemm_pair route their MX8 STORE / SPLITK calls here; bit-identical to the
+ * 128 x 128 MX kernel.  Needs K, lda, ldb multiples of 128 and operands below 2 GB. */
+int cc_gemm_mx8_wide(const cc_gemm_args *g0, const cc_gemm_args *g1, void *stream);
 /* workspace bound for cc_gemm's loss partials: ceil(M/64)*ceil(N/64) doubles */
 int cc_gemm_grid(int32_t M, int32_t N, int32_t *tiles);
 

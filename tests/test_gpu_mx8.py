@@ -177,3 +177,63 @@ def test_mx8_bce_epilogue():
     assert abs(loss.item() - ref_loss) / ref_loss < MFMA_TOL
     assert rel_err(dZ.float().cpu().numpy(), ref_dz) < 5e-3
     assert torch.equal(dZt.t().contiguous(), dZ)
+
+
+@pytest.mark.parametrize('M,N,K,epi,splits', [(512, 1000, 1024, 'store', 1), (300, 260, 384, 'store', 1),
+                                               (37, 129, 256, 'store', 1), (1024, 2100, 512, 'store', 1),
+                                               (512, 1024, 2944, 'splitk', 8), (512, 256, 1024, 'splitk', 32),
+                                               (512, 1000, 1024, 'bce', 1), (300, 700, 256, 'bce', 1)])
+def test_mx8_wide_bit_identical_to_128_kernel(M, N, K, epi, splits, monkeypatch):
+    """The 256 x 256 LDS-DMA kernel (mx8gemm.hip, cc_gemm's MX8 STORE / SPLITK / BCE path) runs the
+    same MFMA sequence per output as the 128 x 128 kernel: bitwise equal products, ragged edges
+    included, empty K splits written as zeros; BCE outputs to the rounding of its epilogue math."""
+    rng = np.random.default_rng(M * 3 + N + K)
+    qa, sa, _ = _mx8_operand(_data(rng, M, K), K)
+    qb, sb, _ = _mx8_operand(_data(rng, N, K), K)
+    bias = torch.from_numpy(rng.standard_normal(N).astype(np.float32)).cuda()
+    bits = torch.from_numpy(rng.integers(0, 2**31, (M, (N + 31) // 32), dtype=np.int64).astype(np.int32)).cuda()
+    outs = []
+    for kern in ('128', '256'):
+        monkeypatch.setenv('CCREC_MX8_GEMM', kern)
+        if epi == 'store':
+            Cf = torch.full((M, N), 7.0, device='cuda')
+            Cb = torch.zeros(M, N, device='cuda', dtype=torch.bfloat16)
+            g = L.GemmArgs(dtype=L.CC_MX8, ta=0, tb=1, epilogue=L.CC_EPI_STORE, M=M, N=N, K=K, lda=K, ldb=K,
+                           ldc=N, splits=1, A=qa.data_ptr(), B=qb.data_ptr(), bias=bias.data_ptr(),
+                           Cf=Cf.data_ptr(), C=Cb.data_ptr(), a_scale=sa.data_ptr(), b_scale=sb.data_ptr())
+            L.call('cc_gemm', L.C.byref(g), L.stream_ptr())
+            outs.append((Cf, Cb))
+        elif epi == 'bce':
+            dZ = torch.zeros(M, N, device='cuda', dtype=torch.bfloat16)
+            dZt = torch.zeros(N, M + 4, device='cuda', dtype=torch.bfloat16)
+            part = torch.zeros(4096, device='cuda', dtype=torch.float64)
+            loss = torch.zeros(1, device='cuda', dtype=torch.float64)
+            ticket = torch.zeros(1, device='cuda', dtype=torch.int32)
+            g = L.GemmArgs(dtype=L.CC_MX8, ta=0, tb=1, epilogue=L.CC_EPI_BCE, M=M, N=N, K=K, lda=K, ldb=K, ldc=N,
+                           splits=1, A=qa.data_ptr(), B=qb.data_ptr(), bias=bias.data_ptr(), C=dZ.data_ptr(),
+                           y_bits=bits.data_ptr(), scale=1.0 / (M * N), loss_partials=part.data_ptr(),
+                           Ct=dZt.data_ptr(), ldct=M + 4, loss_out=loss.data_ptr(), loss_scale=1.0 / (M * N),
+                           ticket=ticket.data_ptr(), a_scale=sa.data_ptr(), b_scale=sb.data_ptr())
+            L.call('cc_gemm', L.C.byref(g), L.stream_ptr())
+            torch.cuda.synchronize()
+            outs.append((dZ, dZt[:, :M], ticket))
+            losses = locals().get('losses', []) + [loss.item()]
+        else:
+            P = torch.full((splits, M, N), 7.0, device='cuda')
+            g = L.GemmArgs(dtype=L.CC_MX8, ta=0, tb=1, epilogue=L.CC_EPI_SPLITK, M=M, N=N, K=K, lda=K, ldb=K,
+                           ldc=N, splits=splits, A=qa.data_ptr(), B=qb.data_ptr(), Cf=P.data_ptr(),
+                           a_scale=sa.data_ptr(), b_scale=sb.data_ptr())
+            L.call('cc_gemm', L.C.byref(g), L.stream_ptr())
+            outs.append((P,))
+    torch.cuda.synchronize()
+    if epi == 'bce':
+        # the 256 x 256 kernel's BCE math is decout.hip's (hardware exp2 / rcp, one log2 per 4
+        # factors): dz within a bf16 ulp, the loss to float rounding; dZ^T is its own dZ transposed
+        (z0, zt0, t0), (z1, zt1, t1) = outs
+        assert torch.equal(zt1.t(), z1) and torch.equal(zt0.t(), z0)
+        assert ((z1.float() - z0.float()).abs() <= z0.float().abs() * 2.0 ** -7 + 1e-30).all()
+        assert abs(losses[0] - losses[1]) <= 1e-5 * abs(losses[0])
+        assert t0.item() == 0 and t1.item() == 0
+        return
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)

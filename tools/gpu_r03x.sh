@@ -4,7 +4,7 @@
 # BCE line (HBM bytes of the roofline kernel; MFMA), then the bench lines with the traffic attached.
 # usage (inside gpurun): bash tools/gpu_r03x.sh [tests|prof|bench|all]
 WHAT=${1:-all}
-R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; O=$R/gpurun_out/r03x; mkdir -p $O
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; O=$R/gpurun_out/${TAG:-r03x}; mkdir -p $O
 if [ "$WHAT" = tests ] || [ "$WHAT" = all ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1
   tail -3 $O/gpu_tests.log
