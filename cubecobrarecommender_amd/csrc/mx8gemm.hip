@@ -25,6 +25,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "mx8.hpp"
 
 namespace {
 
@@ -32,8 +33,8 @@ constexpr int QM = 256, QN = 256, QKB = 128, QNT = 512;
 constexpr int QA_BYTES = QM * QKB, QB_BYTES = QN * QKB;  // 32 KB each
 constexpr int QSTAGE = QA_BYTES + QB_BYTES + (QM + QN) * 4;
 constexpr int QLDS = 2 * QSTAGE;  // 132 KB
-// the BCE epilogue's LDS: a 256 x 129 fp32 pass tile, the 256 x 8 target words, the loss reduction
-constexpr int QLDS_BCE = QM * 129 * 4 + QM * 8 * 4 + 8 * 8 + 16;
+// the BCE epilogue's LDS: a 256 x 130 fp32 pass tile, the 256 x 8 target words, the loss reduction
+constexpr int QLDS_BCE = QM * 130 * 4 + QM * 8 * 4 + 8 * 8 + 16;
 constexpr int QLDS_MAX = QLDS > QLDS_BCE ? QLDS : QLDS_BCE;
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -55,6 +56,12 @@ struct QP {
   double loss_scale;
   float scale;
   int ldct;
+  // optional MX-FP8 images of the bf16-rounded dZ, exactly as cc_quant_mx8 makes them from dZ:
+  // zq [M][ldzq] (K = N; columns [N, ldzq) zero codes) + zqs [M][ldzq/32], ztq [N][ldztq] (K = M)
+  // + ztqs [N][ldztq/32]; colsum[N] += the tile's column sums of the bf16 dZ (the bias gradient)
+  uint8_t *zq, *zqs, *ztq, *ztqs;
+  float *colsum;
+  int ldzq, ldztq;
   int M, N, K, lda, ldb, ldc, splits, kchunk, tiles_m, ntiles, epi;
   uint32_t a_bytes, b_bytes, sa_bytes, sb_bytes;
 };
@@ -203,10 +210,10 @@ __device__ __forceinline__ void q_body(const QP &p, int q, char *smem) {
   }
   if constexpr (bce) {
     // The epilogue runs from LDS, in two passes of 128 columns (the waves' j = 0 accumulators,
-    // then j = 1): the fp32 logits of the pass S[256][QSP] (odd pitch: the column reads of the
-    // dZ^T loop spread over the banks) and the tile's target words ys[cb][row].  Transforming the
+    // then j = 1): the fp32 logits of the pass S[256][QSP] (pitch 130: the column reads of the
+    // dZ^T loop hit distinct banks) and the tile's target words ys[cb][row].  Transforming the
     // 128 accumulators in registers instead spilled (the fully unrolled BCE math of 128 values).
-    constexpr int QSP = 129;
+    constexpr int QSP = 130;
     float *S = reinterpret_cast<float *>(smem);
     uint32_t *ys = reinterpret_cast<uint32_t *>(smem + QM * QSP * 4);
     double *red = reinterpret_cast<double *>(smem + QM * QSP * 4 + QM * 8 * 4);
@@ -229,46 +236,116 @@ __device__ __forceinline__ void q_body(const QP &p, int q, char *smem) {
         for (int r = 0; r < 16; ++r)
           S[(wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * QSP + wn * 32 + (lane & 31)] = acc[i][jp][r];
       __syncthreads();
-      // rows: thread -> (row, 4 consecutive columns of one 32-column group); dz replaces z in S
-      for (int idx = threadIdx.x; idx < QM * 32; idx += QNT) {
-        const int lr = idx >> 5, cq = idx & 31, c = cq * 4, grp = c >> 5;
-        const int gc = bn + grp * 64 + jp * 32 + (c & 31), row = bm + lr;
-        const uint32_t yw = ys[((gc - bn) >> 5) * QM + lr] >> (c & 31);
-        float lprod = 1.f, rsum = 0.f, dz[4];
+      // rows: thread -> 4 consecutive columns c (fixed per thread) of rows tid / 32 + 16 k; dz
+      // replaces z in S.  The 8 lanes of a 32-column block are consecutive (one MX scale).
+      {
+        const int cq = threadIdx.x & 31, c = cq * 4;
+        const int gc = bn + (c >> 5) * 64 + jp * 32 + (c & 31);
+        const int cb = (gc - bn) >> 5;
+        float bias4[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const bool live = row < p.M && gc + e < p.N;
-          const float z = S[lr * QSP + c + e] + (gc + e < p.N ? p.bias[gc + e] : 0.f);
-          dz[e] = q_bce(z, (yw >> e) & 1u, scale, lprod, rsum, live);
-          S[lr * QSP + c + e] = dz[e];
-        }
-        lossf += rsum + __builtin_amdgcn_logf(lprod) * 0.6931471805599453f;
-        if (row < p.M) {
-          bf16_t *dst = p.C + (int64_t)row * p.ldc + gc;
-          if (gc + 3 < p.N && (p.ldc & 3) == 0) {
-            *reinterpret_cast<uint2 *>(dst) = make_uint2((uint32_t)f2bf(dz[0]) | ((uint32_t)f2bf(dz[1]) << 16),
-                                                         (uint32_t)f2bf(dz[2]) | ((uint32_t)f2bf(dz[3]) << 16));
-          } else {
-            for (int e = 0; e < 4 && gc + e < p.N; ++e) dst[e] = f2bf(dz[e]);
+        for (int e = 0; e < 4; ++e) bias4[e] = gc + e < p.N ? p.bias[gc + e] : 0.f;
+#pragma unroll 2
+        for (int lr = threadIdx.x >> 5; lr < QM; lr += QNT / 32) {
+          const int row = bm + lr;
+          const uint32_t yw = ys[cb * QM + lr] >> (c & 31);
+          const float2 z01 = *reinterpret_cast<const float2 *>(S + lr * QSP + c);
+          const float2 z23 = *reinterpret_cast<const float2 *>(S + lr * QSP + c + 2);
+          const float zz[4] = {z01.x, z01.y, z23.x, z23.y};
+          float lprod = 1.f, rsum = 0.f, dz[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool live = row < p.M && gc + e < p.N;
+            dz[e] = live ? q_bce(zz[e] + bias4[e], (yw >> e) & 1u, scale, lprod, rsum, true) : 0.f;
+          }
+          *reinterpret_cast<float2 *>(S + lr * QSP + c) = make_float2(dz[0], dz[1]);
+          *reinterpret_cast<float2 *>(S + lr * QSP + c + 2) = make_float2(dz[2], dz[3]);
+          lossf += rsum + __builtin_amdgcn_logf(lprod) * 0.6931471805599453f;
+          if (p.C && row < p.M) {
+            bf16_t *dst = p.C + (int64_t)row * p.ldc + gc;
+            if (gc + 3 < p.N && (p.ldc & 3) == 0) {
+              *reinterpret_cast<uint2 *>(dst) = make_uint2((uint32_t)f2bf(dz[0]) | ((uint32_t)f2bf(dz[1]) << 16),
+                                                           (uint32_t)f2bf(dz[2]) | ((uint32_t)f2bf(dz[3]) << 16));
+            } else {
+              for (int e = 0; e < 4 && gc + e < p.N; ++e) dst[e] = f2bf(dz[e]);
+            }
+          }
+          if (p.zq) {   // MX-FP8 rows (K = N)
+            float v[4], amax = 0.f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] = bf2f(f2bf(dz[e]));   // dead elements are exact zeros
+              amax = fmaxf(amax, fabsf(v[e]));
+            }
+            amax = fmaxf(amax, __shfl_xor(amax, 1));
+            amax = fmaxf(amax, __shfl_xor(amax, 2));
+            amax = fmaxf(amax, __shfl_xor(amax, 4));
+            const int ex = cc_mx8::block_exp(amax);
+            int word = 0;
+            word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[0], -ex), ldexpf(v[1], -ex), word, false);
+            word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[2], -ex), ldexpf(v[3], -ex), word, true);
+            if (row < p.M && gc < p.ldzq) {
+              *reinterpret_cast<uint32_t *>(p.zq + (int64_t)row * p.ldzq + gc) = (uint32_t)word;
+              if ((cq & 7) == 0) p.zqs[(int64_t)row * (p.ldzq / 32) + gc / 32] = (uint8_t)(ex + 127);
+            }
           }
         }
       }
-      if (p.Ct) {   // columns: thread -> (column, 8 consecutive rows): 16-B stores of dZ^T rows
+      if (p.Ct || p.ztq) {
+        // columns: lane -> (column cc = lane / 4 of the wave's 16, rows 8 (lane & 3) .. + 8 of a
+        // 32-row block); wave w takes columns 16 w .. + 16, the loop walks the 8 row blocks.  Pitch
+        // 130: the 64 lanes' reads of one row offset hit 64 distinct banks.  The 4 lanes of a column
+        // share the block's MX scale; the column sum runs over the blocks in the thread, then the 4 lanes
         __syncthreads();
-        for (int idx = threadIdx.x; idx < 128 * (QM / 8); idx += QNT) {
-          const int c = idx / (QM / 8), lr = (idx % (QM / 8)) * 8;
-          const int gc = bn + (c >> 5) * 64 + jp * 32 + (c & 31), row = bm + lr;
-          if (gc >= p.N || row >= p.M) continue;
+        const int c = w * 16 + (lane >> 2), rc = lane & 3;
+        const int gc = bn + (c >> 5) * 64 + jp * 32 + (c & 31);
+        const bool cok = gc < p.N;
+        float csum = 0.f;
+#pragma unroll 2
+        for (int rb = 0; rb < QM / 32; ++rb) {
+          const int lr = rb * 32 + rc * 8, row = bm + lr;
           uint32_t pk[4];
+          float v[8], amax = 0.f;
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            pk[e] = (uint32_t)f2bf(S[(lr + 2 * e) * QSP + c]) | ((uint32_t)f2bf(S[(lr + 2 * e + 1) * QSP + c]) << 16);
-          bf16_t *dst = p.Ct + (int64_t)gc * p.ldct + row;
-          if (row + 7 < p.M && (p.ldct & 7) == 0) {
-            *reinterpret_cast<uint4 *>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-          } else {
-            for (int e = 0; e < 8 && row + e < p.M; ++e) dst[e] = (bf16_t)(pk[e >> 1] >> (16 * (e & 1)));
+          for (int e = 0; e < 4; ++e) {
+            const bf16_t h0 = f2bf(S[(lr + 2 * e) * QSP + c]), h1 = f2bf(S[(lr + 2 * e + 1) * QSP + c]);
+            pk[e] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+            v[2 * e] = bf2f(h0);   // rows past M hold dz = 0
+            v[2 * e + 1] = bf2f(h1);
           }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            amax = fmaxf(amax, fabsf(v[e]));
+            csum += v[e];
+          }
+          if (p.Ct && cok && row < p.M) {
+            bf16_t *dst = p.Ct + (int64_t)gc * p.ldct + row;
+            if (row + 7 < p.M && (p.ldct & 7) == 0) {
+              *reinterpret_cast<uint4 *>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            } else {
+              for (int e = 0; e < 8 && row + e < p.M; ++e) dst[e] = (bf16_t)(pk[e >> 1] >> (16 * (e & 1)));
+            }
+          }
+          if (p.ztq) {
+            amax = fmaxf(amax, __shfl_xor(amax, 1));
+            amax = fmaxf(amax, __shfl_xor(amax, 2));
+            const int ex = cc_mx8::block_exp(amax);
+            int w0 = 0, w1 = 0;
+            w0 = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[0], -ex), ldexpf(v[1], -ex), w0, false);
+            w0 = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[2], -ex), ldexpf(v[3], -ex), w0, true);
+            w1 = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4], -ex), ldexpf(v[5], -ex), w1, false);
+            w1 = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[6], -ex), ldexpf(v[7], -ex), w1, true);
+            if (cok && row < p.M) {
+              *reinterpret_cast<uint2 *>(p.ztq + (int64_t)gc * p.ldztq + row) = make_uint2((uint32_t)w0, (uint32_t)w1);
+              if (rc == 0) p.ztqs[(int64_t)gc * (p.ldztq / 32) + row / 32] = (uint8_t)(ex + 127);
+            }
+          }
+        }
+        if (p.colsum) {
+          csum += __shfl_xor(csum, 1);
+          csum += __shfl_xor(csum, 2);
+          // two row tiles at most (checked on the host): fl(fl(0 + a) + b) == fl(fl(0 + b) + a)
+          if (cok && rc == 0) atomicAdd(p.colsum + gc, csum);
         }
       }
       __syncthreads();   // S is rewritten by the next pass
@@ -388,6 +465,9 @@ int q_params(const cc_gemm_args *g, QP &p) {
   p.ticket = g->ticket;
   p.loss_scale = g->loss_scale;
   p.scale = g->scale;
+  p.zq = p.zqs = p.ztq = p.ztqs = nullptr;
+  p.colsum = nullptr;
+  p.ldzq = p.ldztq = 0;
   p.splits = g->epilogue == CC_EPI_SPLITK ? g->splits : 1;
   p.kchunk = (int)cdiv(cdiv(g->K, p.splits), QKB) * QKB;
   p.tiles_m = (int)cdiv(g->M, QM);
@@ -431,5 +511,38 @@ extern "C" int cc_gemm_mx8_wide(const cc_gemm_args *g0, const cc_gemm_args *g1, 
   hipLaunchKernelGGL(mx8_wide_pair_kernel, dim3((unsigned)(p0.ntiles * p0.splits + p1.ntiles * p1.splits)),
                      dim3(QNT), QLDS, s, p0, p1);
   CC_LAUNCH_CHECK("mx8_wide_pair_kernel");
+  return CC_OK;
+}
+
+// The decoder output layer's BCE product with the MX-FP8 images of dZ made in the epilogue
+// (config 5): logits -> BCE -> dz, then zq / zqs (K = N, for the dX product), ztq / ztqs (K = M,
+// for the dW product) and the bias gradient colsum = column sums of the bf16 dZ, bit-exact with
+// cc_quant_mx8 of the bf16 dZ / dZ^T (the column sums to fp32 rounding).  g->C / g->Ct optional.
+extern "C" int cc_gemm_mx8_bce_q(const cc_gemm_args *g, uint8_t *zq, int32_t ldzq, uint8_t *zqs, uint8_t *ztq,
+                                 int32_t ldztq, uint8_t *ztqs, float *colsum, void *stream) {
+  CC_REQUIRE(g && g->epilogue == CC_EPI_BCE, "cc_gemm_mx8_bce_q: BCE epilogue");
+  CC_REQUIRE(zq && zqs && ztq && ztqs && colsum, "cc_gemm_mx8_bce_q: null output");
+  CC_REQUIRE(ldzq % 128 == 0 && ldzq >= g->N && ldzq <= (int)cdiv(g->N, QN) * QN && ldztq % 32 == 0 && ldztq >= g->M,
+             "cc_gemm_mx8_bce_q: ldzq % 128, N <= ldzq <= 256-tile cover of N; ldztq % 32, >= M");
+  CC_REQUIRE(g->M % 32 == 0 && g->M <= 2 * QM, "cc_gemm_mx8_bce_q: M % 32 == 0, M <= 512 (two row tiles)");
+  CC_REQUIRE((((uintptr_t)zq | (uintptr_t)ztq) & 7) == 0, "cc_gemm_mx8_bce_q: code images 8-B aligned");
+  cc_gemm_args g2 = *g;
+  QP p;
+  const bool has_c = g->C != nullptr;
+  if (!has_c) g2.C = (void *)zq;  // placeholder for the argument checks; not written
+  if (int rc = q_params(&g2, p)) return rc;
+  if (!has_c) p.C = nullptr;
+  p.zq = zq;
+  p.zqs = zqs;
+  p.ztq = ztq;
+  p.ztqs = ztqs;
+  p.colsum = colsum;
+  p.ldzq = ldzq;
+  p.ldztq = ldztq;
+  CC_REQUIRE(q_attr(), "cc_gemm_mx8_bce_q: dynamic LDS attribute");
+  hipStream_t s = as_stream(stream);
+  CC_HIP(hipMemsetAsync(colsum, 0, (size_t)g->N * sizeof(float), s));
+  hipLaunchKernelGGL(mx8_wide_kernel<true>, dim3((unsigned)p.ntiles), dim3(QNT), QLDS_MAX, s, p);
+  CC_LAUNCH_CHECK("mx8_wide_kernel<bce>");
   return CC_OK;
 }

@@ -364,6 +364,10 @@ class Trainer:
             # config 5 on the wide chains: the tower forward writes D3's MX-FP8 images itself (two
             # quantiser launches less per step)
             self.d3q_in_tower = self.mx8 and d > 256 and self.wpack is not None and R % 32 == 0
+            # the BCE product makes dZ's MX-FP8 images and the bias gradient in its epilogue
+            # (cc_gemm_mx8_bce_q: B % 32 == 0, B <= 512); CCREC_MX8_BCE_Q=0 keeps the quantiser launches
+            self.mx8_bce_q = (self.mx8 and B % 32 == 0 and B <= 512
+                              and os.environ.get('CCREC_MX8_BCE_Q', '1') != '0')
             if self.d3q_in_tower:
                 t = self.targs
                 t.d3q, t.d3qs = self.D3q.data_ptr(), self.D3qs.data_ptr()
@@ -372,6 +376,7 @@ class Trainer:
         else:
             self.targs = None
             self.d3q_in_tower = False
+            self.mx8_bce_q = False
         if not self.fused_tower:
             self.fused_reg = False
         if self.use_reg and not self.fused_reg:
@@ -752,6 +757,14 @@ class Trainer:
                    self.pf('decoder/reconstruct/bias'), B, d, V, L.ptr(self.y_bits), L.ptr(self.dZout),
                    self.gp('decoder/reconstruct/kernel'), self.gp('decoder/reconstruct/bias'),
                    L.ptr(self.bce_part), L.ptr(self.loss_dev), 1.0 / (B * V), L.ptr(self.tickets), s)
+        elif self.mx8_bce_q:   # config 5: the BCE epilogue writes dZ's MX-FP8 images + the bias grad
+            g = self._gemm(B, V, d, **self._dec_fwd(0, 0), tb=1,
+                           epi=L.CC_EPI_BCE, bias=self.pf('decoder/reconstruct/bias'),
+                           y_bits=L.ptr(self.y_bits), scale=1.0 / (B * V), partials=L.ptr(self.bce_part),
+                           loss_out=L.ptr(self.loss_dev), loss_scale=1.0 / (B * V),
+                           ticket=L.ptr(self.tickets), launch=False)
+            L.call('cc_gemm_mx8_bce_q', L.C.byref(g), L.ptr(self.dZq), self.Vp, L.ptr(self.dZqs),
+                   L.ptr(self.dZtq[0]), B, L.ptr(self.dZtqs[0]), self.gp('decoder/reconstruct/bias'), s)
         elif self.fused_tower:   # Wo^T [V][d]: k-contiguous B operand; also writes dZ^T [V][B]
             self._gemm(B, V, d, **self._dec_fwd(0, 0), tb=1,
                        epi=L.CC_EPI_BCE, bias=self.pf('decoder/reconstruct/bias'), C=L.ptr(self.dZout),
@@ -808,7 +821,7 @@ class Trainer:
             nr = r1 - r0
             splits = self.splits if k == 0 else self.splits_reg
             if self.fused_tower:
-                if self.mx8:   # MX-FP8 dZ (dX A, K = V) and dZ^T (dW B, K = rows) + the bias grad
+                if self.mx8 and not (k == 0 and self.mx8_bce_q):   # MX-FP8 dZ (dX A, K = V) and dZ^T (dW B, K = rows) + the bias grad
                     L.call('cc_quant_mx8', L.CC_BF16, L.ptr(dz), nr, V, V, 0, L.ptr(self.dZq[r0:]), self.Vp,
                            L.ptr(self.dZqs[r0:]), None, s)
                     L.call('cc_quant_mx8', L.CC_BF16, L.ptr(self.dZt[k]), V, nr, nr, 0, L.ptr(self.dZtq[k]), nr,

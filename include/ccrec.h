@@ -278,6 +278,12 @@ int cc_gemm_pair(const cc_gemm_args *g0, const cc_gemm_args *g1, void *stream);
  * launch).  cc_gemm / cc_gemm_pair route their MX8 STORE / SPLITK calls here; bit-identical to the
  * 128 x 128 MX kernel.  Needs K, lda, ldb multiples of 128 and operands below 2 GB. */
 int cc_gemm_mx8_wide(const cc_gemm_args *g0, const cc_gemm_args *g1, void *stream);
+/* Config 5's decoder output layer (model.py:64,94; train.py:85) on the 256 x 256 MX-FP8 kernel with
+ * the dZ operand images made in the BCE epilogue: zq [M][ldzq] + zqs (K = N, for dX), ztq [N][ldztq]
+ * + ztqs (K = M, for dW) bit-exact with cc_quant_mx8 of the bf16 dZ / dZ^T, and colsum[N] = the bias
+ * gradient (zeroed here).  g->C / g->Ct (bf16 dZ / dZ^T) optional.  M % 32 == 0, M <= 512. */
+int cc_gemm_mx8_bce_q(const cc_gemm_args *g, uint8_t *zq, int32_t ldzq, uint8_t *zqs, uint8_t *ztq,
+                      int32_t ldztq, uint8_t *ztqs, float *colsum, void *stream);
 /* workspace bound for cc_gemm's loss partials: ceil(M/64)*ceil(N/64) doubles */
 int cc_gemm_grid(int32_t M, int32_t N, int32_t *tiles);
 

@@ -237,3 +237,50 @@ def test_mx8_wide_bit_identical_to_128_kernel(M, N, K, epi, splits, monkeypatch)
         return
     for x, y in zip(*outs):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize('M,N,K', [(512, 1000, 1024), (256, 22000, 256), (128, 300, 128)])
+def test_mx8_bce_q_matches_quantiser(M, N, K):
+    """cc_gemm_mx8_bce_q (config 5's BCE product making dZ's MX-FP8 images in its epilogue) ==
+    the same product's bf16 dZ / dZ^T run through cc_quant_mx8: codes and scales bit for bit
+    (padded columns [N, ldzq) included), the bias gradient to fp32 rounding, the same loss."""
+    rng = np.random.default_rng(M + N)
+    qa, sa, _ = _mx8_operand(rng.standard_normal((M, K)).astype(np.float32), K)
+    qb, sb, _ = _mx8_operand(rng.standard_normal((N, K)).astype(np.float32) * 0.05, K)
+    bias = torch.from_numpy(rng.standard_normal(N).astype(np.float32) * 0.1).cuda()
+    bits = torch.from_numpy(rng.integers(0, 2**31, (M, (N + 31) // 32), dtype=np.int64).astype(np.int32)).cuda()
+    Np = (N + 127) // 128 * 128
+
+    def run(fused):
+        dZ = torch.zeros(M, N, device='cuda', dtype=torch.bfloat16)
+        dZt = torch.zeros(N, M, device='cuda', dtype=torch.bfloat16)
+        part = torch.zeros(4096, device='cuda', dtype=torch.float64)
+        loss = torch.zeros(1, device='cuda', dtype=torch.float64)
+        ticket = torch.zeros(1, device='cuda', dtype=torch.int32)
+        zq = torch.full((M, Np), 0x55, device='cuda', dtype=torch.uint8)
+        zqs = torch.full((M, Np // 32), 0x55, device='cuda', dtype=torch.uint8)
+        ztq = torch.full((N, M), 0x55, device='cuda', dtype=torch.uint8)
+        ztqs = torch.full((N, M // 32), 0x55, device='cuda', dtype=torch.uint8)
+        gb = torch.full((N,), 3.0, device='cuda')
+        g = L.GemmArgs(dtype=L.CC_MX8, ta=0, tb=1, epilogue=L.CC_EPI_BCE, M=M, N=N, K=K, lda=K, ldb=K, ldc=N,
+                       splits=1, A=qa.data_ptr(), B=qb.data_ptr(), bias=bias.data_ptr(),
+                       C=None if fused else dZ.data_ptr(), y_bits=bits.data_ptr(), scale=1.0 / (M * N),
+                       loss_partials=part.data_ptr(), Ct=None if fused else dZt.data_ptr(), ldct=M,
+                       loss_out=loss.data_ptr(), loss_scale=1.0 / (M * N), ticket=ticket.data_ptr(),
+                       a_scale=sa.data_ptr(), b_scale=sb.data_ptr())
+        if fused:
+            L.call('cc_gemm_mx8_bce_q', L.C.byref(g), L.ptr(zq), Np, L.ptr(zqs), L.ptr(ztq), M, L.ptr(ztqs),
+                   L.ptr(gb), L.stream_ptr())
+        else:
+            L.call('cc_gemm', L.C.byref(g), L.stream_ptr())
+            L.call('cc_quant_mx8', L.CC_BF16, L.ptr(dZ), M, N, N, 0, L.ptr(zq), Np, L.ptr(zqs), None, L.stream_ptr())
+            L.call('cc_quant_mx8', L.CC_BF16, L.ptr(dZt), N, M, M, 0, L.ptr(ztq), M, L.ptr(ztqs), L.ptr(gb),
+                   L.stream_ptr())
+        torch.cuda.synchronize()
+        return zq, zqs, ztq, ztqs, gb, loss.item()
+
+    ref, got = run(False), run(True)
+    for a, b in zip(ref[:4], got[:4]):
+        assert torch.equal(a, b)
+    torch.testing.assert_close(got[4], ref[4], rtol=1e-5, atol=1e-12)
+    assert abs(got[5] - ref[5]) <= 1e-9 * abs(ref[5])

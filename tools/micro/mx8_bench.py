@@ -34,6 +34,7 @@ dZtq, dZtqs = codes(V, B), scales(V, B)
 D3 = torch.randn(B, d, **bf)
 WoT = torch.randn(V, d, **bf) * 0.05
 bias = torch.zeros(V, device=dev)
+gbias = torch.zeros(V, device=dev)
 ybits = torch.randint(0, 2**31 - 1, (B, (V + 31) // 32), device=dev, dtype=torch.int32)
 part = torch.zeros(8192, device=dev, dtype=torch.float64)
 Cb = torch.empty(B, V, **bf)
@@ -71,6 +72,9 @@ def main(only=None):
     variants = {
         'mx8 logits+bce+C+Ct': lambda: gemm(B, V, d, D3q, d, WoT8, d, L.CC_EPI_BCE, sa=D3qs, sb=WoT8s, bias=bias,
                                             C=Cb, y_bits=ybits, loss_partials=part, Ct=Ct, ldct=B),
+        'mx8 bce_q': lambda: L.call('cc_gemm_mx8_bce_q', C.byref(args(
+            B, V, d, D3q, d, WoT8, d, L.CC_EPI_BCE, sa=D3qs, sb=WoT8s, bias=bias, y_bits=ybits, loss_partials=part)),
+            L.ptr(dZq), Vp, L.ptr(dZqs), L.ptr(dZtq), B, L.ptr(dZtqs), L.ptr(gbias), L.stream_ptr()),
         'mx8 logits compute': lambda: gemm(B, V, d, D3q, d, WoT8, d, L.CC_EPI_STORE, sa=D3qs, sb=WoT8s),
         'mx8 reg logits Cf': lambda: gemm(B, V, d, D3q, d, WoT8, d, L.CC_EPI_STORE, sa=D3qs, sb=WoT8s, bias=bias, Cf=Z2),
         'mx8 dX splitk16': lambda: gemm(B, d, Vp, dZq, Vp, Wo8, Vp, L.CC_EPI_SPLITK, sa=dZqs, sb=Wo8s, Cf=split, splits=S),
