@@ -82,6 +82,18 @@ __device__ __forceinline__ float q_bce(float z, uint32_t ybit, float scale, floa
   return (sig - (float)ybit) * scale;
 }
 
+// cross-lane steps of the epilogue's MX block reductions as DPP moves (no LDS round trip, unlike
+// __shfl_xor's ds_bpermute): lane ^ 1, lane ^ 2 (quad_perm) and the mirror inside 8 lanes (after the
+// two quad steps every lane of a quad holds the quad's value, so the mirror pairs the two quads)
+__device__ __forceinline__ float dpp_f(float v, int ctrl_sel) {
+  const int x = __builtin_bit_cast(int, v);
+  int y;
+  if (ctrl_sel == 0) y = __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);       // quad_perm [1,0,3,2]
+  else if (ctrl_sel == 1) y = __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  else y = __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false);                    // row_half_mirror
+  return __builtin_bit_cast(float, y);
+}
+
 __device__ __forceinline__ int xcd_run(int b, int nb) {  // bijective: block -> XCD-contiguous id
   const int q = nb / 8, r = nb % 8, x = b % 8, slot = b / 8;
   return x < r ? x * (q + 1) + slot : r * (q + 1) + (x - r) * q + slot;
@@ -277,9 +289,9 @@ __device__ __forceinline__ void q_body(const QP &p, int q, char *smem) {
               v[e] = bf2f(f2bf(dz[e]));   // dead elements are exact zeros
               amax = fmaxf(amax, fabsf(v[e]));
             }
-            amax = fmaxf(amax, __shfl_xor(amax, 1));
-            amax = fmaxf(amax, __shfl_xor(amax, 2));
-            amax = fmaxf(amax, __shfl_xor(amax, 4));
+            amax = fmaxf(amax, dpp_f(amax, 0));
+            amax = fmaxf(amax, dpp_f(amax, 1));
+            amax = fmaxf(amax, dpp_f(amax, 2));
             const int ex = cc_mx8::block_exp(amax);
             int word = 0;
             word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[0], -ex), ldexpf(v[1], -ex), word, false);
@@ -327,8 +339,8 @@ __device__ __forceinline__ void q_body(const QP &p, int q, char *smem) {
             }
           }
           if (p.ztq) {
-            amax = fmaxf(amax, __shfl_xor(amax, 1));
-            amax = fmaxf(amax, __shfl_xor(amax, 2));
+            amax = fmaxf(amax, dpp_f(amax, 0));
+            amax = fmaxf(amax, dpp_f(amax, 1));
             const int ex = cc_mx8::block_exp(amax);
             int w0 = 0, w1 = 0;
             w0 = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[0], -ex), ldexpf(v[1], -ex), w0, false);
@@ -342,8 +354,8 @@ __device__ __forceinline__ void q_body(const QP &p, int q, char *smem) {
           }
         }
         if (p.colsum) {
-          csum += __shfl_xor(csum, 1);
-          csum += __shfl_xor(csum, 2);
+          csum += dpp_f(csum, 0);
+          csum += dpp_f(csum, 1);
           // two row tiles at most (checked on the host): fl(fl(0 + a) + b) == fl(fl(0 + b) + a)
           if (cok && rc == 0) atomicAdd(p.colsum + gc, csum);
         }

@@ -271,7 +271,7 @@ class Trainer:
         self.gH2 = torch.zeros(R, 256, **T)
         self.gPre1 = torch.zeros(R, d, **f32)
         self.Z2 = None             # materialised fp32 D2 logits (the unfused regulariser path only)
-        self.splits = max(1, min(int(os.environ.get('CCREC_DX_SPLITS', '32')), V // 512))   # decoder dX: K = V
+        self.splits = max(1, min(int(os.environ.get('CCREC_DX_SPLITS', '16' if cfg.dtype == 'fp8' else '32')), V // 512))   # decoder dX: K = V (fp8: 256 x 256 tiles, 16 splits measured best)
         # the regulariser branch's dX: M = Breg rows; with thousands of rows (full mode) the output
         # tiles alone fill the chip — no split-K
         # full-mode regulariser (~|V| rows): 2 K-splits (tools/micro/dx_full_micro.py at |V| = 22,000:
