@@ -2,6 +2,7 @@
 // TF-Adam (train.py:84 'adam' -> ResourceApplyAdam) and the device step counter.
 #include "adam.hpp"
 #include "common.hpp"
+#include "mx8.hpp"
 
 namespace {
 
@@ -107,12 +108,18 @@ __global__ __launch_bounds__(NTR) void softmax_kl_rows_kernel(const float *__res
                                                               const float *__restrict__ Mt,
                                                               const int32_t *__restrict__ reg_idx,
                                                               float scale, T *__restrict__ dZ,
-                                                              double *__restrict__ kl_part) {
+                                                              double *__restrict__ kl_part,
+                                                              uint8_t *__restrict__ zq = nullptr, int ldzq = 0,
+                                                              uint8_t *__restrict__ zqs = nullptr) {
   __shared__ float redf[NTR / 64];
   __shared__ double redd[NTR / 64];
   const int b = blockIdx.x, V4 = V >> 2;
   if (reg_idx[b] < 0) {  // padding row (owner-computes capacity): no KL term, zero gradient
     for (int j = threadIdx.x; j < V; j += NTR) DT<T>::st(dZ + (int64_t)b * V + j, 0.f);
+    if (zq) {            // zero codes, scale 2^0 (the quantiser's all-zero block)
+      for (int j = threadIdx.x; j < ldzq / 4; j += NTR) reinterpret_cast<uint32_t *>(zq + (int64_t)b * ldzq)[j] = 0u;
+      for (int j = threadIdx.x; j < ldzq / 32; j += NTR) zqs[(int64_t)b * (ldzq / 32) + j] = 127;
+    }
     if (threadIdx.x == 0) kl_part[b] = 0.0;
     return;
   }
@@ -177,6 +184,54 @@ __global__ __launch_bounds__(NTR) void softmax_kl_rows_kernel(const float *__res
       reinterpret_cast<uint2 *>(dZ + (int64_t)b * V)[j] = pk;
     } else {
       reinterpret_cast<float4 *>(dZ + (int64_t)b * V)[j] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  if (zq) {   // the MX-FP8 row image of the bf16 dZ row (K = V; columns [V, ldzq) zero codes), as
+              // cc_quant_mx8 makes it: the 8 lanes of a 32-column block share its scale
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int j = threadIdx.x + i * NTR;
+      float v[4], amax = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = j < V4 ? bf2f(f2bf(scale * (t[i][e] + z[i][e] * Sf))) : 0.f;
+        amax = fmaxf(amax, fabsf(v[e]));
+      }
+      amax = fmaxf(amax, __shfl_xor(amax, 1));
+      amax = fmaxf(amax, __shfl_xor(amax, 2));
+      amax = fmaxf(amax, __shfl_xor(amax, 4));
+      const int ex = cc_mx8::block_exp(amax);
+      int word = 0;
+      word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[0], -ex), ldexpf(v[1], -ex), word, false);
+      word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[2], -ex), ldexpf(v[3], -ex), word, true);
+      if (j < ldzq / 4) {
+        reinterpret_cast<uint32_t *>(zq + (int64_t)b * ldzq)[j] = (uint32_t)word;
+        if ((j & 7) == 0) zqs[(int64_t)b * (ldzq / 32) + j / 8] = (uint8_t)(ex + 127);
+      }
+    }
+  }
+  if (zq) {   // the MX-FP8 row image of the bf16 dZ row (K = V; columns [V, ldzq) zero codes), as
+              // cc_quant_mx8 makes it: the 8 lanes of a 32-column block share its scale
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int j = threadIdx.x + i * NTR;
+      float v[4], amax = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = j < V4 ? bf2f(f2bf(scale * (t[i][e] + z[i][e] * Sf))) : 0.f;
+        amax = fmaxf(amax, fabsf(v[e]));
+      }
+      amax = fmaxf(amax, __shfl_xor(amax, 1));
+      amax = fmaxf(amax, __shfl_xor(amax, 2));
+      amax = fmaxf(amax, __shfl_xor(amax, 4));
+      const int ex = cc_mx8::block_exp(amax);
+      int word = 0;
+      word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[0], -ex), ldexpf(v[1], -ex), word, false);
+      word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[2], -ex), ldexpf(v[3], -ex), word, true);
+      if (j < ldzq / 4) {
+        reinterpret_cast<uint32_t *>(zq + (int64_t)b * ldzq)[j] = (uint32_t)word;
+        if ((j & 7) == 0) zqs[(int64_t)b * (ldzq / 32) + j / 8] = (uint8_t)(ex + 127);
+      }
     }
   }
   if (threadIdx.x == 0) kl_part[b] = kl;
@@ -469,5 +524,35 @@ extern "C" int cc_to_bf16(const float *x, uint16_t *y, int64_t n, void *stream) 
   hipLaunchKernelGGL(to_bf16_kernel, dim3((unsigned)blocks), dim3(NT), 0, as_stream(stream), x,
                      (bf16_t *)y, n);
   CC_LAUNCH_CHECK("to_bf16_kernel");
+  return CC_OK;
+}
+
+// cc_dec_softmax_kl_fused (bf16 dZ) that also writes the MX-FP8 row image of dZ (zq [B][ldzq] codes,
+// zqs [B][ldzq/32] scales; bit-exact with cc_quant_mx8 of the bf16 dZ): config 5's regulariser
+// branch without the separate row quantiser launch
+extern "C" int cc_dec_softmax_kl_q(const float *Z2, int32_t B, int32_t V, const float *y_reg,
+                                   const int32_t *reg_idx, float scale, void *dZ, double *kl_partials,
+                                   uint8_t *zq, int32_t ldzq, uint8_t *zqs, void *stream) {
+  CC_REQUIRE(Z2 && y_reg && reg_idx && dZ && kl_partials && zq && zqs, "cc_dec_softmax_kl_q: null pointer");
+  CC_REQUIRE(ldzq % 128 == 0 && ldzq >= V && (uintptr_t)zq % 4 == 0, "cc_dec_softmax_kl_q: ldzq % 128, >= V");
+  CC_REQUIRE((V % 4 == 0) && ((uintptr_t)Z2 % 16 == 0) && ((uintptr_t)y_reg % 16 == 0) && ((uintptr_t)dZ % 16 == 0),
+             "cc_dec_softmax_kl_q: V % 4 == 0, 16-B aligned rows");
+  if (B == 0) return CC_OK;
+  const int nv = (int)cdiv(ldzq, 4 * NTR);
+  CC_REQUIRE(nv <= 8, "cc_dec_softmax_kl_q: ldzq <= 32768");
+  const hipStream_t s = as_stream(stream);
+#define KL_ROWS_Q(NVV)                                                                              \
+  if (nv <= NVV) {                                                                                  \
+    hipLaunchKernelGGL((softmax_kl_rows_kernel<bf16_t, NVV>), dim3(B), dim3(NTR), 0, s, Z2, V, y_reg, \
+                       reg_idx, scale, (bf16_t *)dZ, kl_partials, zq, ldzq, zqs);                   \
+    CC_LAUNCH_CHECK("softmax_kl_rows_kernel<q>");                                                   \
+    return CC_OK;                                                                                   \
+  }
+  KL_ROWS_Q(1)
+  KL_ROWS_Q(2)
+  KL_ROWS_Q(4)
+  KL_ROWS_Q(6)
+  KL_ROWS_Q(8)
+#undef KL_ROWS_Q
   return CC_OK;
 }

@@ -70,10 +70,13 @@ __global__ __launch_bounds__(64) void quant_rows_kernel(const T *__restrict__ sr
 // thread (rb = tid / 64, c = tid % 64) emits dst row (64 bx + c)'s block 4 by + rb, so the four
 // waves of a block write one whole 128-B line of each of its 64 dst rows.
 constexpr int QT_C = 64, QT_R = 128;
-template <typename T>
+// ROWS: the same tile also yields the row image (K = cols): 128 rows x 2 blocks of 32 columns, one
+// block per thread, from the staged tile — both images of a weight from one read of it
+template <typename T, bool ROWS = false>
 __global__ __launch_bounds__(256) void quant_t_kernel(const T *__restrict__ src, int rows, int cols,
                                                       int ld_src, uint8_t *__restrict__ dst, int ld_dst,
-                                                      uint8_t *__restrict__ scales) {
+                                                      uint8_t *__restrict__ scales, uint8_t *__restrict__ dst_r = nullptr,
+                                                      int ld_r = 0, uint8_t *__restrict__ scales_r = nullptr) {
   __shared__ float tile[QT_R][QT_C + 1];
   const int c0 = blockIdx.x * QT_C, r0 = blockIdx.y * QT_R;
   if (sizeof(T) == 2 && c0 + QT_C <= cols && (ld_src % 8) == 0 && ((uintptr_t)src % 16) == 0) {
@@ -118,6 +121,25 @@ __global__ __launch_bounds__(256) void quant_t_kernel(const T *__restrict__ src,
   uint32_t w[8];
   encode32(v, ex, w);
   if (c < cols) scales[(int64_t)c * (ld_dst / 32) + 4 * blockIdx.y + rb] = (uint8_t)(ex + 127);
+  if constexpr (ROWS) {  // row blocks (K = cols): thread -> row t / 2, columns 32 (t & 1) .. + 32
+    const int rr = threadIdx.x >> 1, b = threadIdx.x & 1;
+    float u[32];
+    float um = 0.f;
+#pragma unroll
+    for (int e = 0; e < 32; ++e) {
+      u[e] = tile[rr][32 * b + e];   // zero past cols (and past rows)
+      um = fmaxf(um, fabsf(u[e]));
+    }
+    const int eu = block_exp(um);
+    uint32_t wu[8];
+    encode32(u, eu, wu);
+    if (r0 + rr < rows) {
+      uint4 *d4 = reinterpret_cast<uint4 *>(dst_r + (int64_t)(r0 + rr) * ld_r + c0 + 32 * b);
+      d4[0] = make_uint4(wu[0], wu[1], wu[2], wu[3]);
+      d4[1] = make_uint4(wu[4], wu[5], wu[6], wu[7]);
+      scales_r[(int64_t)(r0 + rr) * (ld_r / 32) + c0 / 32 + b] = (uint8_t)(eu + 127);
+    }
+  }
   // re-lay the codes through LDS so each store instruction writes whole 128-B lines (8 lanes per dst
   // row) instead of 64 scattered 16-B pieces; rows padded to 9 x 16 B against bank conflicts
   __syncthreads();
@@ -168,5 +190,31 @@ extern "C" int cc_quant_mx8(int32_t dtype, const void *src, int32_t rows, int32_
     hipLaunchKernelGGL(quant_t_kernel<float>, grid, dim3(256), 0, s, (const float *)src, rows, cols, ld_src,
                        dst, ld_dst, scales);
   CC_LAUNCH_CHECK("quant_t_kernel");
+  return CC_OK;
+}
+
+// Both MX-FP8 images of one weight from a single read of it (config 5's decoder output kernel Wo
+// [d][V] after every Adam step): the transposed image dst_t [cols][ld_t] (K = rows, the forward
+// product's B operand) and the row image dst_r [rows][ld_r] (K = cols, the dX product's B operand,
+// columns [cols, ld_r) zero codes) — each bit-exact with cc_quant_mx8 of the same source.
+extern "C" int cc_quant_mx8_both(int32_t dtype, const void *src, int32_t rows, int32_t cols, int32_t ld_src,
+                                 uint8_t *dst_t, int32_t ld_t, uint8_t *scales_t, uint8_t *dst_r, int32_t ld_r,
+                                 uint8_t *scales_r, void *stream) {
+  CC_REQUIRE(src && dst_t && scales_t && dst_r && scales_r, "cc_quant_mx8_both: null pointer");
+  CC_REQUIRE(dtype == CC_BF16 || dtype == CC_F32, "cc_quant_mx8_both: dtype");
+  CC_REQUIRE(rows >= 0 && cols >= 0 && ld_src >= cols, "cc_quant_mx8_both: shape");
+  CC_REQUIRE(ld_t % 128 == 0 && ld_t >= rows && ld_r % 128 == 0 && ld_r >= cols &&
+                 (((uintptr_t)dst_t | (uintptr_t)dst_r) & 15) == 0,
+             "cc_quant_mx8_both: ld_t, ld_r multiples of 128 covering rows / cols, images 16-B aligned");
+  if (rows == 0 || cols == 0) return CC_OK;
+  const dim3 grid((unsigned)cdiv(ld_r, QT_C), (unsigned)(ld_t / QT_R));
+  hipStream_t s = as_stream(stream);
+  if (dtype == CC_BF16)
+    hipLaunchKernelGGL((quant_t_kernel<bf16_t, true>), grid, dim3(256), 0, s, (const bf16_t *)src, rows, cols, ld_src,
+                       dst_t, ld_t, scales_t, dst_r, ld_r, scales_r);
+  else
+    hipLaunchKernelGGL((quant_t_kernel<float, true>), grid, dim3(256), 0, s, (const float *)src, rows, cols, ld_src,
+                       dst_t, ld_t, scales_t, dst_r, ld_r, scales_r);
+  CC_LAUNCH_CHECK("quant_t_kernel<rows>");
   return CC_OK;
 }

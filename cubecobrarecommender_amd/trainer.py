@@ -593,11 +593,10 @@ class Trainer:
                 continue    # cc_dec_bce_dw reads Wo itself: no Wo^T copy for the D1 branch
             if k == 1 and self.fused_reg:
                 continue    # cc_dec_softmax_kl_dw reads Wo itself
-            if self.mx8:
-                L.call('cc_quant_mx8', L.CC_BF16, self.w(pre + '/reconstruct/kernel'), d, V, V, 1,
-                       L.ptr(self.WoT8[k]), d, L.ptr(self.WoT8s[k]), None, s)
-                L.call('cc_quant_mx8', L.CC_BF16, self.w(pre + '/reconstruct/kernel'), d, V, V, 0,
-                       L.ptr(self.Wo8[k]), self.Vp, L.ptr(self.Wo8s[k]), None, s)
+            if self.mx8:   # both images from one read of Wo (cc_quant_mx8_both)
+                L.call('cc_quant_mx8_both', L.CC_BF16, self.w(pre + '/reconstruct/kernel'), d, V, V,
+                       L.ptr(self.WoT8[k]), d, L.ptr(self.WoT8s[k]), L.ptr(self.Wo8[k]), self.Vp,
+                       L.ptr(self.Wo8s[k]), s)
             else:
                 L.call('cc_transpose', self.dtype, self.w(pre + '/reconstruct/kernel'), d, V,
                        L.ptr(self.WoT[k]), s)
@@ -806,9 +805,14 @@ class Trainer:
             # M~ row shard [lo, hi): the kernel indexes y_reg[reg_idx * V], so pass the base of
             # row 0 (reg_idx lies in [lo, hi) or is -1 for a masked padding row)
             y_base = L.C.c_void_p(self.data.y_reg.data_ptr() - self.reg_rows[0] * V * 4)
-            L.call('cc_dec_softmax_kl_fused', self.dtype, L.ptr(self.Z2), Br, V, y_base,
-                   L.ptr(self.reg_idx), float(self.kl_row_scale), L.ptr(self.dZout[B:]),
-                   L.ptr(self.kl_part), s)
+            if self.mx8:   # + dZ's MX-FP8 row image (the dX operand) from the same pass
+                L.call('cc_dec_softmax_kl_q', L.ptr(self.Z2), Br, V, y_base, L.ptr(self.reg_idx),
+                       float(self.kl_row_scale), L.ptr(self.dZout[B:]), L.ptr(self.kl_part),
+                       L.ptr(self.dZq[B:]), self.Vp, L.ptr(self.dZqs[B:]), s)
+            else:
+                L.call('cc_dec_softmax_kl_fused', self.dtype, L.ptr(self.Z2), Br, V, y_base,
+                       L.ptr(self.reg_idx), float(self.kl_row_scale), L.ptr(self.dZout[B:]),
+                       L.ptr(self.kl_part), s)
             t()
             if self.fused_tower:   # dZ2^T [V][Breg]: the k-contiguous operand of the reg branch's dW
                 L.call('cc_transpose', self.dtype, L.ptr(self.dZout[B:]), Br, V, L.ptr(self.dZt[1]), s)
@@ -821,9 +825,11 @@ class Trainer:
             nr = r1 - r0
             splits = self.splits if k == 0 else self.splits_reg
             if self.fused_tower:
-                if self.mx8 and not (k == 0 and self.mx8_bce_q):   # MX-FP8 dZ (dX A, K = V) and dZ^T (dW B, K = rows) + the bias grad
+                if self.mx8 and k == 0 and not self.mx8_bce_q:   # MX-FP8 dZ (dX A, K = V); the reg branch's
+                    # comes out of cc_dec_softmax_kl_q
                     L.call('cc_quant_mx8', L.CC_BF16, L.ptr(dz), nr, V, V, 0, L.ptr(self.dZq[r0:]), self.Vp,
                            L.ptr(self.dZqs[r0:]), None, s)
+                if self.mx8 and not (k == 0 and self.mx8_bce_q):   # MX-FP8 dZ^T (dW B, K = rows) + the bias grad
                     L.call('cc_quant_mx8', L.CC_BF16, L.ptr(self.dZt[k]), V, nr, nr, 0, L.ptr(self.dZtq[k]), nr,
                            L.ptr(self.dZtqs[k]), self.gp(pre + '/reconstruct/bias'), s)
                 gx = self._gemm(nr, d, self.Vp if self.mx8 else V, **self._dec_dx(k, r0, pre), ta=0, tb=1,

@@ -311,6 +311,12 @@ int cc_splitk_reduce_warm(int32_t dtype, const float *partials, int32_t splits, 
 int cc_quant_mx8(int32_t dtype, const void *src, int32_t rows, int32_t cols, int32_t ld_src,
                  int32_t transpose, uint8_t *dst, int32_t ld_dst, uint8_t *scales, float *rowsum,
                  void *stream);
+/* Both MX-FP8 images of src [rows][cols] from one read: dst_t [cols][ld_t] + scales_t (K = rows, =
+ * cc_quant_mx8 transpose=1) and dst_r [rows][ld_r] + scales_r (K = cols, = transpose=0), each
+ * bit-exact with cc_quant_mx8.  Config 5's decoder output kernels after every Adam step. */
+int cc_quant_mx8_both(int32_t dtype, const void *src, int32_t rows, int32_t cols, int32_t ld_src,
+                      uint8_t *dst_t, int32_t ld_t, uint8_t *scales_t, uint8_t *dst_r, int32_t ld_r,
+                      uint8_t *scales_r, void *stream);
 
 /* dst[c][r] = src[r][c] for a [rows, cols] row-major matrix (dtype elements). */
 int cc_transpose(int32_t dtype, const void *src, int32_t rows, int32_t cols, void *dst, void *stream);
@@ -436,6 +442,11 @@ int32_t cc_dec_bce_dw_blocks(int32_t V);
 int cc_dec_softmax_kl_fused(int32_t dtype, const float *Z2, int32_t B, int32_t V,
                             const float *y_reg, const int32_t *reg_idx, float scale, void *dZ,
                             double *kl_partials, void *stream);
+/* cc_dec_softmax_kl_fused (bf16 dZ) also writing dZ's MX-FP8 row image zq [B][ldzq] + zqs (K = V,
+ * bit-exact with cc_quant_mx8 of the bf16 dZ): config 5's regulariser branch. */
+int cc_dec_softmax_kl_q(const float *Z2, int32_t B, int32_t V, const float *y_reg, const int32_t *reg_idx,
+                        float scale, void *dZ, double *kl_partials, uint8_t *zq, int32_t ldzq, uint8_t *zqs,
+                        void *stream);
 /* D2 output layer fused (decreg.hip): logits -> softmax -> KL vs M~ rows -> dZ -> dWo/dbo with
  * no fp32 logits in HBM (model.py:64/98, train.py:85; TF 2.5 clip semantics).  Row r of the
  * regulariser rows is row row0 + r of the packed D3 images D3p ([R/32][d/16][64][8], act6p) and

@@ -284,3 +284,61 @@ def test_mx8_bce_q_matches_quantiser(M, N, K):
         assert torch.equal(a, b)
     torch.testing.assert_close(got[4], ref[4], rtol=1e-5, atol=1e-12)
     assert abs(got[5] - ref[5]) <= 1e-9 * abs(ref[5])
+
+
+@pytest.mark.parametrize('dtype', ['bf16', 'fp32'])
+@pytest.mark.parametrize('rows,cols,ld_t,ld_r', [(1024, 2200, 1024, 2304), (256, 1000, 256, 1024),
+                                                 (100, 257, 128, 384), (130, 64, 256, 128)])
+def test_quant_both_images_bit_exact(dtype, rows, cols, ld_t, ld_r):
+    """cc_quant_mx8_both (config 5's Wo images after Adam, one read) == cc_quant_mx8 transposed and
+    by rows, codes and scales bit for bit, padding included."""
+    rng = np.random.default_rng(rows + 3 * cols)
+    dt = L.CC_BF16 if dtype == 'bf16' else L.CC_F32
+    X = _data(rng, rows, cols)
+    src = (_bf16(X) if dt == L.CC_BF16 else torch.from_numpy(X)).cuda()
+    u8 = dict(device='cuda', dtype=torch.uint8)
+    imgs = []
+    for both in (False, True):
+        qt, st = torch.full((cols, ld_t), 0x5A, **u8), torch.full((cols, ld_t // 32), 0x5A, **u8)
+        qr, sr = torch.full((rows, ld_r), 0x5A, **u8), torch.full((rows, ld_r // 32), 0x5A, **u8)
+        if both:
+            L.call('cc_quant_mx8_both', dt, L.ptr(src), rows, cols, cols, L.ptr(qt), ld_t, L.ptr(st),
+                   L.ptr(qr), ld_r, L.ptr(sr), L.stream_ptr())
+        else:
+            L.call('cc_quant_mx8', dt, L.ptr(src), rows, cols, cols, 1, L.ptr(qt), ld_t, L.ptr(st), None, L.stream_ptr())
+            L.call('cc_quant_mx8', dt, L.ptr(src), rows, cols, cols, 0, L.ptr(qr), ld_r, L.ptr(sr), None, L.stream_ptr())
+        imgs.append((qt, st, qr, sr))
+    torch.cuda.synchronize()
+    for a, b in zip(*imgs):
+        assert torch.equal(a, b)
+
+
+def test_softmax_kl_q_matches_quantiser():
+    """cc_dec_softmax_kl_q (config 5's regulariser branch) == cc_dec_softmax_kl_fused + cc_quant_mx8
+    of its bf16 dZ: dZ, the KL partials, codes and scales bit for bit, a padding row included."""
+    rng = np.random.default_rng(7)
+    B_, V = 64, 3000
+    Vp = (V + 127) // 128 * 128
+    Z2 = torch.from_numpy(rng.standard_normal((B_, V)).astype(np.float32) * 3).cuda()
+    Mt = rng.random((50, V)).astype(np.float32)
+    Mt /= Mt.sum(1, keepdims=True)
+    Mt = torch.from_numpy(Mt).cuda()
+    idx = torch.from_numpy(rng.integers(0, 50, B_).astype(np.int32)).cuda()
+    idx[5] = -1
+    outs = []
+    for fused in (False, True):
+        dZ = torch.zeros(B_, V, device='cuda', dtype=torch.bfloat16)
+        part = torch.zeros(B_, device='cuda', dtype=torch.float64)
+        zq = torch.full((B_, Vp), 0x5A, device='cuda', dtype=torch.uint8)
+        zqs = torch.full((B_, Vp // 32), 0x5A, device='cuda', dtype=torch.uint8)
+        if fused:
+            L.call('cc_dec_softmax_kl_q', L.ptr(Z2), B_, V, L.ptr(Mt), L.ptr(idx), 0.1 / B_, L.ptr(dZ), L.ptr(part),
+                   L.ptr(zq), Vp, L.ptr(zqs), L.stream_ptr())
+        else:
+            L.call('cc_dec_softmax_kl_fused', L.CC_BF16, L.ptr(Z2), B_, V, L.ptr(Mt), L.ptr(idx), 0.1 / B_,
+                   L.ptr(dZ), L.ptr(part), L.stream_ptr())
+            L.call('cc_quant_mx8', L.CC_BF16, L.ptr(dZ), B_, V, V, 0, L.ptr(zq), Vp, L.ptr(zqs), None, L.stream_ptr())
+        outs.append((dZ, part, zq, zqs))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
