@@ -915,6 +915,10 @@ void cs_plan(int V, int d, int R, bool bias, int &tpc, int &nrc, size_t &lds, bo
   const int nsl = d / 32;
   // ~one block per CU (the slice is staged once per block), at most cs_tpw tiles per wave
   nrc = std::max(std::max(1, std::min(NTL, 256 / nsl)), (int)cdiv(NTL, (CS_NT / 64) * cs_tpw(xwm)));
+  // more blocks than CUs (d = 1024: 29 chunks x 32 slices = 928): whole rounds of 256 blocks, so
+  // the last round is not a fraction of the chip holding the whole launch (1024 blocks of 22 tiles
+  // instead of 928 of 24)
+  if (nrc * nsl > 256 && 256 % nsl == 0) nrc = (int)cdiv(nrc, 256 / nsl) * (256 / nsl);
   tpc = (int)cdiv(NTL, nrc);
   nrc = (int)cdiv(NTL, tpc);
   lds = (size_t)2 * xwm * 1024 + cs_lut_bytes(xwm, adam) + (adam ? (size_t)(CS_NT / 64) * 32 * 36 * 4 : 0);
