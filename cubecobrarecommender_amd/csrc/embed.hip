@@ -335,6 +335,107 @@ __global__ __launch_bounds__(64 * GWN) void gather_xcd_kernel(const bf16_t *__re
   l2_warm(warm, warm_bytes, (int)blockIdx.x, (int)gridDim.x);  // the tower forward's packed weights
 }
 
+// Forward, bf16 d = 512 / 1024: the same XCD column slicing with all eight XCDs on one row.  Block
+// nxt8 + b runs on XCD b % 8 and owns the (d / 8)-column slice b % 8 of row b / 8 (d = 1024: 256 B
+// of each W1 row per XCD, 5.6 MB of the 45 MB table; gather_kernel gave every block whole rows, so
+// every XCD's L2 streamed the whole table).  LPC = d / 64 lanes x 16 B cover one card's slice, a
+// wave load fetches G = 64 / LPC cards; the card groups are added lane-wise by xor shuffles, the
+// waves in order through LDS (deterministic).  The first nxt8 blocks (a multiple of 8, so the
+// slice mapping is unchanged) bit-transpose F's x rows into the W1-gradient bitmask when xt is
+// given, and the last block advances the step counters: no separate launches for either.
+template <int D, int GWN, int U>
+__global__ __launch_bounds__(64 * GWN) void gather_xcdw_kernel(const bf16_t *__restrict__ table,
+                                                              const float *__restrict__ bias,
+                                                              const int32_t *__restrict__ x_cnt,
+                                                              const int32_t *__restrict__ x_idx, int x_cap,
+                                                              bf16_t *__restrict__ out, int64_t *state, int64_t bpe,
+                                                              const uint32_t *__restrict__ xb, int V,
+                                                              uint32_t *__restrict__ xt, int xt_rows, int nxt8) {
+  constexpr int SW = D / 8, LPC = SW / 8, G = 64 / LPC;
+  if ((int)blockIdx.x < nxt8) {
+    const int nxt = xt ? (((V + 31) >> 5) + XT_TJ - 1) / XT_TJ : 0;
+    if ((int)blockIdx.x < nxt) xt_transpose_block(xb, V, xt, xt_rows, (int)blockIdx.x);
+    return;
+  }
+  if (state && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {  // the previous step's counters
+    state[0] += 1;
+    state[1] += 1;
+    if (state[1] >= bpe) {
+      state[1] = 0;
+      state[2] += 1;
+    }
+  }
+  __shared__ __attribute__((aligned(16))) float part[GWN][SW];
+  __shared__ int32_t ls[GIDX];
+  const int slice = (int)blockIdx.x & 7;
+  const int row = ((int)blockIdx.x - nxt8) >> 3;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane / LPC;
+  const int cl = (lane % LPC) * 8, c0 = slice * SW + cl;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  const int n = x_cnt[row];
+  const int q = ((n + GWN - 1) / GWN + G - 1) / G * G;  // chunks of whole G-card groups
+  const int i0 = min(n, w * q), i1 = min(n, i0 + q);
+  const int32_t *__restrict__ glst = x_idx + (int64_t)row * x_cap;
+  const bool staged = n <= GIDX;
+  if (staged)
+    for (int t = threadIdx.x; t < n; t += 64 * GWN) ls[t] = glst[t];
+  __syncthreads();
+  const int32_t *lst = staged ? ls : glst;
+  int i = i0;
+  for (; i + G * U <= i1; i += G * U) {
+    int j[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) j[u] = lst[i + G * u + g];
+    g_u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const g_u32x4 *>(table + (int64_t)j[u] * D + c0);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[2 * e] += __uint_as_float(v[u][e] << 16);
+        acc[2 * e + 1] += __uint_as_float(v[u][e] & 0xFFFF0000u);
+      }
+  }
+  for (; i < i1; i += G) {
+    if (i + g < i1) {
+      const g_u32x4 v = *reinterpret_cast<const g_u32x4 *>(table + (int64_t)lst[i + g] * D + c0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[2 * e] += __uint_as_float(v[e] << 16);
+        acc[2 * e + 1] += __uint_as_float(v[e] & 0xFFFF0000u);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = LPC; o < 64; o <<= 1)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += __shfl_xor(acc[e], o);
+  if (g == 0) {
+    *reinterpret_cast<float4 *>(&part[w][cl]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *reinterpret_cast<float4 *>(&part[w][cl + 4]) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  }
+  __syncthreads();
+  if (threadIdx.x < LPC) {
+    const int c = threadIdx.x * 8;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = part[0][c + e];
+#pragma unroll
+      for (int p = 1; p < GWN; ++p) v += part[p][c + e];
+      v += bias[slice * SW + c + e];
+      o[e] = v > 0.f ? v : 0.f;
+    }
+    g_u32x4 pk;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pk[e] = (uint32_t)f2bf(o[2 * e]) | ((uint32_t)f2bf(o[2 * e + 1]) << 16);
+    *reinterpret_cast<g_u32x4 *>(out + (int64_t)row * D + slice * SW + c) = pk;
+  }
+}
+
 // Backward: 4 waves per W1 row (row V = the bias when bias_grad is given); wave w walks the w-th
 // quarter of the row's bit words, collecting up to U set bits before issuing their dPre loads
 // together (heavy Zipf rows have a set bit for nearly every batch row).  Partials added in wave order.
@@ -1146,7 +1247,12 @@ extern "C" int cc_embed_gather_fwd_xt(int32_t dtype, const void *table, const fl
     const char *e = getenv("CCREC_GATHER2");
     return e ? atoi(e) : 48;
   }();
-  if (state && !(dtype == CC_BF16 && d == 256 && g2 > 0)) {  // other kernels: a separate launch
+  static const int gw = [] {  // A/B switch (dev): XCD column-sliced gather at d = 512 / 1024 (0 = gather_kernel)
+    const char *e = getenv("CCREC_GATHER_XCDW");
+    return e ? atoi(e) : 44;
+  }();
+  const bool xcdw = dtype == CC_BF16 && (d == 512 || d == 1024) && gw > 0 && R > 0 && R <= 4096;
+  if (state && !(dtype == CC_BF16 && d == 256 && g2 > 0) && !xcdw) {  // other kernels: a separate launch
     if (int rc = cc_state_advance(state, bpe, stream)) return rc;
     state = nullptr;
   }
@@ -1174,6 +1280,20 @@ extern "C" int cc_embed_gather_fwd_xt(int32_t dtype, const void *table, const fl
       return cc::fail(CC_ERR_UNSUPPORTED, "CCREC_GATHER_XCD: unknown variant");
 #undef GX
     CC_LAUNCH_CHECK("gather_xcd_kernel");
+    return CC_OK;
+  }
+  if (xcdw) {
+    const int nxt8 = (int)cdiv(nxt, 8) * 8;
+    const dim3 gwg((unsigned)(nxt8 + 8 * R));
+#define GW(D, GWN, U)                                                                                           \
+  if (d == D && gw == GWN * 10 + U)                                                                             \
+    hipLaunchKernelGGL((gather_xcdw_kernel<D, GWN, U>), gwg, dim3(64 * GWN), 0, s, (const bf16_t *)table, bias, \
+                       x_cnt, x_idx, x_cap, (bf16_t *)out, state, bpe, x_bits, V, xt_bits, xt_rows, nxt8);        \
+  else
+    GW(512, 4, 4) GW(512, 2, 8) GW(512, 4, 8) GW(1024, 4, 4) GW(1024, 2, 8) GW(1024, 4, 8)
+      return cc::fail(CC_ERR_UNSUPPORTED, "CCREC_GATHER_XCDW: unknown variant");
+#undef GW
+    CC_LAUNCH_CHECK("gather_xcdw_kernel");
     return CC_OK;
   }
   if (dtype == CC_BF16 && d == 256 && g2 > 0) {

@@ -89,7 +89,8 @@ def test_noise_bit_exact_vs_oracle(V, B, sizes, seed, step, glog2):
 
 @pytest.mark.parametrize('V,B,d,sizes,rows', [(22000, 64, 256, (180, 360, 720), 'R'), (1500, 64, 256, (40, 200, 400), 'R'),
                                                (1500, 64, 64, (40, 200, 400), 'R'), (300, 48, 256, (5, 30, 60), 'B'),
-                                               (1000, 40, 128, (5, 30, 60), 'B')])
+                                               (1000, 40, 128, (5, 30, 60), 'B'), (22000, 64, 1024, (180, 360, 720), 'R'),
+                                               (1500, 48, 512, (40, 200, 400), 'B')])
 def test_gather_xt_transpose(V, B, d, sizes, rows):
     """F with x_bits (row bitmasks, no xt atomics) + cc_embed_gather_fwd_xt's bit transpose (fused
     into the bf16 d = 256 gather, a separate kernel otherwise) == the xt bits F's atomics set, and
@@ -290,14 +291,16 @@ def test_gather_and_scatter(dtype, d):
     assert rel_err(grad.cpu().numpy(), gw) < 1e-6
 
 
+@pytest.mark.parametrize('d', [256, 512, 1024])
 @pytest.mark.parametrize('R', [51, 64])
-def test_gather_xcd_slices_edge_rows(R):
-    """The bf16 d = 256 E1 gather (XCD column slices: 4 slices x 2 row parities per 8 blocks): odd R
-    (the last block pair half empty), empty rows, one card, a row longer than the LDS index stage
-    (2,100 > 2,048: read from global), list tails that are not whole 8-card groups; every output
-    element within bf16 rounding of the fp64 sum, the counters advanced once."""
+def test_gather_xcd_slices_edge_rows(R, d):
+    """The bf16 E1 gathers by XCD column slices (d = 256: 4 slices x 2 row parities per 8 blocks;
+    d = 512 / 1024: 8 slices of one row, gather_xcdw_kernel): odd R (the last block pair half
+    empty), empty rows, one card, a row longer than the LDS index stage (2,100 > 2,048: read from
+    global), list tails that are not whole card groups; every output element within bf16 rounding
+    of the fp64 sum, the counters advanced once (inside the gather launch)."""
     rng = np.random.default_rng(R)
-    V, d, cap = 3000, 256, 2112
+    V, cap = 3000, 2112
     W = torch.from_numpy(rng.standard_normal((V, d)).astype(np.float32)).to('cuda', torch.bfloat16)
     b = torch.from_numpy(rng.standard_normal(d).astype(np.float32)).cuda()
     sizes = [0, 1, 2100, 7, 9, 63, 65] + [int(rng.integers(0, 800)) for _ in range(R - 7)]
