@@ -171,54 +171,30 @@ __global__ __launch_bounds__(NTR) void softmax_kl_rows_kernel(const float *__res
   double kl = rows_reduce<double, NTR / 64>((double)klf, redd, false);
   double S = rows_reduce<double, NTR / 64>((double)Sf32, redd, false);
   const float Sf = (float)S;
+  // dZ and, with zq, its MX-FP8 row image (K = V; columns [V, ldzq) zero codes) as cc_quant_mx8
+  // makes it from the bf16 dZ: the 8 lanes of a 32-column block share its scale.  One pass: the
+  // element values are computed once for both
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int j = threadIdx.x + i * NTR;
-    if (j >= V4) break;
+    if (!zq && j >= V4) break;
     float o[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = scale * (t[i][e] + z[i][e] * Sf);
-    if constexpr (sizeof(T) == 2) {
-      uint2 pk = make_uint2((uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16),
-                            (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16));
-      reinterpret_cast<uint2 *>(dZ + (int64_t)b * V)[j] = pk;
-    } else {
-      reinterpret_cast<float4 *>(dZ + (int64_t)b * V)[j] = make_float4(o[0], o[1], o[2], o[3]);
+    if (j < V4) {
+      if constexpr (sizeof(T) == 2) {
+        uint2 pk = make_uint2((uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16),
+                              (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16));
+        reinterpret_cast<uint2 *>(dZ + (int64_t)b * V)[j] = pk;
+      } else {
+        reinterpret_cast<float4 *>(dZ + (int64_t)b * V)[j] = make_float4(o[0], o[1], o[2], o[3]);
+      }
     }
-  }
-  if (zq) {   // the MX-FP8 row image of the bf16 dZ row (K = V; columns [V, ldzq) zero codes), as
-              // cc_quant_mx8 makes it: the 8 lanes of a 32-column block share its scale
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int j = threadIdx.x + i * NTR;
+    if (zq) {
       float v[4], amax = 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        v[e] = j < V4 ? bf2f(f2bf(scale * (t[i][e] + z[i][e] * Sf))) : 0.f;
-        amax = fmaxf(amax, fabsf(v[e]));
-      }
-      amax = fmaxf(amax, __shfl_xor(amax, 1));
-      amax = fmaxf(amax, __shfl_xor(amax, 2));
-      amax = fmaxf(amax, __shfl_xor(amax, 4));
-      const int ex = cc_mx8::block_exp(amax);
-      int word = 0;
-      word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[0], -ex), ldexpf(v[1], -ex), word, false);
-      word = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[2], -ex), ldexpf(v[3], -ex), word, true);
-      if (j < ldzq / 4) {
-        reinterpret_cast<uint32_t *>(zq + (int64_t)b * ldzq)[j] = (uint32_t)word;
-        if ((j & 7) == 0) zqs[(int64_t)b * (ldzq / 32) + j / 8] = (uint8_t)(ex + 127);
-      }
-    }
-  }
-  if (zq) {   // the MX-FP8 row image of the bf16 dZ row (K = V; columns [V, ldzq) zero codes), as
-              // cc_quant_mx8 makes it: the 8 lanes of a 32-column block share its scale
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int j = threadIdx.x + i * NTR;
-      float v[4], amax = 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = j < V4 ? bf2f(f2bf(scale * (t[i][e] + z[i][e] * Sf))) : 0.f;
+        v[e] = j < V4 ? bf2f(f2bf(o[e])) : 0.f;
         amax = fmaxf(amax, fabsf(v[e]));
       }
       amax = fmaxf(amax, __shfl_xor(amax, 1));
