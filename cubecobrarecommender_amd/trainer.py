@@ -46,6 +46,9 @@ class TrainConfig:
     wo_tower_frac: float = -1.0    # ... on this trailing fraction of each; the rest stays in the Adam + F
     #                                launch (< 0: measured per mode — 0.6 BCE only, 0.45 with the
     #                                sampled regulariser; tools/gpu_t8.sh, tools/gpu_t15.sh sweeps)
+    fuse_wo_adam8: bool = False    # fp8 + fuse_w1_adam: TF Adam on the output layers in the MX-FP8 dW
+    #                                epilogue (cc_gemm_mx8_pair_adam).  Bit-identical, but measured
+    #                                slower at config 5 (1000 vs 961-978 us/step): opt-in
     graph_steps: int = 8           # one process: consecutive steady-state steps per hipGraph replay (step_many)
     reg_mode: str = 'sampled'      # 'sampled': B reg rows per step drawn ∝ neg_sampler (generator.py:47-51);
     #                                'full': all |V| identity rows every step, KL(M~, D2(E(I))) as the
@@ -445,6 +448,27 @@ class Trainer:
                     rest.append((lo, a))
                     lo = b
                 self.rest_ranges = rest
+        # config 5 (MX-FP8 decoder products, one process; opt-in fuse_wo_adam8): TF Adam on the
+        # output layers (Wo, bo and with the sampled regulariser Wo_reg, bo_reg) in the dW product's
+        # epilogue (cc_gemm_mx8_pair_adam): their fp32 gradients are never stored nor re-read; the
+        # Adam + F launch covers the complement (rest_ranges).  Slower as measured: the 344 dW tiles
+        # on 256 CUs (one 132-KB-LDS block per CU) leave a second round of 88 tiles whose Adam
+        # streams at the per-CU rate, so the pair launch grows 71 -> 166 us, more than the ~230 us
+        # the Adam + F launch sheds
+        self.fuse_wo8 = (self.mx8 and self.fuse_w1 and self.rest_ranges is None and not self.full_reg
+                         and not self.layout.group_biases
+                         and cfg.V % 4 == 0 and cfg.fuse_wo_adam8)
+        self.fused_spans = []
+        if self.fuse_wo8:
+            lay = self.layout
+            wo_lo = lay.offset('decoder/reconstruct/kernel')
+            self.fused_spans = [(wo_lo, lay.main_total)]
+            rest = [(self.w1_off, wo_lo)]
+            if self.use_reg:
+                wr_lo = lay.offset('decoder_for_reg/reconstruct/kernel')
+                self.fused_spans.append((wr_lo, lay.total))
+                rest.append((lay.main_total, wr_lo))
+            self.rest_ranges = rest
         self.wo_range = self.wo_ranges[0] if self.wo_ranges else None   # (tests: is the placement on)
         self._adv_deferred = False   # the previous step's counter advance rides in the E1 gather
         self.noise_ready = False
@@ -849,6 +873,20 @@ class Trainer:
                            L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None,
                            L.ptr(wb) if wb is not None else None, 2 * wb.numel() if wb is not None else 0, s)
                     continue
+                if self.fuse_wo8:   # dX split-K + dW with TF Adam on Wo, bo in its epilogue
+                    gw = self._gemm(d, V, nr, **self._dec_dw(k, r0), ta=0, tb=1, launch=False)
+                    lay, cfg = self.layout, self.cfg
+                    ko, bo = lay.offset(pre + '/reconstruct/kernel'), lay.offset(pre + '/reconstruct/bias')
+                    t = self._tick('dec_dW')
+                    L.call('cc_gemm_mx8_pair_adam', L.C.byref(gx), L.C.byref(gw), L.ptr(self.params[ko:]),
+                           L.ptr(self.m[ko:]), L.ptr(self.v[ko:]), L.ptr(self.shadow[ko:]), L.ptr(self.params[bo:]),
+                           L.ptr(self.m[bo:]), L.ptr(self.v[bo:]), L.ptr(self.shadow[bo:]),
+                           self.gp(pre + '/reconstruct/bias'), L.ptr(self.state), cfg.lr, cfg.beta1, cfg.beta2,
+                           cfg.eps, s)
+                    t()
+                    L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), splits, nr, d,
+                           L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
+                    continue
                 gw = self._gemm(d, V, nr, **self._dec_dw(k, r0), ta=0, tb=1,
                                 Cf=self.gp(pre + '/reconstruct/kernel'),
                                 colsum=None if self.mx8 else self.gp(pre + '/reconstruct/bias'), launch=False)
@@ -1148,7 +1186,8 @@ class Trainer:
         s.wait_stream(torch.cuda.current_stream())
         saved = self.state.clone()
         # the fused W1 (and Wo) Adam updates them inside forward_backward: undo the warm-up's update
-        spans = ([(0, self.w1_off)] if self.fuse_w1 else []) + (list(self.wo_ranges) if self.wo_ranges else [])
+        spans = (([(0, self.w1_off)] if self.fuse_w1 else []) + (list(self.wo_ranges) if self.wo_ranges else [])
+                 + list(self.fused_spans))
         saved_spans = [[b[lo:hi].clone() for b in (self.params, self.m, self.v, self.shadow)] for lo, hi in spans]
         with torch.cuda.stream(s):           # warm-up launch outside capture (lazy module loads)
             self.forward_backward()

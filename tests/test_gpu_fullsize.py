@@ -244,14 +244,21 @@ def test_config5_full_size_matches_mx8_oracle():
     def y_rows(idx):
         return y_mtx[torch.as_tensor(idx, device='cuda').long()].cpu().numpy()
     lay = Layout(V, d)
+    # gradients the fused Adam placements never store (W1 in its gradient kernel, the output layers
+    # in the dW product's epilogue): recovered from the first moment, m1 = 0.9 m0 + 0.1 g
+    fused = (['encoder/encoded_1/kernel'] if tr.fuse_w1 else []) + (
+        [p + '/reconstruct/' + t for p in ('decoder', 'decoder_for_reg') for t in ('kernel', 'bias')]
+        if tr.fuse_wo8 else [])
+
+    def moments(name):
+        o, shape = tr.layout.offset(name), tr.layout.shape(name)
+        return tr.m[o:o + int(np.prod(shape))].double().cpu().numpy().reshape(shape)
     for step in range(2):
         P = lay.unpack(tr.standard(tr.params))
-        m0 = tr.m[:V * d].double().cpu().numpy()
+        m0 = {k: moments(k) for k in fused}
         tr.forward_backward()
         torch.cuda.synchronize()
-        over = None
-        if tr.fuse_w1:   # W1's gradient is not stored: recover it from the first moment
-            over = {'encoder/encoded_1/kernel': ((tr.m[:V * d].double().cpu().numpy() - 0.9 * m0) / 0.1).reshape(V, d)}
+        over = {k: (moments(k) - 0.9 * m0[k]) / 0.1 for k in fused}
         _check_step(tr, P, lists, perm, ns, step, reg, 'mx8', LOSS_TOL_MX8, GTOL_MX8, y_rows,
                     g_override=over, name='config5_full')
         tr.apply()
