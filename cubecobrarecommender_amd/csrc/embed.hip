@@ -736,7 +736,20 @@ __global__ __launch_bounds__(256, 2) void embed_grad_pk_kernel(const bf16_t *__r
 // by the last of its slice blocks to finish (a ticket per chunk, reset by that block: no spin, no
 // extra launch).
 constexpr int CS_NT = 512;                     // 8 waves, ~one block per CU
-constexpr int cs_tpw(int xwm) { return xwm <= 32 ? 3 : 1; }      // tiles per wave (registers)
+// config 5's instance (XWM = 32, R = 1024, TF Adam in the epilogue): tiles per wave, the Adam-operand
+// prefetch and the k-steps per fragment group trade registers (build-time A/B knobs)
+#ifndef EG_TPW32
+#define EG_TPW32 3
+#endif
+#ifndef EG_PF_XWM
+#define EG_PF_XWM 16
+#endif
+#ifndef EG_CSG32
+#define EG_CSG32 4
+#endif
+constexpr int cs_tpw(int xwm, bool adam = false) {  // tiles per wave (registers)
+  return xwm <= 16 ? 3 : xwm <= 32 ? (adam ? EG_TPW32 : 3) : 1;
+}
 // byte -> 8 bf16 (16 B) LUT lane copies: fewer where the LDS is short (R > 512 with the Adam
 // epilogue's re-layout tiles, R > 1024): 2-way bank conflicts at 8 copies
 constexpr int cs_lut_copies(int xwm, bool adam) { return xwm <= 16 ? 16 : xwm <= 32 ? (adam ? 8 : 16) : 4; }
@@ -824,7 +837,7 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
     }
   };
   constexpr int NW = CS_NT / 64;
-  constexpr int TPW = cs_tpw(XWM);  // tiles per wave (the host sizes tpc <= NW * TPW)
+  constexpr int TPW = cs_tpw(XWM, ADAM);  // tiles per wave (the host sizes tpc <= NW * TPW)
   uint32_t wds[TPW][XWM];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) load_bits(w + NW * i, wds[i]);
@@ -888,7 +901,7 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
   // (the Adam epilogue works on the tile re-laid through LDS: instruction g covers tile rows
   // 8 g .. 8 g + 7, lane l row 8 g + (l >> 3), columns 4 (l & 7) .. +3 — eight whole 128-B lines
   // per wave instruction instead of 32 partial ones)
-  constexpr bool PF = ADAM && EG_PREFETCH && XWM <= 16;
+  constexpr bool PF = ADAM && EG_PREFETCH && XWM <= EG_PF_XWM;
   constexpr int NBUF = PF ? 2 : 1;
   cc_adam::f32x4_t AP[NBUF][ADAM ? 4 : 1], AM[NBUF][ADAM ? 4 : 1], AV[NBUF][ADAM ? 4 : 1];
   auto issue_adam = [&](int t, int b) {
@@ -917,7 +930,7 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
     // ds_read_b128 of the staged slice.  Groups of CS_G k-steps: the next group's 2 CS_G reads are
     // issued (sched_barrier) before this group's MFMAs, so the LDS latency runs under them.  The
     // B address is made opaque per tile so the compiler does not hoist the whole slice into VGPRs.
-    constexpr int CS_G = 4, NG = 2 * XWM / CS_G;
+    constexpr int CS_G = (XWM == 32 && ADAM) ? EG_CSG32 : 4, NG = 2 * XWM / CS_G;
     uint32_t boff = (uint32_t)lane * 16u;  // byte offset of this lane's fragment slot in Bs
     asm volatile("" : "+v"(boff));
     auto fetch = [&](int g, bf16x8_t (&da)[CS_G], bf16x8_t (&db)[CS_G]) {
@@ -1015,7 +1028,7 @@ void cs_plan(int V, int d, int R, bool bias, int &tpc, int &nrc, size_t &lds, bo
   const int xwm = RPE / 32 <= 16 ? 16 : RPE / 32 <= 32 ? 32 : 64;  // the kernel's XWM
   const int nsl = d / 32;
   // ~one block per CU (the slice is staged once per block), at most cs_tpw tiles per wave
-  nrc = std::max(std::max(1, std::min(NTL, 256 / nsl)), (int)cdiv(NTL, (CS_NT / 64) * cs_tpw(xwm)));
+  nrc = std::max(std::max(1, std::min(NTL, 256 / nsl)), (int)cdiv(NTL, (CS_NT / 64) * cs_tpw(xwm, adam)));
   // more blocks than CUs (d = 1024: 29 chunks x 32 slices = 928): whole rounds of 256 blocks, so
   // the last round is not a fraction of the chip holding the whole launch (1024 blocks of 22 tiles
   // instead of 928 of 24)
@@ -1029,10 +1042,11 @@ void cs_plan(int V, int d, int R, bool bias, int &tpc, int &nrc, size_t &lds, bo
 
 extern "C" int32_t cc_embed_grad_cs_tickets(int32_t V, int32_t d, int32_t R) {
   if (V <= 0 || d < 32 || R <= 0) return 0;
-  int tpc, nrc;
+  int tpc, nrc, nrc_adam;
   size_t lds;
   cs_plan(V, d, R, true, tpc, nrc, lds);
-  return nrc;
+  cs_plan(V, d, R, true, tpc, nrc_adam, lds, true);  // (the Adam instance may chunk finer)
+  return std::max(nrc, nrc_adam);
 }
 
 static int embed_grad_cs_launch(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R, int32_t ld_t,

@@ -103,6 +103,31 @@ __device__ __forceinline__ Tv rows_reduce(Tv v, Tv *red, bool is_max) {
   return r;
 }
 
+// two fp64 sums reduced together (the same xor tree and wave order per value as rows_reduce: the
+// same results, one barrier pair instead of two)
+template <int W>
+__device__ __forceinline__ void rows_reduce2(double &a, double &b, double *red) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off);
+    b += __shfl_xor(b, off);
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = a;
+    red[W + (threadIdx.x >> 6)] = b;
+  }
+  __syncthreads();
+  double ra = red[0], rb = red[W];
+#pragma unroll
+  for (int w = 1; w < W; ++w) {
+    ra += red[w];
+    rb += red[W + w];
+  }
+  a = ra;
+  b = rb;
+}
+
 template <typename T, int NV>
 __global__ __launch_bounds__(NTR) void softmax_kl_rows_kernel(const float *__restrict__ Z2, int V,
                                                               const float *__restrict__ Mt,
@@ -112,7 +137,7 @@ __global__ __launch_bounds__(NTR) void softmax_kl_rows_kernel(const float *__res
                                                               uint8_t *__restrict__ zq = nullptr, int ldzq = 0,
                                                               uint8_t *__restrict__ zqs = nullptr) {
   __shared__ float redf[NTR / 64];
-  __shared__ double redd[NTR / 64];
+  __shared__ double redd[2 * (NTR / 64)];
   const int b = blockIdx.x, V4 = V >> 2;
   if (reg_idx[b] < 0) {  // padding row (owner-computes capacity): no KL term, zero gradient
     for (int j = threadIdx.x; j < V; j += NTR) DT<T>::st(dZ + (int64_t)b * V + j, 0.f);
@@ -168,8 +193,8 @@ __global__ __launch_bounds__(NTR) void softmax_kl_rows_kernel(const float *__res
       t[i][e] = p >= 1e-7f ? -tc : 0.f;
     }
   }
-  double kl = rows_reduce<double, NTR / 64>((double)klf, redd, false);
-  double S = rows_reduce<double, NTR / 64>((double)Sf32, redd, false);
+  double kl = (double)klf, S = (double)Sf32;
+  rows_reduce2<NTR / 64>(kl, S, redd);
   const float Sf = (float)S;
   // dZ and, with zq, its MX-FP8 row image (K = V; columns [V, ldzq) zero codes) as cc_quant_mx8
   // makes it from the bf16 dZ: the 8 lanes of a 32-column block share its scale.  One pass: the
