@@ -18,6 +18,7 @@ import torch
 
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA (spec, no sparsity)
+MX8_PEAK_TFLOPS = 5000.0    # dense (MX-)FP8 MFMA (spec, no sparsity)
 
 
 def parse():
@@ -38,6 +39,9 @@ def parse():
     ap.add_argument('--reg-mode', default='sampled', choices=('sampled', 'full'),
                     help="sampled: B reg rows per step drawn from neg_sampler (generator.py:47-51); "
                          "full: all |V| identity rows every step (README.md:27, the |V|x|V| MFMA path)")
+    ap.add_argument('--force-dp', action='store_true',
+                    help='one GPU driving the data-parallel step through a 1-rank RCCL process group '
+                         '(the per-rank kernel and exchange sequence the N-GPU run executes)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-steps', type=int, default=16)
     ap.add_argument('--no-recommend', action='store_true')
@@ -85,6 +89,11 @@ def setup_dist(args):
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
         else:
             dist.init_process_group(args.backend)
+    elif args.force_dp:   # a 1-rank RCCL group: zero.py's collectives on device tensors
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', store=dist.HashStore(), rank=0, world_size=1,
+                                device_id=torch.device('cuda', local))
     return world, rank, local
 
 
@@ -94,10 +103,17 @@ def barrier(world):
         dist.barrier()
 
 
+PEAKS = {'hbm': (HBM_PEAK_GBS, 'GB/s'), 'mfma': (BF16_PEAK_TFLOPS, 'TFLOP/s'),
+         'mfma_mx8': (MX8_PEAK_TFLOPS, 'TFLOP/s')}
+
+
 def roofline_for(name, ms, tr):
-    """Algorithmic bytes/flops per launch of the instrumented kernel."""
+    """Algorithmic bytes (HBM-bound kernels) or flops (MFMA products) per launch of an
+    instrumented kernel, and the achieved rate at the measured duration `ms`."""
     cfg = tr.cfg
     V, d, B = cfg.V, cfg.d, cfg.batch_size
+    fl = byt = None
+    kind = 'mfma'
     if name == 'cc_adam_dense':
         n = tr.layout.total if tr.use_reg else tr.layout.main_total
         if getattr(tr, 'fuse_w1', False):     # W1's Adam runs in its gradient kernel
@@ -105,29 +121,75 @@ def roofline_for(name, ms, tr):
         for lo, hi in (getattr(tr, 'wo_ranges', None) or ()):   # (the output layers' tails: in the
             n -= hi - lo                                          # tower backward launch)
         byt = n * (16 + 12 + 2)                    # read p,m,v,g; write p,m,v; write bf16 shadow
-        return {'bound': 'hbm', 'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
-                'unit': 'GB/s', 'bytes_per_launch': byt}
-    if name in ('dec_bce_fwd', 'dec_dW', 'dec_dX'):
+        what = ('adam_noise_kernel (TF Adam over the parameters not updated elsewhere + F of the next step; '
+                'bytes counted are Adam\'s only, F adds <2%)' if getattr(tr, 'prefetch', False)
+                else 'adam_kernel (cc_adam_dense)')
+    elif name == 'dec_bce_fwd':
+        if getattr(tr, 'fused_out', False):  # logits + dWo = D3^T dZ in one pass (dX: its own launch)
+            fl = 2 * 2.0 * B * d * V
+            what = 'dec_bce_dw_kernel (fused D1: logits + sigmoid/BCE + dZ + dWo/dbo; flops = logits + dWo)'
+        else:
+            fl = 2.0 * B * d * V
+            what = ('mx8_wide_kernel (MX-FP8 logits + BCE epilogue)' if tr.mx8 else 'gemm (D1 logits + BCE epilogue)')
+        if tr.mx8:
+            kind = 'mfma_mx8'
+    elif name == 'dec_softmax_kl' and getattr(tr, 'fused_reg', False):
+        fl = 3 * 2.0 * tr.Breg * d * V      # logits twice (stats, main) + dWo
+        what = 'kl_stats + kl_main (fused D2: logits twice, softmax/KL, dZ, dWo/dbo)'
+    elif name == 'dec_dX':
         fl = 2.0 * B * d * V
-        return {'bound': 'mfma', 'achieved': fl / (ms * 1e-3) / 1e12, 'peak': BF16_PEAK_TFLOPS,
-                'unit': 'TFLOP/s', 'flops_per_launch': fl}
-    if name == 'cc_embed_gather_fwd':
-        xs = tr.x_cnt.float().mean().item()
-        byt = tr.R * xs * d * 2 + tr.R * d * 2
-        return {'bound': 'hbm', 'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
-                'unit': 'GB/s', 'bytes_per_launch': byt}
-    if name == 'cc_embed_scatter_bwd' and getattr(tr, 'fuse_w1', False):
+        what = 'dX split-K (dD3 = dZ Wo^T) + reduce'
+        if tr.mx8:
+            kind = 'mfma_mx8'
+    elif name == 'cc_embed_scatter_bwd' and getattr(tr, 'fuse_w1', False):
         # W1 [V][d]: p, m, v read + written (24 B), bf16 shadow written (2 B); the row bit matrix
         # (V x ceil(rows/32) words) and the packed dPre1 image (rows x d bf16) read; b1's gradient row
         rows = getattr(tr, 'xt_rows', tr.R)
         byt = V * d * 26 + V * ((rows + 31) // 32) * 4 + ((rows + 63) // 64 * 64) * d * 2 + d * 4
-        return {'bound': 'hbm', 'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
-                'unit': 'GB/s', 'bytes_per_launch': byt}
-    if name == 'cc_embed_scatter_bwd':
+        what = ('embed_grad_cs_kernel<.., ADAM> (cc_embed_grad_cs_adam: the W1 gradient X^T dPre1 from the '
+                'bit-transposed batch on MFMA, TF Adam on W1 in its epilogue; bytes: W1 p/m/v read + write, '
+                'the bf16 shadow, the bit matrix and the dPre1 image)')
+    elif name == 'cc_embed_scatter_bwd':
         byt = V * d * 4 + V * ((tr.R + 31) // 32) * 4
-        return {'bound': 'hbm', 'achieved': byt / (ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
-                'unit': 'GB/s', 'bytes_per_launch': byt}
-    return None
+        what = 'embed_grad (the W1 gradient X^T dPre1, stored fp32)'
+    else:
+        return None
+    if byt is not None:
+        kind, work = 'hbm', byt
+        rate = byt / (ms * 1e-3) / 1e9
+    else:
+        work = fl
+        rate = fl / (ms * 1e-3) / 1e12
+    peak, unit = PEAKS[kind]
+    return {'bound': 'hbm' if kind == 'hbm' else 'mfma', 'achieved': rate, 'peak': peak, 'unit': unit,
+            'frac': rate / peak, ('bytes_per_launch' if byt is not None else 'flops_per_launch'): work,
+            'avg_us': ms * 1e3, 'kernel': what, 'tick': name}
+
+
+# rocprofv3 kernel-name keys of the PMC traffic table (profiles/traffic_*.json) per instrumented tick
+TRAFFIC_KEYS = {'cc_embed_scatter_bwd': 'embed_grad_cs_kernel', 'cc_adam_dense': 'adam_noise_kernel',
+                'dec_bce_fwd': 'dec_bce_dw_kernel'}
+
+
+def kernel_rooflines(tr, kt, traffic_json):
+    """Roofline entries of the step's instrumented kernels, longest first.  kt: steady-state
+    per-kernel durations (us) from kernel_profile (HIP events on the launching stream)."""
+    tj = json.load(open(traffic_json)) if traffic_json and os.path.exists(traffic_json) else {}
+    out = []
+    for name, us in sorted(kt.items(), key=lambda kv: -kv[1]):
+        r = roofline_for(name, us * 1e-3, tr)
+        if r is None:
+            continue
+        r['traffic'] = None
+        t = tj.get(TRAFFIC_KEYS.get(name, ''), {})
+        tb = t.get('bytes_per_launch')
+        ref = r.get('bytes_per_launch') or t.get('algorithmic_bytes')
+        # PMC bytes were collected on one build / configuration: attach only to the same launch
+        if tb and ref and (r['bound'] == 'mfma' or abs(tb - ref) <= 0.10 * ref):
+            r['traffic'] = tb
+            r['traffic_detail'] = t
+        out.append(r)
+    return out
 
 
 def workload_label(args, world):
@@ -137,7 +199,7 @@ def workload_label(args, world):
         ' + backward + Adam)'
     if args.dtype == 'fp8':
         idx = 4
-    elif world > 1:
+    elif world > 1 or args.force_dp:
         idx = 3
     else:
         idx = 2 if args.reg > 0 else 1
@@ -163,6 +225,62 @@ def kernel_profile(tr, step, samples=8):
             torch.cuda.synchronize()
             tr.events = {}
     return {k: 1e3 * v for k, v in tr.kernel_times_ms().items()}
+
+
+def dp_profile(tr, step, samples=8, replays=40):
+    """Data-parallel per-rank report (after the timed region): per gradient bucket the collectives'
+    and the sharded Adam's durations (HIP events on the comm stream, eager steps queued behind graph
+    replays), and the whole-step graph replayed with and without its collectives — the difference is
+    the exchange time the step does not hide behind compute."""
+    import torch.distributed as dist
+    sh = tr.sharded
+    sh.adam_events, sh.comm_events = [], {}
+    for i in range(samples + 1):
+        for _ in range(3):
+            step(True)
+        step(False, timed=True)
+        if i == 0:
+            torch.cuda.synchronize()
+            sh.adam_events, sh.comm_events = [], {}
+    torch.cuda.synchronize()
+    rep = {'buckets': {}}
+    for (bname, what), evs in sorted(sh.comm_events.items()):
+        rep['buckets'].setdefault(bname, {})[what + '_us'] = 1e3 * float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    for b in sh.buckets:
+        ent = rep['buckets'].setdefault(b['name'], {})
+        ent['elements'] = b['hi'] - b['lo']
+        ent['shard'] = b['chunk']
+    n_sh = sum(n for _, _, n in sh.adam_events) / samples
+    adam_us = 1e3 * sum(a.elapsed_time(b) for a, b, _ in sh.adam_events) / samples
+    byt = n_sh * (16 + 12 + 2)
+    rep['_adam'] = {'tick': 'sharded_adam', 'kernel': 'adam_kernel (cc_adam_dense on this rank\'s 1/world shard '
+                    'of every bucket; sum over the buckets per step)', 'bound': 'hbm',
+                    'achieved': byt / (adam_us * 1e-6) / 1e9, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                    'frac': byt / (adam_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 'bytes_per_launch': byt,
+                    'avg_us': adam_us, 'traffic': None}
+    if tr.g_dp is not None:
+        times = {}
+        for key, g in (('step_us', tr.g_dp), ('step_without_exchange_us', tr.g_dp_nocomm),
+                       ('step_us_again', tr.g_dp)):
+            for _ in range(3):
+                g.replay()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(replays):
+                g.replay()
+            torch.cuda.synchronize()
+            dt = torch.tensor([(time.perf_counter() - t0) / replays], device=tr.params.device, dtype=torch.float64)
+            if dist.get_world_size() > 1:
+                dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            times[key] = 1e6 * float(dt.item())
+        rep.update(times)
+        rep['exposed_exchange_us'] = 0.5 * (times['step_us'] + times['step_us_again']) - times['step_without_exchange_us']
+        rep['graph'] = 'whole DP step as one hipGraph (RCCL collectives captured on the comm stream)'
+    else:
+        rep['graph'] = 'graph parts with eager collectives between them (gloo or dp_graph off)'
+    rep['backend'] = dist.get_backend()
+    rep['world'] = dist.get_world_size()
+    return rep
 
 
 def step_roofline(tr, ms_per_step, kt):
@@ -307,11 +425,11 @@ def main():
     indptr, indices = synthetic_cubes(args.cubes, V, seed=20250301, device=dev)
     ns = neg_sampler_from_csr(indptr, indices, V)
     y_mtx, reg_rows = None, None
-    reg_shard = bool(args.reg_shard) and world > 1 and args.reg > 0
+    reg_shard = bool(args.reg_shard) and (world > 1 or args.force_dp) and args.reg > 0
     if args.reg > 0:
         from cubecobrarecommender_amd.adjacency import adjacency_normalised_gpu
         y_mtx = adjacency_normalised_gpu(indptr, indices, V, device=dev)
-        if world > 1 and (reg_shard or args.reg_mode == 'full'):    # keep only this rank's rows of M~
+        if (world > 1 or args.force_dp) and (reg_shard or args.reg_mode == 'full'):   # this rank's rows of M~
             from cubecobrarecommender_amd.trainer import reg_rows_for
             reg_rows = reg_rows_for(ns, world, rank, args.reg_mode)
             y_mtx = y_mtx[reg_rows[0]:reg_rows[1]].clone()
@@ -321,6 +439,7 @@ def main():
     del y_mtx
     cfg = TrainConfig(V=V, d=d, batch_size=B, reg=args.reg, dtype=args.dtype, seed=1234,
                       rank=rank, world=world, reg_shard=reg_shard, reg_mode=args.reg_mode,
+                      force_dp=args.force_dp,
                       fuse_w1_adam=True,   # one process: W1's Adam in its gradient kernel, and (BCE
                       wo_adam_in_tower=True)   # only) Wo's in the tower backward launch (parity:
     #                                        tests/test_gpu_train.py::test_fused_w1_adam_matches_unfused)
@@ -329,54 +448,29 @@ def main():
     tr.set_epoch_permutations(np.stack([rng.permutation(args.cubes) for _ in range(4)]))
     setup_s = time.perf_counter() - t_setup
 
-    n_grad = tr.layout.total if tr.use_reg else tr.layout.main_total
-
-    adam_ev = []
-    ADAM_SAMPLE = 50
+    dp = tr.dp
 
     def step(graphed, timed=False):
-        if world > 1:   # bucketed reduce-scatter + sharded Adam + all-gather (zero.py)
-            if not graphed:
-                saved, tr.graphs = tr.graphs, None
+        if dp:   # bucketed reduce-scatter + sharded Adam + all-gather (zero.py)
+            if graphed:
                 tr.step_dp()
-                tr.graphs = saved
-            else:
-                tr.step_dp(timing=timed)
+            else:             # eager parts (kernel_profile's HIP events need eager launches)
+                tr._dp_call(None, timing=timed)
             return
-        if timed and graphed:
-            # a sampled step, launched eagerly with HIP events on the stream around each kernel
-            # (the host is far ahead of the GPU, so every kernel is queued when its start event
-            # fires: each interval is the kernel's own duration); the HBM-bound W1-gradient + W1
-            # Adam kernel and the Adam + F launch are the roofline candidates
-            saved, tr.graphs = tr.graphs, None
-            tr.events, tr.timing = {}, True
-            tr.step()
-            tr.timing, tr.graphs = False, saved
-            for k in ('cc_embed_scatter_bwd', 'cc_adam_dense'):
-                adam_ev.extend((k, e0, e1) for e0, e1 in tr.events.get(k, ()))
-            tr.events = {}
-        else:
-            saved, tr.graphs = tr.graphs, (tr.graphs if graphed else None)
-            tr.step()
-            tr.graphs = saved
+        saved, tr.graphs = tr.graphs, (tr.graphs if graphed else None)
+        tr.step()
+        tr.graphs = saved
 
-    def steps(n, timed=False):
-        """n graphed steps.  One process: every ADAM_SAMPLE-th timed step is the sampled step above;
-        the others replay tr.step_many's multi-step graph (cfg.graph_steps whole steps per replay,
-        single-step graphs for the remainder).  Data parallel: step by step."""
-        if world > 1:
+    def steps(n):
+        """n steady-state steps: one process replays tr.step_many's multi-step graph (cfg.graph_steps
+        whole steps per replay, single-step graphs for the remainder); data parallel replays the
+        whole DP step graph (RCCL collectives inside) step by step.  Nothing else runs in the timed
+        region: the per-kernel durations come from kernel_profile after it."""
+        if dp:
             for _ in range(n):
-                step(True, timed)
+                step(True)
             return
-        i = 0
-        while i < n:
-            if timed and i % ADAM_SAMPLE == 0:
-                step(True, timed=True)
-                i += 1
-                continue
-            m = min(n - i, ADAM_SAMPLE - i % ADAM_SAMPLE) if timed else n - i
-            tr.step_many(m)
-            i += m
+        tr.step_many(n)
 
     for _ in range(3):          # eager steps: module loads, lazy allocations
         step(False)
@@ -387,7 +481,7 @@ def main():
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    steps(args.steps, timed=True)
+    steps(args.steps)
     barrier(world)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -401,62 +495,26 @@ def main():
     # per-kernel steady-state times (HIP events; with DP the collectives and the sharded Adam run
     # between the ticked kernels and are not in them): every rank runs the same extra steps
     ktimes = kernel_profile(tr, step)
+    dp_report = dp_profile(tr, step) if dp else None
     if rank != 0:
         if world > 1:
             import torch.distributed as dist
             dist.destroy_process_group()
         return
     value = B * world * args.steps / dt
-    if world == 1:
-        ms = {k: float(np.mean([a.elapsed_time(b) for kk, a, b in adam_ev if kk == k]))
-              for k in ('cc_embed_scatter_bwd', 'cc_adam_dense') if any(kk == k for kk, _, _ in adam_ev)}
-        # the dominant HBM-bound kernel: the W1-gradient kernel when W1's Adam rides in it and it
-        # takes longer than the Adam launch (the BCE line), else the Adam launch
-        dom = ('cc_embed_scatter_bwd' if getattr(tr, 'fuse_w1', False) and 'cc_embed_scatter_bwd' in ms
-               and ms['cc_embed_scatter_bwd'] >= ms.get('cc_adam_dense', 0.0) else 'cc_adam_dense')
-        adam_ms = ms[dom]
-        roof = roofline_for(dom, adam_ms, tr)
-        roof['measured'] = ('HIP events around the kernel on its stream in every %d-th timed step (an '
-                            'eager step between the multi-step graph replays); other candidate: %s'
-                            % (ADAM_SAMPLE, {k: round(v * 1e3, 2) for k, v in ms.items()}))
-        roof['traffic'] = None
-        if args.traffic_json and os.path.exists(args.traffic_json):
-            # PMC bytes were collected on one configuration: attach them only to the same launch
-            key = ('embed_grad_cs_kernel' if dom == 'cc_embed_scatter_bwd' else
-                   'adam_noise_kernel' if getattr(tr, 'prefetch', False) else 'adam_kernel')
-            tj = json.load(open(args.traffic_json)).get(key) or {}
-            tb = tj.get('bytes_per_launch')
-            # (the launch also runs the next step's F: its ~12 MB of batch-buffer traffic rides along)
-            if tb and abs(tb - roof['bytes_per_launch']) <= 0.10 * roof['bytes_per_launch']:
-                roof['traffic'] = tb
-                roof['traffic_detail'] = tj
-    else:   # sharded Adam: this rank's 1/world shard of every bucket, per step
-        dom = None
-        torch.cuda.synchronize()
-        ev = tr.sharded.adam_events
-        n_sh = sum(n for _, _, n in ev) / args.steps
-        adam_ms = sum(a.elapsed_time(b) for a, b, _ in ev) / args.steps
-        byt = n_sh * (16 + 12 + 2)
-        roof = {'bound': 'hbm', 'achieved': byt / (adam_ms * 1e-3) / 1e9, 'peak': HBM_PEAK_GBS,
-                'unit': 'GB/s', 'bytes_per_launch': byt, 'traffic': None,
-                'measured': 'HIP events around the sharded Adam kernels on the comm stream (sum per step)'}
-    roof['frac'] = roof['achieved'] / roof['peak']
-    if world == 1 and dom == 'cc_embed_scatter_bwd':
-        roof['kernel'] = ('embed_grad_cs_kernel<.., ADAM> (cc_embed_grad_cs_adam: the W1 gradient X^T dPre1 from '
-                          'the bit-transposed batch on MFMA, TF Adam on W1 in its epilogue; bytes: W1 p/m/v read + '
-                          'write, the bf16 shadow, the bit matrix and the dPre1 image)')
-    elif world == 1 and getattr(tr, 'adam_packs', False):
-        roof['kernel'] = ('adam_noise_kernel<true> (cc_adam_noise_pack: TF Adam over all parameters '
-                          + ('after W1 (W1\'s Adam runs in the W1-gradient kernel, cc_embed_grad_cs_adam) '
-                             if getattr(tr, 'fuse_w1', False) else '')
-                          + '+ F of the next step + the tower kernels\' packed bf16 images in the same launch; '
-                          'bytes counted are Adam\'s only, F and the images add <2%)')
-    elif world == 1 and getattr(tr, 'prefetch', False):
-        roof['kernel'] = ('adam_noise_kernel (cc_adam_noise: TF Adam over all parameters + F of the '
-                          'next step in the same launch; bytes counted are Adam\'s only, F adds <2%)')
-    else:
-        roof['kernel'] = 'adam_kernel (cc_adam_dense)'
-    roof['avg_ms'] = adam_ms
+    kr = kernel_rooflines(tr, ktimes, args.traffic_json)
+    if dp:   # the sharded Adam: this rank's 1/world shard of every bucket, per step
+        ev = dp_report.pop('_adam')
+        kr.append(ev)
+        kr.sort(key=lambda r: -r['avg_us'])
+    roof = dict(kr[0]) if kr else {'bound': 'hbm', 'achieved': None, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                                   'frac': None, 'traffic': None}
+    roof['measured'] = ('the step\'s longest kernel with a stated algorithmic cost; its average duration from '
+                        'HIP events on its stream around the kernels of eager steps queued behind whole-step '
+                        'graph replays, after the timed region (bench.kernel_profile); the timed region '
+                        'replays graphs only')
+    roof['others'] = [{k: r[k] for k in ('tick', 'kernel', 'bound', 'achieved', 'unit', 'frac', 'avg_us', 'traffic')}
+                      for r in kr[1:]]
     out = {
         'metric': 'training cubes/sec at |V|~22k d=256; top-N recommend p50 latency',
         'value': value, 'unit': 'cubes/s', 'n_gpus': world, 'steps': args.steps,
@@ -467,14 +525,18 @@ def main():
                    'V': V, 'd': d, 'batch_per_gpu': B, 'global_batch': B * world, 'reg': args.reg,
                    'reg_mode': args.reg_mode, 'reg_rows_per_gpu': tr.Breg,
                    'reg_shard': 'owner computes' if tr.owner else ('full rows' if tr.full_reg and world > 1 else 'replicated'),
-                   'cubes': args.cubes, 'parallelism': f'dp{world}',
-                   'graph_steps': tr.multi_n if world == 1 else 1},
+                   'cubes': args.cubes,
+                   'parallelism': f'dp{world}' + (' (1-rank RCCL group driving the data-parallel step)'
+                                                  if args.force_dp and world == 1 else ''),
+                   'graph_steps': tr.multi_n if not dp else 1},
         'roofline': roof,
         'step_roofline': step_roofline(tr, dt / args.steps * 1e3, ktimes),
         'kernel_us': ktimes,
         'final_loss': losses,
         'setup_s': setup_s,
     }
+    if dp:
+        out['dp'] = dp_report
     if not args.no_recommend and world == 1:
         out['recommend'] = recommend_latency()
     if not args.no_cpu_baseline and world == 1:

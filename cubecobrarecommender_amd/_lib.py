@@ -97,6 +97,7 @@ SIGNATURES = {
     'cc_embed_scatter_bwd': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_embed_grad_mfma': (C.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_gemm': (C.c_int, [C.POINTER(GemmArgs), _P]),
+    'cc_gemm_tile128': (C.c_int, [C.POINTER(GemmArgs), _P]),
     'cc_gemm_pair': (C.c_int, [C.POINTER(GemmArgs), C.POINTER(GemmArgs), _P]),
     'cc_gemm_mx8_wide': (C.c_int, [C.POINTER(GemmArgs), C.POINTER(GemmArgs), _P]),
     'cc_gemm_mx8_bce_q': (C.c_int, [C.POINTER(GemmArgs), _P, C.c_int32, _P, _P, C.c_int32, _P, _P, _P]),
@@ -143,6 +144,7 @@ SIGNATURES = {
     'cc_embed_identity_ws': (_SZ, [_I32, _I32]),
     'cc_embed_identity_add': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_reg_rows': (C.c_int, [C.POINTER(NoiseArgs), _P]),
+    'cc_noise_next': (C.c_int, [C.POINTER(NoiseArgs), _I64, _P]),
     'cc_tower_slab_elems': (_I64, [_I32]),
     'cc_tower_fwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_bwd': (C.c_int, [C.POINTER(TowerArgs), _P]),

@@ -49,8 +49,13 @@ for _pre, _tag in (('decoder', 'main'), ('decoder_for_reg', 'reg')):
 # compiled metrics' accumulators (keras_api/metrics/<i>/{total,count}).  The reference's own
 # checkpoints pin their total: the GPU shard of every 2-shard save is 391,661,320 B = 12 * P + 40
 # at |V| = 20,884, d = 512 (P = 32,638,440: weights + Adam m + v), i.e. 40 B of scalars beside the
-# object graph (shard 0, 18,317 B) — 8 (iter) + 4 * 4 (learning_rate, beta_1, beta_2, decay) + 2 *
-# 2 * 4 (two Mean accumulators: 'loss' and the first output's loss, model.metrics order).
+# object graph (shard 0, 18,317 B).  The pointer sizes also pin the NUMBER of shard-1 entries: the
+# index of the 2-shard save (5,657 B) is 156 B larger than the same model's 1-shard save
+# (ml_files/recommender, 5,501 B), = 2 B of shard_id per shard-1 entry minus the 6-B offset field
+# of the object graph written last in the 1-shard file -> 81 entries = 72 weight / m / v tensors +
+# 9 scalars, i.e. iter (8 B) + 8 float32 = 40 B: the 4 optimizer hypers and 4 metric floats.
+# WHICH metric accumulators those 4 floats are is an inference (unpinned: TF is absent): two
+# Mean metrics, taken here as 'loss' and the first output's loss.
 OPT_HYPERS = ('learning_rate', 'beta_1', 'beta_2', 'decay')
 METRICS = ('loss', 'output_1_loss')
 
@@ -146,19 +151,53 @@ def _entry_proto(dtype, shape, shard, offset, size, crc):
 
 
 # ---------------------------------------------------------------------------- SSTable
-def _block(entries):
-    """LevelDB block, restart at every entry (no prefix sharing): valid for any reader."""
+# TF's table builder (tensorflow/core/lib/io/table_builder.cc, the LevelDB format): keys
+# prefix-compressed against the previous key, a restart point every RESTART_INTERVAL entries
+# (table::Options default 16; the index block restarts at every entry), blocks of ~BLOCK_SIZE bytes
+# (default 256 KB), each followed by a 1-byte compression type (0: none) and a masked crc32c.
+RESTART_INTERVAL = 16
+BLOCK_SIZE = 262144
+
+
+def _block(entries, interval=RESTART_INTERVAL):
     out = bytearray()
     restarts = []
-    for k, v in entries:
-        restarts.append(len(out))
-        out += _varint(0) + _varint(len(k)) + _varint(len(v)) + k + v
+    last = b''
+    for i, (k, v) in enumerate(entries):
+        shared = 0
+        if i % interval == 0:
+            restarts.append(len(out))
+        else:
+            n = min(len(last), len(k))
+            while shared < n and last[shared] == k[shared]:
+                shared += 1
+        out += _varint(shared) + _varint(len(k) - shared) + _varint(len(v)) + k[shared:] + v
+        last = k
     if not restarts:
         restarts = [0]
     for r in restarts:
         out += struct.pack('<I', r)
     out += struct.pack('<I', len(restarts))
     return bytes(out)
+
+
+def _short_successor(k):
+    """BytewiseComparator::FindShortSuccessor: the shortest key >= k (first non-0xff byte + 1)."""
+    for i, c in enumerate(k):
+        if c != 0xFF:
+            return k[:i] + bytes([c + 1])
+    return k
+
+
+def _short_separator(a, b):
+    """BytewiseComparator::FindShortestSeparator: a short key in [a, b)."""
+    n = min(len(a), len(b))
+    i = 0
+    while i < n and a[i] == b[i]:
+        i += 1
+    if i < n and a[i] < 0xFF and a[i] + 1 < b[i]:
+        return a[:i] + bytes([a[i] + 1])
+    return a
 
 
 def _write_table(path, entries):
@@ -172,10 +211,19 @@ def _write_table(path, entries):
         f.extend(struct.pack('<I', _mask(crc32c(data + b'\x00'))))
         return off, len(data)
 
-    d_off, d_len = put_block(_block(entries))
+    # data blocks of ~BLOCK_SIZE raw bytes; the index names each by a separator key
+    index, blk, size = [], [], 0
+    for j, (k, v) in enumerate(entries):
+        blk.append((k, v))
+        size += len(k) + len(v) + 8
+        if size >= BLOCK_SIZE and j + 1 < len(entries):
+            off, n = put_block(_block(blk))
+            index.append((_short_separator(k, entries[j + 1][0]), _varint(off) + _varint(n)))
+            blk, size = [], 0
+    off, n = put_block(_block(blk))
+    index.append((_short_successor(blk[-1][0]) if blk else b'', _varint(off) + _varint(n)))
     m_off, m_len = put_block(_block([]))
-    last = entries[-1][0] if entries else b''
-    i_off, i_len = put_block(_block([(last, _varint(d_off) + _varint(d_len))]))
+    i_off, i_len = put_block(_block(index, interval=1))
     footer = _varint(m_off) + _varint(m_len) + _varint(i_off) + _varint(i_len)
     footer += b'\x00' * (40 - len(footer)) + struct.pack('<Q', MAGIC)
     f.extend(footer)
@@ -221,16 +269,23 @@ def _read_table(path):
 
 # ---------------------------------------------------------------------------- bundle
 def _string_scalar_bytes(b):
-    """A scalar DT_STRING tensor in a bundle data file (TF tensor_bundle's string layout): varint64
-    element length, the masked crc32c of the length bytes (uint32 LE), then the bytes."""
-    n = _varint(len(b))
-    return n + struct.pack('<I', _mask(crc32c(n))) + b
+    """A scalar DT_STRING tensor in a bundle data file (TF tensor_bundle.cc WriteStringTensor):
+    the varint64 element length, the masked crc32c of the lengths taken as uint32 LE (uint64 above
+    2^32 - 1), then the bytes.  Returns (raw bytes, entry crc): the entry's crc32c runs over the
+    uint32 lengths, the 4 masked-checksum bytes and the string bytes (not over the varints)."""
+    n = len(b)
+    lens = struct.pack('<I', n) if n <= 0xFFFFFFFF else struct.pack('<Q', n)
+    c = crc32c(lens)
+    ck = struct.pack('<I', _mask(c))
+    return _varint(n) + ck + b, crc32c(b, crc32c(ck, c))
 
 
 def write_bundle(prefix, tensors, shard_of=None):
-    """tensors: dict key -> numpy array (float32 / int64) or bytes (a scalar DT_STRING).  Writes
-    <prefix>.index + <prefix>.data-0000K-of-0000N; shard_of(key) -> shard id (default: one shard).
-    TF's multi-device saver writes one shard per device (the object graph on the CPU shard, the
+    """tensors: dict key -> numpy array (float32 / int64) or bytes (a scalar DT_STRING), in the
+    order the data files receive them (TF writes the saveables in object-graph order, the object
+    graph string last; the index is sorted by key).  Writes <prefix>.index +
+    <prefix>.data-0000K-of-0000N; shard_of(key) -> shard id (default: one shard).  TF's
+    multi-device saver writes one shard per device (the object graph on the CPU shard, the
     variables on the GPU shard), which the reference's 2-shard checkpoints show."""
     os.makedirs(os.path.dirname(prefix), exist_ok=True)
     shard_of = shard_of or (lambda key: 0)
@@ -239,18 +294,20 @@ def write_bundle(prefix, tensors, shard_of=None):
     files = [open(f'{prefix}.data-{s:05d}-of-{nshards:05d}', 'wb') for s in range(nshards)]
     offs = [0] * nshards
     try:
-        for key in sorted(tensors):
+        for key in tensors:
             sh = shard_of(key)
             val = tensors[key]
             if isinstance(val, (bytes, bytearray)):
-                dt, shape, raw = DT_STRING, (), _string_scalar_bytes(bytes(val))
+                dt, shape = DT_STRING, ()
+                raw, crc = _string_scalar_bytes(bytes(val))
             else:
                 a = np.array(val, order="C", copy=True)   # keeps 0-d scalars 0-d
                 dt = DT_FLOAT if a.dtype == np.float32 else DT_INT64
                 a = a.astype(_NP[dt], copy=False)
                 shape, raw = a.shape, a.tobytes()
+                crc = crc32c(raw)
             files[sh].write(raw)
-            entries.append((key.encode(), _entry_proto(dt, shape, sh, offs[sh], len(raw), _mask(crc32c(raw)))))
+            entries.append((key.encode(), _entry_proto(dt, shape, sh, offs[sh], len(raw), _mask(crc))))
             offs[sh] += len(raw)
     finally:
         for fh in files:
@@ -275,17 +332,22 @@ def read_bundle(prefix, verify=True):
         shape = [(_parse(dim).get(1, [0])[0]) for dim in _parse(e[2][0]).get(2, [])] if 2 in e else []
         shard, off, size = e.get(3, [0])[0], e.get(4, [0])[0], e.get(5, [0])[0]
         raw = np.asarray(shards[shard][off:off + size])
-        if verify and 6 in e and _unmask(e[6][0]) != crc32c(raw):
-            raise ValueError(f'crc mismatch for {k!r}')
-        if dt == DT_STRING:
+        if dt == DT_STRING:   # TF's string layout (tensor_bundle.cc ReadStringTensor)
             if shape:
                 raise ValueError(f'{k!r}: only scalar strings are supported')
             b = raw.tobytes()
             n, i = _read_varint(b, 0)
-            if verify and _unmask(struct.unpack_from('<I', b, i)[0]) != crc32c(b[:i]):
+            lens = struct.pack('<I', n) if n <= 0xFFFFFFFF else struct.pack('<Q', n)
+            c = crc32c(lens)
+            if verify and _unmask(struct.unpack_from('<I', b, i)[0]) != c:
                 raise ValueError(f'length crc mismatch for {k!r}')
-            out[k.decode()] = b[i + 4:i + 4 + n]
+            val = b[i + 4:i + 4 + n]
+            if verify and 6 in e and _unmask(e[6][0]) != crc32c(val, crc32c(b[i:i + 4], c)):
+                raise ValueError(f'crc mismatch for {k!r}')
+            out[k.decode()] = val
             continue
+        if verify and 6 in e and _unmask(e[6][0]) != crc32c(raw):
+            raise ValueError(f'crc mismatch for {k!r}')
         out[k.decode()] = raw.view(_NP[dt]).reshape(shape).copy()
     return out
 
@@ -337,7 +399,8 @@ def object_graph(keys, metrics=METRICS):
                 if path + VAR_SUFFIX in keys:
                     nodes.append({'children': [], 'attrs': [], 'slots': []})
                     sv = len(nodes) - 1
-                    var(sv, path, f'Adam/cc__recommender/{n}/{slot}')
+                    sub, layer, w = n.split('/')
+                    var(sv, path, f'Adam/cc__recommender/{sub}/{_LAYER_NAMES[sub + "/" + layer]}/{w}/{slot}')
                     nodes[opt]['slots'].append((vid, slot, sv))
     if any(k.startswith('keras_api/metrics/') for k in keys):
         api = new(0, 'keras_api')
@@ -382,20 +445,26 @@ def save_model(dest, V, d, params, m=None, v=None, step=0, lr=1e-3, beta1=0.9, b
     object graph in shard 0 and every variable in shard 1, as the reference's GPU-trained
     checkpoints are laid out (ml_files/cc_rec_1000_regularization/variables/)."""
     os.makedirs(os.path.join(dest, 'variables'), exist_ok=True)
+    # data-file order = TF's saveable order (the object graph's breadth-first node order,
+    # util.py / graph_view.py): depth 2 the optimizer's own variables (iter, then the hypers in
+    # sorted-name creation order), depth 3 the Dense kernels / biases, depth 4 the metrics'
+    # accumulators, then the slot variables (all m, then all v: OptimizerV2 slot-name order), and
+    # the object-graph string last
     t = {}
-    for n in NAMES:
-        t[n + VAR_SUFFIX] = np.asarray(params[n], np.float32)
-        if m is not None:
-            t[n + '/.OPTIMIZER_SLOT/optimizer/m' + VAR_SUFFIX] = np.asarray(m[n], np.float32)
-            t[n + '/.OPTIMIZER_SLOT/optimizer/v' + VAR_SUFFIX] = np.asarray(v[n], np.float32)
     if m is not None:
         t['optimizer/iter' + VAR_SUFFIX] = np.array(step, np.int64)
-        for h, val in zip(OPT_HYPERS, (lr, beta1, beta2, 0.0)):
+        for h, val in sorted(zip(OPT_HYPERS, (lr, beta1, beta2, 0.0))):
             t[f'optimizer/{h}' + VAR_SUFFIX] = np.array(val, np.float32)
+    for n in NAMES:
+        t[n + VAR_SUFFIX] = np.asarray(params[n], np.float32)
+    if m is not None:
         for i, name in enumerate(METRICS):
             tot, cnt = (metrics or {}).get(name, (0.0, 0.0))
             t[f'keras_api/metrics/{i}/total' + VAR_SUFFIX] = np.array(tot, np.float32)
             t[f'keras_api/metrics/{i}/count' + VAR_SUFFIX] = np.array(cnt, np.float32)
+        for s, src in (('m', m), ('v', v)):
+            for n in NAMES:
+                t[n + f'/.OPTIMIZER_SLOT/optimizer/{s}' + VAR_SUFFIX] = np.asarray(src[n], np.float32)
     t[OBJECT_GRAPH_KEY] = object_graph(t.keys())
     write_bundle(os.path.join(dest, 'variables', 'variables'), t,
                  shard_of=(lambda k: 0 if k == OBJECT_GRAPH_KEY else 1) if shards == 2 else None)

@@ -17,6 +17,11 @@
 
 #include "common.hpp"
 
+// build knob (A/B builds: CCREC_EXTRA_FLAGS=-DCCREC_DX_WIDE_MIN=..., a tagged library; no run-time switch)
+#ifndef CCREC_DX_WIDE_MIN
+#define CCREC_DX_WIDE_MIN 4096
+#endif
+
 namespace {
 
 constexpr int XBM = 128, XBN = 128, XBK = 64, XST = 4, XNT = 256;
@@ -257,10 +262,7 @@ extern "C" int cc_gemm_dx_splitk(const void *A, int32_t lda, const void *B, int3
   p.tiles_m = M / XBM;
   p.a_bytes = (uint32_t)((int64_t)M * lda * 2);
   p.b_bytes = (uint32_t)((int64_t)N * ldb * 2);
-  static const int wide_min = [] {  // A/B switch (dev): smallest M for the 128 x 256 tiles (0: never)
-    const char *e = getenv("CCREC_DX_WIDE_MIN");
-    return e ? atoi(e) : 4096;
-  }();
+  constexpr int wide_min = CCREC_DX_WIDE_MIN;  // build knob: smallest M for the 128 x 256 tiles (0: never)
   if (wide_min > 0 && M >= wide_min && N % WBN == 0) {  // tall M (full-mode regulariser)
     static bool attr = [] {
       return hipFuncSetAttribute((const void *)dx_wide_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, WLDS) ==

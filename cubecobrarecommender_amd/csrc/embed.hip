@@ -17,6 +17,24 @@
 #include "common.hpp"
 #include "xt.hpp"
 
+// build knobs (A/B builds: CCREC_EXTRA_FLAGS=-D..., a tagged library; the library reads no
+// environment): the gather / scatter variants below default to the measured-fastest ones
+#ifndef CCREC_GATHER2
+#define CCREC_GATHER2 48
+#endif
+#ifndef CCREC_GATHER_XCDW
+#define CCREC_GATHER_XCDW 44
+#endif
+#ifndef CCREC_GATHER_XCD
+#define CCREC_GATHER_XCD 44
+#endif
+#ifndef CCREC_GATHER_U
+#define CCREC_GATHER_U 8
+#endif
+#ifndef CCREC_SCATTER_U
+#define CCREC_SCATTER_U 8
+#endif
+
 // dev-only timing hook (tools/micro/eg_probe.hip defines it); compiled out of the library
 #ifndef EG_PROBE
 #define EG_PROBE(k)
@@ -1257,14 +1275,8 @@ extern "C" int cc_embed_gather_fwd_xt(int32_t dtype, const void *table, const fl
   CC_REQUIRE(!state || bpe >= 1, "cc_embed_gather_fwd_warm: batches_per_epoch");
   CC_REQUIRE(!xt_bits || (x_bits && xt_rows >= 1 && xt_rows <= R),
              "cc_embed_gather_fwd_xt: xt_bits needs x_bits and 1 <= xt_rows <= R");
-  static const int g2 = [] {  // A/B switch (dev): 16-B lanes, two rows per load; waves x loads
-    const char *e = getenv("CCREC_GATHER2");
-    return e ? atoi(e) : 48;
-  }();
-  static const int gw = [] {  // A/B switch (dev): XCD column-sliced gather at d = 512 / 1024 (0 = gather_kernel)
-    const char *e = getenv("CCREC_GATHER_XCDW");
-    return e ? atoi(e) : 44;
-  }();
+  constexpr int g2 = CCREC_GATHER2;    // build knob: 16-B lanes, two rows per load; waves x loads
+  constexpr int gw = CCREC_GATHER_XCDW;  // build knob: XCD column-sliced gather at d = 512 / 1024 (0 = gather_kernel)
   const bool xcdw = dtype == CC_BF16 && (d == 512 || d == 1024) && gw > 0 && R > 0 && R <= 4096;
   if (state && !(dtype == CC_BF16 && d == 256 && g2 > 0) && !xcdw) {  // other kernels: a separate launch
     if (int rc = cc_state_advance(state, bpe, stream)) return rc;
@@ -1278,10 +1290,7 @@ extern "C" int cc_embed_gather_fwd_xt(int32_t dtype, const void *table, const fl
   const int nxt = xt_bits ? (int)cdiv((V + 31) / 32, XT_TJ) : 0;  // xt transpose blocks
   const int epl = d / 64;
   hipStream_t s = as_stream(stream);
-  static const int gx = [] {  // A/B switch (dev): XCD column-sliced gather (0 = gather2); waves x loads
-    const char *e = getenv("CCREC_GATHER_XCD");
-    return e ? atoi(e) : 44;
-  }();
+  constexpr int gx = CCREC_GATHER_XCD;  // build knob: XCD column-sliced gather (0 = gather2); waves x loads
   // (tall R — the full-mode regulariser's |V| one-card identity rows — stays on gather2: a block
   // per 64-column slice of a one-card row is mostly overhead; measured 48 -> 121 us at R = 22,528)
   if (dtype == CC_BF16 && d == 256 && g2 > 0 && gx > 0 && !xt_bits && R <= 4096) {
@@ -1291,7 +1300,7 @@ extern "C" int cc_embed_gather_fwd_xt(int32_t dtype, const void *table, const fl
                                              (const bf16_t *)table, bias, R, x_cnt, x_idx, x_cap, (bf16_t *)out, \
                                              warm, warm_bytes, state, bpe); else
     GX(4, 4) GX(4, 8) GX(2, 4) GX(2, 8) GX(8, 4) GX(8, 2)
-      return cc::fail(CC_ERR_UNSUPPORTED, "CCREC_GATHER_XCD: unknown variant");
+      return cc::fail(CC_ERR_UNSUPPORTED, "CCREC_GATHER_XCD: unknown variant (build knob)");
 #undef GX
     CC_LAUNCH_CHECK("gather_xcd_kernel");
     return CC_OK;
@@ -1324,10 +1333,8 @@ extern "C" int cc_embed_gather_fwd_xt(int32_t dtype, const void *table, const fl
     hipLaunchKernelGGL(xt_transpose_kernel, dim3((unsigned)nxt), dim3(256), 0, s, x_bits, V, xt_bits, xt_rows);
     CC_LAUNCH_CHECK("xt_transpose_kernel");
   }
-  static const int gu = [] {  // A/B switch: row loads in flight per lane (bf16, d = 256)
-    const char *e = getenv("CCREC_GATHER_U");
-    return e ? atoi(e) : 8;  // measured at cfg 2: 8 -> 328.5 us/step, 16 -> 337, 32 -> 341
-  }();
+  constexpr int gu = CCREC_GATHER_U;  // build knob: row loads in flight per lane (bf16, d = 256);
+  //                                     measured at cfg 2: 8 -> 328.5 us/step, 16 -> 337, 32 -> 341
   if (dtype == CC_BF16 && epl == 4 && (gu == 16 || gu == 32)) {
     if (gu == 16)
       hipLaunchKernelGGL((gather_kernel<bf16_t, 4, 16>), grid, block, 0, s, (const bf16_t *)table,
@@ -1368,10 +1375,8 @@ extern "C" int cc_embed_scatter_bwd(const float *dpre, int32_t V, int32_t d, int
   CC_REQUIRE(d % 64 == 0 && d >= 64 && d <= 1024, "cc_embed_scatter_bwd: d must be 64..1024, %64");
   const dim3 grid((unsigned)(bias_grad ? V + 1 : V)), block(64 * SGW);
   hipStream_t s = as_stream(stream);
-  static const int su = [] {  // A/B switch: dPre row loads in flight per lane (d = 256)
-    const char *e = getenv("CCREC_SCATTER_U");
-    return e ? atoi(e) : 8;  // measured at cfg 2: 8 -> 45.5 us, 16 -> 54.8
-  }();
+  constexpr int su = CCREC_SCATTER_U;  // build knob: dPre row loads in flight per lane (d = 256);
+  //                                      measured at cfg 2: 8 -> 45.5 us, 16 -> 54.8
   if (d == 256 && su == 16) {
     hipLaunchKernelGGL((scatter_bwd_kernel<4, 16>), grid, block, 0, s, dpre, V, d, R, xt_bits, grad, bias_grad);
     CC_LAUNCH_CHECK("scatter_bwd_kernel");

@@ -13,6 +13,14 @@
 
 #include "common.hpp"
 
+// build knobs (A/B builds: CCREC_EXTRA_FLAGS=-D..., a tagged library; the library reads no environment)
+#ifndef CCREC_NT_BM
+#define CCREC_NT_BM 0
+#endif
+#ifndef CCREC_GEMM_NT
+#define CCREC_GEMM_NT 1
+#endif
+
 namespace {
 
 constexpr int BM = 64, BN = 64, NT = 256;
@@ -768,10 +776,7 @@ int launch_nt_bm(const cc_gemm_args *g, const GemmParams &p, hipStream_t s) {
 // slower on the decoder shapes, tools/micro/gemm_bench.py); CCREC_NT_BM=256/512 selects them.
 template <int EPI>
 int launch_nt(const cc_gemm_args *g, const GemmParams &p, hipStream_t s) {
-  static const int forced = [] {  // A/B switch for benchmarking tile heights
-    const char *e = getenv("CCREC_NT_BM");
-    return e ? atoi(e) : 0;
-  }();
+  constexpr int forced = CCREC_NT_BM;  // build knob for benchmarking tile heights (0: 128)
   int bm = 128;  // measured fastest for the decoder shapes (K = 256 / 512 / split V)
   if (forced == 128 || forced == 256 || forced == 512) bm = forced;
   if (bm == 512) return launch_nt_bm<EPI, 512>(g, p, s);
@@ -968,19 +973,14 @@ static int gemm_params(const cc_gemm_args *g, GemmParams &p) {
 
 // bf16 with both operands K-contiguous and 16-B aligned rows: the 128x128 NT kernel
 static bool nt_path(const cc_gemm_args *g, const GemmParams &p) {
-  static const bool nt_enabled = [] {
-    const char *e = getenv("CCREC_GEMM_NT");  // A/B switch for benchmarking the generic kernel
-    return !(e && e[0] == '0');
-  }();
+  constexpr bool nt_enabled = CCREC_GEMM_NT;  // build knob for benchmarking the generic kernel
   return nt_enabled && g->dtype == CC_BF16 && !g->ta && g->tb && p.vec_a && p.vec_b &&
          g->epilogue != CC_EPI_MASK;
 }
 
 // MX-FP8 STORE / split-K / BCE products go to the 256 x 256 LDS-DMA kernel (mx8gemm.hip; bit-identical
-// results).  CCREC_MX8_GEMM=128 (dev A/B switch, read per call) keeps them on the 128 x 128 kernel.
+// results); cc_gemm_tile128 keeps them on the 128 x 128 kernel (the reference of the bit-identity tests).
 static bool mx8_wide_ok(const cc_gemm_args *g) {
-  const char *e = getenv("CCREC_MX8_GEMM");
-  if (e && atoi(e) == 128) return false;
   const bool bce_ok = g->epilogue == CC_EPI_BCE && g->C && (int64_t)g->M * g->ldc * 2 < 0x100000000ll &&
                       (!g->Ct || ((uintptr_t)g->Ct % 8 == 0 && g->ldct % 4 == 0 && g->M % 4 == 0 &&
                                   (int64_t)g->N * g->ldct * 2 < 0x80000000ll));
@@ -990,12 +990,12 @@ static bool mx8_wide_ok(const cc_gemm_args *g) {
          (g->epilogue == CC_EPI_SPLITK || g->ldc >= g->N);
 }
 
-extern "C" int cc_gemm(const cc_gemm_args *g, void *stream) {
+static int gemm_dispatch(const cc_gemm_args *g, void *stream, bool wide) {
   GemmParams p;
   if (int rc = gemm_params(g, p)) return rc;
   if (g->M == 0 || g->N == 0) return CC_OK;
   hipStream_t s = as_stream(stream);
-  if (mx8_wide_ok(g)) return cc_gemm_mx8_wide(g, nullptr, stream);
+  if (wide && mx8_wide_ok(g)) return cc_gemm_mx8_wide(g, nullptr, stream);
   if (g->dtype == CC_MX8) {
     switch (g->epilogue) {
       case CC_EPI_STORE: return launch_nt_mx8<CC_EPI_STORE>(g, p, s);
@@ -1019,6 +1019,10 @@ extern "C" int cc_gemm(const cc_gemm_args *g, void *stream) {
   cc_gemm_grid(g->M, g->N, &tiles);
   return cc_reduce_loss(g->loss_partials, tiles, g->loss_scale, g->loss_out, stream);
 }
+
+extern "C" int cc_gemm(const cc_gemm_args *g, void *stream) { return gemm_dispatch(g, stream, true); }
+
+extern "C" int cc_gemm_tile128(const cc_gemm_args *g, void *stream) { return gemm_dispatch(g, stream, false); }
 
 extern "C" int cc_gemm_pair(const cc_gemm_args *g0, const cc_gemm_args *g1, void *stream) {
   GemmParams p0, p1;

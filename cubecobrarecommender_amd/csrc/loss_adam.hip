@@ -422,7 +422,7 @@ extern "C" int cc_dec_softmax_kl_fused(int32_t dtype, const float *Z2, int32_t B
   const bool aligned = (V % 4 == 0) && ((uintptr_t)Z2 % 16 == 0) && ((uintptr_t)y_reg % 16 == 0) &&
                        ((uintptr_t)dZ % 16 == 0);
   const int nv = (int)cdiv(V, 4 * NTR);
-  if (aligned && nv <= 8 && getenv("CCREC_KL_ROWS") == nullptr) {  // register-resident rows
+  if (aligned && nv <= 8) {  // register-resident rows
     const hipStream_t s = as_stream(stream);
 #define KL_ROWS(NVV)                                                                            \
   if (nv <= NVV) {                                                                              \

@@ -382,6 +382,16 @@ extern "C" int cc_adam_noise(float *p, float *m, float *v, const float *g, uint1
   return CC_OK;
 }
 
+extern "C" int cc_noise_next(const cc_noise_args *a, int64_t batches_per_epoch, void *stream) {
+  CC_REQUIRE(batches_per_epoch >= 1, "cc_noise_next: batches_per_epoch");
+  size_t lds = 0;
+  if (int rc = noise_check(a, lds)) return rc;
+  hipLaunchKernelGGL(adam_noise_kernel<false>, dim3((unsigned)a->B), dim3(NT), lds, as_stream(stream),
+                     cc_adam::Args{}, *a, 0, batches_per_epoch, cc_adam::Pack{}, cc_adam::Args{}, 0);
+  CC_LAUNCH_CHECK("adam_noise_kernel (F only)");
+  return CC_OK;
+}
+
 extern "C" int cc_adam_noise_pack2(float *p, float *m, float *v, const float *g, uint16_t *shadow,
                                    int64_t lo0, int64_t n0, int64_t lo1, int64_t n1, float lr, float beta1,
                                    float beta2, float eps, const cc_noise_args *next, int64_t batches_per_epoch,

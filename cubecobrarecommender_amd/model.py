@@ -13,6 +13,7 @@ fit runs the device-resident training step (trainer.py) with TF Adam semantics. 
 fallback: every compute call goes through libccrec_hip.so.
 """
 import time
+import warnings
 
 import numpy as np
 import torch
@@ -106,6 +107,14 @@ class CC_Recommender:
             raise ValueError(f'loss must be {list(_LOSSES)} (train.py:85)')
         if float(loss_weights[0]) != 1.0:
             raise ValueError('loss_weights[0] must be 1.0 (train.py:86)')
+        # metrics=['accuracy'] (train.py:87) only reports per-epoch accuracies in Keras' progress
+        # bar; it does not enter the loss, the gradients or the update.  It is accepted for the call
+        # surface and NOT computed (the fused output-layer kernels never materialise the logits)
+        for mname in (metrics or ()):
+            if mname != 'accuracy':
+                raise ValueError(f'metric {mname!r}: only the reference\'s metrics=[\'accuracy\'] is accepted')
+            warnings.warn("compile(metrics=['accuracy']): accepted, not computed (the reference only "
+                          "logs it; training is unaffected)", stacklevel=2)
         self.reg = float(loss_weights[1])
         self.lr = float(learning_rate)
 

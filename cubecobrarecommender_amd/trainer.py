@@ -10,7 +10,6 @@ torch is used only to own device memory and the stream; every computation is a H
 """
 from dataclasses import dataclass
 
-import os
 
 import numpy as np
 import torch
@@ -49,7 +48,13 @@ class TrainConfig:
     fuse_wo_adam8: bool = False    # fp8 + fuse_w1_adam: TF Adam on the output layers in the MX-FP8 dW
     #                                epilogue (cc_gemm_mx8_pair_adam).  Bit-identical, but measured
     #                                slower at config 5 (1000 vs 961-978 us/step): opt-in
+    dx_splits: int = 0             # decoder dX K-splits (0: measured default, 32 bf16 / 16 fp8)
+    dx_splits_reg: int = 0         # ... of the full-mode regulariser branch (0: 4)
+    mx8_bce_q: bool = True         # fp8: the BCE product writes dZ's MX-FP8 images (else quantiser launches)
     graph_steps: int = 8           # one process: consecutive steady-state steps per hipGraph replay (step_many)
+    force_dp: bool = False         # one process driving the data-parallel step (a 1-rank process group:
+    #                                zero.py's collectives on device tensors; tests and the per-rank DP profile)
+    dp_graph: bool = True          # data parallel over RCCL: the whole step (collectives included) as one hipGraph
     reg_mode: str = 'sampled'      # 'sampled': B reg rows per step drawn ∝ neg_sampler (generator.py:47-51);
     #                                'full': all |V| identity rows every step, KL(M~, D2(E(I))) as the
     #                                reference README states the objective (README.md:27)
@@ -191,9 +196,10 @@ class Trainer:
         self.dev = torch.device(device)
         # data-parallel: gradient buckets aligned to world*64 so every rank owns an equal shard
         self.std_layout = Layout(V, d)
+        self.dp = cfg.world > 1 or cfg.force_dp    # zero.py's sharded step (buckets, collectives)
         # (with a bf16 shadow the biases are grouped so zero.py all-gathers the kernels' bf16 shadow)
         self.layout = (Layout(V, d, align=cfg.world * 64, group_biases=cfg.dtype in ('bf16', 'fp8'))
-                       if cfg.world > 1 else self.std_layout)
+                       if self.dp else self.std_layout)
         self.use_reg = cfg.reg > 0
         if self.use_reg and data.y_reg is None:
             raise ValueError('reg > 0 needs the M~ matrix on the device')
@@ -201,7 +207,7 @@ class Trainer:
             raise ValueError(f"reg_mode {cfg.reg_mode!r}: 'sampled' or 'full'")
         W = cfg.world
         self.full_reg = self.use_reg and cfg.reg_mode == 'full'
-        self.owner = self.use_reg and not self.full_reg and cfg.reg_shard and W > 1
+        self.owner = self.use_reg and not self.full_reg and cfg.reg_shard and self.dp
         ralign = 128 if cfg.dtype == 'fp8' else 32
         # regulariser rows of this rank: rows [B, B + Breg) of every row-indexed buffer.
         #   sampled: B draws per step (slot b of cube b), dz weight reg/B;
@@ -274,13 +280,13 @@ class Trainer:
         self.gH2 = torch.zeros(R, 256, **T)
         self.gPre1 = torch.zeros(R, d, **f32)
         self.Z2 = None             # materialised fp32 D2 logits (the unfused regulariser path only)
-        self.splits = max(1, min(int(os.environ.get('CCREC_DX_SPLITS', '16' if cfg.dtype == 'fp8' else '32')), V // 512))   # decoder dX: K = V (fp8: 256 x 256 tiles, 16 splits measured best)
+        self.splits = max(1, min(cfg.dx_splits or (16 if cfg.dtype == 'fp8' else 32), V // 512))   # decoder dX: K = V (fp8: 256 x 256 tiles, 16 splits measured best)
         # the regulariser branch's dX: M = Breg rows; with thousands of rows (full mode) the output
         # tiles alone fill the chip — no split-K
         # full-mode regulariser (~|V| rows): 2 K-splits (tools/micro/dx_full_micro.py at |V| = 22,000:
         # 1 split 643 us, 2 or 4 splits 515 us, the library GEMM 391-399 us)
         # (the 128 x 256-tile kernel of dxgemm.hip for tall M: 4 splits)
-        self.splits_reg = self.splits if self.Breg <= 1024 else int(os.environ.get('CCREC_DX_SPLITS_REG', '4'))
+        self.splits_reg = self.splits if self.Breg <= 1024 else (cfg.dx_splits_reg or 4)
         self.tsplits = max(1, min(8, B // 128))             # tower dW: K = rows (B or 2B)
         self.split_buf = torch.zeros(max(self.splits * B * d, self.splits_reg * self.Breg * d,
                                          2 * self.tsplits * max(d, 256) * 256), **f32)
@@ -368,9 +374,8 @@ class Trainer:
             # quantiser launches less per step)
             self.d3q_in_tower = self.mx8 and d > 256 and self.wpack is not None and R % 32 == 0
             # the BCE product makes dZ's MX-FP8 images and the bias gradient in its epilogue
-            # (cc_gemm_mx8_bce_q: B % 32 == 0, B <= 512); CCREC_MX8_BCE_Q=0 keeps the quantiser launches
-            self.mx8_bce_q = (self.mx8 and B % 32 == 0 and B <= 512
-                              and os.environ.get('CCREC_MX8_BCE_Q', '1') != '0')
+            # (cc_gemm_mx8_bce_q: B % 32 == 0, B <= 512); mx8_bce_q=False keeps the quantiser launches
+            self.mx8_bce_q = self.mx8 and B % 32 == 0 and B <= 512 and cfg.mx8_bce_q
             if self.d3q_in_tower:
                 t = self.targs
                 t.d3q, t.d3qs = self.D3q.data_ptr(), self.D3qs.data_ptr()
@@ -396,7 +401,10 @@ class Trainer:
         # F for the next step in the Adam launch (cc_adam_noise): Adam is HBM-bound, F latency-
         # bound; F then leaves the forward's critical path.  noise_ready: the batch buffers
         # already hold the batch the next forward_backward consumes.
-        self.prefetch = cfg.prefetch_noise and cfg.world == 1
+        self.prefetch = cfg.prefetch_noise and not self.dp
+        # data parallel: F of the next step is its own launch (cc_noise_next) beside the exchange of
+        # the last gradient buckets (zero.py after_b), off the next forward's critical path
+        self.prefetch_dp = cfg.prefetch_noise and self.dp
         # one process: F (in the Adam launch) writes its x rows as bitmasks and the next E1 gather
         # launch bit-transposes them into the W1-gradient bitmask (cc_embed_gather_fwd_xt) — F's
         # scattered xt atomics queued behind the Adam streams (measured: the Adam + F launch
@@ -435,7 +443,7 @@ class Trainer:
         if (cfg.wo_adam_in_tower and self.fuse_w1 and self.fused_out and (not self.use_reg or self.fused_reg)
                 and self.targs is not None and self.dtype == L.CC_BF16 and cfg.d <= 256):
             frac = cfg.wo_tower_frac if cfg.wo_tower_frac >= 0 else (0.45 if self.use_reg else 0.6)
-            frac = min(max(float(os.environ.get('CCREC_WO_TOWER_FRAC', frac)), 0.0), 1.0)  # (dev A/B knob)
+            frac = min(max(float(frac), 0.0), 1.0)
             lay = self.layout
             spans = [(lay.offset('decoder/reconstruct/kernel'), lay.main_total)]
             if self.use_reg:
@@ -476,6 +484,8 @@ class Trainer:
         self.batches_per_epoch = max(1, data.C // (B * cfg.world))   # generator.py:36 (__len__)
         self.graphs = None
         self.g_multi, self.multi_n, self.multi_acc = None, 0, None   # capture(): step_many's graph
+        self.g_dp = self.g_dp_nocomm = None   # capture(): the whole data-parallel step (RCCL inside)
+        self.sharded = None
         self.pending_rest = False    # one process: step k's counters/transposes run at the head
         #                              of step k+1's forward graph (one graph launch less per step)
         self.side = torch.cuda.Stream(device=self.dev)   # dW / slab reduce / losses / transposes
@@ -1084,20 +1094,42 @@ class Trainer:
             L.call('cc_to_bf16', L.ptr(self.params[lo:]), L.ptr(self.shadow[lo:]), hi - lo,
                    L.stream_ptr(stream))
 
-    def step_dp(self, timing=False):
-        """One data-parallel step: bucketed reduce-scatter overlapped with the towers' backward,
-        Adam on this rank's shards, all-gathered parameters (zero.py)."""
-        if getattr(self, 'sharded', None) is None:
+    def noise_next(self, stream=None):
+        """F of the NEXT step (cc_noise_next: the state advanced as apply_rest will) — data
+        parallel: issued after this step's backward, beside the exchange of the last buckets."""
+        t = self._tick('cc_noise_fwd')
+        L.call('cc_noise_next', L.C.byref(self._noise_args()), self.batches_per_epoch, L.stream_ptr(stream))
+        t()
+
+    def _sharded(self):
+        if self.sharded is None:
             from .zero import ShardedStep
             self.sharded = ShardedStep(self)
-        g = self.graphs
-        self.sharded.step(
+        return self.sharded
+
+    def _dp_call(self, g=None, timing=False):
+        """The sharded step (zero.py) over graph replays of its parts (g) or eager launches."""
+        self._sharded().step(
             phase_a=g[0].replay if g else self.forward_backward_a,
             phase_b=g[1].replay if g else self.forward_backward_b,
             rest=g[2].replay if g else self.apply_rest,
             adam_fn=lambda lo, n, gs: self.adam_range(lo, n, gs),
             refresh_fn=lambda lo, hi: self.refresh_range(lo, hi),
-            timing=timing)
+            timing=timing,
+            after_b=self.noise_next if self.prefetch_dp else None)
+        self.noise_ready = self.prefetch_dp
+
+    def step_dp(self, timing=False, no_comm=False):
+        """One data-parallel step: bucketed reduce-scatter overlapped with the towers' backward,
+        Adam on this rank's shards, all-gathered parameters (zero.py); the next step's F beside the
+        last buckets' exchange.  Steady state over RCCL: one replay of the whole-step graph.
+        no_comm: replay the timing reference captured without the collectives (bench.py)."""
+        g = self.graphs
+        gd = self.g_dp_nocomm if no_comm else self.g_dp
+        if gd is not None and not timing and (self.noise_ready or not self.prefetch_dp):
+            gd.replay()
+            return
+        self._dp_call(g, timing)
 
     def flush(self, stream=None, defer=False):
         """Run the previous step's deferred counters/transposes (before reading state or the
@@ -1141,7 +1173,7 @@ class Trainer:
                 and (self.noise_ready or not self.prefetch))
 
     def step(self, stream=None):
-        if self.cfg.world > 1:
+        if self.dp:
             self.step_dp()
             return
         if self._steady():
@@ -1197,8 +1229,9 @@ class Trainer:
             for b, c in zip((self.params, self.m, self.v, self.shadow), cs):
                 b[lo:hi].copy_(c)
         g_fb, g_adam, g_rest = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        if self.cfg.world > 1:   # (forward_backward_a | forward_backward_b | counters): the
-            with torch.cuda.graph(g_fb):       # sharded optimizer's collectives run between them
+        if self.dp:   # (forward_backward_a | forward_backward_b | counters): the
+            self.noise_ready = False           # sharded optimizer's collectives run between them
+            with torch.cuda.graph(g_fb):       # (F inside: the first step after a capture)
                 self.forward_backward_a()
             with torch.cuda.graph(g_adam):
                 self.forward_backward_b()
@@ -1211,7 +1244,10 @@ class Trainer:
         g_main = g_all = None
         with torch.cuda.graph(g_rest):
             self.apply_rest()
-        if self.cfg.world == 1:   # rest of step k + forward/backward of step k+1 (+ its Adam)
+        self.g_dp = self.g_dp_nocomm = None
+        if self.dp and self.cfg.dp_graph and self._sharded().nccl:
+            self._capture_dp()
+        if not self.dp:   # rest of step k + forward/backward of step k+1 (+ its Adam)
             g_main, g_all = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             self.noise_ready = self.prefetch   # F already drawn by step k's Adam launch
             with torch.cuda.graph(g_main):
@@ -1223,7 +1259,7 @@ class Trainer:
                 self.forward_backward()
                 self.apply_adam()
         self.g_multi, self.multi_n, self.multi_acc = None, 0, None
-        if self.cfg.world == 1 and self.cfg.graph_steps > 1:   # step_many: graph_steps whole steps
+        if not self.dp and self.cfg.graph_steps > 1:   # step_many: graph_steps whole steps
             self.g_multi = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_multi):
                 for _ in range(self.cfg.graph_steps):
@@ -1241,6 +1277,29 @@ class Trainer:
         self.noise_ready = False
         self.graphs = (g_fb, g_adam, g_rest, g_main, g_all)
         self.timing = timing
+
+    def _capture_dp(self):
+        """The whole data-parallel step as ONE graph: forward_backward_a, the first bucket's
+        reduce-scatter / sharded Adam / all-gather on the comm stream beside forward_backward_b, the
+        next step's F beside the later buckets' exchange, then the counters and transposed operands.
+        RCCL collectives are captured on the comm stream (it forks from and joins the capturing
+        stream); the communicator's lazy set-up runs first (ShardedStep.warm).  Assumes F already
+        drawn (noise_ready) — the first step after a capture runs the parts instead.  Also captures
+        the same step without the collectives (bench.py's exposed-exchange reference)."""
+        sh = self._sharded()
+        sh.warm()
+        graphs = []
+        for no_comm in (False, True):
+            g = torch.cuda.CUDAGraph()
+            self.noise_ready = self.prefetch_dp
+            sh.no_comm = no_comm
+            try:
+                with torch.cuda.graph(g):
+                    self._dp_call(None, False)
+            finally:
+                sh.no_comm = False
+            graphs.append(g)
+        self.g_dp, self.g_dp_nocomm = graphs
 
     # ------------------------------------------------------------------ inspection (tests)
     def losses(self, loss_dev=None):

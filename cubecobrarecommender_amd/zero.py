@@ -56,44 +56,74 @@ class ShardedStep:
             bb['gfull'] = torch.zeros(bb['hi'] - bb['lo'], device=trainer.params.device, dtype=torch.float32)
         self.comm = torch.cuda.Stream(device=trainer.params.device) if trainer.params.is_cuda else None
         self.adam_events = []          # (e0, e1, n) around each shard's Adam when timing
+        self.comm_events = {}          # (bucket, collective) -> [(e0, e1)] when timing
+        self.timing = False
+        self.no_comm = False           # capture a timing reference of the step without the exchange
 
     def bucket(self, name):
         return next(b for b in self.buckets if b['name'] == name)
 
     # ------------------------------------------------------------------ collectives
+    def _ev(self, b, what):
+        """Record a timing event on the comm stream (timing mode); returns a closer."""
+        if not self.timing:
+            return lambda: None
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+
+        def close():
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.comm_events.setdefault((b['name'], what), []).append((e0, e1))
+        return close
+
     def reduce_scatter(self, b, grads):
         src = grads[b['lo']:b['hi']]
-        if self.stage:
+        t = self._ev(b, 'reduce_scatter')
+        if self.no_comm:      # (timing reference: the same step without the exchange)
+            off = b['s0'] - b['lo']
+            b['gshard'].copy_(src[off:off + b['chunk']])
+        elif self.stage:
             out = torch.empty(b['chunk'], dtype=torch.float32)
             dist.reduce_scatter_tensor(out, src.cpu(), op=dist.ReduceOp.SUM, group=self.group)
             b['gshard'].copy_(out)
         else:
             dist.reduce_scatter_tensor(b['gshard'], src, op=dist.ReduceOp.SUM, group=self.group)
-        b['gshard'].mul_(1.0 / self.world)
+        if self.world > 1:
+            b['gshard'].mul_(1.0 / self.world)
+        t()
 
     def all_gather(self, b, buf):
         full = buf[b['lo']:b['hi']]
         off = b['s0'] - b['lo']
+        if self.no_comm:
+            return
+        t = self._ev(b, 'all_gather')
         if self.stage:
             host = full.cpu()
             dist.all_gather_into_tensor(host, host[off:off + b['chunk']], group=self.group)
             full.copy_(host)
         else:           # in place: my shard already sits at rank * chunk inside the output
             dist.all_gather_into_tensor(full, full[off:off + b['chunk']], group=self.group)
+        t()
 
     def all_reduce_mean(self, b, grads):
         """The biases bucket: the full mean gradient on every rank (b['gfull'])."""
         src = grads[b['lo']:b['hi']]
+        t = self._ev(b, 'all_reduce')
         if self.stage:
             host = src.cpu()
             dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group)
             b['gfull'].copy_(host)
         else:
             b['gfull'].copy_(src)
-            dist.all_reduce(b['gfull'], op=dist.ReduceOp.SUM, group=self.group)
-        b['gfull'].mul_(1.0 / self.world)
+            if not self.no_comm:
+                dist.all_reduce(b['gfull'], op=dist.ReduceOp.SUM, group=self.group)
+        if self.world > 1:
+            b['gfull'].mul_(1.0 / self.world)
+        t()
 
-    def update(self, b, adam_fn, timing=False):
+    def update(self, b, adam_fn):
         """Reduce-scatter bucket b, Adam on this rank's shard, all-gather the parameters (the
         bf16 shadow in shadow_gather mode); the biases bucket: all-reduce, Adam on every rank."""
         full = self.shadow_gather and b['name'] == 'biases'
@@ -101,19 +131,36 @@ class ShardedStep:
             self.all_reduce_mean(b, self.tr.grads)
         else:
             self.reduce_scatter(b, self.tr.grads)
-        if timing:
+        if self.timing:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         if full:
             adam_fn(b['lo'], b['hi'] - b['lo'], b['gfull'])
         else:
             adam_fn(b['s0'], b['chunk'], b['gshard'])
-        if timing:
+        if self.timing:
             e1.record()
             self.adam_events.append((e0, e1, b['hi'] - b['lo'] if full else b['chunk']))
         if full:
             return
         self.all_gather(b, self.tr.shadow if self.shadow_gather else self.tr.params)
+
+    def warm(self):
+        """Run every collective of the step once on scratch tensors of the buckets' sizes, so the
+        communicator's lazy set-up happens before a step is captured into a graph."""
+        if self.stage:
+            return
+        for b in self.buckets:
+            src = torch.zeros(b['hi'] - b['lo'], device=self.tr.params.device, dtype=torch.float32)
+            if self.shadow_gather and b['name'] == 'biases':
+                dist.all_reduce(src, op=dist.ReduceOp.SUM, group=self.group)
+                continue
+            out = torch.empty(b['chunk'], device=src.device, dtype=torch.float32)
+            dist.reduce_scatter_tensor(out, src, op=dist.ReduceOp.SUM, group=self.group)
+            g = src.to(torch.bfloat16) if self.shadow_gather else src
+            off = b['s0'] - b['lo']
+            dist.all_gather_into_tensor(g, g[off:off + b['chunk']], group=self.group)
+        torch.cuda.synchronize()
 
     def gather_state(self):
         """Make m and v (and, in shadow_gather mode, the fp32 kernel parameters) complete on every
@@ -127,18 +174,26 @@ class ShardedStep:
                 self.all_gather(b, self.tr.params)
 
     # ------------------------------------------------------------------ one training step
-    def step(self, phase_a, phase_b, rest, adam_fn, refresh_fn, timing=False):
+    def step(self, phase_a, phase_b, rest, adam_fn, refresh_fn, timing=False, after_b=None):
         """phase_a / phase_b: the two halves of forward_backward (graph replays or eager);
-        rest: counters + transposed operand copies; adam_fn(lo, n, g) / refresh_fn(lo, hi)."""
+        rest: counters + transposed operand copies; adam_fn(lo, n, g) / refresh_fn(lo, hi);
+        after_b: main-stream work that needs phase_b's consumers of the batch buffers done but not
+        the exchange (the next step's F), issued beside the later buckets' exchange.  The whole
+        call can be captured into one graph (RCCL: the collectives run on the comm stream, which
+        forks from and joins the capturing stream)."""
+        self.timing = timing
         first, later = self.buckets[0], self.buckets[1:]
         refresh = (lambda lo, hi: None) if self.shadow_gather else refresh_fn   # (shadow gathered)
         if self.comm is None:          # CPU (gloo tests): no streams
             phase_a()
             phase_b()
+            if after_b is not None:
+                after_b()
             for b in self.buckets:
                 self.update(b, adam_fn)
                 refresh(b['lo'], b['hi'])
             rest()
+            self.timing = False
             return
         main = torch.cuda.current_stream()
         phase_a()
@@ -146,15 +201,18 @@ class ShardedStep:
         ev.record(main)
         with torch.cuda.stream(self.comm):
             self.comm.wait_event(ev)
-            self.update(first, adam_fn, timing)
+            self.update(first, adam_fn)
             refresh(first['lo'], first['hi'])
         phase_b()
         ev2 = torch.cuda.Event()
         ev2.record(main)
+        if after_b is not None:
+            after_b()
         with torch.cuda.stream(self.comm):
             self.comm.wait_event(ev2)
             for b in later:
-                self.update(b, adam_fn, timing)
+                self.update(b, adam_fn)
                 refresh(b['lo'], b['hi'])
         main.wait_stream(self.comm)
         rest()
+        self.timing = False

@@ -125,6 +125,11 @@ int cc_reg_rows(const cc_noise_args *a, void *stream);
 int cc_adam_noise(float *p, float *m, float *v, const float *g, uint16_t *shadow, int64_t n,
                   float lr, float beta1, float beta2, float eps, const cc_noise_args *next,
                   int64_t batches_per_epoch, void *stream);
+/* cc_noise_fwd for the step AFTER a->state (the F half of cc_adam_noise alone): the data-parallel
+ * step issues it beside its last gradient buckets' exchange (zero.py), so the next step's forward
+ * starts without F.  Replaces the next __getitem__ (generator.py:38-103) the Keras fit loop makes
+ * (train.py:99-102).  The state itself is not modified. */
+int cc_noise_next(const cc_noise_args *a, int64_t batches_per_epoch, void *stream);
 /* cc_adam_noise that also writes the updated bf16 values of the tower kernels into their
  * fragment-packed images (cc_tower_args.wpf / wpb order), so no cc_tower_transpose launch is
  * needed before the next forward (the step counters are then advanced by
@@ -267,6 +272,10 @@ typedef struct cc_gemm_args {
   const uint8_t *a_scale, *b_scale;  /* CC_MX8: E8M0 scales [M][lda/32] of A, [N][ldb/32] of B */
 } cc_gemm_args;
 int cc_gemm(const cc_gemm_args *g, void *stream);
+/* cc_gemm with the MX-FP8 products kept on the 128 x 128 register-staged kernel instead of the
+ * 256 x 256 LDS-DMA one (identical MFMA order per output): the reference side of the bit-identity
+ * tests (tests/test_gpu_mx8.py); other dtypes behave as cc_gemm. */
+int cc_gemm_tile128(const cc_gemm_args *g, void *stream);
 /* CC_MX8 runs v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 x e4m3, block scales applied in the MFMA):
  * NT only (ta = 0, tb = 1), K % 128 == 0, lda % 128 == ldb % 128 == 0, epilogues STORE / BCE /
  * SPLITK without colsum; outputs as for CC_BF16 (C is bf16, Cf fp32). */

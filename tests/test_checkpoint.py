@@ -42,7 +42,7 @@ def test_model_save_load(tmp_path):
     size = os.path.getsize(os.path.join(dest, 'variables', 'variables.data-00000-of-00001'))
     nparam = sum(int(np.prod(P[n].shape)) for n in NAMES)
     og = ck.read_bundle(os.path.join(dest, 'variables', 'variables'))[ck.OBJECT_GRAPH_KEY]
-    assert size == 3 * 4 * nparam + 40 + len(ck._string_scalar_bytes(og))
+    assert size == 3 * 4 * nparam + 40 + len(ck._string_scalar_bytes(og)[0])
     _, _, flat = ck.flat_params(dest)
     assert np.array_equal(Layout(V, d).unpack(flat)['decoder/reconstruct/kernel'], P['decoder/reconstruct/kernel'])
 
@@ -88,6 +88,52 @@ def test_two_shard_layout_matches_reference_pointer_sizes(tmp_path):
     vdir = os.path.join(dest, 'variables')
     assert os.path.getsize(os.path.join(vdir, 'variables.data-00001-of-00002')) == 391661320
     og = ck.read_bundle(os.path.join(vdir, 'variables'), verify=False)[ck.OBJECT_GRAPH_KEY]
-    assert os.path.getsize(os.path.join(vdir, 'variables.data-00000-of-00002')) == len(ck._string_scalar_bytes(og))
+    assert os.path.getsize(os.path.join(vdir, 'variables.data-00000-of-00002')) == len(ck._string_scalar_bytes(og)[0])
     V2, d2, P2, M2, _, step = ck.load_variables(dest)
     assert (V2, d2, step) == (V, d, 100)
+
+
+def _crc32c_py(data, crc=0):
+    """Bitwise CRC-32C (Castagnoli, reflected 0x82F63B78): independent of the library's table."""
+    crc ^= 0xFFFFFFFF
+    for b in data:
+        crc ^= b
+        for _ in range(8):
+            crc = (crc >> 1) ^ (0x82F63B78 if crc & 1 else 0)
+    return crc ^ 0xFFFFFFFF
+
+
+def test_string_entry_bytes_follow_tf_write_string_tensor():
+    """A scalar DT_STRING entry laid out by the spec of TF's WriteStringTensor (tensor_bundle.cc):
+    varint64 length, masked crc32c of the length as uint32 LE, the bytes; the entry crc32c runs over
+    the uint32 length, the 4 checksum bytes and the string (not over the varint)."""
+    import struct
+    assert _crc32c_py(b'123456789') == 0xE3069283          # the CRC-32C check value
+    s = b'x' * 200                                          # a 2-byte varint length
+    raw, crc = ck._string_scalar_bytes(s)
+    c = _crc32c_py(struct.pack('<I', 200))
+    ck_bytes = struct.pack('<I', ck._mask(c))
+    assert raw == bytes([0xC8, 0x01]) + ck_bytes + s
+    assert crc == _crc32c_py(s, _crc32c_py(ck_bytes, c))
+
+
+def test_index_layout_against_reference_pointer_sizes(tmp_path):
+    """variables.index as TF's table builder writes it (prefix-compressed keys, restart interval
+    16, shortest-successor index key; tensors in object-graph order, the object graph last).  The
+    reference's pointers pin the 2-shard minus 1-shard index size of one model: 5,657 B
+    (cc_rec_1000_regularization/variables/variables.index:3) - 5,501 B (recommender/variables/
+    variables.index:3) = 156 B (81 shard-1 entries x 2 B of shard_id - the object graph's 6-B offset
+    field).  The absolute size depends on the exact key set (TF absent: which metrics' accumulators
+    hold the 4 scalar floats is unpinned), so it is checked within 5 % of 5,657."""
+    V, d = 20884, 512
+    lay = Layout(V, d)
+    P = {n: np.zeros(lay.entries[n][1], np.float32) for n in NAMES}
+    sizes = {}
+    for shards in (1, 2):
+        dest = str(tmp_path / f's{shards}')
+        ck.save_model(dest, V, d, P, P, P, step=100, shards=shards)
+        sizes[shards] = os.path.getsize(os.path.join(dest, 'variables', 'variables.index'))
+        t = ck.read_bundle(os.path.join(dest, 'variables', 'variables'))   # crc-verified
+        assert len(t) == 82
+    assert sizes[2] - sizes[1] == 5657 - 5501
+    assert abs(sizes[2] - 5657) < 0.05 * 5657, sizes

@@ -283,3 +283,200 @@ def test_bench_dp_configuration_matches_single_process_and_oracle():
     assert errs['loss/bce'] < 2e-6 and errs['loss/kl'] < 2e-6, errs
     bad = {k: v for k, v in errs.items() if not k.startswith('loss/') and not v < 2.4e-3}
     assert not bad, bad
+
+
+# ---------------------------------------------------------------------------------------------
+# The RCCL branch (VERDICT r3 "run the code the 8-GPU run will execute"): one process drives the
+# data-parallel step through a 1-rank RCCL ("nccl") process group — zero.py's reduce_scatter_tensor,
+# in-place all_gather_into_tensor and the biases' all_reduce on device tensors, the next step's F
+# beside the exchange (cc_noise_next), and the whole step (collectives included) captured as ONE
+# hipGraph.  With one rank the shard is the whole bucket, so the step must equal the one-process
+# step (different kernels for F's bit transpose, Adam and the tower images; same arithmetic).
+RCCL_SHAPES = {'bench': dict(V=2500, d=256, B=128, C=1024, dtype='bf16'),
+               'c5': dict(V=2500, d=1024, B=128, C=1024, dtype='fp8')}
+
+
+def _rccl_trainer(shape, reg, force_dp, reg_shard):
+    from cubecobrarecommender_amd.layout import Layout
+    from cubecobrarecommender_amd.trainer import DeviceDataset, TrainConfig, Trainer
+    from oracle import model_ref
+    S = RCCL_SHAPES[shape]
+    lists, Mt, ns = problem(5, S['C'], S['V'], (20, 40, 80))
+    P = model_ref.init_params(S['V'], S['d'], seed=3, bias_std=0.01)
+    cfg = TrainConfig(V=S['V'], d=S['d'], batch_size=S['B'], reg=reg, dtype=S['dtype'], seed=3,
+                      force_dp=force_dp, reg_shard=reg_shard)
+    data = DeviceDataset(lists, S['V'], y_mtx=Mt.astype(np.float32) if reg else None, neg_sampler=ns)
+    tr = Trainer(cfg, data, params_flat=Layout(S['V'], S['d']).pack(P))
+    tr.set_epoch_permutations(np.random.default_rng(4).permutation(S['C'])[None, :])
+    return tr
+
+
+def _rccl_run(tr, eager=2, graphed=3):
+    losses = []
+    for _ in range(eager):
+        tr.step()
+        torch.cuda.synchronize()
+        losses.append(tr.losses()['loss'])
+    tr.capture()
+    for _ in range(graphed):
+        tr.step()
+        torch.cuda.synchronize()
+        losses.append(tr.losses()['loss'])
+    tr.flush()
+    torch.cuda.synchronize()
+    return losses
+
+
+def _rccl_worker(shape, reg, reg_shard, q):
+    os.environ.update(HSA_ENABLE_IPC_MODE_LEGACY='0')
+    try:
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        # the process group first: RCCL's communicator before any other GPU work of this process
+        dist.init_process_group('nccl', store=dist.HashStore(), rank=0, world_size=1,
+                                device_id=torch.device('cuda', 0))
+        tr = _rccl_trainer(shape, reg, True, reg_shard)
+        assert tr.dp and tr.prefetch_dp and tr.owner == (reg_shard and reg > 0)
+        dl = _rccl_run(tr)
+        assert tr._sharded().nccl and tr.g_dp is not None, 'whole-step DP graph not captured'
+        tr.sharded.gather_state()
+        tr.check_status()
+        one = _rccl_trainer(shape, reg, False, False)
+        assert not one.dp
+        ol = _rccl_run(one)
+        one.check_status()
+        q.put((tr.standard(tr.params), tr.standard(tr.m), tr.standard(tr.v), dl,
+               one.standard(one.params), one.standard(one.m), one.standard(one.v), ol))
+        dist.destroy_process_group()
+    except Exception as e:   # surface the error in the parent
+        import traceback
+        q.put((repr(e) + traceback.format_exc(),) + (None,) * 7)
+        raise
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('shape,reg,reg_shard', [('bench', 0.0, False), ('bench', 0.1, True), ('c5', 0.1, True)])
+def test_rccl_one_rank_dp_step_matches_one_process(shape, reg, reg_shard):
+    """The data-parallel step over RCCL (1 rank), eager then as the captured whole-step graph, ==
+    the one-process step on the same draws: parameters, Adam moments and losses over 5 steps."""
+    from tests.gpu_helpers import record_errors
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(shape, reg, reg_shard, q))
+    p.start()
+    res = q.get(timeout=280)
+    p.join(60)
+    assert res[1] is not None, res[0]
+    assert p.exitcode == 0
+    dp_p, dp_m, dp_v, dl, p1, m1, v1, ol = res
+    errs = {'params': rel_err(dp_p, p1), 'm': rel_err(dp_m, m1), 'v': rel_err(dp_v, v1),
+            'loss': max(abs(a - b) / b for a, b in zip(dl, ol)),
+            'exact_params': float(np.array_equal(dp_p, p1))}
+    record_errors(f'rccl1_vs_one_{shape}_{reg}', 5, errs)
+    assert errs['loss'] < 1e-6 and errs['params'] < 1e-6 and errs['m'] < 1e-5 and errs['v'] < 1e-5, errs
+
+
+# ---------------------------------------------------------------------------------------------
+# configs[4]'s step in its data-parallel form (VERDICT r3 Missing 2): d = 1024, MX-FP8 decoder
+# output / regulariser GEMMs, reg 0.1, two ranks (gloo, sharing the GPU) == one process of 2B,
+# with M~ replicated (the MX scale blocks along the batch rows fall on the same 32 rows) and
+# row-sharded (owner computes: the regulariser branch's dW blocks group other rows, so only the
+# fp8 rounding of that product differs); the one process's first step against the MX-FP8 oracle.
+FP8_DP = dict(V=3000, d=1024, B=128, C=1024, reg=0.1, steps=3)
+
+
+def _fp8_trainer(rank, world, batch, reg_shard):
+    from cubecobrarecommender_amd.layout import Layout
+    from cubecobrarecommender_amd.trainer import DeviceDataset, TrainConfig, Trainer
+    from oracle import model_ref
+    S = FP8_DP
+    lists, Mt, ns = problem(9, S['C'], S['V'], (40, 80, 160))
+    P = model_ref.init_params(S['V'], S['d'], seed=6, bias_std=0.01)
+    cfg = TrainConfig(V=S['V'], d=S['d'], batch_size=batch, reg=S['reg'], dtype='fp8', seed=11,
+                      rank=rank, world=world, reg_shard=reg_shard)
+    data = DeviceDataset(lists, S['V'], y_mtx=Mt.astype(np.float32), neg_sampler=ns)
+    tr = Trainer(cfg, data, params_flat=Layout(S['V'], S['d']).pack(P))
+    perm = np.random.default_rng(8).permutation(S['C']).astype(np.int32)
+    tr.set_epoch_permutations(perm[None, :])
+    return tr, (lists, Mt, ns, P, perm)
+
+
+def _fp8_worker(rank, port, reg_shard, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(W), LOCAL_RANK='0', HSA_ENABLE_IPC_MODE_LEGACY='0')
+    try:
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dist.init_process_group('gloo', rank=rank, world_size=W)
+        tr, _ = _fp8_trainer(rank, W, FP8_DP['B'], reg_shard)
+        assert tr.mx8 and tr.dp and tr.owner == reg_shard
+        tr.capture()
+        losses = []
+        for _ in range(FP8_DP['steps']):
+            tr.step()
+            torch.cuda.synchronize()
+            losses.append(tr.losses())
+        tr.sharded.gather_state()
+        tr.check_status()
+        q.put((rank, tr.standard(tr.params), tr.standard(tr.m), losses))
+        dist.destroy_process_group()
+    except Exception as e:   # surface the error in the parent
+        q.put((rank, repr(e), None, None))
+        raise
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('reg_shard', [False, True])
+def test_fp8_dp_step_matches_single_process_and_oracle(reg_shard):
+    from oracle import adjacency_ref, model_ref, noise_ref
+    from cubecobrarecommender_amd.layout import Layout
+    from tests.gpu_helpers import record_errors
+    S = FP8_DP
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 29700 + (os.getpid() + 13 * int(reg_shard)) % 97
+    ps = [ctx.Process(target=_fp8_worker, args=(r, port, reg_shard, q)) for r in range(W)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in ps:
+        r, prm, m, losses = q.get(timeout=500)
+        assert m is not None, prm
+        res[r] = (prm, m, losses)
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    single, (lists, Mt, ns, P0, perm) = _fp8_trainer(0, 1, W * S['B'], False)
+    single.capture()
+    want = []
+    for step in range(S['steps']):
+        single.step()
+        torch.cuda.synchronize()
+        want.append(single.losses())
+        if step == 0:
+            g0 = single.layout.unpack(single.standard(single.grads))
+    single.flush()
+    np.testing.assert_array_equal(res[0][0], res[1][0])         # ranks agree exactly
+    ep = rel_err(res[0][0], single.params.cpu().numpy())
+    em = rel_err(res[0][1], single.m.cpu().numpy())
+    el = [abs(np.mean([res[r][2][s]['loss'] for r in range(W)]) - want[s]['loss']) / want[s]['loss']
+          for s in range(S['steps'])]
+    record_errors(f'fp8_dp_vs_single_shard{int(reg_shard)}', S['steps'],
+                  {'params': ep, 'm': em, **{f'loss{s}': v for s, v in enumerate(el)}})
+    if reg_shard:   # the regulariser dW's MX blocks group different rows: fp8 rounding apart
+        assert ep < 2e-2 and em < 1e-1 and max(el) < 1e-3, (ep, em, el)
+    else:
+        assert ep < 1e-3 and em < 2e-2 and max(el) < 1e-5, (ep, em, el)
+    # the one process's first step against the MX-FP8-emulating oracle
+    B2 = W * S['B']
+    cdf = noise_ref.cdf_of(ns)
+    oxs, oys, oreg, _ = noise_ref.philox_noise_batch([lists[c] for c in perm[:B2]], cdf, ns, 11, 0)
+    lo, go = model_ref.train_forward_backward(P0, oxs, oys, S['V'], S['d'], reg=S['reg'], reg_idx=oreg,
+                                              y_reg=Mt[oreg], mode='mx8')
+    errs = {'loss/bce': abs(want[0]['bce'] - lo['bce']) / lo['bce'],
+            'loss/kl': abs(want[0]['kl'] - lo['kl']) / lo['kl']}
+    errs.update({k: rel_err(g0[k], go[k]) for k in go})
+    record_errors('fp8_dp_single_vs_oracle', 0, errs)
+    assert errs['loss/bce'] < 1e-5 and errs['loss/kl'] < 1e-5, errs
+    bad = {k: v for k, v in errs.items() if not k.startswith('loss/') and not v < 5e-3}
+    assert not bad, bad

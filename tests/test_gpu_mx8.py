@@ -183,7 +183,7 @@ def test_mx8_bce_epilogue():
                                                (37, 129, 256, 'store', 1), (1024, 2100, 512, 'store', 1),
                                                (512, 1024, 2944, 'splitk', 8), (512, 256, 1024, 'splitk', 32),
                                                (512, 1000, 1024, 'bce', 1), (300, 700, 256, 'bce', 1)])
-def test_mx8_wide_bit_identical_to_128_kernel(M, N, K, epi, splits, monkeypatch):
+def test_mx8_wide_bit_identical_to_128_kernel(M, N, K, epi, splits):
     """The 256 x 256 LDS-DMA kernel (mx8gemm.hip, cc_gemm's MX8 STORE / SPLITK / BCE path) runs the
     same MFMA sequence per output as the 128 x 128 kernel: bitwise equal products, ragged edges
     included, empty K splits written as zeros; BCE outputs to the rounding of its epilogue math."""
@@ -193,15 +193,14 @@ def test_mx8_wide_bit_identical_to_128_kernel(M, N, K, epi, splits, monkeypatch)
     bias = torch.from_numpy(rng.standard_normal(N).astype(np.float32)).cuda()
     bits = torch.from_numpy(rng.integers(0, 2**31, (M, (N + 31) // 32), dtype=np.int64).astype(np.int32)).cuda()
     outs = []
-    for kern in ('128', '256'):
-        monkeypatch.setenv('CCREC_MX8_GEMM', kern)
+    for kern in ('cc_gemm_tile128', 'cc_gemm'):
         if epi == 'store':
             Cf = torch.full((M, N), 7.0, device='cuda')
             Cb = torch.zeros(M, N, device='cuda', dtype=torch.bfloat16)
             g = L.GemmArgs(dtype=L.CC_MX8, ta=0, tb=1, epilogue=L.CC_EPI_STORE, M=M, N=N, K=K, lda=K, ldb=K,
                            ldc=N, splits=1, A=qa.data_ptr(), B=qb.data_ptr(), bias=bias.data_ptr(),
                            Cf=Cf.data_ptr(), C=Cb.data_ptr(), a_scale=sa.data_ptr(), b_scale=sb.data_ptr())
-            L.call('cc_gemm', L.C.byref(g), L.stream_ptr())
+            L.call(kern, L.C.byref(g), L.stream_ptr())
             outs.append((Cf, Cb))
         elif epi == 'bce':
             dZ = torch.zeros(M, N, device='cuda', dtype=torch.bfloat16)
@@ -214,7 +213,7 @@ def test_mx8_wide_bit_identical_to_128_kernel(M, N, K, epi, splits, monkeypatch)
                            y_bits=bits.data_ptr(), scale=1.0 / (M * N), loss_partials=part.data_ptr(),
                            Ct=dZt.data_ptr(), ldct=M + 4, loss_out=loss.data_ptr(), loss_scale=1.0 / (M * N),
                            ticket=ticket.data_ptr(), a_scale=sa.data_ptr(), b_scale=sb.data_ptr())
-            L.call('cc_gemm', L.C.byref(g), L.stream_ptr())
+            L.call(kern, L.C.byref(g), L.stream_ptr())
             torch.cuda.synchronize()
             outs.append((dZ, dZt[:, :M], ticket))
             losses = locals().get('losses', []) + [loss.item()]
@@ -223,7 +222,7 @@ def test_mx8_wide_bit_identical_to_128_kernel(M, N, K, epi, splits, monkeypatch)
             g = L.GemmArgs(dtype=L.CC_MX8, ta=0, tb=1, epilogue=L.CC_EPI_SPLITK, M=M, N=N, K=K, lda=K, ldb=K,
                            ldc=N, splits=splits, A=qa.data_ptr(), B=qb.data_ptr(), Cf=P.data_ptr(),
                            a_scale=sa.data_ptr(), b_scale=sb.data_ptr())
-            L.call('cc_gemm', L.C.byref(g), L.stream_ptr())
+            L.call(kern, L.C.byref(g), L.stream_ptr())
             outs.append((P,))
     torch.cuda.synchronize()
     if epi == 'bce':
