@@ -24,7 +24,6 @@
 // reduced in tile order by the last block when loss_out is set).
 #include <cstdlib>
 
-#include "adam.hpp"
 #include "common.hpp"
 #include "mx8.hpp"
 
@@ -65,14 +64,6 @@ struct QP {
   int ldzq, ldztq;
   int M, N, K, lda, ldb, ldc, splits, kchunk, tiles_m, ntiles, epi;
   uint32_t a_bytes, b_bytes, sa_bytes, sb_bytes;
-  // STORE with TF Adam (cc_gemm_mx8_pair_adam): the outputs are the gradient of ap [M][ldc]; the
-  // epilogue updates ap / am / av and the bf16 shadow ash instead of storing them, and the first row
-  // tile's blocks update the bias (bp / bm_ / bv / bsh) from bgrad[N].  t = astate[0] + 1
-  float *ap, *am, *av, *bp, *bm_, *bv;
-  bf16_t *ash, *bsh;
-  const float *bgrad;
-  const int64_t *astate;
-  float lr, b1, b2, eps;
 };
 
 // sigmoid_cross_entropy_with_logits (TF 2.5 Keras BCE on a sigmoid output):
@@ -145,7 +136,7 @@ __device__ __forceinline__ i32x8_t q_frag(const char *S, int row, int c0) {
   return i32x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <bool BCE, bool ADAM = false>
+template <bool BCE>
 __device__ __forceinline__ void q_body(const QP &p, int q, char *smem) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5;
   const int wm = w >> 2, wn = w & 3;
@@ -408,84 +399,6 @@ __device__ __forceinline__ void q_body(const QP &p, int q, char *smem) {
     }
     return;
   }
-  if constexpr (ADAM) {
-    // TF Adam on the finished gradient tile (cc_adam::range's constants and element rule), from LDS
-    // in two passes of 128 columns (the waves' j = 0 accumulators, then j = 1): pass column
-    // lc = 32 wn + c holds tile column 64 wn + 32 j + c.  Each thread then streams float4 groups of
-    // p / m / v (a wave: two rows x four 128-B runs), QAU groups in flight (default cache policy:
-    // non-temporal measured slower here, 166 -> 200 us per launch).
-    constexpr int QAP = 132;  // pitch (floats): 16-B aligned rows
-    // float4 groups in flight per thread: 344 dW tiles on 256 CUs leave a second round on a third
-    // of the chip, whose per-CU streaming rate (bytes in flight / latency) then sets the pace (8 spills
-// at the 256-VGPR cap: the j = 1 accumulators stay live through pass 0)
-#ifndef QAU_N
-#define QAU_N 4
-#endif
-    constexpr int QAU = QAU_N;
-    float *S = reinterpret_cast<float *>(smem);
-    const float tt = (float)(p.astate[0] + 1);
-    const float b1p = powf(p.b1, tt), b2p = powf(p.b2, tt);
-    const float alpha = p.lr * sqrtf(1.f - b2p) / (1.f - b1p);
-    const float omb1 = 1.f - p.b1, omb2 = 1.f - p.b2;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();   // every wave left the K loop: the stage buffers are free
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          S[(wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * QAP + wn * 32 + (lane & 31)] = acc[i][j][r];
-      __syncthreads();
-#pragma unroll 1
-      for (int g0 = 0; g0 < QM * 32; g0 += QAU * QNT) {
-        int64_t off[QAU];
-        bool ok[QAU];
-        int lrow[QAU], lc[QAU];
-        cc_adam::f32x4_t pv[QAU], mv[QAU], vv[QAU];
-#pragma unroll
-        for (int u = 0; u < QAU; ++u) {
-          const int gi = g0 + u * QNT + (int)threadIdx.x;
-          lrow[u] = gi >> 5;
-          lc[u] = (gi & 31) * 4;
-          const int row = bm + lrow[u], col = bn + (lc[u] >> 5) * 64 + j * 32 + (lc[u] & 31);
-          ok[u] = row < p.M && col < p.N;
-          off[u] = ok[u] ? (int64_t)row * p.ldc + col : 0;
-          pv[u] = *reinterpret_cast<const cc_adam::f32x4_t *>(p.ap + off[u]);
-          mv[u] = *reinterpret_cast<const cc_adam::f32x4_t *>(p.am + off[u]);
-          vv[u] = *reinterpret_cast<const cc_adam::f32x4_t *>(p.av + off[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < QAU; ++u) {
-          const float4 gq = *reinterpret_cast<const float4 *>(S + lrow[u] * QAP + lc[u]);
-          const float ge[4] = {gq.x, gq.y, gq.z, gq.w};
-          float pe[4] = {pv[u][0], pv[u][1], pv[u][2], pv[u][3]}, me[4] = {mv[u][0], mv[u][1], mv[u][2], mv[u][3]};
-          float ve[4] = {vv[u][0], vv[u][1], vv[u][2], vv[u][3]};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) cc_adam::elem(pe[e], me[e], ve[e], ge[e], alpha, omb1, omb2, p.eps);
-          if (ok[u]) {
-            *reinterpret_cast<cc_adam::f32x4_t *>(p.ap + off[u]) = cc_adam::f32x4_t{pe[0], pe[1], pe[2], pe[3]};
-            *reinterpret_cast<cc_adam::f32x4_t *>(p.am + off[u]) = cc_adam::f32x4_t{me[0], me[1], me[2], me[3]};
-            *reinterpret_cast<cc_adam::f32x4_t *>(p.av + off[u]) = cc_adam::f32x4_t{ve[0], ve[1], ve[2], ve[3]};
-            *reinterpret_cast<uint2 *>(p.ash + off[u]) =
-                make_uint2((uint32_t)f2bf(pe[0]) | ((uint32_t)f2bf(pe[1]) << 16),
-                           (uint32_t)f2bf(pe[2]) | ((uint32_t)f2bf(pe[3]) << 16));
-          }
-        }
-      }
-      if (j == 0) __syncthreads();   // pass 0's LDS reads done before pass 1 overwrites
-    }
-    if (bm == 0 && (int)threadIdx.x < QN && bn + (int)threadIdx.x < p.N) {  // the bias, once per column
-      const int col = bn + (int)threadIdx.x;
-      float pb = p.bp[col], mb = p.bm_[col], vb = p.bv[col];
-      cc_adam::elem(pb, mb, vb, p.bgrad[col], alpha, omb1, omb2, p.eps);
-      p.bp[col] = pb;
-      p.bm_[col] = mb;
-      p.bv[col] = vb;
-      p.bsh[col] = f2bf(pb);
-    }
-    return;
-  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int col = bn + wn * 64 + j * 32 + (lane & 31);
@@ -512,14 +425,13 @@ __global__ __launch_bounds__(QNT) void mx8_wide_kernel(QP p) {
 
 // two independent problems in one launch (the decoder's dX split-K and dW products): blocks
 // [0, n0) are problem 0's, the rest problem 1's, each dealt to the XCDs in contiguous runs
-template <bool ADAM1 = false>
 __global__ __launch_bounds__(QNT) void mx8_wide_pair_kernel(QP p0, QP p1) {
   extern __shared__ __attribute__((aligned(1024))) char qsmem[];
   const int n0 = p0.ntiles * p0.splits;
   if ((int)blockIdx.x < n0)
     q_body<false>(p0, xcd_run(blockIdx.x, n0), qsmem);
   else
-    q_body<false, ADAM1>(p1, xcd_run(blockIdx.x - n0, p1.ntiles * p1.splits), qsmem);
+    q_body<false>(p1, xcd_run(blockIdx.x - n0, p1.ntiles * p1.splits), qsmem);
 }
 
 int q_params(const cc_gemm_args *g, QP &p) {
@@ -568,11 +480,6 @@ int q_params(const cc_gemm_args *g, QP &p) {
   p.zq = p.zqs = p.ztq = p.ztqs = nullptr;
   p.colsum = nullptr;
   p.ldzq = p.ldztq = 0;
-  p.ap = p.am = p.av = p.bp = p.bm_ = p.bv = nullptr;
-  p.ash = p.bsh = nullptr;
-  p.bgrad = nullptr;
-  p.astate = nullptr;
-  p.lr = p.b1 = p.b2 = p.eps = 0.f;
   p.splits = g->epilogue == CC_EPI_SPLITK ? g->splits : 1;
   p.kchunk = (int)cdiv(cdiv(g->K, p.splits), QKB) * QKB;
   p.tiles_m = (int)cdiv(g->M, QM);
@@ -589,9 +496,7 @@ bool q_attr() {
                                              hipFuncAttributeMaxDynamicSharedMemorySize, QLDS) == hipSuccess &&
                          hipFuncSetAttribute((const void *)mx8_wide_kernel<true>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, QLDS_MAX) == hipSuccess &&
-                         hipFuncSetAttribute((const void *)mx8_wide_pair_kernel<false>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, QLDS) == hipSuccess &&
-                         hipFuncSetAttribute((const void *)mx8_wide_pair_kernel<true>,
+                         hipFuncSetAttribute((const void *)mx8_wide_pair_kernel,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, QLDS) == hipSuccess;
   return ok;
 }
@@ -615,7 +520,7 @@ extern "C" int cc_gemm_mx8_wide(const cc_gemm_args *g0, const cc_gemm_args *g1, 
     CC_LAUNCH_CHECK("mx8_wide_kernel");
     return CC_OK;
   }
-  hipLaunchKernelGGL(mx8_wide_pair_kernel<false>, dim3((unsigned)(p0.ntiles * p0.splits + p1.ntiles * p1.splits)),
+  hipLaunchKernelGGL(mx8_wide_pair_kernel, dim3((unsigned)(p0.ntiles * p0.splits + p1.ntiles * p1.splits)),
                      dim3(QNT), QLDS, s, p0, p1);
   CC_LAUNCH_CHECK("mx8_wide_pair_kernel");
   return CC_OK;
@@ -654,47 +559,3 @@ extern "C" int cc_gemm_mx8_bce_q(const cc_gemm_args *g, uint8_t *zq, int32_t ldz
   return CC_OK;
 }
 
-// Config 5's decoder output-layer backward (model.py:64 Dense(V); train.py:84-85 one Adam step)
-// with TF Adam in the dW product's epilogue — one process: the dW tile (K = the branch's batch rows,
-// no split) and the bias gradient (made earlier by the BCE epilogue / the dZ^T quantiser) are final
-// there, so the fp32 gradient is never written nor read back by the Adam launch.  gx: the dX
-// split-K product; gw: the dW STORE product (M = d, N = V) whose outputs are the gradient of
-// p [M][ldc]; pb / mb / vb / shb: the bias's parameter, moments and shadow, bias_grad[N].
-extern "C" int cc_gemm_mx8_pair_adam(const cc_gemm_args *gx, const cc_gemm_args *gw, float *p, float *m, float *v,
-                                     uint16_t *shadow, float *pb, float *mb, float *vb, uint16_t *shb,
-                                     const float *bias_grad, const int64_t *state, float lr, float beta1,
-                                     float beta2, float eps, void *stream) {
-  CC_REQUIRE(gx && gw && gw->epilogue == CC_EPI_STORE && gx->epilogue == CC_EPI_SPLITK,
-             "cc_gemm_mx8_pair_adam: gx split-K, gw STORE");
-  CC_REQUIRE(p && m && v && shadow && pb && mb && vb && shb && bias_grad && state, "cc_gemm_mx8_pair_adam: null pointer");
-  CC_REQUIRE(!gw->bias && !gw->C && !gw->Cf, "cc_gemm_mx8_pair_adam: gw stores nothing itself (no bias, C, Cf)");
-  CC_REQUIRE(gw->N % 4 == 0 && gw->ldc % 4 == 0 && ((((uintptr_t)p | (uintptr_t)m | (uintptr_t)v) & 15) == 0) &&
-                 ((uintptr_t)shadow & 7) == 0,
-             "cc_gemm_mx8_pair_adam: N, ldc multiples of 4; p / m / v 16-B, shadow 8-B aligned");
-  cc_gemm_args g2 = *gw;
-  g2.Cf = p;  // placeholder for the argument checks; not written
-  QP p0, p1;
-  if (int rc = q_params(gx, p0)) return rc;
-  if (int rc = q_params(&g2, p1)) return rc;
-  p1.Cf = nullptr;
-  p1.ap = p;
-  p1.am = m;
-  p1.av = v;
-  p1.ash = (bf16_t *)shadow;
-  p1.bp = pb;
-  p1.bm_ = mb;
-  p1.bv = vb;
-  p1.bsh = (bf16_t *)shb;
-  p1.bgrad = bias_grad;
-  p1.astate = state;
-  p1.lr = lr;
-  p1.b1 = beta1;
-  p1.b2 = beta2;
-  p1.eps = eps;
-  CC_REQUIRE(q_attr(), "cc_gemm_mx8_pair_adam: dynamic LDS attribute");
-  hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(mx8_wide_pair_kernel<true>, dim3((unsigned)(p0.ntiles * p0.splits + p1.ntiles * p1.splits)),
-                     dim3(QNT), QLDS, s, p0, p1);
-  CC_LAUNCH_CHECK("mx8_wide_pair_kernel<adam>");
-  return CC_OK;
-}

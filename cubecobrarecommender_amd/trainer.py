@@ -45,9 +45,6 @@ class TrainConfig:
     wo_tower_frac: float = -1.0    # ... on this trailing fraction of each; the rest stays in the Adam + F
     #                                launch (< 0: measured per mode — 0.6 BCE only, 0.45 with the
     #                                sampled regulariser; tools/gpu_t8.sh, tools/gpu_t15.sh sweeps)
-    fuse_wo_adam8: bool = False    # fp8 + fuse_w1_adam: TF Adam on the output layers in the MX-FP8 dW
-    #                                epilogue (cc_gemm_mx8_pair_adam).  Bit-identical, but measured
-    #                                slower at config 5 (1000 vs 961-978 us/step): opt-in
     dx_splits: int = 0             # decoder dX K-splits (0: measured default, 32 bf16 / 16 fp8)
     dx_splits_reg: int = 0         # ... of the full-mode regulariser branch (0: 4)
     mx8_bce_q: bool = True         # fp8: the BCE product writes dZ's MX-FP8 images (else quantiser launches)
@@ -456,27 +453,6 @@ class Trainer:
                     rest.append((lo, a))
                     lo = b
                 self.rest_ranges = rest
-        # config 5 (MX-FP8 decoder products, one process; opt-in fuse_wo_adam8): TF Adam on the
-        # output layers (Wo, bo and with the sampled regulariser Wo_reg, bo_reg) in the dW product's
-        # epilogue (cc_gemm_mx8_pair_adam): their fp32 gradients are never stored nor re-read; the
-        # Adam + F launch covers the complement (rest_ranges).  Slower as measured: the 344 dW tiles
-        # on 256 CUs (one 132-KB-LDS block per CU) leave a second round of 88 tiles whose Adam
-        # streams at the per-CU rate, so the pair launch grows 71 -> 166 us, more than the ~230 us
-        # the Adam + F launch sheds
-        self.fuse_wo8 = (self.mx8 and self.fuse_w1 and self.rest_ranges is None and not self.full_reg
-                         and not self.layout.group_biases
-                         and cfg.V % 4 == 0 and cfg.fuse_wo_adam8)
-        self.fused_spans = []
-        if self.fuse_wo8:
-            lay = self.layout
-            wo_lo = lay.offset('decoder/reconstruct/kernel')
-            self.fused_spans = [(wo_lo, lay.main_total)]
-            rest = [(self.w1_off, wo_lo)]
-            if self.use_reg:
-                wr_lo = lay.offset('decoder_for_reg/reconstruct/kernel')
-                self.fused_spans.append((wr_lo, lay.total))
-                rest.append((lay.main_total, wr_lo))
-            self.rest_ranges = rest
         self.wo_range = self.wo_ranges[0] if self.wo_ranges else None   # (tests: is the placement on)
         self._adv_deferred = False   # the previous step's counter advance rides in the E1 gather
         self.noise_ready = False
@@ -496,6 +472,10 @@ class Trainer:
         self.overlap = False
         self.timing = False          # bench.py: HIP events around the main kernels
         self.events = {}
+        # zero.py (one captured data-parallel step): called on the launching stream once the decoder
+        # output layer's gradient is final (hook_out) and once the branch's dX product no longer
+        # reads its bf16 shadow (hook_dx), so that bucket's reduce-scatter starts before dX
+        self.hook_out = self.hook_dx = None
 
     def branch_rows(self):
         """Rows of each decoder branch: B cubes, then Breg regulariser rows."""
@@ -790,6 +770,7 @@ class Trainer:
                    self.pf('decoder/reconstruct/bias'), B, d, V, L.ptr(self.y_bits), L.ptr(self.dZout),
                    self.gp('decoder/reconstruct/kernel'), self.gp('decoder/reconstruct/bias'),
                    L.ptr(self.bce_part), L.ptr(self.loss_dev), 1.0 / (B * V), L.ptr(self.tickets), s)
+            self._fire('hook_out')     # dWo / dbo of the D1 output layer final
         elif self.mx8_bce_q:   # config 5: the BCE epilogue writes dZ's MX-FP8 images + the bias grad
             g = self._gemm(B, V, d, **self._dec_fwd(0, 0), tb=1,
                            epi=L.CC_EPI_BCE, bias=self.pf('decoder/reconstruct/bias'),
@@ -855,6 +836,9 @@ class Trainer:
         # ---- backward through the output layers and decoder towers.  The output layers' dW
         # (side stream) and dX -> towers (this stream) only share read-only inputs.
         for k, (pre, (r0, r1)) in enumerate(branches):
+            if k == 1:                 # branch 0 (D1) done: its dW final, its Wo shadow read
+                self._fire('hook_out')
+                self._fire('hook_dx')
             dz = self.dZout[r0:]
             nr = r1 - r0
             splits = self.splits if k == 0 else self.splits_reg
@@ -882,20 +866,6 @@ class Trainer:
                     L.call('cc_splitk_reduce_warm', self.dtype, L.ptr(self.split_buf), splits, nr, d,
                            L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None,
                            L.ptr(wb) if wb is not None else None, 2 * wb.numel() if wb is not None else 0, s)
-                    continue
-                if self.fuse_wo8:   # dX split-K + dW with TF Adam on Wo, bo in its epilogue
-                    gw = self._gemm(d, V, nr, **self._dec_dw(k, r0), ta=0, tb=1, launch=False)
-                    lay, cfg = self.layout, self.cfg
-                    ko, bo = lay.offset(pre + '/reconstruct/kernel'), lay.offset(pre + '/reconstruct/bias')
-                    t = self._tick('dec_dW')
-                    L.call('cc_gemm_mx8_pair_adam', L.C.byref(gx), L.C.byref(gw), L.ptr(self.params[ko:]),
-                           L.ptr(self.m[ko:]), L.ptr(self.v[ko:]), L.ptr(self.shadow[ko:]), L.ptr(self.params[bo:]),
-                           L.ptr(self.m[bo:]), L.ptr(self.v[bo:]), L.ptr(self.shadow[bo:]),
-                           self.gp(pre + '/reconstruct/bias'), L.ptr(self.state), cfg.lr, cfg.beta1, cfg.beta2,
-                           cfg.eps, s)
-                    t()
-                    L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), splits, nr, d,
-                           L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
                     continue
                 gw = self._gemm(d, V, nr, **self._dec_dw(k, r0), ta=0, tb=1,
                                 Cf=self.gp(pre + '/reconstruct/kernel'),
@@ -927,7 +897,15 @@ class Trainer:
             self._dense_bwd(self.D2, self.gD3, rows, 256, d, pre + '/decoded_3', gIn=self.gD2, mask=self.D2)
             self._dense_bwd(self.D1, self.gD2, rows, 128, 256, pre + '/decoded_2', gIn=self.gD1, mask=self.D1)
             self._dense_bwd(self.Zl, self.gD1, rows, 64, 128, pre + '/decoded_1', gIn=self.gZl, mask=self.Zl)
+        self._fire('hook_out')
+        self._fire('hook_dx')
         self._join()
+
+    def _fire(self, name):
+        f = getattr(self, name)
+        if f is not None:
+            setattr(self, name, None)
+            f()
 
     def _dx(self, gx, r0, nr, splits, pre, s):
         """Decoder dX split-K partials into split_buf: the LDS-DMA pipelined kernel (dxgemm.hip)
@@ -1116,7 +1094,8 @@ class Trainer:
             adam_fn=lambda lo, n, gs: self.adam_range(lo, n, gs),
             refresh_fn=lambda lo, hi: self.refresh_range(lo, hi),
             timing=timing,
-            after_b=self.noise_next if self.prefetch_dp else None)
+            after_b=self.noise_next if self.prefetch_dp else None,
+            hooks=g is None and self._sharded().comm is not None)
         self.noise_ready = self.prefetch_dp
 
     def step_dp(self, timing=False, no_comm=False):
@@ -1218,8 +1197,7 @@ class Trainer:
         s.wait_stream(torch.cuda.current_stream())
         saved = self.state.clone()
         # the fused W1 (and Wo) Adam updates them inside forward_backward: undo the warm-up's update
-        spans = (([(0, self.w1_off)] if self.fuse_w1 else []) + (list(self.wo_ranges) if self.wo_ranges else [])
-                 + list(self.fused_spans))
+        spans = ([(0, self.w1_off)] if self.fuse_w1 else []) + (list(self.wo_ranges) if self.wo_ranges else [])
         saved_spans = [[b[lo:hi].clone() for b in (self.params, self.m, self.v, self.shadow)] for lo, hi in spans]
         with torch.cuda.stream(s):           # warm-up launch outside capture (lazy module loads)
             self.forward_backward()

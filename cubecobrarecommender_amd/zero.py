@@ -123,14 +123,17 @@ class ShardedStep:
             b['gfull'].mul_(1.0 / self.world)
         t()
 
-    def update(self, b, adam_fn):
+    def update(self, b, adam_fn, gate=None):
         """Reduce-scatter bucket b, Adam on this rank's shard, all-gather the parameters (the
-        bf16 shadow in shadow_gather mode); the biases bucket: all-reduce, Adam on every rank."""
+        bf16 shadow in shadow_gather mode); the biases bucket: all-reduce, Adam on every rank.
+        gate: an event the Adam waits for (the step's last reader of the bucket's old shadow)."""
         full = self.shadow_gather and b['name'] == 'biases'
         if full:
             self.all_reduce_mean(b, self.tr.grads)
         else:
             self.reduce_scatter(b, self.tr.grads)
+        if gate is not None:
+            torch.cuda.current_stream().wait_event(gate)
         if self.timing:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -174,13 +177,15 @@ class ShardedStep:
                 self.all_gather(b, self.tr.params)
 
     # ------------------------------------------------------------------ one training step
-    def step(self, phase_a, phase_b, rest, adam_fn, refresh_fn, timing=False, after_b=None):
+    def step(self, phase_a, phase_b, rest, adam_fn, refresh_fn, timing=False, after_b=None, hooks=False):
         """phase_a / phase_b: the two halves of forward_backward (graph replays or eager);
         rest: counters + transposed operand copies; adam_fn(lo, n, g) / refresh_fn(lo, hi);
         after_b: main-stream work that needs phase_b's consumers of the batch buffers done but not
         the exchange (the next step's F), issued beside the later buckets' exchange.  The whole
         call can be captured into one graph (RCCL: the collectives run on the comm stream, which
-        forks from and joins the capturing stream)."""
+        forks from and joins the capturing stream).  hooks (phase_a launched eagerly or captured in
+        the same graph, not a separate graph replay): the first bucket's reduce-scatter starts at
+        the trainer's hook_out and its Adam / all-gather wait for hook_dx."""
         self.timing = timing
         first, later = self.buckets[0], self.buckets[1:]
         refresh = (lambda lo, hi: None) if self.shadow_gather else refresh_fn   # (shadow gathered)
@@ -196,12 +201,19 @@ class ShardedStep:
             self.timing = False
             return
         main = torch.cuda.current_stream()
+        ev, gate = torch.cuda.Event(), None
+        if hooks:   # the first bucket's reduce-scatter as soon as its gradient is final (before dX)
+            gate = torch.cuda.Event()
+            self.tr.hook_out = lambda: ev.record(main)
+            self.tr.hook_dx = lambda: gate.record(main)
         phase_a()
-        ev = torch.cuda.Event()
-        ev.record(main)
+        if hooks:
+            assert self.tr.hook_out is None and self.tr.hook_dx is None, 'forward_backward_a fired no hooks'
+        else:
+            ev.record(main)
         with torch.cuda.stream(self.comm):
             self.comm.wait_event(ev)
-            self.update(first, adam_fn)
+            self.update(first, adam_fn, gate)
             refresh(first['lo'], first['hi'])
         phase_b()
         ev2 = torch.cuda.Event()

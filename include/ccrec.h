@@ -293,15 +293,6 @@ int cc_gemm_mx8_wide(const cc_gemm_args *g0, const cc_gemm_args *g1, void *strea
  * gradient (zeroed here).  g->C / g->Ct (bf16 dZ / dZ^T) optional.  M % 32 == 0, M <= 512. */
 int cc_gemm_mx8_bce_q(const cc_gemm_args *g, uint8_t *zq, int32_t ldzq, uint8_t *zqs, uint8_t *ztq,
                       int32_t ldztq, uint8_t *ztqs, float *colsum, void *stream);
-/* Config 5's decoder output-layer backward (one process) with TF Adam in the dW epilogue: gx = the
- * dX split-K product, gw = the dW STORE product (M = d, N = V; no bias / C / Cf) whose outputs are
- * the gradient of p [M][gw->ldc]; the epilogue applies TF Adam (t = state[0] + 1, cc_adam_dense's
- * element rule) to p, m, v and rewrites the bf16 shadow; the first row tile also updates the bias
- * (pb, mb, vb, shb) from bias_grad[N].  The gradient is never stored.  Replaces the reference's
- * optimizer step on the output layer (/root/reference/src/ml/train.py:99-102, Keras Adam). */
-int cc_gemm_mx8_pair_adam(const cc_gemm_args *gx, const cc_gemm_args *gw, float *p, float *m, float *v,
-                          uint16_t *shadow, float *pb, float *mb, float *vb, uint16_t *shb, const float *bias_grad,
-                          const int64_t *state, float lr, float beta1, float beta2, float eps, void *stream);
 /* workspace bound for cc_gemm's loss partials: ceil(M/64)*ceil(N/64) doubles */
 int cc_gemm_grid(int32_t M, int32_t N, int32_t *tiles);
 

@@ -244,11 +244,9 @@ def test_config5_full_size_matches_mx8_oracle():
     def y_rows(idx):
         return y_mtx[torch.as_tensor(idx, device='cuda').long()].cpu().numpy()
     lay = Layout(V, d)
-    # gradients the fused Adam placements never store (W1 in its gradient kernel, the output layers
-    # in the dW product's epilogue): recovered from the first moment, m1 = 0.9 m0 + 0.1 g
-    fused = (['encoder/encoded_1/kernel'] if tr.fuse_w1 else []) + (
-        [p + '/reconstruct/' + t for p in ('decoder', 'decoder_for_reg') for t in ('kernel', 'bias')]
-        if tr.fuse_wo8 else [])
+    # gradients the fused Adam placement never stores (W1 in its gradient kernel): recovered from the
+    # first moment, m1 = 0.9 m0 + 0.1 g
+    fused = ['encoder/encoded_1/kernel'] if tr.fuse_w1 else []
 
     def moments(name):
         o, shape = tr.layout.offset(name), tr.layout.shape(name)

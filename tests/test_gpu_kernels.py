@@ -472,12 +472,15 @@ def _nt_gemm(M, N, K, A, lda, Bm, ldb, epi, **kw):
 
 
 @pytest.mark.parametrize('B,d,V', [(512, 256, 2500), (128, 128, 700), (256, 256, 64), (512, 512, 2500),
-                                   (128, 512, 700)])
+                                   (128, 512, 700), (512, 256, 2504), (128, 128, 712), (256, 128, 22000),
+                                   (512, 256, 22000)])
 def test_dec_bce_dw_matches_unfused(B, d, V):
     """cc_dec_bce_dw (logits + BCE + dZ + dWo/dbo in one pass) vs the unfused NT-GEMM path (BCE
     epilogue writing dZ and dZ^T, then dW = D3^T dZ^T with the colsum bias gradient): dZ and dWo
     to a bf16 ulp, dbo (fused: the fp32 dz summed; unfused: the rounded dZ) to the same level; the
-    fp64 oracle of the same bf16 operands bounds both."""
+    fp64 oracle of the same bf16 operands bounds both.  With Wo read in place at d <= 256 and
+    V % 8 == 0 the kernel stages its slice by LDS-DMA (tr-read B fragments, dWo from the swapped
+    product): bit-identical to the Wo^T-copy kernel."""
     torch.manual_seed(B + d + V)
     bf = dict(device='cuda', dtype=torch.bfloat16)
     D3 = (torch.randn(B, d, device='cuda') * 0.5).to(torch.bfloat16)

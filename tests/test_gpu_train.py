@@ -363,41 +363,6 @@ def test_fused_w1_adam_matches_unfused(reg):
 
 
 @pytest.mark.parametrize('reg', [0.0, 0.1])
-def test_fp8_fused_output_adam_matches_unfused(reg):
-    """Config 5 with fuse_w1_adam and the opt-in fuse_wo_adam8: TF Adam on the decoder output layers
-    (Wo, bo and Wo_reg, bo_reg) in the MX-FP8 dW product's epilogue (cc_gemm_mx8_pair_adam), the
-    Adam + F launch over the complement (cc_adam_noise_pack2) — bit-identical parameters, bf16
-    shadow, moments and losses to the same step with that Adam left in the Adam + F launch
-    (bench.py's configuration), over eager steps and graph replays (N = V = 2,500 is not a multiple of the
-    256-column tile: the edge tiles' masked columns)."""
-    out = {}
-    for nofuse in (True, False):
-        lists, Mt, ns = problem(17, 1024, 2500, (20, 40, 80))
-        P = model_ref.init_params(2500, 1024, seed=17, bias_std=0.01)
-        lay = Layout(2500, 1024)
-        cfg = TrainConfig(V=2500, d=1024, batch_size=128, reg=reg, dtype='fp8', seed=17, fuse_w1_adam=True,
-                          fuse_wo_adam8=not nofuse)
-        tr = Trainer(cfg, DeviceDataset(lists, 2500, y_mtx=Mt.astype(np.float32) if reg > 0 else None,
-                                        neg_sampler=ns), params_flat=lay.pack(P))
-        tr.set_epoch_permutation(np.random.default_rng(17).permutation(1024).astype(np.int32))
-        assert tr.mx8 and tr.fuse_w1 and tr.fuse_wo8 == (not nofuse)
-        losses = []
-        for _ in range(2):
-            tr.step()
-            losses.append(tr.losses())
-        tr.capture()
-        for _ in range(3):
-            tr.step()
-            losses.append(tr.losses())
-        tr.flush()
-        torch.cuda.synchronize()
-        out[nofuse] = (tr.params.cpu(), tr.m.cpu(), tr.v.cpu(), tr.shadow.cpu(), losses)
-    for a, b in zip(out[True][:4], out[False][:4]):
-        assert torch.equal(a, b)
-    assert out[True][4] == out[False][4]
-
-
-@pytest.mark.parametrize('reg', [0.0, 0.1])
 def test_step_many_multi_graph_matches_single_steps(reg):
     """step_many — graph_steps (here 3) whole steps per captured graph replay, the loss
     accumulated inside the graph — gives bit-identical parameters, moments, shadow, device

@@ -7,6 +7,7 @@
 #   prof[:<bench.py args>]    rocprofv3 --kernel-trace --stats of a bench run  -> $O/prof_<i>/
 #   pmc:<COUNTER>[:<args>]    one rocprofv3 --pmc pass of a short bench run    -> $O/pmc_<COUNTER>_<i>/
 #   py:<script args>          python -u <script args>                          -> $O/py_<i>.log
+#   cmd:<command>             any command (a built probe binary)               -> $O/cmd_<i>.log
 # Every GPU step runs under its own time limit; the first failing step ends the session.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R" || exit 1
 TAG=$1; shift
@@ -51,6 +52,9 @@ for st in "$@"; do
     py)
       timeout -k 10 600 python -u $arg > "$O/py_$i.log" 2>&1 || { tail -30 "$O/py_$i.log"; exit 1; }
       tail -15 "$O/py_$i.log" ;;
+    cmd)
+      timeout -k 10 300 $arg > "$O/cmd_$i.log" 2>&1 || { tail -30 "$O/cmd_$i.log"; exit 1; }
+      tail -12 "$O/cmd_$i.log" ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done

@@ -1,7 +1,7 @@
 // Per-block phase timestamps of dec_bce_dw_kernel at the bench shape (B = 512, d = 256, V = 22000, Wo read
 // in place, packed D3 images) on random operands (dev tool): HIP-event time of the call, start / end spread
 // over blocks and per-phase medians.
-// hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I cubecobrarecommender_amd/csrc tools/micro/dec_probe2.hip \
+// hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I cubecobrarecommender_amd/csrc [-DDEC_SRC=\"decout_exp.hip\" -D...] tools/micro/dec_probe2.hip \
 //   cubecobrarecommender_amd/csrc/api.cpp cubecobrarecommender_amd/csrc/host_util.cpp -o tools/micro/bin/dec_probe2
 #include <hip/hip_runtime.h>
 
@@ -19,7 +19,10 @@ __device__ unsigned long long g_wav[1024][8][16];
     if (threadIdx.x == 0 && blockIdx.x < 1024) g_blk[blockIdx.x][(k)] = wall_clock64(); \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) g_wav[blockIdx.x][threadIdx.x >> 6][(k)] = wall_clock64(); \
   } while (0)
-#include "decout.hip"
+#ifndef DEC_SRC
+#define DEC_SRC "decout.hip"
+#endif
+#include DEC_SRC
 
 static uint16_t f2bf(float f) {
   uint32_t u;

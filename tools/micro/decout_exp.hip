@@ -37,20 +37,8 @@ constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
 #ifndef DEC_GW_CPOL
 #define DEC_GW_CPOL 0
 #endif
-// The two waves of a SIMD run the VALU-bound BCE epilogue together; issue arbitration favours the
-// older one, so waves 4-7 finish ~3.6 us later and the barrier after phase 1 waits for them (probe:
-// tools/micro/dec_probe2.hip).  DEC_PRIO_TOGGLE: in pass ps the half (w >> 2) == (ps & 1) runs at
-// s_setprio 1, so the half that lagged in pass 0 leads in pass 1 (build knob; DMA kernels only)
-#ifndef CCREC_DEC_DMA   // build knob: 0 keeps the register-staged kernel for every shape
-#define CCREC_DEC_DMA 1
-#endif
-#ifndef DEC_PRIO_TOGGLE
-#define DEC_PRIO_TOGGLE 1
-#endif
 
 typedef __attribute__((ext_vector_type(4))) uint32_t v4u;  // staging registers (stay in VGPRs)
-typedef __attribute__((address_space(3))) void lds_void;
-typedef short v4s __attribute__((ext_vector_type(4)));
 
 struct DecOutP {
   const bf16_t *D3;        // [B][d]
@@ -94,14 +82,7 @@ __device__ __forceinline__ uint32_t bf16_pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
 }
 
-// DMA = true (d <= 256, V % 8 == 0: every Wo row segment 16-B aligned): the Wo slice is copied
-// global -> LDS by buffer_load_dwordx4 ... lds as raw rows Wk[d][NB] (192 B: the tr-read banks of
-// 4 consecutive k rows are disjoint, no swizzle) and the target words by buffer_load_dword ... lds
-// as ys[row][NJ] — no VGPR round trip and no transposing LDS writes; phase 1 takes its B fragments
-// from Wk with ds_read_b64_tr_b16 (column n, 4 consecutive k per read); phase 2 runs with the
-// operands swapped (dZ^T rows = A, D3^T = B), so a lane holds 4 consecutive dWo columns of one row
-// per register group and the gradient leaves as 16-B stores.
-template <int D, int BB, bool DMA>
+template <int D, int BB>
 __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   constexpr int d = D, B = BB;
   constexpr int NB = nb_of<D>(), NJ = NB / 32;    // slice columns, 32-column accumulators per wave
@@ -112,9 +93,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   // a ring of 16 through the pass's 32 k-steps
   constexpr bool RING1 = nkk > 16;
   constexpr int NAF = RING1 ? 16 : nkk;
-  // LDS map (bytes): the Wo^T slice [NB][d] (DMA: Wo rows [d][NB]); dZ^T [NB][B]; the target bits
-  // [NJ][B] (DMA: [B][NJ])
-  static_assert(!DMA || NB == 96, "dec_bce_dw_kernel: the DMA staging assumes 96-column slices");
+  // LDS map (bytes): the Wo^T slice [NB][d]; dZ^T [NB][B]; the target bits [NJ][B]
   constexpr int ZT_OFF = NB * d * 2, ZT_BYTES = NB * B * 2;
   constexpr int YS_OFF = ZT_OFF + ZT_BYTES, LDS_BYTES = YS_OFF + B * NJ * 4;
   static_assert(LDS_BYTES <= 150 * 1024, "dec_bce_dw_kernel: LDS");
@@ -154,32 +133,6 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   load_a(af[0], 0);
   // ---- resident operands: Wo^T slice (rows clamped at the edge: they feed masked columns only)
   // and the target bits; every load of the batch issued before the first LDS store
-  if constexpr (DMA) {
-    // Wo rows k, columns [n0, n0 + 96) -> Wk[k][96]: chunk q = 12 k + c (16 B) of the image is
-    // lane q % 64 of DMA instruction q / 64; columns past V read the next row (masked columns
-    // only) and rows past d read zeros (beyond the descriptor's range)
-    constexpr int NI = d * 12 / 64 / (NTH / 64);   // DMA instructions per wave (6 at d = 256)
-    const __amdgpu_buffer_rsrc_t wr =
-        __builtin_amdgcn_make_buffer_rsrc((void *)p.Wo, (short)0, (uint32_t)d * (uint32_t)V * 2u, 0x00020000);
-#pragma unroll
-    for (int u = 0; u < NI; ++u) {
-      const int i = w * NI + u, q = i * 64 + lane, k = q / 12, c = q % 12;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void *)(Wt + i * 512), 16,
-                                               (uint32_t)((k * V + n0 + 8 * c) * 2), 0, 0, 0);
-    }
-    // target words: ys[row][j] = y_bits[row][n0 / 32 + j], 4 B per lane (words past the row's end
-    // belong to masked columns)
-    constexpr int NYT = B * NJ / 64;                // DMA instructions in all (24 at B = 512)
-    const __amdgpu_buffer_rsrc_t yr =
-        __builtin_amdgcn_make_buffer_rsrc((void *)p.y_bits, (short)0, (uint32_t)B * (uint32_t)VW * 4u, 0x00020000);
-#pragma unroll
-    for (int u = 0; u < (NYT + 7) / 8; ++u) {
-      const int i = w + 8 * u, q = i * 64 + lane, r = q / NJ, j = q % NJ;
-      if (i >= NYT) break;                          // (wave-uniform)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_void *)(ys + i * 64), 4,
-                                               (uint32_t)((r * VW + (n0 >> 5) + j) * 4), 0, 0, 0);
-    }
-  } else
   {
     constexpr int NW = NB * CHD / NTH, NY = (B * NJ + NTH - 1) / NTH;
     // from Wo [d][V]: task = (4 consecutive k, 8 consecutive columns) -> 4 row loads, then 8
@@ -277,12 +230,8 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   bf16x8_t ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (__bf16)(half == 0 && e < 3 ? 1.f : 0.f);
-  // LDS-only barrier: __syncthreads would also wait for pass 0's A fragments (vmcnt counts loads).
-  // DMA: the wave's own DMAs (issued after pass 0's A fragments) must have landed first
-  if constexpr (DMA)
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  // LDS-only barrier: __syncthreads would also wait for pass 0's A fragments (vmcnt counts loads)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   DEC_PROBE(1);
   const float scale = p.scale;
   // dZ and gW through buffer descriptors: a 32-bit byte offset per store instead of a 64-bit
@@ -303,27 +252,13 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     for (int kk = 0; kk < nkk; ++kk) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        bf16x8_t b;
-        if constexpr (DMA) {   // column n = 32 j + (lane & 31), k = 16 kk + 8 half + 0..7: two transposed reads
-          const bf16_t *tb = Wt + (kk * 16 + 8 * half + ((lane >> 2) & 3)) * NB + j * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)tb);
-          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)(tb + 4 * NB));
-          b = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-        } else {
-          b = frag(Wt, sw_off(j * 32 + (lane & 31), kk * 16 + 8 * half, CHD));
-        }
+        const bf16x8_t b = frag(Wt, sw_off(j * 32 + (lane & 31), kk * 16 + 8 * half, CHD));
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[RING1 ? 0 : ps & 1][kk % NAF], b, acc[j], 0, 0, 0);
       }
       if (RING1 && kk + NAF < nkk) af[0][kk % NAF] = *reinterpret_cast<const bf16x8_t *>(asrc + (kk + NAF) * astr);
     }
     if (RING1 && ps + 1 < npass) load_a(af[0], ps + 1);   // the next pass's head under this epilogue
     DEC_PROBE(2 + 2 * ps);
-    if constexpr (DMA && DEC_PRIO_TOGGLE && npass > 1) {   // (wave-uniform: w from readfirstlane)
-      if ((__builtin_amdgcn_readfirstlane(w) >> 2) == (ps & 1))
-        __builtin_amdgcn_s_setprio(1);
-      else
-        __builtin_amdgcn_s_setprio(0);
-    }
     const int rb = ps * 256 + w * 32;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -337,19 +272,12 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         // quarter-rate instruction; summed log2 scaled by ln 2 at the end
         // store offsets: the lane part in a VGPR, the row part (r) as the scalar soffset
         const uint32_t zv = 2u * (uint32_t)((rb + 4 * half) * V + n0 + col);
+        const uint32_t zv4 = 2u * (uint32_t)((rb + 4 * half + (lane & 1)) * V + n0 + (col & ~1));
         f32x2_t lprod = {1.f, 1.f}, rs2 = {0.f, 0.f}, cs2 = {0.f, 0.f};  // even / odd rows: packed math
         // the 16 rows' target words: 4 runs of 4 consecutive rows -> 4 LDS reads of 16 B
         uint4 yw[4];
-        if constexpr (DMA) {   // ys[row][NJ]: word j of rows rb + 8g + 4 half + 0..3
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const uint32_t *yr4 = ys + (rb + 8 * g + 4 * half) * NJ + j;
-            yw[g] = uint4{yr4[0], yr4[NJ], yr4[2 * NJ], yr4[3 * NJ]};
-          }
-        } else {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) yw[g] = *reinterpret_cast<const uint4 *>(ys + j * B + rb + 8 * g + 4 * half);
-        }
+        for (int g = 0; g < 4; ++g) yw[g] = *reinterpret_cast<const uint4 *>(ys + j * B + rb + 8 * g + 4 * half);
 #pragma unroll
         for (int r2 = 0; r2 < 16; r2 += 2) {
           f32x2_t z2, a2, opa2, rp2, sel2, rl2, ys2;
@@ -375,12 +303,20 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
           cs2 += dzp;   // the bias gradient sums the fp32 dz (the reference's arithmetic)
           const uint32_t pk = bf16_pack2(dzp[0], dzp[1]);
           tt[r2 >> 1] = pk;
+#if defined(DEC_DZ_W4)
+          {  // lane pairs (c, c + 1): even lane -> row r2 cols (c, c+1), odd lane -> row r2 + 1 cols (c-1, c)
+            const uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)pk, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+            const uint32_t o = __builtin_amdgcn_perm(x, pk, (lane & 1) ? 0x07060302u : 0x05040100u);
+            __builtin_amdgcn_raw_buffer_store_b32(o, dz_rs, zv4, 2u * (uint32_t)(((r2 & 3) + 8 * (r2 >> 2)) * V), DEC_DZ_CPOL);
+          }
+#elif !defined(DEC_NO_DZ)
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
             const int r = r2 + e;
             __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(e ? pk >> 16 : pk), dz_rs, zv,
                                                   2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), DEC_DZ_CPOL);
           }
+#endif
         }
         lsum += __builtin_amdgcn_logf(lprod[0] * lprod[1]);
         rsum += rs2[0] + rs2[1];
@@ -396,7 +332,6 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     }
     DEC_PROBE(3 + 2 * ps);
   }
-  if constexpr (DMA && DEC_PRIO_TOGGLE && npass > 1) __builtin_amdgcn_s_setprio(0);
 
   // bias gradient: column sums of dz in a fixed order (lane halves, then waves)
 #pragma unroll
@@ -466,10 +401,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const bf16x8_t b = frag(Zt, sw_off(j * 32 + (lane & 31), kc * BK + kk * 16 + 8 * half, CHB));
-          if constexpr (DMA)   // dWo^T tile: lane = d row, registers = columns
-            acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, ring[q][kk], acc2[j], 0, 0, 0);
-          else
-            acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[q][kk], b, acc2[j], 0, 0, 0);
+          acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[q][kk], b, acc2[j], 0, 0, 0);
         }
       }
       if (kc + P2D < nk2) {
@@ -481,29 +413,20 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     DEC_PROBE(7);
     const __amdgpu_buffer_rsrc_t gw_rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)p.gW, (short)0, (uint32_t)d * (uint32_t)V * 4u, 0x00020000);
-    if constexpr (DMA) {   // row dr0 + (lane & 31), columns n0 + 32 j + 8 g + 4 half + 0..3: 16 B
-      const uint32_t rowoff = 4u * (uint32_t)((dr0 + (lane & 31)) * V + n0 + 4 * half);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j) {
+      const int gc2 = n0 + j * 32 + (lane & 31);
+      if (gc2 < V) {
+        uint32_t g0 = (uint32_t)((dr0 + 4 * half) * V + gc2);
+        asm volatile("" : "+v"(g0));
+#ifndef DEC_NO_GW
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          if (n0 + j * 32 + 8 * g + 4 * half < V)   // (V % 8 == 0: a run is all in or all out)
-            __builtin_amdgcn_raw_buffer_store_b128(
-                v4u{__float_as_uint(acc2[j][4 * g]), __float_as_uint(acc2[j][4 * g + 1]),
-                    __float_as_uint(acc2[j][4 * g + 2]), __float_as_uint(acc2[j][4 * g + 3])},
-                gw_rs, rowoff + 4u * (uint32_t)(j * 32 + 8 * g), 0, DEC_GW_CPOL);
-    } else {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int gc2 = n0 + j * 32 + (lane & 31);
-        if (gc2 < V) {
-          uint32_t g0 = (uint32_t)((dr0 + 4 * half) * V + gc2);
-          asm volatile("" : "+v"(g0));
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc2[j][r]), gw_rs,
-                                                  4u * (g0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V)), 0, DEC_GW_CPOL);
-        }
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc2[j][r]), gw_rs,
+                                                4u * (g0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V)), 0, DEC_GW_CPOL);
+#else
+        if (acc2[j][0] == 12345.f) p.gW[0] = acc2[j][1];
+#endif
       }
     }
   }
@@ -583,17 +506,8 @@ extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const
   p.ldt = ldt;
   const dim3 grid((unsigned)cdiv(V, d <= 256 ? nb_of<256>() : nb_of<512>())), block(NTH);
   hipStream_t s = as_stream(stream);
-  // the DMA staging: Wo read in place with every row segment 16-B aligned (V % 8 == 0), the
-  // 96-column slices of d <= 256
-  const bool dma = CCREC_DEC_DMA && Wo != nullptr && WoT == nullptr && V % 8 == 0 && d <= 256 && (((uintptr_t)y_bits) & 3) == 0 &&
-                   (int64_t)d * V * 2 <= 0xFFFFFFFFll && (int64_t)B * ((V + 31) / 32) * 4 <= 0xFFFFFFFFll;
-#define DO_LAUNCH(DD, BBB)                                                                    \
-  if (d == DD && B == BBB) {                                                                  \
-    if (dma && DD <= 256)                                                                     \
-      hipLaunchKernelGGL((dec_bce_dw_kernel<DD, BBB, DD <= 256>), grid, block, 0, s, p);      \
-    else                                                                                      \
-      hipLaunchKernelGGL((dec_bce_dw_kernel<DD, BBB, false>), grid, block, 0, s, p);          \
-  }
+#define DO_LAUNCH(DD, BBB) \
+  if (d == DD && B == BBB) hipLaunchKernelGGL((dec_bce_dw_kernel<DD, BBB>), grid, block, 0, s, p);
   DO_LAUNCH(256, 512) DO_LAUNCH(256, 256) DO_LAUNCH(256, 128)
   DO_LAUNCH(128, 512) DO_LAUNCH(128, 256) DO_LAUNCH(128, 128)
   DO_LAUNCH(512, 512) DO_LAUNCH(512, 256) DO_LAUNCH(512, 128)
