@@ -44,6 +44,9 @@ constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
 #ifndef CCREC_DEC_DMA   // build knob: 0 keeps the register-staged kernel for every shape
 #define CCREC_DEC_DMA 1
 #endif
+#ifndef DEC_SPLIT2       // build knob: 0 keeps phase 2 whole after the barrier
+#define DEC_SPLIT2 1
+#endif
 #ifndef DEC_PRIO_TOGGLE
 #define DEC_PRIO_TOGGLE 1
 #endif
@@ -88,7 +91,12 @@ __device__ __forceinline__ uint16_t bf16_bits(float f) {  // RNE (v_cvt_pk_bf16_
   return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
 typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+// x ^ (m & 0x80000000): the sign of x flipped by bit 31 of m — ONE v_bitop3_b32 (LUT 0x78 = a ^ (b & c))
+__device__ __forceinline__ uint32_t xor_sign(uint32_t x, uint32_t m) {
+  return __builtin_amdgcn_bitop3_b32(x, m, 0x80000000u, 0x78);
+}
 // two floats -> one packed bf16 pair (lo = a, hi = b), RNE: ONE v_cvt_pk_bf16_f32
 __device__ __forceinline__ uint32_t bf16_pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
@@ -96,17 +104,24 @@ __device__ __forceinline__ uint32_t bf16_pack2(float a, float b) {
 
 // DMA = true (d <= 256, V % 8 == 0: every Wo row segment 16-B aligned): the Wo slice is copied
 // global -> LDS by buffer_load_dwordx4 ... lds as raw rows Wk[d][NB] (192 B: the tr-read banks of
-// 4 consecutive k rows are disjoint, no swizzle) and the target words by buffer_load_dword ... lds
-// as ys[row][NJ] — no VGPR round trip and no transposing LDS writes; phase 1 takes its B fragments
-// from Wk with ds_read_b64_tr_b16 (column n, 4 consecutive k per read); phase 2 runs with the
-// operands swapped (dZ^T rows = A, D3^T = B), so a lane holds 4 consecutive dWo columns of one row
-// per register group and the gradient leaves as 16-B stores.
+// 4 consecutive k rows are disjoint, no swizzle) — no VGPR round trip and no transposing LDS
+// writes; phase 1 takes its B fragments from Wk with ds_read_b64_tr_b16 (column n, 4 consecutive
+// k per read).  (Measured and dropped with it: the target words by 4-B LDS-DMA as [row][NJ] — the
+// epilogue's strided reads cost more than the staging saved — and phase 2 with the operands swapped
+// for 16-B dWo stores: 32 rows x 32 B per store instruction ran slower than 2 x 128-B rows of
+// 4-B stores; tools/micro/dec_probe2.hip)
 template <int D, int BB, bool DMA>
 __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   constexpr int d = D, B = BB;
   constexpr int NB = nb_of<D>(), NJ = NB / 32;    // slice columns, 32-column accumulators per wave
   constexpr int CHD = d / 8, CHB = B / 8;
   constexpr int nkk = d / 16;                     // 16-k steps of phase 1
+  // SPLIT2 (d = 256, B = 512): phase 2 in two parts.  The dZ rows of waves 0-3 (K chunks 0, 1, 4, 5
+  // of 64 rows) are ready while waves 4-7 — which lose the VALU arbitration of the shared SIMDs —
+  // are still in their epilogue; waves 0-3 multiply them then (their d tile w and the partner's
+  // w + 4, the partner's partial handed over through LDS), and after the barrier each wave adds
+  // only the other half's chunks 2, 3, 6, 7 of its own tile: half the MFMAs after the barrier.
+  constexpr bool SPLIT2 = DEC_SPLIT2 && d == 256 && B == 512;
   constexpr int npass = (B + 255) / 256;          // 256-row passes of phase 1
   // phase-1 A fragments: d <= 256 holds a whole pass (and the next one in flight); d = 512 walks
   // a ring of 16 through the pass's 32 k-steps
@@ -122,6 +137,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   __shared__ float red_cs[NTH / 64][NB];
   __shared__ double red_loss[NTH / 64];
   __shared__ int lastflag;
+  __shared__ int cnt_wt, cnt_z;   // SPLIT2 hand-offs between the wave halves (LDS counters)
   // the slice's bias as MFMA B fragments: k = 0, 1, 2 carry the exact three-bf16 split of bo
   // (hi + mid + lo == bo in fp32), so one MFMA against a ones A fragment starts the accumulators at
   // the bias with no per-element moves (the epilogue is VALU-bound; the MFMA pipe has room)
@@ -167,19 +183,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void *)(Wt + i * 512), 16,
                                                (uint32_t)((k * V + n0 + 8 * c) * 2), 0, 0, 0);
     }
-    // target words: ys[row][j] = y_bits[row][n0 / 32 + j], 4 B per lane (words past the row's end
-    // belong to masked columns)
-    constexpr int NYT = B * NJ / 64;                // DMA instructions in all (24 at B = 512)
-    const __amdgpu_buffer_rsrc_t yr =
-        __builtin_amdgcn_make_buffer_rsrc((void *)p.y_bits, (short)0, (uint32_t)B * (uint32_t)VW * 4u, 0x00020000);
-#pragma unroll
-    for (int u = 0; u < (NYT + 7) / 8; ++u) {
-      const int i = w + 8 * u, q = i * 64 + lane, r = q / NJ, j = q % NJ;
-      if (i >= NYT) break;                          // (wave-uniform)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_void *)(ys + i * 64), 4,
-                                               (uint32_t)((r * VW + (n0 >> 5) + j) * 4), 0, 0, 0);
-    }
-  } else
+  }
   {
     constexpr int NW = NB * CHD / NTH, NY = (B * NJ + NTH - 1) / NTH;
     // from Wo [d][V]: task = (4 consecutive k, 8 consecutive columns) -> 4 row loads, then 8
@@ -189,10 +193,12 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     constexpr int NT4 = (d / 4 * CN + NTH - 1) / NTH;  // tasks per thread
     const bool fromWo = p.WoT == nullptr;
     const bool vec = fromWo && (V % 8 == 0) && n0 + NB <= V;
+    constexpr bool STAGE = !DMA;   // the Wo^T slice through registers (DMA: already in flight)
     v4u wv[fromWo ? 1 : NW];
     v4u w4[NT4][4];
     uint32_t yv[NY];
-    if (!fromWo) {
+    if (!STAGE) {
+    } else if (!fromWo) {
 #pragma unroll
       for (int q = 0; q < NW; ++q) {
         const int c = tid + NTH * q, n = c / CHD, ch = c % CHD;
@@ -225,7 +231,8 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
       yv[q] = gw < VW ? p.y_bits[(int64_t)r * VW + gw] : 0u;
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (!fromWo) {
+    if (!STAGE) {
+    } else if (!fromWo) {
 #pragma unroll
       for (int q = 0; q < NW; ++q) {
         const int c = tid + NTH * q, n = c / CHD, ch = c % CHD;
@@ -277,6 +284,10 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   bf16x8_t ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (__bf16)(half == 0 && e < 3 ? 1.f : 0.f);
+  if (tid == 0) {
+    cnt_wt = 0;
+    cnt_z = 0;
+  }
   // LDS-only barrier: __syncthreads would also wait for pass 0's A fragments (vmcnt counts loads).
   // DMA: the wave's own DMAs (issued after pass 0's A fragments) must have landed first
   if constexpr (DMA)
@@ -318,6 +329,12 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     }
     if (RING1 && ps + 1 < npass) load_a(af[0], ps + 1);   // the next pass's head under this epilogue
     DEC_PROBE(2 + 2 * ps);
+    if constexpr (SPLIT2) {
+      if (ps == npass - 1) {   // this wave reads the Wo slice no more (its fragment reads returned)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add(&cnt_wt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
     if constexpr (DMA && DEC_PRIO_TOGGLE && npass > 1) {   // (wave-uniform: w from readfirstlane)
       if ((__builtin_amdgcn_readfirstlane(w) >> 2) == (ps & 1))
         __builtin_amdgcn_s_setprio(1);
@@ -332,36 +349,34 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
       if (valid[j]) {
         // sigmoid_cross_entropy_with_logits (TF 2.5 Keras BCE on a sigmoid output):
         //   loss = max(z, 0) - z y + log1p(exp(-|z|)),  dz = (sigmoid(z) - y) / (B V)
-        // a = exp(-|z|) once; log1p and 1/(1+a) from it.  The 16 factors 1 + a in (1, 2] of a
-        // lane's column are multiplied (<= 2^16) and one log2 per column taken: the log is a
-        // quarter-rate instruction; summed log2 scaled by ln 2 at the end
+        // in the target-signed logit s = (1 - 2y) z (the sign bit of z flipped where y = 1):
+        //   loss = max(s, 0) + log1p(exp(-|s|)),  dz = (1 - 2y) sigmoid(s) / (B V)
+        // (sigmoid(z) - 1 = -sigmoid(-z)), so the target bit enters as one sign mask shared by s
+        // and dz — two 3-input bit ops — and sigmoid(s) never cancels against y.  a = exp(-|s|)
+        // once; log1p and 1/(1+a) from it.  The 16 factors 1 + a in (1, 2] of a lane's column are
+        // multiplied (<= 2^16) and one log2 per column taken: the log is a quarter-rate
+        // instruction; summed log2 scaled by ln 2 at the end
         // store offsets: the lane part in a VGPR, the row part (r) as the scalar soffset
         const uint32_t zv = 2u * (uint32_t)((rb + 4 * half) * V + n0 + col);
         f32x2_t lprod = {1.f, 1.f}, rs2 = {0.f, 0.f}, cs2 = {0.f, 0.f};  // even / odd rows: packed math
         // the 16 rows' target words: 4 runs of 4 consecutive rows -> 4 LDS reads of 16 B
         uint4 yw[4];
-        if constexpr (DMA) {   // ys[row][NJ]: word j of rows rb + 8g + 4 half + 0..3
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const uint32_t *yr4 = ys + (rb + 8 * g + 4 * half) * NJ + j;
-            yw[g] = uint4{yr4[0], yr4[NJ], yr4[2 * NJ], yr4[3 * NJ]};
-          }
-        } else {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) yw[g] = *reinterpret_cast<const uint4 *>(ys + j * B + rb + 8 * g + 4 * half);
-        }
+        for (int g = 0; g < 4; ++g) yw[g] = *reinterpret_cast<const uint4 *>(ys + j * B + rb + 8 * g + 4 * half);
+        const uint32_t ysh = 31u - (uint32_t)(lane & 31);   // the lane's target bit -> bit 31
 #pragma unroll
         for (int r2 = 0; r2 < 16; r2 += 2) {
-          f32x2_t z2, a2, opa2, rp2, sel2, rl2, ys2;
+          f32x2_t s2, a2, opa2, rp2, sel2, rl2;
+          uint32_t ym[2];
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
             const int r = r2 + e;
             const uint32_t ywr = (r & 3) == 0 ? yw[r >> 2].x : (r & 3) == 1 ? yw[r >> 2].y : (r & 3) == 2 ? yw[r >> 2].z : yw[r >> 2].w;
-            const bool yb = (ywr >> (lane & 31)) & 1u;
-            z2[e] = acc[j][r];
-            a2[e] = __builtin_amdgcn_exp2f(-fabsf(z2[e]) * LOG2E);
-            rl2[e] = fmaxf(yb ? -z2[e] : z2[e], 0.f);
-            ys2[e] = yb ? -scale : 0.f;
+            ym[e] = ywr << ysh;
+            const float z = acc[j][r];
+            s2[e] = __uint_as_float(xor_sign(__float_as_uint(z), ym[e]));
+            a2[e] = __builtin_amdgcn_exp2f(-fabsf(z) * LOG2E);
+            rl2[e] = fmaxf(s2[e], 0.f);
           }
           opa2 = 1.f + a2;
 #pragma unroll
@@ -370,8 +385,11 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
           rs2 += rl2;
           const f32x2_t arp2 = a2 * rp2;
 #pragma unroll
-          for (int e = 0; e < 2; ++e) sel2[e] = z2[e] >= 0.f ? rp2[e] : arp2[e];
-          const f32x2_t dzp = sel2 * scale + ys2;   // fma: (sigmoid(z) - y) / (B V)
+          for (int e = 0; e < 2; ++e) sel2[e] = s2[e] >= 0.f ? rp2[e] : arp2[e];   // sigmoid(s)
+          const f32x2_t mag2 = sel2 * scale;
+          f32x2_t dzp;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) dzp[e] = __uint_as_float(xor_sign(__float_as_uint(mag2[e]), ym[e]));
           cs2 += dzp;   // the bias gradient sums the fp32 dz (the reference's arithmetic)
           const uint32_t pk = bf16_pack2(dzp[0], dzp[1]);
           tt[r2 >> 1] = pk;
@@ -397,6 +415,10 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     DEC_PROBE(3 + 2 * ps);
   }
   if constexpr (DMA && DEC_PRIO_TOGGLE && npass > 1) __builtin_amdgcn_s_setprio(0);
+  if constexpr (SPLIT2) {   // waves 0-3: this wave's dZ^T rows are in LDS
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (w < 4 && lane == 0) __hip_atomic_fetch_add(&cnt_z, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
 
   // bias gradient: column sums of dz in a fixed order (lane halves, then waves)
 #pragma unroll
@@ -408,6 +430,124 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) lossf += __shfl_xor(lossf, off);
   if (lane == 0) red_loss[w] = (double)lossf;
+  const bool pk = p.D3tp != nullptr;
+  if constexpr (SPLIT2) {
+    // A fragment (chunk kc, step kk) of d tile t: 1 KB contiguous from the packed D3^T image, or
+    // row-strided from D3^T
+    auto arow_t = [&](int t) -> const bf16_t * {
+      return pk ? p.D3tp + ((int64_t)t * (p.ldt / 16) * 64 + lane) * 8
+                : p.D3t + (int64_t)(t * 32 + (lane & 31)) * p.ldt + 8 * half;
+    };
+    auto af_t = [&](const bf16_t *ar, int kc, int kk) {
+      return *reinterpret_cast<const bf16x8_t *>(ar + (pk ? (kc * 4 + kk) * 512 : kc * BK + kk * 16));
+    };
+    const bool fast = __builtin_amdgcn_readfirstlane(w) < 4;   // (wave-uniform)
+    const bf16_t *ar = arow_t(w);
+    f32x16_t acc2[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
+    // the partner's partial: 16 x 64 fp32 per 32-column tile, [j][group g][lane][4]
+    float *part = reinterpret_cast<float *>(smem) + (w & 3) * (NJ * 16 * 64);
+    static_assert(4 * NJ * 16 * 64 * 4 <= ZT_OFF, "dec_bce_dw_kernel: partials fit the Wo slice's LDS");
+    if (fast) {
+      const bf16_t *arx = arow_t(w + 4);
+      f32x16_t accx[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accx[j][r] = 0.f;
+      constexpr int KF[4] = {0, 1, 4, 5};
+      bf16x8_t fa[2][4], fx[2][4];   // two chunks in flight
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          fa[q][kk] = af_t(ar, KF[q], kk);
+          fx[q][kk] = af_t(arx, KF[q], kk);
+        }
+      while (__hip_atomic_load(&cnt_z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int kc = KF[c], q = c & 1;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const bf16x8_t b = frag(Zt, sw_off(j * 32 + (lane & 31), kc * BK + kk * 16 + 8 * half, CHB));
+            acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q][kk], b, acc2[j], 0, 0, 0);
+            accx[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fx[q][kk], b, accx[j], 0, 0, 0);
+          }
+        if (c + 2 < 4) {
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            fa[q][kk] = af_t(ar, KF[c + 2], kk);
+            fx[q][kk] = af_t(arx, KF[c + 2], kk);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      // the Wo slice's LDS is free once every wave is past its phase-1 MFMAs
+      while (__hip_atomic_load(&cnt_wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < NTH / 64) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4_t *>(part + ((j * 4 + g) * 64 + lane) * 4) =
+              f32x4_t{accx[j][4 * g], accx[j][4 * g + 1], accx[j][4 * g + 2], accx[j][4 * g + 3]};
+    }
+    // this wave's own tile, the slow half's chunks: fragments in flight across the barrier
+    constexpr int KS[4] = {2, 3, 6, 7};
+    bf16x8_t fs[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) fs[c][kk] = af_t(ar, KS[c], kk);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // dZ^T rows, partials, red_cs, red_loss
+    DEC_PROBE(6);
+    if (tid < NB && n0 + tid < V) {
+      float g = 0.f;
+      for (int i = 0; i < NTH / 64; ++i) g += red_cs[i][tid];
+      p.gb[n0 + tid] = g;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const bf16x8_t b = frag(Zt, sw_off(j * 32 + (lane & 31), KS[c] * BK + kk * 16 + 8 * half, CHB));
+          acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fs[c][kk], b, acc2[j], 0, 0, 0);
+        }
+    if (!fast) {   // + the fast partner's chunks 0, 1, 4, 5 of this tile
+      const float *pp = reinterpret_cast<const float *>(smem) + (w & 3) * (NJ * 16 * 64);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4_t x = *reinterpret_cast<const f32x4_t *>(pp + ((j * 4 + g) * 64 + lane) * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc2[j][4 * g + e] += x[e];
+        }
+    }
+    DEC_PROBE(7);
+    const int dr0 = w * 32;
+    const __amdgpu_buffer_rsrc_t gw_rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)p.gW, (short)0, (uint32_t)d * (uint32_t)V * 4u, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int gc2 = n0 + j * 32 + (lane & 31);
+      if (gc2 < V) {
+        uint32_t g0 = (uint32_t)((dr0 + 4 * half) * V + gc2);
+        asm volatile("" : "+v"(g0));
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc2[j][r]), gw_rs,
+                                                4u * (g0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V)), 0, DEC_GW_CPOL);
+      }
+    }
+  } else {
   // phase 2's first A fragments in flight before the barrier.  The barrier waits for LDS only:
   // __syncthreads' release fence would also drain every wave's dZ stores (vmcnt(0), ~4 us), and
   // nothing below reads them.
@@ -415,7 +555,6 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   constexpr int nk2 = B / BK;
   constexpr int ND2 = (d + 255) / 256;   // 32-row d tiles per wave: w (and w + 8 at d = 512)
   // A fragment (kc, kk) of d tile dt: row-strided from D3^T, or 1 KB contiguous from the packed image
-  const bool pk = p.D3tp != nullptr;
   auto arow_of = [&](int dt) -> const bf16_t * {
     const int t = min(w + 8 * dt, d / 32 - 1);
     return pk ? p.D3tp + ((int64_t)t * (p.ldt / 16) * 64 + lane) * 8
@@ -466,10 +605,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const bf16x8_t b = frag(Zt, sw_off(j * 32 + (lane & 31), kc * BK + kk * 16 + 8 * half, CHB));
-          if constexpr (DMA)   // dWo^T tile: lane = d row, registers = columns
-            acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, ring[q][kk], acc2[j], 0, 0, 0);
-          else
-            acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[q][kk], b, acc2[j], 0, 0, 0);
+          acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[q][kk], b, acc2[j], 0, 0, 0);
         }
       }
       if (kc + P2D < nk2) {
@@ -481,18 +617,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     DEC_PROBE(7);
     const __amdgpu_buffer_rsrc_t gw_rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)p.gW, (short)0, (uint32_t)d * (uint32_t)V * 4u, 0x00020000);
-    if constexpr (DMA) {   // row dr0 + (lane & 31), columns n0 + 32 j + 8 g + 4 half + 0..3: 16 B
-      const uint32_t rowoff = 4u * (uint32_t)((dr0 + (lane & 31)) * V + n0 + 4 * half);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          if (n0 + j * 32 + 8 * g + 4 * half < V)   // (V % 8 == 0: a run is all in or all out)
-            __builtin_amdgcn_raw_buffer_store_b128(
-                v4u{__float_as_uint(acc2[j][4 * g]), __float_as_uint(acc2[j][4 * g + 1]),
-                    __float_as_uint(acc2[j][4 * g + 2]), __float_as_uint(acc2[j][4 * g + 3])},
-                gw_rs, rowoff + 4u * (uint32_t)(j * 32 + 8 * g), 0, DEC_GW_CPOL);
-    } else {
+    {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int gc2 = n0 + j * 32 + (lane & 31);
@@ -506,6 +631,8 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         }
       }
     }
+  }
+
   }
 
   // loss: the block partial, published after phase 2's stores (the ticket's vmcnt(0) drains them)

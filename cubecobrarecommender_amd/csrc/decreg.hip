@@ -6,11 +6,13 @@
 //
 //   stats  (slice, 256-row group) blocks: z = D3 Wo + bo on MFMA over a 96-column slice, per-row
 //          max and sum exp(z - max) of the slice -> partials [rows][slices]
-//   merge  one wave per row: m = max_i m_i, s = sum_i s_i exp(m_i - m) -> {m, 1/s, ln s, S}, where
-//          S = sum_j clip(M~[row], 1e-7, 1) is the clipped row mass (cc_kl_tsum, once per M~)
+//   merge  one wave per row: m = max_i m_i, s = sum_i s_i exp(m_i - m) -> {m, ln s, S, C}, where
+//          S = sum_j t and C = sum_j t ln t over t = clip(M~[row], 1e-7, 1) (cc_kl_tsum, once per M~)
 //   main   slice blocks over every row tile: z again, p = exp(z - m)/s, t = clip(M~ row, 1e-7, 1),
-//          KL += t (ln t - ln clip(p, 1e-7, 1)), dz = scale (p S - [p >= 1e-7] t) written row-major
-//          for the dX product and kept as dZ^T in LDS -> dWo[d][96] = D3^T dZ, dbo = colsum
+//          KL -= t ln clip(p, 1e-7, 1) (+ C once per row: KL = sum t (ln t - ln clip(p))), dz =
+//          scale (p S - [p >= 1e-7] t) written row-major for the dX product and kept as dZ^T in
+//          LDS -> dWo[d][96] = D3^T dZ, dbo = colsum.  Many row tiles (full mode): dWo instead by
+//          kl_dwo_kernel from the stored dZ (after the fix)
 //   fix    TF's gradient passes through clip only where p >= 1e-7, so the exact S is
 //          S - delta, delta = sum_{p < 1e-7} t.  The main kernel writes each (row, slice)'s delta
 //          partial (zero unless a wave saw such an element) and raises a flag; the fix kernel
@@ -337,7 +339,8 @@ __global__ __launch_bounds__(256) void kl_merge_kernel(KlP p) {
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
   if (lane == 0) {
     const int card = p.reg_idx[row];
-    p.rowstat[row] = make_float4(m, __logf(s), card >= 0 ? p.tsum[card] : 0.f, 0.f);
+    const float2 ts = card >= 0 ? reinterpret_cast<const float2 *>(p.tsum)[card] : make_float2(0.f, 0.f);
+    p.rowstat[row] = make_float4(m, __logf(s), ts.x, ts.y);
   }
 }
 
@@ -358,7 +361,7 @@ struct MainSmem {
 // waves' accumulators across all row tiles instead of the per-tile gW read-modify-write — the
 // 48 extra registers pushed the logits' fragment ring from 16 to 8 and spilled, and the logits
 // phases then waited on L2 twice as long: 1,620 -> 2,015 us per block, tools/micro/kl_probe_full.hip.)
-template <int D, bool FIX, int CPOL = 0>
+template <int D, bool FIX, int CPOL = 0, bool DW = true>
 __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt, MainSmem<kl_nb<D>()> &sm) {
   constexpr int NB = kl_nb<D>(), NJ = NB / 32;
   constexpr int CHB = TR / 8;
@@ -376,7 +379,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
     bias[j] = valid[j] ? p.bo[gc] : 0.f;
     cs[j] = 0.f;
   }
-  float klsum = 0.f;
+  float klsum = 0.f, klc = 0.f;   // klc: slice 0 adds each live row's sum_j t ln t once
   bool dead = false;
   // M~ rows and dZ through buffer descriptors: a 32-bit byte offset per access instead of a 64-bit
   // address (M~ < 4 GB at |V| <= 32k; dZ rows x V x 2 B < 4 GB)
@@ -400,6 +403,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       }
       sm.rs[i] = st;
       const int card = p.reg_idx[t0 + i];
+      if (!FIX && sl == 0 && card >= 0) klc += st.w;
       sm.card[i] = card >= 0 ? (int32_t)((uint32_t)card * (uint32_t)V * 4u) : (int32_t)0x80000000u;
     }
     lds_barrier();
@@ -461,7 +465,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
             const float lp = acc[j][r] - st.x - st.y;  // ln p = z - m - ln s
             const float pr = __builtin_amdgcn_exp2f(lp * LOG2E);
             const float tc = __builtin_amdgcn_fmed3f(tv[j][r], PMIN, 1.f);
-            klsum = fmaf(tc, fmaf(__builtin_amdgcn_logf(tc), LN2, -__builtin_amdgcn_fmed3f(lp, LN_PMIN, 0.f)), klsum);
+            klsum = fmaf(-tc, __builtin_amdgcn_fmed3f(lp, LN_PMIN, 0.f), klsum);   // (+ t ln t: rowstat.w)
             mn = fminf(mn, pr);
             const float dzf = scale * fmaf(pr, st.z, pr >= PMIN ? -tc : 0.f);
             const uint16_t zb = bf16_bits(dzf);
@@ -484,7 +488,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
             if constexpr (!FIX) {
               const float tc = __builtin_amdgcn_fmed3f(tv[j][r], PMIN, 1.f);
               const float lq = live ? fminf(lp, 0.f) : LN_PMIN;  // ln clip(p, 1e-7, 1)
-              const float term = tc * fmaf(__builtin_amdgcn_logf(tc), LN2, -lq);
+              const float term = -tc * lq;   // (the row's sum of t ln t: rowstat.w, added once)
               klsum += live_row ? term : 0.f;
               deadp |= live_row && !live;
               dz = live_row ? scale * (pr * st.z - (live ? tc : 0.f)) : 0.f;
@@ -507,10 +511,12 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
             if (valid[j]) __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, CPOL);
           }
         }
+        if constexpr (DW) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<uint2 *>(sm.Zt + sw_off(col, rb + 8 * g + 4 * half, CHB)) =
-              *reinterpret_cast<const uint2 *>(&tt[4 * g]);
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<uint2 *>(sm.Zt + sw_off(col, rb + 8 * g + 4 * half, CHB)) =
+                *reinterpret_cast<const uint2 *>(&tt[4 * g]);
+        }
       }
       deadp |= mn < PMIN;
 
@@ -540,6 +546,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       KL_PROBE(3 + 2 * ps);
       if constexpr (!FIX) dead |= deadp;
     }
+    if constexpr (!DW) continue;   // dWo by kl_dwo_kernel from the stored dZ
     lds_barrier();
     KL_PROBE(6);
     // ---- phase 2: dWo[d][NB] (+)= D3^T[d][tile rows] dZ[tile rows][NB] (wave w: d rows 32w..).
@@ -622,6 +629,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   if constexpr (!FIX) {
     if (__ballot(dead) != 0ull && lane == 0)
       __hip_atomic_fetch_or(p.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    klsum += klc;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) klsum += __shfl_xor(klsum, off);
     if (lane == 0) sm.red_loss[w] = (double)klsum;
@@ -670,37 +678,158 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   }
 }
 
-template <int D, int CPOL>
+template <int D, int CPOL, bool DW>
 __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
   __shared__ __attribute__((aligned(16))) bf16_t Wt[kl_nb<D>() * D];
   __shared__ __attribute__((aligned(16))) MainSmem<kl_nb<D>()> sm;
-  kl_slice<D, false, CPOL>(p, blockIdx.x, Wt, sm);
+  kl_slice<D, false, CPOL, DW>(p, blockIdx.x, Wt, sm);
 }
 
 // The exact-clip correction: a small persistent grid (FIXG blocks) that leaves at once when the
 // step saw no p < 1e-7, and otherwise walks the slices.
 constexpr int FIXG = 64;
-template <int D>
+template <int D, bool DW>
 __global__ __launch_bounds__(NTH) void kl_fix_kernel(KlP p) {
   __shared__ __attribute__((aligned(16))) bf16_t Wt[kl_nb<D>() * D];
   __shared__ __attribute__((aligned(16))) MainSmem<kl_nb<D>()> sm;
   if (__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
   for (int sl = blockIdx.x; sl < p.nsl; sl += gridDim.x) {
-    kl_slice<D, true>(p, sl, Wt, sm);
+    kl_slice<D, true, 0, DW>(p, sl, Wt, sm);
     __syncthreads();  // LDS reuse by the next slice
   }
 }
 
-__global__ __launch_bounds__(256) void kl_tsum_kernel(const float *__restrict__ Mt, int V, float *__restrict__ tsum) {
-  __shared__ float red[4];
-  const float *row = Mt + (int64_t)blockIdx.x * V;
-  float s = 0.f;
-  for (int j = threadIdx.x; j < V; j += 256) s += __builtin_amdgcn_fmed3f(row[j], PMIN, 1.f);
+// ---------------------------------------------------------------- dWo from the stored dZ
+// Many row tiles (the full-mode regulariser: all |V| identity rows): dWo[d][V] = D3^T[d][rows]
+// dZ[rows][V] as its own product, after the main (and fix) pass stored the final bf16 dZ — the
+// product the main pass folded into every row tile as a per-tile read-modify-write of the block's
+// slice (~16 of ~38 us per 512-row tile, tools/micro/kl_probe_full.hip).  One block per 96-column
+// slice and 256 rows of d owns its dWo tile over the whole K = rows reduction in registers: no
+// partial sums, one store per element, the same MFMA k order for every element (deterministic).
+// dZ chunks of DW_KC rows x 96 columns are staged global -> registers -> LDS as raw rows (each
+// thread 3 x 16 B per chunk, written one chunk ahead of its use; two LDS stages, one barrier per
+// chunk); B fragments by ds_read_b64_tr_b16 (column n, 4 consecutive rows per read; the 192-B rows
+// put 4 consecutive rows on disjoint banks); A fragments from the packed D3^T image (1 KB per wave
+// load), one chunk ahead in registers.  Wave w owns 32 rows of d x the 3 column tiles.
+// (Staged by LDS-DMA instead, the compiler waits for every outstanding copy — vmcnt(0) — before
+// each chunk's LDS reads, so nothing stays in flight.)
+constexpr int DW_NB = 96, DW_KC = 128;
+template <int D, bool V8>
+__global__ __launch_bounds__(NTH) void kl_dwo_kernel(KlP p) {
+  constexpr int NB = DW_NB, NJ = NB / 32, KC = DW_KC, KS = KC / 16;
+  constexpr int PPR = NB / 8;                    // 16-B pieces per chunk row
+  constexpr int NPC = KC * PPR / NTH;            // pieces per thread per chunk
+  static_assert(KC * PPR % NTH == 0, "kl_dwo_kernel: whole pieces per thread");
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) bf16_t Zs[2][KC * NB];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
+  const int n0 = blockIdx.x * NB, V = p.V;
+  const int wt = blockIdx.y * 8 + w;              // this wave's 32 rows of d
+  const bool active = wt * 32 < D;                // (d = 128: waves 4-7 only copy)
+  const int nch = (p.rows + KC - 1) / KC;
+  const __amdgpu_buffer_rsrc_t zr =
+      __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)p.rows * (uint32_t)V * 2u, 0x00020000);
+  // piece q = tid + NTH u of chunk c = (row q / PPR, 16 B e = q % PPR); rows past `rows` read 0
+  // (beyond the descriptor's range), columns past V read the next row (finite; not stored)
+  v4u stg[NPC];
+  auto gload = [&](int c) {
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    for (int u = 0; u < NPC; ++u) {
+      const int q = tid + NTH * u, r = q / PPR, e = q % PPR;
+      const uint32_t off = (uint32_t)(((c * KC + r) * V + n0) * 2 + e * 16);
+      if constexpr (V8) {
+        stg[u] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(zr, off, 0, 0));
+      } else {   // 4-B aligned rows (V even)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) stg[u][h] = __builtin_amdgcn_raw_buffer_load_b32(zr, off + 4 * h, 0, 0);
+      }
+    }
+  };
+  auto swrite = [&](int st) {
+#pragma unroll
+    for (int u = 0; u < NPC; ++u) *reinterpret_cast<v4u *>(Zs[st] + (tid + NTH * u) * 8) = stg[u];
+  };
+  // A fragment (k step ks of chunk c): packed D3^T, clamped to the last k step (its dZ rows are 0)
+  const bf16_t *abase = p.D3tp + ((int64_t)min(wt, D / 32 - 1) * (p.ldt / 16) * 64 + lane) * 8;
+  const int k0 = p.row0 / 16, klast = (p.row0 + p.rows) / 16 - 1;
+  auto load_a = [&](bf16x8_t (&dst)[KS], int c) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      dst[ks] = *reinterpret_cast<const bf16x8_t *>(abase + (int64_t)min(k0 + c * KS + ks, klast) * 512);
+  };
+  f32x16_t acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  bf16x8_t af[2][KS];
+  gload(0);
+  load_a(af[0], 0);
+  swrite(0);
+  gload(1);
+  lds_barrier();
+  // chunk c: stage st = c & 1.  Write chunk c + 1 (loaded one chunk ago) into the other stage, load
+  // chunk c + 2 and chunk c + 1's A fragments, multiply chunk c, barrier.
+  auto body = [&](bf16x8_t (&cur)[KS], bf16x8_t (&nxt)[KS], int c, const int st) {
+    // unconditional (past the last chunk: zeros / clamped fragments, never read) so the compiler's
+    // counted waits for `cur` and the staged pieces stay exact (a branch merges them to the minimum)
+    swrite(st ^ 1);
+    gload(c + 2);
+    load_a(nxt, c + 1);
+    if (active) {
+      const bf16_t *Zc = Zs[st];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const bf16_t *tb = Zc + (ks * 16 + 8 * half + ((lane >> 2) & 3)) * NB + j * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)tb);
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)(tb + 4 * NB));
+          const bf16x8_t b = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[ks], b, acc[j], 0, 0, 0);
+        }
+    }
+    lds_barrier();   // chunk c + 1 written; chunk c read (its stage is rewritten next)
+  };
+  int c = 0;
+  for (; c + 1 < nch; c += 2) {
+    body(af[0], af[1], c, 0);
+    body(af[1], af[0], c + 1, 1);
+  }
+  if (c < nch) body(af[0], af[1], c, 0);
+  if (!active) return;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int gc = n0 + j * 32 + (lane & 31);
+    if (gc < V) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) p.gW[(int64_t)(wt * 32 + acc_row(r, lane)) * V + gc] = acc[j][r];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void kl_tsum_kernel(const float *__restrict__ Mt, int V, float *__restrict__ tsum) {
+  __shared__ float red[2][4];
+  const float *row = Mt + (int64_t)blockIdx.x * V;
+  float s = 0.f, c = 0.f;
+  for (int j = threadIdx.x; j < V; j += 256) {
+    const float t = __builtin_amdgcn_fmed3f(row[j], PMIN, 1.f);
+    s += t;
+    c = fmaf(t, __logf(t), c);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off);
+    c += __shfl_xor(c, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = s;
+    red[1][threadIdx.x >> 6] = c;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) tsum[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (threadIdx.x == 0)
+    reinterpret_cast<float2 *>(tsum)[blockIdx.x] =
+        make_float2((red[0][0] + red[0][1]) + (red[0][2] + red[0][3]), (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]));
 }
 
 }  // namespace
@@ -769,19 +898,35 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
   p.flag = (uint32_t *)(p.part_d + pn);
   hipStream_t s = as_stream(stream);
   const dim3 gs((unsigned)p.nsl), gm((unsigned)p.nsl);
+  // many row tiles (full mode): dWo from the stored dZ by kl_dwo_kernel (even V: 4-B aligned rows);
+  // one tile (the sampled regulariser): in the main pass, from its LDS dZ^T tile
+  const bool dw_sep = a->rows > TR && a->V % 2 == 0;
 #define KL_LAUNCH(DD)                                                                                          \
   if (a->d == DD) {                                                                                          \
     hipLaunchKernelGGL((kl_stats_kernel<DD>), gs, dim3(NTH), 0, s, p);                                      \
     CC_LAUNCH_CHECK("kl_stats_kernel");                                                                      \
     hipLaunchKernelGGL(kl_merge_kernel, dim3((unsigned)cdiv(a->rows, 4)), dim3(256), 0, s, p);              \
     CC_LAUNCH_CHECK("kl_merge_kernel");                                                                      \
-    if (a->rows > TR)                                                                                        \
-      hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT>), gm, dim3(NTH), 0, s, p);                          \
-    else                                                                                                     \
-      hipLaunchKernelGGL((kl_main_kernel<DD, 0>), gm, dim3(NTH), 0, s, p);                                   \
-    CC_LAUNCH_CHECK("kl_main_kernel");                                                                       \
-    hipLaunchKernelGGL((kl_fix_kernel<DD>), dim3(FIXG), dim3(NTH), 0, s, p);                                \
-    CC_LAUNCH_CHECK("kl_fix_kernel");                                                                        \
+    if (dw_sep) {                                                                                            \
+      hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, false>), gm, dim3(NTH), 0, s, p);                   \
+      CC_LAUNCH_CHECK("kl_main_kernel");                                                                     \
+      hipLaunchKernelGGL((kl_fix_kernel<DD, false>), dim3(FIXG), dim3(NTH), 0, s, p);                       \
+      CC_LAUNCH_CHECK("kl_fix_kernel");                                                                      \
+      const dim3 gd((unsigned)cdiv(a->V, DW_NB), (unsigned)(DD > 256 ? DD / 256 : 1));                     \
+      if (a->V % 8 == 0)                                                                                     \
+        hipLaunchKernelGGL((kl_dwo_kernel<DD, true>), gd, dim3(NTH), 0, s, p);                               \
+      else                                                                                                   \
+        hipLaunchKernelGGL((kl_dwo_kernel<DD, false>), gd, dim3(NTH), 0, s, p);                              \
+      CC_LAUNCH_CHECK("kl_dwo_kernel");                                                                      \
+    } else {                                                                                                 \
+      if (a->rows > TR)                                                                                      \
+        hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, true>), gm, dim3(NTH), 0, s, p);                  \
+      else                                                                                                   \
+        hipLaunchKernelGGL((kl_main_kernel<DD, 0, true>), gm, dim3(NTH), 0, s, p);                           \
+      CC_LAUNCH_CHECK("kl_main_kernel");                                                                     \
+      hipLaunchKernelGGL((kl_fix_kernel<DD, true>), dim3(FIXG), dim3(NTH), 0, s, p);                        \
+      CC_LAUNCH_CHECK("kl_fix_kernel");                                                                      \
+    }                                                                                                        \
   }
   KL_LAUNCH(256)
   KL_LAUNCH(128)

@@ -388,7 +388,7 @@ class Trainer:
             self.Z2 = torch.zeros(self.Breg, V, **f32)
         if self.fused_reg:
             lo, hi = self.reg_rows
-            self.tsum = torch.zeros(hi - lo, **f32)       # clipped M~ row sums, once (static M~)
+            self.tsum = torch.zeros(hi - lo, 2, **f32)    # per M~ row {sum t, sum t ln t} (t clipped), once
             L.call('cc_kl_tsum', L.ptr(data.y_reg), hi - lo, V, L.ptr(self.tsum), L.stream_ptr())
             self.kl_ws = torch.zeros(int(L.lib().cc_dec_kl_ws_size(self.Breg, V)) // 4 + 4, **f32)
             self.kl_part = torch.zeros(max(int(L.lib().cc_dec_kl_blocks(V)), 1), device=self.dev,
@@ -800,7 +800,7 @@ class Trainer:
             ka = L.DecKlArgs(d=d, V=V, rows=Br, ldt=R, row0=B, D3p=L.ptr(self.D3p), D3tp=L.ptr(self.D3tp),
                              Wo=self.w('decoder_for_reg/reconstruct/kernel'),
                              bo=self.pf('decoder_for_reg/reconstruct/bias'),
-                             Mt=self.data.y_reg.data_ptr() - lo * V * 4, tsum=self.tsum.data_ptr() - lo * 4,
+                             Mt=self.data.y_reg.data_ptr() - lo * V * 4, tsum=self.tsum.data_ptr() - lo * 8,
                              mt_bytes=hi * V * 4, mt_lo=lo, reg_idx=L.ptr(self.reg_idx),
                              scale=float(self.kl_row_scale), dZ=L.ptr(self.dZout[B:]),
                              gW=self.gp('decoder_for_reg/reconstruct/kernel'),
@@ -1143,6 +1143,7 @@ class Trainer:
             events[1].record()
         elif self.graphs is not None:
             self.graphs[1].replay()
+            self.noise_ready = self.prefetch   # (captured with the next step's F in the launch)
         else:
             self.apply_adam(stream)
         self.pending_rest = True

@@ -460,12 +460,13 @@ int cc_dec_softmax_kl_q(const float *Z2, int32_t B, int32_t V, const float *y_re
  * no fp32 logits in HBM (model.py:64/98, train.py:85; TF 2.5 clip semantics).  Row r of the
  * regulariser rows is row row0 + r of the packed D3 images D3p ([R/32][d/16][64][8], act6p) and
  * D3tp ([d/32][ldt/16][64][8], act6tp); Wo [d][V] bf16 is read in place; Mt + card * V is the
- * M~ row of card reg_idx[r] (-1: padding row, contributes nothing); tsum[card] =
- * sum_j clip(M~[card, j], 1e-7, 1) (cc_kl_tsum), indexed like Mt.  Outputs: dZ [rows][V] bf16
- * (= scale * ([p >= 1e-7](-t) + p * sum_{p>=1e-7} t), for the dX product), gW [d][V], gb [V],
- * loss_partials (cc_dec_kl_blocks(V) doubles) and, with ticket, loss_out = sum * loss_scale.
- * d in {128, 256, 512} (96-column slices, 64 at d = 512), rows % 32 == 0.  ws:
- * cc_dec_kl_ws_size(rows, V) bytes, 16-B aligned. */
+ * M~ row of card reg_idx[r] (-1: padding row, contributes nothing); tsum[2 card], tsum[2 card + 1]
+ * = sum_j t, sum_j t ln t over t = clip(M~[card, j], 1e-7, 1) (cc_kl_tsum), indexed like Mt.
+ * Outputs: dZ [rows][V] bf16 (= scale * ([p >= 1e-7](-t) + p * sum_{p>=1e-7} t), for the dX
+ * product), gW [d][V], gb [V], loss_partials (cc_dec_kl_blocks(V) doubles) and, with ticket,
+ * loss_out = sum * loss_scale.  d in {128, 256, 512} (96-column slices, 64 at d = 512), rows % 32
+ * == 0.  More than 512 rows (the full-mode regulariser) with V even: gW = D3^T dZ by a separate
+ * launch over the stored dZ.  ws: cc_dec_kl_ws_size(rows, V) bytes, 16-B aligned. */
 typedef struct cc_dec_kl_args {
   int32_t d, V, rows, ldt, row0;
   const void *D3p, *D3tp, *Wo;
@@ -484,7 +485,8 @@ typedef struct cc_dec_kl_args {
 size_t cc_dec_kl_ws_size(int32_t rows, int32_t V);
 int32_t cc_dec_kl_blocks(int32_t V);
 int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream);
-/* tsum[i] = sum_j clip(Mt[i * V + j], 1e-7, 1) for the n rows of Mt (once per M~) */
+/* Row constants of the n rows of Mt (once per M~), t = clip(Mt[i * V + j], 1e-7, 1):
+ * tsum[2i] = sum_j t, tsum[2i + 1] = sum_j t ln t (the KL's target-entropy part) */
 int cc_kl_tsum(const float *Mt, int32_t n, int32_t V, float *tsum, void *stream);
 /* Decoder dX split-K on bf16 MFMA with an LDS-DMA pipeline (dxgemm.hip): partials[s][M][N] =
  * A[M][k in split s] . B[N][k in split s]^T, A [M][lda] (dZ), B [N][ldb] (Wo as [d][V]), splits of

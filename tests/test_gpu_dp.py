@@ -296,7 +296,7 @@ RCCL_SHAPES = {'bench': dict(V=2500, d=256, B=128, C=1024, dtype='bf16'),
                'c5': dict(V=2500, d=1024, B=128, C=1024, dtype='fp8')}
 
 
-def _rccl_trainer(shape, reg, force_dp, reg_shard):
+def _rccl_trainer(shape, reg, force_dp, reg_shard, **kw):
     from cubecobrarecommender_amd.layout import Layout
     from cubecobrarecommender_amd.trainer import DeviceDataset, TrainConfig, Trainer
     from oracle import model_ref
@@ -304,7 +304,7 @@ def _rccl_trainer(shape, reg, force_dp, reg_shard):
     lists, Mt, ns = problem(5, S['C'], S['V'], (20, 40, 80))
     P = model_ref.init_params(S['V'], S['d'], seed=3, bias_std=0.01)
     cfg = TrainConfig(V=S['V'], d=S['d'], batch_size=S['B'], reg=reg, dtype=S['dtype'], seed=3,
-                      force_dp=force_dp, reg_shard=reg_shard)
+                      force_dp=force_dp, reg_shard=reg_shard, **kw)
     data = DeviceDataset(lists, S['V'], y_mtx=Mt.astype(np.float32) if reg else None, neg_sampler=ns)
     tr = Trainer(cfg, data, params_flat=Layout(S['V'], S['d']).pack(P))
     tr.set_epoch_permutations(np.random.default_rng(4).permutation(S['C'])[None, :])

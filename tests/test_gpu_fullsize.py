@@ -119,6 +119,50 @@ def test_bench_configuration_matches_oracle(reg):
     assert tr.graphs is not None and tr.graphs[4] is not None
 
 
+@pytest.mark.timeout(900)
+def test_full_mode_at_full_size():
+    """configs[2]'s |V| x |V| regulariser at the size it runs (VERDICT r3, Missing 3): reg_mode='full'
+    at |V| = 22,000, d = 256, B = 512, bf16 — the KL over all 22,000 identity rows (43 row tiles x
+    230 column slices), their dZ, the separate dWo launch over the stored dZ, dX on the tall tiles —
+    against model_ref(mode='bf16') with reg_idx = arange(V), y_reg = the device M~, one step.
+    (README.md:27, generator.py:23-24, model.py:98,122.)"""
+    from cubecobrarecommender_amd.adjacency import adjacency_normalised_gpu
+    V, d, B, C = 22000, 256, 512, 2048
+    indptr_t, indices_t = synthetic_cubes(C, V, seed=20250301, device='cuda')
+    indptr, indices = np.asarray(indptr_t), np.asarray(indices_t)
+    ns = neg_sampler_from_csr(indptr, indices, V)
+    lists = _csr_lists(indptr, indices)
+    y_mtx = adjacency_normalised_gpu(indptr, indices, V, device='cuda')
+    data = DeviceDataset(csr=(indptr, indices), num_cards=V, neg_sampler=ns, y_mtx=y_mtx, device='cuda')
+    cfg = TrainConfig(V=V, d=d, batch_size=B, reg=0.1, dtype='bf16', seed=1234, reg_mode='full')
+    tr = Trainer(cfg, data, params_flat=glorot_flat(V, d, seed=42))
+    assert tr.full_reg and tr.fused_reg and tr.Breg >= V
+    perm = np.random.default_rng(99).permutation(C).astype(np.int32)
+    tr.set_epoch_permutations(perm[None, :])
+    lay = Layout(V, d)
+    P = lay.unpack(tr.standard(tr.params))
+    tr.forward_backward()
+    torch.cuda.synchronize()
+    got_l = tr.losses()
+    g = lay.unpack(tr.standard(tr.grads))
+    cubes = [lists[c] for c in perm[:B]]
+    oxs, oys, _, _ = noise_ref.philox_noise_batch(cubes, noise_ref.cdf_of(ns), ns, cfg.seed, 0, with_reg=False)
+    Mt = y_mtx.cpu().numpy()
+    del tr, data, y_mtx
+    torch.cuda.empty_cache()
+    losses, grads = model_ref.train_forward_backward(P, oxs, oys, V, d, reg=0.1, reg_idx=np.arange(V), y_reg=Mt,
+                                                     mode='bf16')
+    errs = {'loss/bce': abs(got_l['bce'] - losses['bce']) / losses['bce'],
+            'loss/kl': abs(got_l['kl'] - losses['kl']) / losses['kl']}
+    errs.update({k: rel_err(g[k], grads[k]) for k in grads})
+    record_errors('full_mode_22k', 0, errs)
+    # the KL is a sum of 484 M terms in fp32 per-lane partials (fp64 across blocks); gradients as
+    # test_gpu_train.py's full-mode bar (TOL['bf16_full'])
+    assert errs['loss/bce'] < LOSS_TOL_BF16 and errs['loss/kl'] < 2e-5, errs
+    bad = {k: v for k, v in errs.items() if not k.startswith('loss/') and not v < 2e-2}
+    assert not bad, bad
+
+
 @pytest.mark.parametrize('reg', [0.0, 0.1])
 def test_reference_architecture_fp32(reg):
     """The reference model (d = 512, fp32 everywhere; model.py:27-33, 58-64) at the reference

@@ -389,12 +389,14 @@ def test_step_many_multi_graph_matches_single_steps(reg):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize('dtype,V,d,B', [('fp32', 700, 64, 32), ('bf16', 1500, 256, 128), ('bf16', 1500, 512, 128)])
+@pytest.mark.parametrize('dtype,V,d,B', [('fp32', 700, 64, 32), ('bf16', 1500, 256, 128), ('bf16', 1500, 512, 128),
+                                         ('bf16', 5000, 256, 256)])
 def test_full_mode_regulariser_matches_oracle(dtype, V, d, B):
     """reg_mode='full' (README.md:27: KL(M~, D2(E(I))) over ALL |V| identity rows every step):
     the rows are static (x row = {card}, reg_idx = card, padded rows masked), their W1 gradient is
     added row by row (cc_embed_identity_add), the KL is the mean over V rows — against the oracle
-    with reg_idx = arange(V), y_reg = M~, for two steps with Adam between them."""
+    with reg_idx = arange(V), y_reg = M~, for two steps with Adam between them.  bf16: dWo by the
+    separate kl_dwo_kernel over the stored dZ (V = 1,500: 4-B staged rows; V = 5,000: 16-B)."""
     C = 4 * B
     lists, Mt, ns = problem(5, C, V, (20, 40, 80))
     P = model_ref.init_params(V, d, seed=5, bias_std=0.01)

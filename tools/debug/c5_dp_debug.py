@@ -1,5 +1,7 @@
-"""Debug: the fp8 (config 5 class) data-parallel step over a 1-rank RCCL group vs the one-process
-step, tensor by tensor (gradients after step 0, parameters / moments after each step)."""
+"""Debug: the fp8 (config 5 class) step, tensor by tensor, after each step (gradients after step 0,
+parameters / moments after each).  Trainers: 'dp' = the data-parallel step over a 1-rank RCCL group,
+'one' = the one-process step (both captured at step 2), 'bceq0' = 'one' without the BCE product's
+MX-FP8 epilogue, all checked against 'eager' (one-process, never captured)."""
 import os
 import sys
 
@@ -15,27 +17,34 @@ from tests.test_gpu_dp import _rccl_trainer  # noqa: E402
 
 shape = sys.argv[1] if len(sys.argv) > 1 else 'c5'
 reg = float(sys.argv[2]) if len(sys.argv) > 2 else 0.1
-shard = bool(int(sys.argv[3])) if len(sys.argv) > 3 else True
-a = _rccl_trainer(shape, reg, True, shard)
-b = _rccl_trainer(shape, reg, False, False)
-for step in range(3):
-    for t in (a, b):
-        if t is a:
-            t._dp_call(None)
-        else:
-            t.forward_backward()
-            t.apply()
+tr = {'eager': _rccl_trainer(shape, reg, False, False),
+      'one': _rccl_trainer(shape, reg, False, False),
+      'bceq0': _rccl_trainer(shape, reg, False, False, mx8_bce_q=False),
+      'dp': _rccl_trainer(shape, reg, True, True)}
+for step in range(6):
+    if step == 2:
+        for k in ('one', 'bceq0', 'dp'):
+            tr[k].capture()
+    for k, t in tr.items():
+        t.step()
+        t.flush()
         torch.cuda.synchronize()
-    print('step', step, 'losses', a.losses(), b.losses())
-    for what in ('grads', 'params', 'm', 'v'):
-        ua = a.layout.unpack(a.standard(getattr(a, what)))
-        ub = b.layout.unpack(b.standard(getattr(b, what)))
-        bad = []
-        for k in ua:
-            x, y = ua[k].astype(np.float64), ub[k].astype(np.float64)
-            nx, ny = np.isnan(x).sum(), np.isnan(y).sum()
-            e = np.linalg.norm(x - y) / max(np.linalg.norm(y), 1e-30)
-            if nx or ny or e > 1e-6:
-                bad.append((k, int(nx), int(ny), float(e), float(np.abs(x).max()), float(np.abs(y).max())))
-        print(' ', what, 'mismatches:', bad if bad else 'none')
+    print('step', step, 'losses', {k: t.losses()['loss'] for k, t in tr.items()})
+    ref = tr['eager']
+    for name in ('one', 'bceq0', 'dp'):
+        a = tr[name]
+        for what in ('grads', 'params', 'm', 'v'):
+            if what == 'grads' and step >= 2:
+                continue
+            ua = a.std_layout.unpack(a.standard(getattr(a, what)))
+            ub = ref.std_layout.unpack(ref.standard(getattr(ref, what)))
+            bad = []
+            for k in ua:
+                x, y = ua[k].astype(np.float64), ub[k].astype(np.float64)
+                nx, ny = np.isnan(x).sum(), np.isnan(y).sum()
+                e = np.linalg.norm(x - y) / max(np.linalg.norm(y), 1e-30)
+                if nx or ny or e > 1e-6:
+                    i = int(np.argmax(np.abs(x - y).ravel()))
+                    bad.append((k, int(nx), int(ny), float(e), float(np.abs(x).max()), float(np.abs(y).max()), i))
+            print(' ', name, what, 'mismatches:', bad if bad else 'none')
 dist.destroy_process_group()

@@ -29,7 +29,7 @@ for st in "$@"; do
   i=$((i + 1)); kind=${st%%:*}; arg=${st#*:}; [ "$arg" == "$st" ] && arg=""
   case $kind in
     tests)
-      timeout -k 10 1000 python -u -m pytest ${arg:-tests} -m gpu -x -v --timeout 300 --timeout-method thread \
+      eval "timeout -k 10 1000 python -u -m pytest ${arg:-tests} -m gpu -x -v --timeout 300 --timeout-method thread" \
         > "$O/tests_$i.log" 2>&1; rc=$?; tail -3 "$O/tests_$i.log"; [ $rc -ne 0 ] && { grep -E "FAIL|Error|error" "$O/tests_$i.log" | tail -20; exit $rc; } ;;
     bench)
       timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-recommend $arg > "$O/bench_$i.log" 2>&1 \
