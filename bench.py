@@ -497,7 +497,7 @@ def main():
     ktimes = kernel_profile(tr, step)
     dp_report = dp_profile(tr, step) if dp else None
     if rank != 0:
-        if world > 1:
+        if dp:
             import torch.distributed as dist
             dist.destroy_process_group()
         return
@@ -542,7 +542,7 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         out['cpu_baseline'] = cpu_baseline(args)
     print(json.dumps(out), flush=True)
-    if world > 1:
+    if dp:
         import torch.distributed as dist
         dist.destroy_process_group()
 

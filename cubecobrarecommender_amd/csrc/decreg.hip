@@ -707,8 +707,8 @@ __global__ __launch_bounds__(NTH) void kl_fix_kernel(KlP p) {
 // slice and 256 rows of d owns its dWo tile over the whole K = rows reduction in registers: no
 // partial sums, one store per element, the same MFMA k order for every element (deterministic).
 // dZ chunks of DW_KC rows x 96 columns are staged global -> registers -> LDS as raw rows (each
-// thread 3 x 16 B per chunk, written one chunk ahead of its use; two LDS stages, one barrier per
-// chunk); B fragments by ds_read_b64_tr_b16 (column n, 4 consecutive rows per read; the 192-B rows
+// thread 3 x 16 B per chunk, loaded three chunks and written one chunk ahead of its use; two LDS
+// stages, one barrier per chunk); B fragments by ds_read_b64_tr_b16 (column n, 4 consecutive rows per read; the 192-B rows
 // put 4 consecutive rows on disjoint banks); A fragments from the packed D3^T image (1 KB per wave
 // load), one chunk ahead in registers.  Wave w owns 32 rows of d x the 3 column tiles.
 // (Staged by LDS-DMA instead, the compiler waits for every outstanding copy — vmcnt(0) — before
@@ -731,8 +731,11 @@ __global__ __launch_bounds__(NTH) void kl_dwo_kernel(KlP p) {
       __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)p.rows * (uint32_t)V * 2u, 0x00020000);
   // piece q = tid + NTH u of chunk c = (row q / PPR, 16 B e = q % PPR); rows past `rows` read 0
   // (beyond the descriptor's range), columns past V read the next row (finite; not stored)
-  v4u stg[NPC];
-  auto gload = [&](int c) {
+  // two register sets: chunk c's pieces are loaded at iteration c - 3 and written to LDS at
+  // iteration c - 1, two chunk times of lead (one chunk time, ~0.7 us, left the HBM latency exposed:
+  // 24 KB in flight per CU, ~2.7 TB/s)
+  v4u stg0[NPC], stg1[NPC];
+  auto gload = [&](v4u (&stg)[NPC], int c) {
 #pragma unroll
     for (int u = 0; u < NPC; ++u) {
       const int q = tid + NTH * u, r = q / PPR, e = q % PPR;
@@ -745,7 +748,7 @@ __global__ __launch_bounds__(NTH) void kl_dwo_kernel(KlP p) {
       }
     }
   };
-  auto swrite = [&](int st) {
+  auto swrite = [&](const v4u (&stg)[NPC], int st) {
 #pragma unroll
     for (int u = 0; u < NPC; ++u) *reinterpret_cast<v4u *>(Zs[st] + (tid + NTH * u) * 8) = stg[u];
   };
@@ -763,19 +766,23 @@ __global__ __launch_bounds__(NTH) void kl_dwo_kernel(KlP p) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
   bf16x8_t af[2][KS];
-  gload(0);
+  gload(stg0, 0);
   load_a(af[0], 0);
-  swrite(0);
-  gload(1);
+  swrite(stg0, 0);
+  gload(stg1, 1);
+  gload(stg0, 2);
   lds_barrier();
-  // chunk c: stage st = c & 1.  Write chunk c + 1 (loaded one chunk ago) into the other stage, load
-  // chunk c + 2 and chunk c + 1's A fragments, multiply chunk c, barrier.
-  auto body = [&](bf16x8_t (&cur)[KS], bf16x8_t (&nxt)[KS], int c, const int st) {
+  // chunk c: stage st = c & 1.  Write chunk c + 1 (register set (c + 1) & 1, loaded two chunks ago)
+  // into the other stage, load chunk c + 3 into that set and chunk c + 1's A fragments, multiply
+  // chunk c, barrier.
+  auto body = [&](bf16x8_t (&cur)[KS], bf16x8_t (&nxt)[KS], v4u (&sw)[NPC], int c, const int st) {
     // unconditional (past the last chunk: zeros / clamped fragments, never read) so the compiler's
     // counted waits for `cur` and the staged pieces stay exact (a branch merges them to the minimum)
-    swrite(st ^ 1);
-    gload(c + 2);
+    // (A before the pieces: waiting for chunk c + 1's A fragments — vmcnt counts in issue order —
+    // must not wait for chunk c + 3's pieces)
+    swrite(sw, st ^ 1);
     load_a(nxt, c + 1);
+    gload(sw, c + 3);
     if (active) {
       const bf16_t *Zc = Zs[st];
 #pragma unroll
@@ -793,10 +800,10 @@ __global__ __launch_bounds__(NTH) void kl_dwo_kernel(KlP p) {
   };
   int c = 0;
   for (; c + 1 < nch; c += 2) {
-    body(af[0], af[1], c, 0);
-    body(af[1], af[0], c + 1, 1);
+    body(af[0], af[1], stg1, c, 0);
+    body(af[1], af[0], stg0, c + 1, 1);
   }
-  if (c < nch) body(af[0], af[1], c, 0);
+  if (c < nch) body(af[0], af[1], stg1, c, 0);
   if (!active) return;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {

@@ -356,8 +356,14 @@ __device__ __forceinline__ void q_body(const QP &p, int q, char *smem) {
         if (p.colsum) {
           csum += dpp_f(csum, 0);
           csum += dpp_f(csum, 1);
-          // two row tiles at most (checked on the host): fl(fl(0 + a) + b) == fl(fl(0 + b) + a)
-          if (cok && rc == 0) atomicAdd(p.colsum + gc, csum);
+          // one row tile: stored; two (checked on the host): added onto the zeros of
+          // colsum_zero_kernel, fl(fl(0 + a) + b) == fl(fl(0 + b) + a)
+          if (cok && rc == 0) {
+            if (p.tiles_m == 1)
+              p.colsum[gc] = csum;
+            else
+              atomicAdd(p.colsum + gc, csum);
+          }
         }
       }
       __syncthreads();   // S is rewritten by the next pass
@@ -501,6 +507,11 @@ bool q_attr() {
   return ok;
 }
 
+__global__ __launch_bounds__(256) void colsum_zero_kernel(float *__restrict__ c, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) c[i] = 0.f;
+}
+
 }  // namespace
 
 extern "C" int cc_gemm_mx8_wide(const cc_gemm_args *g0, const cc_gemm_args *g1, void *stream) {
@@ -553,7 +564,10 @@ extern "C" int cc_gemm_mx8_bce_q(const cc_gemm_args *g, uint8_t *zq, int32_t ldz
   p.ldztq = ldztq;
   CC_REQUIRE(q_attr(), "cc_gemm_mx8_bce_q: dynamic LDS attribute");
   hipStream_t s = as_stream(stream);
-  CC_HIP(hipMemsetAsync(colsum, 0, (size_t)g->N * sizeof(float), s));
+  if (p.tiles_m > 1) {   // (a kernel, not hipMemsetAsync: the same node kind eagerly and in a captured graph)
+    hipLaunchKernelGGL(colsum_zero_kernel, dim3((unsigned)cdiv(g->N, 256)), dim3(256), 0, s, colsum, g->N);
+    CC_LAUNCH_CHECK("colsum_zero_kernel");
+  }
   hipLaunchKernelGGL(mx8_wide_kernel<true>, dim3((unsigned)p.ntiles), dim3(QNT), QLDS_MAX, s, p);
   CC_LAUNCH_CHECK("mx8_wide_kernel<bce>");
   return CC_OK;

@@ -16,7 +16,8 @@
  *     cross the ABI.  cc_last_error_string() gives the calling thread's last message.
  *   - Re-entrant: no global mutable state besides the thread-local error string.
  *   - Deterministic: given (seed, step) every kernel produces bit-identical outputs
- *     run to run (no float atomics on any output).
+ *     run to run (fixed-order reductions; the one float atomic — cc_gemm_mx8_bce_q's bias
+ *     gradient over two 256-row tiles — adds two partials onto zero, which commutes).
  */
 #ifndef CCREC_H
 #define CCREC_H

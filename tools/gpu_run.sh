@@ -16,7 +16,7 @@ export CCREC_PARITY_LOG=$O/parity.jsonl
 i=0
 summ() { python - "$1" <<'PY'
 import json, sys
-d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+d = json.loads([l for l in open(sys.argv[1]).read().strip().splitlines() if l.startswith('{')][-1])
 k = d.get('kernel_us') or {}
 r = d.get('roofline') or {}
 print(round(d['ms_per_step'] * 1e3, 1), 'us/step', d['config']['workload'][:60], '| roof', r.get('tick'),
@@ -39,7 +39,7 @@ for st in "$@"; do
       timeout -k 10 400 python -u bench.py $arg > "$O/bench_$i.log" 2>&1 || { tail -30 "$O/bench_$i.log"; exit 1; }
       summ "$O/bench_$i.log" ;;
     prof)
-      ( export TMPDIR=/tmp; cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof_$i" -o run -- \
+      ( export TMPDIR=/tmp; cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$i" -o run -- \
         python3 "$R/bench.py" --no-cpu-baseline --no-recommend $arg > "$O/prof_$i.log" 2>&1 ) \
         || { tail -30 "$O/prof_$i.log"; exit 1; }
       summ "$O/prof_$i.log" ;;

@@ -29,7 +29,7 @@ int main(int argc, char **argv) {
   (void)hipMalloc(&Wo, (size_t)V * d * 2);
   (void)hipMalloc(&bo, V * 4);
   (void)hipMalloc(&Mt, (size_t)V * V * 4);
-  (void)hipMalloc(&tsum, V * 4);
+  (void)hipMalloc(&tsum, V * 8);
   (void)hipMalloc(&ridx, rows * 4);
   (void)hipMalloc(&dZ, (size_t)rows * V * 2);
   (void)hipMalloc(&gW, (size_t)d * V * 4);
@@ -42,7 +42,7 @@ int main(int argc, char **argv) {
   (void)hipMemset(Wo, 0, (size_t)V * d * 2);
   (void)hipMemset(bo, 0, V * 4);
   (void)hipMemset(Mt, 0, (size_t)V * V * 4);
-  (void)hipMemset(tsum, 0, V * 4);
+  (void)hipMemset(tsum, 0, V * 8);
   (void)hipMemset(tick, 0, 8);
   std::vector<int> h(rows);
   for (int i = 0; i < rows; ++i) h[i] = i < V ? i : -1;
