@@ -101,6 +101,8 @@ SIGNATURES = {
     'cc_gemm_pair': (C.c_int, [C.POINTER(GemmArgs), C.POINTER(GemmArgs), _P]),
     'cc_gemm_mx8_wide': (C.c_int, [C.POINTER(GemmArgs), C.POINTER(GemmArgs), _P]),
     'cc_gemm_mx8_bce_q': (C.c_int, [C.POINTER(GemmArgs), _P, C.c_int32, _P, _P, C.c_int32, _P, _P, _P]),
+    'cc_gemm_mx8_bce_q2': (C.c_int, [C.POINTER(GemmArgs), _P, C.c_int32, _P, _P, C.c_int32, _P, _P,
+                                     C.POINTER(GemmArgs), _P]),
     'cc_gemm_grid': (C.c_int, [_I32, _I32, _P]),
     'cc_splitk_reduce': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     'cc_splitk_reduce_warm': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _I64, _P]),

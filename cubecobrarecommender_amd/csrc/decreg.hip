@@ -389,6 +389,15 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)p.rows * (uint32_t)V * 2u, 0x00020000);
   const float scale = p.scale;
   constexpr int ND2 = (D + 255) / 256;   // phase 2's d tiles of wave w: 32w .. (and 32(w + 8) .. at d = 512)
+  // PF (the main pass with dWo done elsewhere: many row tiles, nothing of phase 2 live): the next
+  // row block's A fragments load right after this block's logits MFMAs, so their L2 / MALL round
+  // trip runs under this block's epilogue instead of heading the next logits phase (tools/micro/
+  // kl_probe_full.hip: ~5 of the ~12 us per 256-row pass were logits waiting on their fragments)
+  constexpr bool PF = !FIX && !DW && D <= 256;
+  // all A fragments first in the memory queue, then M~ (d = 512: a ring of 16; PF: the next block's
+  // first 8 under the epilogue, the other 8 refilled during the MFMAs — 16 would spill)
+  LFrag<D, PF ? 8 : (D / 16 < 16 ? D / 16 : 16)> lf;
+  bool lf_ready = false;
 
   for (int t0 = 0; t0 < p.rows; t0 += TR) {
     const int nt = min(TR, p.rows - t0);
@@ -422,8 +431,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       for (int r = 0; r < 16; ++r) roff[r] = (uint32_t)sm.card[rb + acc_row(r, lane)];
       uint32_t zrow = (uint32_t)((t0 + rb + 4 * half) * V + n0 + (lane & 31));
       asm volatile("" : "+v"(zrow));  // per-pass base of the dZ stores (no hoisted 64-bit addresses)
-      LFrag<D, (D / 16 < 16 ? D / 16 : 16)> lf;  // all A fragments first in the memory queue, then M~ (d = 512: a ring of 16)
-      logits_load(p, (p.row0 + t0 + rb) / 32, lf);
+      if (!PF || !lf_ready) logits_load(p, (p.row0 + t0 + rb) / 32, lf);
       float tv[NJ][16];
       if constexpr (!FIX) {
 #pragma unroll
@@ -437,6 +445,12 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       __builtin_amdgcn_sched_barrier(0);
       f32x16_t acc[NJ];
       logits_mfma(Wt, lf, bias, acc);
+      if constexpr (PF) {   // this wave's next row block: pass 1 of this tile, or pass 0 of the next
+        const int t1 = ps == 0 && 256 + w * 32 < nt ? t0 : t0 + TR;
+        const int rb1 = t1 == t0 ? 256 + w * 32 : w * 32;
+        lf_ready = t1 < p.rows && rb1 < min(TR, p.rows - t1);   // (wave-uniform)
+        if (lf_ready) logits_load(p, (p.row0 + t1 + rb1) / 32, lf);
+      }
       KL_PROBE(2 + 2 * ps);
       bool deadp = false;   // an element of this pass has p < 1e-7
       float mn = 1.f;       // (fast path) the smallest p of the lane's elements

@@ -440,6 +440,19 @@ __global__ __launch_bounds__(QNT) void mx8_wide_pair_kernel(QP p0, QP p1) {
     q_body<false>(p1, xcd_run(blockIdx.x - n0, p1.ntiles * p1.splits), qsmem);
 }
 
+// the BCE product with dZ's MX-FP8 images (problem 0, the first n0 blocks) and an independent
+// STORE product (problem 1: config 5's regulariser logits, which read the same D3 launch's other
+// rows) in one launch: 172 + 172 tiles at B = 512, |V| = 22,000 fill the 256 CUs that either
+// alone leaves a third idle
+__global__ __launch_bounds__(QNT) void mx8_bce_pair_kernel(QP p0, QP p1) {
+  extern __shared__ __attribute__((aligned(1024))) char qsmem[];
+  const int n0 = p0.ntiles;
+  if ((int)blockIdx.x < n0)
+    q_body<true>(p0, xcd_run(blockIdx.x, n0), qsmem);
+  else
+    q_body<false>(p1, xcd_run(blockIdx.x - n0, p1.ntiles * p1.splits), qsmem);
+}
+
 int q_params(const cc_gemm_args *g, QP &p) {
   CC_REQUIRE(g && g->dtype == CC_MX8 && !g->ta && g->tb, "cc_gemm_mx8_wide: MX8 NT only");
   CC_REQUIRE(g->A && g->B && g->a_scale && g->b_scale, "cc_gemm_mx8_wide: null operand");
@@ -503,7 +516,9 @@ bool q_attr() {
                          hipFuncSetAttribute((const void *)mx8_wide_kernel<true>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, QLDS_MAX) == hipSuccess &&
                          hipFuncSetAttribute((const void *)mx8_wide_pair_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, QLDS) == hipSuccess;
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, QLDS) == hipSuccess &&
+                         hipFuncSetAttribute((const void *)mx8_bce_pair_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, QLDS_MAX) == hipSuccess;
   return ok;
 }
 
@@ -543,6 +558,12 @@ extern "C" int cc_gemm_mx8_wide(const cc_gemm_args *g0, const cc_gemm_args *g1, 
 // cc_quant_mx8 of the bf16 dZ / dZ^T (the column sums to fp32 rounding).  g->C / g->Ct optional.
 extern "C" int cc_gemm_mx8_bce_q(const cc_gemm_args *g, uint8_t *zq, int32_t ldzq, uint8_t *zqs, uint8_t *ztq,
                                  int32_t ldztq, uint8_t *ztqs, float *colsum, void *stream) {
+  return cc_gemm_mx8_bce_q2(g, zq, ldzq, zqs, ztq, ldztq, ztqs, colsum, nullptr, stream);
+}
+
+extern "C" int cc_gemm_mx8_bce_q2(const cc_gemm_args *g, uint8_t *zq, int32_t ldzq, uint8_t *zqs, uint8_t *ztq,
+                                  int32_t ldztq, uint8_t *ztqs, float *colsum, const cc_gemm_args *gx,
+                                  void *stream) {
   CC_REQUIRE(g && g->epilogue == CC_EPI_BCE, "cc_gemm_mx8_bce_q: BCE epilogue");
   CC_REQUIRE(zq && zqs && ztq && ztqs && colsum, "cc_gemm_mx8_bce_q: null output");
   CC_REQUIRE(ldzq % 128 == 0 && ldzq >= g->N && ldzq <= (int)cdiv(g->N, QN) * QN && ldztq % 32 == 0 && ldztq >= g->M,
@@ -564,9 +585,20 @@ extern "C" int cc_gemm_mx8_bce_q(const cc_gemm_args *g, uint8_t *zq, int32_t ldz
   p.ldztq = ldztq;
   CC_REQUIRE(q_attr(), "cc_gemm_mx8_bce_q: dynamic LDS attribute");
   hipStream_t s = as_stream(stream);
+  QP p2;
+  if (gx) {
+    if (int rc = q_params(gx, p2)) return rc;
+    CC_REQUIRE(p2.epi != CC_EPI_BCE, "cc_gemm_mx8_bce_q2: the second problem STORE or SPLITK");
+  }
   if (p.tiles_m > 1) {   // (a kernel, not hipMemsetAsync: the same node kind eagerly and in a captured graph)
     hipLaunchKernelGGL(colsum_zero_kernel, dim3((unsigned)cdiv(g->N, 256)), dim3(256), 0, s, colsum, g->N);
     CC_LAUNCH_CHECK("colsum_zero_kernel");
+  }
+  if (gx) {
+    hipLaunchKernelGGL(mx8_bce_pair_kernel, dim3((unsigned)(p.ntiles + p2.ntiles * p2.splits)), dim3(QNT), QLDS_MAX,
+                       s, p, p2);
+    CC_LAUNCH_CHECK("mx8_bce_pair_kernel");
+    return CC_OK;
   }
   hipLaunchKernelGGL(mx8_wide_kernel<true>, dim3((unsigned)p.ntiles), dim3(QNT), QLDS_MAX, s, p);
   CC_LAUNCH_CHECK("mx8_wide_kernel<bce>");

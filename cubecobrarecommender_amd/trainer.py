@@ -48,10 +48,13 @@ class TrainConfig:
     dx_splits: int = 0             # decoder dX K-splits (0: measured default, 32 bf16 / 16 fp8)
     dx_splits_reg: int = 0         # ... of the full-mode regulariser branch (0: 4)
     mx8_bce_q: bool = True         # fp8: the BCE product writes dZ's MX-FP8 images (else quantiser launches)
+    mx8_pair_reg_logits: bool = True   # fp8: the regulariser logits as extra blocks of the BCE product's launch
     graph_steps: int = 8           # one process: consecutive steady-state steps per hipGraph replay (step_many)
     force_dp: bool = False         # one process driving the data-parallel step (a 1-rank process group:
     #                                zero.py's collectives on device tensors; tests and the per-rank DP profile)
     dp_graph: bool = True          # data parallel over RCCL: the whole step (collectives included) as one hipGraph
+    dp_f_in_adam: bool = True      # data parallel: the next step's F as extra blocks of the towers + E1
+    #                                bucket's sharded Adam launch (else its own launch, cc_noise_next)
     reg_mode: str = 'sampled'      # 'sampled': B reg rows per step drawn ∝ neg_sampler (generator.py:47-51);
     #                                'full': all |V| identity rows every step, KL(M~, D2(E(I))) as the
     #                                reference README states the objective (README.md:27)
@@ -386,6 +389,9 @@ class Trainer:
             self.fused_reg = False
         if self.use_reg and not self.fused_reg:
             self.Z2 = torch.zeros(self.Breg, V, **f32)
+        # config 5: the regulariser logits ride in the BCE product's launch (cc_gemm_mx8_bce_q2)
+        self.reg_logits_paired = (self.mx8_bce_q and self.use_reg and not self.fused_reg and self.fused_tower
+                                  and cfg.mx8_pair_reg_logits)
         if self.fused_reg:
             lo, hi = self.reg_rows
             self.tsum = torch.zeros(hi - lo, 2, **f32)    # per M~ row {sum t, sum t ln t} (t clipped), once
@@ -777,8 +783,14 @@ class Trainer:
                            y_bits=L.ptr(self.y_bits), scale=1.0 / (B * V), partials=L.ptr(self.bce_part),
                            loss_out=L.ptr(self.loss_dev), loss_scale=1.0 / (B * V),
                            ticket=L.ptr(self.tickets), launch=False)
-            L.call('cc_gemm_mx8_bce_q', L.C.byref(g), L.ptr(self.dZq), self.Vp, L.ptr(self.dZqs),
-                   L.ptr(self.dZtq[0]), B, L.ptr(self.dZtqs[0]), self.gp('decoder/reconstruct/bias'), s)
+            # + the regulariser branch's logits (independent: the same D3 launch's other rows) as
+            # extra blocks of the same launch, filling the CUs the BCE tiles leave idle
+            g2 = (self._gemm(self.Breg, V, d, **self._dec_fwd(1, B), tb=1,
+                             bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2), launch=False)
+                  if self.reg_logits_paired else None)
+            L.call('cc_gemm_mx8_bce_q2', L.C.byref(g), L.ptr(self.dZq), self.Vp, L.ptr(self.dZqs),
+                   L.ptr(self.dZtq[0]), B, L.ptr(self.dZtqs[0]), self.gp('decoder/reconstruct/bias'),
+                   L.C.byref(g2) if g2 is not None else None, s)
         elif self.fused_tower:   # Wo^T [V][d]: k-contiguous B operand; also writes dZ^T [V][B]
             self._gemm(B, V, d, **self._dec_fwd(0, 0), tb=1,
                        epi=L.CC_EPI_BCE, bias=self.pf('decoder/reconstruct/bias'), C=L.ptr(self.dZout),
@@ -810,7 +822,9 @@ class Trainer:
             L.call('cc_dec_softmax_kl_dw', L.C.byref(ka), s)
             t()
         elif self.use_reg:
-            if self.fused_tower:
+            if self.reg_logits_paired:
+                pass   # in the BCE product's launch above
+            elif self.fused_tower:
                 self._gemm(Br, V, d, **self._dec_fwd(1, B), tb=1,
                            bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2))
             else:
@@ -1072,6 +1086,15 @@ class Trainer:
             L.call('cc_to_bf16', L.ptr(self.params[lo:]), L.ptr(self.shadow[lo:]), hi - lo,
                    L.stream_ptr(stream))
 
+    def adam_noise_range(self, lo, n, g, stream=None):
+        """adam_range + F of the NEXT step in the same launch (cc_adam_noise: F's latency-bound blocks
+        first, the shard's Adam blocks streaming around them) — data parallel, on the bucket whose
+        update starts once this step's backward has released the batch buffers."""
+        cfg = self.cfg
+        L.call('cc_adam_noise', L.ptr(self.params[lo:]), L.ptr(self.m[lo:]), L.ptr(self.v[lo:]), L.ptr(g),
+               L.ptr(self.shadow[lo:]) if self.shadow is not None else None, n, cfg.lr, cfg.beta1,
+               cfg.beta2, cfg.eps, L.C.byref(self._noise_args()), self.batches_per_epoch, L.stream_ptr(stream))
+
     def noise_next(self, stream=None):
         """F of the NEXT step (cc_noise_next: the state advanced as apply_rest will) — data
         parallel: issued after this step's backward, beside the exchange of the last buckets."""
@@ -1086,16 +1109,27 @@ class Trainer:
         return self.sharded
 
     def _dp_call(self, g=None, timing=False):
-        """The sharded step (zero.py) over graph replays of its parts (g) or eager launches."""
-        self._sharded().step(
+        """The sharded step (zero.py) over graph replays of its parts (g) or eager launches.  The next
+        step's F: inside the towers + E1 bucket's sharded Adam launch (dp_f_in_adam; that bucket's
+        update waits for the end of backward, as F must), else its own launch after backward."""
+        sh = self._sharded()
+        fuse_f = self.prefetch_dp and self.cfg.dp_f_in_adam
+        tb = sh.bucket('towers_e1')['gshard'] if fuse_f else None
+
+        def adam_fn(lo, n, gs):
+            if gs is tb:
+                self.adam_noise_range(lo, n, gs)
+            else:
+                self.adam_range(lo, n, gs)
+        sh.step(
             phase_a=g[0].replay if g else self.forward_backward_a,
             phase_b=g[1].replay if g else self.forward_backward_b,
             rest=g[2].replay if g else self.apply_rest,
-            adam_fn=lambda lo, n, gs: self.adam_range(lo, n, gs),
+            adam_fn=adam_fn,
             refresh_fn=lambda lo, hi: self.refresh_range(lo, hi),
             timing=timing,
-            after_b=self.noise_next if self.prefetch_dp else None,
-            hooks=g is None and self._sharded().comm is not None)
+            after_b=self.noise_next if self.prefetch_dp and not fuse_f else None,
+            hooks=g is None and sh.comm is not None)
         self.noise_ready = self.prefetch_dp
 
     def step_dp(self, timing=False, no_comm=False):

@@ -294,6 +294,10 @@ int cc_gemm_mx8_wide(const cc_gemm_args *g0, const cc_gemm_args *g1, void *strea
  * gradient (zeroed here).  g->C / g->Ct (bf16 dZ / dZ^T) optional.  M % 32 == 0, M <= 512. */
 int cc_gemm_mx8_bce_q(const cc_gemm_args *g, uint8_t *zq, int32_t ldzq, uint8_t *zqs, uint8_t *ztq,
                       int32_t ldztq, uint8_t *ztqs, float *colsum, void *stream);
+/* cc_gemm_mx8_bce_q + an independent MX8 STORE / SPLITK product g2 (config 5: the regulariser
+ * branch's logits) as extra blocks of the same launch; g2 = NULL is cc_gemm_mx8_bce_q. */
+int cc_gemm_mx8_bce_q2(const cc_gemm_args *g, uint8_t *zq, int32_t ldzq, uint8_t *zqs, uint8_t *ztq,
+                       int32_t ldztq, uint8_t *ztqs, float *colsum, const cc_gemm_args *g2, void *stream);
 /* workspace bound for cc_gemm's loss partials: ceil(M/64)*ceil(N/64) doubles */
 int cc_gemm_grid(int32_t M, int32_t N, int32_t *tiles);
 

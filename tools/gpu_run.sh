@@ -5,7 +5,7 @@
 #   tests[:<pytest args>]     GPU tests (default: the whole -m gpu suite; args replace 'tests')      -> $O/tests_<i>.log
 #   bench[:<bench.py args>]   one bench line                                   -> $O/bench_<i>.log
 #   prof[:<bench.py args>]    rocprofv3 --kernel-trace --stats of a bench run  -> $O/prof_<i>/
-#   pmc:<COUNTER>[:<args>]    one rocprofv3 --pmc pass of a short bench run    -> $O/pmc_<COUNTER>_<i>/
+#   pmc:<C1,C2,..>[:<args>]   one rocprofv3 --pmc pass of a short bench run    -> $O/pmc_<i>.json (per-kernel averages)
 #   py:<script args>          python -u <script args>                          -> $O/py_<i>.log
 #   cmd:<command>             any command (a built probe binary)               -> $O/cmd_<i>.log
 # Every GPU step runs under its own time limit; the first failing step ends the session.
@@ -45,10 +45,10 @@ for st in "$@"; do
       summ "$O/prof_$i.log" ;;
     pmc)
       c=${arg%%:*}; a=${arg#*:}; [ "$a" == "$arg" ] && a=""
-      ( export TMPDIR=/tmp; cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $c -d "$O/pmc_${c}_$i" -o run -- \
-        python3 "$R/bench.py" --steps 16 --warmup 4 --no-cpu-baseline --no-recommend $a > "$O/pmc_${c}_$i.log" 2>&1 ) \
-        || { tail -30 "$O/pmc_${c}_$i.log"; exit 1; }
-      echo "pmc $c ok" ;;
+      ( export TMPDIR=/tmp; cd /tmp && timeout -s KILL 150 rocprofv3 --pmc ${c//,/ } -d "$O/pmc_$i" -o run -- \
+        python3 "$R/bench.py" --steps 16 --warmup 4 --no-cpu-baseline --no-recommend $a > "$O/pmc_$i.log" 2>&1 ) \
+        || { tail -30 "$O/pmc_$i.log"; exit 1; }
+      python tools/prof_collect.py pmc "$O/pmc_$i" "$O/pmc_$i.json" && echo "pmc $c ok" ;;
     py)
       timeout -k 10 600 python -u $arg > "$O/py_$i.log" 2>&1 || { tail -30 "$O/py_$i.log"; exit 1; }
       tail -15 "$O/py_$i.log" ;;
