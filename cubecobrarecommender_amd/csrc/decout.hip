@@ -184,8 +184,29 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
                                                (uint32_t)((k * V + n0 + 8 * c) * 2), 0, 0, 0);
     }
   }
+  // YS_LATE (DMA, B >= 256: every wave has rows in pass 0): the target words are loaded last and
+  // written to LDS only after pass 0's logits MFMAs, so the first barrier waits for the Wo slice and
+  // the A fragments but not for the 1.5-K strided word loads
+  constexpr bool YS_LATE = DMA && B >= 256;
+  constexpr int NY = (B * NJ + NTH - 1) / NTH;
+  uint32_t yv[NY];
+  auto load_ys = [&]() {
+#pragma unroll
+    for (int q = 0; q < NY; ++q) {
+      const int i = tid + NTH * q, r = min(i / NJ, B - 1), gw = (n0 >> 5) + i % NJ;
+      yv[q] = gw < VW ? p.y_bits[(int64_t)r * VW + gw] : 0u;
+    }
+  };
+  auto store_ys = [&]() {
+#pragma unroll
+    for (int q = 0; q < NY; ++q)
+      if (tid + NTH * q < B * NJ) {  // target words column-tile-major: ys[j][row]
+        const int i = tid + NTH * q;
+        ys[(i % NJ) * B + i / NJ] = yv[q];
+      }
+  };
   {
-    constexpr int NW = NB * CHD / NTH, NY = (B * NJ + NTH - 1) / NTH;
+    constexpr int NW = NB * CHD / NTH;
     // from Wo [d][V]: task = (4 consecutive k, 8 consecutive columns) -> 4 row loads, then 8
     // 8-byte LDS writes (the 4 k of one column are contiguous in the k-contiguous image);
     // columns past V clamp to V - 1
@@ -196,7 +217,6 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     constexpr bool STAGE = !DMA;   // the Wo^T slice through registers (DMA: already in flight)
     v4u wv[fromWo ? 1 : NW];
     v4u w4[NT4][4];
-    uint32_t yv[NY];
     if (!STAGE) {
     } else if (!fromWo) {
 #pragma unroll
@@ -225,11 +245,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         }
       }
     }
-#pragma unroll
-    for (int q = 0; q < NY; ++q) {
-      const int i = tid + NTH * q, r = min(i / NJ, B - 1), gw = (n0 >> 5) + i % NJ;
-      yv[q] = gw < VW ? p.y_bits[(int64_t)r * VW + gw] : 0u;
-    }
+    if (!YS_LATE) load_ys();
     __builtin_amdgcn_sched_barrier(0);
     if (!STAGE) {
     } else if (!fromWo) {
@@ -252,12 +268,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         }
       }
     }
-#pragma unroll
-    for (int q = 0; q < NY; ++q)
-      if (tid + NTH * q < B * NJ) {  // target words column-tile-major: ys[j][row]
-        const int i = tid + NTH * q;
-        ys[(i % NJ) * B + i / NJ] = yv[q];
-      }
+    if (!YS_LATE) store_ys();
   }
 
   // ---- phase 1: logits, BCE, dZ (global + LDS dZ^T), bias-gradient partial, loss.  Wave w owns
@@ -289,11 +300,20 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     cnt_z = 0;
   }
   // LDS-only barrier: __syncthreads would also wait for pass 0's A fragments (vmcnt counts loads).
-  // DMA: the wave's own DMAs (issued after pass 0's A fragments) must have landed first
-  if constexpr (DMA)
+  // DMA: the wave's own DMAs (issued after pass 0's A fragments) must have landed first — and with
+  // YS_LATE only they: the NY target-word loads, issued last, stay in flight
+  if constexpr (YS_LATE) {
+    // (the builtin, not inline asm: the compiler's wait insertion then knows the Wo slice's DMA has
+    // landed and does not wait for every older load, the target words included, at the first LDS
+    // read.  s_waitcnt encoding: vmcnt[3:0], expcnt[6:4] (7: none), lgkmcnt[11:8] (0))
+    static_assert(NY <= 15, "dec_bce_dw_kernel: vmcnt immediate");
+    __builtin_amdgcn_s_waitcnt(7 << 4);
+    __builtin_amdgcn_s_barrier();
+  } else if constexpr (DMA) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else
+  } else {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
   DEC_PROBE(1);
   const float scale = p.scale;
   // dZ and gW through buffer descriptors: a 32-bit byte offset per store instead of a 64-bit
@@ -303,6 +323,9 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 #pragma unroll
   for (int ps = 0; ps < npass; ++ps) {
     if (!RING1 && ps + 1 < npass) load_a(af[(ps + 1) & 1], ps + 1);
+    if constexpr (YS_LATE) {
+      if (ps == 0) load_ys();   // the youngest loads: nothing before pass 0's epilogue waits for them
+    }
     if (ps * 256 + w * 32 >= B) continue;          // wave-uniform: rows beyond B
     f32x16_t acc[NJ];  // starts at the bias (exactly): z = bo + sum_k D3 Wo accumulates in the MFMA
 #pragma unroll
@@ -328,6 +351,12 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
       if (RING1 && kk + NAF < nkk) af[0][kk % NAF] = *reinterpret_cast<const bf16x8_t *>(asrc + (kk + NAF) * astr);
     }
     if (RING1 && ps + 1 < npass) load_a(af[0], ps + 1);   // the next pass's head under this epilogue
+    if constexpr (YS_LATE) {
+      if (ps == 0) {   // (every wave is here: B >= 256)
+        store_ys();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+    }
     DEC_PROBE(2 + 2 * ps);
     if constexpr (SPLIT2) {
       if (ps == npass - 1) {   // this wave reads the Wo slice no more (its fragment reads returned)
