@@ -67,7 +67,7 @@ struct KlP {
   uint32_t mt_bytes;               // extent of Mt from its base (buffer range check)
   int mt_lo;                        // first card whose M~ row is resident
   float *part_m, *part_s, *part_d;  // [rows][nsl]
-  float4 *rowstat;                  // [rows] {m, ln s, S, -}
+  float4 *rowstat;                  // [rows] {m + ln s, -, S, sum t ln t}
   uint32_t *flag;                   // [1] an element with p < 1e-7 was seen this step
 };
 
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256) void kl_merge_kernel(KlP p) {
   if (lane == 0) {
     const int card = p.reg_idx[row];
     const float2 ts = card >= 0 ? reinterpret_cast<const float2 *>(p.tsum)[card] : make_float2(0.f, 0.f);
-    p.rowstat[row] = make_float4(m, __logf(s), ts.x, ts.y);
+    p.rowstat[row] = make_float4(m + __logf(s), 0.f, ts.x, ts.y);   // {m + ln s, -, S, C}: ln p = z - .x
   }
 }
 
@@ -476,7 +476,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const float4 st = rsp[rb + acc_row(r, lane)];
-            const float lp = acc[j][r] - st.x - st.y;  // ln p = z - m - ln s
+            const float lp = acc[j][r] - st.x;  // ln p = z - (m + ln s)
             const float pr = __builtin_amdgcn_exp2f(lp * LOG2E);
             const float tc = __builtin_amdgcn_fmed3f(tv[j][r], PMIN, 1.f);
             klsum = fmaf(-tc, __builtin_amdgcn_fmed3f(lp, LN_PMIN, 0.f), klsum);   // (+ t ln t: rowstat.w)
@@ -495,7 +495,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
             const int lr = rb + acc_row(r, lane);
             const float4 st = rsp[lr];
             const bool live_row = roff[r] < 0x80000000u && valid[j];
-            const float lp = acc[j][r] - st.x - st.y;  // ln p = z - m - ln s
+            const float lp = acc[j][r] - st.x;  // ln p = z - (m + ln s)
             const float pr = __builtin_amdgcn_exp2f(lp * LOG2E);
             const bool live = pr >= PMIN;
             float dz;
@@ -546,7 +546,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
             float a = 0.f;
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
-              const float pr = __builtin_amdgcn_exp2f((acc[j][r] - st.x - st.y) * LOG2E);
+              const float pr = __builtin_amdgcn_exp2f((acc[j][r] - st.x) * LOG2E);
               const bool live_row = roff[r] < 0x80000000u && valid[j];
               a += live_row && !(pr >= PMIN) ? __builtin_amdgcn_fmed3f(tv[j][r], PMIN, 1.f) : 0.f;
             }

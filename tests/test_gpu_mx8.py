@@ -285,6 +285,54 @@ def test_mx8_bce_q_matches_quantiser(M, N, K):
     assert abs(got[5] - ref[5]) <= 1e-9 * abs(ref[5])
 
 
+@pytest.mark.parametrize('M,N,K', [(512, 1000, 1024), (128, 700, 256)])
+def test_mx8_bce_q2_pair_equals_separate_launches(M, N, K):
+    """cc_gemm_mx8_bce_q2 (config 5: the BCE product with the regulariser's logits as extra blocks of
+    the same launch) == cc_gemm_mx8_bce_q and a separate cc_gemm of the second product, bit for bit;
+    M = 512 spans two 256-row tiles (bias gradient added onto a zeroing kernel's zeros), M = 128 one
+    (stored)."""
+    rng = np.random.default_rng(M * 5 + N)
+    qa, sa, _ = _mx8_operand(rng.standard_normal((M, K)).astype(np.float32), K)
+    qb, sb, _ = _mx8_operand(rng.standard_normal((N, K)).astype(np.float32) * 0.05, K)
+    qa2, sa2, _ = _mx8_operand(rng.standard_normal((M, K)).astype(np.float32), K)
+    qb2, sb2, _ = _mx8_operand(rng.standard_normal((N, K)).astype(np.float32) * 0.05, K)
+    bias = torch.from_numpy(rng.standard_normal(N).astype(np.float32) * 0.1).cuda()
+    bias2 = torch.from_numpy(rng.standard_normal(N).astype(np.float32) * 0.1).cuda()
+    bits = torch.from_numpy(rng.integers(0, 2**31, (M, (N + 31) // 32), dtype=np.int64).astype(np.int32)).cuda()
+    Np = (N + 127) // 128 * 128
+
+    def run(paired):
+        u8 = dict(device='cuda', dtype=torch.uint8)
+        part = torch.zeros(4096, device='cuda', dtype=torch.float64)
+        loss = torch.zeros(1, device='cuda', dtype=torch.float64)
+        ticket = torch.zeros(1, device='cuda', dtype=torch.int32)
+        zq, zqs = torch.full((M, Np), 0x55, **u8), torch.full((M, Np // 32), 0x55, **u8)
+        ztq, ztqs = torch.full((N, M), 0x55, **u8), torch.full((N, M // 32), 0x55, **u8)
+        gb = torch.full((N,), 3.0, device='cuda')
+        Z2 = torch.full((M, N), 7.0, device='cuda')
+        g = L.GemmArgs(dtype=L.CC_MX8, ta=0, tb=1, epilogue=L.CC_EPI_BCE, M=M, N=N, K=K, lda=K, ldb=K, ldc=N,
+                       splits=1, A=qa.data_ptr(), B=qb.data_ptr(), bias=bias.data_ptr(), y_bits=bits.data_ptr(),
+                       scale=1.0 / (M * N), loss_partials=part.data_ptr(), ldct=M, loss_out=loss.data_ptr(),
+                       loss_scale=1.0 / (M * N), ticket=ticket.data_ptr(), a_scale=sa.data_ptr(),
+                       b_scale=sb.data_ptr())
+        g2 = L.GemmArgs(dtype=L.CC_MX8, ta=0, tb=1, epilogue=L.CC_EPI_STORE, M=M, N=N, K=K, lda=K, ldb=K, ldc=N,
+                        splits=1, A=qa2.data_ptr(), B=qb2.data_ptr(), bias=bias2.data_ptr(), Cf=Z2.data_ptr(),
+                        a_scale=sa2.data_ptr(), b_scale=sb2.data_ptr())
+        if paired:
+            L.call('cc_gemm_mx8_bce_q2', L.C.byref(g), L.ptr(zq), Np, L.ptr(zqs), L.ptr(ztq), M, L.ptr(ztqs),
+                   L.ptr(gb), L.C.byref(g2), L.stream_ptr())
+        else:
+            L.call('cc_gemm_mx8_bce_q', L.C.byref(g), L.ptr(zq), Np, L.ptr(zqs), L.ptr(ztq), M, L.ptr(ztqs),
+                   L.ptr(gb), L.stream_ptr())
+            L.call('cc_gemm', L.C.byref(g2), L.stream_ptr())
+        torch.cuda.synchronize()
+        assert int(ticket.item()) == 0
+        return zq, zqs, ztq, ztqs, gb, loss, Z2
+
+    for a, b in zip(run(False), run(True)):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize('dtype', ['bf16', 'fp32'])
 @pytest.mark.parametrize('rows,cols,ld_t,ld_r', [(1024, 2200, 1024, 2304), (256, 1000, 256, 1024),
                                                  (100, 257, 128, 384), (130, 64, 256, 128)])
