@@ -3,6 +3,7 @@ GPU, gloo for the collectives) run Trainer.step() — bucketed reduce-scatter ov
 towers' backward, Adam on each rank's shard, all-gathered parameters (zero.py) — eagerly and as
 graph replays, and must match one process training on the concatenated batch."""
 import os
+import queue
 
 import numpy as np
 import pytest
@@ -43,6 +44,8 @@ def _problem(shape):
 
 
 def _worker(rank, port, reg, graphs, q, shape='small', reg_shard=False):
+    import faulthandler
+    faulthandler.dump_traceback_later(170, exit=True)   # a stuck child names where it is stuck
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(W), LOCAL_RANK='0', HSA_ENABLE_IPC_MODE_LEGACY='0')
     try:
@@ -199,6 +202,8 @@ def _bench_trainer(rank, world, batch, reg_shard, fuse_w1_adam=True):
 
 
 def _bench_worker(rank, port, q):
+    import faulthandler
+    faulthandler.dump_traceback_later(170, exit=True)   # a stuck child names where it is stuck
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(W), LOCAL_RANK='0', HSA_ENABLE_IPC_MODE_LEGACY='0')
     try:
@@ -265,8 +270,10 @@ def test_bench_dp_configuration_matches_single_process_and_oracle():
     el = [abs(np.mean([res[r][2][s]['loss'] for r in range(W)]) - want_losses[s]['loss']) / want_losses[s]['loss']
           for s in range(S['steps'])]
     record_errors('bench_dp_vs_single', S['steps'], {'params': ep, 'm': em, **{f'loss{s}': v for s, v in enumerate(el)}})
-    # ~3x the observed (r03p): params 3.8e-5, m 1.5e-3 (Adam moments of ~0 gradients), loss 3e-8
-    assert ep < 1.2e-4 and em < 4.5e-3 and max(el) < 1e-7, (ep, em, el)
+    # ~3x the observed (r03p): params 3.8e-5, m 1.5e-3 (Adam moments of ~0 gradients); loss 1e-7
+    # (r04j: the KL as sum t ln t - sum t ln p, two sums of ~10x the KL's size, in per-lane fp32
+    # partials over the ranks' and the one process's different row groupings)
+    assert ep < 1.2e-4 and em < 4.5e-3 and max(el) < 3e-7, (ep, em, el)
     # the one-process step 0 against the oracle (bf16 operands emulated)
     lists = [indices[indptr[c]:indptr[c + 1]] for c in range(S['C'])]
     B2 = W * S['B']
@@ -313,15 +320,18 @@ def _rccl_trainer(shape, reg, force_dp, reg_shard, **kw):
 
 def _rccl_run(tr, eager=2, graphed=3):
     losses = []
-    for _ in range(eager):
+    for i in range(eager):
         tr.step()
         torch.cuda.synchronize()
         losses.append(tr.losses()['loss'])
+        print(f'rccl step {i} (eager, dp={tr.dp}) loss {losses[-1]}', flush=True)
     tr.capture()
-    for _ in range(graphed):
+    print('rccl captured', flush=True)
+    for i in range(graphed):
         tr.step()
         torch.cuda.synchronize()
         losses.append(tr.losses()['loss'])
+        print(f'rccl step {eager + i} (graph, dp={tr.dp}) loss {losses[-1]}', flush=True)
     tr.flush()
     torch.cuda.synchronize()
     return losses
@@ -329,6 +339,8 @@ def _rccl_run(tr, eager=2, graphed=3):
 
 def _rccl_worker(shape, reg, reg_shard, q):
     os.environ.update(HSA_ENABLE_IPC_MODE_LEGACY='0')
+    import faulthandler
+    faulthandler.dump_traceback_later(150, exit=True)   # a stuck child names where it is stuck
     try:
         import torch.distributed as dist
         torch.cuda.set_device(0)
@@ -364,7 +376,15 @@ def test_rccl_one_rank_dp_step_matches_one_process(shape, reg, reg_shard):
     q = ctx.Queue()
     p = ctx.Process(target=_rccl_worker, args=(shape, reg, reg_shard, q))
     p.start()
-    res = q.get(timeout=280)
+    res = None
+    for _ in range(56):        # (a child that dies without a result fails the test at once)
+        try:
+            res = q.get(timeout=5)
+            break
+        except queue.Empty:
+            if not p.is_alive():
+                break
+    assert res is not None, f'the RCCL worker exited ({p.exitcode}) without a result'
     p.join(60)
     assert res[1] is not None, res[0]
     assert p.exitcode == 0
@@ -402,6 +422,8 @@ def _fp8_trainer(rank, world, batch, reg_shard):
 
 
 def _fp8_worker(rank, port, reg_shard, q):
+    import faulthandler
+    faulthandler.dump_traceback_later(170, exit=True)   # a stuck child names where it is stuck
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(W), LOCAL_RANK='0', HSA_ENABLE_IPC_MODE_LEGACY='0')
     try:
