@@ -1,0 +1,129 @@
+// Keras' compiled metrics=['accuracy'] of the reference's two outputs (train.py:83-88), counted
+// on the device per step when the trainer runs with TrainConfig(metrics=True):
+//   output_1 (sigmoid + binary_crossentropy): binary_accuracy = mean(y == (sigmoid(z) > 0.5)),
+//            counted as y == (z > 0) (sigmoid(z) > 0.5 in fp32 exactly when z > 0, up to the
+//            |z| < 2^-23 rounding band around 0);
+//   output_2 (softmax + kullback_leibler_divergence): categorical_accuracy = mean over rows of
+//            argmax(y_true) == argmax(y_pred), y_true the row's M~ target (argmax precomputed once
+//            per M~ by cc_row_argmax) and argmax(softmax(z)) = argmax(z) (first index on ties, as
+//            tf.argmax).
+// Counts are integers added with one atomic per block: the totals are order-free (deterministic).
+// Off the training step's path (the fused output-layer kernels never store their logits): the
+// trainer recomputes the logits for the metrics with cc_gemm from the same bf16 / fp32 operands.
+#include "common.hpp"
+
+namespace {
+
+constexpr int MT = 256;
+
+// one block per batch row: the row's correct predictions over V columns (32 per target word)
+__global__ __launch_bounds__(MT) void bce_accuracy_kernel(const float *__restrict__ Z, int ldz,
+                                                          const uint32_t *__restrict__ y_bits, int V,
+                                                          unsigned long long *__restrict__ count) {
+  __shared__ unsigned int red[MT / 64];
+  const int row = blockIdx.x, VW = (V + 31) >> 5;
+  const float *z = Z + (int64_t)row * ldz;
+  const uint32_t *y = y_bits + (int64_t)row * VW;
+  unsigned int c = 0;
+  for (int w = threadIdx.x; w < VW; w += MT) {
+    uint32_t pred = 0;
+    const int n = min(32, V - 32 * w);
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i)
+      if (i < n && z[32 * w + i] > 0.f) pred |= 1u << i;
+    const uint32_t valid = n == 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
+    c += __popc(~(pred ^ y[w]) & valid);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int i = 0; i < MT / 64; ++i) t += red[i];
+    atomicAdd(count, t);
+  }
+}
+
+// first index of the row's maximum (NaN-free rows)
+__device__ __forceinline__ void argmax_pair(float &v, int &i, float v2, int i2) {
+  if (v2 > v || (v2 == v && i2 < i)) {
+    v = v2;
+    i = i2;
+  }
+}
+
+__device__ int block_argmax(const float *__restrict__ x, int V) {
+  __shared__ float sv[MT / 64];
+  __shared__ int si[MT / 64];
+  float v = -INFINITY;
+  int idx = 0x7FFFFFFF;
+  for (int j = threadIdx.x; j < V; j += MT) argmax_pair(v, idx, x[j], j);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float v2 = __shfl_xor(v, off);
+    const int i2 = __shfl_xor(idx, off);
+    argmax_pair(v, idx, v2, i2);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sv[threadIdx.x >> 6] = v;
+    si[threadIdx.x >> 6] = idx;
+  }
+  __syncthreads();
+  float bv = sv[0];
+  int bi = si[0];
+  for (int i = 1; i < MT / 64; ++i) argmax_pair(bv, bi, sv[i], si[i]);
+  __syncthreads();
+  return bi;
+}
+
+__global__ __launch_bounds__(MT) void row_argmax_kernel(const float *__restrict__ X, int64_t ld, int V,
+                                                        int32_t *__restrict__ out) {
+  const int a = block_argmax(X + (int64_t)blockIdx.x * ld, V);
+  if (threadIdx.x == 0) out[blockIdx.x] = a;
+}
+
+// rows with reg_idx >= 0 (padding rows are skipped): argmax(z row) == t_argmax[card - t_lo]
+__global__ __launch_bounds__(MT) void cat_accuracy_kernel(const float *__restrict__ Z, int ldz, int V,
+                                                          const int32_t *__restrict__ reg_idx,
+                                                          const int32_t *__restrict__ t_argmax, int t_lo,
+                                                          unsigned long long *__restrict__ count) {
+  const int card = reg_idx[blockIdx.x];
+  if (card < 0) return;   // (block-uniform)
+  const int a = block_argmax(Z + (int64_t)blockIdx.x * ldz, V);
+  if (threadIdx.x == 0) {
+    atomicAdd(count + 1, 1ull);   // rows counted
+    if (a == t_argmax[card - t_lo]) atomicAdd(count, 1ull);
+  }
+}
+
+}  // namespace
+
+extern "C" int cc_bce_accuracy(const float *Z, int32_t ldz, const uint32_t *y_bits, int32_t B, int32_t V,
+                               unsigned long long *count, void *stream) {
+  CC_REQUIRE(Z && y_bits && count && B >= 0 && V > 0 && ldz >= V, "cc_bce_accuracy: args");
+  if (B == 0) return CC_OK;
+  hipLaunchKernelGGL(bce_accuracy_kernel, dim3((unsigned)B), dim3(MT), 0, as_stream(stream), Z, ldz, y_bits, V,
+                     count);
+  CC_LAUNCH_CHECK("bce_accuracy_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_row_argmax(const float *X, int64_t ld, int32_t rows, int32_t V, int32_t *out, void *stream) {
+  CC_REQUIRE(X && out && rows >= 0 && V > 0 && ld >= V, "cc_row_argmax: args");
+  if (rows == 0) return CC_OK;
+  hipLaunchKernelGGL(row_argmax_kernel, dim3((unsigned)rows), dim3(MT), 0, as_stream(stream), X, ld, V, out);
+  CC_LAUNCH_CHECK("row_argmax_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_cat_accuracy(const float *Z, int32_t ldz, int32_t rows, int32_t V, const int32_t *reg_idx,
+                               const int32_t *t_argmax, int32_t t_lo, unsigned long long *count, void *stream) {
+  CC_REQUIRE(Z && reg_idx && t_argmax && count && rows >= 0 && V > 0 && ldz >= V && t_lo >= 0,
+             "cc_cat_accuracy: args");
+  if (rows == 0) return CC_OK;
+  hipLaunchKernelGGL(cat_accuracy_kernel, dim3((unsigned)rows), dim3(MT), 0, as_stream(stream), Z, ldz, V, reg_idx,
+                     t_argmax, t_lo, count);
+  CC_LAUNCH_CHECK("cat_accuracy_kernel");
+  return CC_OK;
+}

@@ -13,7 +13,6 @@ fit runs the device-resident training step (trainer.py) with TF Adam semantics. 
 fallback: every compute call goes through libccrec_hip.so.
 """
 import time
-import warnings
 
 import numpy as np
 import torch
@@ -90,6 +89,7 @@ class CC_Recommender:
         self._m = self._v = None
         self._step = 0
         self._metrics = None
+        self.metrics = []
         self.reg = 0.0
         self.lr = 1e-3
         self.trainer = None
@@ -107,14 +107,15 @@ class CC_Recommender:
             raise ValueError(f'loss must be {list(_LOSSES)} (train.py:85)')
         if float(loss_weights[0]) != 1.0:
             raise ValueError('loss_weights[0] must be 1.0 (train.py:86)')
-        # metrics=['accuracy'] (train.py:87) only reports per-epoch accuracies in Keras' progress
-        # bar; it does not enter the loss, the gradients or the update.  It is accepted for the call
-        # surface and NOT computed (the fused output-layer kernels never materialise the logits)
+        # metrics=['accuracy'] (train.py:87): Keras resolves it per output — binary_accuracy for the
+        # sigmoid/BCE output, categorical_accuracy for the softmax/KL one — and reports their epoch
+        # means; fit() counts both on the device (TrainConfig(metrics=True), metrics.hip).  They do
+        # not enter the loss, the gradients or the update.
+        self.metrics = []
         for mname in (metrics or ()):
-            if mname != 'accuracy':
-                raise ValueError(f'metric {mname!r}: only the reference\'s metrics=[\'accuracy\'] is accepted')
-            warnings.warn("compile(metrics=['accuracy']): accepted, not computed (the reference only "
-                          "logs it; training is unaffected)", stacklevel=2)
+            if mname not in ('accuracy', 'acc'):
+                raise ValueError(f'metric {mname!r}: only the reference\'s metrics=[\'accuracy\'] is implemented')
+            self.metrics = ['accuracy']
         self.reg = float(loss_weights[1])
         self.lr = float(learning_rate)
 
@@ -132,7 +133,8 @@ class CC_Recommender:
                           # supports it (bit-identical to the unfused step,
                           # tests/test_gpu_train.py::test_fused_w1_adam_matches_unfused) — the
                           # configuration bench.py measures
-                          fuse_w1_adam=(world == 1), wo_adam_in_tower=(world == 1))
+                          fuse_w1_adam=(world == 1), wo_adam_in_tower=(world == 1),
+                          metrics=bool(self.metrics))
         tr = Trainer(cfg, generator.data, params_flat=self._current_flat())
         if self._m is not None:
             tr.load_standard(tr.m, self._m)
@@ -164,6 +166,8 @@ class CC_Recommender:
                 torch.distributed.all_reduce(t)
                 l = {'bce': float(t[0]) / world, 'kl': float(t[1]) / world}
                 l['loss'] = l['bce'] + self.reg * l['kl']
+            if tr.acc_counts is not None:   # Keras' history keys of the two outputs' accuracies
+                l.update(tr.take_metrics(steps))
             self.history.append(l)
             # the compiled metrics' Mean accumulators as Keras leaves them after the epoch
             # (reset per epoch; update_state(value, sample_weight=batch)): 'loss' and the first
@@ -172,8 +176,9 @@ class CC_Recommender:
             self._metrics = {'loss': (l['loss'] * n, n), 'output_1_loss': (l['bce'] * n, n)}
             if verbose and rank == 0:
                 dt = time.perf_counter() - t0
+                acc = ''.join(f' - {k}: {l[k]:.4f}' for k in ('output_1_accuracy', 'output_2_accuracy') if k in l)
                 log(f'Epoch {ep + 1}/{epochs} - {steps} steps - {dt:.3f}s - loss: {l["loss"]:.6f} '
-                    f'- bce: {l["bce"]:.6f} - kl: {l["kl"]:.6f} - {steps * cfg.batch_size * world / dt:.0f} cubes/s')
+                    f'- bce: {l["bce"]:.6f} - kl: {l["kl"]:.6f}{acc} - {steps * cfg.batch_size * world / dt:.0f} cubes/s')
 
         tr.flush()
         if getattr(tr, 'sharded', None) is not None:   # data parallel: m, v are sharded — gather

@@ -55,6 +55,9 @@ class TrainConfig:
     dp_graph: bool = True          # data parallel over RCCL: the whole step (collectives included) as one hipGraph
     dp_f_in_adam: bool = True      # data parallel: the next step's F as extra blocks of the towers + E1
     #                                bucket's sharded Adam launch (else its own launch, cc_noise_next)
+    metrics: bool = False          # Keras metrics=['accuracy'] (train.py:87): each step counts output 1's
+    #                                binary and output 2's categorical accuracy on the device from logits
+    #                                recomputed for the purpose (metrics.hip; take_metrics() per epoch)
     reg_mode: str = 'sampled'      # 'sampled': B reg rows per step drawn ∝ neg_sampler (generator.py:47-51);
     #                                'full': all |V| identity rows every step, KL(M~, D2(E(I))) as the
     #                                reference README states the objective (README.md:27)
@@ -401,6 +404,16 @@ class Trainer:
                                        dtype=torch.float64)
         if self.full_reg:
             self._init_full_rows()
+        # metrics=['accuracy']: {output 1 correct, output 2 correct, output 2 rows} summed on the device
+        self.acc_counts = None
+        if cfg.metrics:
+            self.acc_counts = torch.zeros(3, device=self.dev, dtype=torch.int64)
+            self.Z1m = torch.zeros(B, V, **f32)
+            if self.use_reg:
+                self.Z2m = self.Z2 if self.Z2 is not None else torch.zeros(self.Breg, V, **f32)
+                lo, hi = self.reg_rows       # argmax of every resident M~ row (y_true), once
+                self.t_argmax = torch.zeros(hi - lo, device=self.dev, dtype=torch.int32)
+                L.call('cc_row_argmax', L.ptr(data.y_reg), V, hi - lo, V, L.ptr(self.t_argmax), L.stream_ptr())
         # F for the next step in the Adam launch (cc_adam_noise): Adam is HBM-bound, F latency-
         # bound; F then leaves the forward's critical path.  noise_ready: the batch buffers
         # already hold the batch the next forward_backward consumes.
@@ -847,6 +860,8 @@ class Trainer:
                 L.call('cc_transpose', self.dtype, L.ptr(self.dZout[B:]), Br, V, L.ptr(self.dZt[1]), s)
             ss = self._fork()
             L.call('cc_reduce_loss', L.ptr(self.kl_part), Br, self.kl_loss_scale, L.ptr(self.loss_dev[1:]), ss)
+        if self.acc_counts is not None:
+            self._metrics_step(s)
         # ---- backward through the output layers and decoder towers.  The output layers' dW
         # (side stream) and dX -> towers (this stream) only share read-only inputs.
         for k, (pre, (r0, r1)) in enumerate(branches):
@@ -954,6 +969,37 @@ class Trainer:
             return dict(A=L.ptr(self.D3tq[:, r0:]), lda=R, B=L.ptr(self.dZtq[k]), ldb=nr, dtype=L.CC_MX8,
                         a_scale=L.ptr(self.D3tqs[:, r0 // 32:]), b_scale=L.ptr(self.dZtqs[k]))
         return dict(A=L.ptr(self.D3t[:, r0:]), lda=R, B=L.ptr(self.dZt[k]), ldb=nr)
+
+    def _metrics_step(self, s):
+        """Keras metrics=['accuracy'] of this step (train.py:87): both outputs' logits recomputed from
+        the operands the step used (D3 and the output layers' bf16 / fp32 weights) into fp32, then
+        output 1's binary accuracy against the noised targets and output 2's categorical accuracy
+        against the M~ rows' argmax (metrics.hip).  Off the training arithmetic."""
+        cfg, V, d, B = self.cfg, self.cfg.V, self.cfg.d, self.cfg.batch_size
+        self._gemm(B, V, d, L.ptr(self.D3), d, self.w('decoder/reconstruct/kernel'), V,
+                   bias=self.pf('decoder/reconstruct/bias'), Cf=L.ptr(self.Z1m), stream=s)
+        L.call('cc_bce_accuracy', L.ptr(self.Z1m), V, L.ptr(self.y_bits), B, V, L.ptr(self.acc_counts), s)
+        if self.use_reg:
+            Br = self.Breg
+            self._gemm(Br, V, d, L.ptr(self.D3[B:]), d, self.w('decoder_for_reg/reconstruct/kernel'), V,
+                       bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2m), stream=s)
+            L.call('cc_cat_accuracy', L.ptr(self.Z2m), V, Br, V, L.ptr(self.reg_idx), L.ptr(self.t_argmax),
+                   self.reg_rows[0], L.ptr(self.acc_counts[1:]), s)
+
+    def take_metrics(self, steps):
+        """{'output_1_accuracy', ['output_2_accuracy']} over the steps since the last call (Keras'
+        per-epoch Mean of binary / categorical accuracy) and reset the device counts.  Data
+        parallel: the counts are summed over the ranks first."""
+        c = self.acc_counts.clone()
+        self.acc_counts.zero_()
+        if self.dp:
+            torch.distributed.all_reduce(c)
+        c = c.cpu().numpy()
+        n1 = float(steps) * self.cfg.batch_size * self.cfg.world * self.cfg.V
+        out = {'output_1_accuracy': float(c[0]) / n1}
+        if self.use_reg:
+            out['output_2_accuracy'] = float(c[1]) / max(float(c[2]), 1.0)
+        return out
 
     def forward_backward_b(self, stream=None):
         """Towers backward (both branches' rows together through the shared encoder) and the E1

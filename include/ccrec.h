@@ -493,6 +493,20 @@ int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream);
 /* Row constants of the n rows of Mt (once per M~), t = clip(Mt[i * V + j], 1e-7, 1):
  * tsum[2i] = sum_j t, tsum[2i + 1] = sum_j t ln t (the KL's target-entropy part) */
 int cc_kl_tsum(const float *Mt, int32_t n, int32_t V, float *tsum, void *stream);
+
+/* ----------------------------------------------------------------------------------
+ * Keras metrics=['accuracy'] of the two outputs (train.py:83-88; metrics.hip), counted on the device
+ * (integer atomics: order-free totals).  Z: fp32 logits [rows][ldz].
+ * cc_bce_accuracy: count += #{(r, j) : (Z[r][j] > 0) == y(r, j)} over B rows x V (binary_accuracy of
+ *   the sigmoid output: sigmoid(z) > 0.5 <=> z > 0); y_bits [B][ceil(V/32)] as cc_dec_bce_dw's.
+ * cc_row_argmax: out[r] = first index of the maximum of X[r][0..V) (tf.argmax).
+ * cc_cat_accuracy: for the rows with reg_idx[r] >= 0: count[1] += 1 and count[0] += [argmax Z[r] ==
+ *   t_argmax[reg_idx[r] - t_lo]] (categorical_accuracy of the softmax output vs the M~ row). */
+int cc_bce_accuracy(const float *Z, int32_t ldz, const uint32_t *y_bits, int32_t B, int32_t V,
+                    unsigned long long *count, void *stream);
+int cc_row_argmax(const float *X, int64_t ld, int32_t rows, int32_t V, int32_t *out, void *stream);
+int cc_cat_accuracy(const float *Z, int32_t ldz, int32_t rows, int32_t V, const int32_t *reg_idx,
+                    const int32_t *t_argmax, int32_t t_lo, unsigned long long *count, void *stream);
 /* Decoder dX split-K on bf16 MFMA with an LDS-DMA pipeline (dxgemm.hip): partials[s][M][N] =
  * A[M][k in split s] . B[N][k in split s]^T, A [M][lda] (dZ), B [N][ldb] (Wo as [d][V]), splits of
  * ceil64(ceil(K / splits)) — the same partials (and split boundaries) as cc_gemm's EPI_SPLITK NT

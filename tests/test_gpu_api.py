@@ -86,6 +86,9 @@ def test_fit_save_load_recommend(tmp_path):
     model.fit(gen, epochs=4, verbose=0)
     h = [x['loss'] for x in model.history]
     assert h[-1] < h[0], h
+    # metrics=['accuracy']: Keras' per-output history keys, fractions in [0, 1]
+    for x in model.history:
+        assert 0.0 <= x['output_1_accuracy'] <= 1.0 and 0.0 <= x['output_2_accuracy'] <= 1.0, x
     dest = str(tmp_path / 'ml_files' / 'recommender')
     model.save(dest, save_format='tf')
     m2 = load_model(dest)

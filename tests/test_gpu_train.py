@@ -447,3 +447,53 @@ def test_fused_regulariser_clip_fix_path(V, B, d):
     _assert_within({k: e[k] for k in ('loss/kl', 'decoder_for_reg/reconstruct/kernel',
                                       'decoder_for_reg/reconstruct/bias', 'decoder_for_reg/decoded_3/kernel',
                                       'encoder/encoded_1/kernel')}, TOL['bf16'], 0)
+
+
+@pytest.mark.parametrize('dtype,reg,mode', [('bf16', 0.1, 'sampled'), ('fp32', 0.1, 'sampled'),
+                                            ('bf16', 0.1, 'full'), ('bf16', 0.0, 'sampled')])
+def test_accuracy_metrics_match_torch(dtype, reg, mode):
+    """TrainConfig(metrics=True) — compile(metrics=['accuracy']) (train.py:87): output 1's binary
+    accuracy (z > 0 vs the noised target bits) and output 2's categorical accuracy (argmax of the
+    logits vs argmax of the M~ row) counted on the device == the same counts from torch fp32 logits
+    of the step's own operands (D3, the bf16 / fp32 output-layer weights), over two steps."""
+    V, d, B, C = 2500, 256, 128, 1024
+    lists, Mt, ns = problem(21, C, V, (20, 40, 80))
+    P = model_ref.init_params(V, d, seed=21, bias_std=0.01)
+    lay = Layout(V, d)
+    cfg = TrainConfig(V=V, d=d, batch_size=B, reg=reg, dtype=dtype, seed=21, metrics=True, reg_mode=mode)
+    Mt32 = Mt.astype(np.float32)
+    tr = Trainer(cfg, DeviceDataset(lists, V, y_mtx=Mt32 if reg > 0 else None, neg_sampler=ns),
+                 params_flat=lay.pack(P))
+    tr.set_epoch_permutation(np.random.default_rng(21).permutation(C).astype(np.int32))
+    t_am = torch.from_numpy(np.argmax(Mt32, axis=1)).cuda()
+    want = np.zeros(3)
+    for _ in range(2):
+        tr.forward_backward()
+        torch.cuda.synchronize()
+        flat = (tr.shadow if tr.shadow is not None else tr.params).float()
+        D3 = tr.D3.float()
+
+        def logits(pre, rows):
+            o = lay.offset(pre + '/reconstruct/kernel')
+            ob = lay.offset(pre + '/reconstruct/bias')
+            return D3[rows] @ flat[o:o + d * V].view(d, V) + tr.params[ob:ob + V]
+        z1 = logits('decoder', slice(0, B))
+        yb = tr.y_bits[:B].to(torch.int64) & 0xFFFFFFFF
+        y = ((yb.unsqueeze(-1) >> torch.arange(32, device='cuda')) & 1).reshape(B, -1)[:, :V].bool()
+        want[0] += float(((z1 > 0) == y).sum())
+        if reg > 0:
+            idx = tr.reg_idx[:tr.Breg].long()
+            live = idx >= 0
+            z2 = logits('decoder_for_reg', slice(B, B + tr.Breg))[live]
+            want[1] += float((torch.argmax(z2, dim=1) == t_am[idx[live]]).sum())
+            want[2] += float(live.sum())
+        tr.apply()
+    torch.cuda.synchronize()
+    got = tr.acc_counts.cpu().numpy().astype(np.float64)
+    # logits within a rounding of 0 may fall either side between cc_gemm's and torch's summation
+    # orders: a few elements at most
+    assert abs(got[0] - want[0]) <= 1e-5 * 2 * B * V, (got, want)
+    assert got[2] == want[2] and abs(got[1] - want[1]) <= 2, (got, want)
+    m = tr.take_metrics(2)
+    assert abs(m['output_1_accuracy'] - got[0] / (2 * B * V)) < 1e-12 and tr.acc_counts.sum().item() == 0
+    assert ('output_2_accuracy' in m) == (reg > 0)
