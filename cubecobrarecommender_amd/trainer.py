@@ -479,6 +479,7 @@ class Trainer:
         self.batches_per_epoch = max(1, data.C // (B * cfg.world))   # generator.py:36 (__len__)
         self.graphs = None
         self.g_multi, self.multi_n, self.multi_acc = None, 0, None   # capture(): step_many's graph
+        self.g_multi_sizes = {}      # capture(): step_many's graphs by step count (graph_steps and halves)
         self.g_dp = self.g_dp_nocomm = None   # capture(): the whole data-parallel step (RCCL inside)
         self.sharded = None
         self.pending_rest = False    # one process: step k's counters/transposes run at the head
@@ -1250,15 +1251,16 @@ class Trainer:
         step() launches them; the device counters advance inside): the ~6-9 us boundary between
         two graph replays is paid once per graph_steps steps.  loss_acc: a [2] fp64 device tensor
         that accumulates every step's (bce, kl) — it must be the tensor capture() was given."""
-        gm = self.g_multi
         while n > 0:
-            if (gm is not None and n >= self.multi_n and self._steady()
-                    and (loss_acc is None) == (self.multi_acc is None)
+            # the largest captured multi-step graph that fits (graph_steps, then halves of it: a
+            # remainder of n replays in log2 graphs, not step by step)
+            m = max((k for k in self.g_multi_sizes if k <= n), default=0)
+            if (m > 0 and self._steady() and (loss_acc is None) == (self.multi_acc is None)
                     and (loss_acc is None or loss_acc is self.multi_acc)):
-                gm.replay()
+                self.g_multi_sizes[m].replay()
                 self.pending_rest = True
                 self.noise_ready = self.prefetch
-                n -= self.multi_n
+                n -= m
                 continue
             self.step()
             if loss_acc is not None:
@@ -1317,17 +1319,22 @@ class Trainer:
                 self.apply_rest(defer=True)
                 self.forward_backward()
                 self.apply_adam()
-        self.g_multi, self.multi_n, self.multi_acc = None, 0, None
-        if not self.dp and self.cfg.graph_steps > 1:   # step_many: graph_steps whole steps
-            self.g_multi = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_multi):
-                for _ in range(self.cfg.graph_steps):
-                    self.noise_ready = self.prefetch
-                    self.apply_rest(defer=True)
-                    self.forward_backward()
-                    self.apply_adam()
-                    if loss_acc is not None:
-                        loss_acc += self.loss_dev
+        self.g_multi, self.multi_n, self.multi_acc, self.g_multi_sizes = None, 0, None, {}
+        if not self.dp and self.cfg.graph_steps > 1:   # step_many: graph_steps whole steps (and
+            m = self.cfg.graph_steps                    # graphs of its halves, for remainders)
+            while m > 1:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(m):
+                        self.noise_ready = self.prefetch
+                        self.apply_rest(defer=True)
+                        self.forward_backward()
+                        self.apply_adam()
+                        if loss_acc is not None:
+                            loss_acc += self.loss_dev
+                self.g_multi_sizes[m] = g
+                m //= 2
+            self.g_multi = self.g_multi_sizes[self.cfg.graph_steps]
             self.multi_n, self.multi_acc = self.cfg.graph_steps, loss_acc
         torch.cuda.synchronize()
         self.state.copy_(saved)

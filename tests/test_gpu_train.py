@@ -364,7 +364,7 @@ def test_fused_w1_adam_matches_unfused(reg):
 
 @pytest.mark.parametrize('reg', [0.0, 0.1])
 def test_step_many_multi_graph_matches_single_steps(reg):
-    """step_many — graph_steps (here 3) whole steps per captured graph replay, the loss
+    """step_many — graph_steps (here 4; remainders by the graphs of its halves) whole steps per captured graph replay, the loss
     accumulated inside the graph — gives bit-identical parameters, moments, shadow, device
     counters and accumulated losses to the same number of single step() calls (bench.py's
     configuration: fused W1 / Wo Adam placement)."""
@@ -374,14 +374,14 @@ def test_step_many_multi_graph_matches_single_steps(reg):
         P = model_ref.init_params(2500, 256, seed=13, bias_std=0.01)
         lay = Layout(2500, 256)
         cfg = TrainConfig(V=2500, d=256, batch_size=128, reg=reg, dtype='bf16', seed=13, fuse_w1_adam=True,
-                          wo_adam_in_tower=True, graph_steps=3 if multi else 1)
+                          wo_adam_in_tower=True, graph_steps=4 if multi else 1)
         tr = Trainer(cfg, DeviceDataset(lists, 2500, y_mtx=Mt.astype(np.float32) if reg > 0 else None,
                                         neg_sampler=ns), params_flat=lay.pack(P))
         tr.set_epoch_permutation(np.random.default_rng(13).permutation(1024).astype(np.int32))
         acc = torch.zeros(2, dtype=torch.float64, device='cuda')
         tr.capture(loss_acc=acc)
         assert (tr.g_multi is not None) == multi
-        tr.step_many(11, loss_acc=acc)   # 1 single (reaching the steady state) + 3 x 3 + 1
+        tr.step_many(11, loss_acc=acc)   # 1 single (reaching the steady state) + 4 + 4 + 2 (the half graph)
         tr.flush()
         torch.cuda.synchronize()
         out[multi] = (tr.params.cpu(), tr.m.cpu(), tr.v.cpu(), tr.shadow.cpu(), tr.state.cpu(), acc.cpu())
