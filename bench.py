@@ -39,6 +39,8 @@ def parse():
     ap.add_argument('--reg-mode', default='sampled', choices=('sampled', 'full'),
                     help="sampled: B reg rows per step drawn from neg_sampler (generator.py:47-51); "
                          "full: all |V| identity rows every step (README.md:27, the |V|x|V| MFMA path)")
+    ap.add_argument('--dz-pad', type=int, default=1,
+                    help='the fused D1 kernel\'s dZ rows at a 64-element pitch (TrainConfig.dz_pad)')
     ap.add_argument('--force-dp', action='store_true',
                     help='one GPU driving the data-parallel step through a 1-rank RCCL process group '
                          '(the per-rank kernel and exchange sequence the N-GPU run executes)')
@@ -440,6 +442,7 @@ def main():
     cfg = TrainConfig(V=V, d=d, batch_size=B, reg=args.reg, dtype=args.dtype, seed=1234,
                       rank=rank, world=world, reg_shard=reg_shard, reg_mode=args.reg_mode,
                       force_dp=args.force_dp,
+                      dz_pad=bool(args.dz_pad),
                       fuse_w1_adam=True,   # one process: W1's Adam in its gradient kernel, and (BCE
                       wo_adam_in_tower=True)   # only) Wo's in the tower backward launch (parity:
     #                                        tests/test_gpu_train.py::test_fused_w1_adam_matches_unfused)

@@ -113,6 +113,8 @@ SIGNATURES = {
     'cc_quant_mx8_both': (C.c_int, [C.c_int32, _P, C.c_int32, C.c_int32, C.c_int32, _P, C.c_int32, _P, _P, C.c_int32, _P, _P]),
     'cc_dec_bce_fused': (C.c_int, [_I32, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     'cc_dec_bce_dw': (C.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _F64, _P, _P]),
+    'cc_dec_bce_dw_ld': (C.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _P,
+                                   _P, _F64, _P, _P]),
     'cc_dec_bce_dw_blocks': (_I32, [_I32]),
     'cc_dec_softmax_kl_fused': (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _F32, _P, _P, _P]),
     'cc_reduce_loss': (C.c_int, [_P, _I32, _F64, _P, _P]),

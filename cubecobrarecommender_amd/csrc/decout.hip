@@ -73,6 +73,7 @@ struct DecOutP {
   double loss_scale;
   float scale;
   int V, ldt;
+  int ldz;                 // dZ row pitch (elements, >= V; a multiple of 64 keeps every dZ row 128-B aligned)
 };
 
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
@@ -319,7 +320,8 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   // dZ and gW through buffer descriptors: a 32-bit byte offset per store instead of a 64-bit
   // address (dZ = B x V x 2 B and gW = d x V x 4 B stay below 4 GB: checked on the host)
   const __amdgpu_buffer_rsrc_t dz_rs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)B * (uint32_t)V * 2u, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)B * (uint32_t)p.ldz * 2u, 0x00020000);
+  const int LZ = p.ldz;
 #pragma unroll
   for (int ps = 0; ps < npass; ++ps) {
     if (!RING1 && ps + 1 < npass) load_a(af[(ps + 1) & 1], ps + 1);
@@ -386,7 +388,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         // multiplied (<= 2^16) and one log2 per column taken: the log is a quarter-rate
         // instruction; summed log2 scaled by ln 2 at the end
         // store offsets: the lane part in a VGPR, the row part (r) as the scalar soffset
-        const uint32_t zv = 2u * (uint32_t)((rb + 4 * half) * V + n0 + col);
+        const uint32_t zv = 2u * (uint32_t)((rb + 4 * half) * LZ + n0 + col);
         f32x2_t lprod = {1.f, 1.f}, rs2 = {0.f, 0.f}, cs2 = {0.f, 0.f};  // even / odd rows: packed math
         // the 16 rows' target words: 4 runs of 4 consecutive rows -> 4 LDS reads of 16 B
         uint4 yw[4];
@@ -426,7 +428,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
           for (int e = 0; e < 2; ++e) {
             const int r = r2 + e;
             __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(e ? pk >> 16 : pk), dz_rs, zv,
-                                                  2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), DEC_DZ_CPOL);
+                                                  2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * LZ), DEC_DZ_CPOL);
           }
         }
         lsum += __builtin_amdgcn_logf(lprod[0] * lprod[1]);
@@ -702,11 +704,12 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 
 }  // namespace
 
-extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const void *D3p,
-                             const void *D3tp, const void *WoT, const void *Wo,
-                             const float *bo, int32_t B, int32_t d, int32_t V, const uint32_t *y_bits,
-                             void *dZ, float *gW, float *gb, double *loss_partials, double *loss_out,
-                             double loss_scale, uint32_t *ticket, void *stream) {
+extern "C" int cc_dec_bce_dw_ld(const void *D3, const void *D3t, int32_t ldt, const void *D3p,
+                                const void *D3tp, const void *WoT, const void *Wo,
+                                const float *bo, int32_t B, int32_t d, int32_t V, const uint32_t *y_bits,
+                                void *dZ, int32_t ldz, float *gW, float *gb, double *loss_partials,
+                                double *loss_out, double loss_scale, uint32_t *ticket, void *stream) {
+  CC_REQUIRE(ldz >= V && (int64_t)B * ldz * 2 <= 0xFFFFFFFFll, "cc_dec_bce_dw: ldz >= V, dZ below 4 GB");
   CC_REQUIRE(D3 && D3t && (WoT || Wo) && bo && y_bits && dZ && gW && gb && loss_partials,
              "cc_dec_bce_dw: null pointer");
   CC_REQUIRE(B == 128 || B == 256 || B == 512, "cc_dec_bce_dw: B must be 128, 256 or 512");
@@ -737,6 +740,7 @@ extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const
   p.scale = 1.0f / ((float)B * (float)V);
   p.V = V;
   p.ldt = ldt;
+  p.ldz = ldz;
   const dim3 grid((unsigned)cdiv(V, d <= 256 ? nb_of<256>() : nb_of<512>())), block(NTH);
   hipStream_t s = as_stream(stream);
   // the DMA staging: Wo read in place with every row segment 16-B aligned (V % 8 == 0), the
@@ -756,6 +760,15 @@ extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const
 #undef DO_LAUNCH
   CC_LAUNCH_CHECK("dec_bce_dw_kernel");
   return CC_OK;
+}
+
+extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const void *D3p,
+                             const void *D3tp, const void *WoT, const void *Wo,
+                             const float *bo, int32_t B, int32_t d, int32_t V, const uint32_t *y_bits,
+                             void *dZ, float *gW, float *gb, double *loss_partials, double *loss_out,
+                             double loss_scale, uint32_t *ticket, void *stream) {
+  return cc_dec_bce_dw_ld(D3, D3t, ldt, D3p, D3tp, WoT, Wo, bo, B, d, V, y_bits, dZ, V, gW, gb, loss_partials,
+                          loss_out, loss_scale, ticket, stream);
 }
 
 // an upper bound over every d (the narrowest slice)

@@ -55,6 +55,7 @@ class TrainConfig:
     dp_graph: bool = True          # data parallel over RCCL: the whole step (collectives included) as one hipGraph
     dp_f_in_adam: bool = True      # data parallel: the next step's F as extra blocks of the towers + E1
     #                                bucket's sharded Adam launch (else its own launch, cc_noise_next)
+    dz_pad: bool = True            # the fused D1 kernel's dZ rows at a 64-element pitch (whole cache lines)
     metrics: bool = False          # Keras metrics=['accuracy'] (train.py:87): each step counts output 1's
     #                                binary and output 2's categorical accuracy on the device from logits
     #                                recomputed for the purpose (metrics.hip; take_metrics() per epoch)
@@ -311,6 +312,16 @@ class Trainer:
         # D1 output layer fused (logits + BCE + dZ + dWo, csrc/decout.hip) where its shape fits
         self.fused_out = (self.dtype == L.CC_BF16 and self.fused_tower and not self.mx8 and d in (128, 256, 512)
                           and B in (128, 256, 512))
+        # the fused D1 kernel's dZ rows at a pitch of whole 64-element (128-B) groups: at |V| = 22,000
+        # the natural pitch (44,000 B) starts every other row mid-line, so a wave's 64-B row segments
+        # straddle lines shared with the next row / the next 96-column slice; the dX product reads
+        # dZ at the padded pitch (measured r04u: 154.0 / 154.2 -> 153.3 / 152.5 us/step, FETCH_SIZE
+        # of the kernel unchanged)
+        self.dz1_ld = V
+        self.dZ1 = None
+        if self.fused_out:
+            self.dz1_ld = -(-V // 64) * 64 if cfg.dz_pad else V
+            self.dZ1 = torch.zeros(B, self.dz1_ld, **T)
         self.gPre1T = torch.zeros(d, self.RP, **T) if self.embed_mfma else None
         if self.mx8 and not self.fused_tower:
             raise ValueError('fp8 needs the fused towers (fused_tower=True, B % 32 == 0)')
@@ -783,12 +794,12 @@ class Trainer:
                    L.ptr(self.D3tqs), None, s)
         t = self._tick('dec_bce_fwd')
         if self.fused_out:     # logits + BCE + dZ + dWo/dbo in one pass (csrc/decout.hip)
-            L.call('cc_dec_bce_dw', L.ptr(self.D3), L.ptr(self.D3t), R,
+            L.call('cc_dec_bce_dw_ld', L.ptr(self.D3), L.ptr(self.D3t), R,
                    L.ptr(self.D3p) if self.D3p is not None else None,
                    L.ptr(self.D3tp) if self.D3p is not None else None, None,
                    self.w('decoder/reconstruct/kernel'),   # Wo [d][V]: slices transposed in LDS
-                   self.pf('decoder/reconstruct/bias'), B, d, V, L.ptr(self.y_bits), L.ptr(self.dZout),
-                   self.gp('decoder/reconstruct/kernel'), self.gp('decoder/reconstruct/bias'),
+                   self.pf('decoder/reconstruct/bias'), B, d, V, L.ptr(self.y_bits), L.ptr(self.dZ1),
+                   self.dz1_ld, self.gp('decoder/reconstruct/kernel'), self.gp('decoder/reconstruct/bias'),
                    L.ptr(self.bce_part), L.ptr(self.loss_dev), 1.0 / (B * V), L.ptr(self.tickets), s)
             self._fire('hook_out')     # dWo / dbo of the D1 output layer final
         elif self.mx8_bce_q:   # config 5: the BCE epilogue writes dZ's MX-FP8 images + the bias grad
@@ -941,9 +952,10 @@ class Trainer:
         """Decoder dX split-K partials into split_buf: the LDS-DMA pipelined kernel (dxgemm.hip)
         on the bf16 shapes it takes, else cc_gemm's register-staged NT path (same partials)."""
         d, V = self.cfg.d, self.cfg.V
+        A, lda = self._dz_of(r0)
         if (self.dx_glds and not self.mx8 and nr % 128 == 0 and d % 128 == 0 and V % 8 == 0
                 and dx_splitk_fits(nr, V, d)):
-            L.call('cc_gemm_dx_splitk', L.ptr(self.dZout[r0:]), V, self.w(pre + '/reconstruct/kernel'), V,
+            L.call('cc_gemm_dx_splitk', L.ptr(A), lda, self.w(pre + '/reconstruct/kernel'), V,
                    nr, d, V, splits, L.ptr(self.split_buf), s)
         else:
             L.call('cc_gemm', L.C.byref(gx), s)
@@ -962,7 +974,14 @@ class Trainer:
         if self.mx8:
             return dict(A=L.ptr(self.dZq[r0:]), lda=self.Vp, B=L.ptr(self.Wo8[k]), ldb=self.Vp,
                         dtype=L.CC_MX8, a_scale=L.ptr(self.dZqs[r0:]), b_scale=L.ptr(self.Wo8s[k]))
-        return dict(A=L.ptr(self.dZout[r0:]), lda=V, B=self.w(pre + '/reconstruct/kernel'), ldb=V)
+        A, lda = self._dz_of(r0)
+        return dict(A=L.ptr(A), lda=lda, B=self.w(pre + '/reconstruct/kernel'), ldb=V)
+
+    def _dz_of(self, r0):
+        """dZ of the branch starting at row r0 and its row pitch (the fused D1 kernel's own buffer)."""
+        if r0 == 0 and self.dZ1 is not None:
+            return self.dZ1, self.dz1_ld
+        return self.dZout[r0:], self.cfg.V
 
     def _dec_dw(self, k, r0):
         R, nr = self.R, self.branch_rows()[k]

@@ -448,6 +448,13 @@ int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const void *D3p,
                   int32_t B, int32_t d, int32_t V, const uint32_t *y_bits, void *dZ, float *gW,
                   float *gb, double *loss_partials, double *loss_out, double loss_scale,
                   uint32_t *ticket, void *stream);
+/* cc_dec_bce_dw with dZ's row pitch ldz (>= V; a multiple of 64 keeps every dZ row 128-B aligned, so
+ * no cache line of dZ is written in parts by two output slices or two rows: no partial-line
+ * read-modify-write). */
+int cc_dec_bce_dw_ld(const void *D3, const void *D3t, int32_t ldt, const void *D3p, const void *D3tp,
+                     const void *WoT, const void *Wo, const float *bo, int32_t B, int32_t d, int32_t V,
+                     const uint32_t *y_bits, void *dZ, int32_t ldz, float *gW, float *gb, double *loss_partials,
+                     double *loss_out, double loss_scale, uint32_t *ticket, void *stream);
 int32_t cc_dec_bce_dw_blocks(int32_t V);
 /* D2 softmax + KL on materialised fp32 logits Z2 [B][V] (model.py:98, train.py:85, TF 2.5 clip
  * semantics): row b uses the M~ row y_reg + reg_idx[b] * V; dZ[b] = scale * ([p >= 1e-7](-t) +
