@@ -29,7 +29,11 @@
 
 namespace {
 
-constexpr int NT = 256;
+#ifndef NOISE_NT
+#define NOISE_NT 256
+#endif
+constexpr int NT = NOISE_NT;   // threads per cube (and per Adam block of the Adam + F launch)
+static_assert(NT % 64 == 0 && NT <= 1024, "whole waves");
 constexpr uint32_t KIND_NOISE = 0, KIND_CUT = 1, KIND_YCUT = 2, KIND_ADD = 3, KIND_ADD_FB = 4,
                    KIND_REG = 5;
 constexpr int ADD_MAX_TRIES = 256;
@@ -200,8 +204,9 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
   int wbase = 0;
 #pragma unroll
   for (int w = 0; w < NT / 64; ++w) wbase += w < wv ? scan[w] : 0;
-  const int total = scan[0] + scan[1] + scan[2] + scan[3];
-  static_assert(NT == 256, "block scan assumes 4 waves");
+  int total = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) total += scan[w];
   int pos = wbase + inc_sum - cnt;
   int32_t *xrow = a.x_idx + (int64_t)b * a.x_cap;
   for (int w = w0; w < w1; ++w) {
