@@ -26,6 +26,15 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=200)
     ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--prespin-ms', type=float, default=300.0,
+                    help='untimed non-training GPU work (a memory-bound scale + a bf16 matmul loop) before '
+                         'warmup: the GPU out of its idle clocks, so that a short --warmup already times the '
+                         'steady state (DESIGN.md: the timed bracket)')
+    ap.add_argument('--prespin-kind', default='both', choices=('mem', 'mfma', 'both'))
+    ap.add_argument('--graph-steps', type=int, default=0,
+                    help='steps per multi-step graph replay (0: the largest of 8, 7, ..., 1 that divides '
+                         '--steps and is <= --warmup, so warmup has replayed every graph the timed region '
+                         'replays: a graph\'s first replay costs extra)')
     ap.add_argument('--V', type=int, default=22000)
     ap.add_argument('--d', type=int, default=256)
     ap.add_argument('--batch', type=int, default=512)
@@ -439,10 +448,12 @@ def main():
     data = DeviceDataset(csr=(indptr, indices), num_cards=V, neg_sampler=ns, y_mtx=y_mtx, device=dev,
                          reg_rows=reg_rows)
     del y_mtx
+    graph_steps = args.graph_steps or next(g for g in range(8, 0, -1)
+                                           if args.steps % g == 0 and (g <= args.warmup or g == 1))
     cfg = TrainConfig(V=V, d=d, batch_size=B, reg=args.reg, dtype=args.dtype, seed=1234,
                       rank=rank, world=world, reg_shard=reg_shard, reg_mode=args.reg_mode,
                       force_dp=args.force_dp,
-                      dz_pad=bool(args.dz_pad),
+                      dz_pad=bool(args.dz_pad), graph_steps=graph_steps,
                       fuse_w1_adam=True,   # one process: W1's Adam in its gradient kernel, and (BCE
                       wo_adam_in_tower=True)   # only) Wo's in the tower backward launch (parity:
     #                                        tests/test_gpu_train.py::test_fused_w1_adam_matches_unfused)
@@ -478,6 +489,18 @@ def main():
     for _ in range(3):          # eager steps: module loads, lazy allocations
         step(False)
     tr.capture()
+    if args.prespin_ms > 0:     # untimed non-training GPU work: the clocks out of idle before warmup
+        big = torch.empty(256 << 20, device=dev, dtype=torch.float32)
+        spin = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
+        t_end = time.perf_counter() + args.prespin_ms / 1e3
+        while time.perf_counter() < t_end:
+            for _ in range(4):
+                if args.prespin_kind in ('mem', 'both'):
+                    big.mul_(1.0)
+                if args.prespin_kind in ('mfma', 'both'):
+                    spin = torch.tanh(spin @ spin)
+            torch.cuda.synchronize()
+        del big, spin
 
     steps(args.warmup)
     torch.cuda.synchronize()
@@ -531,7 +554,8 @@ def main():
                    'cubes': args.cubes,
                    'parallelism': f'dp{world}' + (' (1-rank RCCL group driving the data-parallel step)'
                                                   if args.force_dp and world == 1 else ''),
-                   'graph_steps': tr.multi_n if not dp else 1},
+                   'graph_steps': tr.multi_n if not dp else 1,
+                   'prespin_ms': args.prespin_ms, 'prespin_kind': args.prespin_kind},
         'roofline': roof,
         'step_roofline': step_roofline(tr, dt / args.steps * 1e3, ktimes),
         'kernel_us': ktimes,
