@@ -26,6 +26,8 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=200)
     ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--wo-tower-frac', type=float, default=-1.0,
+                    help="the trailing fraction of Wo's Adam run in the tower backward launch (-1: TrainConfig's default)")
     ap.add_argument('--prespin-ms', type=float, default=300.0,
                     help='untimed non-training GPU work (a memory-bound scale + a bf16 matmul loop) before '
                          'warmup: the GPU out of its idle clocks, so that a short --warmup already times the '
@@ -453,7 +455,7 @@ def main():
     cfg = TrainConfig(V=V, d=d, batch_size=B, reg=args.reg, dtype=args.dtype, seed=1234,
                       rank=rank, world=world, reg_shard=reg_shard, reg_mode=args.reg_mode,
                       force_dp=args.force_dp,
-                      dz_pad=bool(args.dz_pad), graph_steps=graph_steps,
+                      dz_pad=bool(args.dz_pad), graph_steps=graph_steps, wo_tower_frac=args.wo_tower_frac,
                       fuse_w1_adam=True,   # one process: W1's Adam in its gradient kernel, and (BCE
                       wo_adam_in_tower=True)   # only) Wo's in the tower backward launch (parity:
     #                                        tests/test_gpu_train.py::test_fused_w1_adam_matches_unfused)

@@ -43,8 +43,8 @@ class TrainConfig:
     wo_adam_in_tower: bool = False  # with fuse_w1_adam, bf16 d <= 256 (fused output layers): TF Adam on
     #                                the decoder output layers' tails in the tower backward launch (bench.py)
     wo_tower_frac: float = -1.0    # ... on this trailing fraction of each; the rest stays in the Adam + F
-    #                                launch (< 0: measured per mode — 0.6 BCE only, 0.45 with the
-    #                                sampled regulariser; tools/gpu_t8.sh, tools/gpu_t15.sh sweeps)
+    #                                launch (< 0: measured per mode — 0.6 BCE only, 0.55 with the
+    #                                sampled regulariser; bench.py --wo-tower-frac sweeps)
     dx_splits: int = 0             # decoder dX K-splits (0: measured default, 32 bf16 / 16 fp8)
     dx_splits_reg: int = 0         # ... of the full-mode regulariser branch (0: 4)
     mx8_bce_q: bool = True         # fp8: the BCE product writes dZ's MX-FP8 images (else quantiser launches)
@@ -469,7 +469,7 @@ class Trainer:
         self.wo_ranges, self.rest_ranges = None, None
         if (cfg.wo_adam_in_tower and self.fuse_w1 and self.fused_out and (not self.use_reg or self.fused_reg)
                 and self.targs is not None and self.dtype == L.CC_BF16 and cfg.d <= 256):
-            frac = cfg.wo_tower_frac if cfg.wo_tower_frac >= 0 else (0.45 if self.use_reg else 0.6)
+            frac = cfg.wo_tower_frac if cfg.wo_tower_frac >= 0 else (0.55 if self.use_reg else 0.6)
             frac = min(max(float(frac), 0.0), 1.0)
             lay = self.layout
             spans = [(lay.offset('decoder/reconstruct/kernel'), lay.main_total)]
