@@ -123,7 +123,7 @@ SIGNATURES = {
     'cc_dec_kl_blocks': (_I32, [_I32]),
     'cc_dec_softmax_kl_dw': (C.c_int, [C.POINTER(DecKlArgs), _P]),
     'cc_kl_tsum': (C.c_int, [_P, _I32, _I32, _P, _P]),
-    'cc_bce_accuracy': (C.c_int, [_P, _I32, _P, _I32, _I32, _P, _P]),
+    'cc_sigmoid_cat_accuracy': (C.c_int, [_P, _I32, _P, _I32, _I32, _P, _P]),
     'cc_row_argmax': (C.c_int, [_P, _I64, _I32, _I32, _P, _P]),
     'cc_cat_accuracy': (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _I32, _P, _P]),
     'cc_adam_noise': (C.c_int, [_P, _P, _P, _P, _P, _I64, _F32, _F32, _F32, _F32, C.POINTER(NoiseArgs), _I64, _P]),

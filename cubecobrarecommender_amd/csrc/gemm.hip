@@ -396,7 +396,7 @@ struct NtStage {
 };
 
 // MX-FP8 fragment of the 32x32x64 block-scaled MFMA.  The instruction's K order (probed on
-// gfx950, tools/debug/mx8_probe.py): lane half h holds k 16h .. 16h+15 in its low 16 bytes and
+// gfx950, a one-off probe of round 3): lane half h holds k 16h .. 16h+15 in its low 16 bytes and
 // 32+16h .. 32+16h+15 in its high 16 bytes, and lane half h's scale byte covers k 32h .. 32h+31.
 // So for scale block b = 2kk + h of the K-tile, lane half g loads 16-B chunks 4kk + g (low) and
 // 4kk + 2 + g (high): chunks {4kk, 4kk+1} form block 2kk, {4kk+2, 4kk+3} block 2kk + 1.

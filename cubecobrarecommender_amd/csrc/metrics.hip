@@ -1,49 +1,27 @@
 // Keras' compiled metrics=['accuracy'] of the reference's two outputs (train.py:83-88), counted
-// on the device per step when the trainer runs with TrainConfig(metrics=True):
-//   output_1 (sigmoid + binary_crossentropy): binary_accuracy = mean(y == (sigmoid(z) > 0.5)),
-//            counted as y == (z > 0) (sigmoid(z) > 0.5 in fp32 exactly when z > 0, up to the
-//            |z| < 2^-23 rounding band around 0);
-//   output_2 (softmax + kullback_leibler_divergence): categorical_accuracy = mean over rows of
-//            argmax(y_true) == argmax(y_pred), y_true the row's M~ target (argmax precomputed once
-//            per M~ by cc_row_argmax) and argmax(softmax(z)) = argmax(z) (first index on ties, as
-//            tf.argmax).
+// on the device per step when the trainer runs with TrainConfig(metrics=True).  TF 2.5 resolves the
+// string 'accuracy' per output by SHAPE, not by loss (keras/engine/compile_utils.py,
+// MetricsContainer._get_metric_object): binary_accuracy only when y_pred's last dim is 1, sparse
+// categorical when y_true has a lower rank, else categorical_accuracy.  Both outputs here are
+// [B, |V|] against [B, |V|] targets, so BOTH are categorical_accuracy =
+// mean over rows of [argmax(y_true) == argmax(y_pred)] (tf.argmax: first index on ties):
+//   output_1 (sigmoid): y_pred = sigmoid(z) in fp32.  Eigen's float logistic (TF 2.5's CPU kernel)
+//            saturates to exactly 1.0 from z >= 15.7243833541870117 on, so saturated logits tie and
+//            the first one wins; below that the fp32 sigmoid is taken (ties there need two logits
+//            within an fp32 rounding of each other).  y_true = the noised target row (0/1): its
+//            argmax is its first set bit, 0 for an all-zero row;
+//   output_2 (softmax): argmax(softmax(z)) = argmax(z) (first index on ties), y_true the row's M~
+//            target (argmax precomputed once per M~ by cc_row_argmax).
 // Counts are integers added with one atomic per block: the totals are order-free (deterministic).
 // Off the training step's path (the fused output-layer kernels never store their logits): the
 // trainer recomputes the logits for the metrics with cc_gemm from the same bf16 / fp32 operands.
+// Parity unpinned (TF absent): the published rule and formulas are restated, Eigen's rational
+// sigmoid approximation below the cut-off is not.
 #include "common.hpp"
 
 namespace {
 
 constexpr int MT = 256;
-
-// one block per batch row: the row's correct predictions over V columns (32 per target word)
-__global__ __launch_bounds__(MT) void bce_accuracy_kernel(const float *__restrict__ Z, int ldz,
-                                                          const uint32_t *__restrict__ y_bits, int V,
-                                                          unsigned long long *__restrict__ count) {
-  __shared__ unsigned int red[MT / 64];
-  const int row = blockIdx.x, VW = (V + 31) >> 5;
-  const float *z = Z + (int64_t)row * ldz;
-  const uint32_t *y = y_bits + (int64_t)row * VW;
-  unsigned int c = 0;
-  for (int w = threadIdx.x; w < VW; w += MT) {
-    uint32_t pred = 0;
-    const int n = min(32, V - 32 * w);
-#pragma unroll 8
-    for (int i = 0; i < 32; ++i)
-      if (i < n && z[32 * w + i] > 0.f) pred |= 1u << i;
-    const uint32_t valid = n == 32 ? 0xFFFFFFFFu : ((1u << n) - 1u);
-    c += __popc(~(pred ^ y[w]) & valid);
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long t = 0;
-    for (int i = 0; i < MT / 64; ++i) t += red[i];
-    atomicAdd(count, t);
-  }
-}
 
 // first index of the row's maximum (NaN-free rows)
 __device__ __forceinline__ void argmax_pair(float &v, int &i, float v2, int i2) {
@@ -53,12 +31,10 @@ __device__ __forceinline__ void argmax_pair(float &v, int &i, float v2, int i2) 
   }
 }
 
-__device__ int block_argmax(const float *__restrict__ x, int V) {
+// the block's (first) argmax from every thread's running (v, idx); contains __syncthreads
+__device__ int block_argmax_reduce(float v, int idx) {
   __shared__ float sv[MT / 64];
   __shared__ int si[MT / 64];
-  float v = -INFINITY;
-  int idx = 0x7FFFFFFF;
-  for (int j = threadIdx.x; j < V; j += MT) argmax_pair(v, idx, x[j], j);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const float v2 = __shfl_xor(v, off);
@@ -75,6 +51,13 @@ __device__ int block_argmax(const float *__restrict__ x, int V) {
   for (int i = 1; i < MT / 64; ++i) argmax_pair(bv, bi, sv[i], si[i]);
   __syncthreads();
   return bi;
+}
+
+__device__ int block_argmax(const float *__restrict__ x, int V) {
+  float v = -INFINITY;
+  int idx = 0x7FFFFFFF;
+  for (int j = threadIdx.x; j < V; j += MT) argmax_pair(v, idx, x[j], j);
+  return block_argmax_reduce(v, idx);
 }
 
 __global__ __launch_bounds__(MT) void row_argmax_kernel(const float *__restrict__ X, int64_t ld, int V,
@@ -97,15 +80,51 @@ __global__ __launch_bounds__(MT) void cat_accuracy_kernel(const float *__restric
   }
 }
 
+
+// Eigen scalar_logistic_op<float>: the rational approximation evaluates to exactly 1 from here on
+constexpr float SIG_SAT = 15.7243833541870117f;
+__device__ __forceinline__ float keras_sigmoid(float z) {
+  return z >= SIG_SAT ? 1.0f : 1.0f / (1.0f + expf(-z));
+}
+
+// one block per batch row: [argmax_j sigmoid(z_j) == first set bit of the target row (0 if none)]
+__global__ __launch_bounds__(MT) void sigmoid_cat_accuracy_kernel(const float *__restrict__ Z, int ldz,
+                                                                  const uint32_t *__restrict__ y_bits, int V,
+                                                                  unsigned long long *__restrict__ count) {
+  __shared__ int sfirst[MT / 64];
+  const int row = blockIdx.x, VW = (V + 31) >> 5;
+  const float *z = Z + (int64_t)row * ldz;
+  const uint32_t *y = y_bits + (int64_t)row * VW;
+  int first = 0x7FFFFFFF;
+  for (int w = threadIdx.x; w < VW; w += MT) {
+    const uint32_t n = (uint32_t)min(32, V - 32 * w);
+    const uint32_t bits = y[w] & (n == 32 ? 0xFFFFFFFFu : ((1u << n) - 1u));
+    if (bits) first = min(first, 32 * w + __builtin_ctz(bits));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) first = min(first, __shfl_xor(first, off));
+  if ((threadIdx.x & 63) == 0) sfirst[threadIdx.x >> 6] = first;
+  float v = -INFINITY;
+  int idx = 0x7FFFFFFF;
+  for (int j = threadIdx.x; j < V; j += MT) argmax_pair(v, idx, keras_sigmoid(z[j]), j);
+  const int a = block_argmax_reduce(v, idx);   // (its barrier also publishes sfirst)
+  if (threadIdx.x == 0) {
+    int t = sfirst[0];
+    for (int i = 1; i < MT / 64; ++i) t = min(t, sfirst[i]);
+    if (t == 0x7FFFFFFF) t = 0;   // tf.argmax of an all-zero row
+    if (a == t) atomicAdd(count, 1ull);
+  }
+}
+
 }  // namespace
 
-extern "C" int cc_bce_accuracy(const float *Z, int32_t ldz, const uint32_t *y_bits, int32_t B, int32_t V,
-                               unsigned long long *count, void *stream) {
-  CC_REQUIRE(Z && y_bits && count && B >= 0 && V > 0 && ldz >= V, "cc_bce_accuracy: args");
+extern "C" int cc_sigmoid_cat_accuracy(const float *Z, int32_t ldz, const uint32_t *y_bits, int32_t B, int32_t V,
+                                       unsigned long long *count, void *stream) {
+  CC_REQUIRE(Z && y_bits && count && B >= 0 && V > 0 && ldz >= V, "cc_sigmoid_cat_accuracy: args");
   if (B == 0) return CC_OK;
-  hipLaunchKernelGGL(bce_accuracy_kernel, dim3((unsigned)B), dim3(MT), 0, as_stream(stream), Z, ldz, y_bits, V,
-                     count);
-  CC_LAUNCH_CHECK("bce_accuracy_kernel");
+  hipLaunchKernelGGL(sigmoid_cat_accuracy_kernel, dim3((unsigned)B), dim3(MT), 0, as_stream(stream), Z, ldz, y_bits,
+                     V, count);
+  CC_LAUNCH_CHECK("sigmoid_cat_accuracy_kernel");
   return CC_OK;
 }
 

@@ -107,10 +107,11 @@ class CC_Recommender:
             raise ValueError(f'loss must be {list(_LOSSES)} (train.py:85)')
         if float(loss_weights[0]) != 1.0:
             raise ValueError('loss_weights[0] must be 1.0 (train.py:86)')
-        # metrics=['accuracy'] (train.py:87): Keras resolves it per output — binary_accuracy for the
-        # sigmoid/BCE output, categorical_accuracy for the softmax/KL one — and reports their epoch
-        # means; fit() counts both on the device (TrainConfig(metrics=True), metrics.hip).  They do
-        # not enter the loss, the gradients or the update.
+        # metrics=['accuracy'] (train.py:87): TF 2.5 resolves it per output by shape
+        # (compile_utils._get_metric_object: binary_accuracy only when y_pred's last dim is 1), so
+        # both [B, |V|] outputs report categorical_accuracy, as epoch means over rows; fit() counts
+        # both on the device (TrainConfig(metrics=True), metrics.hip).  They do not enter the loss,
+        # the gradients or the update.
         self.metrics = []
         for mname in (metrics or ()):
             if mname not in ('accuracy', 'acc'):

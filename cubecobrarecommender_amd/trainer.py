@@ -56,9 +56,9 @@ class TrainConfig:
     dp_f_in_adam: bool = True      # data parallel: the next step's F as extra blocks of the towers + E1
     #                                bucket's sharded Adam launch (else its own launch, cc_noise_next)
     dz_pad: bool = True            # the fused D1 kernel's dZ rows at a 64-element pitch (whole cache lines)
-    metrics: bool = False          # Keras metrics=['accuracy'] (train.py:87): each step counts output 1's
-    #                                binary and output 2's categorical accuracy on the device from logits
-    #                                recomputed for the purpose (metrics.hip; take_metrics() per epoch)
+    metrics: bool = False          # Keras metrics=['accuracy'] (train.py:87): each step counts both
+    #                                outputs' categorical accuracy (TF 2.5's shape rule) on the device from
+    #                                logits recomputed for the purpose (metrics.hip; take_metrics() per epoch)
     reg_mode: str = 'sampled'      # 'sampled': B reg rows per step drawn ∝ neg_sampler (generator.py:47-51);
     #                                'full': all |V| identity rows every step, KL(M~, D2(E(I))) as the
     #                                reference README states the objective (README.md:27)
@@ -415,13 +415,15 @@ class Trainer:
                                        dtype=torch.float64)
         if self.full_reg:
             self._init_full_rows()
-        # metrics=['accuracy']: {output 1 correct, output 2 correct, output 2 rows} summed on the device
+        # metrics=['accuracy']: {output 1 correct rows, output 2 correct rows, output 2 rows} summed on
+        # the device
         self.acc_counts = None
         if cfg.metrics:
             self.acc_counts = torch.zeros(3, device=self.dev, dtype=torch.int64)
             self.Z1m = torch.zeros(B, V, **f32)
             if self.use_reg:
-                self.Z2m = self.Z2 if self.Z2 is not None else torch.zeros(self.Breg, V, **f32)
+                # (full mode's |V| identity rows go through a bounded buffer in row chunks)
+                self.Z2m = self.Z2 if self.Z2 is not None else torch.zeros(min(self.Breg, 1024), V, **f32)
                 lo, hi = self.reg_rows       # argmax of every resident M~ row (y_true), once
                 self.t_argmax = torch.zeros(hi - lo, device=self.dev, dtype=torch.int32)
                 L.call('cc_row_argmax', L.ptr(data.y_reg), V, hi - lo, V, L.ptr(self.t_argmax), L.stream_ptr())
@@ -878,6 +880,8 @@ class Trainer:
         # (side stream) and dX -> towers (this stream) only share read-only inputs.
         for k, (pre, (r0, r1)) in enumerate(branches):
             if k == 1:                 # branch 0 (D1) done: its dW final, its Wo shadow read
+                if self.hook_out is not None:
+                    self._join()       # (dW may have been issued on the side stream)
                 self._fire('hook_out')
                 self._fire('hook_dx')
             dz = self.dZout[r0:]
@@ -993,18 +997,21 @@ class Trainer:
     def _metrics_step(self, s):
         """Keras metrics=['accuracy'] of this step (train.py:87): both outputs' logits recomputed from
         the operands the step used (D3 and the output layers' bf16 / fp32 weights) into fp32, then
-        output 1's binary accuracy against the noised targets and output 2's categorical accuracy
+        both outputs' categorical accuracy — TF 2.5 picks binary_accuracy only for a last dim of 1
+        (compile_utils._get_metric_object) — output 1's against the noised target rows, output 2's
         against the M~ rows' argmax (metrics.hip).  Off the training arithmetic."""
         cfg, V, d, B = self.cfg, self.cfg.V, self.cfg.d, self.cfg.batch_size
         self._gemm(B, V, d, L.ptr(self.D3), d, self.w('decoder/reconstruct/kernel'), V,
                    bias=self.pf('decoder/reconstruct/bias'), Cf=L.ptr(self.Z1m), stream=s)
-        L.call('cc_bce_accuracy', L.ptr(self.Z1m), V, L.ptr(self.y_bits), B, V, L.ptr(self.acc_counts), s)
+        L.call('cc_sigmoid_cat_accuracy', L.ptr(self.Z1m), V, L.ptr(self.y_bits), B, V, L.ptr(self.acc_counts), s)
         if self.use_reg:
-            Br = self.Breg
-            self._gemm(Br, V, d, L.ptr(self.D3[B:]), d, self.w('decoder_for_reg/reconstruct/kernel'), V,
-                       bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2m), stream=s)
-            L.call('cc_cat_accuracy', L.ptr(self.Z2m), V, Br, V, L.ptr(self.reg_idx), L.ptr(self.t_argmax),
-                   self.reg_rows[0], L.ptr(self.acc_counts[1:]), s)
+            ch = self.Z2m.shape[0]
+            for r0 in range(0, self.Breg, ch):
+                nr = min(ch, self.Breg - r0)
+                self._gemm(nr, V, d, L.ptr(self.D3[B + r0:]), d, self.w('decoder_for_reg/reconstruct/kernel'), V,
+                           bias=self.pf('decoder_for_reg/reconstruct/bias'), Cf=L.ptr(self.Z2m), stream=s)
+                L.call('cc_cat_accuracy', L.ptr(self.Z2m), V, nr, V, L.ptr(self.reg_idx[r0:]), L.ptr(self.t_argmax),
+                       self.reg_rows[0], L.ptr(self.acc_counts[1:]), s)
 
     def take_metrics(self, steps):
         """{'output_1_accuracy', ['output_2_accuracy']} over the steps since the last call (Keras'
@@ -1015,7 +1022,7 @@ class Trainer:
         if self.dp:
             torch.distributed.all_reduce(c)
         c = c.cpu().numpy()
-        n1 = float(steps) * self.cfg.batch_size * self.cfg.world * self.cfg.V
+        n1 = float(steps) * self.cfg.batch_size * self.cfg.world   # rows (categorical accuracy)
         out = {'output_1_accuracy': float(c[0]) / n1}
         if self.use_reg:
             out['output_2_accuracy'] = float(c[1]) / max(float(c[2]), 1.0)
@@ -1359,6 +1366,8 @@ class Trainer:
         self.state.copy_(saved)
         if loss_acc is not None:
             loss_acc.zero_()
+        if self.acc_counts is not None:   # the eager warm-up step above counted its metrics
+            self.acc_counts.zero_()
         self.noise_ready = False
         self.graphs = (g_fb, g_adam, g_rest, g_main, g_all)
         self.timing = timing

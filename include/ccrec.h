@@ -503,14 +503,17 @@ int cc_kl_tsum(const float *Mt, int32_t n, int32_t V, float *tsum, void *stream)
 
 /* ----------------------------------------------------------------------------------
  * Keras metrics=['accuracy'] of the two outputs (train.py:83-88; metrics.hip), counted on the device
- * (integer atomics: order-free totals).  Z: fp32 logits [rows][ldz].
- * cc_bce_accuracy: count += #{(r, j) : (Z[r][j] > 0) == y(r, j)} over B rows x V (binary_accuracy of
- *   the sigmoid output: sigmoid(z) > 0.5 <=> z > 0); y_bits [B][ceil(V/32)] as cc_dec_bce_dw's.
+ * (integer atomics: order-free totals).  Z: fp32 logits [rows][ldz].  TF 2.5 resolves 'accuracy' by
+ * shape (compile_utils._get_metric_object: binary only for a last dim of 1), so both [B, V] outputs
+ * report categorical_accuracy.
+ * cc_sigmoid_cat_accuracy: count += #{r : argmax_j sigmoid(Z[r][j]) == first set bit of y row r (0 if
+ *   none)} over B rows, sigmoid in fp32 saturating to 1 from z >= 15.7243833541870117 (Eigen's float
+ *   logistic), first index on ties; y_bits [B][ceil(V/32)] as cc_dec_bce_dw's.
  * cc_row_argmax: out[r] = first index of the maximum of X[r][0..V) (tf.argmax).
  * cc_cat_accuracy: for the rows with reg_idx[r] >= 0: count[1] += 1 and count[0] += [argmax Z[r] ==
  *   t_argmax[reg_idx[r] - t_lo]] (categorical_accuracy of the softmax output vs the M~ row). */
-int cc_bce_accuracy(const float *Z, int32_t ldz, const uint32_t *y_bits, int32_t B, int32_t V,
-                    unsigned long long *count, void *stream);
+int cc_sigmoid_cat_accuracy(const float *Z, int32_t ldz, const uint32_t *y_bits, int32_t B, int32_t V,
+                            unsigned long long *count, void *stream);
 int cc_row_argmax(const float *X, int64_t ld, int32_t rows, int32_t V, int32_t *out, void *stream);
 int cc_cat_accuracy(const float *Z, int32_t ldz, int32_t rows, int32_t V, const int32_t *reg_idx,
                     const int32_t *t_argmax, int32_t t_lo, unsigned long long *count, void *stream);

@@ -30,6 +30,21 @@ def rel_err(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
+def progress(msg):
+    """A progress line for multi-process GPU tests: printed (pytest shows a failing test's captured
+    output) and appended to progress.log beside $CCREC_PARITY_LOG (if set), so a stuck child leaves
+    its last completed stage in gpurun_out/ even when the session is cut before the test's own
+    time limits fire (the r04j stall: DESIGN.md §5)."""
+    import os
+    import time
+    print(msg, flush=True)
+    path = os.environ.get('CCREC_PARITY_LOG')
+    if path:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(os.path.join(os.path.dirname(os.path.abspath(path)), 'progress.log'), 'a') as fh:
+            fh.write(f'{time.strftime("%H:%M:%S")} pid {os.getpid()} {msg}\n')
+
+
 def record_errors(test, step, errs):
     """Append observed parity errors as a JSON line to $CCREC_PARITY_LOG (if set): the tolerances
     in the tests are set from these observations (about 3x the largest one seen)."""

@@ -10,7 +10,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from tests.gpu_helpers import problem, rel_err
+from tests.gpu_helpers import problem, progress, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -324,14 +324,14 @@ def _rccl_run(tr, eager=2, graphed=3):
         tr.step()
         torch.cuda.synchronize()
         losses.append(tr.losses()['loss'])
-        print(f'rccl step {i} (eager, dp={tr.dp}) loss {losses[-1]}', flush=True)
+        progress(f'rccl step {i} (eager, dp={tr.dp}) loss {losses[-1]}')
     tr.capture()
-    print('rccl captured', flush=True)
+    progress('rccl captured')
     for i in range(graphed):
         tr.step()
         torch.cuda.synchronize()
         losses.append(tr.losses()['loss'])
-        print(f'rccl step {eager + i} (graph, dp={tr.dp}) loss {losses[-1]}', flush=True)
+        progress(f'rccl step {eager + i} (graph, dp={tr.dp}) loss {losses[-1]}')
     tr.flush()
     torch.cuda.synchronize()
     return losses
@@ -345,21 +345,26 @@ def _rccl_worker(shape, reg, reg_shard, q):
         import torch.distributed as dist
         torch.cuda.set_device(0)
         # the process group first: RCCL's communicator before any other GPU work of this process
+        progress(f'rccl {shape} reg {reg}: init_process_group')
         dist.init_process_group('nccl', store=dist.HashStore(), rank=0, world_size=1,
                                 device_id=torch.device('cuda', 0))
+        progress('rccl: process group up; building the DP trainer')
         tr = _rccl_trainer(shape, reg, True, reg_shard)
         assert tr.dp and tr.prefetch_dp and tr.owner == (reg_shard and reg > 0)
         dl = _rccl_run(tr)
         assert tr._sharded().nccl and tr.g_dp is not None, 'whole-step DP graph not captured'
         tr.sharded.gather_state()
         tr.check_status()
+        progress('rccl: DP steps done; building the one-process trainer')
         one = _rccl_trainer(shape, reg, False, False)
         assert not one.dp
         ol = _rccl_run(one)
         one.check_status()
+        progress('rccl: one-process steps done; sending the result')
         q.put((tr.standard(tr.params), tr.standard(tr.m), tr.standard(tr.v), dl,
                one.standard(one.params), one.standard(one.m), one.standard(one.v), ol))
         dist.destroy_process_group()
+        progress('rccl: process group destroyed')
     except Exception as e:   # surface the error in the parent
         import traceback
         q.put((repr(e) + traceback.format_exc(),) + (None,) * 7)
@@ -393,7 +398,12 @@ def test_rccl_one_rank_dp_step_matches_one_process(shape, reg, reg_shard):
             'loss': max(abs(a - b) / b for a, b in zip(dl, ol)),
             'exact_params': float(np.array_equal(dp_p, p1))}
     record_errors(f'rccl1_vs_one_{shape}_{reg}', 5, errs)
-    assert errs['loss'] < 1e-6 and errs['params'] < 1e-6 and errs['m'] < 1e-5 and errs['v'] < 1e-5, errs
+    # one rank: the shard is the whole bucket, the collectives are copies — the same kernels on the
+    # same draws, so the step is bit-identical (observed r04: every error exactly 0)
+    np.testing.assert_array_equal(dp_p, p1)
+    np.testing.assert_array_equal(dp_m, m1)
+    np.testing.assert_array_equal(dp_v, v1)
+    assert list(dl) == list(ol), (dl, ol)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -485,10 +495,13 @@ def test_fp8_dp_step_matches_single_process_and_oracle(reg_shard):
           for s in range(S['steps'])]
     record_errors(f'fp8_dp_vs_single_shard{int(reg_shard)}', S['steps'],
                   {'params': ep, 'm': em, **{f'loss{s}': v for s, v in enumerate(el)}})
-    if reg_shard:   # the regulariser dW's MX blocks group different rows: fp8 rounding apart
-        assert ep < 2e-2 and em < 1e-1 and max(el) < 1e-3, (ep, em, el)
+    # ~3x the observed (r04ao, deterministic kernels: the same on every box): params 3.7e-9 /
+    # 5.7e-9 (replicated / row-sharded M~; sharded, the regulariser dW's MX blocks group other
+    # rows), m 8.6e-8 / 8.2e-8, loss 6.4e-9 (the ranks' fp32 loss partials over 128-row groups)
+    if reg_shard:
+        assert ep < 1.8e-8 and em < 2.6e-7 and max(el) < 2e-8, (ep, em, el)
     else:
-        assert ep < 1e-3 and em < 2e-2 and max(el) < 1e-5, (ep, em, el)
+        assert ep < 1.2e-8 and em < 2.6e-7 and max(el) < 2e-8, (ep, em, el)
     # the one process's first step against the MX-FP8-emulating oracle
     B2 = W * S['B']
     cdf = noise_ref.cdf_of(ns)

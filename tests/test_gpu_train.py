@@ -449,16 +449,29 @@ def test_fused_regulariser_clip_fix_path(V, B, d):
                                       'encoder/encoded_1/kernel')}, TOL['bf16'], 0)
 
 
+# Eigen's float logistic (TF 2.5's CPU sigmoid) is exactly 1 from this logit on (metrics.hip)
+SIG_SAT = 15.7243833541870117
+
+
+def keras_out1_pred_argmax(z):
+    """argmax over the row of the fp32 sigmoid output, first index on ties (tf.argmax)."""
+    p = torch.where(z >= SIG_SAT, torch.ones_like(z), torch.sigmoid(z))
+    return torch.argmax(p, dim=1)
+
+
 @pytest.mark.parametrize('dtype,reg,mode', [('bf16', 0.1, 'sampled'), ('fp32', 0.1, 'sampled'),
                                             ('bf16', 0.1, 'full'), ('bf16', 0.0, 'sampled')])
 def test_accuracy_metrics_match_torch(dtype, reg, mode):
-    """TrainConfig(metrics=True) — compile(metrics=['accuracy']) (train.py:87): output 1's binary
-    accuracy (z > 0 vs the noised target bits) and output 2's categorical accuracy (argmax of the
-    logits vs argmax of the M~ row) counted on the device == the same counts from torch fp32 logits
+    """TrainConfig(metrics=True) — compile(metrics=['accuracy']) (train.py:87), resolved as TF 2.5
+    does (categorical for both [B, |V|] outputs): output 1's argmax of the fp32 sigmoid (Eigen's
+    saturation at 1.0, first index on ties) vs the first set target bit, output 2's argmax of the
+    logits vs argmax of the M~ row — counted on the device == the same counts from torch fp32 logits
     of the step's own operands (D3, the bf16 / fp32 output-layer weights), over two steps."""
     V, d, B, C = 2500, 256, 128, 1024
     lists, Mt, ns = problem(21, C, V, (20, 40, 80))
     P = model_ref.init_params(V, d, seed=21, bias_std=0.01)
+    # a spread of output-1 biases: some logits saturate the sigmoid (ties at 1.0: the first wins)
+    P['decoder/reconstruct/bias'] = np.random.default_rng(5).uniform(-4, 17, V).astype(np.float32)
     lay = Layout(V, d)
     cfg = TrainConfig(V=V, d=d, batch_size=B, reg=reg, dtype=dtype, seed=21, metrics=True, reg_mode=mode)
     Mt32 = Mt.astype(np.float32)
@@ -479,8 +492,8 @@ def test_accuracy_metrics_match_torch(dtype, reg, mode):
             return D3[rows] @ flat[o:o + d * V].view(d, V) + tr.params[ob:ob + V]
         z1 = logits('decoder', slice(0, B))
         yb = tr.y_bits[:B].to(torch.int64) & 0xFFFFFFFF
-        y = ((yb.unsqueeze(-1) >> torch.arange(32, device='cuda')) & 1).reshape(B, -1)[:, :V].bool()
-        want[0] += float(((z1 > 0) == y).sum())
+        y = ((yb.unsqueeze(-1) >> torch.arange(32, device='cuda')) & 1).reshape(B, -1)[:, :V]
+        want[0] += float((keras_out1_pred_argmax(z1) == torch.argmax(y, dim=1)).sum())
         if reg > 0:
             idx = tr.reg_idx[:tr.Breg].long()
             live = idx >= 0
@@ -490,10 +503,30 @@ def test_accuracy_metrics_match_torch(dtype, reg, mode):
         tr.apply()
     torch.cuda.synchronize()
     got = tr.acc_counts.cpu().numpy().astype(np.float64)
-    # logits within a rounding of 0 may fall either side between cc_gemm's and torch's summation
-    # orders: a few elements at most
-    assert abs(got[0] - want[0]) <= 1e-5 * 2 * B * V, (got, want)
+    # top logits within a rounding of each other may order differently between cc_gemm's and
+    # torch's summation orders (and the device's and torch's exp): a couple of rows at most
+    assert 0 < want[0] < 2 * B and abs(got[0] - want[0]) <= 2, (got, want)
     assert got[2] == want[2] and abs(got[1] - want[1]) <= 2, (got, want)
     m = tr.take_metrics(2)
-    assert abs(m['output_1_accuracy'] - got[0] / (2 * B * V)) < 1e-12 and tr.acc_counts.sum().item() == 0
+    assert abs(m['output_1_accuracy'] - got[0] / (2 * B)) < 1e-12 and tr.acc_counts.sum().item() == 0
     assert ('output_2_accuracy' in m) == (reg > 0)
+
+
+def test_metric_counts_exact_after_capture():
+    """capture()'s eager warm-up step must not leave its counts behind: after capture +
+    step_many(n) the device has counted exactly n steps' rows (output 2's row count = n * B)."""
+    V, d, B, C = 2500, 256, 128, 1024
+    lists, Mt, ns = problem(22, C, V, (20, 40, 80))
+    P = model_ref.init_params(V, d, seed=22, bias_std=0.01)
+    cfg = TrainConfig(V=V, d=d, batch_size=B, reg=0.1, dtype='bf16', seed=22, metrics=True, graph_steps=4)
+    tr = Trainer(cfg, DeviceDataset(lists, V, y_mtx=Mt.astype(np.float32), neg_sampler=ns),
+                 params_flat=Layout(V, d).pack(P))
+    tr.set_epoch_permutation(np.random.default_rng(22).permutation(C).astype(np.int32))
+    tr.capture()
+    assert tr.acc_counts.sum().item() == 0
+    tr.step_many(6)
+    torch.cuda.synchronize()
+    c = tr.acc_counts.cpu().numpy()
+    assert c[2] == 6 * B and 0 <= c[0] <= 6 * B and 0 <= c[1] <= c[2], c
+    m = tr.take_metrics(6)
+    assert 0.0 <= m['output_1_accuracy'] <= 1.0 and 0.0 <= m['output_2_accuracy'] <= 1.0

@@ -1,8 +1,8 @@
 """Bit fingerprint of a few training steps under whichever library CCREC_LIB names (dev A/B:
 a build variant that only re-times kernels must leave every bit unchanged).
 
-    CCREC_LIB=.../libccrec_hip_x.so python tools/debug/lib_bits.py OUT.json [--reg-mode full] [--V 22000]
-Then compare two OUT files (python tools/debug/lib_bits.py --cmp A.json B.json)."""
+    CCREC_LIB=.../libccrec_hip_x.so python tools/lib_bits.py OUT.json [--reg-mode full] [--V 22000]
+Then compare two OUT files (python tools/lib_bits.py --cmp A.json B.json)."""
 import argparse
 import hashlib
 import json
