@@ -31,18 +31,28 @@ class Layout:
     three gradient buckets (towers + E1 | decoder output layer | decoder_for_reg) split into equal
     per-rank shards (zero.py).  align == 1 is exactly cc_param_layout.
 
-    group_biases (data parallel with a bf16 shadow): the kernels keep that order and bucket
-    alignment, and every bias moves into one trailing 'biases' block.  zero.py then all-gathers
-    the kernels' bf16 shadow (half the bytes of the fp32 parameters) and keeps the fp32 biases —
-    which the kernels read in fp32 — exact on every rank by all-reducing their gradients and
-    running their Adam on every rank."""
+    group_biases (data parallel with a bf16 shadow): every bias moves into one trailing 'biases'
+    block, and the kernels are ordered by when backward finalises their gradients' exchange
+    buckets (each bucket a multiple of `align`):
+      W1 (row chunks: w1_chunks buckets, exchanged chunk by chunk as the W1-gradient kernel runs
+      them) | the encoder / decoder towers | the decoder_for_reg towers | the decoder output layer
+      | the decoder_for_reg output layer | biases.
+    The two output layers are one early bucket (final after the output-layer kernels, exchanged
+    beside the towers' backward); without the regulariser the decoder_for_reg tensors sit outside
+    every bucket (never updated, as the one-process Adam range skips them).  zero.py then
+    all-gathers the kernels' bf16 shadow (half the bytes of the fp32 parameters) and keeps the
+    fp32 biases — which the kernels read in fp32 — exact on every rank by all-reducing their
+    gradients and running their Adam on every rank."""
 
-    def __init__(self, V, d, align=1, group_biases=False):
+    def __init__(self, V, d, align=1, group_biases=False, w1_chunks=1):
         self.V, self.d, self.align = int(V), int(d), int(align)
         self.group_biases = bool(group_biases)
         self.entries = {}
-        o = 0
         shapes = layer_shapes(V, d)
+        if self.group_biases:
+            self._init_grouped(shapes, max(1, int(w1_chunks)))
+            return
+        o = 0
         for li, (fi, fo) in enumerate(shapes):
             if li in (7, 8):
                 o = _round_up(o, self.align)
@@ -54,24 +64,59 @@ class Layout:
             if li == 7:
                 o = _round_up(o, self.align)
                 self.main_total = o
-        if self.group_biases:
-            o = _round_up(o, self.align)
-            self.bias_lo = o
-            for li, (fi, fo) in enumerate(shapes):
-                self.entries[LAYERS[li] + '/bias'] = (o, (fo,))
-                o += (fo + 63) // 64 * 64
-            self.main_total = _round_up(o, self.align)   # (the main model is no longer a prefix)
         self.total = _round_up(o, self.align)
+
+    def _init_grouped(self, shapes, nchunks):
+        """The data-parallel bf16 / fp8 layout (class docstring): kernels in bucket order, biases last."""
+        a = self.align
+        o = 0
+        marks = {}
+
+        def put(li, name, shape):
+            nonlocal o
+            self.entries[LAYERS[li] + name] = (o, shape)
+            o += (int(np.prod(shape)) + 63) // 64 * 64
+        put(0, '/kernel', shapes[0])
+        w1 = self.V * self.d
+        # W1 row chunks: boundaries at multiples of 64 rows (every chunk a multiple of align
+        # elements for align <= 64 * d), the last one padded with the block
+        rows = [min(self.V, (self.V * c // nchunks + 63) // 64 * 64) for c in range(nchunks + 1)]
+        rows[0], rows[-1] = 0, self.V
+        o = _round_up(o, a)
+        self.w1_chunks = [(r0, r1) for r0, r1 in zip(rows[:-1], rows[1:]) if r1 > r0]
+        self.w1_bounds = [r0 * self.d for r0, _ in self.w1_chunks] + [o]
+        assert all(b % a == 0 for b in self.w1_bounds), ('W1 chunk boundaries off the bucket alignment', a)
+        assert w1 <= o
+        marks['towers_lo'] = o
+        for li in (1, 2, 3, 4, 5, 6):
+            put(li, '/kernel', shapes[li])
+        o = _round_up(o, a)
+        marks['towers_hi'] = o
+        for li in (8, 9, 10):
+            put(li, '/kernel', shapes[li])
+        o = _round_up(o, a)
+        marks['reg_towers_hi'] = o
+        put(7, '/kernel', shapes[7])
+        o = _round_up(o, a)
+        marks['out_hi'] = o
+        put(11, '/kernel', shapes[11])
+        o = _round_up(o, a)
+        marks['reg_out_hi'] = o
+        self.bias_lo = o
+        for li, (fi, fo) in enumerate(shapes):
+            self.entries[LAYERS[li] + '/bias'] = (o, (fo,))
+            o += (fo + 63) // 64 * 64
+        self.total = self.main_total = _round_up(o, a)   # (the main model is no longer a prefix)
+        self.marks = marks
 
     def buckets(self, with_reg):
         """Gradient buckets in the order backward produces them: (name, lo, hi)."""
         if self.group_biases:
-            reg_lo = self.offset('decoder_for_reg/decoded_1/kernel')
-            reg_lo = reg_lo - reg_lo % self.align if reg_lo % self.align else reg_lo
-            out = [('decoder_output', self.offset('decoder/reconstruct/kernel'), reg_lo),
-                   ('towers_e1', 0, self.offset('decoder/reconstruct/kernel'))]
-            if with_reg:
-                out.append(('decoder_for_reg', reg_lo, self.bias_lo))
+            m = self.marks
+            out = [('output_layers', m['reg_towers_hi'], m['reg_out_hi'] if with_reg else m['out_hi']),
+                   ('towers', m['towers_lo'], m['reg_towers_hi'] if with_reg else m['towers_hi'])]
+            b = self.w1_bounds
+            out += [(f'w1_{i}', b[i], b[i + 1]) for i in range(len(b) - 1)]
             out.append(('biases', self.bias_lo, self.total))
             return out
         out = [('decoder_output', self.offset('decoder/reconstruct/kernel'), self.main_total),

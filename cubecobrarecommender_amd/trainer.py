@@ -56,6 +56,9 @@ class TrainConfig:
     dp_f_in_adam: bool = True      # data parallel: the next step's F as extra blocks of the towers + E1
     #                                bucket's sharded Adam launch (else its own launch, cc_noise_next)
     dz_pad: bool = True            # the fused D1 kernel's dZ rows at a 64-element pitch (whole cache lines)
+    w1_chunks: int = 4             # data parallel (bf16 / fp8 layout, column-slice W1 gradient): W1's
+    #                                gradient launched and exchanged in this many row chunks (zero.py
+    #                                reduce-scatters chunk i while chunk i+1's gradient runs)
     metrics: bool = False          # Keras metrics=['accuracy'] (train.py:87): each step counts both
     #                                outputs' categorical accuracy (TF 2.5's shape rule) on the device from
     #                                logits recomputed for the purpose (metrics.hip; take_metrics() per epoch)
@@ -202,7 +205,8 @@ class Trainer:
         self.std_layout = Layout(V, d)
         self.dp = cfg.world > 1 or cfg.force_dp    # zero.py's sharded step (buckets, collectives)
         # (with a bf16 shadow the biases are grouped so zero.py all-gathers the kernels' bf16 shadow)
-        self.layout = (Layout(V, d, align=cfg.world * 64, group_biases=cfg.dtype in ('bf16', 'fp8'))
+        self.layout = (Layout(V, d, align=cfg.world * 64, group_biases=cfg.dtype in ('bf16', 'fp8'),
+                              w1_chunks=cfg.w1_chunks if cfg.reg_mode != 'full' else 1)
                        if self.dp else self.std_layout)
         self.use_reg = cfg.reg > 0
         if self.use_reg and data.y_reg is None:
@@ -509,6 +513,13 @@ class Trainer:
         # output layer's gradient is final (hook_out) and once the branch's dX product no longer
         # reads its bf16 shadow (hook_dx), so that bucket's reduce-scatter starts before dX
         self.hook_out = self.hook_dx = None
+        # ... and per gradient bucket finalised inside forward_backward_b (the towers, each W1 row
+        # chunk): name -> callable, fired once on the launching stream right after the bucket's
+        # last kernel
+        self.bucket_hooks = {}
+        # the data-parallel bf16 / fp8 layout: both output layers are one early bucket, so its
+        # exchange waits for the regulariser branch's output-layer gradient and dX too
+        self.early_reg_out = self.dp and self.layout.group_biases and self.use_reg
 
     def branch_rows(self):
         """Rows of each decoder branch: B cubes, then Breg regulariser rows."""
@@ -745,7 +756,7 @@ class Trainer:
 
     def forward_backward_a(self, stream=None):
         """F, E, towers forward, both output layers with their losses and weight/input gradients.
-        After it the 'decoder_output' gradient bucket is final (zero.py overlaps its reduction
+        After it the output-layer gradient bucket is final (zero.py overlaps its reduction
         with forward_backward_b)."""
         cfg, lay = self.cfg, self.layout
         V, d, B, R = cfg.V, cfg.d, cfg.batch_size, self.R
@@ -880,10 +891,11 @@ class Trainer:
         # (side stream) and dX -> towers (this stream) only share read-only inputs.
         for k, (pre, (r0, r1)) in enumerate(branches):
             if k == 1:                 # branch 0 (D1) done: its dW final, its Wo shadow read
-                if self.hook_out is not None:
+                if self.hook_out is not None and (not self.early_reg_out or self.fused_reg):
                     self._join()       # (dW may have been issued on the side stream)
-                self._fire('hook_out')
-                self._fire('hook_dx')
+                    self._fire('hook_out')   # (fused D2: the regulariser's output layer is final too)
+                if not self.early_reg_out:
+                    self._fire('hook_dx')
             dz = self.dZout[r0:]
             nr = r1 - r0
             splits = self.splits if k == 0 else self.splits_reg
@@ -951,6 +963,25 @@ class Trainer:
         if f is not None:
             setattr(self, name, None)
             f()
+
+    def _fire_bucket(self, name):
+        f = self.bucket_hooks.pop(name, None)
+        if f is not None:
+            f()
+
+    def bucket_hook_names(self):
+        """Gradient buckets forward_backward_b finalises one by one and fires a hook for (zero.py
+        starts each one's exchange there): the towers, then W1's row chunks."""
+        if not self.layout.group_biases:
+            return ()
+        return ('towers',) + tuple(f'w1_{i}' for i in range(len(self.layout.w1_chunks)))
+
+    def f_bucket_name(self):
+        """The bucket whose sharded Adam launch also draws the next step's F (its update waits for
+        the end of backward, as F must): the last W1 chunk, or the towers + E1 bucket."""
+        if self.layout.group_biases:
+            return f'w1_{len(self.layout.w1_chunks) - 1}'
+        return 'towers_e1'
 
     def _dx(self, gx, r0, nr, splits, pre, s):
         """Decoder dX split-K partials into split_buf: the LDS-DMA pipelined kernel (dxgemm.hip)
@@ -1052,12 +1083,16 @@ class Trainer:
             else:
                 L.call('cc_tower_bwd_dw', L.C.byref(self.targs), ss)
                 L.call('cc_tower_reduce', L.C.byref(self.targs), ss)
+            if self.bucket_hooks:
+                self._join()
         else:
             self._dense_bwd(self.H3, self.gZl, (0, R), 128, 64, 'encoder/bottleneck', gIn=self.gH3, mask=self.H3)
             self._dense_bwd(self.H2, self.gH3, (0, R), 256, 128, 'encoder/encoded_3', gIn=self.gH2, mask=self.H2)
             self._dense_bwd(self.H1, self.gH2, (0, R), d, 256, 'encoder/encoded_2', gIn_f32=self.gPre1, mask=self.H1)
+        self._fire_bucket('towers')   # (data parallel: the towers' gradients are final)
         t = self._tick('cc_embed_scatter_bwd')
         XR = self.xt_rows          # rows in the bitmask product (full mode: the cubes only)
+        chunks = self.layout.w1_chunks if self.layout.group_biases else [(0, V)]
         if self.eg_tickets is not None and self.fuse_w1:   # column slices + TF Adam on W1 in the epilogue
             cfg_ = self.cfg
             src, pk = (self.gpre1p, 1) if self.gpre1p is not None else (self.gPre1T, 0)
@@ -1067,8 +1102,15 @@ class Trainer:
                    cfg_.eps, s)
         elif self.eg_tickets is not None:   # column slices (cc_embed_grad_cs), from the packed image or dPre1^T
             src, pk = (self.gpre1p, 1) if self.gpre1p is not None else (self.gPre1T, 0)
-            L.call('cc_embed_grad_cs', L.ptr(src), pk, V, d, XR, self.RP, L.ptr(self.xt_bits),
-                   self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), self._eg_tk(), s)
+            # data parallel: W1's row chunks one launch each (the bias row with the last), each
+            # chunk's exchange starting as soon as its launch is issued (zero.py bucket hooks);
+            # every W1 tile is computed as in the one-launch product (bit-identical)
+            gw, gb = self.layout.offset('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias')
+            for i, (r0, r1) in enumerate(chunks):
+                L.call('cc_embed_grad_cs', L.ptr(src), pk, r1 - r0, d, XR, self.RP, L.ptr(self.xt_bits[r0:]),
+                       L.ptr(self.grads[gw + r0 * d:]), gb if i == len(chunks) - 1 else None, self._eg_tk(), s)
+                if i + 1 < len(chunks):
+                    self._fire_bucket(f'w1_{i}')
         elif self.gpre1p is not None:
             L.call('cc_embed_grad_packed', L.ptr(self.gpre1p), V, d, XR, self.RP, L.ptr(self.xt_bits),
                    self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), s)
@@ -1084,6 +1126,8 @@ class Trainer:
                    self.reg_rows[1] - self.reg_rows[0], d, self.reg_rows[0],
                    self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), L.ptr(self.id_ws), s)
         t()
+        for i in range(len(chunks)):   # (the W1 chunks not fired above: the last, or all of them)
+            self._fire_bucket(f'w1_{i}')
         if self.fused_tower:
             self._join()
 
@@ -1187,7 +1231,7 @@ class Trainer:
         update waits for the end of backward, as F must), else its own launch after backward."""
         sh = self._sharded()
         fuse_f = self.prefetch_dp and self.cfg.dp_f_in_adam
-        tb = sh.bucket('towers_e1')['gshard'] if fuse_f else None
+        tb = sh.bucket(self.f_bucket_name())['gshard'] if fuse_f else None
 
         def adam_fn(lo, n, gs):
             if gs is tb:

@@ -6,8 +6,13 @@ the GPUs of one node with one exchange step, the gradient reduction.  A plain al
 HBM traffic world times over.  Here (ZeRO-1):
 
   * the flat buffers are split into gradient buckets in the order backward finishes them
-    (Layout.buckets: the decoder output layer first — final after forward_backward_a —, then
-    the towers + E1, then decoder_for_reg), each padded to a multiple of world*64;
+    (Layout.buckets, bf16 / fp8: both output layers first — final after forward_backward_a —,
+    then the towers, then W1 in row chunks; fp32: the decoder output layer, the towers + E1,
+    decoder_for_reg), each padded to a multiple of world*64;
+  * each bucket's exchange is issued on the comm stream the moment its gradient is final: the
+    output layers' at the trainer's hook inside forward_backward_a, the towers' and every W1 row
+    chunk's at the trainer's bucket hooks inside forward_backward_b (chunk i's reduce-scatter then
+    runs beside chunk i+1's gradient launch);
   * each bucket is reduce-scattered (SUM, then 1/world: the mean over the global batch, exactly
     the single-process gradient of world*B cubes) as soon as it is final, on a side stream, so
     the decoder-output bucket's exchange overlaps the towers' backward;
@@ -202,10 +207,22 @@ class ShardedStep:
             return
         main = torch.cuda.current_stream()
         ev, gate = torch.cuda.Event(), None
+        early = []   # later buckets started from the trainer's bucket hooks inside phase_b
         if hooks:   # the first bucket's reduce-scatter as soon as its gradient is final (before dX)
             gate = torch.cuda.Event()
             self.tr.hook_out = lambda: ev.record(main)
             self.tr.hook_dx = lambda: gate.record(main)
+            names = set(self.tr.bucket_hook_names()) if hasattr(self.tr, 'bucket_hook_names') else set()
+            early = [b for b in later if b['name'] in names]
+
+            def launch(b):   # on the comm stream after everything issued so far on main
+                e = torch.cuda.Event()
+                e.record(main)
+                with torch.cuda.stream(self.comm):
+                    self.comm.wait_event(e)
+                    self.update(b, adam_fn)
+                    refresh(b['lo'], b['hi'])
+            self.tr.bucket_hooks = {b['name']: (lambda b=b: launch(b)) for b in early}
         phase_a()
         if hooks:
             assert self.tr.hook_out is None and self.tr.hook_dx is None, 'forward_backward_a fired no hooks'
@@ -216,6 +233,8 @@ class ShardedStep:
             self.update(first, adam_fn, gate)
             refresh(first['lo'], first['hi'])
         phase_b()
+        if hooks:
+            assert not self.tr.bucket_hooks, f'forward_backward_b left bucket hooks {list(self.tr.bucket_hooks)}'
         ev2 = torch.cuda.Event()
         ev2.record(main)
         if after_b is not None:
@@ -223,6 +242,8 @@ class ShardedStep:
         with torch.cuda.stream(self.comm):
             self.comm.wait_event(ev2)
             for b in later:
+                if any(b is e for e in early):
+                    continue
                 self.update(b, adam_fn)
                 refresh(b['lo'], b['hi'])
         main.wait_stream(self.comm)

@@ -51,11 +51,11 @@ def _adam(p, m, v, g, t, lr=1e-3, b1=0.9, b2=0.999, eps=1e-7):
 
 
 class _FakeTrainer:
-    def __init__(self, world, rank, with_reg, shadow=False):
+    def __init__(self, world, rank, with_reg, shadow=False, chunks=1):
         from types import SimpleNamespace
         from cubecobrarecommender_amd.layout import Layout
         self.cfg = SimpleNamespace(world=world, rank=rank)
-        self.layout = Layout(300, 64, align=world * 64, group_biases=shadow)
+        self.layout = Layout(300, 64, align=world * 64, group_biases=shadow, w1_chunks=chunks)
         self.use_reg = with_reg
         n = self.layout.total
         gen = torch.Generator().manual_seed(7)
@@ -66,13 +66,13 @@ class _FakeTrainer:
         self.shadow = self.params.to(torch.bfloat16) if shadow else None
 
 
-def _zero_worker(rank, world, port, q, shadow=False):
+def _zero_worker(rank, world, port, q, shadow=False, chunks=1):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from cubecobrarecommender_amd import distributed as D
     from cubecobrarecommender_amd.zero import ShardedStep
     D.init(backend='gloo')
-    tr = _FakeTrainer(world, rank, with_reg=True, shadow=shadow)
+    tr = _FakeTrainer(world, rank, with_reg=True, shadow=shadow, chunks=chunks)
     zs = ShardedStep(tr)
     assert zs.shadow_gather == shadow
     for t in (1, 2):
@@ -88,26 +88,27 @@ def _zero_worker(rank, world, port, q, shadow=False):
     D.finish()
 
 
-@pytest.mark.parametrize('shadow', [False, True])
-def test_gloo_world2_sharded_adam_equals_allreduce_adam(shadow):
+@pytest.mark.parametrize('shadow,chunks', [(False, 1), (True, 1), (True, 3)])
+def test_gloo_world2_sharded_adam_equals_allreduce_adam(shadow, chunks):
     """ZeRO-1 step (bucketed reduce-scatter, Adam on the rank's shard, all-gather; zero.py)
     leaves every rank with exactly the parameters of a full Adam on the averaged gradient.
     shadow: the bf16 path's grouped-bias layout — the kernels' bf16 shadow is all-gathered and the
     biases bucket all-reduced (Adam on every rank): after the steps every rank holds the exact
-    shadow and fp32 biases, and gather_state() completes the fp32 kernels, m and v."""
+    shadow and fp32 biases, and gather_state() completes the fp32 kernels, m and v.  chunks: W1's
+    gradient exchanged in row-chunk buckets (the bf16 layout's early output-layer bucket too)."""
     world = 2
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    port = 29500 + (os.getpid() + 7 + 11 * shadow) % 1000
-    ps = [ctx.Process(target=_zero_worker, args=(r, world, port, q, shadow)) for r in range(world)]
+    port = 29500 + (os.getpid() + 7 + 11 * shadow + 23 * chunks) % 1000
+    ps = [ctx.Process(target=_zero_worker, args=(r, world, port, q, shadow, chunks)) for r in range(world)]
     for p in ps:
         p.start()
     res = {r: rest for r, *rest in [q.get(timeout=120) for _ in ps]}
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
-    ref = _FakeTrainer(world, 0, with_reg=True, shadow=shadow)
-    g = sum(_FakeTrainer(world, r, True, shadow=shadow).grads for r in range(world)) * (1.0 / world)
+    ref = _FakeTrainer(world, 0, with_reg=True, shadow=shadow, chunks=chunks)
+    g = sum(_FakeTrainer(world, r, True, shadow=shadow, chunks=chunks).grads for r in range(world)) * (1.0 / world)
     for t in (1, 2):
         _adam(ref.params, ref.m, ref.v, g, t)
     for r in range(world):
@@ -118,3 +119,39 @@ def test_gloo_world2_sharded_adam_equals_allreduce_adam(shadow):
         if shadow:
             np.testing.assert_array_equal(sh, ref.params.to(torch.bfloat16).float().numpy())
             np.testing.assert_array_equal(bias, ref.params[ref.layout.bias_lo:].numpy())
+
+
+@pytest.mark.parametrize('V,d,world,chunks', [(22000, 256, 8, 4), (22000, 1024, 8, 4), (300, 64, 2, 3),
+                                              (2500, 256, 1, 4), (3000, 1024, 2, 4), (301, 64, 4, 2)])
+def test_grouped_layout_buckets(V, d, world, chunks):
+    """The data-parallel bf16 / fp8 layout (layout.Layout(group_biases=True)): the buckets are
+    disjoint, aligned to world*64, in backward order (output layers, towers, W1 chunks, biases),
+    cover every tensor with the regulariser and skip exactly the decoder_for_reg tensors without
+    it; W1's row chunks tile [V, d] contiguously; packing round-trips every tensor."""
+    from cubecobrarecommender_amd.layout import NAMES, Layout
+    lay = Layout(V, d, align=world * 64, group_biases=True, w1_chunks=chunks)
+    a = world * 64
+    for with_reg in (True, False):
+        bk = lay.buckets(with_reg)
+        names = [n for n, _, _ in bk]
+        assert names[:2] == ['output_layers', 'towers'] and names[-1] == 'biases'
+        assert names[2:-1] == [f'w1_{i}' for i in range(len(lay.w1_chunks))]
+        spans = sorted((lo, hi) for _, lo, hi in bk)
+        assert all(lo % a == 0 and hi % a == 0 and lo < hi for lo, hi in spans)
+        assert all(h0 <= l1 for (_, h0), (l1, _) in zip(spans, spans[1:]))
+        for n in NAMES:
+            o, shape = lay.entries[n]
+            size = int(np.prod(shape))
+            inside = [b for b, lo, hi in bk if lo <= o and o + size <= hi]
+            skip = not with_reg and n.startswith('decoder_for_reg/') and n.endswith('/kernel')
+            if n == 'encoder/encoded_1/kernel':   # W1: exactly the union of the chunk buckets
+                w1b = [(lo, hi) for b, lo, hi in bk if b.startswith('w1_')]
+                assert w1b[0][0] == o and o + size <= w1b[-1][1] and w1b[-1][1] - (o + size) < a
+                continue
+            assert len(inside) == (0 if skip else 1), (n, with_reg, inside)
+    assert lay.w1_chunks[0][0] == 0 and lay.w1_chunks[-1][1] == V
+    assert all(r1 == r0n for (_, r1), (r0n, _) in zip(lay.w1_chunks, lay.w1_chunks[1:]))
+    rng = np.random.default_rng(0)
+    P = {n: rng.standard_normal(lay.shape(n)).astype(np.float32) for n in NAMES}
+    back = lay.unpack(lay.pack(P))
+    assert all(np.array_equal(back[n], P[n]) for n in NAMES)
