@@ -50,6 +50,25 @@ constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
 #ifndef DEC_PRIO_TOGGLE
 #define DEC_PRIO_TOGGLE 1
 #endif
+// DEC_YS_FIRST: pass 0 issues the target-word loads BEFORE the next pass's A-fragment prefetch, so
+// the wait for the words (before the epilogue stages them in LDS) leaves the prefetch in flight
+// (after it, that wait was a vmcnt(0) that also drained the prefetch)
+#ifndef DEC_YS_FIRST
+#define DEC_YS_FIRST 0
+#endif
+// DEC_D16HI: the odd row of each packed dz pair stored by buffer_store_short_d16_hi straight from
+// the packed register (no shift)
+#ifndef DEC_D16HI
+#define DEC_D16HI 1
+#endif
+// DEC_SCALAR: the BCE epilogue in scalar fp32 ops (built with -fno-slp-vectorize) instead of
+// packed v_pk_* pairs
+#ifndef DEC_SCALAR
+#define DEC_SCALAR 1
+#endif
+#ifndef DEC_YS_LATE   // build knob: 0 stages the target words with the Wo slice, before the first barrier
+#define DEC_YS_LATE 1
+#endif
 
 typedef __attribute__((ext_vector_type(4))) uint32_t v4u;  // staging registers (stay in VGPRs)
 typedef __attribute__((address_space(3))) void lds_void;
@@ -188,7 +207,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   // YS_LATE (DMA, B >= 256: every wave has rows in pass 0): the target words are loaded last and
   // written to LDS only after pass 0's logits MFMAs, so the first barrier waits for the Wo slice and
   // the A fragments but not for the 1.5-K strided word loads
-  constexpr bool YS_LATE = DMA && B >= 256;
+  constexpr bool YS_LATE = DEC_YS_LATE && DMA && B >= 256;
   constexpr int NY = (B * NJ + NTH - 1) / NTH;
   uint32_t yv[NY];
   auto load_ys = [&]() {
@@ -322,10 +341,28 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   const __amdgpu_buffer_rsrc_t dz_rs =
       __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)B * (uint32_t)p.ldz * 2u, 0x00020000);
   const int LZ = p.ldz;
+  // dz of rows (r2, r2 + 1) as one packed bf16 pair -> two 2-B stores (row offsets as the scalar
+  // soffset).  DEC_D16HI: the odd row by buffer_store_short_d16_hi straight from the pair (inline
+  // asm: the compiler counts no vmcnt for it — a later counted wait can only over-wait, never
+  // under-wait, since this store is younger than every load it counts)
+#define DEC_STORE_PAIR(PK, R2)                                                                           \
+  do {                                                                                                    \
+    const uint32_t so0 = 2u * (uint32_t)((((R2) & 3) + 8 * ((R2) >> 2)) * LZ);                           \
+    const uint32_t so1 = 2u * (uint32_t)(((((R2) + 1) & 3) + 8 * (((R2) + 1) >> 2)) * LZ);                \
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(PK), dz_rs, zv, so0, DEC_DZ_CPOL);                  \
+    if constexpr (DEC_D16HI)                                                                              \
+      asm volatile("buffer_store_short_d16_hi %0, %1, %2, %3 offen" ::"v"(PK), "v"(zv), "s"(dz_rs), "s"(so1) \
+                   : "memory");                                                                           \
+    else                                                                                                  \
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)((PK) >> 16), dz_rs, zv, so1, DEC_DZ_CPOL);         \
+  } while (0)
 #pragma unroll
   for (int ps = 0; ps < npass; ++ps) {
+    if constexpr (YS_LATE && DEC_YS_FIRST) {
+      if (ps == 0) load_ys();   // before the prefetch: the epilogue's wait for them leaves it in flight
+    }
     if (!RING1 && ps + 1 < npass) load_a(af[(ps + 1) & 1], ps + 1);
-    if constexpr (YS_LATE) {
+    if constexpr (YS_LATE && !DEC_YS_FIRST) {
       if (ps == 0) load_ys();   // the youngest loads: nothing before pass 0's epilogue waits for them
     }
     if (ps * 256 + w * 32 >= B) continue;          // wave-uniform: rows beyond B
@@ -389,6 +426,43 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         // instruction; summed log2 scaled by ln 2 at the end
         // store offsets: the lane part in a VGPR, the row part (r) as the scalar soffset
         const uint32_t zv = 2u * (uint32_t)((rb + 4 * half) * LZ + n0 + col);
+#if DEC_SCALAR
+        // even / odd rows accumulate apart (the packed form's lanes), one fp32 op per element:
+        // packed v_pk_* f32 ops issue slower than two scalar ones beside the MFMAs
+        // (MI355X_MICROARCH.md, per-instruction constants) and gain nothing on the VALU
+        float lp[2] = {1.f, 1.f}, rsa[2] = {0.f, 0.f}, csa[2] = {0.f, 0.f};
+        uint4 yw[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) yw[g] = *reinterpret_cast<const uint4 *>(ys + j * B + rb + 8 * g + 4 * half);
+        const uint32_t ysh = 31u - (uint32_t)(lane & 31);   // the lane's target bit -> bit 31
+#pragma unroll
+        for (int r2 = 0; r2 < 16; r2 += 2) {
+          float dz2[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int r = r2 + e;
+            const uint32_t ywr = (r & 3) == 0 ? yw[r >> 2].x : (r & 3) == 1 ? yw[r >> 2].y : (r & 3) == 2 ? yw[r >> 2].z : yw[r >> 2].w;
+            const uint32_t ym = ywr << ysh;
+            const float z = acc[j][r];
+            const float sv = __uint_as_float(xor_sign(__float_as_uint(z), ym));
+            const float a = __builtin_amdgcn_exp2f(-fabsf(z) * LOG2E);
+            const float opa = 1.f + a;
+            const float rp = __builtin_amdgcn_rcpf(opa);
+            lp[e] *= opa;
+            rsa[e] += fmaxf(sv, 0.f);
+            const float sel = sv >= 0.f ? rp : a * rp;   // sigmoid(s)
+            const float dzv = __uint_as_float(xor_sign(__float_as_uint(sel * scale), ym));
+            csa[e] += dzv;   // the bias gradient sums the fp32 dz (the reference's arithmetic)
+            dz2[e] = dzv;
+          }
+          const uint32_t pk = bf16_pack2(dz2[0], dz2[1]);
+          tt[r2 >> 1] = pk;
+          DEC_STORE_PAIR(pk, r2);
+        }
+        lsum += __builtin_amdgcn_logf(lp[0] * lp[1]);
+        rsum += rsa[0] + rsa[1];
+        cs[j] += csa[0] + csa[1];
+#else
         f32x2_t lprod = {1.f, 1.f}, rs2 = {0.f, 0.f}, cs2 = {0.f, 0.f};  // even / odd rows: packed math
         // the 16 rows' target words: 4 runs of 4 consecutive rows -> 4 LDS reads of 16 B
         uint4 yw[4];
@@ -424,16 +498,12 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
           cs2 += dzp;   // the bias gradient sums the fp32 dz (the reference's arithmetic)
           const uint32_t pk = bf16_pack2(dzp[0], dzp[1]);
           tt[r2 >> 1] = pk;
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const int r = r2 + e;
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(e ? pk >> 16 : pk), dz_rs, zv,
-                                                  2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * LZ), DEC_DZ_CPOL);
-          }
+          DEC_STORE_PAIR(pk, r2);
         }
         lsum += __builtin_amdgcn_logf(lprod[0] * lprod[1]);
         rsum += rs2[0] + rs2[1];
         cs[j] += cs2[0] + cs2[1];
+#endif
       } else {
 #pragma unroll
         for (int r = 0; r < 8; ++r) tt[r] = 0;

@@ -32,11 +32,12 @@ class Layout:
     per-rank shards (zero.py).  align == 1 is exactly cc_param_layout.
 
     group_biases (data parallel with a bf16 shadow): every bias moves into one trailing 'biases'
-    block, and the kernels are ordered by when backward finalises their gradients' exchange
-    buckets (each bucket a multiple of `align`):
+    block, and the kernels are ordered by their gradients' exchange buckets (each bucket a
+    multiple of `align`):
       W1 (row chunks: w1_chunks buckets, exchanged chunk by chunk as the W1-gradient kernel runs
-      them) | the encoder / decoder towers | the decoder_for_reg towers | the decoder output layer
-      | the decoder_for_reg output layer | biases.
+      them; the towers, final just before W1's gradient, ride in the last chunk's bucket) | the
+      encoder / decoder towers | the decoder_for_reg towers | the decoder output layer | the
+      decoder_for_reg output layer | biases.
     The two output layers are one early bucket (final after the output-layer kernels, exchanged
     beside the towers' backward); without the regulariser the decoder_for_reg tensors sit outside
     every bucket (never updated, as the one-process Adam range skips them).  zero.py then
@@ -113,9 +114,9 @@ class Layout:
         """Gradient buckets in the order backward produces them: (name, lo, hi)."""
         if self.group_biases:
             m = self.marks
-            out = [('output_layers', m['reg_towers_hi'], m['reg_out_hi'] if with_reg else m['out_hi']),
-                   ('towers', m['towers_lo'], m['reg_towers_hi'] if with_reg else m['towers_hi'])]
-            b = self.w1_bounds
+            out = [('output_layers', m['reg_towers_hi'], m['reg_out_hi'] if with_reg else m['out_hi'])]
+            b = list(self.w1_bounds)
+            b[-1] = m['reg_towers_hi'] if with_reg else m['towers_hi']   # the towers ride in the last chunk
             out += [(f'w1_{i}', b[i], b[i + 1]) for i in range(len(b) - 1)]
             out.append(('biases', self.bias_lo, self.total))
             return out

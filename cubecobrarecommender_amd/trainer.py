@@ -56,9 +56,10 @@ class TrainConfig:
     dp_f_in_adam: bool = True      # data parallel: the next step's F as extra blocks of the towers + E1
     #                                bucket's sharded Adam launch (else its own launch, cc_noise_next)
     dz_pad: bool = True            # the fused D1 kernel's dZ rows at a 64-element pitch (whole cache lines)
-    w1_chunks: int = 4             # data parallel (bf16 / fp8 layout, column-slice W1 gradient): W1's
+    w1_chunks: int = 0             # data parallel (bf16 / fp8 layout, column-slice W1 gradient): W1's
     #                                gradient launched and exchanged in this many row chunks (zero.py
-    #                                reduce-scatters chunk i while chunk i+1's gradient runs)
+    #                                reduce-scatters chunk i while chunk i+1's gradient runs); 0: by the
+    #                                exchange model (tools/dp_model.py) — 1 at d <= 512, 2 above
     metrics: bool = False          # Keras metrics=['accuracy'] (train.py:87): each step counts both
     #                                outputs' categorical accuracy (TF 2.5's shape rule) on the device from
     #                                logits recomputed for the purpose (metrics.hip; take_metrics() per epoch)
@@ -206,7 +207,8 @@ class Trainer:
         self.dp = cfg.world > 1 or cfg.force_dp    # zero.py's sharded step (buckets, collectives)
         # (with a bf16 shadow the biases are grouped so zero.py all-gathers the kernels' bf16 shadow)
         self.layout = (Layout(V, d, align=cfg.world * 64, group_biases=cfg.dtype in ('bf16', 'fp8'),
-                              w1_chunks=cfg.w1_chunks if cfg.reg_mode != 'full' else 1)
+                              w1_chunks=(1 if cfg.reg_mode == 'full' else cfg.w1_chunks if cfg.w1_chunks > 0
+                                         else 1 if d <= 512 else 2))
                        if self.dp else self.std_layout)
         self.use_reg = cfg.reg > 0
         if self.use_reg and data.y_reg is None:
@@ -971,10 +973,10 @@ class Trainer:
 
     def bucket_hook_names(self):
         """Gradient buckets forward_backward_b finalises one by one and fires a hook for (zero.py
-        starts each one's exchange there): the towers, then W1's row chunks."""
+        starts each one's exchange there): W1's row chunks (the last with the towers)."""
         if not self.layout.group_biases:
             return ()
-        return ('towers',) + tuple(f'w1_{i}' for i in range(len(self.layout.w1_chunks)))
+        return tuple(f'w1_{i}' for i in range(len(self.layout.w1_chunks)))
 
     def f_bucket_name(self):
         """The bucket whose sharded Adam launch also draws the next step's F (its update waits for
@@ -1083,13 +1085,10 @@ class Trainer:
             else:
                 L.call('cc_tower_bwd_dw', L.C.byref(self.targs), ss)
                 L.call('cc_tower_reduce', L.C.byref(self.targs), ss)
-            if self.bucket_hooks:
-                self._join()
         else:
             self._dense_bwd(self.H3, self.gZl, (0, R), 128, 64, 'encoder/bottleneck', gIn=self.gH3, mask=self.H3)
             self._dense_bwd(self.H2, self.gH3, (0, R), 256, 128, 'encoder/encoded_3', gIn=self.gH2, mask=self.H2)
             self._dense_bwd(self.H1, self.gH2, (0, R), d, 256, 'encoder/encoded_2', gIn_f32=self.gPre1, mask=self.H1)
-        self._fire_bucket('towers')   # (data parallel: the towers' gradients are final)
         t = self._tick('cc_embed_scatter_bwd')
         XR = self.xt_rows          # rows in the bitmask product (full mode: the cubes only)
         chunks = self.layout.w1_chunks if self.layout.group_biases else [(0, V)]

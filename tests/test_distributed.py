@@ -125,17 +125,18 @@ def test_gloo_world2_sharded_adam_equals_allreduce_adam(shadow, chunks):
                                               (2500, 256, 1, 4), (3000, 1024, 2, 4), (301, 64, 4, 2)])
 def test_grouped_layout_buckets(V, d, world, chunks):
     """The data-parallel bf16 / fp8 layout (layout.Layout(group_biases=True)): the buckets are
-    disjoint, aligned to world*64, in backward order (output layers, towers, W1 chunks, biases),
+    disjoint, aligned to world*64, in backward order (output layers, W1 chunks, biases),
     cover every tensor with the regulariser and skip exactly the decoder_for_reg tensors without
-    it; W1's row chunks tile [V, d] contiguously; packing round-trips every tensor."""
+    it; W1's row chunks tile [V, d] contiguously (the towers in the last chunk's bucket); packing
+    round-trips every tensor."""
     from cubecobrarecommender_amd.layout import NAMES, Layout
     lay = Layout(V, d, align=world * 64, group_biases=True, w1_chunks=chunks)
     a = world * 64
     for with_reg in (True, False):
         bk = lay.buckets(with_reg)
         names = [n for n, _, _ in bk]
-        assert names[:2] == ['output_layers', 'towers'] and names[-1] == 'biases'
-        assert names[2:-1] == [f'w1_{i}' for i in range(len(lay.w1_chunks))]
+        assert names[0] == 'output_layers' and names[-1] == 'biases'
+        assert names[1:-1] == [f'w1_{i}' for i in range(len(lay.w1_chunks))]
         spans = sorted((lo, hi) for _, lo, hi in bk)
         assert all(lo % a == 0 and hi % a == 0 and lo < hi for lo, hi in spans)
         assert all(h0 <= l1 for (_, h0), (l1, _) in zip(spans, spans[1:]))
@@ -144,9 +145,10 @@ def test_grouped_layout_buckets(V, d, world, chunks):
             size = int(np.prod(shape))
             inside = [b for b, lo, hi in bk if lo <= o and o + size <= hi]
             skip = not with_reg and n.startswith('decoder_for_reg/') and n.endswith('/kernel')
-            if n == 'encoder/encoded_1/kernel':   # W1: exactly the union of the chunk buckets
+            if n == 'encoder/encoded_1/kernel':   # W1: the chunk buckets (the last also holds the towers)
                 w1b = [(lo, hi) for b, lo, hi in bk if b.startswith('w1_')]
-                assert w1b[0][0] == o and o + size <= w1b[-1][1] and w1b[-1][1] - (o + size) < a
+                assert w1b[0][0] == o and o + size <= w1b[-1][1]
+                assert [lo for lo, _ in w1b] == [r0 * d for r0, _ in lay.w1_chunks]
                 continue
             assert len(inside) == (0 if skip else 1), (n, with_reg, inside)
     assert lay.w1_chunks[0][0] == 0 and lay.w1_chunks[-1][1] == V

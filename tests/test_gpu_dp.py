@@ -337,7 +337,7 @@ def _rccl_run(tr, eager=2, graphed=3):
     return losses
 
 
-def _rccl_worker(shape, reg, reg_shard, q):
+def _rccl_worker(shape, reg, reg_shard, q, chunks=0):
     os.environ.update(HSA_ENABLE_IPC_MODE_LEGACY='0')
     import faulthandler
     faulthandler.dump_traceback_later(150, exit=True)   # a stuck child names where it is stuck
@@ -349,8 +349,9 @@ def _rccl_worker(shape, reg, reg_shard, q):
         dist.init_process_group('nccl', store=dist.HashStore(), rank=0, world_size=1,
                                 device_id=torch.device('cuda', 0))
         progress('rccl: process group up; building the DP trainer')
-        tr = _rccl_trainer(shape, reg, True, reg_shard)
+        tr = _rccl_trainer(shape, reg, True, reg_shard, w1_chunks=chunks)
         assert tr.dp and tr.prefetch_dp and tr.owner == (reg_shard and reg > 0)
+        assert chunks == 0 or len(tr.layout.w1_chunks) == chunks
         dl = _rccl_run(tr)
         assert tr._sharded().nccl and tr.g_dp is not None, 'whole-step DP graph not captured'
         tr.sharded.gather_state()
@@ -372,14 +373,16 @@ def _rccl_worker(shape, reg, reg_shard, q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize('shape,reg,reg_shard', [('bench', 0.0, False), ('bench', 0.1, True), ('c5', 0.1, True)])
-def test_rccl_one_rank_dp_step_matches_one_process(shape, reg, reg_shard):
+@pytest.mark.parametrize('shape,reg,reg_shard,chunks', [('bench', 0.0, False, 0), ('bench', 0.1, True, 0),
+                                                        ('bench', 0.1, True, 3), ('c5', 0.1, True, 0)])
+def test_rccl_one_rank_dp_step_matches_one_process(shape, reg, reg_shard, chunks):
     """The data-parallel step over RCCL (1 rank), eager then as the captured whole-step graph, ==
-    the one-process step on the same draws: parameters, Adam moments and losses over 5 steps."""
+    the one-process step on the same draws: parameters, Adam moments and losses over 5 steps.
+    chunks: W1's gradient launched and exchanged in that many row chunks (0: the default)."""
     from tests.gpu_helpers import record_errors
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    p = ctx.Process(target=_rccl_worker, args=(shape, reg, reg_shard, q))
+    p = ctx.Process(target=_rccl_worker, args=(shape, reg, reg_shard, q, chunks))
     p.start()
     res = None
     for _ in range(56):        # (a child that dies without a result fails the test at once)
@@ -397,7 +400,7 @@ def test_rccl_one_rank_dp_step_matches_one_process(shape, reg, reg_shard):
     errs = {'params': rel_err(dp_p, p1), 'm': rel_err(dp_m, m1), 'v': rel_err(dp_v, v1),
             'loss': max(abs(a - b) / b for a, b in zip(dl, ol)),
             'exact_params': float(np.array_equal(dp_p, p1))}
-    record_errors(f'rccl1_vs_one_{shape}_{reg}', 5, errs)
+    record_errors(f'rccl1_vs_one_{shape}_{reg}_c{chunks}', 5, errs)
     # one rank: the shard is the whole bucket, the collectives are copies — the same kernels on the
     # same draws, so the step is bit-identical (observed r04: every error exactly 0)
     np.testing.assert_array_equal(dp_p, p1)
