@@ -129,6 +129,8 @@ SIGNATURES = {
     'cc_adam_noise': (C.c_int, [_P, _P, _P, _P, _P, _I64, _F32, _F32, _F32, _F32, C.POINTER(NoiseArgs), _I64, _P]),
     'cc_adam_noise_pack2': (C.c_int, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F32, _F32, _F32, _F32,
                                       C.POINTER(NoiseArgs), _I64, C.POINTER(AdamPack), _P]),
+    'cc_adam_pack2': (C.c_int, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F32, _F32, _F32, _F32,
+                                C.POINTER(NoiseArgs), _I64, C.POINTER(AdamPack), _P]),
     'cc_adam_noise_pack': (C.c_int, [_P, _P, _P, _P, _P, _I64, _F32, _F32, _F32, _F32, C.POINTER(NoiseArgs), _I64,
                                      C.POINTER(AdamPack), _P]),
     'cc_adam_dense': (C.c_int, [_P, _P, _P, _P, _P, _I64, _P, _F32, _F32, _F32, _F32, _P]),
@@ -156,6 +158,8 @@ SIGNATURES = {
     'cc_tower_bwd_chain': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_bwd_chain_adam': (C.c_int, [C.POINTER(TowerArgs), _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _P,
                                           _F32, _F32, _F32, _F32, _P]),
+    'cc_tower_bwd_chain_noise': (C.c_int, [C.POINTER(TowerArgs), C.POINTER(NoiseArgs), _I64, _P, _P, _P, _P, _P,
+                                           _I64, _I64, _I64, _I64, _P, _F32, _F32, _F32, _F32, _P]),
     'cc_tower_bwd_dw': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_reduce': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_transpose': (C.c_int, [C.POINTER(TowerArgs), _P]),

@@ -64,7 +64,7 @@ constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
 // DEC_SCALAR: the BCE epilogue in scalar fp32 ops (built with -fno-slp-vectorize) instead of
 // packed v_pk_* pairs
 #ifndef DEC_SCALAR
-#define DEC_SCALAR 1
+#define DEC_SCALAR 0
 #endif
 #ifndef DEC_YS_LATE   // build knob: 0 stages the target words with the Wo slice, before the first barrier
 #define DEC_YS_LATE 1
@@ -345,6 +345,9 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   // soffset).  DEC_D16HI: the odd row by buffer_store_short_d16_hi straight from the pair (inline
   // asm: the compiler counts no vmcnt for it — a later counted wait can only over-wait, never
   // under-wait, since this store is younger than every load it counts)
+#ifdef DEC_DIAG_NODZ   // diagnostic builds only (tools/micro/dec_probe2.hip): no dz stores
+#define DEC_STORE_PAIR(PK, R2) do { (void)(PK); } while (0)
+#else
 #define DEC_STORE_PAIR(PK, R2)                                                                           \
   do {                                                                                                    \
     const uint32_t so0 = 2u * (uint32_t)((((R2) & 3) + 8 * ((R2) >> 2)) * LZ);                           \
@@ -356,14 +359,19 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     else                                                                                                  \
       __builtin_amdgcn_raw_buffer_store_b16((uint16_t)((PK) >> 16), dz_rs, zv, so1, DEC_DZ_CPOL);         \
   } while (0)
+#endif
 #pragma unroll
   for (int ps = 0; ps < npass; ++ps) {
     if constexpr (YS_LATE && DEC_YS_FIRST) {
+#ifndef DEC_DIAG_NOY
       if (ps == 0) load_ys();   // before the prefetch: the epilogue's wait for them leaves it in flight
+#endif
     }
     if (!RING1 && ps + 1 < npass) load_a(af[(ps + 1) & 1], ps + 1);
     if constexpr (YS_LATE && !DEC_YS_FIRST) {
+#ifndef DEC_DIAG_NOY
       if (ps == 0) load_ys();   // the youngest loads: nothing before pass 0's epilogue waits for them
+#endif
     }
     if (ps * 256 + w * 32 >= B) continue;          // wave-uniform: rows beyond B
     f32x16_t acc[NJ];  // starts at the bias (exactly): z = bo + sum_k D3 Wo accumulates in the MFMA
@@ -390,12 +398,14 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
       if (RING1 && kk + NAF < nkk) af[0][kk % NAF] = *reinterpret_cast<const bf16x8_t *>(asrc + (kk + NAF) * astr);
     }
     if (RING1 && ps + 1 < npass) load_a(af[0], ps + 1);   // the next pass's head under this epilogue
+#ifndef DEC_DIAG_NOY
     if constexpr (YS_LATE) {
       if (ps == 0) {   // (every wave is here: B >= 256)
         store_ys();
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       }
     }
+#endif
     DEC_PROBE(2 + 2 * ps);
     if constexpr (SPLIT2) {
       if (ps == npass - 1) {   // this wave reads the Wo slice no more (its fragment reads returned)
@@ -404,7 +414,11 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
       }
     }
     if constexpr (DMA && DEC_PRIO_TOGGLE && npass > 1) {   // (wave-uniform: w from readfirstlane)
-      if ((__builtin_amdgcn_readfirstlane(w) >> 2) == (ps & 1))
+      // 1: the half (w >> 2) == (ps & 1) leads pass ps; 3: the reverse (the younger half leads pass
+      // 0); 2: the younger half (waves 4-7, the arbitration loser) at priority 1 throughout
+      const int hw = __builtin_amdgcn_readfirstlane(w) >> 2;
+      const bool hi = DEC_PRIO_TOGGLE == 2 ? hw == 1 : DEC_PRIO_TOGGLE == 3 ? hw != (ps & 1) : hw == (ps & 1);
+      if (hi)
         __builtin_amdgcn_s_setprio(1);
       else
         __builtin_amdgcn_s_setprio(0);
@@ -433,7 +447,13 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         float lp[2] = {1.f, 1.f}, rsa[2] = {0.f, 0.f}, csa[2] = {0.f, 0.f};
         uint4 yw[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) yw[g] = *reinterpret_cast<const uint4 *>(ys + j * B + rb + 8 * g + 4 * half);
+        for (int g = 0; g < 4; ++g) {
+#ifdef DEC_DIAG_NOY   // diagnostic builds only: targets taken as all zero (no staging, no barrier)
+          yw[g] = make_uint4(0u, 0u, 0u, 0u);
+#else
+          yw[g] = *reinterpret_cast<const uint4 *>(ys + j * B + rb + 8 * g + 4 * half);
+#endif
+        }
         const uint32_t ysh = 31u - (uint32_t)(lane & 31);   // the lane's target bit -> bit 31
 #pragma unroll
         for (int r2 = 0; r2 < 16; r2 += 2) {
@@ -467,7 +487,13 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         // the 16 rows' target words: 4 runs of 4 consecutive rows -> 4 LDS reads of 16 B
         uint4 yw[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) yw[g] = *reinterpret_cast<const uint4 *>(ys + j * B + rb + 8 * g + 4 * half);
+        for (int g = 0; g < 4; ++g) {
+#ifdef DEC_DIAG_NOY   // diagnostic builds only: targets taken as all zero (no staging, no barrier)
+          yw[g] = make_uint4(0u, 0u, 0u, 0u);
+#else
+          yw[g] = *reinterpret_cast<const uint4 *>(ys + j * B + rb + 8 * g + 4 * half);
+#endif
+        }
         const uint32_t ysh = 31u - (uint32_t)(lane & 31);   // the lane's target bit -> bit 31
 #pragma unroll
         for (int r2 = 0; r2 < 16; r2 += 2) {

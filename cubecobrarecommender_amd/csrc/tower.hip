@@ -15,6 +15,7 @@
 #include "adam.hpp"
 #include "common.hpp"
 #include "mx8.hpp"
+#include "noise_dev.hpp"
 #include "xt.hpp"
 
 // dev-only timing hook (tools/micro/tower_probe.hip defines it); compiled out of the library
@@ -315,6 +316,9 @@ __global__ __launch_bounds__(NT) void tower_bwd_chain_kernel(TowerP p) {
 // current layer's MFMAs run — weights do not depend on the activations, so every layer after
 // the first starts with its operands already in flight.
 constexpr int FNT = 512;  // 8 waves
+#ifndef TF_CPB   // cc_tower_bwd_chain_noise: cubes of F per 512-thread workgroup (2 or 4)
+#define TF_CPB 4
+#endif
 constexpr int FB = 16;    // fragments per tile: reduction length <= 256
 
 struct Frags {
@@ -544,12 +548,36 @@ __global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
 
 // ADAM: blocks past the chains run TF Adam over a flat range (cc_tower_bwd_chain_adam) on the CUs
 // the 16-32 latency-bound chain blocks leave idle; the chains launch first, so they start at once.
-template <int D, bool ADAM>
+// NOISE (cc_tower_bwd_chain_noise): the next blocks draw F of the NEXT step, one cube per block on
+// all 512 threads (noise_dev.hpp) — F is latency-bound like the chains, and by the tower backward
+// every batch buffer F writes (x rows / bits, y bits, reg rows) has been read for this step.
+template <int D, bool ADAM, bool NOISE = false>
 __global__ __launch_bounds__(FNT) void tower_bwd_chain_fast_kernel(TowerP p, cc_adam::Args ad,
-                                                                   cc_adam::Args ad1, const int64_t *ad_state) {
-  if (ADAM && (int)blockIdx.x >= p.R / RB) {  // (two flat ranges, one after the other)
-    cc_adam::range_u<4>(ad, ad_state[0], (int)blockIdx.x - p.R / RB, (int)gridDim.x - p.R / RB);
-    if (ad1.n > 0) cc_adam::range_u<4>(ad1, ad_state[0], (int)blockIdx.x - p.R / RB, (int)gridDim.x - p.R / RB);
+                                                                   cc_adam::Args ad1, const int64_t *ad_state,
+                                                                   cc_noise_args na = {}, int64_t bpe = 1) {
+  // F: TF_CPB cubes per block, one per FNT / TF_CPB threads (the chains' 173 VGPRs allow one
+  // 512-thread block per CU: a cube per block would need two rounds of the ~240 free CUs)
+  constexpr int FT = FNT / TF_CPB;
+  const int nchain = p.R / RB, nf = NOISE ? (na.B + TF_CPB - 1) / TF_CPB : 0;
+  if (NOISE && (int)blockIdx.x >= nchain && (int)blockIdx.x < nchain + nf) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t fsm[];
+    __shared__ int s_k[TF_CPB];
+    const int64_t step = na.state[0];
+    int64_t batch = na.state[1] + 1, epoch = na.state[2];
+    if (batch >= bpe) {
+      batch = 0;
+      epoch += 1;
+    }
+    const int h = threadIdx.x / FT, cube = TF_CPB * ((int)blockIdx.x - nchain) + h;
+    const int fw = 4 * ((na.V + 31) / 32) + FT + 1;   // one slice's LDS words
+    // (the last block's slices past B end here: their waves leave the barriers to the others)
+    if (cube < na.B) ccnoise::noise_block<FT>(na, fsm + h * fw, s_k[h], cube, step + 1, batch, epoch);
+    return;
+  }
+  if (ADAM && (int)blockIdx.x >= nchain + nf) {  // (two flat ranges, one after the other)
+    const int b = (int)blockIdx.x - nchain - nf, nb = (int)gridDim.x - nchain - nf;
+    cc_adam::range_u<4>(ad, ad_state[0], b, nb);
+    if (ad1.n > 0) cc_adam::range_u<4>(ad1, ad_state[0], b, nb);
     return;
   }
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1365,7 +1393,8 @@ extern "C" int cc_tower_fwd(const cc_tower_args *t, void *stream) {
 
 static int tower_bwd_launch(const cc_tower_args *t, void *stream, bool chain, bool dw,
                             const cc_adam::Args *ad = nullptr, const int64_t *ad_state = nullptr,
-                            int ad_blocks = 0, const cc_adam::Args *ad1 = nullptr) {
+                            int ad_blocks = 0, const cc_adam::Args *ad1 = nullptr,
+                            const cc_noise_args *na = nullptr, int64_t bpe = 1) {
   TowerP p;
   int rc = make_params(t, p);
   if (rc) return rc;
@@ -1379,14 +1408,26 @@ static int tower_bwd_launch(const cc_tower_args *t, void *stream, bool chain, bo
   if (t->dtype == CC_BF16) {
     if (chain && p.d <= 256) {
       const cc_adam::Args a0 = ad ? *ad : cc_adam::Args{}, a1 = ad1 ? *ad1 : cc_adam::Args{};
-      const dim3 ga(gc.x + (ad ? ad_blocks : 0));
-#define CHAIN_FAST(DD)                                                                              \
-  if (ad)                                                                                           \
-    hipLaunchKernelGGL((tower_bwd_chain_fast_kernel<DD, true>), ga, dim3(FNT), lds_chain, s, p, a0, \
-                       a1, ad_state);                                                               \
-  else                                                                                              \
-    hipLaunchKernelGGL((tower_bwd_chain_fast_kernel<DD, false>), gc, dim3(FNT), lds_chain, s, p, a0, \
-                       a1, ad_state);
+      const int nf = na ? (na->B + TF_CPB - 1) / TF_CPB : 0;
+      const dim3 ga(gc.x + nf + (ad ? ad_blocks : 0));
+      // F's blocks (TF_CPB cubes each): their cube / cut / ycut / add bitmasks and scans in the same
+      // dynamic LDS
+      const size_t lds_f = na ? (size_t)TF_CPB * (4 * ((na->V + 31) / 32) + FNT / TF_CPB + 1) * 4 : 0;
+      const size_t lds_cf = std::max(lds_chain, lds_f);
+      const cc_noise_args nn = na ? *na : cc_noise_args{};
+#define CHAIN_FAST(DD)                                                                                    \
+  if (na && ad)                                                                                           \
+    hipLaunchKernelGGL((tower_bwd_chain_fast_kernel<DD, true, true>), ga, dim3(FNT), lds_cf, s, p, a0, a1, \
+                       ad_state, nn, bpe);                                                                \
+  else if (na)                                                                                            \
+    hipLaunchKernelGGL((tower_bwd_chain_fast_kernel<DD, false, true>), ga, dim3(FNT), lds_cf, s, p, a0,    \
+                       a1, ad_state, nn, bpe);                                                            \
+  else if (ad)                                                                                            \
+    hipLaunchKernelGGL((tower_bwd_chain_fast_kernel<DD, true>), ga, dim3(FNT), lds_chain, s, p, a0, a1,    \
+                       ad_state, cc_noise_args{}, (int64_t)1);                                            \
+  else                                                                                                    \
+    hipLaunchKernelGGL((tower_bwd_chain_fast_kernel<DD, false>), gc, dim3(FNT), lds_chain, s, p, a0, a1,   \
+                       ad_state, cc_noise_args{}, (int64_t)1);
       switch (p.d) {
         case 64: CHAIN_FAST(64) break;
         case 128: CHAIN_FAST(128) break;
@@ -1444,6 +1485,42 @@ extern "C" int cc_tower_bwd_chain_adam(const cc_tower_args *t, float *p, float *
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(cus - t->R / RB, 8)));
   return tower_bwd_launch(t, stream, true, false, &a, state, blocks, &a1);
 }
+// the chains + F of the NEXT step (cc_noise_fwd's arguments; {step, batch, epoch} advanced as the
+// Adam + F launch does) + optionally TF Adam over [lo0, lo0 + n0) and [lo1, lo1 + n1) (n0 = n1 = 0:
+// none), in one launch
+extern "C" int cc_tower_bwd_chain_noise(const cc_tower_args *t, const cc_noise_args *next, int64_t batches_per_epoch,
+                                        float *p, float *m, float *v, const float *g, uint16_t *shadow,
+                                        int64_t lo0, int64_t n0, int64_t lo1, int64_t n1, const int64_t *state,
+                                        float lr, float beta1, float beta2, float eps, void *stream) {
+  CC_REQUIRE(t && t->dtype == CC_BF16 && t->d <= 256,
+             "cc_tower_bwd_chain_noise: the bf16 fast chains (d <= 256) only");
+  CC_REQUIRE(next && next->V > 0 && next->B > 0 && next->x_cap > 0 && next->cube_ptr && next->cube_idx &&
+                 next->perm && next->cdf && next->neg_sampler && next->state && next->x_cnt && next->x_idx &&
+                 next->y_bits && next->status && (!next->with_reg || next->reg_idx),
+             "cc_tower_bwd_chain_noise: F arguments");
+  CC_REQUIRE(next->xt_bits == nullptr,
+             "cc_tower_bwd_chain_noise: F may not set xt bits here (the W1 gradient still reads them)");
+  CC_REQUIRE(next->num_perms >= 1 && next->num_cubes >= next->batch_stride && batches_per_epoch >= 1,
+             "cc_tower_bwd_chain_noise: num_perms / num_cubes / batches_per_epoch");
+  CC_REQUIRE((size_t)TF_CPB * (4 * ((next->V + 31) / 32) + FNT / TF_CPB + 1) * 4 <= 150 * 1024,
+             "cc_tower_bwd_chain_noise: V too large");
+  const int64_t n = n0 + n1;
+  if (n == 0)
+    return tower_bwd_launch(t, stream, true, false, nullptr, nullptr, 0, nullptr, next, batches_per_epoch);
+  CC_REQUIRE(p && m && v && g && state, "cc_tower_bwd_chain_noise: null Adam pointer");
+  CC_REQUIRE(((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g) % 16 == 0 && lo0 % 4 == 0 && lo1 % 4 == 0,
+             "cc_tower_bwd_chain_noise: buffers must be 16-byte aligned, range starts multiples of 4");
+  CC_REQUIRE(!shadow || (uintptr_t)shadow % 8 == 0, "cc_tower_bwd_chain_noise: shadow must be 8-byte aligned");
+  CC_REQUIRE(lo0 >= 0 && n0 >= 0 && n1 >= 0 && (n1 == 0 || lo1 >= lo0 + n0), "cc_tower_bwd_chain_noise: ranges");
+  const cc_adam::Args a{p + lo0, m + lo0, v + lo0, g + lo0, shadow ? (bf16_t *)shadow + lo0 : nullptr, n0,
+                        lr, beta1, beta2, eps, lo0};
+  const cc_adam::Args a1{p + lo1, m + lo1, v + lo1, g + lo1, shadow ? (bf16_t *)shadow + lo1 : nullptr, n1,
+                         lr, beta1, beta2, eps, lo1};
+  const int64_t want = cdiv(cdiv(n, 4), (int64_t)FNT * 4);
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, 256));
+  return tower_bwd_launch(t, stream, true, false, &a, state, blocks, &a1, next, batches_per_epoch);
+}
+
 extern "C" int cc_tower_bwd_dw(const cc_tower_args *t, void *stream) {
   return tower_bwd_launch(t, stream, false, true);
 }

@@ -42,6 +42,9 @@ class TrainConfig:
     #                                gradient is then never stored; bench.py turns it on)
     wo_adam_in_tower: bool = False  # with fuse_w1_adam, bf16 d <= 256 (fused output layers): TF Adam on
     #                                the decoder output layers' tails in the tower backward launch (bench.py)
+    f_in_tower: bool = False       # one process, bf16 fast chains: the NEXT step's F as extra workgroups
+    #                                of the tower backward launch (cc_tower_bwd_chain_noise; every batch
+    #                                buffer F writes is free by then) instead of the Adam launch (bench.py)
     wo_tower_frac: float = -1.0    # ... on this trailing fraction of each; the rest stays in the Adam + F
     #                                launch (< 0: measured per mode — 0.6 BCE only, 0.55 with the
     #                                sampled regulariser; bench.py --wo-tower-frac sweeps)
@@ -492,6 +495,11 @@ class Trainer:
                     lo = b
                 self.rest_ranges = rest
         self.wo_range = self.wo_ranges[0] if self.wo_ranges else None   # (tests: is the placement on)
+        # the next step's F in the tower backward launch: one process with F prefetched (xt bits by
+        # the tower forward's transpose, so F sets none the W1 gradient still reads), the packed
+        # Adam launch, the fast bf16 chains
+        self.f_in_tower = (cfg.f_in_tower and self.adam_packs and self.xt_in_tower and self.fused_tower
+                           and self.dtype == L.CC_BF16 and cfg.d <= 256 and not self.full_reg)
         self._adv_deferred = False   # the previous step's counter advance rides in the E1 gather
         self.noise_ready = False
         self.perms = None
@@ -1069,7 +1077,14 @@ class Trainer:
         s = self._s
         if self.fused_tower:
             t = self._tick('cc_tower_bwd')
-            if self.wo_ranges is not None:   # + TF Adam on the output layers' tails beside the chains
+            if self.f_in_tower:              # + F of the next step (+ the output layers' Adam tails)
+                rg = list(self.wo_ranges or []) + [(0, 0), (0, 0)]
+                (a0, b0), (a1, b1) = rg[0], rg[1]
+                L.call('cc_tower_bwd_chain_noise', L.C.byref(self.targs), L.C.byref(self._noise_args()),
+                       self.batches_per_epoch, L.ptr(self.params), L.ptr(self.m), L.ptr(self.v), L.ptr(self.grads),
+                       L.ptr(self.shadow), a0, b0 - a0, a1, b1 - a1, L.ptr(self.state), cfg.lr, cfg.beta1,
+                       cfg.beta2, cfg.eps, s)
+            elif self.wo_ranges is not None:   # + TF Adam on the output layers' tails beside the chains
                 (a0, b0), (a1, b1) = self.wo_ranges[0], (self.wo_ranges + [(0, 0)])[1]
                 L.call('cc_tower_bwd_chain_adam', L.C.byref(self.targs), L.ptr(self.params), L.ptr(self.m),
                        L.ptr(self.v), L.ptr(self.grads), L.ptr(self.shadow), a0, b0 - a0, a1, b1 - a1,
@@ -1142,18 +1157,21 @@ class Trainer:
         t = self._tick('cc_adam_dense')
         if self.prefetch:     # + F for the next step in the same launch
             na = self._noise_args()
+            # (f_in_tower: F of the next step is already drawn in the tower backward launch)
+            fn = 'cc_adam_pack2' if self.f_in_tower else 'cc_adam_noise_pack2'
             if self.adam_packs and self.rest_ranges is not None:   # the complement of the tower launch's
                 o = self.w1_off                                      # ranges (pack offsets count from o)
                 (a0, b0), (a1, b1) = self.rest_ranges[0], (self.rest_ranges + [(o, o)])[1]
-                L.call('cc_adam_noise_pack2', L.ptr(self.params[o:]), L.ptr(self.m[o:]), L.ptr(self.v[o:]),
+                L.call(fn, L.ptr(self.params[o:]), L.ptr(self.m[o:]), L.ptr(self.v[o:]),
                        L.ptr(self.grads[o:]), L.ptr(self.shadow[o:]), a0 - o, b0 - a0, a1 - o, b1 - a1,
                        cfg.lr, cfg.beta1, cfg.beta2, cfg.eps, L.C.byref(na), self.batches_per_epoch,
                        L.C.byref(self.adam_pack), L.stream_ptr(stream))
             elif self.adam_packs:   # + packed tower images + step counters
                 o = self.w1_off if self.fuse_w1 else 0   # (W1 already updated by its gradient kernel)
-                L.call('cc_adam_noise_pack', L.ptr(self.params[o:]), L.ptr(self.m[o:]), L.ptr(self.v[o:]),
-                       L.ptr(self.grads[o:]), L.ptr(self.shadow[o:]), n - o, cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,
-                       L.C.byref(na), self.batches_per_epoch, L.C.byref(self.adam_pack), L.stream_ptr(stream))
+                L.call(fn, L.ptr(self.params[o:]), L.ptr(self.m[o:]), L.ptr(self.v[o:]),
+                       L.ptr(self.grads[o:]), L.ptr(self.shadow[o:]), 0, n - o, 0, 0, cfg.lr, cfg.beta1,
+                       cfg.beta2, cfg.eps, L.C.byref(na), self.batches_per_epoch, L.C.byref(self.adam_pack),
+                       L.stream_ptr(stream))
             else:
                 L.call('cc_adam_noise', L.ptr(self.params), L.ptr(self.m), L.ptr(self.v),
                        L.ptr(self.grads), L.ptr(self.shadow), n, cfg.lr, cfg.beta1, cfg.beta2, cfg.eps,

@@ -153,6 +153,11 @@ int cc_adam_noise_pack2(float *p, float *m, float *v, const float *g, uint16_t *
                         int64_t n0, int64_t lo1, int64_t n1, float lr, float beta1, float beta2, float eps,
                         const cc_noise_args *next, int64_t batches_per_epoch, const cc_adam_pack *pack,
                         void *stream);
+/* cc_adam_noise_pack2 without F (the next step's F drawn by cc_tower_bwd_chain_noise); `next` is
+ * checked as there but not drawn. */
+int cc_adam_pack2(float *p, float *m, float *v, const float *g, uint16_t *shadow, int64_t lo0, int64_t n0,
+                  int64_t lo1, int64_t n1, float lr, float beta1, float beta2, float eps,
+                  const cc_noise_args *next, int64_t batches_per_epoch, const cc_adam_pack *pack, void *stream);
 
 /* ----------------------------------------------------------------------------------
  * E1 forward: H[r] = ReLU(sum_{j in x_r} W1[j] + b1).  Replaces Dense(d)(x) on the 0/1
@@ -416,6 +421,16 @@ int cc_tower_bwd_chain(const cc_tower_args *t, void *stream);
 int cc_tower_bwd_chain_adam(const cc_tower_args *t, float *p, float *m, float *v, const float *g,
                             uint16_t *shadow, int64_t lo0, int64_t n0, int64_t lo1, int64_t n1,
                             const int64_t *state, float lr, float beta1, float beta2, float eps, void *stream);
+/* cc_tower_bwd_chain plus F of the NEXT step (generator.py:38-103, exactly cc_noise_fwd's draws for
+ * the state {step + 1, batch + 1 (epoch rollover at batches_per_epoch), epoch}, as the Adam + F
+ * launch draws them) in extra workgroups, two cubes each, and — when n0 + n1 > 0 — TF Adam over two
+ * flat ranges as cc_tower_bwd_chain_adam.  F writes x / y / reg rows but no xt bits (next->xt_bits
+ * must be NULL: the W1 gradient after this launch still reads them); every batch buffer it writes
+ * has been read for this step by the tower backward.  bf16 fast chains (d <= 256) only. */
+int cc_tower_bwd_chain_noise(const cc_tower_args *t, const cc_noise_args *next, int64_t batches_per_epoch,
+                             float *p, float *m, float *v, const float *g, uint16_t *shadow, int64_t lo0,
+                             int64_t n0, int64_t lo1, int64_t n1, const int64_t *state, float lr, float beta1,
+                             float beta2, float eps, void *stream);
 int cc_tower_bwd_dw(const cc_tower_args *t, void *stream);
 int cc_tower_reduce(const cc_tower_args *t, void *stream);
 /* bf16: every layer's dW/db written directly (no slabs, no reduce): cc_tower_bwd_dw +

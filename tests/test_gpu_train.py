@@ -36,12 +36,12 @@ def _assert_within(e, tol, step):
     assert not bad, (step, bad)
 
 
-def _setup(V, d, B, C, reg, dtype, seed=3, sizes=(20, 40, 80), fused_tower=True, prefetch=True):
+def _setup(V, d, B, C, reg, dtype, seed=3, sizes=(20, 40, 80), fused_tower=True, prefetch=True, **kw):
     lists, Mt, ns = problem(seed, C, V, sizes)
     P = model_ref.init_params(V, d, seed=seed, bias_std=0.01)
     lay = Layout(V, d)
     cfg = TrainConfig(V=V, d=d, batch_size=B, reg=reg, dtype=dtype, seed=seed, fused_tower=fused_tower,
-                      prefetch_noise=prefetch)
+                      prefetch_noise=prefetch, **kw)
     data = DeviceDataset(lists, V, y_mtx=Mt.astype(np.float32) if reg > 0 else None, neg_sampler=ns)
     tr = Trainer(cfg, data, params_flat=lay.pack(P))
     perm = np.random.default_rng(seed).permutation(C).astype(np.int32)
@@ -184,13 +184,15 @@ def test_graph_replay_matches_eager_and_epochs_roll_over():
 @pytest.mark.parametrize('reg', [0.0, 0.1])
 def test_noise_prefetch_is_exact(reg):
     """F drawn in the previous step's Adam launch (cc_adam_noise) == F at the head of the step:
-    identical parameters and losses over epoch roll-overs, eager and as graph replays."""
+    identical parameters and losses over epoch roll-overs, eager and as graph replays; and F drawn
+    in the previous step's tower backward launch (f_in_tower, cc_tower_bwd_chain_noise)."""
     V, d, B, C = 700, 64, 32, 128          # 4 batches per epoch
     perms = np.stack([np.random.default_rng(s).permutation(C) for s in (1, 2)]).astype(np.int32)
     trs = []
-    for prefetch, graphs in ((False, False), (True, False), (True, True)):
-        tr, *_ = _setup(V, d, B, C, reg, 'bf16', prefetch=prefetch)
-        assert tr.prefetch == prefetch
+    for prefetch, graphs, ft in ((False, False, False), (True, False, False), (True, True, False),
+                                 (True, False, True), (True, True, True)):
+        tr, *_ = _setup(V, d, B, C, reg, 'bf16', prefetch=prefetch, f_in_tower=ft)
+        assert tr.prefetch == prefetch and tr.f_in_tower == ft
         tr.set_epoch_permutations(perms)
         if graphs:
             tr.capture()
@@ -199,7 +201,7 @@ def test_noise_prefetch_is_exact(reg):
         for tr in trs:
             tr.step()
         torch.cuda.synchronize()
-        assert trs[0].losses() == trs[1].losses() == trs[2].losses()
+        assert all(tr.losses() == trs[0].losses() for tr in trs[1:])
     for tr in trs:
         tr.flush()
     for tr in trs[1:]:
@@ -333,18 +335,21 @@ def test_fused_w1_adam_matches_unfused(reg):
     gradient values), over eager steps and graph replays.  With wo_adam_in_tower as well: the
     output layers' trailing parts (Wo, and Wo_reg with the regulariser) updated in the tower
     backward launch (cc_tower_bwd_chain_adam, cc_adam::range_u) and the rest in two ranges of the
-    Adam + F launch (cc_adam_noise_pack2) — the same bits again."""
+    Adam + F launch (cc_adam_noise_pack2) — the same bits again; and with f_in_tower, the next step's
+    F drawn by the tower backward launch (cc_tower_bwd_chain_noise, two cubes per workgroup) and the
+    Adam launch without it (cc_adam_pack2)."""
     out = {}
-    for fuse, wo in ((False, False), (True, False), (True, True)):
+    for fuse, wo, ft in ((False, False, False), (True, False, False), (True, True, False), (True, True, True),
+                         (True, False, True)):
         lists, Mt, ns = problem(11, 1024, 2500, (20, 40, 80))
         P = model_ref.init_params(2500, 256, seed=11, bias_std=0.01)
         lay = Layout(2500, 256)
         cfg = TrainConfig(V=2500, d=256, batch_size=256, reg=reg, dtype='bf16', seed=11, fuse_w1_adam=fuse,
-                          wo_adam_in_tower=wo)
+                          wo_adam_in_tower=wo, f_in_tower=ft)
         tr = Trainer(cfg, DeviceDataset(lists, 2500, y_mtx=Mt.astype(np.float32) if reg > 0 else None,
                                         neg_sampler=ns), params_flat=lay.pack(P))
         tr.set_epoch_permutation(np.random.default_rng(11).permutation(1024).astype(np.int32))
-        assert tr.fuse_w1 == fuse and tr.adam_packs and (tr.wo_range is not None) == wo
+        assert tr.fuse_w1 == fuse and tr.adam_packs and (tr.wo_range is not None) == wo and tr.f_in_tower == ft
         losses = []
         for _ in range(2):
             tr.step()
@@ -355,15 +360,16 @@ def test_fused_w1_adam_matches_unfused(reg):
             losses.append(tr.losses())
         tr.flush()
         torch.cuda.synchronize()
-        out[fuse, wo] = (tr.params.cpu(), tr.m.cpu(), tr.v.cpu(), tr.shadow.cpu(), losses)
-    for key in ((True, False), (True, True)):
-        for a, b in zip(out[False, False][:4], out[key][:4]):
-            assert torch.equal(a, b)
-        assert out[False, False][4] == out[key][4]
+        out[fuse, wo, ft] = (tr.params.cpu(), tr.m.cpu(), tr.v.cpu(), tr.shadow.cpu(), losses)
+    base = out[False, False, False]
+    for key in ((True, False, False), (True, True, False), (True, True, True), (True, False, True)):
+        for a, b in zip(base[:4], out[key][:4]):
+            assert torch.equal(a, b), key
+        assert base[4] == out[key][4], key
 
 
-@pytest.mark.parametrize('reg', [0.0, 0.1])
-def test_step_many_multi_graph_matches_single_steps(reg):
+@pytest.mark.parametrize('reg,ft', [(0.0, False), (0.1, False), (0.0, True), (0.1, True)])
+def test_step_many_multi_graph_matches_single_steps(reg, ft):
     """step_many — graph_steps (here 4; remainders by the graphs of its halves) whole steps per captured graph replay, the loss
     accumulated inside the graph — gives bit-identical parameters, moments, shadow, device
     counters and accumulated losses to the same number of single step() calls (bench.py's
@@ -374,7 +380,7 @@ def test_step_many_multi_graph_matches_single_steps(reg):
         P = model_ref.init_params(2500, 256, seed=13, bias_std=0.01)
         lay = Layout(2500, 256)
         cfg = TrainConfig(V=2500, d=256, batch_size=128, reg=reg, dtype='bf16', seed=13, fuse_w1_adam=True,
-                          wo_adam_in_tower=True, graph_steps=4 if multi else 1)
+                          wo_adam_in_tower=True, f_in_tower=ft, graph_steps=4 if multi else 1)
         tr = Trainer(cfg, DeviceDataset(lists, 2500, y_mtx=Mt.astype(np.float32) if reg > 0 else None,
                                         neg_sampler=ns), params_flat=lay.pack(P))
         tr.set_epoch_permutation(np.random.default_rng(13).permutation(1024).astype(np.int32))
