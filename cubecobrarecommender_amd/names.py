@@ -12,12 +12,16 @@ restated here:
 The tables are restated for the blocks card names and their typographic variants use: Latin-1
 Supplement (x000), Latin Extended-A (x001), the Latin Extended-B letters with a plain base, Greek
 (x003, basic letters), Cyrillic (x004, basic letters), General Punctuation (x020), Letterlike
-Symbols / Number Forms (x021: the (tm)-style and Roman-numeral entries).  A code point outside
-them is decomposed (NFKD) and its base letters looked up the same way — that matches unidecode
-for the accented letters of other Latin blocks (x01e: Vietnamese etc.).  What neither covers (CJK,
-whose unidecode tables give pinyin/romaji, and other scripts) keeps its characters, so such a
-name simply misses the id map: parity unpinned there (no reference output exists in this
-pipeline: the reference's ml_files/*_id_map.json are Git-LFS pointers).
+Symbols / Number Forms (x021: the (tm)-style and Roman-numeral entries), and for the Korean and
+Japanese printings: the Hangul syllables (xac..xd7, which unidecode's tables spell out as the
+syllable's initial + medial + final jamo romanisation — generated here from the same three
+lists) and the hiragana / katakana of x030 (Kunrei-style: si, ti, tu, hu; small kana as their
+full-size letter; the prolonged-sound mark '-').  A code point outside them is decomposed (NFKD)
+and its base letters looked up the same way — that matches unidecode for the accented letters of
+other Latin blocks (x01e: Vietnamese etc.).  What none covers (CJK ideographs, whose unidecode
+tables give pinyin with a trailing space, and other scripts) keeps its characters, so such a name
+simply misses the id map: parity unpinned everywhere outside ASCII (no reference output exists
+in this pipeline: the reference's ml_files/*_id_map.json are Git-LFS pointers).
 """
 import unicodedata
 
@@ -74,11 +78,35 @@ for i, r in enumerate(['I', 'II', 'III', 'IV', 'V', 'VI', 'VII', 'VIII', 'IX', '
     _PUNCT[chr(0x2160 + i)] = r
     _PUNCT[chr(0x2170 + i)] = r.lower()
 
+# Hangul syllables U+AC00..U+D7A3 = 0xAC00 + (initial * 21 + medial) * 28 + final
+_HANGUL_INITIAL = ['g', 'gg', 'n', 'd', 'dd', 'r', 'm', 'b', 'bb', 's', 'ss', '', 'j', 'jj', 'c', 'k', 't', 'p', 'h']
+_HANGUL_MEDIAL = ['a', 'ae', 'ya', 'yae', 'eo', 'e', 'yeo', 'ye', 'o', 'wa', 'wae', 'oe', 'yo', 'u', 'weo', 'we',
+                  'wi', 'yu', 'eu', 'yi', 'i']
+_HANGUL_FINAL = ['', 'g', 'gg', 'gs', 'n', 'nj', 'nh', 'd', 'l', 'lg', 'lm', 'lb', 'ls', 'lt', 'lp', 'lh', 'm',
+                 'b', 'bs', 's', 'ss', 'ng', 'j', 'c', 'k', 't', 'p', 'h']
+
+
+def _hangul(cp):
+    i = cp - 0xAC00
+    return _HANGUL_INITIAL[i // (21 * 28)] + _HANGUL_MEDIAL[(i // 28) % 21] + _HANGUL_FINAL[i % 28]
+
+
+# x030: hiragana U+3041..U+3094 (katakana U+30A1..U+30F4 are the same syllables + 0x60)
+_KANA = ('a a i i u u e e o o ka ga ki gi ku gu ke ge ko go sa za si zi su zu se ze so zo ta da ti di tu tu du '
+         'te de to do na ni nu ne no ha ba pa hi bi pi hu bu pu he be pe ho bo po ma mi mu me mo ya ya yu yu '
+         'yo yo ra ri ru re ro wa wa wi we wo n vu').split(' ')
+assert len(_KANA) == 0x3094 - 0x3041 + 1
+_JP = {chr(0x3041 + i): r for i, r in enumerate(_KANA)}
+_JP.update({chr(0x30A1 + i): r for i, r in enumerate(_KANA)})
+_JP.update({'ヵ': 'ka', 'ヶ': 'ke', 'ヷ': 'va', 'ヸ': 'vi', 'ヹ': 've', 'ヺ': 'vo', 'ー': '-', '・': '*',
+            '　': ' ', '、': ',', '。': '.', '「': '[', '」': ']', '『': '[[', '』': ']]'})
+
 _TABLE = {chr(0x80 + i): r for i, r in enumerate(_X000)}
 _TABLE.update({chr(0x100 + i): r for i, r in enumerate(_X001A)})
 _TABLE.update(_GREEK)
 _TABLE.update(_CYR)
 _TABLE.update(_PUNCT)
+_TABLE.update(_JP)
 
 
 def _repl(ch):
@@ -90,6 +118,8 @@ def _repl(ch):
     r = _TABLE.get(ch)
     if r is not None:
         return r
+    if 0xAC00 <= cp <= 0xD7A3:
+        return _hangul(cp)
     # other blocks: NFKD base letters, each looked up again (combining marks -> '')
     dec = unicodedata.normalize('NFKD', ch)
     if dec != ch:

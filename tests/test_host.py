@@ -81,7 +81,7 @@ def test_fused_kernel_extent_gates():
 
 def test_names_unidecode_restatement():
     """N3 (ml_recommend.py:44): unidecode(name.lower()) restated for Latin-1 / Latin Extended-A,
-    Greek, Cyrillic, punctuation and number forms (Unidecode 1.1.1's per-code-point tables);
+    Greek, Cyrillic, punctuation and number forms, Hangul and kana (Unidecode 1.1.1's tables);
     ASCII passes through unchanged, combining marks vanish, private use maps to ''."""
     from cubecobrarecommender_amd.names import normalize, unidecode
     cases = {
@@ -99,3 +99,10 @@ def test_names_unidecode_restatement():
     # every restated Latin-1 / Extended-A entry is ASCII
     for cp in range(0x80, 0x180):
         assert unidecode(chr(cp)).isascii(), hex(cp)
+    # Korean printings: Hangul syllables as initial + medial + final jamo romanisation (unidecode's
+    # xac..xd7 tables); Japanese kana (x030, Kunrei style).  Parity unpinned (no reference output)
+    assert unidecode('안녕') == 'annyeong' and unidecode('한국어') == 'hangugeo'
+    assert unidecode('힣') == 'hih' and unidecode('가') == 'ga'
+    assert unidecode('ドラゴン') == 'doragon' and unidecode('しつ') == 'situ' and unidecode('カード') == 'ka-do'
+    for cp in list(range(0xAC00, 0xD7A4, 97)) + list(range(0x3041, 0x3095)) + list(range(0x30A1, 0x30F5)):
+        assert unidecode(chr(cp)).isascii() and unidecode(chr(cp)), hex(cp)

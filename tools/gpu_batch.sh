@@ -1,1 +1,1 @@
-bash tools/gpu_run.sh r05g "tests:tests/test_gpu_train.py -k \"fused_w1 or prefetch\"" "bench:--f-in-tower 0" "bench:--f-in-tower 1 --wo-tower-frac 0.3" "bench:--f-in-tower 1" "bench:--f-in-tower 1 --wo-tower-frac 0" "bench:--f-in-tower 0"
+bash tools/gpu_run.sh r05h2 "py:tools/run_smoke.py" "fullbench:--steps 20 --warmup 5" "prof:" 
