@@ -9,6 +9,7 @@ LIB_PATH = os.environ.get('CCREC_LIB') or os.path.join(_HERE, 'libccrec_hip.so')
 CC_F32, CC_BF16, CC_MX8 = 0, 1, 2
 CC_EPI_STORE, CC_EPI_BCE, CC_EPI_MASK, CC_EPI_SPLITK = 0, 1, 2, 3
 CC_NUM_TENSORS = 24
+CC_KL_REGISTER_TARGETS = 1     # cc_dec_kl_args.flags bit 0
 
 
 class CCError(RuntimeError):
@@ -70,7 +71,7 @@ class DecKlArgs(C.Structure):
         ('reg_idx', C.c_void_p),
         ('scale', C.c_float), ('dZ', C.c_void_p), ('gW', C.c_void_p), ('gb', C.c_void_p),
         ('loss_partials', C.c_void_p), ('loss_out', C.c_void_p), ('loss_scale', C.c_double),
-        ('ticket', C.c_void_p), ('ws', C.c_void_p),
+        ('ticket', C.c_void_p), ('ws', C.c_void_p), ('flags', C.c_int32),
     ]
 
 

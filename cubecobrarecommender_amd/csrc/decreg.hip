@@ -27,6 +27,11 @@
 
 #include "common.hpp"
 
+// build knob (dev A/B, tools/micro/kl_probe_full.hip -DKL_MS=0): the main pass's M~ staged through LDS
+#ifndef KL_MS
+#define KL_MS 1
+#endif
+
 // dev-only timing hook (tools/micro/kl_probe.hip defines it); compiled out of the library
 #ifndef KL_PROBE
 #define KL_PROBE(k)
@@ -52,6 +57,7 @@ constexpr float LN_PMIN = -16.11809565095832f;  // ln(1e-7)
 
 
 typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
+typedef __attribute__((address_space(3))) void lds_void;
 
 struct KlP {
   int d, V, rows, ldt, row0, nsl;
@@ -68,6 +74,7 @@ struct KlP {
   int mt_lo;                        // first card whose M~ row is resident
   float *part_m, *part_s, *part_d;  // [rows][nsl]
   float4 *rowstat;                  // [rows] {m + ln s, -, S, sum t ln t}
+  float2 *rowst2;                   // [rows] {m + ln s, S} (the main pass's MS staging)
   uint32_t *flag;                   // [1] an element with p < 1e-7 was seen this step
 };
 
@@ -84,6 +91,12 @@ __device__ __forceinline__ bf16x8_t frag(const bf16_t *S, int off) {
   return *reinterpret_cast<const bf16x8_t *>(S + off);
 }
 __device__ __forceinline__ uint16_t bf16_bits(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+// a + b never contracted into an fma with b's producer (-ffp-contract=fast would, or not, depending
+// on the surrounding code): the bias column sums carry the same bits in every code shape
+__device__ __forceinline__ float add_nc(float a, float b) {
+  asm volatile("" : "+v"(b));
+  return a + b;
+}
 
 // Wo [d][V] slice [n0, n0 + NB) -> LDS k-contiguous image Wt[NB][d] (swizzled); columns past V clamp
 template <int D>
@@ -340,16 +353,20 @@ __global__ __launch_bounds__(256) void kl_merge_kernel(KlP p) {
   if (lane == 0) {
     const int card = p.reg_idx[row];
     const float2 ts = card >= 0 ? reinterpret_cast<const float2 *>(p.tsum)[card] : make_float2(0.f, 0.f);
-    p.rowstat[row] = make_float4(m + __logf(s), 0.f, ts.x, ts.y);   // {m + ln s, -, S, C}: ln p = z - .x
+    // (one value for both images: m + ln s contracts differently if written twice)
+    const float lse = m + __logf(s);
+    p.rowstat[row] = make_float4(lse, 0.f, ts.x, ts.y);   // {m + ln s, -, S, C}: ln p = z - .x
+    p.rowst2[row] = make_float2(lse, ts.x);
   }
 }
 
 // ---------------------------------------------------------------- main
 template <int NB>
 struct MainSmem {
-  bf16_t Zt[NB * TR];       // dZ^T tile [NB][TR] (swizzled)
+  bf16_t Zt[NB * TR];       // dZ^T tile [NB][TR] (swizzled); staged M~ (kl_slice's MS mode)
   float4 rs[TR];            // row stats of the tile
-  int32_t card[TR];         // M~ row byte offset of the tile's rows (0x80000000: padding row)
+  int32_t card[2][TR];      // M~ row byte offset of the tile's rows (0x80000000: padding row) in [0];
+                            // MS: the raw card of tile t's rows in [t & 1]
   float red_cs[NTH / 64][NB];
   double red_loss[NTH / 64];
   int lastflag;
@@ -361,11 +378,55 @@ struct MainSmem {
 // waves' accumulators across all row tiles instead of the per-tile gW read-modify-write — the
 // 48 extra registers pushed the logits' fragment ring from 16 to 8 and spilled, and the logits
 // phases then waited on L2 twice as long: 1,620 -> 2,015 us per block, tools/micro/kl_probe_full.hip.)
-template <int D, bool FIX, int CPOL = 0, bool DW = true>
+__device__ __forceinline__ int32_t card_off(int card, int V) {
+  return card >= 0 ? (int32_t)((uint32_t)card * (uint32_t)V * 4u) : (int32_t)0x80000000u;
+}
+
+// MS's LDS-DMAs are written as inline asm: the compiler's wait insertion treats a pending
+// LDS-DMA as a possible writer of every later LDS read (no alias information here) and put a
+// vmcnt(0) before the logits' Wo-slice reads and the epilogue's row-stat reads, draining the
+// very DMAs meant to run under them.  Invisible to it, they only make its own counted waits
+// stricter than needed (it counts fewer younger accesses than there are); the slots' own waits
+// are the explicit ones in kl_slice.
+typedef __attribute__((ext_vector_type(4))) int32_t v4i;
+__device__ __forceinline__ v4i sgpr_rsrc(const void *base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  return v4i{__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)a), __builtin_amdgcn_readfirstlane((int32_t)(a >> 32) & 0xFFFF),
+             __builtin_amdgcn_readfirstlane((int32_t)bytes), 0x00020000};
+}
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const lds_void *)p);
+}
+// lane L: 'size' bytes at rsrc + voff + soff -> LDS lds + size L.  (M0 is reserved — not a
+// clobber the compiler takes — and nothing else in these kernels reads it: checked in the ISA.)
+template <int SIZE, int CPOL>
+__device__ __forceinline__ void dma_asm(const v4i &rs, uint32_t voff, uint32_t soff, uint32_t lds) {
+  static_assert(SIZE == 16 || SIZE == 4, "dwordx4 / dword");
+  if constexpr (SIZE == 16 && CPOL == KL_CPOL_NT)
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, %3 offen nt lds" ::"v"(voff), "s"(rs), "s"(lds), "s"(soff) : "memory");
+  else if constexpr (SIZE == 16)
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds" ::"v"(voff), "s"(rs), "s"(lds), "s"(soff) : "memory");
+  else
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dword %0, %1, %3 offen lds" ::"v"(voff), "s"(rs), "s"(lds), "s"(soff) : "memory");
+}
+
+// MS: the DMA of M~ [32 rows][32 columns] (column tile j of a wave's row block) into the wave's LDS
+// slot, row-major: instruction i moves rows 8i .. 8i + 7, lane L 16 B of row 8i + (L >> 3) at
+// columns 4 (L & 7) .. (sof: the rows' byte offsets + the lane's column chunk)
+template <int CPOL>
+__device__ __forceinline__ void ms_dma(const v4i &rs, const uint32_t (&sof)[4], int j, const float *slot) {
+  const uint32_t a = lds_addr(slot);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dma_asm<16, CPOL>(rs, sof[i], 128u * j, a + 1024u * i);
+}
+
+template <int D, bool FIX, int CPOL = 0, bool DW = true, bool MS = false>
 __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt, MainSmem<kl_nb<D>()> &sm) {
   constexpr int NB = kl_nb<D>(), NJ = NB / 32;
   constexpr int CHB = TR / 8;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
+  // (w through readfirstlane: wave-uniform to the compiler, so the per-wave conditions below are
+  // scalar branches and the counted waits of each path stay exact)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), half = lane >> 5;
   const int n0 = sl * NB;
   const int V = p.V;
   KL_PROBE(0);
@@ -388,20 +449,81 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   const __amdgpu_buffer_rsrc_t dz_rs =
       __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)p.rows * (uint32_t)V * 2u, 0x00020000);
   const float scale = p.scale;
+  const v4i mt_rs4 = sgpr_rsrc(p.Mt, p.mt_bytes);
   constexpr int ND2 = (D + 255) / 256;   // phase 2's d tiles of wave w: 32w .. (and 32(w + 8) .. at d = 512)
   // PF (the main pass with dWo done elsewhere: many row tiles, nothing of phase 2 live): the next
   // row block's A fragments load right after this block's logits MFMAs, so their L2 / MALL round
   // trip runs under this block's epilogue instead of heading the next logits phase (tools/micro/
   // kl_probe_full.hip: ~5 of the ~12 us per 256-row pass were logits waiting on their fragments)
   constexpr bool PF = !FIX && !DW && D <= 256;
+  // MS (PF; the launcher checks |V| % 4 == 0 and the offsets' ranges): M~ staged through the LDS
+  // the dZ^T tile would use (free without phase 2): each wave DMAs its next row block's M~ into
+  // its own NJ slots [32 rows][32 columns], slot j right after this pass's epilogue has read it,
+  // so a slot's HBM round trip runs under the rest of the epilogue and the next logits instead of
+  // being issued at the head of the pass it feeds (~7 of ~12 us per pass were the logits waiting
+  // behind the M~ loads, tools/micro/kl_probe_full.hip).  The slots hold no registers, which pays
+  // for the full 16-fragment ring: the logits no longer refill A fragments behind M~ either.
+  constexpr bool MSX = MS && PF;
   // all A fragments first in the memory queue, then M~ (d = 512: a ring of 16; PF: the next block's
   // first 8 under the epilogue, the other 8 refilled during the MFMAs — 16 would spill)
-  LFrag<D, PF ? 8 : (D / 16 < 16 ? D / 16 : 16)> lf;
+  LFrag<D, (PF && !MSX) ? 8 : (D / 16 < 16 ? D / 16 : 16)> lf;
   bool lf_ready = false;
+  float *const stg = reinterpret_cast<float *>(sm.Zt) + w * (32 * NB);
+  static_assert(!MSX || NB * TR * 2 == 8 * 32 * NB * 4, "MS: 8 waves' slots fill the Zt tile");
+  // MSX: the slots' waits.  An LDS-DMA is counted by vmcnt like any other vector-memory access.
+  // Slot j's DMA is issued after that slot's 16 dZ stores, so between it (the previous pass) and
+  // the wait for it lie, in issue order: the later slots' (NJ - 1 - j) x (stores 16 + DMA 4), the
+  // part_d store (1); this pass's A prefetch (nkk, when it has a next pass) and its earlier
+  // slots' j x (stores 16 + DMA 4 when it has a next pass).  The counts below are the minimum of
+  // those over j — lower bounds of the younger accesses — so a wait never releases before its
+  // slot has landed.  (Stores before the DMA: the compiler's own wait for the A prefetch, which
+  // sees only the 48 + 1 stores behind it, then releases on the oldest stores, not on a DMA.)
+  constexpr int NKK = D / 16;
+  constexpr int MS_CNT_N = 20 * (NJ - 1) + NKK;   // this pass has a next pass (part_d not counted)
+  constexpr int MS_CNT_L = 16 * (NJ - 1);         // the wave's last pass
+  static_assert(!MSX || MS_CNT_N <= 63, "vmcnt's range");
+  // MSX: no global load may wait behind the slots' DMAs (a wait on a load also waits on every
+  // older access), so the next tile's row stats {m + ln s, S} and raw cards are DMA'd too, at the
+  // head of this tile's pass 0, into the other half of double-buffered LDS (rs2, card); the
+  // slots' waits of pass 1 cover them (older) and the tile-top barrier publishes them.  Slice 0's
+  // sum of t ln t over the live rows (rowstat.w) is then added after the tile loop.
+  float2(*const rs2)[TR] = reinterpret_cast<float2(*)[TR]>(sm.rs);
+  static_assert(sizeof(sm.rs) == 2 * TR * sizeof(float2), "rs2 overlays rs");
+  const v4i st_rs = sgpr_rsrc(p.rowst2, (uint32_t)p.rows * 8u), ri_rs = sgpr_rsrc(p.reg_idx, (uint32_t)p.rows * 4u);
+
+  if constexpr (MSX) {   // the first tile: staged by the threads (published by the tile-top barrier)
+    for (int i = tid; i < min(TR, p.rows); i += NTH) {
+      rs2[0][i] = p.rowst2[i];
+      sm.card[0][i] = p.reg_idx[i];
+    }
+    // the wave's first row block (tile 0, rows 32w ..): A fragments and slots, all landed before
+    // the loop (a wait the compiler sees, so its state entering the loop holds no pending
+    // fragment loads to merge with the loop's own counted waits)
+    if (w * 32 < min(TR, p.rows)) {
+      logits_load(p, (p.row0 + w * 32) / 32, lf);
+      const uint32_t c4 = 4u * (uint32_t)(n0 + 4 * (lane & 7));
+      uint32_t s0[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = w * 32 + (lane >> 3) + 8 * i;
+        s0[i] = (uint32_t)card_off(row < p.rows ? p.reg_idx[row] : -1, V) + c4;
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) ms_dma<CPOL>(mt_rs4, s0, j, stg + j * 1024);
+      lf_ready = true;
+    }
+    asm volatile("" ::: "memory");   // (the loads may not sink below the wait)
+    __builtin_amdgcn_s_waitcnt(0);
+  }
 
   for (int t0 = 0; t0 < p.rows; t0 += TR) {
     const int nt = min(TR, p.rows - t0);
-    lds_barrier();  // previous tile's phase 2 done with Zt / rs
+    const int cur = MSX ? (t0 / TR) & 1 : 0;
+    const int32_t *const cardc = sm.card[cur];
+    // the row offset of tile row i (MSX: from the raw card)
+    auto rowoff = [&](int i) -> uint32_t { return MSX ? (uint32_t)card_off(cardc[i], V) : (uint32_t)cardc[i]; };
+    lds_barrier();  // previous tile's phase 2 done with Zt / rs (MSX: this tile's staged stats landed)
+    if constexpr (!MSX)
     for (int i = tid; i < nt; i += NTH) {
       float4 st = p.rowstat[t0 + i];
       if constexpr (FIX) {  // .z <- delta of the row: the sum of its slices' partials, in order
@@ -413,7 +535,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       sm.rs[i] = st;
       const int card = p.reg_idx[t0 + i];
       if (!FIX && sl == 0 && card >= 0) klc += st.w;
-      sm.card[i] = card >= 0 ? (int32_t)((uint32_t)card * (uint32_t)V * 4u) : (int32_t)0x80000000u;
+      sm.card[0][i] = card_off(card, V);
     }
     lds_barrier();
     KL_PROBE(1);
@@ -428,12 +550,44 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       // issued before its logits, so their HBM latency runs under the MFMAs.
       uint32_t roff[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) roff[r] = (uint32_t)sm.card[rb + acc_row(r, lane)];
+      for (int r = 0; r < 16; ++r) roff[r] = rowoff(rb + acc_row(r, lane));
       uint32_t zrow = (uint32_t)((t0 + rb + 4 * half) * V + n0 + (lane & 31));
       asm volatile("" : "+v"(zrow));  // per-pass base of the dZ stores (no hoisted 64-bit addresses)
-      if (!PF || !lf_ready) logits_load(p, (p.row0 + t0 + rb) / 32, lf);
+      if (!MSX && (!PF || !lf_ready)) logits_load(p, (p.row0 + t0 + rb) / 32, lf);
+      // PF: this wave's next row block — pass 1 of this tile, or pass 0 of the next (wave-uniform)
+      int t1 = 0, rb1 = 0;
+      bool nxt = false;
+      if constexpr (PF) {
+        t1 = ps == 0 && 256 + w * 32 < nt ? t0 : t0 + TR;
+        rb1 = t1 == t0 ? 256 + w * 32 : w * 32;
+        nxt = t1 < p.rows && rb1 < min(TR, p.rows - t1);
+      }
       float tv[NJ][16];
-      if constexpr (!FIX) {
+      uint32_t sof[4];      // MSX: the next block's DMA rows
+      if constexpr (MSX) {
+        const uint32_t c4 = 4u * (uint32_t)(n0 + 4 * (lane & 7));
+        if (ps == 0 && t0 + TR < p.rows) {
+          // the next tile's stats (waves 0-3) and cards (4, 5), read after the tile-top barrier;
+          // and each wave's own next-tile rows 32w .. 32w + 63 again (identical values), read by
+          // this wave alone before that barrier (below: its own vmcnt covers them)
+          const int nx = cur ^ 1;
+          int lane = threadIdx.x & 63;
+          asm volatile("" : "+v"(lane));   // per tile: no per-lane offsets held across the loop
+          if (w < 4)
+            dma_asm<16, 0>(st_rs, 16u * lane, (uint32_t)(t0 + TR + 128 * w) * 8u, lds_addr(&rs2[nx][128 * w]));
+          else if (w < 6)
+            dma_asm<16, 0>(ri_rs, 16u * lane, (uint32_t)(t0 + TR + 256 * (w - 4)) * 4u, lds_addr(&sm.card[nx][256 * (w - 4)]));
+          dma_asm<4, 0>(ri_rs, 4u * lane, (uint32_t)(t0 + TR + 32 * w) * 4u, lds_addr(&sm.card[nx][32 * w]));
+        }
+        if (nxt) {
+          const int32_t *cn = sm.card[(t1 / TR) & 1];
+          // the next tile's rows (this wave's own DMA of pass 0; younger since: that pass's A
+          // prefetch nkk, stores 16 NJ, slot DMAs 4 NJ, part_d 1 — more than 63)
+          if (t1 != t0) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sof[i] = (uint32_t)card_off(cn[rb1 + (lane >> 3) + 8 * i], V) + c4;
+        }
+      } else if constexpr (!FIX) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const uint32_t gc4 = 4u * (uint32_t)(n0 + j * 32 + (lane & 31));
@@ -445,11 +599,10 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       __builtin_amdgcn_sched_barrier(0);
       f32x16_t acc[NJ];
       logits_mfma(Wt, lf, bias, acc);
-      if constexpr (PF) {   // this wave's next row block: pass 1 of this tile, or pass 0 of the next
-        const int t1 = ps == 0 && 256 + w * 32 < nt ? t0 : t0 + TR;
-        const int rb1 = t1 == t0 ? 256 + w * 32 : w * 32;
-        lf_ready = t1 < p.rows && rb1 < min(TR, p.rows - t1);   // (wave-uniform)
+      if constexpr (PF) {
+        lf_ready = nxt;
         if (lf_ready) logits_load(p, (p.row0 + t1 + rb1) / 32, lf);
+        __builtin_amdgcn_sched_barrier(0);
       }
       KL_PROBE(2 + 2 * ps);
       bool deadp = false;   // an element of this pass has p < 1e-7
@@ -462,12 +615,31 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int col = j * 32 + (lane & 31);
+        if constexpr (MSX) {
+          if (nxt)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MS_CNT_N) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MS_CNT_L) : "memory");
+          const float *slot = stg + j * 1024;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) tv[j][r] = slot[acc_row(r, lane) * 32 + (lane & 31)];
+        }
         uint16_t tt[16];
         // row stats re-read per column tile (an opaque base): held across the three tiles they
         // cost 64 VGPRs, LDS has the bandwidth
         int rsofs = 0;
         asm volatile("" : "+v"(rsofs));
         const float4 *rsp = sm.rs + rsofs;
+        const float2 *rsp2 = rs2[cur] + rsofs;
+        // {m + ln s, S (FIX: delta)} of tile row i
+        auto rstat = [&](int i) -> float2 {
+          if constexpr (MSX) {
+            return rsp2[i];
+          } else {
+            const float4 q = rsp[i];
+            return make_float2(q.x, q.z);
+          }
+        };
         // the common case — all rows real, all 32 columns inside V: no per-element masks, the
         // clip of q folded into one med3 (ln clip(p, 1e-7, 1) = med3(ln p, ln 1e-7, 0)), the
         // dead-element test as a running min of p
@@ -475,25 +647,28 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
         if (fast) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const float4 st = rsp[rb + acc_row(r, lane)];
+            const float2 st = rstat(rb + acc_row(r, lane));
             const float lp = acc[j][r] - st.x;  // ln p = z - (m + ln s)
             const float pr = __builtin_amdgcn_exp2f(lp * LOG2E);
             const float tc = __builtin_amdgcn_fmed3f(tv[j][r], PMIN, 1.f);
             klsum = fmaf(-tc, __builtin_amdgcn_fmed3f(lp, LN_PMIN, 0.f), klsum);   // (+ t ln t: rowstat.w)
             mn = fminf(mn, pr);
-            const float dzf = scale * fmaf(pr, st.z, pr >= PMIN ? -tc : 0.f);
+            const float dzf = scale * fmaf(pr, st.y, pr >= PMIN ? -tc : 0.f);
             const uint16_t zb = bf16_bits(dzf);
             tt[r] = zb;
-            cs[j] += dzf;  // the bias gradient sums the fp32 dz
+            // the bias gradient sums the fp32 dz (an uncontracted add: the same bits whichever way
+            // the compiler shapes the surrounding code — MS vs register targets)
+            cs[j] = add_nc(cs[j], dzf);
             // the lane part of the offset in a VGPR, the row part (r) as the scalar soffset
-            __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, 2u * (zrow + (uint32_t)(j * 32)),
-                                                  2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), CPOL);
+            if constexpr (!MSX)
+              __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, 2u * (zrow + (uint32_t)(j * 32)),
+                                                    2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), CPOL);
           }
         } else {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int lr = rb + acc_row(r, lane);
-            const float4 st = rsp[lr];
+            const float2 st = rstat(lr);
             const bool live_row = roff[r] < 0x80000000u && valid[j];
             const float lp = acc[j][r] - st.x;  // ln p = z - (m + ln s)
             const float pr = __builtin_amdgcn_exp2f(lp * LOG2E);
@@ -505,9 +680,9 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
               const float term = -tc * lq;   // (the row's sum of t ln t: rowstat.w, added once)
               klsum += live_row ? term : 0.f;
               deadp |= live_row && !live;
-              dz = live_row ? scale * (pr * st.z - (live ? tc : 0.f)) : 0.f;
+              dz = live_row ? scale * (pr * st.y - (live ? tc : 0.f)) : 0.f;
             } else {
-              dz = live_row ? -scale * pr * st.z : 0.f;  // st.z = delta
+              dz = live_row ? -scale * pr * st.y : 0.f;  // st.y = delta
             }
             const uint32_t zoff = 2u * (zrow + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V + j * 32));
             uint16_t zb;
@@ -520,9 +695,9 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
             } else {
               zb = bf16_bits(dz);
               tt[r] = zb;
-              cs[j] += dz;
+              cs[j] = add_nc(cs[j], dz);
             }
-            if (valid[j]) __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, CPOL);
+            if (!MSX && valid[j]) __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, CPOL);
           }
         }
         if constexpr (DW) {
@@ -530,6 +705,19 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
           for (int g = 0; g < 4; ++g)
             *reinterpret_cast<uint2 *>(sm.Zt + sw_off(col, rb + 8 * g + 4 * half, CHB)) =
                 *reinterpret_cast<const uint2 *>(&tt[4 * g]);
+        }
+        if constexpr (MSX) {
+          // the tile's 16 dZ stores after the fast / slow branches merge: in either they would sit
+          // in blocks the compiler's flow graph can bypass (infeasibly), and its counted waits then
+          // assume no store behind the A prefetch and drain the slots' DMAs before the logits
+          const uint32_t zl = valid[j] ? 2u * (zrow + (uint32_t)(j * 32)) : 0x80000000u;   // past V: dropped
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            __builtin_amdgcn_raw_buffer_store_b16(tt[r], dz_rs, zl, 2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), CPOL);
+          if (nxt) {   // slot j is free (read above): the next block's column tile j
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            ms_dma<CPOL>(mt_rs4, sof, j, stg + j * 1024);
+          }
         }
       }
       deadp |= mn < PMIN;
@@ -539,18 +727,25 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
         // p < 1e-7 (rare: zero unless the wave saw such an element); read by the fix kernel
         float red = 0.f;
         if (__ballot(deadp) != 0ull) {
+          // per column tile (one tile's targets live at a time), the same order of additions
           float dl[16];
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float4 st = sm.rs[rb + acc_row(r, lane)];
-            float a = 0.f;
+          for (int r = 0; r < 16; ++r) dl[r] = 0.f;
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-              const float pr = __builtin_amdgcn_exp2f((acc[j][r] - st.x) * LOG2E);
+          for (int j = 0; j < NJ; ++j) {
+            float tj[16];
+            const uint32_t gc4 = 4u * (uint32_t)(n0 + j * 32 + (lane & 31));
+#pragma unroll
+            for (int r = 0; r < 16; ++r)   // MSX: the slots hold the next block by now: from memory
+              tj[r] = MSX ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mt_rs, roff[r] + gc4, 0, CPOL))
+                          : tv[j][r];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float st_x = MSX ? rs2[cur][rb + acc_row(r, lane)].x : sm.rs[rb + acc_row(r, lane)].x;
+              const float pr = __builtin_amdgcn_exp2f((acc[j][r] - st_x) * LOG2E);
               const bool live_row = roff[r] < 0x80000000u && valid[j];
-              a += live_row && !(pr >= PMIN) ? __builtin_amdgcn_fmed3f(tv[j][r], PMIN, 1.f) : 0.f;
+              dl[r] += live_row && !(pr >= PMIN) ? __builtin_amdgcn_fmed3f(tj[r], PMIN, 1.f) : 0.f;
             }
-            dl[r] = a;
           }
           red = rs16<false>(dl);
         }
@@ -633,6 +828,11 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
     }
   }
 
+  if constexpr (MSX) {   // slice 0: each live row's sum_j t ln t, once (see rs2 above)
+    if (sl == 0)
+      for (int i = tid; i < p.rows; i += NTH)
+        if (p.reg_idx[i] >= 0) klc += p.rowstat[i].w;
+  }
   KL_PROBE(7);
   // ---- epilogue: dbo, loss partial, the fix flag
 #pragma unroll
@@ -692,11 +892,11 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   }
 }
 
-template <int D, int CPOL, bool DW>
+template <int D, int CPOL, bool DW, bool MS = false>
 __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
   __shared__ __attribute__((aligned(16))) bf16_t Wt[kl_nb<D>() * D];
   __shared__ __attribute__((aligned(16))) MainSmem<kl_nb<D>()> sm;
-  kl_slice<D, false, CPOL, DW>(p, blockIdx.x, Wt, sm);
+  kl_slice<D, false, CPOL, DW, MS>(p, blockIdx.x, Wt, sm);
 }
 
 // The exact-clip correction: a small persistent grid (FIXG blocks) that leaves at once when the
@@ -857,7 +1057,7 @@ __global__ __launch_bounds__(256) void kl_tsum_kernel(const float *__restrict__ 
 
 extern "C" size_t cc_dec_kl_ws_size(int32_t rows, int32_t V) {
   const int64_t nsl = cdiv(V, NB_MIN);   // an upper bound over every d
-  return (size_t)(3 * rows * nsl * sizeof(float) + rows * sizeof(float4) + 256);
+  return (size_t)(3 * rows * nsl * sizeof(float) + rows * sizeof(float4) + 256 + rows * sizeof(float2));
 }
 
 extern "C" int32_t cc_dec_kl_blocks(int32_t V) { return (int32_t)cdiv(V, NB_MIN); }   // upper bound over d
@@ -917,11 +1117,16 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
   p.part_s = p.part_m + pn;
   p.part_d = p.part_s + pn;
   p.flag = (uint32_t *)(p.part_d + pn);
+  p.rowst2 = (float2 *)(ws + a->rows * sizeof(float4) + 3 * pn * sizeof(float) + 256);   // (16-B aligned: rows % 32)
   hipStream_t s = as_stream(stream);
   const dim3 gs((unsigned)p.nsl), gm((unsigned)p.nsl);
   // many row tiles (full mode): dWo from the stored dZ by kl_dwo_kernel (even V: 4-B aligned rows);
   // one tile (the sampled regulariser): in the main pass, from its LDS dZ^T tile
   const bool dw_sep = a->rows > TR && a->V % 2 == 0;
+  // M~ staged through LDS by 16-B DMAs (kl_slice's MS): 16-B aligned rows, and the padding /
+  // past-V sentinel 0x80000000 outside both buffers' ranges
+  const bool ms = a->V % 4 == 0 && ((uintptr_t)a->Mt & 15) == 0 && (int64_t)a->rows * a->V * 2 < 0x80000000ll && KL_MS &&
+                  !(a->flags & CC_KL_REGISTER_TARGETS);
 #define KL_LAUNCH(DD)                                                                                          \
   if (a->d == DD) {                                                                                          \
     hipLaunchKernelGGL((kl_stats_kernel<DD>), gs, dim3(NTH), 0, s, p);                                      \
@@ -929,7 +1134,10 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
     hipLaunchKernelGGL(kl_merge_kernel, dim3((unsigned)cdiv(a->rows, 4)), dim3(256), 0, s, p);              \
     CC_LAUNCH_CHECK("kl_merge_kernel");                                                                      \
     if (dw_sep) {                                                                                            \
-      hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, false>), gm, dim3(NTH), 0, s, p);                   \
+      if (ms)                                                                                                \
+        hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, false, (DD <= 256)>), gm, dim3(NTH), 0, s, p);    \
+      else                                                                                                   \
+        hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, false>), gm, dim3(NTH), 0, s, p);                 \
       CC_LAUNCH_CHECK("kl_main_kernel");                                                                     \
       hipLaunchKernelGGL((kl_fix_kernel<DD, false>), dim3(FIXG), dim3(NTH), 0, s, p);                       \
       CC_LAUNCH_CHECK("kl_fix_kernel");                                                                      \

@@ -420,6 +420,7 @@ class Trainer:
             self.tsum = torch.zeros(hi - lo, 2, **f32)    # per M~ row {sum t, sum t ln t} (t clipped), once
             L.call('cc_kl_tsum', L.ptr(data.y_reg), hi - lo, V, L.ptr(self.tsum), L.stream_ptr())
             self.kl_ws = torch.zeros(int(L.lib().cc_dec_kl_ws_size(self.Breg, V)) // 4 + 4, **f32)
+            self.kl_flags = 0   # cc_dec_kl_args.flags (tests: CC_KL_REGISTER_TARGETS, the A/B of decreg.hip's M~ staging)
             self.kl_part = torch.zeros(max(int(L.lib().cc_dec_kl_blocks(V)), 1), device=self.dev,
                                        dtype=torch.float64)
         if self.full_reg:
@@ -866,7 +867,7 @@ class Trainer:
                              gW=self.gp('decoder_for_reg/reconstruct/kernel'),
                              gb=self.gp('decoder_for_reg/reconstruct/bias'), loss_partials=L.ptr(self.kl_part),
                              loss_out=L.ptr(self.loss_dev[1:]), loss_scale=float(self.kl_loss_scale),
-                             ticket=L.ptr(self.tickets[1:]), ws=L.ptr(self.kl_ws))
+                             ticket=L.ptr(self.tickets[1:]), ws=L.ptr(self.kl_ws), flags=self.kl_flags)
             L.call('cc_dec_softmax_kl_dw', L.C.byref(ka), s)
             t()
         elif self.use_reg:

@@ -508,7 +508,10 @@ typedef struct cc_dec_kl_args {
   double loss_scale;
   uint32_t *ticket;
   void *ws;
+  int32_t flags;             /* bit 0 CC_KL_REGISTER_TARGETS: the main pass keeps M~ in registers instead
+                                of staging it through LDS (an A/B knob: bit-identical results; 0 default) */
 } cc_dec_kl_args;
+#define CC_KL_REGISTER_TARGETS 1
 size_t cc_dec_kl_ws_size(int32_t rows, int32_t V);
 int32_t cc_dec_kl_blocks(int32_t V);
 int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream);

@@ -455,6 +455,49 @@ def test_fused_regulariser_clip_fix_path(V, B, d):
                                       'encoder/encoded_1/kernel')}, TOL['bf16'], 0)
 
 
+@pytest.mark.parametrize('V,spread', [(2500, True), (2502, True), (2500, False)])
+def test_full_mode_clip_fix_path(V, spread):
+    """Full mode (all |V| identity rows, several 512-row tiles per slice) with the exact-clip
+    path live: the bias spread of the clip test above pushes part of every softmax row below
+    1e-7.  V = 2,500: the main pass stages M~ through LDS (decreg.hip MS: its rare-path reload of
+    M~ for the clip partials, its counted waits across tiles); V = 2,502 (V % 4 = 2): the
+    register path.  Against the bf16-emulating oracle over reg_idx = arange(V)."""
+    d, B = 256, 128
+
+    def run(flags):
+        tr, lists, Mt, ns, P, perm = _setup(V, d, B, 4 * B, 0.5, 'bf16', reg_mode='full')
+        assert tr.full_reg and tr.fused_reg
+        rng = np.random.default_rng(V)
+        if spread:
+            P['decoder_for_reg/reconstruct/bias'] = np.linspace(-40, 6, V)[rng.permutation(V)].astype(np.float32)
+        tr.params.copy_(torch.from_numpy(tr.layout.pack(P)))
+        tr.refresh_shadow()
+        tr.kl_flags = flags
+        tr.forward_backward()
+        torch.cuda.synchronize()
+        return tr, lists, Mt, ns, P, perm
+
+    tr, lists, Mt, ns, P, perm = run(0)
+    cdf = noise_ref.cdf_of(ns)
+    cubes = [lists[c] for c in perm[:B]]
+    oxs, oys, _, _ = noise_ref.philox_noise_batch(cubes, cdf, ns, tr.cfg.seed, 0, with_reg=False)
+    losses, grads = model_ref.train_forward_backward(P, oxs, oys, V, d, reg=0.5, reg_idx=np.arange(V), y_reg=Mt,
+                                                     mode='bf16')
+    e = _errs(f'fullclip_{V}_{int(spread)}', 0, tr.losses(), losses, grads, tr.layout.unpack(tr.grads.cpu().numpy()), 0.5)
+    # (the KL loss: most terms at the ln(1e-7) floor, a large total summed in fp32 lanes — 2.3e-6
+    # relative at V = 2,500, the same with M~ in registers: checked bit for bit below)
+    _assert_within({k: e[k] for k in ('decoder_for_reg/reconstruct/kernel', 'decoder_for_reg/reconstruct/bias',
+                                      'decoder_for_reg/decoded_3/kernel', 'encoder/encoded_1/kernel')},
+                   TOL['bf16_full'], 0)
+    assert e['loss/kl'] < 5e-6, e['loss/kl']
+    # the LDS staging of M~ (decreg.hip MS, V % 4 == 0) against the register path: identical bits
+    tr2 = run(L.CC_KL_REGISTER_TARGETS)[0]
+    g1, g2 = tr.layout.unpack(tr.grads.cpu().numpy()), tr.layout.unpack(tr2.grads.cpu().numpy())
+    diff = {k: float(np.abs(g1[k] - g2[k]).max()) for k in g1 if not np.array_equal(g1[k], g2[k])}
+    assert torch.equal(tr2.dZout, tr.dZout) and not diff, diff
+    assert tr2.losses() == tr.losses(), (tr2.losses(), tr.losses())
+
+
 # Eigen's float logistic (TF 2.5's CPU sigmoid) is exactly 1 from this logit on (metrics.hip)
 SIG_SAT = 15.7243833541870117
 
