@@ -27,9 +27,13 @@
 
 #include "common.hpp"
 
-// build knob (dev A/B, tools/micro/kl_probe_full.hip -DKL_MS=0): the main pass's M~ staged through LDS
-#ifndef KL_MS
-#define KL_MS 1
+// diagnostic builds only (tools/micro/kl_probe_full.hip): the register path without its dZ stores /
+// its M~ loads (wrong results; what they cost)
+#ifndef KL_DIAG_NOSTORE
+#define KL_DIAG_NOSTORE 0
+#endif
+#ifndef KL_DIAG_NOMT
+#define KL_DIAG_NOMT 0
 #endif
 
 // dev-only timing hook (tools/micro/kl_probe.hip defines it); compiled out of the library
@@ -91,12 +95,7 @@ __device__ __forceinline__ bf16x8_t frag(const bf16_t *S, int off) {
   return *reinterpret_cast<const bf16x8_t *>(S + off);
 }
 __device__ __forceinline__ uint16_t bf16_bits(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
-// a + b never contracted into an fma with b's producer (-ffp-contract=fast would, or not, depending
-// on the surrounding code): the bias column sums carry the same bits in every code shape
-__device__ __forceinline__ float add_nc(float a, float b) {
-  asm volatile("" : "+v"(b));
-  return a + b;
-}
+
 
 // Wo [d][V] slice [n0, n0 + NB) -> LDS k-contiguous image Wt[NB][d] (swizzled); columns past V clamp
 template <int D>
@@ -420,7 +419,7 @@ __device__ __forceinline__ void ms_dma(const v4i &rs, const uint32_t (&sof)[4], 
   for (int i = 0; i < 4; ++i) dma_asm<16, CPOL>(rs, sof[i], 128u * j, a + 1024u * i);
 }
 
-template <int D, bool FIX, int CPOL = 0, bool DW = true, bool MS = false>
+template <int D, bool FIX, int CPOL = 0, bool DW = true, bool MS = false, bool WS = false>
 __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt, MainSmem<kl_nb<D>()> &sm) {
   constexpr int NB = kl_nb<D>(), NJ = NB / 32;
   constexpr int CHB = TR / 8;
@@ -456,14 +455,27 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   // trip runs under this block's epilogue instead of heading the next logits phase (tools/micro/
   // kl_probe_full.hip: ~5 of the ~12 us per 256-row pass were logits waiting on their fragments)
   constexpr bool PF = !FIX && !DW && D <= 256;
-  // MS (PF; the launcher checks |V| % 4 == 0 and the offsets' ranges): M~ staged through the LDS
-  // the dZ^T tile would use (free without phase 2): each wave DMAs its next row block's M~ into
-  // its own NJ slots [32 rows][32 columns], slot j right after this pass's epilogue has read it,
-  // so a slot's HBM round trip runs under the rest of the epilogue and the next logits instead of
-  // being issued at the head of the pass it feeds (~7 of ~12 us per pass were the logits waiting
-  // behind the M~ loads, tools/micro/kl_probe_full.hip).  The slots hold no registers, which pays
-  // for the full 16-fragment ring: the logits no longer refill A fragments behind M~ either.
+  // MS (PF, opt-in CC_KL_LDS_TARGETS; the launcher checks |V| % 4 == 0 and the offsets' ranges):
+  // M~ staged through the LDS the dZ^T tile would use (free without phase 2): each wave DMAs its
+  // next row block's M~ into its own NJ slots [32 rows][32 columns], slot j right after this pass's
+  // epilogue has read it, so a slot's HBM round trip runs under the rest of the epilogue and the
+  // next logits instead of being issued at the head of the pass it feeds.  The slots hold no
+  // registers, which pays for the full 16-fragment ring: the logits no longer refill A fragments
+  // behind M~.  Measured (tools/micro/kl_probe_full.hip, r05o / r05r): the logits phases halve
+  // (295 -> 138 us over block 0's tiles) but the epilogues wait on the slots longer than that saves
+  // (the four launches 1,583 -> 1,824 us against the register path with 16-B stores) — off.
   constexpr bool MSX = MS && PF;
+  // WSX (PF with M~ in registers; the launcher checks |V| % 8 == 0 and the offsets' range): dZ leaves
+  // through the free dZ^T LDS as 16-B row stores.  The accumulator layout gives a lane one column
+  // of 16 rows, so a direct store writes 2 B per lane — 48 buffer_store_short per lane and pass,
+  // issue-bound (the pass without its dZ stores ran ~20 % faster, kl_probe_full KL_DIAG_NOSTORE).
+  // Instead adjacent lanes pair their bf16 values by one DPP swap into row-major dwords, the wave
+  // writes its [32][96] tile to a private LDS image (208-B pitch: no bank conflicts between the
+  // half-waves' rows), reads it back as 16-B row chunks and stores 6 x 16 B per lane.
+  constexpr bool WSX = WS && PF && !MSX;
+  constexpr int WS_PITCH = 52;   // dwords per image row (96 bf16 + 8 pad)
+  uint32_t *const zimg = reinterpret_cast<uint32_t *>(sm.Zt) + w * (32 * WS_PITCH);
+  static_assert(!WSX || 8 * 32 * WS_PITCH * 4 <= (int)sizeof(sm.Zt), "WS: the images fit the dZ^T tile");
   // all A fragments first in the memory queue, then M~ (d = 512: a ring of 16; PF: the next block's
   // first 8 under the epilogue, the other 8 refilled during the MFMAs — 16 would spill)
   LFrag<D, (PF && !MSX) ? 8 : (D / 16 < 16 ? D / 16 : 16)> lf;
@@ -593,7 +605,8 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
           const uint32_t gc4 = 4u * (uint32_t)(n0 + j * 32 + (lane & 31));
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            tv[j][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mt_rs, roff[r] + gc4, 0, CPOL));
+            tv[j][r] = KL_DIAG_NOMT ? (float)(r + j) * 1e-3f
+                                    : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mt_rs, roff[r] + gc4, 0, CPOL));
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -644,6 +657,17 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
         // clip of q folded into one med3 (ln clip(p, 1e-7, 1) = med3(ln p, ln 1e-7, 0)), the
         // dead-element test as a running min of p
         const bool fast = !FIX && rows_ok && __ballot(!valid[j]) == 0ull;
+        // WSX: rows r - 1, r (r odd) of columns c, c ^ 1 -> one dword per lane, right after row r's
+        // value (so no more than a pair of them is live)
+        auto ws_pair = [&](int r, uint32_t lo, uint32_t hi) {
+          if constexpr (WSX) {
+            const bool odd = lane & 1;
+            const uint32_t give = odd ? lo : hi;
+            const uint32_t got = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)give, 0xB1, 0xF, 0xF, false);   // lane ^ 1
+            const uint32_t dw = odd ? (got | (hi << 16)) : (lo | (got << 16));
+            zimg[(acc_row(r - 1, lane) + (odd ? 1 : 0)) * WS_PITCH + j * 16 + ((lane & 31) >> 1)] = dw;
+          }
+        };
         if (fast) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -653,16 +677,17 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
             const float tc = __builtin_amdgcn_fmed3f(tv[j][r], PMIN, 1.f);
             klsum = fmaf(-tc, __builtin_amdgcn_fmed3f(lp, LN_PMIN, 0.f), klsum);   // (+ t ln t: rowstat.w)
             mn = fminf(mn, pr);
-            const float dzf = scale * fmaf(pr, st.y, pr >= PMIN ? -tc : 0.f);
+            // (the product as fma(.., +0): a rounded value the column sum below cannot contract into
+            // an fma with it — the same bits whichever way the compiler shapes the code, MS or not)
+            const float dzf = fmaf(scale, fmaf(pr, st.y, pr >= PMIN ? -tc : 0.f), 0.f);
             const uint16_t zb = bf16_bits(dzf);
             tt[r] = zb;
-            // the bias gradient sums the fp32 dz (an uncontracted add: the same bits whichever way
-            // the compiler shapes the surrounding code — MS vs register targets)
-            cs[j] = add_nc(cs[j], dzf);
+            cs[j] += dzf;  // the bias gradient sums the fp32 dz
             // the lane part of the offset in a VGPR, the row part (r) as the scalar soffset
-            if constexpr (!MSX)
+            if constexpr (!MSX && !WSX && !KL_DIAG_NOSTORE)
               __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, 2u * (zrow + (uint32_t)(j * 32)),
                                                     2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), CPOL);
+            if (r & 1) ws_pair(r, tt[r - 1], zb);
           }
         } else {
 #pragma unroll
@@ -680,7 +705,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
               const float term = -tc * lq;   // (the row's sum of t ln t: rowstat.w, added once)
               klsum += live_row ? term : 0.f;
               deadp |= live_row && !live;
-              dz = live_row ? scale * (pr * st.y - (live ? tc : 0.f)) : 0.f;
+              dz = live_row ? fmaf(scale, fmaf(pr, st.y, live ? -tc : 0.f), 0.f) : 0.f;
             } else {
               dz = live_row ? -scale * pr * st.y : 0.f;  // st.y = delta
             }
@@ -695,9 +720,11 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
             } else {
               zb = bf16_bits(dz);
               tt[r] = zb;
-              cs[j] = add_nc(cs[j], dz);
+              cs[j] += dz;
             }
-            if (!MSX && valid[j]) __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, CPOL);
+            if (!MSX && !WSX && valid[j]) __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, CPOL);
+            if constexpr (!FIX)
+              if (r & 1) ws_pair(r, tt[r - 1], zb);
           }
         }
         if constexpr (DW) {
@@ -721,6 +748,17 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
         }
       }
       deadp |= mn < PMIN;
+      if constexpr (WSX) {   // the wave's [32][96] dZ image -> 6 x 16 B per lane (chunks past V dropped)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+          const int q = lane + 64 * u, row = q / 12, ch = q % 12;
+          const v4u x = *reinterpret_cast<const v4u *>(zimg + row * WS_PITCH + ch * 4);
+          const uint32_t off = n0 + 8 * ch < V ? 2u * ((uint32_t)(t0 + rb + row) * (uint32_t)V + (uint32_t)(n0 + 8 * ch))
+                                               : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b128(x, dz_rs, off, 0, CPOL);
+        }
+      }
 
       if constexpr (!FIX) {
         // the exact-clip delta partial of each row over this slice: sum of its targets where
@@ -892,11 +930,11 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   }
 }
 
-template <int D, int CPOL, bool DW, bool MS = false>
+template <int D, int CPOL, bool DW, bool MS = false, bool WS = false>
 __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
   __shared__ __attribute__((aligned(16))) bf16_t Wt[kl_nb<D>() * D];
   __shared__ __attribute__((aligned(16))) MainSmem<kl_nb<D>()> sm;
-  kl_slice<D, false, CPOL, DW, MS>(p, blockIdx.x, Wt, sm);
+  kl_slice<D, false, CPOL, DW, MS, WS>(p, blockIdx.x, Wt, sm);
 }
 
 // The exact-clip correction: a small persistent grid (FIXG blocks) that leaves at once when the
@@ -1029,6 +1067,115 @@ __global__ __launch_bounds__(NTH) void kl_dwo_kernel(KlP p) {
   }
 }
 
+// The same product with the dZ stream decoupled from the A fragments (|V| % 8 == 0): 4 producer
+// waves copy dZ chunks global -> LDS by 16-B LDS-DMA, DWP_NS - 1 chunks ahead (120 KB in flight
+// per CU instead of the two register sets' 48 KB), and the 8 compute waves of kl_dwo_kernel only
+// load their A fragments and multiply.  vmcnt is per wave, so a compute wave's wait for its A
+// fragments (one chunk ahead, from L2) never waits on the HBM copies; the producers wait for their
+// own copies and one s_barrier per chunk publishes them.  (In one wave the two streams share one
+// in-order counter: each wait for the A fragments also drains the copies issued before them.)
+// The MFMA sequence per output is kl_dwo_kernel's: the same bits.  Measured: no faster than
+// kl_dwo_kernel (356.6 vs 351.4 us, r05o) — the deeper copy pipeline is not what bounds it.
+constexpr int DWP_NS = 6, DWP_NT = NTH + 256;
+template <int D>
+__global__ __launch_bounds__(DWP_NT) void kl_dwo_pc_kernel(KlP p) {
+  constexpr int NB = DW_NB, NJ = NB / 32, KC = DW_KC, KS = KC / 16;
+  constexpr int CHUNK = KC * NB * 2;              // 24 KB: 24 DMA instructions of 1 KB
+  constexpr int NPI = CHUNK / 1024 / 4;           // per producer wave: 6
+  static_assert(CHUNK % 4096 == 0, "whole instructions per producer wave");
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(1024))) char dwsmem[];
+  bf16_t *Zs = reinterpret_cast<bf16_t *>(dwsmem);   // [DWP_NS][KC * NB]
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), half = lane >> 5;
+  const int n0 = blockIdx.x * NB, V = p.V;
+  const int nch = (p.rows + KC - 1) / KC;
+  if (w >= 8) {   // ---- producers
+    const int pw = w - 8;
+    const v4i zr = sgpr_rsrc(p.dZ, (uint32_t)p.rows * (uint32_t)V * 2u);
+    // instruction i (of this wave): LDS bytes [1024 (NPI pw + i), ..) of the chunk = rows of 192 B
+    uint32_t vo[NPI];
+#pragma unroll
+    for (int i = 0; i < NPI; ++i) {
+      const int b = 1024 * (NPI * pw + i) + 16 * lane, r = b / (NB * 2), off = b % (NB * 2);
+      vo[i] = (uint32_t)(r * V + n0) * 2u + (uint32_t)off;
+    }
+    auto issue = [&](int c) {
+      const uint32_t so = (uint32_t)c * (uint32_t)KC * (uint32_t)V * 2u;   // (< rows V 2 < 4 GB)
+      const uint32_t base = lds_addr(Zs + (c % DWP_NS) * (KC * NB)) + 1024u * (uint32_t)(NPI * pw);
+#pragma unroll
+      for (int i = 0; i < NPI; ++i) dma_asm<16, 0>(zr, vo[i], so, base + 1024u * i);
+    };
+    for (int c = 0; c < min(DWP_NS - 1, nch); ++c) issue(c);
+    for (int c = 0; c < nch; ++c) {
+      // chunk c landed: this wave's younger copies are those of chunks c + 1 .. min(c + NS - 2, nch - 1)
+      const int younger = min(DWP_NS - 2, nch - 1 - c);
+      if (younger >= 4)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * NPI) : "memory");
+      else if (younger == 3)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPI) : "memory");
+      else if (younger == 2)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPI) : "memory");
+      else if (younger == 1)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPI) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      static_assert(DWP_NS - 2 == 4, "the waits above are written for 6 stages");
+      lds_barrier();   // chunk c published; chunk c - 1's stage read by every compute wave
+      if (c + DWP_NS - 1 < nch) issue(c + DWP_NS - 1);
+    }
+    return;
+  }
+  // ---- compute waves (kl_dwo_kernel's)
+  const int wt = blockIdx.y * 8 + w;
+  const bool active = wt * 32 < D;
+  const bf16_t *abase = p.D3tp + ((int64_t)min(wt, D / 32 - 1) * (p.ldt / 16) * 64 + lane) * 8;
+  const int k0 = p.row0 / 16, klast = (p.row0 + p.rows) / 16 - 1;
+  auto load_a = [&](bf16x8_t (&dst)[KS], int c) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      dst[ks] = *reinterpret_cast<const bf16x8_t *>(abase + (int64_t)min(k0 + c * KS + ks, klast) * 512);
+  };
+  f32x16_t acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  bf16x8_t af[2][KS];
+  load_a(af[0], 0);
+  auto body = [&](bf16x8_t (&cur)[KS], bf16x8_t (&nxt)[KS], int c) {
+    lds_barrier();   // chunk c published (the producers' copies landed)
+    load_a(nxt, c + 1);   // (unconditional: clamped past the end, never used)
+    if (active) {
+      const bf16_t *Zc = Zs + (c % DWP_NS) * (KC * NB);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const bf16_t *tb = Zc + (ks * 16 + 8 * half + ((lane >> 2) & 3)) * NB + j * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)tb);
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)(tb + 4 * NB));
+          const bf16x8_t b = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[ks], b, acc[j], 0, 0, 0);
+        }
+    }
+  };
+  int c = 0;
+  for (; c + 1 < nch; c += 2) {
+    body(af[0], af[1], c);
+    body(af[1], af[0], c + 1);
+  }
+  if (c < nch) body(af[0], af[1], c);
+  if (!active) return;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int gc = n0 + j * 32 + (lane & 31);
+    if (gc < V) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) p.gW[(int64_t)(wt * 32 + acc_row(r, lane)) * V + gc] = acc[j][r];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void kl_tsum_kernel(const float *__restrict__ Mt, int V, float *__restrict__ tsum) {
   __shared__ float red[2][4];
   const float *row = Mt + (int64_t)blockIdx.x * V;
@@ -1125,8 +1272,13 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
   const bool dw_sep = a->rows > TR && a->V % 2 == 0;
   // M~ staged through LDS by 16-B DMAs (kl_slice's MS): 16-B aligned rows, and the padding /
   // past-V sentinel 0x80000000 outside both buffers' ranges
-  const bool ms = a->V % 4 == 0 && ((uintptr_t)a->Mt & 15) == 0 && (int64_t)a->rows * a->V * 2 < 0x80000000ll && KL_MS &&
-                  !(a->flags & CC_KL_REGISTER_TARGETS);
+  const bool ms = a->V % 4 == 0 && ((uintptr_t)a->Mt & 15) == 0 && (int64_t)a->rows * a->V * 2 < 0x80000000ll &&
+                  (a->flags & CC_KL_LDS_TARGETS);
+  // the register path's dZ through LDS as 16-B row stores (16-B aligned rows; the sentinel past range)
+  const bool wstore = a->V % 8 == 0 && ((uintptr_t)a->dZ & 15) == 0 && (int64_t)a->rows * a->V * 2 < 0x80000000ll &&
+                      !(a->flags & CC_KL_SHORT_STORES);
+  // dWo's dZ stream by producer waves' LDS-DMA (16-B aligned rows): opt-in (measured no faster)
+  const bool dwo_pc = a->V % 8 == 0 && ((uintptr_t)a->dZ & 15) == 0 && (a->flags & CC_KL_DWO_PRODUCER_WAVES);
 #define KL_LAUNCH(DD)                                                                                          \
   if (a->d == DD) {                                                                                          \
     hipLaunchKernelGGL((kl_stats_kernel<DD>), gs, dim3(NTH), 0, s, p);                                      \
@@ -1136,13 +1288,21 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
     if (dw_sep) {                                                                                            \
       if (ms)                                                                                                \
         hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, false, (DD <= 256)>), gm, dim3(NTH), 0, s, p);    \
+      else if (wstore)                                                                                       \
+        hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, false, false, (DD <= 256)>), gm, dim3(NTH), 0, s, p); \
       else                                                                                                   \
         hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, false>), gm, dim3(NTH), 0, s, p);                 \
       CC_LAUNCH_CHECK("kl_main_kernel");                                                                     \
       hipLaunchKernelGGL((kl_fix_kernel<DD, false>), dim3(FIXG), dim3(NTH), 0, s, p);                       \
       CC_LAUNCH_CHECK("kl_fix_kernel");                                                                      \
       const dim3 gd((unsigned)cdiv(a->V, DW_NB), (unsigned)(DD > 256 ? DD / 256 : 1));                     \
-      if (a->V % 8 == 0)                                                                                     \
+      if (dwo_pc) {                                                                                          \
+        static const bool attr = hipFuncSetAttribute((const void *)kl_dwo_pc_kernel<DD>,                     \
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize,             \
+                                                      DWP_NS * DW_KC * DW_NB * 2) == hipSuccess;              \
+        CC_REQUIRE(attr, "cc_dec_softmax_kl_dw: dynamic LDS attribute");                                     \
+        hipLaunchKernelGGL((kl_dwo_pc_kernel<DD>), gd, dim3(DWP_NT), DWP_NS * DW_KC * DW_NB * 2, s, p);      \
+      } else if (a->V % 8 == 0)                                                                              \
         hipLaunchKernelGGL((kl_dwo_kernel<DD, true>), gd, dim3(NTH), 0, s, p);                               \
       else                                                                                                   \
         hipLaunchKernelGGL((kl_dwo_kernel<DD, false>), gd, dim3(NTH), 0, s, p);                              \

@@ -420,7 +420,7 @@ class Trainer:
             self.tsum = torch.zeros(hi - lo, 2, **f32)    # per M~ row {sum t, sum t ln t} (t clipped), once
             L.call('cc_kl_tsum', L.ptr(data.y_reg), hi - lo, V, L.ptr(self.tsum), L.stream_ptr())
             self.kl_ws = torch.zeros(int(L.lib().cc_dec_kl_ws_size(self.Breg, V)) // 4 + 4, **f32)
-            self.kl_flags = 0   # cc_dec_kl_args.flags (tests: CC_KL_REGISTER_TARGETS, the A/B of decreg.hip's M~ staging)
+            self.kl_flags = 0   # cc_dec_kl_args.flags (tests: the A/B of decreg.hip's alternative full-mode paths)
             self.kl_part = torch.zeros(max(int(L.lib().cc_dec_kl_blocks(V)), 1), device=self.dev,
                                        dtype=torch.float64)
         if self.full_reg:

@@ -508,10 +508,15 @@ typedef struct cc_dec_kl_args {
   double loss_scale;
   uint32_t *ticket;
   void *ws;
-  int32_t flags;             /* bit 0 CC_KL_REGISTER_TARGETS: the main pass keeps M~ in registers instead
-                                of staging it through LDS (an A/B knob: bit-identical results; 0 default) */
+  int32_t flags;             /* A/B knobs of the many-row (full-mode) path, bit-identical results; 0 = the
+                                measured-fastest default.  CC_KL_LDS_TARGETS: the main pass stages M~
+                                through LDS by DMA one pass ahead (slower, r05r); CC_KL_DWO_PRODUCER_WAVES:
+                                dWo's dZ stream by producer waves' LDS-DMA (slower); CC_KL_SHORT_STORES:
+                                dZ stored 2 B per lane instead of 16-B rows through LDS (slower) */
 } cc_dec_kl_args;
-#define CC_KL_REGISTER_TARGETS 1
+#define CC_KL_LDS_TARGETS 1
+#define CC_KL_DWO_PRODUCER_WAVES 2
+#define CC_KL_SHORT_STORES 4
 size_t cc_dec_kl_ws_size(int32_t rows, int32_t V);
 int32_t cc_dec_kl_blocks(int32_t V);
 int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream);

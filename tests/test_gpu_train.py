@@ -455,13 +455,15 @@ def test_fused_regulariser_clip_fix_path(V, B, d):
                                       'encoder/encoded_1/kernel')}, TOL['bf16'], 0)
 
 
-@pytest.mark.parametrize('V,spread', [(2500, True), (2502, True), (2500, False)])
+@pytest.mark.parametrize('V,spread', [(2500, True), (2502, True), (2504, True), (2504, False)])
 def test_full_mode_clip_fix_path(V, spread):
     """Full mode (all |V| identity rows, several 512-row tiles per slice) with the exact-clip
     path live: the bias spread of the clip test above pushes part of every softmax row below
-    1e-7.  V = 2,500: the main pass stages M~ through LDS (decreg.hip MS: its rare-path reload of
-    M~ for the clip partials, its counted waits across tiles); V = 2,502 (V % 4 = 2): the
-    register path.  Against the bf16-emulating oracle over reg_idx = arange(V)."""
+    1e-7.  Against the bf16-emulating oracle over reg_idx = arange(V) (spread off: no clip), then
+    the alternative paths of decreg.hip (cc_dec_kl_args.flags) bit for bit against the default:
+    M~ staged through LDS (MS, V % 4 == 0: its rare-path reload of M~ for the clip partials, its
+    counted waits across tiles) with dWo's producer-wave dZ stream (V % 8 == 0), and the 2-B dZ
+    stores instead of 16-B rows through LDS (V % 8 == 0; V = 2,502 has neither)."""
     d, B = 256, 128
 
     def run(flags):
@@ -490,12 +492,16 @@ def test_full_mode_clip_fix_path(V, spread):
                                       'decoder_for_reg/decoded_3/kernel', 'encoder/encoded_1/kernel')},
                    TOL['bf16_full'], 0)
     assert e['loss/kl'] < 5e-6, e['loss/kl']
-    # the LDS staging of M~ (decreg.hip MS, V % 4 == 0) against the register path: identical bits
-    tr2 = run(L.CC_KL_REGISTER_TARGETS)[0]
-    g1, g2 = tr.layout.unpack(tr.grads.cpu().numpy()), tr.layout.unpack(tr2.grads.cpu().numpy())
-    diff = {k: float(np.abs(g1[k] - g2[k]).max()) for k in g1 if not np.array_equal(g1[k], g2[k])}
-    assert torch.equal(tr2.dZout, tr.dZout) and not diff, diff
-    assert tr2.losses() == tr.losses(), (tr2.losses(), tr.losses())
+    # the LDS staging of M~ (decreg.hip MS, V % 4 == 0), dWo's producer-wave dZ stream and the 16-B dZ
+    # stores through LDS (V % 8 == 0)
+    # against the register-staged paths: identical bits
+    g1 = tr.layout.unpack(tr.grads.cpu().numpy())
+    for flags in (L.CC_KL_LDS_TARGETS | L.CC_KL_DWO_PRODUCER_WAVES, L.CC_KL_SHORT_STORES):
+        tr2 = run(flags)[0]
+        g2 = tr.layout.unpack(tr2.grads.cpu().numpy())
+        diff = {k: float(np.abs(g1[k] - g2[k]).max()) for k in g1 if not np.array_equal(g1[k], g2[k])}
+        assert torch.equal(tr2.dZout, tr.dZout) and not diff, (flags, diff)
+        assert tr2.losses() == tr.losses(), (flags, tr2.losses(), tr.losses())
 
 
 # Eigen's float logistic (TF 2.5's CPU sigmoid) is exactly 1 from this logit on (metrics.hip)

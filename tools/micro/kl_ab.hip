@@ -1,6 +1,6 @@
-// A/B of cc_dec_softmax_kl_dw's main pass: M~ staged through LDS (default) against M~ in registers
-// (CC_KL_REGISTER_TARGETS) on random full-mode inputs; prints how many dZ / dWo / dbo elements and
-// which losses differ, and the first differing dbo column (dev tool).
+// A/B of cc_dec_softmax_kl_dw's many-row paths: the default (flags 0) against cc_dec_kl_args.flags
+// argv[2] (default: CC_KL_LDS_TARGETS | CC_KL_DWO_PRODUCER_WAVES) on random full-mode inputs; prints
+// how many dZ / dWo / dbo elements and which losses differ, and the first differing dbo column.
 // hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I cubecobrarecommender_amd/csrc tools/micro/kl_ab.hip \
 //   cubecobrarecommender_amd/csrc/decreg.hip cubecobrarecommender_amd/csrc/api.cpp \
 //   cubecobrarecommender_amd/csrc/host_util.cpp -o tools/micro/gpubin/kl_ab
@@ -68,7 +68,7 @@ int main(int argc, char **argv) {
     a.tsum = (const float *)tsum; a.mt_bytes = (int64_t)V * V * 4; a.mt_lo = 0; a.reg_idx = (const int32_t *)ridx;
     a.scale = 1.f / rows; a.dZ = dZ; a.gW = (float *)gW; a.gb = (float *)gb; a.loss_partials = (double *)part;
     a.loss_out = (double *)loss; a.loss_scale = 1.0 / rows; a.ticket = (uint32_t *)tick; a.ws = ws;
-    a.flags = f ? CC_KL_REGISTER_TARGETS : 0;
+    a.flags = f ? (argc > 2 ? atoi(argv[2]) : CC_KL_LDS_TARGETS | CC_KL_DWO_PRODUCER_WAVES) : 0;
     const int rc = cc_dec_softmax_kl_dw(&a, nullptr);
     (void)hipDeviceSynchronize();
     o[f].dz.resize((size_t)rows * V);

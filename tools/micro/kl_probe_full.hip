@@ -53,6 +53,7 @@ int main(int argc, char **argv) {
   a.tsum = (const float *)tsum; a.mt_bytes = (int64_t)V * V * 4; a.mt_lo = 0; a.reg_idx = (const int32_t *)ridx;
   a.scale = 1e-4f; a.dZ = dZ; a.gW = (float *)gW; a.gb = (float *)gb; a.loss_partials = (double *)part;
   a.loss_out = (double *)loss; a.loss_scale = 1.0 / rows; a.ticket = (uint32_t *)tick; a.ws = ws;
+  a.flags = argc > 2 ? atoi(argv[2]) : 0;   // cc_dec_kl_args.flags (A/B of the main pass's paths)
   const char *names[8] = {"", "tile stats staged", "p0 logits", "p0 epilogue", "p1 logits", "p1 epilogue", "phase-2 wait", "phase 2 (+last)"};
   for (int rep = 0; rep < 3; ++rep) {
     unsigned long long z[16] = {0};
@@ -70,7 +71,7 @@ int main(int argc, char **argv) {
     unsigned long long g[16], c[16];
     (void)hipMemcpyFromSymbol(g, HIP_SYMBOL(g_acc), sizeof(g));
     (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(g_cnt), sizeof(c));
-    printf("rep %d rc %d rows %d: all four launches %.1f us; block 0 of kl_main, totals over tiles (us):", rep, rc, rows, ms * 1000);
+    printf("rep %d rc %d rows %d flags %d: all four launches %.1f us; block 0 of kl_main, totals over tiles (us):", rep, rc, rows, a.flags, ms * 1000);
     double tot = 0;
     for (int k = 1; k < 8; ++k) { printf(" [%s] %.1f", names[k], g[k] * 0.01); tot += g[k] * 0.01; }
     printf("  sum %.1f; stats kernel block 0: %.1f\n", tot, (g[9] + g[10] + g[11]) * 0.01);
