@@ -29,16 +29,41 @@
 
 namespace {
 
-constexpr int QM = 256, QN = 256, QKB = 128, QNT = 512;
-constexpr int QA_BYTES = QM * QKB, QB_BYTES = QN * QKB;  // 32 KB each
-constexpr int QSTAGE = QA_BYTES + QB_BYTES + (QM + QN) * 4;
-constexpr int QLDS = 2 * QSTAGE;  // 132 KB
+// MX8_QNS (build knob): 2 = K tiles of 128 in two LDS stages (one tile of lead); 4 = K tiles of 64
+// (one 32x32x64 step) in four stages, three tiles in flight while the fourth is multiplied.  Split-K
+// chunks stay multiples of 128 either way (the same partition, the same bits).
+#ifndef MX8_QNS
+#define MX8_QNS 2
+#endif
+constexpr int QNS = MX8_QNS;
+static_assert(QNS == 2 || QNS == 4, "MX8_QNS: 2 or 4");
+constexpr int QM = 256, QN = 256, QKB = QNS == 2 ? 128 : 64, QNT = 512;
+constexpr int QA_BYTES = QM * QKB, QB_BYTES = QN * QKB;
+constexpr int QSTAGE = QA_BYTES + QB_BYTES + (QM + QN) * 4;   // + each row's E8M0 word of the 128 k
+constexpr int QLDS = QNS * QSTAGE;  // 132 KB
 // the BCE epilogue's LDS: a 256 x 130 fp32 pass tile, the 256 x 8 target words, the loss reduction
 constexpr int QLDS_BCE = QM * 130 * 4 + QM * 8 * 4 + 8 * 8 + 16;
 constexpr int QLDS_MAX = QLDS > QLDS_BCE ? QLDS : QLDS_BCE;
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+// the stage copies as inline asm (M0 = the wave-uniform LDS address): the compiler does not count
+// them, so it inserts no vmcnt before the fragment reads (LDS-DMA alias tracking would drain the
+// copies in flight); q_body's waits are explicit
+__device__ __forceinline__ i32x4_t q_rsrc(const void *base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  return i32x4_t{__builtin_amdgcn_readfirstlane((int)(uint32_t)a), __builtin_amdgcn_readfirstlane((int)(a >> 32) & 0xFFFF),
+                 __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000};
+}
+__device__ __forceinline__ uint32_t q_lds(const void *p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const lds_void *)p);
+}
+__device__ __forceinline__ void q_dma16(const i32x4_t &rs, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void q_dma4(const i32x4_t &rs, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dword %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(lds) : "memory");
+}
 typedef __attribute__((ext_vector_type(8))) int i32x8_t;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
 
@@ -99,40 +124,47 @@ __device__ __forceinline__ int xcd_run(int b, int nb) {  // bijective: block -> 
   return x < r ? x * (q + 1) + slot : r * (q + 1) + (x - r) * q + slot;
 }
 
-// stage st <- K-tile at k0: wave w moves A rows [32w, 32w + 32) and B rows [32w, 32w + 32) (4 + 4
-// instructions of 8 rows x 128 B), waves 0-3 the A scale words of rows [64w, 64w + 64), waves 4-7
-// the B scale words (one 4-B-per-lane instruction each): 9 DMA instructions per wave per tile
-__device__ __forceinline__ void q_dma(const QP &p, const __amdgpu_buffer_rsrc_t &ra, const __amdgpu_buffer_rsrc_t &rb,
-                                      const __amdgpu_buffer_rsrc_t &rsa, const __amdgpu_buffer_rsrc_t &rsb,
-                                      char *smem, int st, int bm, int bn, int k0) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int rl = lane >> 3, slot = lane & 7;
+// stage st <- K-tile at k0 (64 k): wave w moves A rows [32w, 32w + 32) and B rows [32w, 32w + 32)
+// (2 + 2 instructions of 16 rows x 64 B, the 16-B chunk swizzle chunk ^ (row >> 2 & 3) applied on
+// the global source address), and one 4-B-per-lane instruction of scale words (the 4 E8M0 bytes of
+// the 128 k holding the tile: its 2 are picked by the tile's parity): waves 0-3 the A rows
+// [64w, 64w + 64), waves 4-7 the B rows: 5 DMA instructions per wave per tile
+// (QKB = 128: 4 + 4 instructions of 8 rows x 128 B, swizzle chunk ^ row & 7; 9 per wave per tile)
+constexpr int QNI = QA_BYTES / 1024 / 8;        // A (and B) instructions per wave per tile
+constexpr int QDMA_PER_TILE = 2 * QNI + 1;
+constexpr int QRPI = 1024 / QKB;                // rows per instruction
+__device__ __forceinline__ int q_swz(int row) { return QKB == 128 ? (row & 7) : ((row >> 2) & 3); }
+__device__ __forceinline__ void q_dma(const QP &p, const i32x4_t &ra, const i32x4_t &rb, const i32x4_t &rsa,
+                                      const i32x4_t &rsb, char *smem, int st, int bm, int bn, int k0) {
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   char *sA = smem + st * QSTAGE, *sB = sA + QA_BYTES, *sS = sB + QB_BYTES;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int i = w * 4 + u;  // rows 8i .. 8i + 7
-    const int row = 8 * i + rl;
-    const int c = slot ^ (row & 7);
+  for (int u = 0; u < QNI; ++u) {
+    const int i = w * QNI + u;  // rows QRPI i .. QRPI (i + 1) - 1
+    const int row = QRPI * i + lane / (QKB / 16);
+    const int c = (lane % (QKB / 16)) ^ q_swz(row);
     const uint32_t oa = bm + row < p.M ? (uint32_t)(bm + row) * (uint32_t)p.lda + (uint32_t)(k0 + 16 * c) : 0x80000000u;
     const uint32_t ob = bn + row < p.N ? (uint32_t)(bn + row) * (uint32_t)p.ldb + (uint32_t)(k0 + 16 * c) : 0x80000000u;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void *)(sA + i * 1024), 16, oa, 0, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void *)(sB + i * 1024), 16, ob, 0, 0, 0);
+    q_dma16(ra, oa, q_lds(sA + i * 1024));
+    q_dma16(rb, ob, q_lds(sB + i * 1024));
   }
   const int row = (w & 3) * 64 + lane;
   if (w < 4) {
-    const uint32_t os = bm + row < p.M ? (uint32_t)(bm + row) * (uint32_t)(p.lda / 32) + (uint32_t)(k0 / 32) : 0x80000000u;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_void *)(sS + (w & 3) * 256), 4, os, 0, 0, 0);
+    const uint32_t os = bm + row < p.M ? (uint32_t)(bm + row) * (uint32_t)(p.lda / 32) + (uint32_t)(k0 / 128 * 4) : 0x80000000u;
+    q_dma4(rsa, os, q_lds(sS + (w & 3) * 256));
   } else {
-    const uint32_t os = bn + row < p.N ? (uint32_t)(bn + row) * (uint32_t)(p.ldb / 32) + (uint32_t)(k0 / 32) : 0x80000000u;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_void *)(sS + QM * 4 + (w & 3) * 256), 4, os, 0, 0, 0);
+    const uint32_t os = bn + row < p.N ? (uint32_t)(bn + row) * (uint32_t)(p.ldb / 32) + (uint32_t)(k0 / 128 * 4) : 0x80000000u;
+    q_dma4(rsb, os, q_lds(sS + QM * 4 + (w & 3) * 256));
   }
 }
 
 // the 32 x 64 fp8 fragment of rows `row` (lane & 31) for 64-k step kk: lane half h holds k 16h ..
-// 16h + 15 (low 16 B) and 32 + 16h .. (high 16 B) — chunks 4kk + h and 4kk + 2 + h (gemm.hip nt_frag8)
+// 16h + 15 (low 16 B) and 32 + 16h .. (high 16 B) — chunks 4kk + h and 4kk + 2 + h (gemm.hip
+// nt_frag8), under the stage's chunk swizzle (64-B rows: row >> 2 & 3 puts 16 consecutive rows on
+// 16 distinct 16-B bank groups)
 __device__ __forceinline__ i32x8_t q_frag(const char *S, int row, int c0) {
-  const i32x4_t lo = *reinterpret_cast<const i32x4_t *>(S + row * QKB + ((c0 ^ (row & 7)) << 4));
-  const i32x4_t hi = *reinterpret_cast<const i32x4_t *>(S + row * QKB + (((c0 + 2) ^ (row & 7)) << 4));
+  const i32x4_t lo = *reinterpret_cast<const i32x4_t *>(S + row * QKB + ((c0 ^ q_swz(row)) << 4));
+  const i32x4_t hi = *reinterpret_cast<const i32x4_t *>(S + row * QKB + (((c0 + 2) ^ q_swz(row)) << 4));
   return i32x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
@@ -144,10 +176,8 @@ __device__ __forceinline__ void q_body(const QP &p, int q, char *smem) {
   const int bm = (tile % p.tiles_m) * QM, bn = (tile / p.tiles_m) * QN;
   const int kbeg = split * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
   const int nk = kbeg < kend ? (kend - kbeg) / QKB : 0;  // K % 128 == 0 and kchunk % 128 == 0
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void *)p.A, (short)0, p.a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void *)p.B, (short)0, p.b_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void *)p.sa, (short)0, p.sa_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void *)p.sb, (short)0, p.sb_bytes, 0x00020000);
+  const i32x4_t ra = q_rsrc(p.A, p.a_bytes), rb = q_rsrc(p.B, p.b_bytes);
+  const i32x4_t rsa = q_rsrc(p.sa, p.sa_bytes), rsb = q_rsrc(p.sb, p.sb_bytes);
   f32x16_t acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -155,8 +185,8 @@ __device__ __forceinline__ void q_body(const QP &p, int q, char *smem) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  if (nk > 0) q_dma(p, ra, rb, rsa, rsb, smem, 0, bm, bn, kbeg);
   // BCE: the tile's target words (256 rows x 8 words), 4 per thread, in flight during the K loop
+  // (issued before the stage copies: older than every copy the loop waits for)
   constexpr bool bce = BCE;
   const int YW = (p.N + 31) >> 5;
   uint32_t yv[4] = {0u, 0u, 0u, 0u};
@@ -168,14 +198,24 @@ __device__ __forceinline__ void q_body(const QP &p, int q, char *smem) {
     }
   }
   const int ar = wm * 128 + (lane & 31), br = wn * 64 + (lane & 31);
+#pragma unroll
+  for (int s = 0; s < QNS - 1; ++s)
+    if (s < nk) q_dma(p, ra, rb, rsa, rsb, smem, s, bm, bn, kbeg + s * QKB);
   for (int t = 0; t < nk; ++t) {
-    // tile t landed in every wave (own DMAs drained, then the barrier), and every wave finished
-    // reading the other buffer in iteration t - 1 (its LDS reads retired before the barrier)
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    // tile t landed in every wave (own copies counted: those of the tiles after t, up to QNS - 2 of
+    // them, may stay in flight; then the barrier), and every wave finished reading the stage the
+    // copy below overwrites (tile t - 1's: its LDS reads retired before the barrier)
+    const int younger = min(QNS - 2, nk - 1 - t);
+    if (younger >= 2)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * QDMA_PER_TILE) : "memory");
+    else if (younger == 1)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(QDMA_PER_TILE) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 1 < nk) q_dma(p, ra, rb, rsa, rsb, smem, (t + 1) & 1, bm, bn, kbeg + (t + 1) * QKB);
-    const char *sA = smem + (t & 1) * QSTAGE, *sB = sA + QA_BYTES;
+    if (t + QNS - 1 < nk) q_dma(p, ra, rb, rsa, rsb, smem, (t + QNS - 1) % QNS, bm, bn, kbeg + (t + QNS - 1) * QKB);
+    const char *sA = smem + (t % QNS) * QSTAGE, *sB = sA + QA_BYTES;
     const uint32_t *sS = reinterpret_cast<const uint32_t *>(sB + QB_BYTES);
     uint32_t wa[4], wb[2];
 #pragma unroll
@@ -183,8 +223,9 @@ __device__ __forceinline__ void q_body(const QP &p, int q, char *smem) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) wb[j] = sS[QM + br + 32 * j];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int c0 = 4 * kk + half, sh = 8 * (2 * kk + half);
+    for (int kk = 0; kk < QKB / 64; ++kk) {
+      // (QKB = 64: kbeg % 128 == 0, so t's parity places the tile's 64 k in the scale word's 128)
+      const int c0 = 4 * kk + half, sh = QKB == 128 ? 8 * (2 * kk + half) : 8 * (2 * (t & 1) + half);
       i32x8_t b[2];
       int sb[2];
 #pragma unroll
@@ -500,7 +541,7 @@ int q_params(const cc_gemm_args *g, QP &p) {
   p.colsum = nullptr;
   p.ldzq = p.ldztq = 0;
   p.splits = g->epilogue == CC_EPI_SPLITK ? g->splits : 1;
-  p.kchunk = (int)cdiv(cdiv(g->K, p.splits), QKB) * QKB;
+  p.kchunk = (int)cdiv(cdiv(g->K, p.splits), 128) * 128;   // (128: the partition of the 128-k tiles)
   p.tiles_m = (int)cdiv(g->M, QM);
   p.ntiles = p.tiles_m * (int)cdiv(g->N, QN);
   p.a_bytes = (uint32_t)((int64_t)g->M * g->lda);
