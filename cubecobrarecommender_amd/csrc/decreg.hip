@@ -419,7 +419,7 @@ __device__ __forceinline__ void ms_dma(const v4i &rs, const uint32_t (&sof)[4], 
   for (int i = 0; i < 4; ++i) dma_asm<16, CPOL>(rs, sof[i], 128u * j, a + 1024u * i);
 }
 
-template <int D, bool FIX, int CPOL = 0, bool DW = true, bool MS = false, bool WS = false>
+template <int D, bool FIX, int CPOL = 0, bool DW = true, bool MS = false, bool WS = false, bool WM = false>
 __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt, MainSmem<kl_nb<D>()> &sm) {
   constexpr int NB = kl_nb<D>(), NJ = NB / 32;
   constexpr int CHB = TR / 8;
@@ -475,7 +475,16 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   constexpr bool WSX = WS && PF && !MSX;
   constexpr int WS_PITCH = 52;   // dwords per image row (96 bf16 + 8 pad)
   uint32_t *const zimg = reinterpret_cast<uint32_t *>(sm.Zt) + w * (32 * WS_PITCH);
-  static_assert(!WSX || 8 * 32 * WS_PITCH * 4 <= (int)sizeof(sm.Zt), "WS: the images fit the dZ^T tile");
+  // WMX (opt-in CC_KL_WIDE_TARGETS, with WSX; M~ 16-B aligned): the pass's M~ loaded 16 B per lane
+  // (4 columns of one row; 12 loads per lane instead of 48 4-B ones) and turned into the
+  // accumulator layout per column tile through a wave-private [32][40]-float LDS stage next to the
+  // dZ image.  Bit-identical but slower (the four launches 1,548-1,586 -> 1,610-1,654 us, r05v):
+  // unlike the stores, the 4-B loads were not issue-bound enough to pay for the stage round trip
+  constexpr bool WMX = WM && WSX;
+  constexpr int WM_PITCH = 40;   // floats per stage row (32 + 8: the half-waves' rows on disjoint banks)
+  float *const mstage = reinterpret_cast<float *>(reinterpret_cast<uint32_t *>(sm.Zt) + 8 * 32 * WS_PITCH) + w * (32 * WM_PITCH);
+  static_assert(!WSX || 8 * 32 * WS_PITCH * 4 + (WM ? 8 * 32 * WM_PITCH * 4 : 0) <= (int)sizeof(sm.Zt),
+                "WS / WM: the images and stages fit the dZ^T tile");
   // all A fragments first in the memory queue, then M~ (d = 512: a ring of 16; PF: the next block's
   // first 8 under the epilogue, the other 8 refilled during the MFMAs — 16 would spill)
   LFrag<D, (PF && !MSX) ? 8 : (D / 16 < 16 ? D / 16 : 16)> lf;
@@ -575,6 +584,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
         nxt = t1 < p.rows && rb1 < min(TR, p.rows - t1);
       }
       float tv[NJ][16];
+      v4u wv[NJ][4];        // WMX: row (lane >> 3) + 8 u, columns 32 j + 4 (lane & 7) .. of the pass
       uint32_t sof[4];      // MSX: the next block's DMA rows
       if constexpr (MSX) {
         const uint32_t c4 = 4u * (uint32_t)(n0 + 4 * (lane & 7));
@@ -599,6 +609,15 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
 #pragma unroll
           for (int i = 0; i < 4; ++i) sof[i] = (uint32_t)card_off(cn[rb1 + (lane >> 3) + 8 * i], V) + c4;
         }
+      } else if constexpr (WMX) {
+        uint32_t wro[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) wro[u] = rowoff(rb + (lane >> 3) + 8 * u) + 4u * (uint32_t)(n0 + 4 * (lane & 7));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            wv[j][u] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(mt_rs, wro[u] + 128u * j, 0, CPOL));
       } else if constexpr (!FIX) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -636,6 +655,13 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
           const float *slot = stg + j * 1024;
 #pragma unroll
           for (int r = 0; r < 16; ++r) tv[j][r] = slot[acc_row(r, lane) * 32 + (lane & 31)];
+        }
+        if constexpr (WMX) {   // column tile j's M~: rows x 16 B -> the stage -> the accumulator layout
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            *reinterpret_cast<v4u *>(mstage + ((lane >> 3) + 8 * u) * WM_PITCH + 4 * (lane & 7)) = wv[j][u];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) tv[j][r] = mstage[acc_row(r, lane) * WM_PITCH + (lane & 31)];
         }
         uint16_t tt[16];
         // row stats re-read per column tile (an opaque base): held across the three tiles they
@@ -774,9 +800,9 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
             float tj[16];
             const uint32_t gc4 = 4u * (uint32_t)(n0 + j * 32 + (lane & 31));
 #pragma unroll
-            for (int r = 0; r < 16; ++r)   // MSX: the slots hold the next block by now: from memory
-              tj[r] = MSX ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mt_rs, roff[r] + gc4, 0, CPOL))
-                          : tv[j][r];
+            for (int r = 0; r < 16; ++r)   // MSX / WMX: M~ not held in registers: from memory
+              tj[r] = MSX || WMX ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mt_rs, roff[r] + gc4, 0, CPOL))
+                                 : tv[j][r];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const float st_x = MSX ? rs2[cur][rb + acc_row(r, lane)].x : sm.rs[rb + acc_row(r, lane)].x;
@@ -930,11 +956,11 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   }
 }
 
-template <int D, int CPOL, bool DW, bool MS = false, bool WS = false>
+template <int D, int CPOL, bool DW, bool MS = false, bool WS = false, bool WM = false>
 __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
   __shared__ __attribute__((aligned(16))) bf16_t Wt[kl_nb<D>() * D];
   __shared__ __attribute__((aligned(16))) MainSmem<kl_nb<D>()> sm;
-  kl_slice<D, false, CPOL, DW, MS, WS>(p, blockIdx.x, Wt, sm);
+  kl_slice<D, false, CPOL, DW, MS, WS, WM>(p, blockIdx.x, Wt, sm);
 }
 
 // The exact-clip correction: a small persistent grid (FIXG blocks) that leaves at once when the
@@ -1277,6 +1303,8 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
   // the register path's dZ through LDS as 16-B row stores (16-B aligned rows; the sentinel past range)
   const bool wstore = a->V % 8 == 0 && ((uintptr_t)a->dZ & 15) == 0 && (int64_t)a->rows * a->V * 2 < 0x80000000ll &&
                       !(a->flags & CC_KL_SHORT_STORES);
+  // ... and its M~ loaded 16 B per lane through LDS (16-B aligned rows): opt-in (measured slower)
+  const bool wload = ((uintptr_t)a->Mt & 15) == 0 && (a->flags & CC_KL_WIDE_TARGETS);
   // dWo's dZ stream by producer waves' LDS-DMA (16-B aligned rows): opt-in (measured no faster)
   const bool dwo_pc = a->V % 8 == 0 && ((uintptr_t)a->dZ & 15) == 0 && (a->flags & CC_KL_DWO_PRODUCER_WAVES);
 #define KL_LAUNCH(DD)                                                                                          \
@@ -1288,6 +1316,8 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
     if (dw_sep) {                                                                                            \
       if (ms)                                                                                                \
         hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, false, (DD <= 256)>), gm, dim3(NTH), 0, s, p);    \
+      else if (wstore && wload)                                                                              \
+        hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, false, false, (DD <= 256), (DD <= 256)>), gm, dim3(NTH), 0, s, p); \
       else if (wstore)                                                                                       \
         hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, false, false, (DD <= 256)>), gm, dim3(NTH), 0, s, p); \
       else                                                                                                   \

@@ -512,11 +512,14 @@ typedef struct cc_dec_kl_args {
                                 measured-fastest default.  CC_KL_LDS_TARGETS: the main pass stages M~
                                 through LDS by DMA one pass ahead (slower, r05r); CC_KL_DWO_PRODUCER_WAVES:
                                 dWo's dZ stream by producer waves' LDS-DMA (slower); CC_KL_SHORT_STORES:
-                                dZ stored 2 B per lane instead of 16-B rows through LDS (slower) */
+                                dZ stored 2 B per lane instead of 16-B rows through LDS (slower);
+                                CC_KL_WIDE_TARGETS: M~ loaded as 16-B rows turned into the accumulator
+                                layout through LDS instead of 4 B per lane (slower) */
 } cc_dec_kl_args;
 #define CC_KL_LDS_TARGETS 1
 #define CC_KL_DWO_PRODUCER_WAVES 2
 #define CC_KL_SHORT_STORES 4
+#define CC_KL_WIDE_TARGETS 8
 size_t cc_dec_kl_ws_size(int32_t rows, int32_t V);
 int32_t cc_dec_kl_blocks(int32_t V);
 int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream);

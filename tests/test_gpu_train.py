@@ -462,8 +462,9 @@ def test_full_mode_clip_fix_path(V, spread):
     1e-7.  Against the bf16-emulating oracle over reg_idx = arange(V) (spread off: no clip), then
     the alternative paths of decreg.hip (cc_dec_kl_args.flags) bit for bit against the default:
     M~ staged through LDS (MS, V % 4 == 0: its rare-path reload of M~ for the clip partials, its
-    counted waits across tiles) with dWo's producer-wave dZ stream (V % 8 == 0), and the 2-B dZ
-    stores instead of 16-B rows through LDS (V % 8 == 0; V = 2,502 has neither)."""
+    counted waits across tiles) with dWo's producer-wave dZ stream (V % 8 == 0), M~ loaded as 16-B
+    rows through LDS, and the 2-B dZ stores instead of 16-B rows through LDS (V % 8 == 0;
+    V = 2,502 has none of them)."""
     d, B = 256, 128
 
     def run(flags):
@@ -496,7 +497,7 @@ def test_full_mode_clip_fix_path(V, spread):
     # stores through LDS (V % 8 == 0)
     # against the register-staged paths: identical bits
     g1 = tr.layout.unpack(tr.grads.cpu().numpy())
-    for flags in (L.CC_KL_LDS_TARGETS | L.CC_KL_DWO_PRODUCER_WAVES, L.CC_KL_SHORT_STORES):
+    for flags in (L.CC_KL_LDS_TARGETS | L.CC_KL_DWO_PRODUCER_WAVES, L.CC_KL_WIDE_TARGETS, L.CC_KL_SHORT_STORES):
         tr2 = run(flags)[0]
         g2 = tr.layout.unpack(tr2.grads.cpu().numpy())
         diff = {k: float(np.abs(g1[k] - g2[k]).max()) for k in g1 if not np.array_equal(g1[k], g2[k])}
