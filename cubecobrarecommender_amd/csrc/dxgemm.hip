@@ -9,8 +9,12 @@
 // 32 KB) is copied global -> LDS by buffer_load_dwordx4 ... lds (no VGPR staging), four LDS stages
 // deep (three tiles in flight while the fourth is multiplied), counted vmcnt waits and raw
 // s_barrier (a __syncthreads would drain the DMA queue).  The LDS images are lane-linear per wave
-// instruction (8 rows x 128 B); the 16-B chunk XOR swizzle (chunk ^ row & 7) is applied on the
-// global source address.  k >= kend chunks point past the buffer's range: the DMA writes zeros.
+// instruction (8 rows x 128 B); the 16-B chunk XOR swizzle (chunk ^ (row >> 1 & 7)) is applied on
+// the global source address.  (row >> 1, not row: a ds_read_b128 is serviced in four lane groups of
+// 16 — lanes {0-3, 12-15, 20-27}, ... — whose rows r and r + 8 / r + 24 share a 16-B bank slot under
+// chunk ^ (row & 7), a 2-way conflict on every fragment read; under (row >> 1 & 7) the 16 rows of
+// each group land on 16 distinct slots: SQ_LDS_BANK_CONFLICT 30 M -> 0 per dx_wide launch (r05x,
+// r05y); the kernel's time did not move with them — its fragment reads were not its bound.)  k >= kend chunks point past the buffer's range: the DMA writes zeros.
 // (tile, split) pairs are dealt split-major over the 8 XCDs so a split's A and B panels are
 // fetched into one XCD's L2 once.  The split partials are summed by cc_splitk_reduce.
 #include <cstdlib>
@@ -54,7 +58,7 @@ __device__ __forceinline__ void dma_tile(const DxP &p, const __amdgpu_buffer_rsr
   for (int u = 0; u < 4; ++u) {
     const int i = w * 4 + u;       // instruction index: rows 8i .. 8i + 7
     const int row = 8 * i + rl;
-    const int c = slot ^ (row & 7);
+    const int c = slot ^ ((row >> 1) & 7);
     const int k = k0 + 8 * c;
     const uint32_t oa = k < kend ? (uint32_t)(((bm + row) * p.lda + k) * 2) : 0x80000000u;
     const uint32_t ob = k < kend ? (uint32_t)(((bn + row) * p.ldb + k) * 2) : 0x80000000u;
@@ -74,7 +78,7 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 __device__ __forceinline__ bf16x8_t frag(const char *s, int row, int c) {  // 16 B: row, k-chunk c
-  return *reinterpret_cast<const bf16x8_t *>(s + row * 128 + ((c ^ (row & 7)) << 4));
+  return *reinterpret_cast<const bf16x8_t *>(s + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
 }
 
 __global__ __launch_bounds__(XNT) void dx_splitk_kernel(DxP p) {
@@ -163,7 +167,7 @@ __device__ __forceinline__ void dma_tile_w(const DxP &p, const __amdgpu_buffer_r
   for (int u = 0; u < 2; ++u) {
     const int i = w * 2 + u;  // A rows 8i .. 8i + 7
     const int row = 8 * i + rl;
-    const int k = k0 + 8 * (slot ^ (row & 7));
+    const int k = k0 + 8 * (slot ^ ((row >> 1) & 7));
     const uint32_t oa = k < kend ? (uint32_t)(((bm + row) * p.lda + k) * 2) : 0x80000000u;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void *)(sa + i * 1024), 16, oa, 0, 0, 2);  // dZ is read once: non-temporal
   }
@@ -171,7 +175,7 @@ __device__ __forceinline__ void dma_tile_w(const DxP &p, const __amdgpu_buffer_r
   for (int u = 0; u < 4; ++u) {
     const int i = w * 4 + u;  // B rows 8i .. 8i + 7
     const int row = 8 * i + rl;
-    const int k = k0 + 8 * (slot ^ (row & 7));
+    const int k = k0 + 8 * (slot ^ ((row >> 1) & 7));
     const uint32_t ob = k < kend ? (uint32_t)(((bn + row) * p.ldb + k) * 2) : 0x80000000u;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void *)(sb + i * 1024), 16, ob, 0, 0, 0);
   }

@@ -12,7 +12,7 @@
 //   * a K-tile is 128 fp8 of every row: A 256 x 128 B + B 256 x 128 B + the 4 scale bytes of each
 //     row, copied global -> LDS by buffer_load ... lds (16-B chunks, 8 rows x 128 B per wave
 //     instruction; scale words 4 B per lane), two stages: tile t + 1's DMA runs under tile t's
-//     MFMAs.  The LDS images are lane-linear; the 16-B chunk swizzle (chunk ^ row & 7) is applied
+//     MFMAs.  The LDS images are lane-linear; the 16-B chunk swizzle (chunk ^ (row >> 1 & 7)) is applied
 //     on the global source address, so fragment reads are the conflict-free pattern of gemm.hip's
 //     nt_frag8.  Rows past M / N read zeros (their outputs are not stored);
 //   * (tile, split) pairs are dealt to the XCDs in contiguous runs (tiles sharing a B panel, or a
@@ -133,7 +133,9 @@ __device__ __forceinline__ int xcd_run(int b, int nb) {  // bijective: block -> 
 constexpr int QNI = QA_BYTES / 1024 / 8;        // A (and B) instructions per wave per tile
 constexpr int QDMA_PER_TILE = 2 * QNI + 1;
 constexpr int QRPI = 1024 / QKB;                // rows per instruction
-__device__ __forceinline__ int q_swz(int row) { return QKB == 128 ? (row & 7) : ((row >> 2) & 3); }
+// (128-B rows: row >> 1 & 7 — see dxgemm.hip: under row & 7 the rows r and r + 8 of a ds_read_b128
+// lane group share a bank slot)
+__device__ __forceinline__ int q_swz(int row) { return QKB == 128 ? ((row >> 1) & 7) : ((row >> 2) & 3); }
 __device__ __forceinline__ void q_dma(const QP &p, const i32x4_t &ra, const i32x4_t &rb, const i32x4_t &rsa,
                                       const i32x4_t &rsb, char *smem, int st, int bm, int bn, int k0) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
