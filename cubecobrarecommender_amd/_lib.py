@@ -13,6 +13,7 @@ CC_KL_LDS_TARGETS = 1          # cc_dec_kl_args.flags bit 0
 CC_KL_DWO_PRODUCER_WAVES = 2   # ... bit 1
 CC_KL_SHORT_STORES = 4         # ... bit 2
 CC_KL_WIDE_TARGETS = 8         # ... bit 3
+CC_KL_DWO_NARROW = 16          # ... bit 4 (dWo's rounding differs: one pass over all rows)
 
 
 class CCError(RuntimeError):

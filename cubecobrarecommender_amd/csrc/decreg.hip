@@ -80,6 +80,7 @@ struct KlP {
   float4 *rowstat;                  // [rows] {m + ln s, -, S, sum t ln t}
   float2 *rowst2;                   // [rows] {m + ln s, S} (the main pass's MS staging)
   uint32_t *flag;                   // [1] an element with p < 1e-7 was seen this step
+  float *dw_part;                   // [d][V] kl_dwo2_kernel's first-half partial dWo
 };
 
 // Workgroup barrier over LDS only.  __syncthreads' release fence also waits for every outstanding
@@ -992,6 +993,15 @@ __global__ __launch_bounds__(NTH) void kl_fix_kernel(KlP p) {
 // (Staged by LDS-DMA instead, the compiler waits for every outstanding copy — vmcnt(0) — before
 // each chunk's LDS reads, so nothing stays in flight.)
 constexpr int DW_NB = 96, DW_KC = 128;
+// build knob (A/B): kl_dwo_kernel's B fragments one k step ahead
+#ifndef DWO_BPF
+#define DWO_BPF 1
+#endif
+// dev diagnostics (tools/micro/dwo_diag.hip; 0 in the library): 1 no MFMA, 2 no B reads, 4 no dZ
+// loads, 8 no A loads
+#ifndef DWO_DIAG
+#define DWO_DIAG 0
+#endif
 template <int D, bool V8>
 __global__ __launch_bounds__(NTH) void kl_dwo_kernel(KlP p) {
   constexpr int NB = DW_NB, NJ = NB / 32, KC = DW_KC, KS = KC / 16;
@@ -1014,6 +1024,7 @@ __global__ __launch_bounds__(NTH) void kl_dwo_kernel(KlP p) {
   // 24 KB in flight per CU, ~2.7 TB/s)
   v4u stg0[NPC], stg1[NPC];
   auto gload = [&](v4u (&stg)[NPC], int c) {
+    if constexpr (DWO_DIAG & 4) return;
 #pragma unroll
     for (int u = 0; u < NPC; ++u) {
       const int q = tid + NTH * u, r = q / PPR, e = q % PPR;
@@ -1034,6 +1045,7 @@ __global__ __launch_bounds__(NTH) void kl_dwo_kernel(KlP p) {
   const bf16_t *abase = p.D3tp + ((int64_t)min(wt, D / 32 - 1) * (p.ldt / 16) * 64 + lane) * 8;
   const int k0 = p.row0 / 16, klast = (p.row0 + p.rows) / 16 - 1;
   auto load_a = [&](bf16x8_t (&dst)[KS], int c) {
+    if constexpr (DWO_DIAG & 8) return;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
       dst[ks] = *reinterpret_cast<const bf16x8_t *>(abase + (int64_t)min(k0 + c * KS + ks, klast) * 512);
@@ -1044,10 +1056,13 @@ __global__ __launch_bounds__(NTH) void kl_dwo_kernel(KlP p) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
   bf16x8_t af[2][KS];
+  // (issue order as in the steady state — chunk c + 1's pieces, chunk c's A fragments, chunk c + 2's
+  // pieces — so the compiler's counted waits at the loop head, merged over entry and back edge, are
+  // the steady state's and not a drain to the newest chunk)
   gload(stg0, 0);
-  load_a(af[0], 0);
   swrite(stg0, 0);
   gload(stg1, 1);
+  load_a(af[0], 0);
   gload(stg0, 2);
   lds_barrier();
   // chunk c: stage st = c & 1.  Write chunk c + 1 (register set (c + 1) & 1, loaded two chunks ago)
@@ -1063,16 +1078,43 @@ __global__ __launch_bounds__(NTH) void kl_dwo_kernel(KlP p) {
     gload(sw, c + 3);
     if (active) {
       const bf16_t *Zc = Zs[st];
+      auto bfrag = [&](int ks, int j) {
+        if constexpr (DWO_DIAG & 2) return cur[(ks + j) % KS];
+        const bf16_t *tb = Zc + (ks * 16 + 8 * half + ((lane >> 2) & 3)) * NB + j * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)tb);
+        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)(tb + 4 * NB));
+        return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      };
+      if constexpr (DWO_BPF) {
+        // B fragments one k step ahead (two register sets): the k step's MFMAs wait on reads issued
+        // a whole step earlier, not on the ones just before them
+        bf16x8_t bq[2][NJ];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
+        for (int j = 0; j < NJ; ++j) bq[0][j] = bfrag(0, j);
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const bf16_t *tb = Zc + (ks * 16 + 8 * half + ((lane >> 2) & 3)) * NB + j * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)tb);
-          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)(tb + 4 * NB));
-          const bf16x8_t b = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[ks], b, acc[j], 0, 0, 0);
+        for (int ks = 0; ks < KS; ++ks) {
+          if (ks + 1 < KS) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) bq[(ks + 1) & 1][j] = bfrag(ks + 1, j);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            if constexpr (DWO_DIAG & 1) {
+              acc[j][0] += __builtin_bit_cast(float, __builtin_shufflevector(bq[ks & 1][j], bq[ks & 1][j], 0, 1));
+              acc[j][1] += __builtin_bit_cast(float, __builtin_shufflevector(cur[ks], cur[ks], 0, 1));
+            } else {
+              acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[ks], bq[ks & 1][j], acc[j], 0, 0, 0);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
         }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[ks], bfrag(ks, j), acc[j], 0, 0, 0);
+      }
     }
     lds_barrier();   // chunk c + 1 written; chunk c read (its stage is rewritten next)
   };
@@ -1202,6 +1244,203 @@ __global__ __launch_bounds__(DWP_NT) void kl_dwo_pc_kernel(KlP p) {
   }
 }
 
+// ---- dWo in wide slices (the default for d = 256, |V| % 8 == 0): kl_dwo_kernel spends its time
+// on the per-CU operand streams, not on the MFMAs: every 96-column block re-reads the whole packed
+// D3^T (11 MB at the full-mode shape — 2.7x the block's dZ bytes) and each of its 8 waves reads the
+// whole dZ chunk from LDS (tools/micro/dwo_diag.hip: the D3^T loads alone 134 us of its 345).
+// Here a block owns a 192-column slice and HALF of the rows (K split in two: 2 x 115 blocks), eight
+// waves (two per SIMD) of 32 rows of d x all 192 columns (6 accumulator tiles): per column, half
+// the D3^T bytes of kl_dwo_kernel.  dZ chunks of 128 rows x 192 columns (48 KB) are copied
+// global -> LDS by 16-B LDS-DMA (non-temporal: read once) two chunks ahead of use in a ring of
+// three stages; A fragments (8 k steps per wave) load one chunk ahead into registers.
+// Measured alone at the full-mode shape (tools/micro/dwo_diag.hip, r05z): 242 us + 13 us for the
+// halves' sum vs kl_dwo_kernel's 343; four waves of 64 rows (accumulators in AGPRs, one wave per
+// SIMD) 273, default cache policy on the copies 264, copies issued before the A loads (one chunk
+// of effective lead: the in-order wait for A(c) also waited for DMA(c + 1)) 294.  Both streams are inline asm with counted waits written here (the
+// compiler's own waits would count only what it sees; see dma_asm), in one fixed per-wave issue
+// order — A(c + 1), DMA(c + 2) per chunk c — so the counts are constants.  The LDS rows (384 B)
+// are stored with 16-B pieces XOR 4 on rows with bit 1 set (the DMA picks the source piece), which
+// puts the four rows of a ds_read_b64_tr_b16 lane group on disjoint banks.  The first half's
+// partial tile goes to the workspace, the second's to gW, and kl_dwo2_sum_kernel adds them (an
+// arrival ticket per slice with the second block adding instead cost ~100 us: the agent-scope
+// fences' L2 write-back / invalidate under the still-streaming blocks).
+#ifndef CCREC_DWO2
+#define CCREC_DWO2 1   // build knob (A/B builds): 0 = dWo by the 96-column kernels always
+#endif
+// dev diagnostics (tools/micro/dwo_diag.hip; 0 in the library): 2 no MFMA, 4 no dZ DMA, 8 no A
+// loads
+#ifndef DW2_DIAG
+#define DW2_DIAG 0
+#endif
+#ifndef DW2_CPOL
+#define DW2_CPOL KL_CPOL_NT   // build knob: the dZ copies' cache policy (0: default)
+#endif
+#ifndef DW2_WAVES
+#define DW2_WAVES 8   // build knob: 8 waves of 32 rows of d (two per SIMD) or 4 of 64 (one per SIMD)
+#endif
+constexpr int DW2_NB = 192, DW2_KC = 128, DW2_NS = 3, DW2_NT = 64 * DW2_WAVES, DW2_SPLIT = 2;
+constexpr int DW2_STAGE = DW2_KC * DW2_NB * 2;          // 48 KB
+constexpr int DW2_LDS = DW2_NS * DW2_STAGE;             // 144 KB
+
+template <int N>
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// 16 B per lane into registers, invisible to the compiler's counters: the caller waits (vm_wait)
+// and then re-defines the registers through an empty asm before any use
+__device__ __forceinline__ v4u a_load(const v4i &rs, uint32_t voff, uint32_t soff) {
+  v4u r;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(r) : "v"(voff), "s"(rs), "s"(soff));
+  return r;
+}
+
+template <int D>
+__global__ __launch_bounds__(DW2_NT) void kl_dwo2_kernel(KlP p) {
+  constexpr int NW = DW2_NT / 64, NBD = D / 32 / NW;    // waves; 32-row bands of d per wave
+  static_assert(D == 256 && NBD * NW * 32 == D, "d = 256 over the waves");
+  constexpr int NB = DW2_NB, NJ = NB / 32, KC = DW2_KC, KS = KC / 16, NS = DW2_NS;
+  constexpr int PPR = NB / 8;                            // 16-B pieces per chunk row
+  constexpr int NPW = DW2_STAGE / 1024 / NW;             // DMA instructions per wave per chunk
+  constexpr int NA = NBD * KS;                           // A loads per wave per chunk
+  static_assert(DW2_STAGE % (1024 * NW) == 0 && NPW + NA + NPW <= 63, "whole DMA instructions; vmcnt range");
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(1024))) char dw2mem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), half = lane >> 5;
+  const int sl = blockIdx.x, kh = blockIdx.y;
+  const int n0 = sl * NB, V = p.V;
+  const int nall = (p.rows + KC - 1) / KC;
+  const int cb = nall * kh / DW2_SPLIT, nch = nall * (kh + 1) / DW2_SPLIT - cb;
+  const v4i zr = sgpr_rsrc(p.dZ, (uint32_t)p.rows * (uint32_t)V * 2u);
+  const v4i ar = sgpr_rsrc(p.D3tp, (uint32_t)p.ldt * (uint32_t)D * 2u);
+  // DMA instruction t of this wave: LDS bytes [1024 (NPW w + t), ..) of the stage; lane L's 16 B are
+  // stage piece s = 64 (NPW w + t) + L = row s / PPR, position s % PPR, holding dZ piece
+  // position ^ 4 (row >> 1 & 1) of that row.  Columns past V read the next row / past the range
+  // (finite or 0; never stored), chunks past this half's end the sentinel (zeros, no traffic).
+  uint32_t vo[NPW];
+#pragma unroll
+  for (int t = 0; t < NPW; ++t) {
+    const int s = (NPW * w + t) * 64 + lane, r = s / PPR, e = (s % PPR) ^ (4 * ((r >> 1) & 1));
+    vo[t] = (uint32_t)(r * V + n0) * 2u + 16u * (uint32_t)e;
+  }
+  const uint32_t lbase = lds_addr(dw2mem) + 1024u * (uint32_t)(NPW * w);
+  auto dma = [&](int c) {
+    if constexpr (DW2_DIAG & 4) return;
+    const uint32_t so = c < nch ? (uint32_t)(cb + c) * (uint32_t)KC * (uint32_t)V * 2u : 0x80000000u;
+    const uint32_t base = lbase + (uint32_t)(c % NS) * (uint32_t)DW2_STAGE;
+#pragma unroll
+    for (int t = 0; t < NPW; ++t) dma_asm<16, DW2_CPOL>(zr, vo[t], so, base + 1024u * t);
+  };
+  // A fragment (band b, k step kk): the packed D3^T's 1-KB fragment (band NBD w + b, kk)
+  uint32_t va[NBD];
+#pragma unroll
+  for (int b = 0; b < NBD; ++b) va[b] = ((uint32_t)(NBD * w + b) * (uint32_t)(p.ldt / 16) * 64u + (uint32_t)lane) * 16u;
+  const int k0 = p.row0 / 16, klast = (p.row0 + p.rows) / 16 - 1;
+  auto aload = [&](v4u (&dst)[NBD][KS], int c) {   // (c past the end: clamped, never used)
+    if constexpr (DW2_DIAG & 8) return;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const uint32_t so = (uint32_t)min(k0 + (cb + c) * KS + ks, klast) * 1024u;
+#pragma unroll
+      for (int b = 0; b < NBD; ++b) dst[b][ks] = a_load(ar, va[b], so);
+    }
+  };
+  f32x16_t acc[NBD][NJ];
+#pragma unroll
+  for (int b = 0; b < NBD; ++b)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[b][j][r] = 0.f;
+  v4u af[2][NBD][KS];
+  // (a load's destination must stay allocated until its wait: a dead result register reused for
+  // something else would be overwritten when the load lands — hence no dummy loads, and every
+  // set kept live to the final wait)
+  dma(0);
+  aload(af[0], 0);
+  dma(1);
+  // B fragment (k step ks, column tile j) of a stage: rows ks 16 + 8 half + (lane >> 2 & 3) (+ 4),
+  // 4 columns at j 32 + 16 (lane >> 4 & 1) + 4 (lane & 3), XOR 32 on rows with bit 1 set (= lane
+  // bit 3): column tile j ^ 1 there, i.e. + 32 for even j and - 32 for odd j
+  const int sw = 32 * ((lane >> 3) & 1);
+  const int boff0 = (8 * half + ((lane >> 2) & 3)) * NB + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  const int boff[2] = {boff0 + sw, boff0 - sw};
+  // per chunk c: A(c + 1), then DMA(c + 2) — the wait for A(c) does not wait for DMA(c + 1), so
+  // the copies keep two chunks of lead (DMA first, measured: one)
+  auto body = [&](v4u (&cur)[NBD][KS], v4u (&nxt)[NBD][KS], int c) {
+    vm_wait<NA + NPW>();        // own DMA(c) landed (younger: A(c), DMA(c + 1))
+    lds_barrier();              // every wave's DMA(c) landed; stage (c - 1) % NS read by all
+    aload(nxt, c + 1);
+    dma(c + 2);
+    vm_wait<NPW + NA + NPW>();  // A(c) landed (younger: DMA(c + 1), A(c + 1), DMA(c + 2))
+#pragma unroll
+    for (int b = 0; b < NBD; ++b)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(cur[b][ks]));
+    const bf16_t *Zc = reinterpret_cast<const bf16_t *>(dw2mem + (c % NS) * DW2_STAGE);
+    auto bfrag = [&](int ks, int j) {
+      const bf16_t *tb = Zc + boff[j & 1] + ks * 16 * NB + j * 32;
+      const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)tb);
+      const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)(tb + 4 * NB));
+      return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    bf16x8_t bq[2][NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bq[0][j] = bfrag(0, j);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bq[(ks + 1) & 1][j] = bfrag(ks + 1, j);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int b = 0; b < NBD; ++b) {
+        const bf16x8_t a = __builtin_bit_cast(bf16x8_t, cur[b][ks]);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          if constexpr (DW2_DIAG & 2)
+            acc[b][j][0] += __builtin_bit_cast(float, __builtin_shufflevector(bq[ks & 1][j], a, 0, 9));
+          else
+            acc[b][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq[ks & 1][j], acc[b][j], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  int c = 0;
+  for (; c + 1 < nch; c += 2) {
+    body(af[0], af[1], c);
+    body(af[1], af[0], c + 1);
+  }
+  if (c < nch) body(af[0], af[1], c);
+  vm_wait<0>();   // the trailing (sentinel) DMAs land before the block's LDS is released
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int b = 0; b < NBD; ++b)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(af[u][b][ks]));   // (live to here: see above)
+  // this half's partial: the first half into dw_part, the second into gW (kl_dwo2_sum_kernel adds)
+  float *mine = kh == 0 ? p.dw_part : p.gW;
+#pragma unroll
+  for (int b = 0; b < NBD; ++b)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int gc = n0 + j * 32 + (lane & 31);
+      if (gc < V) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mine[(int64_t)(32 * (NBD * w + b) + acc_row(r, lane)) * V + gc] = acc[b][j][r];
+      }
+    }
+}
+
+// gW = dw_part + gW (the two row halves' partial dWo; n4 float4)
+__global__ __launch_bounds__(256) void kl_dwo2_sum_kernel(const float4 *__restrict__ part, float4 *__restrict__ gw, int64_t n4) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 a = part[i], b = gw[i];
+    gw[i] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  }
+}
+
 __global__ __launch_bounds__(256) void kl_tsum_kernel(const float *__restrict__ Mt, int V, float *__restrict__ tsum) {
   __shared__ float red[2][4];
   const float *row = Mt + (int64_t)blockIdx.x * V;
@@ -1230,7 +1469,9 @@ __global__ __launch_bounds__(256) void kl_tsum_kernel(const float *__restrict__ 
 
 extern "C" size_t cc_dec_kl_ws_size(int32_t rows, int32_t V) {
   const int64_t nsl = cdiv(V, NB_MIN);   // an upper bound over every d
-  return (size_t)(3 * rows * nsl * sizeof(float) + rows * sizeof(float4) + 256 + rows * sizeof(float2));
+  // (+ kl_dwo2_kernel's first-half partial dWo, d = 256, when rows take many tiles)
+  const size_t dw2 = rows > TR ? (size_t)256 * V * sizeof(float) : 0;
+  return (size_t)(3 * rows * nsl * sizeof(float) + rows * sizeof(float4) + 256 + rows * sizeof(float2)) + dw2;
 }
 
 extern "C" int32_t cc_dec_kl_blocks(int32_t V) { return (int32_t)cdiv(V, NB_MIN); }   // upper bound over d
@@ -1291,6 +1532,8 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
   p.part_d = p.part_s + pn;
   p.flag = (uint32_t *)(p.part_d + pn);
   p.rowst2 = (float2 *)(ws + a->rows * sizeof(float4) + 3 * pn * sizeof(float) + 256);   // (16-B aligned: rows % 32)
+  // kl_dwo2_kernel's region (sized by cc_dec_kl_ws_size for rows > TR; 16-B aligned)
+  p.dw_part = a->rows > TR ? (float *)(p.rowst2 + a->rows) : nullptr;
   hipStream_t s = as_stream(stream);
   const dim3 gs((unsigned)p.nsl), gm((unsigned)p.nsl);
   // many row tiles (full mode): dWo from the stored dZ by kl_dwo_kernel (even V: 4-B aligned rows);
@@ -1307,6 +1550,11 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
   const bool wload = ((uintptr_t)a->Mt & 15) == 0 && (a->flags & CC_KL_WIDE_TARGETS);
   // dWo's dZ stream by producer waves' LDS-DMA (16-B aligned rows): opt-in (measured no faster)
   const bool dwo_pc = a->V % 8 == 0 && ((uintptr_t)a->dZ & 15) == 0 && (a->flags & CC_KL_DWO_PRODUCER_WAVES);
+  // dWo in 192-column slices x two row halves (kl_dwo2_kernel): 16-B aligned rows, the chunk
+  // sentinel 0x80000000 past dZ's range, at least one chunk per half
+  const bool dwo2 = CCREC_DWO2 && a->d == 256 && a->V % 8 == 0 && (((uintptr_t)a->dZ | (uintptr_t)a->gW) & 15) == 0 &&
+                    (int64_t)a->rows * a->V * 2 < 0x80000000ll && cdiv(a->rows, DW2_KC) >= DW2_SPLIT &&
+                    p.dw_part && !(a->flags & (CC_KL_DWO_NARROW | CC_KL_DWO_PRODUCER_WAVES));
 #define KL_LAUNCH(DD)                                                                                          \
   if (a->d == DD) {                                                                                          \
     hipLaunchKernelGGL((kl_stats_kernel<DD>), gs, dim3(NTH), 0, s, p);                                      \
@@ -1332,6 +1580,16 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
                                                       DWP_NS * DW_KC * DW_NB * 2) == hipSuccess;              \
         CC_REQUIRE(attr, "cc_dec_softmax_kl_dw: dynamic LDS attribute");                                     \
         hipLaunchKernelGGL((kl_dwo_pc_kernel<DD>), gd, dim3(DWP_NT), DWP_NS * DW_KC * DW_NB * 2, s, p);      \
+      } else if (dwo2 && DD == 256) {                                                                        \
+        static const bool attr2 = hipFuncSetAttribute((const void *)kl_dwo2_kernel<256>,                     \
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, DW2_LDS) == \
+                                  hipSuccess;                                                                \
+        CC_REQUIRE(attr2, "cc_dec_softmax_kl_dw: dynamic LDS attribute");                                    \
+        hipLaunchKernelGGL((kl_dwo2_kernel<256>), dim3((unsigned)cdiv(a->V, DW2_NB), DW2_SPLIT), dim3(DW2_NT), \
+                           DW2_LDS, s, p);                                                                   \
+        CC_LAUNCH_CHECK("kl_dwo2_kernel");                                                                   \
+        hipLaunchKernelGGL(kl_dwo2_sum_kernel, dim3(1024), dim3(256), 0, s, (const float4 *)p.dw_part,        \
+                           (float4 *)p.gW, (int64_t)256 * a->V / 4);                                         \
       } else if (a->V % 8 == 0)                                                                              \
         hipLaunchKernelGGL((kl_dwo_kernel<DD, true>), gd, dim3(NTH), 0, s, p);                               \
       else                                                                                                   \

@@ -514,12 +514,16 @@ typedef struct cc_dec_kl_args {
                                 dWo's dZ stream by producer waves' LDS-DMA (slower); CC_KL_SHORT_STORES:
                                 dZ stored 2 B per lane instead of 16-B rows through LDS (slower);
                                 CC_KL_WIDE_TARGETS: M~ loaded as 16-B rows turned into the accumulator
-                                layout through LDS instead of 4 B per lane (slower) */
+                                layout through LDS instead of 4 B per lane (slower).  CC_KL_DWO_NARROW
+                                (not bit-identical: dWo summed over all rows in one pass instead of two
+                                row halves added): dWo by the 96-column kernel of round 4 (slower);
+                                CC_KL_DWO_PRODUCER_WAVES implies it */
 } cc_dec_kl_args;
 #define CC_KL_LDS_TARGETS 1
 #define CC_KL_DWO_PRODUCER_WAVES 2
 #define CC_KL_SHORT_STORES 4
 #define CC_KL_WIDE_TARGETS 8
+#define CC_KL_DWO_NARROW 16
 size_t cc_dec_kl_ws_size(int32_t rows, int32_t V);
 int32_t cc_dec_kl_blocks(int32_t V);
 int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream);

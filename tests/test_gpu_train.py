@@ -464,7 +464,9 @@ def test_full_mode_clip_fix_path(V, spread):
     M~ staged through LDS (MS, V % 4 == 0: its rare-path reload of M~ for the clip partials, its
     counted waits across tiles) with dWo's producer-wave dZ stream (V % 8 == 0), M~ loaded as 16-B
     rows through LDS, and the 2-B dZ stores instead of 16-B rows through LDS (V % 8 == 0;
-    V = 2,502 has none of them)."""
+    V = 2,502 has none of them).  dWo: the default at V % 8 == 0 is kl_dwo2_kernel (two row halves
+    added); the 96-column kernels (CC_KL_DWO_NARROW, the producer-wave variant) sum all rows in one
+    pass — every other output identical, dWo equal to float rounding."""
     d, B = 256, 128
 
     def run(flags):
@@ -497,10 +499,16 @@ def test_full_mode_clip_fix_path(V, spread):
     # stores through LDS (V % 8 == 0)
     # against the register-staged paths: identical bits
     g1 = tr.layout.unpack(tr.grads.cpu().numpy())
-    for flags in (L.CC_KL_LDS_TARGETS | L.CC_KL_DWO_PRODUCER_WAVES, L.CC_KL_WIDE_TARGETS, L.CC_KL_SHORT_STORES):
+    dwo = 'decoder_for_reg/reconstruct/kernel'
+    for flags in (L.CC_KL_LDS_TARGETS | L.CC_KL_DWO_PRODUCER_WAVES, L.CC_KL_WIDE_TARGETS, L.CC_KL_SHORT_STORES,
+                  L.CC_KL_DWO_NARROW):
         tr2 = run(flags)[0]
         g2 = tr.layout.unpack(tr2.grads.cpu().numpy())
         diff = {k: float(np.abs(g1[k] - g2[k]).max()) for k in g1 if not np.array_equal(g1[k], g2[k])}
+        narrow = V % 8 == 0 and flags & (L.CC_KL_DWO_NARROW | L.CC_KL_DWO_PRODUCER_WAVES)
+        if narrow and dwo in diff:   # one K order vs two row halves: float rounding only
+            scale = float(np.abs(g1[dwo]).max())
+            assert diff.pop(dwo) <= 2e-6 * scale, (flags, scale)
         assert torch.equal(tr2.dZout, tr.dZout) and not diff, (flags, diff)
         assert tr2.losses() == tr.losses(), (flags, tr2.losses(), tr.losses())
 
