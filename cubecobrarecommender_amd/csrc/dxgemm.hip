@@ -152,6 +152,10 @@ __global__ __launch_bounds__(XNT) void dx_splitk_kernel(DxP p) {
 // B 256 x 64 (48 KB each).  Splits are dealt split-major over the XCDs as above, so a split's Wo
 // panel (256 x K/splits bf16) stays in one XCD's L2.
 constexpr int WBM = 128, WBN = 256, WST = 3, WNT = 512;
+// dev diagnostics (tools/micro/dx_diag.hip; 0 in the library): 1 no Wo copies, 2 no dZ copies, 4 no MFMA
+#ifndef DXW_DIAG
+#define DXW_DIAG 0
+#endif
 constexpr int WTILE_BYTES = (WBM + WBN) * XBK * 2;  // 48 KB
 constexpr int WLDS = WST * WTILE_BYTES;              // 144 KB
 
@@ -165,6 +169,7 @@ __device__ __forceinline__ void dma_tile_w(const DxP &p, const __amdgpu_buffer_r
   char *sa = smem + st * WTILE_BYTES, *sb = sa + WBM * XBK * 2;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
+    if constexpr (DXW_DIAG & 2) break;
     const int i = w * 2 + u;  // A rows 8i .. 8i + 7
     const int row = 8 * i + rl;
     const int k = k0 + 8 * (slot ^ ((row >> 1) & 7));
@@ -173,6 +178,7 @@ __device__ __forceinline__ void dma_tile_w(const DxP &p, const __amdgpu_buffer_r
   }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
+    if constexpr (DXW_DIAG & 1) break;
     const int i = w * 4 + u;  // B rows 8i .. 8i + 7
     const int row = 8 * i + rl;
     const int k = k0 + 8 * (slot ^ ((row >> 1) & 7));
@@ -217,6 +223,11 @@ __global__ __launch_bounds__(WNT) void dx_wide_kernel(DxP p) {
     const char *sa = wsmem + (t % WST) * WTILE_BYTES, *sb = sa + WBM * XBK * 2;
 #pragma unroll
     for (int kk = 0; kk < XBK / 16; ++kk) {
+      if constexpr (DXW_DIAG & 4) {
+        const int c = 2 * kk + half;
+        acc[0][0][0] += __builtin_bit_cast(float, __builtin_shufflevector(frag(sa, ar, c), frag(sb, br, c), 0, 9));
+        continue;
+      }
       const int c = 2 * kk + half;
       const bf16x8_t a0 = frag(sa, ar, c), a1 = frag(sa, ar + 32, c);
       const bf16x8_t b0 = frag(sb, br, c), b1 = frag(sb, br + 32, c);
