@@ -30,6 +30,8 @@ def parse():
                     help="the trailing fraction of Wo's Adam run in the tower backward launch (-1: TrainConfig's default)")
     ap.add_argument('--f-in-tower', type=int, default=0,
                     help='one process: the next step\'s F in the tower backward launch (1) or the Adam launch (0)')
+    ap.add_argument('--dx-packed-wo', type=int, default=1,
+                    help="full mode: the regulariser's dX from Wo's fragment image (1) or the row-major Wo (0)")
     ap.add_argument('--prespin-ms', type=float, default=300.0,
                     help='untimed non-training GPU work (a memory-bound scale + a bf16 matmul loop) before '
                          'warmup: the GPU out of its idle clocks, so that a short --warmup already times the '
@@ -460,7 +462,8 @@ def main():
                       dz_pad=bool(args.dz_pad), graph_steps=graph_steps, wo_tower_frac=args.wo_tower_frac,
                       fuse_w1_adam=True,   # one process: W1's Adam in its gradient kernel, and (BCE
                       wo_adam_in_tower=True,   # only) Wo's in the tower backward launch, with the next
-                      f_in_tower=bool(args.f_in_tower))   # step's F (parity:
+                      f_in_tower=bool(args.f_in_tower),   # step's F (parity:
+                      dx_packed_wo=bool(args.dx_packed_wo))
     #                                        tests/test_gpu_train.py::test_fused_w1_adam_matches_unfused)
     tr = Trainer(cfg, data, params_flat=glorot_flat(V, d, seed=42), device=dev)
     rng = np.random.default_rng(99)      # same permutations on every rank

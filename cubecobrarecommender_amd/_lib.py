@@ -124,6 +124,9 @@ SIGNATURES = {
     'cc_dec_softmax_kl_fused': (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _F32, _P, _P, _P]),
     'cc_reduce_loss': (C.c_int, [_P, _I32, _F64, _P, _P]),
     'cc_gemm_dx_splitk': (C.c_int, [_P, _I32, _P, _I32, _I32, _I32, _I32, _I32, _P, _P]),
+    'cc_pack_frag_b_size': (_SZ, [_I32, _I32]),
+    'cc_pack_frag_b': (C.c_int, [_P, _I32, _I32, _I32, _P, _P]),
+    'cc_gemm_dx_splitk_pk': (C.c_int, [_P, _I32, _P, _I32, _I32, _I32, _I32, _P, _P]),
     'cc_dec_kl_ws_size': (_SZ, [_I32, _I32]),
     'cc_dec_kl_blocks': (_I32, [_I32]),
     'cc_dec_softmax_kl_dw': (C.c_int, [C.POINTER(DecKlArgs), _P]),

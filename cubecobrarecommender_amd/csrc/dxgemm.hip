@@ -251,7 +251,167 @@ __global__ __launch_bounds__(WNT) void dx_wide_kernel(DxP p) {
     }
 }
 
+// ---- the tall shape with Wo from its packed fragment image (cc_pack_frag_b): only the dZ tile goes
+// through LDS (LDS-DMA, 16 KB per K-tile, three stages); each wave owns 32 columns of N and all 128
+// rows and loads its Wo fragments — 1 KB per wave instruction, one fragment (32 columns x 16 k) per
+// load — one K-tile ahead into registers: each Wo element once per block, fully coalesced, no LDS
+// round trip (dx_wide_kernel: copies 361 of its 388 us; the same loads from the row-major Wo, 16 B
+// from each of 32 rows per instruction, were slower: 440).  Per K-tile and wave: B(t + 1) loads,
+// then DMA(t + 2), so the counted wait for B(t) does not wait on the newest copies; copies and
+// loads past the end use the range sentinel (zeros, no traffic) so every iteration issues the same
+// count.  The MFMA chain per output is the other paths' (bit-identical partials).
+constexpr int W3ST = 3, W3NT = 512;
+constexpr int W3TILE = WBM * XBK * 2;   // 16 KB: the dZ tile only
+
+__global__ __launch_bounds__(W3NT) void dx_wide3_kernel(DxP p) {
+  extern __shared__ __attribute__((aligned(1024))) char w3mem[];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), half = lane >> 5;
+  const int ntiles = p.tiles_m * (p.N / WBN);
+  const int q = xcd_remap(blockIdx.x, ntiles * p.splits);
+  const int split = q / ntiles, tile = q % ntiles;
+  const int bm = (tile % p.tiles_m) * WBM, bn = (tile / p.tiles_m) * WBN;
+  const int kbeg = split * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
+  const int nk = kbeg < kend ? (kend - kbeg + XBK - 1) / XBK : 0;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void *)p.A, (short)0, p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void *)p.B, (short)0, p.b_bytes, 0x00020000);
+  const int rl = lane >> 3, slot = lane & 7;
+  auto dma = [&](int t) {   // dZ K-tile t -> stage t % W3ST: 2 instructions of 8 rows x 128 B per wave
+    char *sa = w3mem + (t % W3ST) * W3TILE;
+    const int k0 = kbeg + t * XBK;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = w * 2 + u, row = 8 * i + rl;
+      const int k = k0 + 8 * (slot ^ ((row >> 1) & 7));
+      const uint32_t oa = k < kend ? (uint32_t)(((bm + row) * p.lda + k) * 2) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void *)(sa + i * 1024), 16, oa, 0, 0, 2);   // dZ: nt
+    }
+  };
+  // fragment (band, k step) of the packed image: 1 KB at (band * nks + k step) KB, lane L's 16 B at 16 L
+  const int nks = (p.K + 15) / 16;
+  const uint32_t bbase = (uint32_t)((bn / 32 + w) * nks) * 1024u + 16u * (uint32_t)lane;
+  auto bload = [&](bf16x8_t (&dst)[XBK / 16], int t) {   // Wo fragments of K-tile t
+    const int k0 = kbeg + t * XBK;
+#pragma unroll
+    for (int ks = 0; ks < XBK / 16; ++ks) {
+      const int k = k0 + 16 * ks;
+      const uint32_t ob = k < kend ? bbase + (uint32_t)(k / 16) * 1024u : 0x80000000u;
+      dst[ks] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(rb, ob, 0, 0));
+    }
+  };
+  f32x16_t acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+  bf16x8_t bf[2][XBK / 16];
+  // prologue in the steady order: DMA(0), B(0), DMA(1) (sched barriers: the waits count on the order)
+  dma(0);
+  __builtin_amdgcn_sched_barrier(0);
+  bload(bf[0], 0);
+  __builtin_amdgcn_sched_barrier(0);
+  dma(1);
+  __builtin_amdgcn_sched_barrier(0);
+  const int ar = lane & 31;
+  auto body = [&](bf16x8_t (&cur)[XBK / 16], bf16x8_t (&nxt)[XBK / 16], int t) {
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // own DMA(t) landed (younger: B(t), DMA(t + 1))
+    __builtin_amdgcn_s_barrier();   // every wave's DMA(t) landed; stage (t - 1) % 3 read by all
+    asm volatile("" ::: "memory");
+    bload(nxt, t + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    dma(t + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    const char *sa = w3mem + (t % W3ST) * W3TILE;
+#pragma unroll
+    for (int ks = 0; ks < XBK / 16; ++ks) {
+      const int c = 2 * ks + half;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(sa, ar + 32 * i, c), cur[ks], acc[i], 0, 0, 0);
+    }
+  };
+  int t = 0;
+  for (; t + 1 < nk; t += 2) {
+    body(bf[0], bf[1], t);
+    body(bf[1], bf[0], t + 1);
+  }
+  if (t < nk) body(bf[0], bf[1], t);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing copies land before the LDS is released
+  float *out = p.P + (int64_t)split * p.M * p.N;
+  const int n = bn + 32 * w + (lane & 31);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = bm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+      out[(int64_t)row * p.N + n] = acc[i][r];
+    }
+  }
+}
+
+// B [N][K] bf16 (row pitch ldb) -> MFMA B-fragment image [N / 32][ceil(K / 16)][64 lanes][8]: lane L
+// of fragment (band, k step) holds B[32 band + (L & 31)][16 k step + 8 (L >> 5) ..][8]; k >= K zero
+__global__ __launch_bounds__(256) void pack_frag_b_kernel(const bf16_t *__restrict__ B, int N, int K, int ldb,
+                                                          uint4 *__restrict__ dst) {
+  const int nks = (K + 15) / 16;
+  const int64_t total = (int64_t)(N / 32) * nks * 64;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int lane = (int)(i & 63);
+    const int64_t f = i >> 6;
+    const int band = (int)(f / nks), ks = (int)(f % nks);
+    const int n = 32 * band + (lane & 31), k = 16 * ks + 8 * (lane >> 5);
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (k < K) v = *reinterpret_cast<const uint4 *>(B + (int64_t)n * ldb + k);   // (K % 8 == 0)
+    dst[i] = v;
+  }
+}
+
 }  // namespace
+
+extern "C" size_t cc_pack_frag_b_size(int32_t N, int32_t K) { return (size_t)(N / 32) * ((K + 15) / 16) * 1024; }
+
+extern "C" int cc_pack_frag_b(const void *B, int32_t N, int32_t K, int32_t ldb, void *dst, void *stream) {
+  CC_REQUIRE(B && dst && N > 0 && N % 32 == 0 && K > 0 && K % 8 == 0 && ldb % 8 == 0 && ldb >= K,
+             "cc_pack_frag_b: N % 32, K % 8, ldb % 8, ldb >= K");
+  CC_REQUIRE((((uintptr_t)B | (uintptr_t)dst) & 15) == 0, "cc_pack_frag_b: 16-B aligned");
+  hipLaunchKernelGGL(pack_frag_b_kernel, dim3(2048), dim3(256), 0, as_stream(stream), (const bf16_t *)B, N, K, ldb,
+                     (uint4 *)dst);
+  CC_LAUNCH_CHECK("pack_frag_b_kernel");
+  return CC_OK;
+}
+
+extern "C" int cc_gemm_dx_splitk_pk(const void *A, int32_t lda, const void *Bp, int32_t M, int32_t N, int32_t K,
+                                    int32_t splits, float *partials, void *stream) {
+  CC_REQUIRE(A && Bp && partials, "cc_gemm_dx_splitk_pk: null pointer");
+  CC_REQUIRE(M > 0 && N > 0 && M % WBM == 0 && N % WBN == 0, "cc_gemm_dx_splitk_pk: M % 128, N % 256");
+  CC_REQUIRE(K > 0 && K % 8 == 0 && lda % 8 == 0 && lda >= K, "cc_gemm_dx_splitk_pk: K, lda multiples of 8, lda >= K");
+  CC_REQUIRE(splits >= 1 && splits <= 1024, "cc_gemm_dx_splitk_pk: splits 1..1024");
+  CC_REQUIRE((int64_t)M * lda * 2 < 0x80000000ll && (int64_t)cc_pack_frag_b_size(N, K) < 0x80000000ll,
+             "cc_gemm_dx_splitk_pk: operands below 2 GB (32-bit buffer offsets)");
+  CC_REQUIRE((((uintptr_t)A | (uintptr_t)Bp) & 15) == 0, "cc_gemm_dx_splitk_pk: operands 16-B aligned");
+  DxP p;
+  p.A = (const bf16_t *)A;
+  p.B = (const bf16_t *)Bp;
+  p.P = partials;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = lda;
+  p.ldb = 0;
+  p.splits = splits;
+  p.kchunk = (int)cdiv(cdiv(K, splits), XBK) * XBK;
+  p.tiles_m = M / WBM;
+  p.a_bytes = (uint32_t)((int64_t)M * lda * 2);
+  p.b_bytes = (uint32_t)cc_pack_frag_b_size(N, K);
+  static bool attr3 = [] {
+    return hipFuncSetAttribute((const void *)dx_wide3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               W3ST * W3TILE) == hipSuccess;
+  }();
+  CC_REQUIRE(attr3, "cc_gemm_dx_splitk_pk: dynamic LDS attribute");
+  const int nb = (M / WBM) * (N / WBN) * splits;
+  hipLaunchKernelGGL(dx_wide3_kernel, dim3((unsigned)nb), dim3(W3NT), W3ST * W3TILE, as_stream(stream), p);
+  CC_LAUNCH_CHECK("dx_wide3_kernel");
+  return CC_OK;
+}
 
 extern "C" int cc_gemm_dx_splitk(const void *A, int32_t lda, const void *B, int32_t ldb, int32_t M, int32_t N,
                                  int32_t K, int32_t splits, float *partials, void *stream) {

@@ -50,6 +50,7 @@ class TrainConfig:
     #                                sampled regulariser; bench.py --wo-tower-frac sweeps)
     dx_splits: int = 0             # decoder dX K-splits (0: measured default, 32 bf16 / 16 fp8)
     dx_splits_reg: int = 0         # ... of the full-mode regulariser branch (0: 4)
+    dx_packed_wo: bool = True      # full-mode regulariser dX from Wo's fragment image (cc_gemm_dx_splitk_pk)
     mx8_bce_q: bool = True         # fp8: the BCE product writes dZ's MX-FP8 images (else quantiser launches)
     mx8_pair_reg_logits: bool = True   # fp8: the regulariser logits as extra blocks of the BCE product's launch
     graph_steps: int = 8           # one process: consecutive steady-state steps per hipGraph replay (step_many)
@@ -318,6 +319,7 @@ class Trainer:
         self.RP = (R + 63) // 64 * 64
         # decoder dX on the LDS-DMA pipelined split-K kernel (dxgemm.hip; other dtypes: gemm.hip's)
         self.dx_glds = self.dtype == L.CC_BF16
+        self.WoP = None   # the full-mode regulariser's Wo as its MFMA fragment image (below)
         # D1 output layer fused (logits + BCE + dZ + dWo, csrc/decout.hip) where its shape fits
         self.fused_out = (self.dtype == L.CC_BF16 and self.fused_tower and not self.mx8 and d in (128, 256, 512)
                           and B in (128, 256, 512))
@@ -377,6 +379,11 @@ class Trainer:
             self.dZt = [torch.zeros(V, n, **T) if not (k == 1 and self.fused_reg) else None
                         for k, n in enumerate(self.branch_rows())]   # [branch][V][rows]
             self.WoT = torch.zeros(len(branches_of(self.use_reg)), V, d, **T)
+            # the full-mode regulariser's dX takes Wo as its MFMA B-fragment image (cc_pack_frag_b,
+            # refreshed with the other decoder operands after each update; cc_gemm_dx_splitk_pk)
+            if (self.full_reg and self.fused_reg and self.dx_glds and d % 256 == 0 and V % 8 == 0
+                    and self.Breg % 128 == 0 and cfg.dx_packed_wo):
+                self.WoP = torch.zeros(int(L.lib().cc_pack_frag_b_size(d, V)) // 2, **T)
             if self.mx8:   # MX-FP8 operand images of the decoder output layers (csrc/mx8.hip)
                 nbr, u8 = len(branches_of(self.use_reg)), dict(device=self.dev, dtype=torch.uint8)
                 self.Vp = (V + 127) // 128 * 128
@@ -660,8 +667,10 @@ class Trainer:
         for k, pre in enumerate(branches_of(self.use_reg)):
             if k == 0 and self.fused_out:
                 continue    # cc_dec_bce_dw reads Wo itself: no Wo^T copy for the D1 branch
-            if k == 1 and self.fused_reg:
-                continue    # cc_dec_softmax_kl_dw reads Wo itself
+            if k == 1 and self.fused_reg:   # cc_dec_softmax_kl_dw reads Wo itself
+                if self.WoP is not None:     # ... the dX product its fragment image
+                    L.call('cc_pack_frag_b', self.w(pre + '/reconstruct/kernel'), d, V, V, L.ptr(self.WoP), s)
+                continue
             if self.mx8:   # both images from one read of Wo (cc_quant_mx8_both)
                 L.call('cc_quant_mx8_both', L.CC_BF16, self.w(pre + '/reconstruct/kernel'), d, V, V,
                        L.ptr(self.WoT8[k]), d, L.ptr(self.WoT8s[k]), L.ptr(self.Wo8[k]), self.Vp,
@@ -922,7 +931,7 @@ class Trainer:
                                 epi=L.CC_EPI_SPLITK, Cf=L.ptr(self.split_buf), splits=splits,
                                 launch=False)
                 if k == 1 and self.fused_reg:   # dWo/dbo came out of cc_dec_softmax_kl_dw: dX only
-                    self._dx(gx, r0, nr, splits, pre, s)
+                    self._dx(gx, r0, nr, splits, pre, s, k=1)
                     L.call('cc_splitk_reduce', self.dtype, L.ptr(self.split_buf), splits, nr, d,
                            L.ptr(self.D3[r0:]), L.ptr(self.gD3[r0:]), None, None, None, s)
                     continue
@@ -994,12 +1003,16 @@ class Trainer:
             return f'w1_{len(self.layout.w1_chunks) - 1}'
         return 'towers_e1'
 
-    def _dx(self, gx, r0, nr, splits, pre, s):
+    def _dx(self, gx, r0, nr, splits, pre, s, k=0):
         """Decoder dX split-K partials into split_buf: the LDS-DMA pipelined kernel (dxgemm.hip)
-        on the bf16 shapes it takes, else cc_gemm's register-staged NT path (same partials)."""
+        on the bf16 shapes it takes (the full-mode regulariser's with Wo's fragment image), else
+        cc_gemm's register-staged NT path (same partials)."""
         d, V = self.cfg.d, self.cfg.V
         A, lda = self._dz_of(r0)
-        if (self.dx_glds and not self.mx8 and nr % 128 == 0 and d % 128 == 0 and V % 8 == 0
+        if k == 1 and self.WoP is not None and nr % 128 == 0 and dx_splitk_fits(nr, V, d):
+            L.call('cc_gemm_dx_splitk_pk', L.ptr(A), lda, L.ptr(self.WoP), nr, d, V, splits,
+                   L.ptr(self.split_buf), s)
+        elif (self.dx_glds and not self.mx8 and nr % 128 == 0 and d % 128 == 0 and V % 8 == 0
                 and dx_splitk_fits(nr, V, d)):
             L.call('cc_gemm_dx_splitk', L.ptr(A), lda, self.w(pre + '/reconstruct/kernel'), V,
                    nr, d, V, splits, L.ptr(self.split_buf), s)

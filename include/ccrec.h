@@ -553,6 +553,16 @@ int cc_cat_accuracy(const float *Z, int32_t ldz, int32_t rows, int32_t V, const 
  * path; reduce with cc_splitk_reduce.  M, N multiples of 128, K % 8 == 0, operands < 2 GB. */
 int cc_gemm_dx_splitk(const void *A, int32_t lda, const void *B, int32_t ldb, int32_t M, int32_t N,
                       int32_t K, int32_t splits, float *partials, void *stream);
+/* B [N][K] bf16 (pitch ldb) -> its MFMA B-fragment image dst [N/32][ceil(K/16)][64][8] bf16 (lane L of
+ * fragment (band, k step): B[32 band + (L & 31)][16 k step + 8 (L >> 5) + 0..7], zeros past K);
+ * cc_pack_frag_b_size bytes.  N % 32 == 0, K % 8 == 0, 16-B aligned. */
+size_t cc_pack_frag_b_size(int32_t N, int32_t K);
+int cc_pack_frag_b(const void *B, int32_t N, int32_t K, int32_t ldb, void *dst, void *stream);
+/* cc_gemm_dx_splitk with B given as its cc_pack_frag_b image Bp (the tall full-mode dX: Wo's
+ * fragments loaded straight into registers, only dZ through LDS): the same partials bit for bit.
+ * M % 128 == 0, N % 256 == 0. */
+int cc_gemm_dx_splitk_pk(const void *A, int32_t lda, const void *Bp, int32_t M, int32_t N, int32_t K,
+                         int32_t splits, float *partials, void *stream);
 /* loss_out[0] = sum(partials[0:n]) * scale (fixed order, fp64) */
 int cc_reduce_loss(const double *partials, int32_t n, double scale, double *loss_out, void *stream);
 

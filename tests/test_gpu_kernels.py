@@ -644,3 +644,29 @@ def test_dx_splitk_glds_matches_nt_gemm(M, N, K, splits):
     want = (A.float() @ Bm.float().t()).cpu().numpy()
     assert rel_err(p1.sum(0).cpu().numpy(), want) < 1e-5
     np.testing.assert_array_equal(p1.cpu().numpy(), p0.cpu().numpy())
+
+
+@pytest.mark.parametrize('M,N,K,splits', [(4096, 256, 3000, 4), (512, 512, 2008, 3), (128, 256, 64, 1),
+                                          (1024, 256, 22000, 5)])
+def test_dx_splitk_packed_b_matches(M, N, K, splits):
+    """cc_pack_frag_b's fragment image (checked element by element against its layout) and
+    cc_gemm_dx_splitk_pk (Wo fragments straight into registers) == cc_gemm_dx_splitk bit for bit,
+    ragged last K-tile and K % 16 != 0 (zero-padded last k step) included."""
+    rng = np.random.default_rng(M + K + 1)
+    A = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32)).to(torch.bfloat16).cuda()
+    Bm = torch.from_numpy(rng.standard_normal((N, K)).astype(np.float32)).to(torch.bfloat16).cuda()
+    nks = (K + 15) // 16
+    assert L.lib().cc_pack_frag_b_size(N, K) == (N // 32) * nks * 1024
+    Bp = torch.full(((N // 32) * nks * 512,), 3.0, dtype=torch.bfloat16, device='cuda')
+    L.call('cc_pack_frag_b', L.ptr(Bm), N, K, K, L.ptr(Bp), L.stream_ptr())
+    p0 = torch.zeros(splits, M, N, device='cuda')
+    p1 = torch.full((splits, M, N), 7.0, device='cuda')
+    L.call('cc_gemm_dx_splitk', L.ptr(A), K, L.ptr(Bm), K, M, N, K, splits, L.ptr(p0), L.stream_ptr())
+    L.call('cc_gemm_dx_splitk_pk', L.ptr(A), K, L.ptr(Bp), M, N, K, splits, L.ptr(p1), L.stream_ptr())
+    torch.cuda.synchronize()
+    img = Bp.view(N // 32, nks, 2, 32, 8).cpu().float().numpy()   # [band][k step][lane >> 5][lane & 31][8]
+    Bpad = np.zeros((N, nks * 16), np.float32)
+    Bpad[:, :K] = Bm.cpu().float().numpy()
+    want = Bpad.reshape(N // 32, 32, nks, 2, 8).transpose(0, 2, 3, 1, 4)
+    np.testing.assert_array_equal(img, want)
+    np.testing.assert_array_equal(p1.cpu().numpy(), p0.cpu().numpy())

@@ -9,7 +9,9 @@
 
 int main(int argc, char **argv) {
   const int M = 22016, N = 256, K = 22000, splits = argc > 1 ? atoi(argv[1]) : 4;
-  void *A, *B, *P;
+  const bool pk = argc > 2 && atoi(argv[2]) != 0;   // B from its packed fragment image (cc_gemm_dx_splitk_pk)
+  void *A, *B, *P, *Bp;
+  (void)hipMalloc(&Bp, cc_pack_frag_b_size(N, K));
   (void)hipMalloc(&A, (size_t)M * K * 2);
   (void)hipMalloc(&B, (size_t)N * K * 2);
   (void)hipMalloc(&P, (size_t)splits * M * N * 4);
@@ -21,7 +23,9 @@ int main(int argc, char **argv) {
   float best = 1e9f, sum = 0.f;
   for (int rep = 0; rep < 12; ++rep) {
     (void)hipEventRecord(e0);
-    const int rc = cc_gemm_dx_splitk(A, K, B, K, M, N, K, splits, (float *)P, nullptr);
+    if (pk && rep == 0) (void)cc_pack_frag_b(B, N, K, K, Bp, nullptr);
+    const int rc = pk ? cc_gemm_dx_splitk_pk(A, K, Bp, M, N, K, splits, (float *)P, nullptr)
+                      : cc_gemm_dx_splitk(A, K, B, K, M, N, K, splits, (float *)P, nullptr);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms;
@@ -29,7 +33,7 @@ int main(int argc, char **argv) {
     if (rc != 0) printf("rc %d\n", rc);
     if (rep >= 2) { best = ms < best ? ms : best; sum += ms; }
   }
-  printf("DXW_DIAG %d splits %d: dx_wide best %.1f us, mean %.1f us (%s)\n", DXW_DIAG, splits, best * 1e3, sum * 1e2,
+  printf("DXW_DIAG %d splits %d packed %d: dx_wide best %.1f us, mean %.1f us (%s)\n", DXW_DIAG, splits, (int)pk, best * 1e3, sum * 1e2,
          hipGetErrorString(hipGetLastError()));
   return 0;
 }
