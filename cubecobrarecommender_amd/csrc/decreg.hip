@@ -325,6 +325,93 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   }
 }
 
+// The same row stats with two adjacent slices per block and the rows split in two halves (the
+// full-mode shape, d = 256): kl_stats_kernel's blocks each re-read all of the packed D3 (11 MB at
+// |V| = 22,000, ~42 B/clk per CU of fragment loads at its MFMA rate) — the pattern kl_dwo2_kernel
+// removed from the dWo product.  Here each loaded row block feeds 6 column tiles instead of 3 (half
+// the D3 bytes per output), with the row block's fragments in ONE register ring (each k step's
+// fragment reloaded for the wave's next row block right after its MFMAs: registers for the 6
+// accumulators).  Per 96-column slice the MFMA order, the max and the sum are kl_stats_kernel's:
+// the same partials bit for bit.  Grid: ceil(nsl / 2) slice pairs x 2 row halves.
+#ifndef CCREC_KL_STATS2
+#define CCREC_KL_STATS2 1   // build knob (A/B builds): 0 = kl_stats_kernel for every shape
+#endif
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(1, 2))) void kl_stats2_kernel(KlP p) {
+  constexpr int D = 256, NB = kl_nb<D>(), NJ = NB / 32, CHD = D / 8, nkk = D / 16, W8 = NTH / 64;
+  __shared__ __attribute__((aligned(16))) bf16_t Wt[2][NB * D];
+  __shared__ __attribute__((aligned(16))) float bs[2][NB];   // the slices' biases, -inf past V
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5;
+  const int sp = blockIdx.x, rh = blockIdx.y;
+  if (sp == 0 && rh == 0 && threadIdx.x == 0) *p.flag = 0u;  // this step's fix flag starts clear
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int n0 = (2 * sp + q) * NB;
+    if (threadIdx.x < NB) bs[q][threadIdx.x] = n0 + (int)threadIdx.x < p.V ? p.bo[n0 + threadIdx.x] : -INFINITY;
+    load_wo_slice<D>(p.Wo, p.V, min(n0, (p.nsl - 1) * NB), Wt[q]);   // (a pair past nsl: never written)
+  }
+  __syncthreads();
+  const int nrb = p.rows / 32, rb0 = nrb * rh / 2, rb1 = nrb * (rh + 1) / 2;
+  auto src_of = [&](int rb) {
+    return p.D3p + ((int64_t)((p.row0 + 32 * min(rb, nrb - 1)) / 32) * nkk * 64 + lane) * 8;
+  };
+  bf16x8_t af[nkk];
+  {
+    const bf16_t *src = src_of(rb0 + w);
+#pragma unroll
+    for (int kk = 0; kk < nkk; ++kk) af[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * 512);
+  }
+  for (int rb = rb0 + w; rb < rb1; rb += W8) {
+    f32x16_t acc[2][NJ];  // bias-initialised: registers 4g..4g+3 are columns 8g + 4 half .. +3
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 b = *reinterpret_cast<const float4 *>(&bs[q][j * 32 + 8 * g + 4 * half]);
+          acc[q][j][4 * g] = b.x;
+          acc[q][j][4 * g + 1] = b.y;
+          acc[q][j][4 * g + 2] = b.z;
+          acc[q][j][4 * g + 3] = b.w;
+        }
+    const bf16_t *nsrc = src_of(rb + W8);   // (clamped past the end: loaded, never used)
+    int wofs = 0;   // opaque per row block: the Wo-slice fragments are not hoisted out of the loop
+    asm volatile("" : "+v"(wofs));
+#pragma unroll
+    for (int kk = 0; kk < nkk; ++kk) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const bf16x8_t a = frag(Wt[q] + wofs, sw_off(j * 32 + (lane & 31), kk * 16 + 8 * half, CHD));
+          acc[q][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, af[kk], acc[q][j], 0, 0, 0);
+        }
+      af[kk] = *reinterpret_cast<const bf16x8_t *>(nsrc + kk * 512);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) m = fmaxf(m, acc[q][j][r]);
+      m = fmaxf(m, __shfl_xor(m, 32));
+      float e = 0.f;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) e += __builtin_amdgcn_exp2f((acc[q][j][r] - m) * LOG2E);
+      e += __shfl_xor(e, 32);
+      const int sl = 2 * sp + q;
+      if (half == 0 && sl < p.nsl) {
+        const int row = 32 * rb + lane;
+        p.part_m[(int64_t)row * p.nsl + sl] = m;
+        p.part_s[(int64_t)row * p.nsl + sl] = e;
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- merge (one wave per row)
 // The row's slice partials are loaded once (MRG per lane in registers) — one memory round trip.
 constexpr int MRG = 8;  // nsl <= 512 (|V| <= 49,152): checked on the host
@@ -1549,6 +1636,8 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
   // ... and its M~ loaded 16 B per lane through LDS (16-B aligned rows): opt-in (measured slower)
   const bool wload = ((uintptr_t)a->Mt & 15) == 0 && (a->flags & CC_KL_WIDE_TARGETS);
   // dWo's dZ stream by producer waves' LDS-DMA (16-B aligned rows): opt-in (measured no faster)
+  // the stats in slice pairs x row halves (kl_stats2_kernel): many row tiles (full mode), d = 256
+  const bool stats2 = CCREC_KL_STATS2 && a->d == 256 && a->rows > TR;
   const bool dwo_pc = a->V % 8 == 0 && ((uintptr_t)a->dZ & 15) == 0 && (a->flags & CC_KL_DWO_PRODUCER_WAVES);
   // dWo in 192-column slices x two row halves (kl_dwo2_kernel): 16-B aligned rows, the chunk
   // sentinel 0x80000000 past dZ's range, at least one chunk per half
@@ -1557,7 +1646,10 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
                     p.dw_part && !(a->flags & (CC_KL_DWO_NARROW | CC_KL_DWO_PRODUCER_WAVES));
 #define KL_LAUNCH(DD)                                                                                          \
   if (a->d == DD) {                                                                                          \
-    hipLaunchKernelGGL((kl_stats_kernel<DD>), gs, dim3(NTH), 0, s, p);                                      \
+    if (stats2 && DD == 256)                                                                                 \
+      hipLaunchKernelGGL(kl_stats2_kernel, dim3((unsigned)cdiv(p.nsl, 2), 2), dim3(NTH), 0, s, p);          \
+    else                                                                                                     \
+      hipLaunchKernelGGL((kl_stats_kernel<DD>), gs, dim3(NTH), 0, s, p);                                    \
     CC_LAUNCH_CHECK("kl_stats_kernel");                                                                      \
     hipLaunchKernelGGL(kl_merge_kernel, dim3((unsigned)cdiv(a->rows, 4)), dim3(256), 0, s, p);              \
     CC_LAUNCH_CHECK("kl_merge_kernel");                                                                      \

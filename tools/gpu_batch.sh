@@ -1,1 +1,2 @@
-bash tools/gpu_run.sh r05z9 "tests:tests/test_gpu_kernels.py -k dx_splitk" "tests:tests/test_gpu_train.py -k full_mode" "tests:tests/test_gpu_fullsize.py -k full_mode" "bench:--reg 0.1 --reg-mode full --steps 10 --warmup 3" "bench:--reg 0.1 --reg-mode full --steps 10 --warmup 3 --dx-packed-wo 0" "bench:--reg 0.1 --reg-mode full --steps 10 --warmup 3" "bench:--reg 0.1 --reg-mode full --steps 10 --warmup 3 --dx-packed-wo 0"
+for v in 22000 2504 5000; do timeout -k 5 120 tools/micro/gpubin/kl_ab $v 16 && timeout -k 5 120 tools/micro/gpubin/kl_ab_s0 $v 16 || exit 1; done
+bash tools/gpu_run.sh r05za "tests:tests/test_gpu_train.py -k full_mode" && bash tools/ab_lib.sh old --reg 0.1 --reg-mode full --steps 10 --warmup 3

@@ -89,6 +89,17 @@ int main(int argc, char **argv) {
       ++ngb;
       if (first < 0) first = i;
     }
+  // FNV-1a over the default path's outputs: equal across two builds = the same bits
+  uint64_t h = 1469598103934665603ull;
+  auto fnv = [&](const void *p, size_t n) {
+    const unsigned char *c = (const unsigned char *)p;
+    for (size_t i = 0; i < n; ++i) h = (h ^ c[i]) * 1099511628211ull;
+  };
+  fnv(o[0].dz.data(), o[0].dz.size() * 2);
+  fnv(o[0].gw.data(), o[0].gw.size() * 4);
+  fnv(o[0].gb.data(), o[0].gb.size() * 4);
+  fnv(&o[0].loss, 8);
+  printf("default-path outputs hash %016llx\n", (unsigned long long)h);
   printf("V %d rows %d: differing dZ %zu, dWo %zu, dbo %zu", V, rows, ndz, ngw, ngb);
   if (first >= 0) printf(" (first dbo column %d: %.9g vs %.9g, slice %d)", first, o[0].gb[first], o[1].gb[first], first / 96);
   printf("\n");
