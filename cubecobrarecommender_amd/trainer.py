@@ -51,6 +51,7 @@ class TrainConfig:
     dx_splits: int = 0             # decoder dX K-splits (0: measured default, 32 bf16 / 16 fp8)
     dx_splits_reg: int = 0         # ... of the full-mode regulariser branch (0: 4)
     dx_packed_wo: bool = True      # full-mode regulariser dX from Wo's fragment image (cc_gemm_dx_splitk_pk)
+    dp_defer_out: bool = True      # data parallel: the output layers' all-gather at the next step's head
     mx8_bce_q: bool = True         # fp8: the BCE product writes dZ's MX-FP8 images (else quantiser launches)
     mx8_pair_reg_logits: bool = True   # fp8: the regulariser logits as extra blocks of the BCE product's launch
     graph_steps: int = 8           # one process: consecutive steady-state steps per hipGraph replay (step_many)
@@ -531,6 +532,8 @@ class Trainer:
         # output layer's gradient is final (hook_out) and once the branch's dX product no longer
         # reads its bf16 shadow (hook_dx), so that bucket's reduce-scatter starts before dX
         self.hook_out = self.hook_dx = None
+        # ... and (a deferred output-layer all-gather, zero.py) right before the forward's D1 launch
+        self.hook_d1 = None
         # ... and per gradient bucket finalised inside forward_backward_b (the towers, each W1 row
         # chunk): name -> callable, fired once on the launching stream right after the bucket's
         # last kernel
@@ -825,6 +828,7 @@ class Trainer:
                    L.ptr(self.D3qs), None, s)
             L.call('cc_quant_mx8', L.CC_BF16, L.ptr(self.D3), R, d, d, 1, L.ptr(self.D3tq), R,
                    L.ptr(self.D3tqs), None, s)
+        self._fire('hook_d1')   # (zero.py: the output layers' deferred all-gather landed)
         t = self._tick('dec_bce_fwd')
         if self.fused_out:     # logits + BCE + dZ + dWo/dbo in one pass (csrc/decout.hip)
             L.call('cc_dec_bce_dw_ld', L.ptr(self.D3), L.ptr(self.D3t), R,
@@ -1292,10 +1296,20 @@ class Trainer:
             return
         self._dp_call(g, timing)
 
+    def dp_defer_out_ok(self):
+        """zero.py may defer the output layers' all-gather to the next step's head: nothing between
+        this step's Adam and the next D1 launch reads the output layers' shadow (the decoder kernels
+        read Wo straight from it; no Wo^T, MX-FP8 or fragment image is refreshed from it)."""
+        return bool(self.cfg.dp_defer_out and self.fused_out and (not self.use_reg or self.fused_reg)
+                    and self.WoP is None and not self.mx8)
+
     def flush(self, stream=None, defer=False):
         """Run the previous step's deferred counters/transposes (before reading state or the
-        transposed operands from outside the step).  defer (forward_backward only): the counter
-        advance may ride in the forward's first launch."""
+        transposed operands from outside the step) and, data parallel, a deferred output-layer
+        all-gather (a collective: every rank calls flush).  defer (forward_backward only): the
+        counter advance may ride in the forward's first launch."""
+        if getattr(self, 'sharded', None) is not None:
+            self.sharded.flush_out()
         if self.pending_rest:
             self.pending_rest = False
             self.apply_rest(stream, defer=defer)

@@ -64,6 +64,13 @@ class ShardedStep:
         self.comm_events = {}          # (bucket, collective) -> [(e0, e1)] when timing
         self.timing = False
         self.no_comm = False           # capture a timing reference of the step without the exchange
+        # the output layers' all-gather deferred to the head of the next step, beside its F / E1
+        # gather / tower forward, its D1 launch waiting for it (trainer.hook_d1): nothing reads the
+        # output layers' shadow between this step's Adam and the next D1 when the decoder operands
+        # are read straight from the shadow (no Wo^T / MX-FP8 / fragment images refreshed from it)
+        self.defer_out = (self.shadow_gather and self.comm is not None and bool(self.buckets)
+                          and self.buckets[0]['name'] == 'output_layers' and trainer.dp_defer_out_ok())
+        self.out_pending = False       # a deferred output-layer all-gather not yet issued
 
     def bucket(self, name):
         return next(b for b in self.buckets if b['name'] == name)
@@ -128,10 +135,11 @@ class ShardedStep:
             b['gfull'].mul_(1.0 / self.world)
         t()
 
-    def update(self, b, adam_fn, gate=None):
+    def update(self, b, adam_fn, gate=None, gather=True):
         """Reduce-scatter bucket b, Adam on this rank's shard, all-gather the parameters (the
-        bf16 shadow in shadow_gather mode); the biases bucket: all-reduce, Adam on every rank.
-        gate: an event the Adam waits for (the step's last reader of the bucket's old shadow)."""
+        bf16 shadow in shadow_gather mode; gather=False: left to the caller); the biases bucket:
+        all-reduce, Adam on every rank.  gate: an event the Adam waits for (the step's last reader
+        of the bucket's old shadow)."""
         full = self.shadow_gather and b['name'] == 'biases'
         if full:
             self.all_reduce_mean(b, self.tr.grads)
@@ -149,9 +157,23 @@ class ShardedStep:
         if self.timing:
             e1.record()
             self.adam_events.append((e0, e1, b['hi'] - b['lo'] if full else b['chunk']))
-        if full:
+        if full or not gather:
             return
         self.all_gather(b, self.tr.shadow if self.shadow_gather else self.tr.params)
+
+    def flush_out(self):
+        """Issue a deferred output-layer all-gather now (every rank: a collective) and make the
+        current stream wait for it — before the shadow is read outside a step."""
+        if not self.out_pending:
+            return
+        self.out_pending = False
+        main = torch.cuda.current_stream()
+        e = torch.cuda.Event()
+        e.record(main)
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(e)
+            self.all_gather(self.buckets[0], self.tr.shadow)
+        main.wait_stream(self.comm)
 
     def warm(self):
         """Run every collective of the step once on scratch tensors of the buckets' sizes, so the
@@ -173,6 +195,7 @@ class ShardedStep:
     def gather_state(self):
         """Make m and v (and, in shadow_gather mode, the fp32 kernel parameters) complete on every
         rank (checkpointing): all-gather each sharded bucket."""
+        self.flush_out()
         for b in self.buckets:
             if self.shadow_gather and b['name'] == 'biases':
                 continue      # replicated
@@ -207,6 +230,19 @@ class ShardedStep:
             return
         main = torch.cuda.current_stream()
         ev, gate = torch.cuda.Event(), None
+        if self.defer_out:   # the previous step's output-layer all-gather (idempotent at the first)
+            self.out_pending = False
+            e0 = torch.cuda.Event()
+            e0.record(main)
+            ag = torch.cuda.Event()
+            with torch.cuda.stream(self.comm):
+                self.comm.wait_event(e0)
+                self.all_gather(first, self.tr.shadow)
+                ag.record(self.comm)
+            if hooks:      # the forward's D1 launch waits for it (trainer.hook_d1)
+                self.tr.hook_d1 = lambda: main.wait_event(ag)
+            else:
+                main.wait_event(ag)
         early = []   # later buckets started from the trainer's bucket hooks inside phase_b
         if hooks:   # the first bucket's reduce-scatter as soon as its gradient is final (before dX)
             gate = torch.cuda.Event()
@@ -226,12 +262,14 @@ class ShardedStep:
         phase_a()
         if hooks:
             assert self.tr.hook_out is None and self.tr.hook_dx is None, 'forward_backward_a fired no hooks'
+            assert getattr(self.tr, 'hook_d1', None) is None, 'forward_backward_a fired no hook_d1'
         else:
             ev.record(main)
         with torch.cuda.stream(self.comm):
             self.comm.wait_event(ev)
-            self.update(first, adam_fn, gate)
+            self.update(first, adam_fn, gate, gather=not self.defer_out)
             refresh(first['lo'], first['hi'])
+        self.out_pending = self.defer_out
         phase_b()
         if hooks:
             assert not self.tr.bucket_hooks, f'forward_backward_b left bucket hooks {list(self.tr.bucket_hooks)}'

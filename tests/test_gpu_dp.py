@@ -62,6 +62,8 @@ def _worker(rank, port, reg, graphs, q, shape='small', reg_shard=False):
         for _ in range(STEPS):
             tr.step()
         torch.cuda.synchronize()
+        if shape == 'bench':   # the output layers' all-gather runs at the next step's head (zero.py)
+            assert tr.sharded.defer_out
         tr.sharded.gather_state()
         tr.check_status()
         extra = (tr.reg_idx.cpu().numpy(), tr.reg_rows, tr.Breg) if tr.owner else None
@@ -74,11 +76,14 @@ def _worker(rank, port, reg, graphs, q, shape='small', reg_shard=False):
 
 @pytest.mark.parametrize('reg,graphs,shape,reg_shard', [
     (0.0, False, 'small', False), (0.1, True, 'small', False), (0.1, False, 'small', True),
-    (0.0, True, 'bench', False), (0.1, True, 'bench', False), (0.1, True, 'bench', True)])
+    (0.0, True, 'bench', False), (0.1, True, 'bench', False), (0.1, True, 'bench', True),
+    (0.0, False, 'bench', False)])
 def test_sharded_dp_step_matches_single_process(reg, graphs, shape, reg_shard):
     """Two ranks of B == one process of 2B (same cubes, F draws, regulariser draws and averaged
     gradients).  reg_shard: M~ row-sharded, owner computes — every rank draws the
-    2B global reg rows and keeps the ones in its shard, so the step is still the one-process step."""
+    2B global reg rows and keeps the ones in its shard, so the step is still the one-process step.
+    The bench shape defers the output layers' all-gather to the next step's head (zero.py): before
+    the phase graphs (graphs) or at the forward's hook_d1 (eager launches)."""
     from oracle import noise_ref
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
