@@ -1,1 +1,1 @@
-bash tools/gpu_run.sh r05zi "tests:tests/test_gpu_dp.py tests/test_gpu_api.py"
+bash tools/gpu_run.sh r05zj tests py:tools/run_smoke.py fullbench "fullbench:--steps 20 --warmup 5" "bench:--force-dp --steps 50 --warmup 10"
