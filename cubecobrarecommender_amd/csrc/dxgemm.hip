@@ -152,7 +152,8 @@ __global__ __launch_bounds__(XNT) void dx_splitk_kernel(DxP p) {
 // B 256 x 64 (48 KB each).  Splits are dealt split-major over the XCDs as above, so a split's Wo
 // panel (256 x K/splits bf16) stays in one XCD's L2.
 constexpr int WBM = 128, WBN = 256, WST = 3, WNT = 512;
-// dev diagnostics (tools/micro/dx_diag.hip; 0 in the library): 1 no Wo copies, 2 no dZ copies, 4 no MFMA
+// dev diagnostics (tools/micro/dx_diag.hip; 0 in the library): 1 no Wo copies / fragment loads, 2 no dZ
+// copies, 4 no MFMA (dx_wide_kernel and dx_wide3_kernel)
 #ifndef DXW_DIAG
 #define DXW_DIAG 0
 #endif
@@ -260,7 +261,14 @@ __global__ __launch_bounds__(WNT) void dx_wide_kernel(DxP p) {
 // then DMA(t + 2), so the counted wait for B(t) does not wait on the newest copies; copies and
 // loads past the end use the range sentinel (zeros, no traffic) so every iteration issues the same
 // count.  The MFMA chain per output is the other paths' (bit-identical partials).
-constexpr int W3ST = 3, W3NT = 512;
+#ifndef DX3_LEAD
+#define DX3_LEAD 2   // build knob: dZ K-tiles copied ahead of the one multiplied (stages = lead + 1)
+#endif
+constexpr int W3L = DX3_LEAD, W3ST = W3L + 1, W3NT = 512;
+static_assert(W3L >= 2 && W3L <= 5, "dx_wide3: the startup waits below are written for leads 2..5");
+
+template <int N>
+__device__ __forceinline__ void w2_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 constexpr int W3TILE = WBM * XBK * 2;   // 16 KB: the dZ tile only
 
 __global__ __launch_bounds__(W3NT) void dx_wide3_kernel(DxP p) {
@@ -276,6 +284,7 @@ __global__ __launch_bounds__(W3NT) void dx_wide3_kernel(DxP p) {
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void *)p.B, (short)0, p.b_bytes, 0x00020000);
   const int rl = lane >> 3, slot = lane & 7;
   auto dma = [&](int t) {   // dZ K-tile t -> stage t % W3ST: 2 instructions of 8 rows x 128 B per wave
+    if constexpr (DXW_DIAG & 2) return;
     char *sa = w3mem + (t % W3ST) * W3TILE;
     const int k0 = kbeg + t * XBK;
 #pragma unroll
@@ -290,6 +299,7 @@ __global__ __launch_bounds__(W3NT) void dx_wide3_kernel(DxP p) {
   const int nks = (p.K + 15) / 16;
   const uint32_t bbase = (uint32_t)((bn / 32 + w) * nks) * 1024u + 16u * (uint32_t)lane;
   auto bload = [&](bf16x8_t (&dst)[XBK / 16], int t) {   // Wo fragments of K-tile t
+    if constexpr (DXW_DIAG & 1) return;
     const int k0 = kbeg + t * XBK;
 #pragma unroll
     for (int ks = 0; ks < XBK / 16; ++ks) {
@@ -304,29 +314,42 @@ __global__ __launch_bounds__(W3NT) void dx_wide3_kernel(DxP p) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
   bf16x8_t bf[2][XBK / 16];
-  // prologue in the steady order: DMA(0), B(0), DMA(1) (sched barriers: the waits count on the order)
-  dma(0);
+  // prologue: DMA(0 .. L - 1), then B(0) (sched barriers: the waits count on the issue order).
+  // Per K-tile t: wait for DMA(t), barrier, B(t + 1) (4 loads), DMA(t + L) (2).  The accesses
+  // younger than DMA(t) at that wait: 6 (L - 1) in the steady state; at t < L - 2 (the prologue's
+  // later copies, B(0) and t tiles) 2 L + 2 + 4 t, fewer — those waits use their own counts.
+#pragma unroll
+  for (int j = 0; j < W3L; ++j) dma(j);
   __builtin_amdgcn_sched_barrier(0);
   bload(bf[0], 0);
   __builtin_amdgcn_sched_barrier(0);
-  dma(1);
-  __builtin_amdgcn_sched_barrier(0);
   const int ar = lane & 31;
   auto body = [&](bf16x8_t (&cur)[XBK / 16], bf16x8_t (&nxt)[XBK / 16], int t) {
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // own DMA(t) landed (younger: B(t), DMA(t + 1))
-    __builtin_amdgcn_s_barrier();   // every wave's DMA(t) landed; stage (t - 1) % 3 read by all
+    if (W3L >= 3 && t == 0)
+      w2_wait<(2 * W3L + 2) % 64>();
+    else if (W3L >= 4 && t == 1)
+      w2_wait<(2 * W3L + 6) % 64>();
+    else if (W3L >= 5 && t == 2)
+      w2_wait<(2 * W3L + 10) % 64>();
+    else
+      w2_wait<6 * (W3L - 1)>();   // own DMA(t) landed
+    __builtin_amdgcn_s_barrier();   // every wave's DMA(t) landed; stage (t - 1) % W3ST read by all
     asm volatile("" ::: "memory");
     bload(nxt, t + 1);
     __builtin_amdgcn_sched_barrier(0);
-    dma(t + 2);
+    dma(t + W3L);
     __builtin_amdgcn_sched_barrier(0);
     const char *sa = w3mem + (t % W3ST) * W3TILE;
 #pragma unroll
     for (int ks = 0; ks < XBK / 16; ++ks) {
       const int c = 2 * ks + half;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(sa, ar + 32 * i, c), cur[ks], acc[i], 0, 0, 0);
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (DXW_DIAG & 4)
+          acc[i][0] += __builtin_bit_cast(float, __builtin_shufflevector(frag(sa, ar + 32 * i, c), cur[ks], 0, 9));
+        else
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(sa, ar + 32 * i, c), cur[ks], acc[i], 0, 0, 0);
+      }
     }
   };
   int t = 0;

@@ -1,1 +1,1 @@
-bash tools/gpu_run.sh r05zj tests py:tools/run_smoke.py fullbench "fullbench:--steps 20 --warmup 5" "bench:--force-dp --steps 50 --warmup 10"
+bash tools/gpu_run.sh r05zk "tests:tests/test_gpu_kernels.py -k dx_splitk" "tests:tests/test_gpu_fullsize.py -k full_mode" "tests:tests/test_gpu_train.py -k full_mode"
