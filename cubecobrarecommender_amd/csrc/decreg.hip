@@ -57,6 +57,9 @@ constexpr float PMIN = 1e-7f;
 // (tools/micro/kl_probe_full.hip; either alone gains ~1 %).  One tile (the sampled regulariser):
 // default — the non-temporal pair slowed its epilogues (p1 4.9 -> 6.8 us).
 constexpr int KL_CPOL_NT = 2;  // the SLC/NT bit of the buffer instructions' cache-policy operand
+#ifndef KL_SEP_CPOL
+#define KL_SEP_CPOL KL_CPOL_NT   // build knob: the main pass's policy with dWo in its own kernel
+#endif
 constexpr float LN_PMIN = -16.11809565095832f;  // ln(1e-7)
 
 
@@ -1655,13 +1658,13 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
     CC_LAUNCH_CHECK("kl_merge_kernel");                                                                      \
     if (dw_sep) {                                                                                            \
       if (ms)                                                                                                \
-        hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, false, (DD <= 256)>), gm, dim3(NTH), 0, s, p);    \
+        hipLaunchKernelGGL((kl_main_kernel<DD, KL_SEP_CPOL, false, (DD <= 256)>), gm, dim3(NTH), 0, s, p);    \
       else if (wstore && wload)                                                                              \
-        hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, false, false, (DD <= 256), (DD <= 256)>), gm, dim3(NTH), 0, s, p); \
+        hipLaunchKernelGGL((kl_main_kernel<DD, KL_SEP_CPOL, false, false, (DD <= 256), (DD <= 256)>), gm, dim3(NTH), 0, s, p); \
       else if (wstore)                                                                                       \
-        hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, false, false, (DD <= 256)>), gm, dim3(NTH), 0, s, p); \
+        hipLaunchKernelGGL((kl_main_kernel<DD, KL_SEP_CPOL, false, false, (DD <= 256)>), gm, dim3(NTH), 0, s, p); \
       else                                                                                                   \
-        hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, false>), gm, dim3(NTH), 0, s, p);                 \
+        hipLaunchKernelGGL((kl_main_kernel<DD, KL_SEP_CPOL, false>), gm, dim3(NTH), 0, s, p);                 \
       CC_LAUNCH_CHECK("kl_main_kernel");                                                                     \
       hipLaunchKernelGGL((kl_fix_kernel<DD, false>), dim3(FIXG), dim3(NTH), 0, s, p);                       \
       CC_LAUNCH_CHECK("kl_fix_kernel");                                                                      \

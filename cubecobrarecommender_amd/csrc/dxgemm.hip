@@ -264,6 +264,9 @@ __global__ __launch_bounds__(WNT) void dx_wide_kernel(DxP p) {
 #ifndef DX3_LEAD
 #define DX3_LEAD 2   // build knob: dZ K-tiles copied ahead of the one multiplied (stages = lead + 1)
 #endif
+#ifndef DX3_CPOL
+#define DX3_CPOL 0   // build knob: the dZ copies' cache policy (default; nt measured 343 vs 304 us)
+#endif
 constexpr int W3L = DX3_LEAD, W3ST = W3L + 1, W3NT = 512;
 static_assert(W3L >= 2 && W3L <= 5, "dx_wide3: the startup waits below are written for leads 2..5");
 
@@ -292,7 +295,7 @@ __global__ __launch_bounds__(W3NT) void dx_wide3_kernel(DxP p) {
       const int i = w * 2 + u, row = 8 * i + rl;
       const int k = k0 + 8 * (slot ^ ((row >> 1) & 7));
       const uint32_t oa = k < kend ? (uint32_t)(((bm + row) * p.lda + k) * 2) : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void *)(sa + i * 1024), 16, oa, 0, 0, 2);   // dZ: nt
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void *)(sa + i * 1024), 16, oa, 0, 0, DX3_CPOL);   // dZ: default policy (knob)
     }
   };
   // fragment (band, k step) of the packed image: 1 KB at (band * nks + k step) KB, lane L's 16 B at 16 L

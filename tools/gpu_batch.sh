@@ -1,1 +1,1 @@
-bash tools/gpu_run.sh r05zk "tests:tests/test_gpu_kernels.py -k dx_splitk" "tests:tests/test_gpu_fullsize.py -k full_mode" "tests:tests/test_gpu_train.py -k full_mode"
+bash tools/ab_lib.sh c0 --reg 0.1 --reg-mode full --steps 10 --warmup 3 && bash tools/ab_lib.sh c1 --reg 0.1 --reg-mode full --steps 10 --warmup 3
