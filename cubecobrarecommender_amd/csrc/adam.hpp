@@ -3,7 +3,23 @@
 //   alpha = lr sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1); v += (g^2-v)(1-b2);
 //   p -= m*alpha/(sqrt(v)+eps);  t = state[0] + 1.
 #pragma once
+// build knob (A/B builds): the dense Adam's p / m / v / g streams non-temporal (1) or default (0);
+// measured (r05zm): default policy 149.7 -> 164.8-167.2 us/step (BCE), 961 -> 1,020 (config 5)
+#ifndef ADAM_NT
+#define ADAM_NT 1
+#endif
 #include "common.hpp"
+
+template <typename T>
+__device__ __forceinline__ T ADAM_LD(const T *p) {
+  if constexpr (ADAM_NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <typename T>
+__device__ __forceinline__ void ADAM_ST(T v, T *p) {
+  if constexpr (ADAM_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 
 namespace cc_adam {
 
@@ -73,10 +89,10 @@ __device__ __forceinline__ void range(const Args &a, int64_t step, int bid, int 
     // the packed images, which the next step's kernels read, keep the default policy).  Measured
     // in the step: 180-184 -> 178 us (Adam -1.5 us; the next W1-gradient kernel -2.5 us: Adam no
     // longer evicts the lines it reads)
-    f32x4_t pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.p) + i);
-    f32x4_t mv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.m) + i);
-    f32x4_t vv4 = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.v) + i);
-    const f32x4_t gv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.g) + i);
+    f32x4_t pv = ADAM_LD(reinterpret_cast<const f32x4_t *>(a.p) + i);
+    f32x4_t mv = ADAM_LD(reinterpret_cast<const f32x4_t *>(a.m) + i);
+    f32x4_t vv4 = ADAM_LD(reinterpret_cast<const f32x4_t *>(a.v) + i);
+    const f32x4_t gv = ADAM_LD(reinterpret_cast<const f32x4_t *>(a.g) + i);
     float4 pp = make_float4(pv[0], pv[1], pv[2], pv[3]), mm = make_float4(mv[0], mv[1], mv[2], mv[3]);
     float4 vv = make_float4(vv4[0], vv4[1], vv4[2], vv4[3]);
     const float4 gg = make_float4(gv[0], gv[1], gv[2], gv[3]);
@@ -84,9 +100,9 @@ __device__ __forceinline__ void range(const Args &a, int64_t step, int bid, int 
     const float *ge = &gg.x;
 #pragma unroll
     for (int e = 0; e < 4; ++e) elem(pe[e], me[e], ve[e], ge[e], alpha, omb1, omb2, a.eps);
-    __builtin_nontemporal_store(f32x4_t{pp.x, pp.y, pp.z, pp.w}, reinterpret_cast<f32x4_t *>(a.p) + i);
-    __builtin_nontemporal_store(f32x4_t{mm.x, mm.y, mm.z, mm.w}, reinterpret_cast<f32x4_t *>(a.m) + i);
-    __builtin_nontemporal_store(f32x4_t{vv.x, vv.y, vv.z, vv.w}, reinterpret_cast<f32x4_t *>(a.v) + i);
+    ADAM_ST(f32x4_t{pp.x, pp.y, pp.z, pp.w}, reinterpret_cast<f32x4_t *>(a.p) + i);
+    ADAM_ST(f32x4_t{mm.x, mm.y, mm.z, mm.w}, reinterpret_cast<f32x4_t *>(a.m) + i);
+    ADAM_ST(f32x4_t{vv.x, vv.y, vv.z, vv.w}, reinterpret_cast<f32x4_t *>(a.v) + i);
     if (a.shadow) {
       ushort4 s;
       s.x = f2bf(pp.x);
@@ -128,10 +144,10 @@ __device__ __forceinline__ void range_u(const Args &a, int64_t step, int bid, in
     for (int u = 0; u < U; ++u) {
       const int64_t i = i0 + u * stride;
       if (i < n4) {
-        pv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.p) + i);
-        mv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.m) + i);
-        vv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.v) + i);
-        gv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(a.g) + i);
+        pv[u] = ADAM_LD(reinterpret_cast<const f32x4_t *>(a.p) + i);
+        mv[u] = ADAM_LD(reinterpret_cast<const f32x4_t *>(a.m) + i);
+        vv[u] = ADAM_LD(reinterpret_cast<const f32x4_t *>(a.v) + i);
+        gv[u] = ADAM_LD(reinterpret_cast<const f32x4_t *>(a.g) + i);
       }
     }
 #pragma unroll
@@ -143,9 +159,9 @@ __device__ __forceinline__ void range_u(const Args &a, int64_t step, int bid, in
       float ve[4] = {vv[u][0], vv[u][1], vv[u][2], vv[u][3]};
 #pragma unroll
       for (int e = 0; e < 4; ++e) elem(pe[e], me[e], ve[e], gv[u][e], alpha, omb1, omb2, a.eps);
-      __builtin_nontemporal_store(f32x4_t{pe[0], pe[1], pe[2], pe[3]}, reinterpret_cast<f32x4_t *>(a.p) + i);
-      __builtin_nontemporal_store(f32x4_t{me[0], me[1], me[2], me[3]}, reinterpret_cast<f32x4_t *>(a.m) + i);
-      __builtin_nontemporal_store(f32x4_t{ve[0], ve[1], ve[2], ve[3]}, reinterpret_cast<f32x4_t *>(a.v) + i);
+      ADAM_ST(f32x4_t{pe[0], pe[1], pe[2], pe[3]}, reinterpret_cast<f32x4_t *>(a.p) + i);
+      ADAM_ST(f32x4_t{me[0], me[1], me[2], me[3]}, reinterpret_cast<f32x4_t *>(a.m) + i);
+      ADAM_ST(f32x4_t{ve[0], ve[1], ve[2], ve[3]}, reinterpret_cast<f32x4_t *>(a.v) + i);
       if (a.shadow) {
         ushort4 s;
         s.x = f2bf(pe[0]);
