@@ -57,6 +57,10 @@ constexpr float PMIN = 1e-7f;
 // (tools/micro/kl_probe_full.hip; either alone gains ~1 %).  One tile (the sampled regulariser):
 // default — the non-temporal pair slowed its epilogues (p1 4.9 -> 6.8 us).
 constexpr int KL_CPOL_NT = 2;  // the SLC/NT bit of the buffer instructions' cache-policy operand
+#ifndef KL_ZST_CPOL
+#define KL_ZST_CPOL -1   // build knob: the 16-B dZ row stores' policy (-1: the pass's CPOL; 0 measured
+                         // 2,378 vs 2,199-2,206 us/step, r05zo: the non-temporal stores carry the gain)
+#endif
 #ifndef KL_SEP_CPOL
 #define KL_SEP_CPOL KL_CPOL_NT   // build knob: the main pass's policy with dWo in its own kernel
 #endif
@@ -873,7 +877,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
           const v4u x = *reinterpret_cast<const v4u *>(zimg + row * WS_PITCH + ch * 4);
           const uint32_t off = n0 + 8 * ch < V ? 2u * ((uint32_t)(t0 + rb + row) * (uint32_t)V + (uint32_t)(n0 + 8 * ch))
                                                : 0x80000000u;
-          __builtin_amdgcn_raw_buffer_store_b128(x, dz_rs, off, 0, CPOL);
+          __builtin_amdgcn_raw_buffer_store_b128(x, dz_rs, off, 0, KL_ZST_CPOL < 0 ? CPOL : KL_ZST_CPOL);
         }
       }
 
