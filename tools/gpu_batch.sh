@@ -1,1 +1,1 @@
-bash tools/ab_lib.sh z0 --reg 0.1 --reg-mode full --steps 10 --warmup 3
+bash tools/ab_lib.sh g2 --steps 100 --warmup 20 && bash tools/ab_lib.sh e1 --steps 100 --warmup 20
