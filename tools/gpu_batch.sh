@@ -1,1 +1,1 @@
-bash tools/ab_lib.sh g2 --steps 100 --warmup 20 && bash tools/ab_lib.sh e1 --steps 100 --warmup 20
+bash tools/gpu_run.sh r05zq tests py:tools/run_smoke.py "fullbench:--steps 20 --warmup 5"
