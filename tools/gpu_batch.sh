@@ -1,1 +1,1 @@
-bash tools/gpu_run.sh r05zq tests py:tools/run_smoke.py "fullbench:--steps 20 --warmup 5"
+bash tools/gpu_run.sh r05zr "pmc:FETCH_SIZE:--reg 0.1 --reg-mode full" "pmc:WRITE_SIZE:--reg 0.1 --reg-mode full"
