@@ -19,6 +19,7 @@ import torch
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA (spec, no sparsity)
 MX8_PEAK_TFLOPS = 5000.0    # dense (MX-)FP8 MFMA (spec, no sparsity)
+F32_PEAK_TFLOPS = 157.3     # f32 MFMA (exact f32 in / acc; no xf32 on gfx950): 1/16 of bf16
 
 
 def parse():
@@ -59,6 +60,10 @@ def parse():
     ap.add_argument('--force-dp', action='store_true',
                     help='one GPU driving the data-parallel step through a 1-rank RCCL process group '
                          '(the per-rank kernel and exchange sequence the N-GPU run executes)')
+    ap.add_argument('--dp-graph', type=int, default=1, choices=(0, 1),
+                    help='data parallel over RCCL: 1 = the whole step (collectives included) as one captured '
+                         'hipGraph; 0 = graph replays of the step\'s parts with eager RCCL collectives between '
+                         'them (the fallback if multi-rank capture misbehaves; same arithmetic, bit-identical)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-steps', type=int, default=16)
     ap.add_argument('--no-recommend', action='store_true')
@@ -121,7 +126,12 @@ def barrier(world):
 
 
 PEAKS = {'hbm': (HBM_PEAK_GBS, 'GB/s'), 'mfma': (BF16_PEAK_TFLOPS, 'TFLOP/s'),
-         'mfma_mx8': (MX8_PEAK_TFLOPS, 'TFLOP/s')}
+         'mfma_mx8': (MX8_PEAK_TFLOPS, 'TFLOP/s'), 'mfma_f32': (F32_PEAK_TFLOPS, 'TFLOP/s')}
+
+
+def mfma_kind(tr):
+    """The MFMA peak a product of this trainer is priced against: its operand dtype."""
+    return 'mfma_f32' if tr.cfg.dtype == 'fp32' else 'mfma'
 
 
 def roofline_for(name, ms, tr):
@@ -130,7 +140,7 @@ def roofline_for(name, ms, tr):
     cfg = tr.cfg
     V, d, B = cfg.V, cfg.d, cfg.batch_size
     fl = byt = None
-    kind = 'mfma'
+    kind = mfma_kind(tr)
     if name == 'cc_adam_dense':
         n = tr.layout.total if tr.use_reg else tr.layout.main_total
         if getattr(tr, 'fuse_w1', False):     # W1's Adam runs in its gradient kernel
@@ -292,9 +302,13 @@ def dp_profile(tr, step, samples=8, replays=40):
             times[key] = 1e6 * float(dt.item())
         rep.update(times)
         rep['exposed_exchange_us'] = 0.5 * (times['step_us'] + times['step_us_again']) - times['step_without_exchange_us']
-        rep['graph'] = 'whole DP step as one hipGraph (RCCL collectives captured on the comm stream)'
+        rep['graph'] = 'whole'
+        rep['graph_path'] = 'whole DP step as one hipGraph (RCCL collectives captured on the comm stream)'
     else:
-        rep['graph'] = 'graph parts with eager collectives between them (gloo or dp_graph off)'
+        rep['graph'] = 'parts'
+        rep['graph_path'] = ('graph replays of forward_backward_a / forward_backward_b / counters with eager '
+                             'collectives and sharded Adam between them (' +
+                             ('--dp-graph 0' if not tr.cfg.dp_graph else 'gloo backend') + ')')
     rep['backend'] = dist.get_backend()
     rep['world'] = dist.get_world_size()
     return rep
@@ -321,8 +335,9 @@ def step_roofline(tr, ms_per_step, kt):
     if tr.full_reg:   # the |V| x |V| regulariser product dominates: MFMA-bound
         T = 512 * d + 81920
         fl = 6.0 * (d * V + T) * (B + tr.Breg) + 4.0 * n * d * B   # SURVEY 8(d) FLOP/row
+        pk = PEAKS[mfma_kind(tr)][0]
         out.update({'bound': 'mfma', 'flops_per_step': fl, 'achieved_tflops': fl / (ms_per_step * 1e-3) / 1e12,
-                    'peak_tflops': BF16_PEAK_TFLOPS, 'frac_mfma': fl / (ms_per_step * 1e-3) / 1e12 / BF16_PEAK_TFLOPS})
+                    'peak_tflops': pk, 'frac_mfma': fl / (ms_per_step * 1e-3) / 1e12 / pk})
     if kt and 'dec_bce_fwd' in kt and getattr(tr, 'fused_out', False):
         fl = 2 * 2.0 * B * d * V            # logits + dWo (dX runs in its own GEMM)
         us = kt['dec_bce_fwd']
@@ -330,10 +345,17 @@ def step_roofline(tr, ms_per_step, kt):
                                'flops_per_launch': fl, 'avg_us': us, 'achieved': fl / (us * 1e-6) / 1e12,
                                'peak': BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                                'frac': fl / (us * 1e-6) / 1e12 / BF16_PEAK_TFLOPS}
+    elif kt and 'dec_bce_fwd' in kt:   # (the unfused logits product: fp32 / MX-FP8 / other shapes)
+        fl = 2.0 * B * d * V
+        us = kt['dec_bce_fwd']
+        peak = PEAKS['mfma_mx8' if tr.mx8 else mfma_kind(tr)][0]
+        out['decoder_mfma'] = {'kernel': 'D1 logits product + BCE epilogue', 'flops_per_launch': fl, 'avg_us': us,
+                               'achieved': fl / (us * 1e-6) / 1e12, 'peak': peak, 'unit': 'TFLOP/s',
+                               'frac': fl / (us * 1e-6) / 1e12 / peak}
     if kt and 'dec_dX' in kt:
         out['decoder_dx_mfma'] = {'flops_per_launch': 2.0 * B * d * V, 'avg_us': kt['dec_dX'],
                                   'achieved': 2.0 * B * d * V / (kt['dec_dX'] * 1e-6) / 1e12,
-                                  'peak': BF16_PEAK_TFLOPS, 'unit': 'TFLOP/s'}
+                                  'peak': PEAKS['mfma_mx8' if tr.mx8 else mfma_kind(tr)][0], 'unit': 'TFLOP/s'}
     if kt and 'cc_embed_gather_fwd' in kt:
         gb = tr.R * n * d * e
         out['gather'] = {'bytes_per_launch': gb, 'avg_us': kt['cc_embed_gather_fwd'],
@@ -458,7 +480,7 @@ def main():
                                            if args.steps % g == 0 and (g <= args.warmup or g == 1))
     cfg = TrainConfig(V=V, d=d, batch_size=B, reg=args.reg, dtype=args.dtype, seed=1234,
                       rank=rank, world=world, reg_shard=reg_shard, reg_mode=args.reg_mode,
-                      force_dp=args.force_dp,
+                      force_dp=args.force_dp, dp_graph=bool(args.dp_graph),
                       dz_pad=bool(args.dz_pad), graph_steps=graph_steps, wo_tower_frac=args.wo_tower_frac,
                       fuse_w1_adam=True,   # one process: W1's Adam in its gradient kernel, and (BCE
                       wo_adam_in_tower=True,   # only) Wo's in the tower backward launch, with the next

@@ -79,9 +79,12 @@ class Layout:
             o += (int(np.prod(shape)) + 63) // 64 * 64
         put(0, '/kernel', shapes[0])
         w1 = self.V * self.d
-        # W1 row chunks: boundaries at multiples of 64 rows (every chunk a multiple of align
-        # elements for align <= 64 * d), the last one padded with the block
-        rows = [min(self.V, (self.V * c // nchunks + 63) // 64 * 64) for c in range(nchunks + 1)]
+        # W1 row chunks: boundaries at multiples of q rows — q a multiple of 64 (the gradient
+        # kernel's row tiles) with q * d a multiple of align, so every chunk is whole bucket shards
+        # for any world (align = 64 * world need not divide 64 * d when world is not a power of
+        # two); the last chunk padded with the block, chunks that round away dropped
+        q = int(np.lcm(64, a // int(np.gcd(a, self.d))))
+        rows = [min(self.V, (self.V * c // nchunks + q - 1) // q * q) for c in range(nchunks + 1)]
         rows[0], rows[-1] = 0, self.V
         o = _round_up(o, a)
         self.w1_chunks = [(r0, r1) for r0, r1 in zip(rows[:-1], rows[1:]) if r1 > r0]

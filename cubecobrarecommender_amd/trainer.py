@@ -511,6 +511,7 @@ class Trainer:
                            and self.dtype == L.CC_BF16 and cfg.d <= 256 and not self.full_reg)
         self._adv_deferred = False   # the previous step's counter advance rides in the E1 gather
         self.noise_ready = False
+        self.host_batch = False      # load_batch(): the next step runs on a host-given batch
         self.perms = None
         self.batches_per_epoch = max(1, data.C // (B * cfg.world))   # generator.py:36 (__len__)
         self.graphs = None
@@ -712,6 +713,71 @@ class Trainer:
         self.state[1:3].zero_()
         self.noise_ready = False   # a prefetched batch was drawn from the old order
 
+    def load_batch(self, xs, ys, reg_idx=None):
+        """Host-given batch in place of F for the next forward_backward (one process): the rows of
+        a Keras batch ``[x_cubes, x_reg], [y_cubes, y_reg]`` as generator.py:38-61,74-103 returns
+        them — xs / ys the B noised input / target cubes as card-index lists (or 0/1 rows), reg_idx
+        the B regulariser cards (x_reg = their identity rows, y_reg = their M~ rows).  Written into
+        the device batch buffers F would fill (x CSR, target bitmask, reg indices, the W1 gradient's
+        bit matrix or F's x-row bitmasks), then the step skips F.  Lets the GPU step run on batches
+        the reference's own DataGenerator produced (tests/test_gpu_parity_inputs.py)."""
+        cfg, V, B = self.cfg, self.cfg.V, self.cfg.batch_size
+        if self.dp:
+            raise ValueError('load_batch: one process only (each rank draws its own slots)')
+        if len(xs) != B or len(ys) != B:
+            raise ValueError(f'load_batch: {len(xs)} x rows / {len(ys)} y rows, batch_size is {B}')
+
+        def ids(row):
+            a = np.asarray(row)
+            if a.ndim == 1 and a.shape[0] == V and V > 2 and a.size and a.min() >= 0 and a.max() <= 1:
+                a = np.nonzero(a)[0]            # a dense 0/1 row (an index list of length V holds 2..V-1)
+            a = np.unique(a.astype(np.int64))
+            if a.size and (a[0] < 0 or a[-1] >= V):
+                raise ValueError('load_batch: card index out of range')
+            return a
+        rows = [ids(r) for r in xs]
+        if self.use_reg and not self.full_reg:
+            if reg_idx is None or len(reg_idx) != B:
+                raise ValueError('load_batch: reg > 0 needs the B regulariser cards')
+            reg = np.asarray(reg_idx, np.int64)
+            if reg.min() < 0 or reg.max() >= V:
+                raise ValueError('load_batch: regulariser card out of range')
+            rows += [np.array([j]) for j in reg]
+        nrow = len(rows)                         # full mode: its identity rows stay as they are
+        if max(len(r) for r in rows) > self.x_cap:
+            raise ValueError(f'load_batch: a row holds more than x_cap = {self.x_cap} cards')
+        VW = (V + 31) // 32
+        cnt = np.zeros(nrow, np.int32)
+        idx = np.zeros((nrow, self.x_cap), np.int32)
+        xb = np.zeros((nrow, VW * 32), np.uint8)
+        for r, a in enumerate(rows):
+            cnt[r] = len(a)
+            idx[r, :len(a)] = a
+            xb[r, a] = 1
+        yb = np.zeros((B, VW * 32), np.uint8)
+        for b, row in enumerate(ys):
+            yb[b, ids(row)] = 1
+
+        def words(bits):   # bit k of word w = column 32 w + k (little-endian bit order)
+            return np.packbits(bits, axis=-1, bitorder='little').view(np.int32)
+        dev = self.dev
+        self.x_cnt[:nrow].copy_(torch.from_numpy(cnt).to(dev))
+        self.x_idx[:nrow].copy_(torch.from_numpy(idx).to(dev))
+        self.y_bits.copy_(torch.from_numpy(words(yb)).to(dev))
+        if self.use_reg and not self.full_reg:
+            self.reg_idx[:B].copy_(torch.from_numpy(reg.astype(np.int32)).to(dev))
+        if self.x_bits is not None:   # F's x-row bitmasks: the gather / tower launch transposes them
+            self.x_bits[:nrow].copy_(torch.from_numpy(words(xb)).to(dev))
+        else:                          # the W1 gradient's bit matrix [V][rows/32] directly
+            XR = self.xt_rows
+            xt = np.zeros((V, (XR + 31) // 32 * 32), np.uint8)
+            for r, a in enumerate(rows[:XR]):   # (full mode: the cubes only, XR = B)
+                xt[a, r] = 1
+            self.xt_bits.copy_(torch.from_numpy(words(xt)).to(dev))
+        self.flush()                   # (the previous step's deferred counters / transposes)
+        self.noise_ready = True        # forward_backward consumes these buffers, no F
+        self.host_batch = True         # step(): eager forward_backward (the graphs hold F)
+
     def _noise_args(self):
         cfg, V, B = self.cfg, self.cfg.V, self.cfg.batch_size
         return L.NoiseArgs(V=V, B=B, x_cap=self.x_cap, with_reg=int(self.use_reg and not (self.owner or self.full_reg)),
@@ -787,8 +853,9 @@ class Trainer:
         s = self._s
         # ---- F: noise + reg rows (generator.py:38-103); xt_bits arrives zeroed (the previous
         # step's cc_embed_scatter_bwd consumes it)
-        if self.noise_ready:       # drawn by the previous step's Adam launch (cc_adam_noise)
-            self.noise_ready = False
+        if self.noise_ready:       # drawn by the previous step's Adam launch (cc_adam_noise) or
+            self.noise_ready = False   # written by load_batch()
+            self.host_batch = False
         else:
             na = self._noise_args()
             t = self._tick('cc_noise_fwd')
@@ -978,9 +1045,9 @@ class Trainer:
             self._dense_bwd(self.D2, self.gD3, rows, 256, d, pre + '/decoded_3', gIn=self.gD2, mask=self.D2)
             self._dense_bwd(self.D1, self.gD2, rows, 128, 256, pre + '/decoded_2', gIn=self.gD1, mask=self.D1)
             self._dense_bwd(self.Zl, self.gD1, rows, 64, 128, pre + '/decoded_1', gIn=self.gZl, mask=self.Zl)
+        self._join()               # (the side stream's output-layer work before the bucket's exchange)
         self._fire('hook_out')
         self._fire('hook_dx')
-        self._join()
 
     def _fire(self, name):
         f = getattr(self, name)
@@ -1158,10 +1225,10 @@ class Trainer:
                    self.reg_rows[1] - self.reg_rows[0], d, self.reg_rows[0],
                    self.gp('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias'), L.ptr(self.id_ws), s)
         t()
+        if self.fused_tower:       # the towers' dW (side stream) ride in the last W1 chunk's bucket
+            self._join()
         for i in range(len(chunks)):   # (the W1 chunks not fired above: the last, or all of them)
             self._fire_bucket(f'w1_{i}')
-        if self.fused_tower:
-            self._join()
 
     def _eg_tk(self):
         """W1-gradient tickets (its last block per row chunk clears the chunk's xt words), or None
@@ -1293,6 +1360,9 @@ class Trainer:
         gd = self.g_dp_nocomm if no_comm else self.g_dp
         if gd is not None and not timing and (self.noise_ready or not self.prefetch_dp):
             gd.replay()
+            # the replayed step deferred its output-layer all-gather like an eager one: flush() and
+            # gather_state() must issue it before anything reads the shadow outside a step
+            self.sharded.out_pending = self.sharded.defer_out
             return
         self._dp_call(g, timing)
 
@@ -1345,12 +1415,17 @@ class Trainer:
         self.pending_rest = True
 
     def _steady(self):
-        return (self.graphs is not None and self.graphs[4] is not None and self.pending_rest
+        return (not self.host_batch and self.graphs is not None and self.graphs[4] is not None and self.pending_rest
                 and (self.noise_ready or not self.prefetch))
 
     def step(self, stream=None):
         if self.dp:
             self.step_dp()
+            return
+        if self.host_batch:            # a load_batch() batch: eager forward/backward, no F
+            self.host_batch = False
+            self.forward_backward(stream)
+            self.run_adam(stream)
             return
         if self._steady():
             self.graphs[4].replay()    # steady state: rest(k-1) + fwd/bwd(k) + Adam(k) in one graph
@@ -1479,6 +1554,11 @@ class Trainer:
             try:
                 with torch.cuda.graph(g):
                     self._dp_call(None, False)
+            except Exception as e:   # never a silent fallback: the caller picks the parts path itself
+                raise RuntimeError(
+                    f'capturing the whole data-parallel step (RCCL collectives inside) failed on rank '
+                    f'{self.cfg.rank} of {self.cfg.world}: {e!r}; rerun with TrainConfig(dp_graph=False) / '
+                    f'bench.py --dp-graph 0 (graph parts with eager collectives)') from e
             finally:
                 sh.no_comm = False
             graphs.append(g)

@@ -8,7 +8,7 @@ ORACLE tooling — test infrastructure only.  Imports, read-only, from /root/ref
 Nothing from the reference is copied: the outputs (inputs + expected outputs) are written as
 small ``.npz`` fixtures under ``tests/golden/``; the reference never travels to the GPU box.
 
-Run:  python -m oracle.make_golden   (from the repo root)
+Run:  python -m oracle.make_golden [case ...]   (from the repo root; no case: all of them)
 """
 import os
 import sys
@@ -69,8 +69,14 @@ def main():
         # name, seed, C, V, sizes, B, batches
         ('small', 20250301, 48, 120, (6, 12, 20, 30), 8, 3),
         ('medium', 7, 160, 900, (40, 90, 140, 200), 32, 2),
+        # the bench's kernel class (bf16, d = 256, B = 128: the fused output-layer kernels) on the
+        # reference generator's own batches; M is not stored (50 MB), its oracle is pinned above
+        ('bench', 11, 512, 2500, (20, 40, 80), 128, 2),
     ]
+    only = sys.argv[1:]
     for name, seed, C, V, sizes, B, nb in cases:
+        if only and name not in only:
+            continue
         rng = np.random.default_rng(seed)
         X = synthetic_dense_cubes(rng, C, V, sizes)
         M = ref_utils.create_adjacency_matrix(X, verbose=False)
@@ -97,8 +103,9 @@ def main():
             seed=np.int64(seed % (2 ** 32)), cubes=X.astype(np.int8), B=np.int64(B),
             neg_sampler=gen.neg_sampler, perm0=perm0, perm1=perm1,
             x=np.stack(xs), y=np.stack(ys), reg=np.stack(regs))
-        np.savez_compressed(os.path.join(OUT, f'adjacency_{name}.npz'),
-                            cubes=X.astype(np.int8), M=M, Mt=Mt)
+        if name != 'bench':
+            np.savez_compressed(os.path.join(OUT, f'adjacency_{name}.npz'),
+                                cubes=X.astype(np.int8), M=M, Mt=Mt)
         print(name, 'C', C, 'V', V, 'batches', len(xs), 'M nnz', int((M > 0).sum()))
 
 

@@ -342,10 +342,10 @@ def _rccl_run(tr, eager=2, graphed=3):
     return losses
 
 
-def _rccl_worker(shape, reg, reg_shard, q, chunks=0):
+def _rccl_worker(shape, reg, reg_shard, q, chunks=0, dp_graph=True):
     os.environ.update(HSA_ENABLE_IPC_MODE_LEGACY='0')
     import faulthandler
-    faulthandler.dump_traceback_later(150, exit=True)   # a stuck child names where it is stuck
+    faulthandler.dump_traceback_later(240, exit=True)   # a stuck child names where it is stuck
     try:
         import torch.distributed as dist
         torch.cuda.set_device(0)
@@ -354,21 +354,49 @@ def _rccl_worker(shape, reg, reg_shard, q, chunks=0):
         dist.init_process_group('nccl', store=dist.HashStore(), rank=0, world_size=1,
                                 device_id=torch.device('cuda', 0))
         progress('rccl: process group up; building the DP trainer')
-        tr = _rccl_trainer(shape, reg, True, reg_shard, w1_chunks=chunks)
+        tr = _rccl_trainer(shape, reg, True, reg_shard, w1_chunks=chunks, dp_graph=dp_graph)
         assert tr.dp and tr.prefetch_dp and tr.owner == (reg_shard and reg > 0)
         assert chunks == 0 or len(tr.layout.w1_chunks) == chunks
         dl = _rccl_run(tr)
-        assert tr._sharded().nccl and tr.g_dp is not None, 'whole-step DP graph not captured'
+        assert tr._sharded().nccl
+        if dp_graph:
+            assert tr.g_dp is not None, 'whole-step DP graph not captured'
+        else:        # the parts path: graph replays of the phases, eager RCCL collectives between
+            assert tr.g_dp is None and tr.graphs is not None
+        # a replayed (or eager) step leaves its deferred output-layer all-gather pending for flush()
+        tr.step()
+        assert tr.sharded.out_pending == tr.sharded.defer_out
+        tr.flush()
+        assert not tr.sharded.out_pending
+        torch.cuda.synchronize()
+        dl.append(tr.losses()['loss'])
         tr.sharded.gather_state()
         tr.check_status()
         progress('rccl: DP steps done; building the one-process trainer')
         one = _rccl_trainer(shape, reg, False, False)
         assert not one.dp
         ol = _rccl_run(one)
+        one.step()
+        one.flush()
+        torch.cuda.synchronize()
+        ol.append(one.losses()['loss'])
         one.check_status()
-        progress('rccl: one-process steps done; sending the result')
-        q.put((tr.standard(tr.params), tr.standard(tr.m), tr.standard(tr.v), dl,
-               one.standard(one.params), one.standard(one.m), one.standard(one.v), ol))
+        res = (tr.standard(tr.params), tr.standard(tr.m), tr.standard(tr.v), dl,
+               one.standard(one.params), one.standard(one.m), one.standard(one.v), ol)
+        del tr, one
+        if not dp_graph:   # the parts path against the whole-step graph too, on the same draws
+            progress('rccl: building the whole-step-graph DP trainer')
+            wh = _rccl_trainer(shape, reg, True, reg_shard, w1_chunks=chunks, dp_graph=True)
+            wl = _rccl_run(wh)
+            assert wh.g_dp is not None
+            wh.step()
+            wh.flush()
+            torch.cuda.synchronize()
+            wl.append(wh.losses()['loss'])
+            wh.sharded.gather_state()
+            res = res + (wh.standard(wh.params), wh.standard(wh.m), wh.standard(wh.v), wl)
+        progress('rccl: steps done; sending the result')
+        q.put(res)
         dist.destroy_process_group()
         progress('rccl: process group destroyed')
     except Exception as e:   # surface the error in the parent
@@ -378,16 +406,19 @@ def _rccl_worker(shape, reg, reg_shard, q, chunks=0):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize('shape,reg,reg_shard,chunks', [('bench', 0.0, False, 0), ('bench', 0.1, True, 0),
-                                                        ('bench', 0.1, True, 3), ('c5', 0.1, True, 0)])
-def test_rccl_one_rank_dp_step_matches_one_process(shape, reg, reg_shard, chunks):
-    """The data-parallel step over RCCL (1 rank), eager then as the captured whole-step graph, ==
-    the one-process step on the same draws: parameters, Adam moments and losses over 5 steps.
-    chunks: W1's gradient launched and exchanged in that many row chunks (0: the default)."""
+@pytest.mark.parametrize('shape,reg,reg_shard,chunks,dp_graph', [
+    ('bench', 0.0, False, 0, True), ('bench', 0.1, True, 0, True), ('bench', 0.1, True, 3, True),
+    ('c5', 0.1, True, 0, True), ('bench', 0.0, False, 0, False), ('bench', 0.1, True, 0, False)])
+def test_rccl_one_rank_dp_step_matches_one_process(shape, reg, reg_shard, chunks, dp_graph):
+    """The data-parallel step over RCCL (1 rank), eager then as the captured whole-step graph
+    (dp_graph) or as graph replays of its parts with eager collectives between them (not dp_graph:
+    bench.py --dp-graph 0, the fallback for the multi-rank run), == the one-process step on the same
+    draws: parameters, Adam moments and losses over 6 steps; the parts path also == the whole-step
+    graph.  chunks: W1's gradient launched and exchanged in that many row chunks (0: the default)."""
     from tests.gpu_helpers import record_errors
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    p = ctx.Process(target=_rccl_worker, args=(shape, reg, reg_shard, q, chunks))
+    p = ctx.Process(target=_rccl_worker, args=(shape, reg, reg_shard, q, chunks, dp_graph))
     p.start()
     res = None
     for _ in range(56):        # (a child that dies without a result fails the test at once)
@@ -401,11 +432,17 @@ def test_rccl_one_rank_dp_step_matches_one_process(shape, reg, reg_shard, chunks
     p.join(60)
     assert res[1] is not None, res[0]
     assert p.exitcode == 0
-    dp_p, dp_m, dp_v, dl, p1, m1, v1, ol = res
+    dp_p, dp_m, dp_v, dl, p1, m1, v1, ol = res[:8]
     errs = {'params': rel_err(dp_p, p1), 'm': rel_err(dp_m, m1), 'v': rel_err(dp_v, v1),
             'loss': max(abs(a - b) / b for a, b in zip(dl, ol)),
             'exact_params': float(np.array_equal(dp_p, p1))}
-    record_errors(f'rccl1_vs_one_{shape}_{reg}_c{chunks}', 5, errs)
+    record_errors(f'rccl1_vs_one_{shape}_{reg}_c{chunks}_g{int(dp_graph)}', 6, errs)
+    if not dp_graph:
+        wp, wm, wv, wl = res[8:]
+        np.testing.assert_array_equal(dp_p, wp)
+        np.testing.assert_array_equal(dp_m, wm)
+        np.testing.assert_array_equal(dp_v, wv)
+        assert list(dl) == list(wl), (dl, wl)
     # one rank: the shard is the whole bucket, the collectives are copies — the same kernels on the
     # same draws, so the step is bit-identical (observed r04: every error exactly 0)
     np.testing.assert_array_equal(dp_p, p1)

@@ -594,3 +594,25 @@ def test_metric_counts_exact_after_capture():
     assert c[2] == 6 * B and 0 <= c[0] <= 6 * B and 0 <= c[1] <= c[2], c
     m = tr.take_metrics(6)
     assert 0.0 <= m['output_1_accuracy'] <= 1.0 and 0.0 <= m['output_2_accuracy'] <= 1.0
+
+
+def test_sigmoid_cat_accuracy_tie_rules():
+    """cc_sigmoid_cat_accuracy's claimed tie rules (ccrec.h; parity against TF's Eigen sigmoid is
+    unpinned below the saturation point): logits past 15.7243833541870117 saturate to
+    1.0 so the FIRST saturated column is the argmax even when a later logit is larger; an all-zero
+    target row maps to index 0."""
+    V, Bt = 100, 4
+    Z = np.full((Bt, V), -3.0, np.float32)
+    Z[0, 10], Z[0, 40] = 16.0, 30.0        # both saturate: column 10 wins; target bit 10 -> correct
+    Z[1, 10], Z[1, 40] = 15.0, 30.0        # only 40 saturates: argmax 40; target 10 -> wrong
+    Z[2, 0], Z[2, 7] = 2.0, 1.0            # argmax 0; all-zero target row -> index 0 -> correct
+    Z[3, 5], Z[3, 6] = 40.0, 40.0          # exact tie at 1.0: column 5; target bits {6, 5} -> first 5
+    y = np.zeros((Bt, 128), np.uint8)
+    y[0, 10] = y[1, 10] = 1
+    y[3, 5] = y[3, 6] = 1
+    yw = torch.from_numpy(np.packbits(y, axis=1, bitorder='little').view(np.int32)).cuda()
+    cnt = torch.zeros(3, dtype=torch.int64, device='cuda')
+    L.call('cc_sigmoid_cat_accuracy', L.ptr(torch.from_numpy(Z).cuda()), V, L.ptr(yw), Bt, V, L.ptr(cnt),
+           L.stream_ptr())
+    torch.cuda.synchronize()
+    assert int(cnt[0]) == 3, cnt          # rows 0, 2, 3 correct; row 1 not

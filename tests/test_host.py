@@ -106,3 +106,16 @@ def test_names_unidecode_restatement():
     assert unidecode('ドラゴン') == 'doragon' and unidecode('しつ') == 'situ' and unidecode('カード') == 'ka-do'
     for cp in list(range(0xAC00, 0xD7A4, 97)) + list(range(0x3041, 0x3095)) + list(range(0x30A1, 0x30F5)):
         assert unidecode(chr(cp)).isascii() and unidecode(chr(cp)), hex(cp)
+
+
+def test_dp_layout_w1_chunks_any_world():
+    """W1 row chunks stay whole bucket shards for worlds that are not powers of two (ADVICE r05:
+    d = 1024 with world 3 / 6 used to trip the alignment assert at Trainer construction)."""
+    from cubecobrarecommender_amd.layout import Layout
+    for world in (1, 2, 3, 5, 6, 7, 8):
+        for d, chunks in ((256, 1), (1024, 2), (1024, 3), (512, 4)):
+            lay = Layout(22000, d, align=64 * world, group_biases=True, w1_chunks=chunks)
+            for name, lo, hi in lay.buckets(True):
+                assert (hi - lo) % (64 * world) == 0, (world, d, name)
+            assert all(r0 % 64 == 0 for r0, _ in lay.w1_chunks)
+            assert lay.w1_chunks[0][0] == 0 and lay.w1_chunks[-1][1] == 22000
