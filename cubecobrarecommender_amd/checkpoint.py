@@ -19,8 +19,9 @@ variable, its Keras layer name and Adam slots); the reader parses such files (mu
 prefix-compressed, multi-shard, string tensors).  The reference's Git-LFS pointers pin the data
 sizes (12 * P + 40 B of variables at |V| = 20,884, d = 512; tests/test_checkpoint.py checks the
 writer against them); the byte contents of files written by TF itself stay unpinned (no real
-checkpoint exists in this pipeline).  ``saved_model.pb`` (the TF graph, which TF is needed to
-produce) is written as an empty SavedModel message, and ``ccrec_config.json`` records (V, d).
+checkpoint exists in this pipeline).  ``saved_model.pb`` is a SavedModel proto whose
+SavedObjectGraph mirrors the object graph node for node (savedmodel.py; the traced functions, which
+only TF can produce, are absent), and ``ccrec_config.json`` records (V, d).
 """
 import json
 import os
@@ -438,7 +439,7 @@ def parse_object_graph(b):
 
 # ---------------------------------------------------------------------------- model files
 def save_model(dest, V, d, params, m=None, v=None, step=0, lr=1e-3, beta1=0.9, beta2=0.999,
-               metrics=None, shards=1):
+               metrics=None, shards=1, reg=0.0):
     """ml_files/<name>/ as train.py:112-115 lays it out.  params/m/v: dict name -> array.
     metrics: {'loss': (total, count), 'output_1_loss': (total, count)} — the compiled metrics'
     accumulators after fit (zeros when absent; written with the optimizer state).  shards=2: the
@@ -468,7 +469,9 @@ def save_model(dest, V, d, params, m=None, v=None, step=0, lr=1e-3, beta1=0.9, b
     t[OBJECT_GRAPH_KEY] = object_graph(t.keys())
     write_bundle(os.path.join(dest, 'variables', 'variables'), t,
                  shard_of=(lambda k: 0 if k == OBJECT_GRAPH_KEY else 1) if shards == 2 else None)
-    open(os.path.join(dest, 'saved_model.pb'), 'wb').close()          # empty SavedModel message
+    from .savedmodel import saved_model_proto   # the SavedObjectGraph mirroring the object graph
+    with open(os.path.join(dest, 'saved_model.pb'), 'wb') as fh:
+        fh.write(saved_model_proto(t, V, d, reg=reg, lr=lr, beta1=beta1, beta2=beta2))
     json.dump({'num_cards': int(V), 'd': int(d), 'format': 'ccrec-mi355x/1'},
               open(os.path.join(dest, 'ccrec_config.json'), 'w'))
 

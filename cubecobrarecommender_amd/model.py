@@ -200,7 +200,8 @@ class CC_Recommender:
             m, v = lay.unpack(self._m), lay.unpack(self._v)
         else:
             m = v = None
-        checkpoint.save_model(dest, self.N, self.d, P, m, v, step=self._step, lr=self.lr, metrics=self._metrics)
+        checkpoint.save_model(dest, self.N, self.d, P, m, v, step=self._step, lr=self.lr, metrics=self._metrics,
+                              reg=self.reg)
 
     # --------------------------------------------------------------- internals
     def _current_flat(self):
