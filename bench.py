@@ -64,6 +64,9 @@ def parse():
                     help='data parallel over RCCL: 1 = the whole step (collectives included) as one captured '
                          'hipGraph; 0 = graph replays of the step\'s parts with eager RCCL collectives between '
                          'them (the fallback if multi-rank capture misbehaves; same arithmetic, bit-identical)')
+    ap.add_argument('--reg-by-index', type=int, default=1, choices=(0, 1),
+                    help='sampled regulariser: its one-card rows enter the W1 gradient by index (1, '
+                         'TrainConfig.reg_by_index) or as bits of a 2B-row bit matrix (0); bit-identical')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-steps', type=int, default=16)
     ap.add_argument('--no-recommend', action='store_true')
@@ -480,7 +483,7 @@ def main():
                                            if args.steps % g == 0 and (g <= args.warmup or g == 1))
     cfg = TrainConfig(V=V, d=d, batch_size=B, reg=args.reg, dtype=args.dtype, seed=1234,
                       rank=rank, world=world, reg_shard=reg_shard, reg_mode=args.reg_mode,
-                      force_dp=args.force_dp, dp_graph=bool(args.dp_graph),
+                      force_dp=args.force_dp, dp_graph=bool(args.dp_graph), reg_by_index=bool(args.reg_by_index),
                       dz_pad=bool(args.dz_pad), graph_steps=graph_steps, wo_tower_frac=args.wo_tower_frac,
                       fuse_w1_adam=True,   # one process: W1's Adam in its gradient kernel, and (BCE
                       wo_adam_in_tower=True,   # only) Wo's in the tower backward launch, with the next

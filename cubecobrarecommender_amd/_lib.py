@@ -156,6 +156,9 @@ SIGNATURES = {
     'cc_embed_grad_cs_tickets': (_I32, [_I32, _I32, _I32]),
     'cc_embed_grad_cs_adam': (C.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _P,
                                         _F32, _F32, _F32, _F32, _P]),
+    'cc_embed_grad_cs_reg': (C.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P]),
+    'cc_embed_grad_cs_adam_reg': (C.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _P,
+                                            _F32, _F32, _F32, _F32, _P, _I32, _I32, _P]),
     'cc_embed_identity_ws': (_SZ, [_I32, _I32]),
     'cc_embed_identity_add': (C.c_int, [_I32, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
     'cc_reg_rows': (C.c_int, [C.POINTER(NoiseArgs), _P]),

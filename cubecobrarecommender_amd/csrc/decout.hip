@@ -28,47 +28,16 @@ constexpr int NB_MIN = 64;
 constexpr int BK = 64;      // k per phase-2 ring chunk
 constexpr int NTH = 512;    // 8 waves
 constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
-// cache policy (buffer cache-policy operand; 2 = non-temporal) of the dZ and dWo stores.  Measured
-// (r03 A/B, BCE step): non-temporal dZ slows the next dX kernel, which reads dZ from L2 (16 -> 19
-// us); both default
-#ifndef DEC_DZ_CPOL
-#define DEC_DZ_CPOL 0
-#endif
-#ifndef DEC_GW_CPOL
-#define DEC_GW_CPOL 0
-#endif
+// cache policy of the dZ and dWo stores: default (measured, r03 / r05: non-temporal dZ slows the
+// next dX kernel, which reads dZ from L2, 16 -> 19 us; non-temporal dWo neutral)
+constexpr int DEC_CPOL = 0;
 // The two waves of a SIMD run the VALU-bound BCE epilogue together; issue arbitration favours the
 // older one, so waves 4-7 finish ~3.6 us later and the barrier after phase 1 waits for them (probe:
-// tools/micro/dec_probe2.hip).  DEC_PRIO_TOGGLE: in pass ps the half (w >> 2) == (ps & 1) runs at
-// s_setprio 1, so the half that lagged in pass 0 leads in pass 1 (build knob; DMA kernels only)
-#ifndef CCREC_DEC_DMA   // build knob: 0 keeps the register-staged kernel for every shape
-#define CCREC_DEC_DMA 1
-#endif
-#ifndef DEC_SPLIT2       // build knob: 0 keeps phase 2 whole after the barrier
-#define DEC_SPLIT2 1
-#endif
-#ifndef DEC_PRIO_TOGGLE
-#define DEC_PRIO_TOGGLE 1
-#endif
-// DEC_YS_FIRST: pass 0 issues the target-word loads BEFORE the next pass's A-fragment prefetch, so
-// the wait for the words (before the epilogue stages them in LDS) leaves the prefetch in flight
-// (after it, that wait was a vmcnt(0) that also drained the prefetch)
-#ifndef DEC_YS_FIRST
-#define DEC_YS_FIRST 0
-#endif
-// DEC_D16HI: the odd row of each packed dz pair stored by buffer_store_short_d16_hi straight from
-// the packed register (no shift)
-#ifndef DEC_D16HI
-#define DEC_D16HI 1
-#endif
-// DEC_SCALAR: the BCE epilogue in scalar fp32 ops (built with -fno-slp-vectorize) instead of
-// packed v_pk_* pairs
-#ifndef DEC_SCALAR
-#define DEC_SCALAR 0
-#endif
-#ifndef DEC_YS_LATE   // build knob: 0 stages the target words with the Wo slice, before the first barrier
-#define DEC_YS_LATE 1
-#endif
+// tools/micro/dec_probe2.hip).  In pass ps the half (w >> 2) == (ps & 1) runs at s_setprio 1, so
+// the half that lagged in pass 0 leads in pass 1 (DMA kernels).  (Round 5 measured the alternatives —
+// three other priority modes, the target words staged before the A prefetch or with the Wo slice,
+// the epilogue in scalar instead of packed fp32 ops, the odd dz row by a shift instead of d16_hi —
+// all within +-0.3 us; they live on branch archive/r05-ab-knobs.)
 
 typedef __attribute__((ext_vector_type(4))) uint32_t v4u;  // staging registers (stay in VGPRs)
 typedef __attribute__((address_space(3))) void lds_void;
@@ -141,7 +110,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   // are still in their epilogue; waves 0-3 multiply them then (their d tile w and the partner's
   // w + 4, the partner's partial handed over through LDS), and after the barrier each wave adds
   // only the other half's chunks 2, 3, 6, 7 of its own tile: half the MFMAs after the barrier.
-  constexpr bool SPLIT2 = DEC_SPLIT2 && d == 256 && B == 512;
+  constexpr bool SPLIT2 = d == 256 && B == 512;
   constexpr int npass = (B + 255) / 256;          // 256-row passes of phase 1
   // phase-1 A fragments: d <= 256 holds a whole pass (and the next one in flight); d = 512 walks
   // a ring of 16 through the pass's 32 k-steps
@@ -207,7 +176,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   // YS_LATE (DMA, B >= 256: every wave has rows in pass 0): the target words are loaded last and
   // written to LDS only after pass 0's logits MFMAs, so the first barrier waits for the Wo slice and
   // the A fragments but not for the 1.5-K strided word loads
-  constexpr bool YS_LATE = DEC_YS_LATE && DMA && B >= 256;
+  constexpr bool YS_LATE = DMA && B >= 256;
   constexpr int NY = (B * NJ + NTH - 1) / NTH;
   uint32_t yv[NY];
   auto load_ys = [&]() {
@@ -342,9 +311,9 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
       __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)B * (uint32_t)p.ldz * 2u, 0x00020000);
   const int LZ = p.ldz;
   // dz of rows (r2, r2 + 1) as one packed bf16 pair -> two 2-B stores (row offsets as the scalar
-  // soffset).  DEC_D16HI: the odd row by buffer_store_short_d16_hi straight from the pair (inline
-  // asm: the compiler counts no vmcnt for it — a later counted wait can only over-wait, never
-  // under-wait, since this store is younger than every load it counts)
+  // soffset); the odd row by buffer_store_short_d16_hi straight from the pair (inline asm: the
+  // compiler counts no vmcnt for it — a later counted wait can only over-wait, never under-wait,
+  // since this store is younger than every load it counts)
 #ifdef DEC_DIAG_NODZ   // diagnostic builds only (tools/micro/dec_probe2.hip): no dz stores
 #define DEC_STORE_PAIR(PK, R2) do { (void)(PK); } while (0)
 #else
@@ -352,23 +321,15 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   do {                                                                                                    \
     const uint32_t so0 = 2u * (uint32_t)((((R2) & 3) + 8 * ((R2) >> 2)) * LZ);                           \
     const uint32_t so1 = 2u * (uint32_t)(((((R2) + 1) & 3) + 8 * (((R2) + 1) >> 2)) * LZ);                \
-    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(PK), dz_rs, zv, so0, DEC_DZ_CPOL);                  \
-    if constexpr (DEC_D16HI)                                                                              \
-      asm volatile("buffer_store_short_d16_hi %0, %1, %2, %3 offen" ::"v"(PK), "v"(zv), "s"(dz_rs), "s"(so1) \
-                   : "memory");                                                                           \
-    else                                                                                                  \
-      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)((PK) >> 16), dz_rs, zv, so1, DEC_DZ_CPOL);         \
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(PK), dz_rs, zv, so0, DEC_CPOL);                     \
+    asm volatile("buffer_store_short_d16_hi %0, %1, %2, %3 offen" ::"v"(PK), "v"(zv), "s"(dz_rs), "s"(so1)   \
+                 : "memory");                                                                             \
   } while (0)
 #endif
 #pragma unroll
   for (int ps = 0; ps < npass; ++ps) {
-    if constexpr (YS_LATE && DEC_YS_FIRST) {
-#ifndef DEC_DIAG_NOY
-      if (ps == 0) load_ys();   // before the prefetch: the epilogue's wait for them leaves it in flight
-#endif
-    }
     if (!RING1 && ps + 1 < npass) load_a(af[(ps + 1) & 1], ps + 1);
-    if constexpr (YS_LATE && !DEC_YS_FIRST) {
+    if constexpr (YS_LATE) {
 #ifndef DEC_DIAG_NOY
       if (ps == 0) load_ys();   // the youngest loads: nothing before pass 0's epilogue waits for them
 #endif
@@ -413,12 +374,9 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         if (lane == 0) __hip_atomic_fetch_add(&cnt_wt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
-    if constexpr (DMA && DEC_PRIO_TOGGLE && npass > 1) {   // (wave-uniform: w from readfirstlane)
-      // 1: the half (w >> 2) == (ps & 1) leads pass ps; 3: the reverse (the younger half leads pass
-      // 0); 2: the younger half (waves 4-7, the arbitration loser) at priority 1 throughout
+    if constexpr (DMA && npass > 1) {   // the half (w >> 2) == (ps & 1) leads pass ps (wave-uniform)
       const int hw = __builtin_amdgcn_readfirstlane(w) >> 2;
-      const bool hi = DEC_PRIO_TOGGLE == 2 ? hw == 1 : DEC_PRIO_TOGGLE == 3 ? hw != (ps & 1) : hw == (ps & 1);
-      if (hi)
+      if (hw == (ps & 1))
         __builtin_amdgcn_s_setprio(1);
       else
         __builtin_amdgcn_s_setprio(0);
@@ -440,49 +398,6 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         // instruction; summed log2 scaled by ln 2 at the end
         // store offsets: the lane part in a VGPR, the row part (r) as the scalar soffset
         const uint32_t zv = 2u * (uint32_t)((rb + 4 * half) * LZ + n0 + col);
-#if DEC_SCALAR
-        // even / odd rows accumulate apart (the packed form's lanes), one fp32 op per element:
-        // packed v_pk_* f32 ops issue slower than two scalar ones beside the MFMAs
-        // (MI355X_MICROARCH.md, per-instruction constants) and gain nothing on the VALU
-        float lp[2] = {1.f, 1.f}, rsa[2] = {0.f, 0.f}, csa[2] = {0.f, 0.f};
-        uint4 yw[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-#ifdef DEC_DIAG_NOY   // diagnostic builds only: targets taken as all zero (no staging, no barrier)
-          yw[g] = make_uint4(0u, 0u, 0u, 0u);
-#else
-          yw[g] = *reinterpret_cast<const uint4 *>(ys + j * B + rb + 8 * g + 4 * half);
-#endif
-        }
-        const uint32_t ysh = 31u - (uint32_t)(lane & 31);   // the lane's target bit -> bit 31
-#pragma unroll
-        for (int r2 = 0; r2 < 16; r2 += 2) {
-          float dz2[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const int r = r2 + e;
-            const uint32_t ywr = (r & 3) == 0 ? yw[r >> 2].x : (r & 3) == 1 ? yw[r >> 2].y : (r & 3) == 2 ? yw[r >> 2].z : yw[r >> 2].w;
-            const uint32_t ym = ywr << ysh;
-            const float z = acc[j][r];
-            const float sv = __uint_as_float(xor_sign(__float_as_uint(z), ym));
-            const float a = __builtin_amdgcn_exp2f(-fabsf(z) * LOG2E);
-            const float opa = 1.f + a;
-            const float rp = __builtin_amdgcn_rcpf(opa);
-            lp[e] *= opa;
-            rsa[e] += fmaxf(sv, 0.f);
-            const float sel = sv >= 0.f ? rp : a * rp;   // sigmoid(s)
-            const float dzv = __uint_as_float(xor_sign(__float_as_uint(sel * scale), ym));
-            csa[e] += dzv;   // the bias gradient sums the fp32 dz (the reference's arithmetic)
-            dz2[e] = dzv;
-          }
-          const uint32_t pk = bf16_pack2(dz2[0], dz2[1]);
-          tt[r2 >> 1] = pk;
-          DEC_STORE_PAIR(pk, r2);
-        }
-        lsum += __builtin_amdgcn_logf(lp[0] * lp[1]);
-        rsum += rsa[0] + rsa[1];
-        cs[j] += csa[0] + csa[1];
-#else
         f32x2_t lprod = {1.f, 1.f}, rs2 = {0.f, 0.f}, cs2 = {0.f, 0.f};  // even / odd rows: packed math
         // the 16 rows' target words: 4 runs of 4 consecutive rows -> 4 LDS reads of 16 B
         uint4 yw[4];
@@ -529,7 +444,6 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         lsum += __builtin_amdgcn_logf(lprod[0] * lprod[1]);
         rsum += rs2[0] + rs2[1];
         cs[j] += cs2[0] + cs2[1];
-#endif
       } else {
 #pragma unroll
         for (int r = 0; r < 8; ++r) tt[r] = 0;
@@ -541,7 +455,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     }
     DEC_PROBE(3 + 2 * ps);
   }
-  if constexpr (DMA && DEC_PRIO_TOGGLE && npass > 1) __builtin_amdgcn_s_setprio(0);
+  if constexpr (DMA && npass > 1) __builtin_amdgcn_s_setprio(0);
   if constexpr (SPLIT2) {   // waves 0-3: this wave's dZ^T rows are in LDS
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (w < 4 && lane == 0) __hip_atomic_fetch_add(&cnt_z, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -671,7 +585,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc2[j][r]), gw_rs,
-                                                4u * (g0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V)), 0, DEC_GW_CPOL);
+                                                4u * (g0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V)), 0, DEC_CPOL);
       }
     }
   } else {
@@ -754,7 +668,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 #pragma unroll
           for (int r = 0; r < 16; ++r)
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc2[j][r]), gw_rs,
-                                                  4u * (g0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V)), 0, DEC_GW_CPOL);
+                                                  4u * (g0 + (uint32_t)(((r & 3) + 8 * (r >> 2)) * V)), 0, DEC_CPOL);
         }
       }
     }
@@ -841,7 +755,7 @@ extern "C" int cc_dec_bce_dw_ld(const void *D3, const void *D3t, int32_t ldt, co
   hipStream_t s = as_stream(stream);
   // the DMA staging: Wo read in place with every row segment 16-B aligned (V % 8 == 0), the
   // 96-column slices of d <= 256
-  const bool dma = CCREC_DEC_DMA && Wo != nullptr && WoT == nullptr && V % 8 == 0 && d <= 256 && (((uintptr_t)y_bits) & 3) == 0 &&
+  const bool dma = Wo != nullptr && WoT == nullptr && V % 8 == 0 && d <= 256 && (((uintptr_t)y_bits) & 3) == 0 &&
                    (int64_t)d * V * 2 <= 0xFFFFFFFFll && (int64_t)B * ((V + 31) / 32) * 4 <= 0xFFFFFFFFll;
 #define DO_LAUNCH(DD, BBB)                                                                    \
   if (d == DD && B == BBB) {                                                                  \

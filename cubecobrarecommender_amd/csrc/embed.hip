@@ -803,13 +803,30 @@ struct CsAdam {
   const int64_t *state;  // device step counters: t = state[0] + 1 (cc_adam_dense's t)
   float lr, b1, b2, eps;
 };
+// REG: the sampled regulariser's identity rows by index instead of by bit.  Row B + i of the batch
+// (i < nreg) is the one-card row {rid[i]} (generator.py:47-61: x_reg = identity rows of the reg
+// draws), so in the bit matrix a W1 row holds at most a handful of the nreg reg bits and most of
+// the product's reg k-steps multiply an all-zero A fragment.  With REG the bit matrix covers the B
+// cube rows only (the product's K = B: the XWM = 16 instance at B = 512 instead of XWM = 32), and each
+// tile adds the reg k-steps whose A fragment is not all zero for its 32 rows — found from rid (in
+// LDS), A fragments built from rid compares, B fragments loaded from the same dPre1 image (k-step
+// k0 + ks) — in ascending order after the cube k-steps: the MFMA sequence of the full-K product
+// minus its all-zero k-steps, i.e. the same fp32 results.  The bias row (all rows) takes every
+// reg k-step.
+struct CsReg {
+  const int32_t *rid;  // [nreg] cards of the reg rows (absolute card ids; -1: a padding row)
+  int nreg;            // <= CS_REG_MAX (512)
+  int k0;              // the first reg k-step in the dPre1 image (= B / 16)
+  int card0;           // card of this launch's W1 row 0 (a row chunk's first row)
+};
+constexpr int CS_REG_MAX = 512;   // (one 32-bit mask of reg k-steps per tile)
 
-template <bool PK, int XWM, bool VEC, bool ADAM>
+template <bool PK, int XWM, bool VEC, bool ADAM, bool REG = false>
 __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *__restrict__ gsrc, int V, int d, int R,
                                                             int RP, int tpc, uint32_t *xt,
                                                             float *__restrict__ grad,
                                                             float *__restrict__ bias_grad, uint32_t *tickets,
-                                                            CsAdam ad) {
+                                                            CsAdam ad, CsReg rg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
@@ -825,6 +842,8 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
   bf16_t *Bs = reinterpret_cast<bf16_t *>(smem);                  // fragment j at (j * 64 + lane) * 8
   unsigned char *lut = smem + (size_t)2 * XWM * 1024;             // [256 values][16 copies] x 16 B
   float *tx = reinterpret_cast<float *>(lut + cs_lut_bytes(XWM, ADAM));  // ADAM: per-wave 32 x 36 tiles
+  // REG: the reg rows' cards, padded with -1 to a multiple of 512 entries
+  int32_t *rl = reinterpret_cast<int32_t *>(reinterpret_cast<unsigned char *>(tx) + (ADAM ? (CS_NT / 64) * 32 * 36 * 4 : 0));
   // ---- every global read first: the bit words of all the wave's tiles (wave w takes tiles w,
   // w + 8, ... of the chunk; a lane holds its row's XWM words per tile), then the B slice and LUT
   // (every global load below is unconditional — clamped address, then a select — so the
@@ -881,6 +900,16 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
     }
   }
   for (int e = tid; e < 256 * LC; e += CS_NT) reinterpret_cast<uint4 *>(lut)[e] = byte_bf16((uint32_t)(e / LC));
+  if constexpr (REG) {   // (unconditional loads, clamped index: counted waits stay exact)
+    constexpr int RQ = CS_REG_MAX / CS_NT;
+    const int nr512 = (rg.nreg + 511) & ~511;
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+      const int i = tid + CS_NT * q;
+      const int32_t c = rg.rid[min(i, rg.nreg - 1)];
+      if (i < nr512) rl[i] = i < rg.nreg ? c : -1;
+    }
+  }
   EG_PROBE(1);
   __syncthreads();  // (its release fence: every load of the block, bit words included, has returned)
   EG_PROBE(2);
@@ -935,8 +964,62 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
   if constexpr (PF) {
     if (w < nt) issue_adam(w, 0);
   }
+  // REG: dPre1 fragment of reg k-step ks (clamped: an unconditional load)
+  auto reg_bfrag = [&](int ks) -> bf16x8_t {
+    const int k = rg.k0 + max(ks, 0);
+    if constexpr (PK)
+      return *reinterpret_cast<const bf16x8_t *>(gsrc + ((int64_t)cs * (RP / 16) * 64 + (int64_t)k * 64 + lane) * 8);
+    else
+      return *reinterpret_cast<const bf16x8_t *>(gsrc + (int64_t)(32 * cs + (lane & 31)) * RP + 16 * k + 8 * half);
+  };
   auto tile = [&](int t, const uint32_t (&wd)[XWM], int b, int tn) {
     const int vr = v0 + 32 * t + (lane & 31);
+    // REG: the reg k-steps with an entry in this tile (km: bit ks), the first RPF of them prefetched
+    // under the cube k-steps (the bias tile takes all of them)
+    constexpr int RPF = 2, NKW = REG ? CS_REG_MAX / 512 : 1;
+    uint32_t km[NKW];
+    bf16x8_t rb[REG ? RPF : 1];
+    int rks[REG ? RPF : 1];
+    const int tcard = rg.card0 + v0 + 32 * t;                  // the tile's first card
+    const bool btile = bias_grad && v0 + 32 * t <= V && V < v0 + 32 * t + 32;   // (wave-uniform)
+    auto next_k = [&]() -> int {   // pop the lowest relevant k-step (-1: none left); wave-uniform
+#pragma unroll
+      for (int q = 0; q < NKW; ++q)
+        if (km[q]) {
+          const int k = 32 * q + __builtin_ctz(km[q]);
+          km[q] &= km[q] - 1u;
+          return k;
+        }
+      return -1;
+    };
+    if constexpr (REG) {
+#pragma unroll
+      for (int q = 0; q < NKW; ++q) {
+        km[q] = 0u;
+        if (512 * q < rg.nreg) {
+          const int i0 = 512 * q + 8 * lane;   // lane l: entries i0 .. i0 + 7 = half of k-step i0 / 16
+          const int4 e0 = *reinterpret_cast<const int4 *>(rl + i0), e1 = *reinterpret_cast<const int4 *>(rl + i0 + 4);
+          const uint32_t u = (uint32_t)tcard;
+          const bool hit = btile ? i0 < rg.nreg
+                                 : ((uint32_t)e0.x - u < 32u) | ((uint32_t)e0.y - u < 32u) | ((uint32_t)e0.z - u < 32u) |
+                                       ((uint32_t)e0.w - u < 32u) | ((uint32_t)e1.x - u < 32u) | ((uint32_t)e1.y - u < 32u) |
+                                       ((uint32_t)e1.z - u < 32u) | ((uint32_t)e1.w - u < 32u);
+          uint64_t x = __ballot(hit);
+          x = (x | (x >> 1)) & 0x5555555555555555ull;   // lanes 2k, 2k + 1 -> bit 2k
+          x = (x | (x >> 1)) & 0x3333333333333333ull;   // ... then gather the even bits
+          x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+          x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+          x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+          x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+          km[q] = __builtin_amdgcn_readfirstlane((uint32_t)x);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < RPF; ++u) {
+        rks[u] = next_k();
+        rb[u] = reg_bfrag(rks[u]);
+      }
+    }
     if constexpr (ADAM && !PF) issue_adam(t, 0);
     cc_adam::f32x4_t(&ap)[ADAM ? 4 : 1] = AP[NBUF == 2 ? b : 0];
     cc_adam::f32x4_t(&am)[ADAM ? 4 : 1] = AM[NBUF == 2 ? b : 0];
@@ -973,6 +1056,40 @@ __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *_
       for (int u = 0; u < CS_G; ++u)  // operands swapped: acc = (dW1 tile)^T, see below
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[g & 1][u], af[g & 1][u], acc, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (REG) {   // the tile's reg k-steps, ascending: the prefetched RPF, then batches of RB
+      const int card = tcard + (lane & 31);
+      const bool brl = bias_grad && vr == V;   // this lane's row is the bias row
+      auto reg_mfma = [&](int ks, const bf16x8_t &bfr) {
+        const int i0 = 16 * ks + 8 * half;
+        const int4 e0 = *reinterpret_cast<const int4 *>(rl + i0), e1 = *reinterpret_cast<const int4 *>(rl + i0 + 4);
+        const int ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+        uint32_t byte = 0u;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) byte |= (brl ? i0 + e < rg.nreg : ev[e] == card) ? 1u << e : 0u;
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t *>(lutl + byte * (16 * LC));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr, a, acc, 0, 0, 0);
+      };
+#pragma unroll
+      for (int u = 0; u < RPF; ++u)
+        if (rks[u] >= 0) reg_mfma(rks[u], rb[u]);
+      // the rest (the bias tile: every reg k-step; tiles of popular cards) RB loads in flight at a
+      // time — the k-loop's fragment registers are free here
+      constexpr int RB = 8;
+      int k = next_k();
+      while (k >= 0) {   // (wave-uniform)
+        bf16x8_t bq[RB];
+        int kq[RB];
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+          kq[u] = k;
+          bq[u] = reg_bfrag(k);   // (clamped: an unconditional load)
+          k = next_k();
+        }
+#pragma unroll
+        for (int u = 0; u < RB; ++u)
+          if (kq[u] >= 0) reg_mfma(kq[u], bq[u]);
+      }
     }
     // With the dPre1 fragments as the MFMA's A operand and the bit fragments as its B operand (the
     // same registers), lane l holds W1 row v0 + 32 t + (l & 31) and the slice's columns
@@ -1069,19 +1186,27 @@ extern "C" int32_t cc_embed_grad_cs_tickets(int32_t V, int32_t d, int32_t R) {
 
 static int embed_grad_cs_launch(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R, int32_t ld_t,
                                 uint32_t *xt_bits, float *grad, float *bias_grad, uint32_t *tickets,
-                                const CsAdam *ad, void *stream) {
+                                const CsAdam *ad, void *stream, const CsReg *rg = nullptr) {
   int tpc, nrc;
   size_t lds;
   cs_plan(V, d, R, bias_grad != nullptr, tpc, nrc, lds, ad != nullptr);
+  if (rg) lds += (size_t)((rg->nreg + 511) & ~511) * 4;
   CC_REQUIRE(lds <= 160 * 1024 - 64, "cc_embed_grad_cs: R too large for the LDS stage");
   const dim3 grid((unsigned)(nrc * (d / 32)));
   const int xw = ((R + 63) & ~63) / 32;  // bit words per row in the product
   const bool vec = ((R + 31) / 32) % 4 == 0;  // xt rows 16-B aligned
   const CsAdam a = ad ? *ad : CsAdam{};
+  const CsReg r = rg ? *rg : CsReg{};
   hipStream_t s = as_stream(stream);
 #define CS_LAUNCH(PKV, XWMV, VECV, ADV)                                                                          \
-  hipLaunchKernelGGL((embed_grad_cs_kernel<PKV, XWMV, VECV, ADV>), grid, dim3(CS_NT), lds, s, (const bf16_t *)dpre, \
-                     V, d, R, ld_t, tpc, xt_bits, grad, bias_grad, tickets, a)
+  do {                                                                                                           \
+    if (rg)                                                                                                      \
+      hipLaunchKernelGGL((embed_grad_cs_kernel<PKV, XWMV, VECV, ADV, true>), grid, dim3(CS_NT), lds, s,          \
+                         (const bf16_t *)dpre, V, d, R, ld_t, tpc, xt_bits, grad, bias_grad, tickets, a, r);     \
+    else                                                                                                         \
+      hipLaunchKernelGGL((embed_grad_cs_kernel<PKV, XWMV, VECV, ADV>), grid, dim3(CS_NT), lds, s,                \
+                         (const bf16_t *)dpre, V, d, R, ld_t, tpc, xt_bits, grad, bias_grad, tickets, a, r);     \
+  } while (0)
 #define CS_LAUNCH2(XWMV, ADV)                                                                 \
   if (packed) {                                                                               \
     if (vec) CS_LAUNCH(true, XWMV, true, ADV); else CS_LAUNCH(true, XWMV, false, ADV);        \
@@ -1124,6 +1249,48 @@ extern "C" int cc_embed_grad_cs_adam(const void *dpre, int32_t packed, int32_t V
              "cc_embed_grad_cs_adam: ld_t must be a multiple of 64 covering R, dPre1 image 16-B aligned");
   const CsAdam ad{p, m, v, (bf16_t *)shadow, state, lr, beta1, beta2, eps};
   return embed_grad_cs_launch(dpre, packed, V, d, R, ld_t, xt_bits, nullptr, bias_grad, tickets, &ad, stream);
+}
+
+static const char *cs_reg_check(const int32_t *reg_idx, int32_t nreg, int32_t reg_k0, int32_t R, int32_t ld_t) {
+  if (!reg_idx || nreg < 1 || nreg > CS_REG_MAX) return "reg_idx non-null, nreg in 1..512";
+  if (reg_k0 < 0 || 16 * reg_k0 < R || 16 * (reg_k0 + (nreg + 15) / 16) > ld_t)
+    return "reg rows past the product's rows and inside the dPre1 image (16 reg_k0 >= R, 16 (reg_k0 + ceil(nreg / 16)) <= ld_t)";
+  return nullptr;
+}
+
+extern "C" int cc_embed_grad_cs_reg(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R, int32_t ld_t,
+                                    uint32_t *xt_bits, float *grad, float *bias_grad, uint32_t *tickets,
+                                    const int32_t *reg_idx, int32_t nreg, int32_t reg_k0, int32_t card0, void *stream) {
+  CC_REQUIRE(dpre && xt_bits && grad, "cc_embed_grad_cs_reg: null pointer");
+  CC_REQUIRE((((uintptr_t)grad | (uintptr_t)bias_grad) & 15) == 0, "cc_embed_grad_cs_reg: grad / bias_grad 16-B aligned");
+  CC_REQUIRE(d % 32 == 0 && d >= 32 && d <= 4096, "cc_embed_grad_cs_reg: d must be a multiple of 32");
+  CC_REQUIRE(V > 0 && R > 0 && R <= 2048 && card0 >= 0, "cc_embed_grad_cs_reg: V > 0, R in 1..2048, card0 >= 0");
+  CC_REQUIRE(ld_t % 64 == 0 && ld_t >= R && ((uintptr_t)dpre % 16) == 0,
+             "cc_embed_grad_cs_reg: ld_t must be a multiple of 64 covering R, dPre1 image 16-B aligned");
+  const char *e = cs_reg_check(reg_idx, nreg, reg_k0, R, ld_t);
+  CC_REQUIRE(!e, e);
+  const CsReg rg{reg_idx, nreg, reg_k0, card0};
+  return embed_grad_cs_launch(dpre, packed, V, d, R, ld_t, xt_bits, grad, bias_grad, tickets, nullptr, stream, &rg);
+}
+
+extern "C" int cc_embed_grad_cs_adam_reg(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R,
+                                         int32_t ld_t, uint32_t *xt_bits, float *bias_grad, uint32_t *tickets, float *p,
+                                         float *m, float *v, uint16_t *shadow, const int64_t *state, float lr,
+                                         float beta1, float beta2, float eps, const int32_t *reg_idx, int32_t nreg,
+                                         int32_t reg_k0, void *stream) {
+  CC_REQUIRE(dpre && xt_bits && p && m && v && shadow && state, "cc_embed_grad_cs_adam_reg: null pointer");
+  CC_REQUIRE((((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)bias_grad) & 15) == 0 &&
+                 ((uintptr_t)shadow & 7) == 0,
+             "cc_embed_grad_cs_adam_reg: p, m, v, bias_grad 16-B aligned, shadow 8-B aligned");
+  CC_REQUIRE(d % 32 == 0 && d >= 32 && d <= 4096, "cc_embed_grad_cs_adam_reg: d must be a multiple of 32");
+  CC_REQUIRE(V > 0 && R > 0 && R <= 2048, "cc_embed_grad_cs_adam_reg: V > 0, R in 1..2048");
+  CC_REQUIRE(ld_t % 64 == 0 && ld_t >= R && ((uintptr_t)dpre % 16) == 0,
+             "cc_embed_grad_cs_adam_reg: ld_t must be a multiple of 64 covering R, dPre1 image 16-B aligned");
+  const char *e = cs_reg_check(reg_idx, nreg, reg_k0, R, ld_t);
+  CC_REQUIRE(!e, e);
+  const CsAdam ad{p, m, v, (bf16_t *)shadow, state, lr, beta1, beta2, eps};
+  const CsReg rg{reg_idx, nreg, reg_k0, 0};
+  return embed_grad_cs_launch(dpre, packed, V, d, R, ld_t, xt_bits, nullptr, bias_grad, tickets, &ad, stream, &rg);
 }
 
 extern "C" int cc_embed_gather_fwd_warm(int32_t dtype, const void *table, const float *bias, int32_t V,

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(NTO) void reg_rows_kernel(cc_noise_args a) {
         a.reg_idx[pos] = j;
         a.x_idx[(int64_t)r * a.x_cap] = j;
         a.x_cnt[r] = 1;
-        if (a.xt_bits) atomicOr(&a.xt_bits[(int64_t)j * XW + (r >> 5)], 1u << (r & 31));
+        if (a.xt_bits && r < a.xt_rows) atomicOr(&a.xt_bits[(int64_t)j * XW + (r >> 5)], 1u << (r & 31));
       } else {
         atomicOr(a.status, 2);
       }
@@ -118,8 +118,8 @@ __global__ __launch_bounds__(NT) void adam_noise_kernel(cc_adam::Args ad, cc_noi
 }  // namespace
 
 static int noise_check(const cc_noise_args *a, size_t &lds) {
-  CC_REQUIRE(a != nullptr && a->xt_rows >= a->B + (a->with_reg ? a->B : 0),
-             "cc_noise_fwd: xt_rows must cover the rows that set xt bits");
+  CC_REQUIRE(a != nullptr && a->xt_rows >= a->B,
+             "cc_noise_fwd: xt_rows must cover the cube rows (reg rows past xt_rows set no xt bit)");
   CC_REQUIRE(a != nullptr, "cc_noise_fwd: null args");
   CC_REQUIRE(a->V > 0 && a->B > 0 && a->x_cap > 0, "cc_noise_fwd: bad V/B/x_cap");
   CC_REQUIRE(a->cube_ptr && a->cube_idx && a->perm && a->cdf && a->neg_sampler && a->state,
@@ -148,7 +148,7 @@ extern "C" int cc_reg_rows(const cc_noise_args *a, void *stream) {
   CC_REQUIRE(a->reg_lo >= 0 && a->reg_lo < a->reg_hi && a->reg_hi <= a->V, "cc_reg_rows: shard [lo, hi)");
   CC_REQUIRE(a->cdf && a->state && a->x_cnt && a->x_idx && a->reg_idx && a->status,
              "cc_reg_rows: null pointer");
-  CC_REQUIRE(!a->xt_bits || a->xt_rows >= a->B + a->reg_cap, "cc_reg_rows: xt_rows must cover B + reg_cap");
+  CC_REQUIRE(!a->xt_bits || a->xt_rows >= a->B, "cc_reg_rows: xt_rows must cover the cube rows");
   hipLaunchKernelGGL(reg_rows_kernel, dim3(1), dim3(NTO), 0, as_stream(stream), *a);
   CC_LAUNCH_CHECK("reg_rows_kernel");
   return CC_OK;

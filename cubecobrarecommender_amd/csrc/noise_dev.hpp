@@ -217,7 +217,8 @@ __device__ __forceinline__ void noise_block(const cc_noise_args &a, uint32_t *sm
     const int r = a.B + b;
     a.x_idx[(int64_t)r * a.x_cap] = j;
     a.x_cnt[r] = 1;
-    if (a.xt_bits) atomicOr(&a.xt_bits[(int64_t)j * XW + (r >> 5)], 1u << (r & 31));
+    // (xt_rows == B: the W1 gradient takes the reg rows by index, cc_embed_grad_cs_reg — no bit)
+    if (a.xt_bits && r < a.xt_rows) atomicOr(&a.xt_bits[(int64_t)j * XW + (r >> 5)], 1u << (r & 31));
     s_k = j;
   }
   if (a.with_reg && a.x_bits) {  // the reg row {j} as a bitmask

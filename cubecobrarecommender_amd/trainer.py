@@ -68,6 +68,9 @@ class TrainConfig:
     metrics: bool = False          # Keras metrics=['accuracy'] (train.py:87): each step counts both
     #                                outputs' categorical accuracy (TF 2.5's shape rule) on the device from
     #                                logits recomputed for the purpose (metrics.hip; take_metrics() per epoch)
+    reg_by_index: bool = True      # sampled regulariser, column-slice W1 gradient: the reg rows (one card each)
+    #                                enter the W1 product by index (cc_embed_grad_cs_reg: only the k-steps
+    #                                that touch a tile), not as bits of a 2B-row bit matrix; bit-identical
     reg_mode: str = 'sampled'      # 'sampled': B reg rows per step drawn ∝ neg_sampler (generator.py:47-51);
     #                                'full': all |V| identity rows every step, KL(M~, D2(E(I))) as the
     #                                reference README states the objective (README.md:27)
@@ -243,7 +246,16 @@ class Trainer:
             self.reg_rows = (int(bnd[cfg.rank]), int(bnd[cfg.rank + 1]))
             self.Breg = owner_capacity(mass, B, W, align=ralign)
         self.R = B + self.Breg
-        self.xt_rows = B if self.full_reg else self.R      # rows of the MFMA W1-gradient product
+        # the sampled reg rows by index in the W1 gradient (cc_embed_grad_cs_reg; its column-slice
+        # path runs exactly when the fused towers and the MFMA W1 gradient do: bf16 / fp8, d % 128)
+        # (not with f_in_tower: the next step's F, drawn in the tower backward launch, rewrites the reg
+        # cards before the W1 gradient reads them; the bit matrix is not rewritten by F)
+        self.reg_by_index = bool(cfg.reg_by_index and self.use_reg and not self.full_reg
+                                 and cfg.dtype in ('bf16', 'fp8') and cfg.fused_tower and B % 32 == 0
+                                 and d <= 1024 and d % 128 == 0 and 0 < self.Breg <= 512 and not cfg.f_in_tower)
+        # rows of the MFMA W1-gradient product (its bit matrix): the cubes only when the regulariser
+        # rows enter by index (full mode: cc_embed_identity_add; sampled: cc_embed_grad_cs_reg)
+        self.xt_rows = B if (self.full_reg or self.reg_by_index) else self.R
         self.reg_weight = 1.0
         if self.use_reg and data.reg_rows != self.reg_rows:
             if data.reg_rows != (0, V):
@@ -367,6 +379,7 @@ class Trainer:
                                            device=self.dev, dtype=torch.int32)
                                if (self.gpre1p is not None or self.embed_mfma)
                                else None)
+            assert not self.reg_by_index or self.eg_tickets is not None, 'reg_by_index needs the column-slice W1 gradient'
             slab = int(L.lib().cc_tower_slab_elems(d))
             self.slab = torch.zeros((R // 32) * slab, **f32)
             # D2 output layer fused (logits twice -> softmax -> KL -> dZ -> dWo, csrc/decreg.hip): bf16,
@@ -1195,10 +1208,16 @@ class Trainer:
         if self.eg_tickets is not None and self.fuse_w1:   # column slices + TF Adam on W1 in the epilogue
             cfg_ = self.cfg
             src, pk = (self.gpre1p, 1) if self.gpre1p is not None else (self.gPre1T, 0)
-            L.call('cc_embed_grad_cs_adam', L.ptr(src), pk, V, d, XR, self.RP, L.ptr(self.xt_bits),
-                   self.gp('encoder/encoded_1/bias'), self._eg_tk(), L.ptr(self.params), L.ptr(self.m),
-                   L.ptr(self.v), L.ptr(self.shadow), L.ptr(self.state), cfg_.lr, cfg_.beta1, cfg_.beta2,
-                   cfg_.eps, s)
+            if self.reg_by_index:   # + the reg rows by index (rows B .. of the dPre1 image)
+                L.call('cc_embed_grad_cs_adam_reg', L.ptr(src), pk, V, d, XR, self.RP, L.ptr(self.xt_bits),
+                       self.gp('encoder/encoded_1/bias'), self._eg_tk(), L.ptr(self.params), L.ptr(self.m),
+                       L.ptr(self.v), L.ptr(self.shadow), L.ptr(self.state), cfg_.lr, cfg_.beta1, cfg_.beta2,
+                       cfg_.eps, L.ptr(self.reg_idx), self.Breg, cfg.batch_size // 16, s)
+            else:
+                L.call('cc_embed_grad_cs_adam', L.ptr(src), pk, V, d, XR, self.RP, L.ptr(self.xt_bits),
+                       self.gp('encoder/encoded_1/bias'), self._eg_tk(), L.ptr(self.params), L.ptr(self.m),
+                       L.ptr(self.v), L.ptr(self.shadow), L.ptr(self.state), cfg_.lr, cfg_.beta1, cfg_.beta2,
+                       cfg_.eps, s)
         elif self.eg_tickets is not None:   # column slices (cc_embed_grad_cs), from the packed image or dPre1^T
             src, pk = (self.gpre1p, 1) if self.gpre1p is not None else (self.gPre1T, 0)
             # data parallel: W1's row chunks one launch each (the bias row with the last), each
@@ -1206,8 +1225,14 @@ class Trainer:
             # every W1 tile is computed as in the one-launch product (bit-identical)
             gw, gb = self.layout.offset('encoder/encoded_1/kernel'), self.gp('encoder/encoded_1/bias')
             for i, (r0, r1) in enumerate(chunks):
-                L.call('cc_embed_grad_cs', L.ptr(src), pk, r1 - r0, d, XR, self.RP, L.ptr(self.xt_bits[r0:]),
-                       L.ptr(self.grads[gw + r0 * d:]), gb if i == len(chunks) - 1 else None, self._eg_tk(), s)
+                gbi = gb if i == len(chunks) - 1 else None
+                if self.reg_by_index:
+                    L.call('cc_embed_grad_cs_reg', L.ptr(src), pk, r1 - r0, d, XR, self.RP, L.ptr(self.xt_bits[r0:]),
+                           L.ptr(self.grads[gw + r0 * d:]), gbi, self._eg_tk(), L.ptr(self.reg_idx), self.Breg,
+                           cfg.batch_size // 16, r0, s)
+                else:
+                    L.call('cc_embed_grad_cs', L.ptr(src), pk, r1 - r0, d, XR, self.RP, L.ptr(self.xt_bits[r0:]),
+                           L.ptr(self.grads[gw + r0 * d:]), gbi, self._eg_tk(), s)
                 if i + 1 < len(chunks):
                     self._fire_bucket(f'w1_{i}')
         elif self.gpre1p is not None:

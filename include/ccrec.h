@@ -229,6 +229,22 @@ int cc_embed_grad_cs_adam(const void *dpre, int32_t packed, int32_t V, int32_t d
                           uint32_t *xt_bits, float *bias_grad, uint32_t *tickets, float *p, float *m, float *v,
                           uint16_t *shadow, const int64_t *state, float lr, float beta1, float beta2, float eps,
                           void *stream);
+/* The same two products with the sampled regulariser's identity rows taken by index (reference:
+ * generator.py:47-61, x_reg = the identity rows of the reg draws; train.py:99-102 fits on them): the
+ * bit matrix holds the first R (cube) rows only and the dPre1 image holds the nreg reg rows as its
+ * rows 16 reg_k0 .. (reg_k0 >= R / 16), row 16 reg_k0 + i being the one-card row {reg_idx[i]}
+ * (reg_idx[i] < 0: a padding row, in the bias row's sum only).  Each 32-row tile adds the reg
+ * k-steps whose A fragment is not all zero for it (every one for the bias row), ascending, after
+ * the cube k-steps: bit-identical to the same products over R + nreg rows with the reg rows' bits in
+ * xt_bits.  nreg <= 512; card0: the card of W1 row 0 (a row chunk's first row; 0 for the Adam form). */
+int cc_embed_grad_cs_reg(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R, int32_t ld_t,
+                         uint32_t *xt_bits, float *grad, float *bias_grad, uint32_t *tickets,
+                         const int32_t *reg_idx, int32_t nreg, int32_t reg_k0, int32_t card0, void *stream);
+int cc_embed_grad_cs_adam_reg(const void *dpre, int32_t packed, int32_t V, int32_t d, int32_t R, int32_t ld_t,
+                              uint32_t *xt_bits, float *bias_grad, uint32_t *tickets, float *p, float *m,
+                              float *v, uint16_t *shadow, const int64_t *state, float lr, float beta1,
+                              float beta2, float eps, const int32_t *reg_idx, int32_t nreg, int32_t reg_k0,
+                              void *stream);
 /* Full-mode regulariser (all |V| one-hot identity rows, README.md:27 KL(M, D2(E(I)))): the rows'
  * W1 gradient is dPre1 itself — grad[lo + r] += round(dpre[r]) for r < n and, with bias_grad,
  * bias_grad += sum_r round(dpre[r]) in a fixed order; round = bf16 RNE for dtype CC_BF16 (the

@@ -616,3 +616,47 @@ def test_sigmoid_cat_accuracy_tie_rules():
            L.stream_ptr())
     torch.cuda.synchronize()
     assert int(cnt[0]) == 3, cnt          # rows 0, 2, 3 correct; row 1 not
+
+
+@pytest.mark.parametrize('d,dtype', [(256, 'bf16'), (512, 'bf16'), (1024, 'fp8')])
+@pytest.mark.parametrize('fused', [True, False])
+def test_reg_rows_by_index_bit_identical(d, dtype, fused):
+    """The sampled regulariser's one-card rows by index in the W1 gradient (cc_embed_grad_cs_reg /
+    _adam_reg: only the reg k-steps that touch a tile, from the rows' card list) == the same step with
+    those rows as bits of a B + Breg-row bit matrix (TrainConfig(reg_by_index=False)): parameters,
+    moments, gradients and losses bit for bit over eager steps and graph replays.  fused: W1's Adam in
+    the gradient kernel with F prefetched (bench.py's configuration); else the gradient stored (F's
+    direct xt atomics, which skip the reg rows)."""
+    V, B, C = 2500, 128, 512
+    lists, Mt, ns = problem(17, C, V, (20, 40, 80))
+    P = model_ref.init_params(V, d, seed=17, bias_std=0.01)
+    out = []
+    for by_index in (True, False):
+        cfg = TrainConfig(V=V, d=d, batch_size=B, reg=0.1, dtype=dtype, seed=17, reg_by_index=by_index,
+                          fuse_w1_adam=fused, prefetch_noise=fused)
+        tr = Trainer(cfg, DeviceDataset(lists, V, y_mtx=Mt.astype(np.float32), neg_sampler=ns),
+                     params_flat=Layout(V, d).pack(P))
+        assert tr.reg_by_index == by_index and tr.xt_rows == (B if by_index else 2 * B)
+        assert tr.fuse_w1 == fused
+        tr.set_epoch_permutation(np.random.default_rng(17).permutation(C).astype(np.int32))
+        losses = []
+        for _ in range(2):
+            tr.step()
+            tr.flush()
+            torch.cuda.synchronize()
+            losses.append(tr.losses())
+        g = tr.grads.cpu().numpy().copy()
+        tr.capture()
+        for _ in range(3):
+            tr.step()
+        tr.flush()
+        torch.cuda.synchronize()
+        losses.append(tr.losses())
+        tr.check_status()
+        out.append((tr.params.cpu().numpy(), tr.m.cpu().numpy(), tr.v.cpu().numpy(), g, losses))
+    (p1, m1, v1, g1, l1), (p0, m0, v0, g0, l0) = out
+    assert l1 == l0, (l1, l0)
+    np.testing.assert_array_equal(g1, g0)
+    np.testing.assert_array_equal(p1, p0)
+    np.testing.assert_array_equal(m1, m0)
+    np.testing.assert_array_equal(v1, v0)
