@@ -9,11 +9,7 @@ LIB_PATH = os.environ.get('CCREC_LIB') or os.path.join(_HERE, 'libccrec_hip.so')
 CC_F32, CC_BF16, CC_MX8 = 0, 1, 2
 CC_EPI_STORE, CC_EPI_BCE, CC_EPI_MASK, CC_EPI_SPLITK = 0, 1, 2, 3
 CC_NUM_TENSORS = 24
-CC_KL_LDS_TARGETS = 1          # cc_dec_kl_args.flags bit 0
-CC_KL_DWO_PRODUCER_WAVES = 2   # ... bit 1
-CC_KL_SHORT_STORES = 4         # ... bit 2
-CC_KL_WIDE_TARGETS = 8         # ... bit 3
-CC_KL_DWO_NARROW = 16          # ... bit 4 (dWo's rounding differs: one pass over all rows)
+CC_KL_DWO_NARROW = 16          # cc_dec_kl_args.flags (dWo's rounding differs: one pass over all rows)
 
 
 class CCError(RuntimeError):

@@ -69,6 +69,7 @@ constexpr float LN_PMIN = -16.11809565095832f;  // ln(1e-7)
 
 typedef __attribute__((ext_vector_type(4))) uint32_t v4u;
 typedef __attribute__((address_space(3))) void lds_void;
+typedef short v4s __attribute__((ext_vector_type(4)));
 
 struct KlP {
   int d, V, rows, ldt, row0, nsl;
@@ -459,8 +460,7 @@ template <int NB>
 struct MainSmem {
   bf16_t Zt[NB * TR];       // dZ^T tile [NB][TR] (swizzled); staged M~ (kl_slice's MS mode)
   float4 rs[TR];            // row stats of the tile
-  int32_t card[2][TR];      // M~ row byte offset of the tile's rows (0x80000000: padding row) in [0];
-                            // MS: the raw card of tile t's rows in [t & 1]
+  int32_t card[TR];         // M~ row byte offset of the tile's rows (0x80000000: padding row)
   float red_cs[NTH / 64][NB];
   double red_loss[NTH / 64];
   int lastflag;
@@ -476,12 +476,11 @@ __device__ __forceinline__ int32_t card_off(int card, int V) {
   return card >= 0 ? (int32_t)((uint32_t)card * (uint32_t)V * 4u) : (int32_t)0x80000000u;
 }
 
-// MS's LDS-DMAs are written as inline asm: the compiler's wait insertion treats a pending
-// LDS-DMA as a possible writer of every later LDS read (no alias information here) and put a
-// vmcnt(0) before the logits' Wo-slice reads and the epilogue's row-stat reads, draining the
-// very DMAs meant to run under them.  Invisible to it, they only make its own counted waits
+// LDS-DMAs are written as inline asm (kl_dwo2_kernel): the compiler's wait insertion treats a
+// pending LDS-DMA as a possible writer of every later LDS read (no alias information here) and puts
+// a vmcnt(0) before unrelated LDS reads, draining the very DMAs meant to run under them.  Invisible to it, they only make its own counted waits
 // stricter than needed (it counts fewer younger accesses than there are); the slots' own waits
-// are the explicit ones in kl_slice.
+// are the explicit ones in the kernel.
 typedef __attribute__((ext_vector_type(4))) int32_t v4i;
 __device__ __forceinline__ v4i sgpr_rsrc(const void *base, uint32_t bytes) {
   const uint64_t a = (uint64_t)base;
@@ -504,17 +503,7 @@ __device__ __forceinline__ void dma_asm(const v4i &rs, uint32_t voff, uint32_t s
     asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dword %0, %1, %3 offen lds" ::"v"(voff), "s"(rs), "s"(lds), "s"(soff) : "memory");
 }
 
-// MS: the DMA of M~ [32 rows][32 columns] (column tile j of a wave's row block) into the wave's LDS
-// slot, row-major: instruction i moves rows 8i .. 8i + 7, lane L 16 B of row 8i + (L >> 3) at
-// columns 4 (L & 7) .. (sof: the rows' byte offsets + the lane's column chunk)
-template <int CPOL>
-__device__ __forceinline__ void ms_dma(const v4i &rs, const uint32_t (&sof)[4], int j, const float *slot) {
-  const uint32_t a = lds_addr(slot);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) dma_asm<16, CPOL>(rs, sof[i], 128u * j, a + 1024u * i);
-}
-
-template <int D, bool FIX, int CPOL = 0, bool DW = true, bool MS = false, bool WS = false, bool WM = false>
+template <int D, bool FIX, int CPOL = 0, bool DW = true, bool WS = false>
 __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt, MainSmem<kl_nb<D>()> &sm) {
   constexpr int NB = kl_nb<D>(), NJ = NB / 32;
   constexpr int CHB = TR / 8;
@@ -543,23 +532,12 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   const __amdgpu_buffer_rsrc_t dz_rs =
       __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)p.rows * (uint32_t)V * 2u, 0x00020000);
   const float scale = p.scale;
-  const v4i mt_rs4 = sgpr_rsrc(p.Mt, p.mt_bytes);
   constexpr int ND2 = (D + 255) / 256;   // phase 2's d tiles of wave w: 32w .. (and 32(w + 8) .. at d = 512)
   // PF (the main pass with dWo done elsewhere: many row tiles, nothing of phase 2 live): the next
   // row block's A fragments load right after this block's logits MFMAs, so their L2 / MALL round
   // trip runs under this block's epilogue instead of heading the next logits phase (tools/micro/
   // kl_probe_full.hip: ~5 of the ~12 us per 256-row pass were logits waiting on their fragments)
   constexpr bool PF = !FIX && !DW && D <= 256;
-  // MS (PF, opt-in CC_KL_LDS_TARGETS; the launcher checks |V| % 4 == 0 and the offsets' ranges):
-  // M~ staged through the LDS the dZ^T tile would use (free without phase 2): each wave DMAs its
-  // next row block's M~ into its own NJ slots [32 rows][32 columns], slot j right after this pass's
-  // epilogue has read it, so a slot's HBM round trip runs under the rest of the epilogue and the
-  // next logits instead of being issued at the head of the pass it feeds.  The slots hold no
-  // registers, which pays for the full 16-fragment ring: the logits no longer refill A fragments
-  // behind M~.  Measured (tools/micro/kl_probe_full.hip, r05o / r05r): the logits phases halve
-  // (295 -> 138 us over block 0's tiles) but the epilogues wait on the slots longer than that saves
-  // (the four launches 1,583 -> 1,824 us against the register path with 16-B stores) — off.
-  constexpr bool MSX = MS && PF;
   // WSX (PF with M~ in registers; the launcher checks |V| % 8 == 0 and the offsets' range): dZ leaves
   // through the free dZ^T LDS as 16-B row stores.  The accumulator layout gives a lane one column
   // of 16 rows, so a direct store writes 2 B per lane — 48 buffer_store_short per lane and pass,
@@ -567,79 +545,20 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   // Instead adjacent lanes pair their bf16 values by one DPP swap into row-major dwords, the wave
   // writes its [32][96] tile to a private LDS image (208-B pitch: no bank conflicts between the
   // half-waves' rows), reads it back as 16-B row chunks and stores 6 x 16 B per lane.
-  constexpr bool WSX = WS && PF && !MSX;
+  constexpr bool WSX = WS && PF;
   constexpr int WS_PITCH = 52;   // dwords per image row (96 bf16 + 8 pad)
   uint32_t *const zimg = reinterpret_cast<uint32_t *>(sm.Zt) + w * (32 * WS_PITCH);
-  // WMX (opt-in CC_KL_WIDE_TARGETS, with WSX; M~ 16-B aligned): the pass's M~ loaded 16 B per lane
-  // (4 columns of one row; 12 loads per lane instead of 48 4-B ones) and turned into the
-  // accumulator layout per column tile through a wave-private [32][40]-float LDS stage next to the
-  // dZ image.  Bit-identical but slower (the four launches 1,548-1,586 -> 1,610-1,654 us, r05v):
-  // unlike the stores, the 4-B loads were not issue-bound enough to pay for the stage round trip
-  constexpr bool WMX = WM && WSX;
-  constexpr int WM_PITCH = 40;   // floats per stage row (32 + 8: the half-waves' rows on disjoint banks)
-  float *const mstage = reinterpret_cast<float *>(reinterpret_cast<uint32_t *>(sm.Zt) + 8 * 32 * WS_PITCH) + w * (32 * WM_PITCH);
-  static_assert(!WSX || 8 * 32 * WS_PITCH * 4 + (WM ? 8 * 32 * WM_PITCH * 4 : 0) <= (int)sizeof(sm.Zt),
-                "WS / WM: the images and stages fit the dZ^T tile");
+  static_assert(!WSX || 8 * 32 * WS_PITCH * 4 <= (int)sizeof(sm.Zt), "WS: the images fit the dZ^T tile");
   // all A fragments first in the memory queue, then M~ (d = 512: a ring of 16; PF: the next block's
   // first 8 under the epilogue, the other 8 refilled during the MFMAs — 16 would spill)
-  LFrag<D, (PF && !MSX) ? 8 : (D / 16 < 16 ? D / 16 : 16)> lf;
+  LFrag<D, PF ? 8 : (D / 16 < 16 ? D / 16 : 16)> lf;
   bool lf_ready = false;
-  float *const stg = reinterpret_cast<float *>(sm.Zt) + w * (32 * NB);
-  static_assert(!MSX || NB * TR * 2 == 8 * 32 * NB * 4, "MS: 8 waves' slots fill the Zt tile");
-  // MSX: the slots' waits.  An LDS-DMA is counted by vmcnt like any other vector-memory access.
-  // Slot j's DMA is issued after that slot's 16 dZ stores, so between it (the previous pass) and
-  // the wait for it lie, in issue order: the later slots' (NJ - 1 - j) x (stores 16 + DMA 4), the
-  // part_d store (1); this pass's A prefetch (nkk, when it has a next pass) and its earlier
-  // slots' j x (stores 16 + DMA 4 when it has a next pass).  The counts below are the minimum of
-  // those over j — lower bounds of the younger accesses — so a wait never releases before its
-  // slot has landed.  (Stores before the DMA: the compiler's own wait for the A prefetch, which
-  // sees only the 48 + 1 stores behind it, then releases on the oldest stores, not on a DMA.)
-  constexpr int NKK = D / 16;
-  constexpr int MS_CNT_N = 20 * (NJ - 1) + NKK;   // this pass has a next pass (part_d not counted)
-  constexpr int MS_CNT_L = 16 * (NJ - 1);         // the wave's last pass
-  static_assert(!MSX || MS_CNT_N <= 63, "vmcnt's range");
-  // MSX: no global load may wait behind the slots' DMAs (a wait on a load also waits on every
-  // older access), so the next tile's row stats {m + ln s, S} and raw cards are DMA'd too, at the
-  // head of this tile's pass 0, into the other half of double-buffered LDS (rs2, card); the
-  // slots' waits of pass 1 cover them (older) and the tile-top barrier publishes them.  Slice 0's
-  // sum of t ln t over the live rows (rowstat.w) is then added after the tile loop.
-  float2(*const rs2)[TR] = reinterpret_cast<float2(*)[TR]>(sm.rs);
-  static_assert(sizeof(sm.rs) == 2 * TR * sizeof(float2), "rs2 overlays rs");
-  const v4i st_rs = sgpr_rsrc(p.rowst2, (uint32_t)p.rows * 8u), ri_rs = sgpr_rsrc(p.reg_idx, (uint32_t)p.rows * 4u);
 
-  if constexpr (MSX) {   // the first tile: staged by the threads (published by the tile-top barrier)
-    for (int i = tid; i < min(TR, p.rows); i += NTH) {
-      rs2[0][i] = p.rowst2[i];
-      sm.card[0][i] = p.reg_idx[i];
-    }
-    // the wave's first row block (tile 0, rows 32w ..): A fragments and slots, all landed before
-    // the loop (a wait the compiler sees, so its state entering the loop holds no pending
-    // fragment loads to merge with the loop's own counted waits)
-    if (w * 32 < min(TR, p.rows)) {
-      logits_load(p, (p.row0 + w * 32) / 32, lf);
-      const uint32_t c4 = 4u * (uint32_t)(n0 + 4 * (lane & 7));
-      uint32_t s0[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = w * 32 + (lane >> 3) + 8 * i;
-        s0[i] = (uint32_t)card_off(row < p.rows ? p.reg_idx[row] : -1, V) + c4;
-      }
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) ms_dma<CPOL>(mt_rs4, s0, j, stg + j * 1024);
-      lf_ready = true;
-    }
-    asm volatile("" ::: "memory");   // (the loads may not sink below the wait)
-    __builtin_amdgcn_s_waitcnt(0);
-  }
 
   for (int t0 = 0; t0 < p.rows; t0 += TR) {
     const int nt = min(TR, p.rows - t0);
-    const int cur = MSX ? (t0 / TR) & 1 : 0;
-    const int32_t *const cardc = sm.card[cur];
-    // the row offset of tile row i (MSX: from the raw card)
-    auto rowoff = [&](int i) -> uint32_t { return MSX ? (uint32_t)card_off(cardc[i], V) : (uint32_t)cardc[i]; };
-    lds_barrier();  // previous tile's phase 2 done with Zt / rs (MSX: this tile's staged stats landed)
-    if constexpr (!MSX)
+    auto rowoff = [&](int i) -> uint32_t { return (uint32_t)sm.card[i]; };   // tile row i's M~ offset
+    lds_barrier();  // previous tile's phase 2 done with Zt / rs
     for (int i = tid; i < nt; i += NTH) {
       float4 st = p.rowstat[t0 + i];
       if constexpr (FIX) {  // .z <- delta of the row: the sum of its slices' partials, in order
@@ -651,7 +570,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       sm.rs[i] = st;
       const int card = p.reg_idx[t0 + i];
       if (!FIX && sl == 0 && card >= 0) klc += st.w;
-      sm.card[0][i] = card_off(card, V);
+      sm.card[i] = card_off(card, V);
     }
     lds_barrier();
     KL_PROBE(1);
@@ -669,7 +588,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
       for (int r = 0; r < 16; ++r) roff[r] = rowoff(rb + acc_row(r, lane));
       uint32_t zrow = (uint32_t)((t0 + rb + 4 * half) * V + n0 + (lane & 31));
       asm volatile("" : "+v"(zrow));  // per-pass base of the dZ stores (no hoisted 64-bit addresses)
-      if (!MSX && (!PF || !lf_ready)) logits_load(p, (p.row0 + t0 + rb) / 32, lf);
+      if (!PF || !lf_ready) logits_load(p, (p.row0 + t0 + rb) / 32, lf);
       // PF: this wave's next row block — pass 1 of this tile, or pass 0 of the next (wave-uniform)
       int t1 = 0, rb1 = 0;
       bool nxt = false;
@@ -679,41 +598,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
         nxt = t1 < p.rows && rb1 < min(TR, p.rows - t1);
       }
       float tv[NJ][16];
-      v4u wv[NJ][4];        // WMX: row (lane >> 3) + 8 u, columns 32 j + 4 (lane & 7) .. of the pass
-      uint32_t sof[4];      // MSX: the next block's DMA rows
-      if constexpr (MSX) {
-        const uint32_t c4 = 4u * (uint32_t)(n0 + 4 * (lane & 7));
-        if (ps == 0 && t0 + TR < p.rows) {
-          // the next tile's stats (waves 0-3) and cards (4, 5), read after the tile-top barrier;
-          // and each wave's own next-tile rows 32w .. 32w + 63 again (identical values), read by
-          // this wave alone before that barrier (below: its own vmcnt covers them)
-          const int nx = cur ^ 1;
-          int lane = threadIdx.x & 63;
-          asm volatile("" : "+v"(lane));   // per tile: no per-lane offsets held across the loop
-          if (w < 4)
-            dma_asm<16, 0>(st_rs, 16u * lane, (uint32_t)(t0 + TR + 128 * w) * 8u, lds_addr(&rs2[nx][128 * w]));
-          else if (w < 6)
-            dma_asm<16, 0>(ri_rs, 16u * lane, (uint32_t)(t0 + TR + 256 * (w - 4)) * 4u, lds_addr(&sm.card[nx][256 * (w - 4)]));
-          dma_asm<4, 0>(ri_rs, 4u * lane, (uint32_t)(t0 + TR + 32 * w) * 4u, lds_addr(&sm.card[nx][32 * w]));
-        }
-        if (nxt) {
-          const int32_t *cn = sm.card[(t1 / TR) & 1];
-          // the next tile's rows (this wave's own DMA of pass 0; younger since: that pass's A
-          // prefetch nkk, stores 16 NJ, slot DMAs 4 NJ, part_d 1 — more than 63)
-          if (t1 != t0) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
-#pragma unroll
-          for (int i = 0; i < 4; ++i) sof[i] = (uint32_t)card_off(cn[rb1 + (lane >> 3) + 8 * i], V) + c4;
-        }
-      } else if constexpr (WMX) {
-        uint32_t wro[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) wro[u] = rowoff(rb + (lane >> 3) + 8 * u) + 4u * (uint32_t)(n0 + 4 * (lane & 7));
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            wv[j][u] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(mt_rs, wro[u] + 128u * j, 0, CPOL));
-      } else if constexpr (!FIX) {
+      if constexpr (!FIX) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const uint32_t gc4 = 4u * (uint32_t)(n0 + j * 32 + (lane & 31));
@@ -742,37 +627,16 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int col = j * 32 + (lane & 31);
-        if constexpr (MSX) {
-          if (nxt)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MS_CNT_N) : "memory");
-          else
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MS_CNT_L) : "memory");
-          const float *slot = stg + j * 1024;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) tv[j][r] = slot[acc_row(r, lane) * 32 + (lane & 31)];
-        }
-        if constexpr (WMX) {   // column tile j's M~: rows x 16 B -> the stage -> the accumulator layout
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            *reinterpret_cast<v4u *>(mstage + ((lane >> 3) + 8 * u) * WM_PITCH + 4 * (lane & 7)) = wv[j][u];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) tv[j][r] = mstage[acc_row(r, lane) * WM_PITCH + (lane & 31)];
-        }
         uint16_t tt[16];
         // row stats re-read per column tile (an opaque base): held across the three tiles they
         // cost 64 VGPRs, LDS has the bandwidth
         int rsofs = 0;
         asm volatile("" : "+v"(rsofs));
         const float4 *rsp = sm.rs + rsofs;
-        const float2 *rsp2 = rs2[cur] + rsofs;
         // {m + ln s, S (FIX: delta)} of tile row i
         auto rstat = [&](int i) -> float2 {
-          if constexpr (MSX) {
-            return rsp2[i];
-          } else {
-            const float4 q = rsp[i];
-            return make_float2(q.x, q.z);
-          }
+          const float4 q = rsp[i];
+          return make_float2(q.x, q.z);
         };
         // the common case — all rows real, all 32 columns inside V: no per-element masks, the
         // clip of q folded into one med3 (ln clip(p, 1e-7, 1) = med3(ln p, ln 1e-7, 0)), the
@@ -805,7 +669,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
             tt[r] = zb;
             cs[j] += dzf;  // the bias gradient sums the fp32 dz
             // the lane part of the offset in a VGPR, the row part (r) as the scalar soffset
-            if constexpr (!MSX && !WSX && !KL_DIAG_NOSTORE)
+            if constexpr (!WSX && !KL_DIAG_NOSTORE)
               __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, 2u * (zrow + (uint32_t)(j * 32)),
                                                     2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), CPOL);
             if (r & 1) ws_pair(r, tt[r - 1], zb);
@@ -843,7 +707,7 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
               tt[r] = zb;
               cs[j] += dz;
             }
-            if (!MSX && !WSX && valid[j]) __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, CPOL);
+            if (!WSX && valid[j]) __builtin_amdgcn_raw_buffer_store_b16(zb, dz_rs, zoff, 0, CPOL);
             if constexpr (!FIX)
               if (r & 1) ws_pair(r, tt[r - 1], zb);
           }
@@ -853,19 +717,6 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
           for (int g = 0; g < 4; ++g)
             *reinterpret_cast<uint2 *>(sm.Zt + sw_off(col, rb + 8 * g + 4 * half, CHB)) =
                 *reinterpret_cast<const uint2 *>(&tt[4 * g]);
-        }
-        if constexpr (MSX) {
-          // the tile's 16 dZ stores after the fast / slow branches merge: in either they would sit
-          // in blocks the compiler's flow graph can bypass (infeasibly), and its counted waits then
-          // assume no store behind the A prefetch and drain the slots' DMAs before the logits
-          const uint32_t zl = valid[j] ? 2u * (zrow + (uint32_t)(j * 32)) : 0x80000000u;   // past V: dropped
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            __builtin_amdgcn_raw_buffer_store_b16(tt[r], dz_rs, zl, 2u * (uint32_t)(((r & 3) + 8 * (r >> 2)) * V), CPOL);
-          if (nxt) {   // slot j is free (read above): the next block's column tile j
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            ms_dma<CPOL>(mt_rs4, sof, j, stg + j * 1024);
-          }
         }
       }
       deadp |= mn < PMIN;
@@ -895,12 +746,10 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
             float tj[16];
             const uint32_t gc4 = 4u * (uint32_t)(n0 + j * 32 + (lane & 31));
 #pragma unroll
-            for (int r = 0; r < 16; ++r)   // MSX / WMX: M~ not held in registers: from memory
-              tj[r] = MSX || WMX ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mt_rs, roff[r] + gc4, 0, CPOL))
-                                 : tv[j][r];
+            for (int r = 0; r < 16; ++r) tj[r] = tv[j][r];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const float st_x = MSX ? rs2[cur][rb + acc_row(r, lane)].x : sm.rs[rb + acc_row(r, lane)].x;
+              const float st_x = sm.rs[rb + acc_row(r, lane)].x;
               const float pr = __builtin_amdgcn_exp2f((acc[j][r] - st_x) * LOG2E);
               const bool live_row = roff[r] < 0x80000000u && valid[j];
               dl[r] += live_row && !(pr >= PMIN) ? __builtin_amdgcn_fmed3f(tj[r], PMIN, 1.f) : 0.f;
@@ -987,11 +836,6 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
     }
   }
 
-  if constexpr (MSX) {   // slice 0: each live row's sum_j t ln t, once (see rs2 above)
-    if (sl == 0)
-      for (int i = tid; i < p.rows; i += NTH)
-        if (p.reg_idx[i] >= 0) klc += p.rowstat[i].w;
-  }
   KL_PROBE(7);
   // ---- epilogue: dbo, loss partial, the fix flag
 #pragma unroll
@@ -1051,11 +895,309 @@ __device__ __forceinline__ void kl_slice(const KlP &p, const int sl, bf16_t *Wt,
   }
 }
 
-template <int D, int CPOL, bool DW, bool MS = false, bool WS = false, bool WM = false>
+template <int D, int CPOL, bool DW, bool WS = false>
 __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
   __shared__ __attribute__((aligned(16))) bf16_t Wt[kl_nb<D>() * D];
   __shared__ __attribute__((aligned(16))) MainSmem<kl_nb<D>()> sm;
-  kl_slice<D, false, CPOL, DW, MS, WS, WM>(p, blockIdx.x, Wt, sm);
+  kl_slice<D, false, CPOL, DW, WS>(p, blockIdx.x, Wt, sm);
+}
+
+// ---------------------------------------------------------------- main, operands swapped (full mode)
+// The full-mode main pass (many row tiles, dWo by its own kernel; d = 256, |V| % 8 == 0) with the
+// MFMA operands swapped as in the stats kernels (Wo slice = A, D3 rows = B): a lane holds ONE row
+// and, per 32-column tile, 4 runs of 4 consecutive columns.  Against kl_slice's layout (a lane = one
+// column of 16 rows): M~ arrives as 12 16-B loads per lane and pass instead of 48 4-B ones; dZ leaves
+// as 6 16-B row stores after one permlane32 swap per dword pair instead of a DPP pairing + LDS image
+// round trip; the row statistics are one LDS read per pass instead of one per element; the bias
+// starts the accumulators by one MFMA against a ones fragment (its exact three-bf16 split, as the D1
+// kernel); the bias gradient's column sums are reduce-scattered over the half-wave's 32 rows per
+// pass (rs16); a row's exact-clip delta partial is lane-local plus its partner half.  The same
+// arithmetic per element, its sums in another fixed order (deterministic).
+#ifndef KL_SW
+#define KL_SW 0
+#endif
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+// DW (the sampled regulariser: dWo in this kernel): dZ is also kept in LDS as a row-major image
+// [rows][ZP] (ZP = 100: the 8-B writes of a half-wave's 16 rows and the transposed reads of 4
+// consecutive rows on distinct banks), and phase 2's B fragments are two ds_read_b64_tr_b16 each
+// (8 consecutive rows of one column), as the D1 kernel reads its Wo slice.
+template <int CPOL, bool DW>
+__global__ __launch_bounds__(NTH) void kl_main_sw_kernel(KlP p) {
+  // (DW: a shallower A-fragment ring — the phase-2 state would otherwise spill)
+  constexpr int D = 256, NB = kl_nb<D>(), NJ = NB / 32, CHD = D / 8, nkk = D / 16, RING = DW ? 4 : 8, ZP = 100;
+  static_assert(NB == 96, "kl_main_sw_kernel: 96-column slices");
+  __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
+  __shared__ __attribute__((aligned(16))) bf16_t Zr[DW ? TR * ZP : 8];
+  __shared__ __attribute__((aligned(16))) float2 rs[TR];   // {m + ln s, S}; the column sums at the end
+  __shared__ int32_t card[TR];
+  __shared__ __attribute__((aligned(16))) bf16_t bfr[NJ * 64 * 8];
+  static_assert(sizeof(rs) >= (NTH / 64) * NB * sizeof(float), "red_cs overlays rs");
+  float(*const red_cs)[NB] = reinterpret_cast<float(*)[NB]>(rs);
+  __shared__ double red_loss[NTH / 64];
+  __shared__ int lastflag;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), half = lane >> 5;
+  const int sl = blockIdx.x, n0 = sl * NB, V = p.V;
+  load_wo_slice<D>(p.Wo, V, n0, Wt);
+  if (tid < NJ * 64) {   // bias fragment of tile tid >> 6: column tid & 31, k = 0, 1, 2 = hi, mid, lo
+    const int gc = n0 + (tid >> 6) * 32 + (tid & 31);
+    const float b = ((tid & 32) == 0 && gc < V) ? p.bo[gc] : 0.f;
+    const __bf16 hi = (__bf16)b;
+    const float r1 = b - (float)hi;
+    const __bf16 mid = (__bf16)r1;
+    const __bf16 lo = (__bf16)(r1 - (float)mid);
+    const __bf16 z0 = (__bf16)0.f;
+    *reinterpret_cast<bf16x8_t *>(bfr + tid * 8) = bf16x8_t{hi, mid, lo, z0, z0, z0, z0, z0};
+  }
+  bf16x8_t ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)(half == 0 && e < 3 ? 1.f : 0.f);
+  const __amdgpu_buffer_rsrc_t mt_rs = __builtin_amdgcn_make_buffer_rsrc((void *)p.Mt, (short)0, p.mt_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dz_rs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)p.rows * (uint32_t)V * 2u, 0x00020000);
+  const float scale = p.scale;
+  const bool allcols = n0 + NB <= V;   // (block-uniform)
+  float cs[NJ] = {};                   // column sums: value (lane >> 1) & 15 of each tile, reduce-scattered
+  // the KL: fp32 over a pass's 48 terms per lane, fp64 across passes and tiles (the full-mode KL is
+  // a small difference of two large sums over 484 M terms: fp32 across ~4,000 terms per lane
+  // lost ~1e-4 of it)
+  double klsum = 0.0, klc = 0.0;
+  bool dead = false;
+  LFrag<D, RING> lf;
+  bool lf_ready = false;
+  for (int t0 = 0; t0 < p.rows; t0 += TR) {
+    const int nt = min(TR, p.rows - t0);
+    lds_barrier();   // the previous tile's passes done with rs / card
+    for (int i = tid; i < nt; i += NTH) {
+      const float4 st = p.rowstat[t0 + i];
+      rs[i] = make_float2(st.x, st.z);
+      const int c = p.reg_idx[t0 + i];
+      if (sl == 0 && c >= 0) klc += st.w;
+      card[i] = card_off(c, V);
+    }
+    lds_barrier();
+#pragma unroll 1
+    for (int ps = 0; ps < 2; ++ps) {
+      const int rb = ps * 256 + w * 32;
+      if (rb >= nt) continue;   // wave-uniform
+      const int row = rb + (lane & 31);
+      const uint32_t roff = (uint32_t)card[row];
+      const float2 st = rs[row];   // {m + ln s, S}
+      if (!lf_ready) logits_load(p, (p.row0 + t0 + rb) / 32, lf);
+      const int t1 = ps == 0 && 256 + w * 32 < nt ? t0 : t0 + TR;
+      const int rb1 = t1 == t0 ? 256 + w * 32 : w * 32;
+      const bool nxt = t1 < p.rows && rb1 < min(TR, p.rows - t1);
+      // the row's M~ at columns 32 j + 8 g + 4 half .. + 3 (past V / padding rows: masked below)
+      f32x4v tv[NJ][4];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          tv[j][g] = KL_DIAG_NOMT ? f32x4v{1e-3f, 1e-3f, 1e-3f, 1e-3f}
+                                  : __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                        mt_rs, roff + 4u * (uint32_t)(n0 + 32 * j + 8 * g + 4 * half), 0, CPOL));
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16_t acc[NJ];
+      {
+        int wofs = 0;   // opaque per pass: the Wo-slice fragments are not hoisted out of the loops
+        asm volatile("" : "+v"(wofs));
+        const bf16_t *Wtb = Wt + wofs;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8_t *>(bfr + (j * 64 + lane) * 8),
+                                                           ones, f32x16_t{}, 0, 0, 0);
+#pragma unroll
+        for (int kk = 0; kk < nkk; ++kk) {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const bf16x8_t a = frag(Wtb, sw_off(j * 32 + (lane & 31), kk * 16 + 8 * half, CHD));
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, lf.af[kk % RING], acc[j], 0, 0, 0);
+          }
+          if (kk + RING < nkk) lf.af[kk % RING] = *reinterpret_cast<const bf16x8_t *>(lf.src + (kk + RING) * 512);
+        }
+      }
+      lf_ready = nxt;
+      if (lf_ready) logits_load(p, (p.row0 + t1 + rb1) / 32, lf);
+      __builtin_amdgcn_sched_barrier(0);
+      const bool live_row = roff < 0x80000000u;
+      const bool fast = allcols && __ballot(!live_row) == 0ull;   // (wave-uniform)
+      float mn = 1.f, red = 0.f, klp = 0.f;
+      bool deadp = false;
+      const uint32_t zrow = (uint32_t)(t0 + row) * (uint32_t)V;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        float cv[16];
+        uint32_t pk[8];   // bf16 pairs: pk[2 g], pk[2 g + 1] = columns 8 g + 4 half .. + 3
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float lp = acc[j][r] - st.x;   // ln p = z - (m + ln s)
+          const float pr = __builtin_amdgcn_exp2f(lp * LOG2E);
+          const float tc = __builtin_amdgcn_fmed3f(tv[j][r >> 2][r & 3], PMIN, 1.f);
+          float dz;
+          if (fast) {
+            klp = fmaf(-tc, __builtin_amdgcn_fmed3f(lp, LN_PMIN, 0.f), klp);
+            mn = fminf(mn, pr);
+            dz = fmaf(scale, fmaf(pr, st.y, pr >= PMIN ? -tc : 0.f), 0.f);
+          } else {
+            const bool live = live_row && n0 + 32 * j + 8 * (r >> 2) + 4 * half + (r & 3) < V;
+            const bool big = pr >= PMIN;
+            const float lq = big ? fminf(lp, 0.f) : LN_PMIN;
+            klp += live ? -tc * lq : 0.f;
+            deadp |= live && !big;
+            red += live && !big ? tc : 0.f;
+            dz = live ? fmaf(scale, fmaf(pr, st.y, big ? -tc : 0.f), 0.f) : 0.f;
+          }
+          cv[r] = dz;
+          if (r & 1) pk[r >> 1] = (uint32_t)bf16_bits(cv[r - 1]) | ((uint32_t)bf16_bits(dz) << 16);
+        }
+        cs[j] += rs16<false>(cv);
+        if constexpr (DW) {   // the row-major dZ image for phase 2: 4 columns per 8-B write
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<uint2 *>(Zr + row * ZP + 32 * j + 8 * g + 4 * half) = make_uint2(pk[2 * g], pk[2 * g + 1]);
+        }
+        // 16-B row stores: columns 8 (g + half) .. + 7 for g = 0, 2 after swapping the odd half's
+        // even group with the even half's odd group
+#pragma unroll
+        for (int gp = 0; gp < 4; gp += 2) {
+          const auto s0 = __builtin_amdgcn_permlane32_swap(pk[2 * gp], pk[2 * gp + 2], false, false);
+          const auto s1 = __builtin_amdgcn_permlane32_swap(pk[2 * gp + 1], pk[2 * gp + 3], false, false);
+          const v4u x = v4u{(uint32_t)s0[0], (uint32_t)s1[0], (uint32_t)s0[1], (uint32_t)s1[1]};
+          const int col = n0 + 32 * j + 8 * (gp + half);
+          const uint32_t off = col < V ? 2u * (zrow + (uint32_t)col) : 0x80000000u;   // (padding rows: zeros)
+          if (!KL_DIAG_NOSTORE) __builtin_amdgcn_raw_buffer_store_b128(x, dz_rs, off, 0, CPOL);
+        }
+      }
+      klsum += (double)klp;
+      deadp |= fast && mn < PMIN;
+      if (__ballot(deadp) != 0ull) {   // (rare) the exact-clip delta of the fast path's elements
+        if (fast) {
+          red = 0.f;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float pr = __builtin_amdgcn_exp2f((acc[j][r] - st.x) * LOG2E);
+              red += pr >= PMIN ? 0.f : __builtin_amdgcn_fmed3f(tv[j][r >> 2][r & 3], PMIN, 1.f);
+            }
+        }
+      } else {
+        red = 0.f;
+      }
+      red += __shfl_xor(red, 32);   // the row's other half of the slice
+      if (half == 0) p.part_d[(int64_t)(t0 + row) * p.nsl + sl] = red;
+      dead |= deadp;
+    }
+    if constexpr (DW) {
+      lds_barrier();   // the tile's dZ image
+      // ---- phase 2: dWo[d][NB] (+)= D3^T[d][tile rows] dZ[tile rows][NB] (wave w: d rows 32 w ..),
+      // A fragments from the packed D3^T image in a ring of P2 32-row chunks, B by transposed reads
+      constexpr int P2 = 4;
+      const int nc = nt / 32;
+      const bf16_t *arow = p.D3tp + ((int64_t)w * (p.ldt / 16) * 64 + lane) * 8 + (int64_t)((p.row0 + t0) / 16) * 512;
+      f32x16_t acc2[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
+      bf16x8_t ring[P2][2];
+#pragma unroll
+      for (int q = 0; q < P2; ++q)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) ring[q][h] = *reinterpret_cast<const bf16x8_t *>(arow + (2 * min(q, nc - 1) + h) * 512);
+      for (int c0 = 0; c0 < nc; c0 += P2) {
+#pragma unroll
+        for (int q = 0; q < P2; ++q) {
+          const int c = c0 + q;
+          if (c < nc) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int j = 0; j < NJ; ++j) {
+                // column 32 j + (lane & 31), rows 32 c + 16 h + 8 half .. + 7: two transposed reads
+                const bf16_t *tb = Zr + (32 * c + 16 * h + 8 * half + ((lane >> 2) & 3)) * ZP + j * 32 +
+                                   16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+                const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)tb);
+                const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)(tb + 4 * ZP));
+                const bf16x8_t b = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[q][h], b, acc2[j], 0, 0, 0);
+              }
+            const int cn = min(c + P2, nc - 1);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) ring[q][h] = *reinterpret_cast<const bf16x8_t *>(arow + (2 * cn + h) * 512);
+          }
+        }
+      }
+      const bool first = t0 == 0;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int gc = n0 + j * 32 + (lane & 31);
+        if (gc < V) {
+          uint32_t g0 = (uint32_t)((w * 32 + 4 * half) * V + gc);
+          asm volatile("" : "+v"(g0));
+#pragma unroll
+          for (int h8 = 0; h8 < 16; h8 += 8) {
+            float old[8];
+            if (!first) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) old[r] = p.gW[g0 + (uint32_t)((((h8 + r) & 3) + 8 * ((h8 + r) >> 2)) * V)];
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+              p.gW[g0 + (uint32_t)((((h8 + r) & 3) + 8 * ((h8 + r) >> 2)) * V)] = first ? acc2[j][h8 + r] : old[r] + acc2[j][h8 + r];
+          }
+        }
+      }
+    }
+  }
+  // ---- epilogue: dbo, loss partial, the fix flag (kl_slice's, with the swapped column order)
+  lds_barrier();   // every wave past its last read of rs (red_cs overlays it)
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int q = (lane >> 1) & 15;
+    if ((lane & 1) == 0) red_cs[w][j * 32 + (q & 3) + 8 * (q >> 2) + 4 * half] = cs[j];
+  }
+  if (__ballot(dead) != 0ull && lane == 0) __hip_atomic_fetch_or(p.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  klsum += klc;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) klsum += __shfl_xor(klsum, off);
+  if (lane == 0) red_loss[w] = klsum;
+  lds_barrier();
+  if (tid < NB && n0 + tid < V) {
+    float g = 0.f;
+    for (int i = 0; i < NTH / 64; ++i) g += red_cs[i][tid];
+    p.gb[n0 + tid] = g;
+  }
+  if (tid == 0) {
+    double sum = 0.0;
+    for (int i = 0; i < NTH / 64; ++i) sum += red_loss[i];
+    lastflag = 0;
+    if (!p.loss_out) {
+      p.loss_partials[sl] = sum;
+    } else {
+      __hip_atomic_store(&p.loss_partials[sl], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t tk = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lastflag = tk == gridDim.x - 1;
+    }
+  }
+  if (p.loss_out) {
+    __syncthreads();
+    if (lastflag) {
+      double s2d = 0.0;
+      for (int i = tid; i < (int)gridDim.x; i += NTH)
+        s2d += __hip_atomic_load(&p.loss_partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) s2d += __shfl_xor(s2d, off);
+      if (lane == 0) red_loss[w] = s2d;
+      __syncthreads();
+      if (tid == 0) {
+        double tot = 0.0;
+        for (int i = 0; i < NTH / 64; ++i) tot += red_loss[i];
+        p.loss_out[0] = tot * p.loss_scale;
+        __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 }
 
 // The exact-clip correction: a small persistent grid (FIXG blocks) that leaves at once when the
@@ -1218,115 +1360,6 @@ __global__ __launch_bounds__(NTH) void kl_dwo_kernel(KlP p) {
     body(af[1], af[0], stg0, c + 1, 1);
   }
   if (c < nch) body(af[0], af[1], stg1, c, 0);
-  if (!active) return;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int gc = n0 + j * 32 + (lane & 31);
-    if (gc < V) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) p.gW[(int64_t)(wt * 32 + acc_row(r, lane)) * V + gc] = acc[j][r];
-    }
-  }
-}
-
-// The same product with the dZ stream decoupled from the A fragments (|V| % 8 == 0): 4 producer
-// waves copy dZ chunks global -> LDS by 16-B LDS-DMA, DWP_NS - 1 chunks ahead (120 KB in flight
-// per CU instead of the two register sets' 48 KB), and the 8 compute waves of kl_dwo_kernel only
-// load their A fragments and multiply.  vmcnt is per wave, so a compute wave's wait for its A
-// fragments (one chunk ahead, from L2) never waits on the HBM copies; the producers wait for their
-// own copies and one s_barrier per chunk publishes them.  (In one wave the two streams share one
-// in-order counter: each wait for the A fragments also drains the copies issued before them.)
-// The MFMA sequence per output is kl_dwo_kernel's: the same bits.  Measured: no faster than
-// kl_dwo_kernel (356.6 vs 351.4 us, r05o) — the deeper copy pipeline is not what bounds it.
-constexpr int DWP_NS = 6, DWP_NT = NTH + 256;
-template <int D>
-__global__ __launch_bounds__(DWP_NT) void kl_dwo_pc_kernel(KlP p) {
-  constexpr int NB = DW_NB, NJ = NB / 32, KC = DW_KC, KS = KC / 16;
-  constexpr int CHUNK = KC * NB * 2;              // 24 KB: 24 DMA instructions of 1 KB
-  constexpr int NPI = CHUNK / 1024 / 4;           // per producer wave: 6
-  static_assert(CHUNK % 4096 == 0, "whole instructions per producer wave");
-  typedef short v4s __attribute__((ext_vector_type(4)));
-  extern __shared__ __attribute__((aligned(1024))) char dwsmem[];
-  bf16_t *Zs = reinterpret_cast<bf16_t *>(dwsmem);   // [DWP_NS][KC * NB]
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), half = lane >> 5;
-  const int n0 = blockIdx.x * NB, V = p.V;
-  const int nch = (p.rows + KC - 1) / KC;
-  if (w >= 8) {   // ---- producers
-    const int pw = w - 8;
-    const v4i zr = sgpr_rsrc(p.dZ, (uint32_t)p.rows * (uint32_t)V * 2u);
-    // instruction i (of this wave): LDS bytes [1024 (NPI pw + i), ..) of the chunk = rows of 192 B
-    uint32_t vo[NPI];
-#pragma unroll
-    for (int i = 0; i < NPI; ++i) {
-      const int b = 1024 * (NPI * pw + i) + 16 * lane, r = b / (NB * 2), off = b % (NB * 2);
-      vo[i] = (uint32_t)(r * V + n0) * 2u + (uint32_t)off;
-    }
-    auto issue = [&](int c) {
-      const uint32_t so = (uint32_t)c * (uint32_t)KC * (uint32_t)V * 2u;   // (< rows V 2 < 4 GB)
-      const uint32_t base = lds_addr(Zs + (c % DWP_NS) * (KC * NB)) + 1024u * (uint32_t)(NPI * pw);
-#pragma unroll
-      for (int i = 0; i < NPI; ++i) dma_asm<16, 0>(zr, vo[i], so, base + 1024u * i);
-    };
-    for (int c = 0; c < min(DWP_NS - 1, nch); ++c) issue(c);
-    for (int c = 0; c < nch; ++c) {
-      // chunk c landed: this wave's younger copies are those of chunks c + 1 .. min(c + NS - 2, nch - 1)
-      const int younger = min(DWP_NS - 2, nch - 1 - c);
-      if (younger >= 4)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * NPI) : "memory");
-      else if (younger == 3)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPI) : "memory");
-      else if (younger == 2)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPI) : "memory");
-      else if (younger == 1)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPI) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      static_assert(DWP_NS - 2 == 4, "the waits above are written for 6 stages");
-      lds_barrier();   // chunk c published; chunk c - 1's stage read by every compute wave
-      if (c + DWP_NS - 1 < nch) issue(c + DWP_NS - 1);
-    }
-    return;
-  }
-  // ---- compute waves (kl_dwo_kernel's)
-  const int wt = blockIdx.y * 8 + w;
-  const bool active = wt * 32 < D;
-  const bf16_t *abase = p.D3tp + ((int64_t)min(wt, D / 32 - 1) * (p.ldt / 16) * 64 + lane) * 8;
-  const int k0 = p.row0 / 16, klast = (p.row0 + p.rows) / 16 - 1;
-  auto load_a = [&](bf16x8_t (&dst)[KS], int c) {
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      dst[ks] = *reinterpret_cast<const bf16x8_t *>(abase + (int64_t)min(k0 + c * KS + ks, klast) * 512);
-  };
-  f32x16_t acc[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-  bf16x8_t af[2][KS];
-  load_a(af[0], 0);
-  auto body = [&](bf16x8_t (&cur)[KS], bf16x8_t (&nxt)[KS], int c) {
-    lds_barrier();   // chunk c published (the producers' copies landed)
-    load_a(nxt, c + 1);   // (unconditional: clamped past the end, never used)
-    if (active) {
-      const bf16_t *Zc = Zs + (c % DWP_NS) * (KC * NB);
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const bf16_t *tb = Zc + (ks * 16 + 8 * half + ((lane >> 2) & 3)) * NB + j * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)tb);
-          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)(tb + 4 * NB));
-          const bf16x8_t b = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[ks], b, acc[j], 0, 0, 0);
-        }
-    }
-  };
-  int c = 0;
-  for (; c + 1 < nch; c += 2) {
-    body(af[0], af[1], c);
-    body(af[1], af[0], c + 1);
-  }
-  if (c < nch) body(af[0], af[1], c);
   if (!active) return;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -1633,24 +1666,15 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
   // many row tiles (full mode): dWo from the stored dZ by kl_dwo_kernel (even V: 4-B aligned rows);
   // one tile (the sampled regulariser): in the main pass, from its LDS dZ^T tile
   const bool dw_sep = a->rows > TR && a->V % 2 == 0;
-  // M~ staged through LDS by 16-B DMAs (kl_slice's MS): 16-B aligned rows, and the padding /
-  // past-V sentinel 0x80000000 outside both buffers' ranges
-  const bool ms = a->V % 4 == 0 && ((uintptr_t)a->Mt & 15) == 0 && (int64_t)a->rows * a->V * 2 < 0x80000000ll &&
-                  (a->flags & CC_KL_LDS_TARGETS);
-  // the register path's dZ through LDS as 16-B row stores (16-B aligned rows; the sentinel past range)
-  const bool wstore = a->V % 8 == 0 && ((uintptr_t)a->dZ & 15) == 0 && (int64_t)a->rows * a->V * 2 < 0x80000000ll &&
-                      !(a->flags & CC_KL_SHORT_STORES);
-  // ... and its M~ loaded 16 B per lane through LDS (16-B aligned rows): opt-in (measured slower)
-  const bool wload = ((uintptr_t)a->Mt & 15) == 0 && (a->flags & CC_KL_WIDE_TARGETS);
-  // dWo's dZ stream by producer waves' LDS-DMA (16-B aligned rows): opt-in (measured no faster)
+  // the main pass's dZ through LDS as 16-B row stores (16-B aligned rows; the sentinel past range)
+  const bool wstore = a->V % 8 == 0 && ((uintptr_t)a->dZ & 15) == 0 && (int64_t)a->rows * a->V * 2 < 0x80000000ll;
   // the stats in slice pairs x row halves (kl_stats2_kernel): many row tiles (full mode), d = 256
   const bool stats2 = CCREC_KL_STATS2 && a->d == 256 && a->rows > TR;
-  const bool dwo_pc = a->V % 8 == 0 && ((uintptr_t)a->dZ & 15) == 0 && (a->flags & CC_KL_DWO_PRODUCER_WAVES);
   // dWo in 192-column slices x two row halves (kl_dwo2_kernel): 16-B aligned rows, the chunk
   // sentinel 0x80000000 past dZ's range, at least one chunk per half
   const bool dwo2 = CCREC_DWO2 && a->d == 256 && a->V % 8 == 0 && (((uintptr_t)a->dZ | (uintptr_t)a->gW) & 15) == 0 &&
                     (int64_t)a->rows * a->V * 2 < 0x80000000ll && cdiv(a->rows, DW2_KC) >= DW2_SPLIT &&
-                    p.dw_part && !(a->flags & (CC_KL_DWO_NARROW | CC_KL_DWO_PRODUCER_WAVES));
+                    p.dw_part && !(a->flags & CC_KL_DWO_NARROW);
 #define KL_LAUNCH(DD)                                                                                          \
   if (a->d == DD) {                                                                                          \
     if (stats2 && DD == 256)                                                                                 \
@@ -1661,25 +1685,17 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
     hipLaunchKernelGGL(kl_merge_kernel, dim3((unsigned)cdiv(a->rows, 4)), dim3(256), 0, s, p);              \
     CC_LAUNCH_CHECK("kl_merge_kernel");                                                                      \
     if (dw_sep) {                                                                                            \
-      if (ms)                                                                                                \
-        hipLaunchKernelGGL((kl_main_kernel<DD, KL_SEP_CPOL, false, (DD <= 256)>), gm, dim3(NTH), 0, s, p);    \
-      else if (wstore && wload)                                                                              \
-        hipLaunchKernelGGL((kl_main_kernel<DD, KL_SEP_CPOL, false, false, (DD <= 256), (DD <= 256)>), gm, dim3(NTH), 0, s, p); \
+      if (KL_SW && wstore && DD == 256)                                                                      \
+        hipLaunchKernelGGL((kl_main_sw_kernel<KL_SEP_CPOL, false>), gm, dim3(NTH), 0, s, p);                 \
       else if (wstore)                                                                                       \
-        hipLaunchKernelGGL((kl_main_kernel<DD, KL_SEP_CPOL, false, false, (DD <= 256)>), gm, dim3(NTH), 0, s, p); \
+        hipLaunchKernelGGL((kl_main_kernel<DD, KL_SEP_CPOL, false, (DD <= 256)>), gm, dim3(NTH), 0, s, p);    \
       else                                                                                                   \
         hipLaunchKernelGGL((kl_main_kernel<DD, KL_SEP_CPOL, false>), gm, dim3(NTH), 0, s, p);                 \
       CC_LAUNCH_CHECK("kl_main_kernel");                                                                     \
       hipLaunchKernelGGL((kl_fix_kernel<DD, false>), dim3(FIXG), dim3(NTH), 0, s, p);                       \
       CC_LAUNCH_CHECK("kl_fix_kernel");                                                                      \
       const dim3 gd((unsigned)cdiv(a->V, DW_NB), (unsigned)(DD > 256 ? DD / 256 : 1));                     \
-      if (dwo_pc) {                                                                                          \
-        static const bool attr = hipFuncSetAttribute((const void *)kl_dwo_pc_kernel<DD>,                     \
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize,             \
-                                                      DWP_NS * DW_KC * DW_NB * 2) == hipSuccess;              \
-        CC_REQUIRE(attr, "cc_dec_softmax_kl_dw: dynamic LDS attribute");                                     \
-        hipLaunchKernelGGL((kl_dwo_pc_kernel<DD>), gd, dim3(DWP_NT), DWP_NS * DW_KC * DW_NB * 2, s, p);      \
-      } else if (dwo2 && DD == 256) {                                                                        \
+      if (dwo2 && DD == 256) {                                                                               \
         static const bool attr2 = hipFuncSetAttribute((const void *)kl_dwo2_kernel<256>,                     \
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, DW2_LDS) == \
                                   hipSuccess;                                                                \
@@ -1695,7 +1711,9 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
         hipLaunchKernelGGL((kl_dwo_kernel<DD, false>), gd, dim3(NTH), 0, s, p);                              \
       CC_LAUNCH_CHECK("kl_dwo_kernel");                                                                      \
     } else {                                                                                                 \
-      if (a->rows > TR)                                                                                      \
+      if (KL_SW && wstore && DD == 256 && a->rows <= TR)                                                     \
+        hipLaunchKernelGGL((kl_main_sw_kernel<0, true>), gm, dim3(NTH), 0, s, p);                            \
+      else if (a->rows > TR)                                                                                 \
         hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, true>), gm, dim3(NTH), 0, s, p);                  \
       else                                                                                                   \
         hipLaunchKernelGGL((kl_main_kernel<DD, 0, true>), gm, dim3(NTH), 0, s, p);                           \

@@ -524,21 +524,12 @@ typedef struct cc_dec_kl_args {
   double loss_scale;
   uint32_t *ticket;
   void *ws;
-  int32_t flags;             /* A/B knobs of the many-row (full-mode) path, bit-identical results; 0 = the
-                                measured-fastest default.  CC_KL_LDS_TARGETS: the main pass stages M~
-                                through LDS by DMA one pass ahead (slower, r05r); CC_KL_DWO_PRODUCER_WAVES:
-                                dWo's dZ stream by producer waves' LDS-DMA (slower); CC_KL_SHORT_STORES:
-                                dZ stored 2 B per lane instead of 16-B rows through LDS (slower);
-                                CC_KL_WIDE_TARGETS: M~ loaded as 16-B rows turned into the accumulator
-                                layout through LDS instead of 4 B per lane (slower).  CC_KL_DWO_NARROW
-                                (not bit-identical: dWo summed over all rows in one pass instead of two
-                                row halves added): dWo by the 96-column kernel of round 4 (slower);
-                                CC_KL_DWO_PRODUCER_WAVES implies it */
+  int32_t flags;             /* 0, or CC_KL_DWO_NARROW: with many rows (full mode) dWo by the 96-column
+                                kernel in one pass over all rows instead of kl_dwo2's two row halves
+                                (the default at d = 256, |V| % 8 == 0; dWo differs by float rounding).
+                                The round-5 A/B paths measured slower (M~ staged through LDS, M~ as
+                                16-B rows, dWo by producer waves) were retired (branch archive/r05-ab-knobs). */
 } cc_dec_kl_args;
-#define CC_KL_LDS_TARGETS 1
-#define CC_KL_DWO_PRODUCER_WAVES 2
-#define CC_KL_SHORT_STORES 4
-#define CC_KL_WIDE_TARGETS 8
 #define CC_KL_DWO_NARROW 16
 size_t cc_dec_kl_ws_size(int32_t rows, int32_t V);
 int32_t cc_dec_kl_blocks(int32_t V);

@@ -53,6 +53,7 @@ def _setup(V, d, B, C, reg, dtype, seed=3, sizes=(20, 40, 80), fused_tower=True,
 @pytest.mark.parametrize('reg', [0.0, 0.1])
 @pytest.mark.parametrize('V,d,B,fused', [(700, 64, 32, True), (2500, 128, 64, True), (2500, 256, 64, True),
                                          (700, 64, 32, False), (2500, 128, 48, True), (2500, 256, 128, True),
+                                         (2504, 256, 128, True),
                                          (2500, 128, 128, True), (2500, 512, 128, True)])
 def test_train_steps_match_oracle(dtype, reg, V, d, B, fused):
     C = 4 * B
@@ -429,7 +430,7 @@ def test_full_mode_regulariser_matches_oracle(dtype, V, d, B):
     tr.check_status()
 
 
-@pytest.mark.parametrize('V,B,d', [(2500, 128, 256), (3001, 256, 256), (2500, 128, 512)])
+@pytest.mark.parametrize('V,B,d', [(2500, 128, 256), (3001, 256, 256), (2500, 128, 512), (2504, 128, 256)])
 def test_fused_regulariser_clip_fix_path(V, B, d):
     """The fused D2 kernels' exact-clip path (csrc/decreg.hip): a decoder_for_reg bias spread
     pushes part of every softmax row below 1e-7, so TF's clip gradient mask matters (S shrinks by
@@ -460,13 +461,9 @@ def test_full_mode_clip_fix_path(V, spread):
     """Full mode (all |V| identity rows, several 512-row tiles per slice) with the exact-clip
     path live: the bias spread of the clip test above pushes part of every softmax row below
     1e-7.  Against the bf16-emulating oracle over reg_idx = arange(V) (spread off: no clip), then
-    the alternative paths of decreg.hip (cc_dec_kl_args.flags) bit for bit against the default:
-    M~ staged through LDS (MS, V % 4 == 0: its rare-path reload of M~ for the clip partials, its
-    counted waits across tiles) with dWo's producer-wave dZ stream (V % 8 == 0), M~ loaded as 16-B
-    rows through LDS, and the 2-B dZ stores instead of 16-B rows through LDS (V % 8 == 0;
-    V = 2,502 has none of them).  dWo: the default at V % 8 == 0 is kl_dwo2_kernel (two row halves
-    added); the 96-column kernels (CC_KL_DWO_NARROW, the producer-wave variant) sum all rows in one
-    pass — every other output identical, dWo equal to float rounding."""
+    dWo's 96-column kernel (cc_dec_kl_args.flags = CC_KL_DWO_NARROW) against the default: at
+    V % 8 == 0 the default is kl_dwo2_kernel (two row halves added), the 96-column kernel sums all
+    rows in one pass — every other output identical, dWo equal to float rounding."""
     d, B = 256, 128
 
     def run(flags):
@@ -495,17 +492,13 @@ def test_full_mode_clip_fix_path(V, spread):
                                       'decoder_for_reg/decoded_3/kernel', 'encoder/encoded_1/kernel')},
                    TOL['bf16_full'], 0)
     assert e['loss/kl'] < 5e-6, e['loss/kl']
-    # the LDS staging of M~ (decreg.hip MS, V % 4 == 0), dWo's producer-wave dZ stream and the 16-B dZ
-    # stores through LDS (V % 8 == 0)
-    # against the register-staged paths: identical bits
     g1 = tr.layout.unpack(tr.grads.cpu().numpy())
     dwo = 'decoder_for_reg/reconstruct/kernel'
-    for flags in (L.CC_KL_LDS_TARGETS | L.CC_KL_DWO_PRODUCER_WAVES, L.CC_KL_WIDE_TARGETS, L.CC_KL_SHORT_STORES,
-                  L.CC_KL_DWO_NARROW):
+    for flags in (L.CC_KL_DWO_NARROW,):
         tr2 = run(flags)[0]
         g2 = tr.layout.unpack(tr2.grads.cpu().numpy())
         diff = {k: float(np.abs(g1[k] - g2[k]).max()) for k in g1 if not np.array_equal(g1[k], g2[k])}
-        narrow = V % 8 == 0 and flags & (L.CC_KL_DWO_NARROW | L.CC_KL_DWO_PRODUCER_WAVES)
+        narrow = V % 8 == 0 and flags & L.CC_KL_DWO_NARROW
         if narrow and dwo in diff:   # one K order vs two row halves: float rounding only
             scale = float(np.abs(g1[dwo]).max())
             assert diff.pop(dwo) <= 2e-6 * scale, (flags, scale)
