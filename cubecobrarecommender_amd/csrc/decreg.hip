@@ -902,303 +902,12 @@ __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
   kl_slice<D, false, CPOL, DW, WS>(p, blockIdx.x, Wt, sm);
 }
 
-// ---------------------------------------------------------------- main, operands swapped (full mode)
-// The full-mode main pass (many row tiles, dWo by its own kernel; d = 256, |V| % 8 == 0) with the
-// MFMA operands swapped as in the stats kernels (Wo slice = A, D3 rows = B): a lane holds ONE row
-// and, per 32-column tile, 4 runs of 4 consecutive columns.  Against kl_slice's layout (a lane = one
-// column of 16 rows): M~ arrives as 12 16-B loads per lane and pass instead of 48 4-B ones; dZ leaves
-// as 6 16-B row stores after one permlane32 swap per dword pair instead of a DPP pairing + LDS image
-// round trip; the row statistics are one LDS read per pass instead of one per element; the bias
-// starts the accumulators by one MFMA against a ones fragment (its exact three-bf16 split, as the D1
-// kernel); the bias gradient's column sums are reduce-scattered over the half-wave's 32 rows per
-// pass (rs16); a row's exact-clip delta partial is lane-local plus its partner half.  The same
-// arithmetic per element, its sums in another fixed order (deterministic).
-#ifndef KL_SW
-#define KL_SW 0
-#endif
-typedef float f32x4v __attribute__((ext_vector_type(4)));
-// DW (the sampled regulariser: dWo in this kernel): dZ is also kept in LDS as a row-major image
-// [rows][ZP] (ZP = 100: the 8-B writes of a half-wave's 16 rows and the transposed reads of 4
-// consecutive rows on distinct banks), and phase 2's B fragments are two ds_read_b64_tr_b16 each
-// (8 consecutive rows of one column), as the D1 kernel reads its Wo slice.
-template <int CPOL, bool DW>
-__global__ __launch_bounds__(NTH) void kl_main_sw_kernel(KlP p) {
-  // (DW: a shallower A-fragment ring — the phase-2 state would otherwise spill)
-  constexpr int D = 256, NB = kl_nb<D>(), NJ = NB / 32, CHD = D / 8, nkk = D / 16, RING = DW ? 4 : 8, ZP = 100;
-  static_assert(NB == 96, "kl_main_sw_kernel: 96-column slices");
-  __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
-  __shared__ __attribute__((aligned(16))) bf16_t Zr[DW ? TR * ZP : 8];
-  __shared__ __attribute__((aligned(16))) float2 rs[TR];   // {m + ln s, S}; the column sums at the end
-  __shared__ int32_t card[TR];
-  __shared__ __attribute__((aligned(16))) bf16_t bfr[NJ * 64 * 8];
-  static_assert(sizeof(rs) >= (NTH / 64) * NB * sizeof(float), "red_cs overlays rs");
-  float(*const red_cs)[NB] = reinterpret_cast<float(*)[NB]>(rs);
-  __shared__ double red_loss[NTH / 64];
-  __shared__ int lastflag;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), half = lane >> 5;
-  const int sl = blockIdx.x, n0 = sl * NB, V = p.V;
-  load_wo_slice<D>(p.Wo, V, n0, Wt);
-  if (tid < NJ * 64) {   // bias fragment of tile tid >> 6: column tid & 31, k = 0, 1, 2 = hi, mid, lo
-    const int gc = n0 + (tid >> 6) * 32 + (tid & 31);
-    const float b = ((tid & 32) == 0 && gc < V) ? p.bo[gc] : 0.f;
-    const __bf16 hi = (__bf16)b;
-    const float r1 = b - (float)hi;
-    const __bf16 mid = (__bf16)r1;
-    const __bf16 lo = (__bf16)(r1 - (float)mid);
-    const __bf16 z0 = (__bf16)0.f;
-    *reinterpret_cast<bf16x8_t *>(bfr + tid * 8) = bf16x8_t{hi, mid, lo, z0, z0, z0, z0, z0};
-  }
-  bf16x8_t ones;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)(half == 0 && e < 3 ? 1.f : 0.f);
-  const __amdgpu_buffer_rsrc_t mt_rs = __builtin_amdgcn_make_buffer_rsrc((void *)p.Mt, (short)0, p.mt_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t dz_rs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)p.rows * (uint32_t)V * 2u, 0x00020000);
-  const float scale = p.scale;
-  const bool allcols = n0 + NB <= V;   // (block-uniform)
-  float cs[NJ] = {};                   // column sums: value (lane >> 1) & 15 of each tile, reduce-scattered
-  // the KL: fp32 over a pass's 48 terms per lane, fp64 across passes and tiles (the full-mode KL is
-  // a small difference of two large sums over 484 M terms: fp32 across ~4,000 terms per lane
-  // lost ~1e-4 of it)
-  double klsum = 0.0, klc = 0.0;
-  bool dead = false;
-  LFrag<D, RING> lf;
-  bool lf_ready = false;
-  for (int t0 = 0; t0 < p.rows; t0 += TR) {
-    const int nt = min(TR, p.rows - t0);
-    lds_barrier();   // the previous tile's passes done with rs / card
-    for (int i = tid; i < nt; i += NTH) {
-      const float4 st = p.rowstat[t0 + i];
-      rs[i] = make_float2(st.x, st.z);
-      const int c = p.reg_idx[t0 + i];
-      if (sl == 0 && c >= 0) klc += st.w;
-      card[i] = card_off(c, V);
-    }
-    lds_barrier();
-#pragma unroll 1
-    for (int ps = 0; ps < 2; ++ps) {
-      const int rb = ps * 256 + w * 32;
-      if (rb >= nt) continue;   // wave-uniform
-      const int row = rb + (lane & 31);
-      const uint32_t roff = (uint32_t)card[row];
-      const float2 st = rs[row];   // {m + ln s, S}
-      if (!lf_ready) logits_load(p, (p.row0 + t0 + rb) / 32, lf);
-      const int t1 = ps == 0 && 256 + w * 32 < nt ? t0 : t0 + TR;
-      const int rb1 = t1 == t0 ? 256 + w * 32 : w * 32;
-      const bool nxt = t1 < p.rows && rb1 < min(TR, p.rows - t1);
-      // the row's M~ at columns 32 j + 8 g + 4 half .. + 3 (past V / padding rows: masked below)
-      f32x4v tv[NJ][4];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          tv[j][g] = KL_DIAG_NOMT ? f32x4v{1e-3f, 1e-3f, 1e-3f, 1e-3f}
-                                  : __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                        mt_rs, roff + 4u * (uint32_t)(n0 + 32 * j + 8 * g + 4 * half), 0, CPOL));
-      __builtin_amdgcn_sched_barrier(0);
-      f32x16_t acc[NJ];
-      {
-        int wofs = 0;   // opaque per pass: the Wo-slice fragments are not hoisted out of the loops
-        asm volatile("" : "+v"(wofs));
-        const bf16_t *Wtb = Wt + wofs;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8_t *>(bfr + (j * 64 + lane) * 8),
-                                                           ones, f32x16_t{}, 0, 0, 0);
-#pragma unroll
-        for (int kk = 0; kk < nkk; ++kk) {
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) {
-            const bf16x8_t a = frag(Wtb, sw_off(j * 32 + (lane & 31), kk * 16 + 8 * half, CHD));
-            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, lf.af[kk % RING], acc[j], 0, 0, 0);
-          }
-          if (kk + RING < nkk) lf.af[kk % RING] = *reinterpret_cast<const bf16x8_t *>(lf.src + (kk + RING) * 512);
-        }
-      }
-      lf_ready = nxt;
-      if (lf_ready) logits_load(p, (p.row0 + t1 + rb1) / 32, lf);
-      __builtin_amdgcn_sched_barrier(0);
-      const bool live_row = roff < 0x80000000u;
-      const bool fast = allcols && __ballot(!live_row) == 0ull;   // (wave-uniform)
-      float mn = 1.f, red = 0.f, klp = 0.f;
-      bool deadp = false;
-      const uint32_t zrow = (uint32_t)(t0 + row) * (uint32_t)V;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        float cv[16];
-        uint32_t pk[8];   // bf16 pairs: pk[2 g], pk[2 g + 1] = columns 8 g + 4 half .. + 3
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float lp = acc[j][r] - st.x;   // ln p = z - (m + ln s)
-          const float pr = __builtin_amdgcn_exp2f(lp * LOG2E);
-          const float tc = __builtin_amdgcn_fmed3f(tv[j][r >> 2][r & 3], PMIN, 1.f);
-          float dz;
-          if (fast) {
-            klp = fmaf(-tc, __builtin_amdgcn_fmed3f(lp, LN_PMIN, 0.f), klp);
-            mn = fminf(mn, pr);
-            dz = fmaf(scale, fmaf(pr, st.y, pr >= PMIN ? -tc : 0.f), 0.f);
-          } else {
-            const bool live = live_row && n0 + 32 * j + 8 * (r >> 2) + 4 * half + (r & 3) < V;
-            const bool big = pr >= PMIN;
-            const float lq = big ? fminf(lp, 0.f) : LN_PMIN;
-            klp += live ? -tc * lq : 0.f;
-            deadp |= live && !big;
-            red += live && !big ? tc : 0.f;
-            dz = live ? fmaf(scale, fmaf(pr, st.y, big ? -tc : 0.f), 0.f) : 0.f;
-          }
-          cv[r] = dz;
-          if (r & 1) pk[r >> 1] = (uint32_t)bf16_bits(cv[r - 1]) | ((uint32_t)bf16_bits(dz) << 16);
-        }
-        cs[j] += rs16<false>(cv);
-        if constexpr (DW) {   // the row-major dZ image for phase 2: 4 columns per 8-B write
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-            *reinterpret_cast<uint2 *>(Zr + row * ZP + 32 * j + 8 * g + 4 * half) = make_uint2(pk[2 * g], pk[2 * g + 1]);
-        }
-        // 16-B row stores: columns 8 (g + half) .. + 7 for g = 0, 2 after swapping the odd half's
-        // even group with the even half's odd group
-#pragma unroll
-        for (int gp = 0; gp < 4; gp += 2) {
-          const auto s0 = __builtin_amdgcn_permlane32_swap(pk[2 * gp], pk[2 * gp + 2], false, false);
-          const auto s1 = __builtin_amdgcn_permlane32_swap(pk[2 * gp + 1], pk[2 * gp + 3], false, false);
-          const v4u x = v4u{(uint32_t)s0[0], (uint32_t)s1[0], (uint32_t)s0[1], (uint32_t)s1[1]};
-          const int col = n0 + 32 * j + 8 * (gp + half);
-          const uint32_t off = col < V ? 2u * (zrow + (uint32_t)col) : 0x80000000u;   // (padding rows: zeros)
-          if (!KL_DIAG_NOSTORE) __builtin_amdgcn_raw_buffer_store_b128(x, dz_rs, off, 0, CPOL);
-        }
-      }
-      klsum += (double)klp;
-      deadp |= fast && mn < PMIN;
-      if (__ballot(deadp) != 0ull) {   // (rare) the exact-clip delta of the fast path's elements
-        if (fast) {
-          red = 0.f;
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const float pr = __builtin_amdgcn_exp2f((acc[j][r] - st.x) * LOG2E);
-              red += pr >= PMIN ? 0.f : __builtin_amdgcn_fmed3f(tv[j][r >> 2][r & 3], PMIN, 1.f);
-            }
-        }
-      } else {
-        red = 0.f;
-      }
-      red += __shfl_xor(red, 32);   // the row's other half of the slice
-      if (half == 0) p.part_d[(int64_t)(t0 + row) * p.nsl + sl] = red;
-      dead |= deadp;
-    }
-    if constexpr (DW) {
-      lds_barrier();   // the tile's dZ image
-      // ---- phase 2: dWo[d][NB] (+)= D3^T[d][tile rows] dZ[tile rows][NB] (wave w: d rows 32 w ..),
-      // A fragments from the packed D3^T image in a ring of P2 32-row chunks, B by transposed reads
-      constexpr int P2 = 4;
-      const int nc = nt / 32;
-      const bf16_t *arow = p.D3tp + ((int64_t)w * (p.ldt / 16) * 64 + lane) * 8 + (int64_t)((p.row0 + t0) / 16) * 512;
-      f32x16_t acc2[NJ];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
-      bf16x8_t ring[P2][2];
-#pragma unroll
-      for (int q = 0; q < P2; ++q)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) ring[q][h] = *reinterpret_cast<const bf16x8_t *>(arow + (2 * min(q, nc - 1) + h) * 512);
-      for (int c0 = 0; c0 < nc; c0 += P2) {
-#pragma unroll
-        for (int q = 0; q < P2; ++q) {
-          const int c = c0 + q;
-          if (c < nc) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-              for (int j = 0; j < NJ; ++j) {
-                // column 32 j + (lane & 31), rows 32 c + 16 h + 8 half .. + 7: two transposed reads
-                const bf16_t *tb = Zr + (32 * c + 16 * h + 8 * half + ((lane >> 2) & 3)) * ZP + j * 32 +
-                                   16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-                const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)tb);
-                const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)(tb + 4 * ZP));
-                const bf16x8_t b = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[q][h], b, acc2[j], 0, 0, 0);
-              }
-            const int cn = min(c + P2, nc - 1);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) ring[q][h] = *reinterpret_cast<const bf16x8_t *>(arow + (2 * cn + h) * 512);
-          }
-        }
-      }
-      const bool first = t0 == 0;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int gc = n0 + j * 32 + (lane & 31);
-        if (gc < V) {
-          uint32_t g0 = (uint32_t)((w * 32 + 4 * half) * V + gc);
-          asm volatile("" : "+v"(g0));
-#pragma unroll
-          for (int h8 = 0; h8 < 16; h8 += 8) {
-            float old[8];
-            if (!first) {
-#pragma unroll
-              for (int r = 0; r < 8; ++r) old[r] = p.gW[g0 + (uint32_t)((((h8 + r) & 3) + 8 * ((h8 + r) >> 2)) * V)];
-            }
-#pragma unroll
-            for (int r = 0; r < 8; ++r)
-              p.gW[g0 + (uint32_t)((((h8 + r) & 3) + 8 * ((h8 + r) >> 2)) * V)] = first ? acc2[j][h8 + r] : old[r] + acc2[j][h8 + r];
-          }
-        }
-      }
-    }
-  }
-  // ---- epilogue: dbo, loss partial, the fix flag (kl_slice's, with the swapped column order)
-  lds_barrier();   // every wave past its last read of rs (red_cs overlays it)
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int q = (lane >> 1) & 15;
-    if ((lane & 1) == 0) red_cs[w][j * 32 + (q & 3) + 8 * (q >> 2) + 4 * half] = cs[j];
-  }
-  if (__ballot(dead) != 0ull && lane == 0) __hip_atomic_fetch_or(p.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  klsum += klc;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) klsum += __shfl_xor(klsum, off);
-  if (lane == 0) red_loss[w] = klsum;
-  lds_barrier();
-  if (tid < NB && n0 + tid < V) {
-    float g = 0.f;
-    for (int i = 0; i < NTH / 64; ++i) g += red_cs[i][tid];
-    p.gb[n0 + tid] = g;
-  }
-  if (tid == 0) {
-    double sum = 0.0;
-    for (int i = 0; i < NTH / 64; ++i) sum += red_loss[i];
-    lastflag = 0;
-    if (!p.loss_out) {
-      p.loss_partials[sl] = sum;
-    } else {
-      __hip_atomic_store(&p.loss_partials[sl], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint32_t tk = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      lastflag = tk == gridDim.x - 1;
-    }
-  }
-  if (p.loss_out) {
-    __syncthreads();
-    if (lastflag) {
-      double s2d = 0.0;
-      for (int i = tid; i < (int)gridDim.x; i += NTH)
-        s2d += __hip_atomic_load(&p.loss_partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) s2d += __shfl_xor(s2d, off);
-      if (lane == 0) red_loss[w] = s2d;
-      __syncthreads();
-      if (tid == 0) {
-        double tot = 0.0;
-        for (int i = 0; i < NTH / 64; ++i) tot += red_loss[i];
-        p.loss_out[0] = tot * p.loss_scale;
-        __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-}
+// (Measured and dropped, round 6: the main pass with the MFMA operands swapped as in the stats
+// kernels — a lane = one row: 16-B M~ loads, 16-B dZ row stores after permlane32 swaps, the row
+// stats per lane, the bias by one MFMA against a ones fragment, the column sums reduce-scattered;
+// correct, but full mode 2.78 against 2.23 ms/step and the sampled + KL step 280 against 275.5 us:
+// a 16-B load or store of this layout touches 32 rows per wave instruction where the 4-B / 2-B
+// accesses of kl_slice's layout touch 2.  Source at commit 997c871.)
 
 // The exact-clip correction: a small persistent grid (FIXG blocks) that leaves at once when the
 // step saw no p < 1e-7, and otherwise walks the slices.
@@ -1685,9 +1394,7 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
     hipLaunchKernelGGL(kl_merge_kernel, dim3((unsigned)cdiv(a->rows, 4)), dim3(256), 0, s, p);              \
     CC_LAUNCH_CHECK("kl_merge_kernel");                                                                      \
     if (dw_sep) {                                                                                            \
-      if (KL_SW && wstore && DD == 256)                                                                      \
-        hipLaunchKernelGGL((kl_main_sw_kernel<KL_SEP_CPOL, false>), gm, dim3(NTH), 0, s, p);                 \
-      else if (wstore)                                                                                       \
+      if (wstore)                                                                                            \
         hipLaunchKernelGGL((kl_main_kernel<DD, KL_SEP_CPOL, false, (DD <= 256)>), gm, dim3(NTH), 0, s, p);    \
       else                                                                                                   \
         hipLaunchKernelGGL((kl_main_kernel<DD, KL_SEP_CPOL, false>), gm, dim3(NTH), 0, s, p);                 \
@@ -1711,9 +1418,7 @@ extern "C" int cc_dec_softmax_kl_dw(const cc_dec_kl_args *a, void *stream) {
         hipLaunchKernelGGL((kl_dwo_kernel<DD, false>), gd, dim3(NTH), 0, s, p);                              \
       CC_LAUNCH_CHECK("kl_dwo_kernel");                                                                      \
     } else {                                                                                                 \
-      if (KL_SW && wstore && DD == 256 && a->rows <= TR)                                                     \
-        hipLaunchKernelGGL((kl_main_sw_kernel<0, true>), gm, dim3(NTH), 0, s, p);                            \
-      else if (a->rows > TR)                                                                                 \
+      if (a->rows > TR)                                                                                      \
         hipLaunchKernelGGL((kl_main_kernel<DD, KL_CPOL_NT, true>), gm, dim3(NTH), 0, s, p);                  \
       else                                                                                                   \
         hipLaunchKernelGGL((kl_main_kernel<DD, 0, true>), gm, dim3(NTH), 0, s, p);                           \
