@@ -6,6 +6,7 @@
 #   bench[:<bench.py args>]   one bench line                                   -> $O/bench_<i>.log
 #   prof[:<bench.py args>]    rocprofv3 --kernel-trace --stats of a bench run  -> $O/prof_<i>/
 #   pmc:<C1,C2,..>[:<args>]   one rocprofv3 --pmc pass of a short bench run    -> $O/pmc_<i>.json (per-kernel averages)
+#   pmcx:<C1,C2,..>:<prog>    one rocprofv3 --pmc pass over a built probe binary -> $O/pmc_<i>.json
 #   py:<script args>          python -u <script args>                          -> $O/py_<i>.log
 #   cmd:<command>             any command (a built probe binary)               -> $O/cmd_<i>.log
 # Every GPU step runs under its own time limit; the first failing step ends the session.
@@ -48,6 +49,11 @@ for st in "$@"; do
       ( export TMPDIR=/tmp; cd /tmp && timeout -s KILL 150 rocprofv3 --pmc ${c//,/ } -d "$O/pmc_$i" -o run -- \
         python3 "$R/bench.py" --steps 16 --warmup 4 --no-cpu-baseline --no-recommend $a > "$O/pmc_$i.log" 2>&1 ) \
         || { tail -30 "$O/pmc_$i.log"; exit 1; }
+      python tools/prof_collect.py pmc "$O/pmc_$i" "$O/pmc_$i.json" && echo "pmc $c ok" ;;
+    pmcx)
+      c=${arg%%:*}; a=${arg#*:}
+      ( export TMPDIR=/tmp; cd /tmp && timeout -s KILL 90 rocprofv3 --pmc ${c//,/ } -d "$O/pmc_$i" -o run -- \
+        "$R/$a" > "$O/pmc_$i.log" 2>&1 ) || { tail -30 "$O/pmc_$i.log"; exit 1; }
       python tools/prof_collect.py pmc "$O/pmc_$i" "$O/pmc_$i.json" && echo "pmc $c ok" ;;
     py)
       timeout -k 10 600 python -u $arg > "$O/py_$i.log" 2>&1 || { tail -30 "$O/py_$i.log"; exit 1; }
