@@ -13,6 +13,21 @@ typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 
 #define CC_WAVE 64
 
+// The hardware deals a launch's workgroups to the 8 XCDs round robin (block b on XCD b % 8).  This
+// bijection gives each XCD a contiguous run of ids, so workgroups whose data share 128-B lines
+// (neighbouring column slices) fetch them into one L2 instead of several.
+__device__ __forceinline__ int cc_xcd_run(int b, int nb) {
+  const int q = nb / 8, r = nb % 8, x = b % 8, slot = b / 8;
+  return x < r ? x * (q + 1) + slot : r * (q + 1) + (x - r) * q + slot;
+}
+// CCREC_XCD_SLICES (build knob for the A/B, default on): the fused output-layer kernels (D1's
+// dec_bce_dw, D2's kl_stats / kl_main) take their 96-column slice from cc_xcd_run instead of
+// blockIdx.x
+#ifndef CCREC_XCD_SLICES
+#define CCREC_XCD_SLICES 1
+#endif
+__device__ __forceinline__ int cc_slice_of_block(int b, int nb) { return CCREC_XCD_SLICES ? cc_xcd_run(b, nb) : b; }
+
 // ------------------------------------------------------------------ error plumbing (host)
 namespace cc {
 void set_error(const std::string &msg);

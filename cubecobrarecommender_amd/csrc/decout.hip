@@ -135,7 +135,10 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   bf16_t *Zt = reinterpret_cast<bf16_t *>(smem + ZT_OFF);        // [NB][B]
   uint32_t *ys = reinterpret_cast<uint32_t *>(smem + YS_OFF);    // [NJ][B]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
-  const int n0 = blockIdx.x * NB;
+  // the slice from an XCD-contiguous run (common.hpp): the target words' lines (32 words = ~10
+  // slices) and the Wo lines two slices share are then fetched into one L2, not all 8
+  // (tools/micro/d1_fetch_cal.hip: 11.2 + 17.0 of the launch's 32.8 MB of line fetches)
+  const int sl = cc_slice_of_block(blockIdx.x, gridDim.x), n0 = sl * NB;
   const int V = p.V;
   const int VW = (V + 31) >> 5;
 
@@ -682,16 +685,16 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     for (int i = 0; i < NTH / 64; ++i) sum += red_loss[i];
     lastflag = 0;
     if (!p.loss_out) {
-      p.loss_partials[blockIdx.x] = sum;
+      p.loss_partials[sl] = sum;
     } else {
-      __hip_atomic_store(&p.loss_partials[blockIdx.x], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&p.loss_partials[sl], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint32_t tk = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       lastflag = tk == gridDim.x - 1;
     }
   }
   DEC_PROBE(8);
-  // ---- the last block reduces the loss partials in block order
+  // ---- the last block reduces the loss partials in slice order
   if (p.loss_out) {
     __syncthreads();
     if (lastflag) {

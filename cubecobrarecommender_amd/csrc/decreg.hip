@@ -245,7 +245,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   __shared__ __attribute__((aligned(16))) bf16_t Wt[NB * D];
   constexpr int CHD = D / 8;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5;
-  const int sl = blockIdx.x, n0 = sl * NB;
+  const int sl = cc_slice_of_block(blockIdx.x, gridDim.x), n0 = sl * NB;
   __shared__ __attribute__((aligned(16))) float bs[NB];   // the slice's bias, -inf past V
   KL_PROBE(8);
   if (sl == 0 && threadIdx.x == 0) *p.flag = 0u;  // this step's fix flag starts clear
@@ -899,7 +899,7 @@ template <int D, int CPOL, bool DW, bool WS = false>
 __global__ __launch_bounds__(NTH) void kl_main_kernel(KlP p) {
   __shared__ __attribute__((aligned(16))) bf16_t Wt[kl_nb<D>() * D];
   __shared__ __attribute__((aligned(16))) MainSmem<kl_nb<D>()> sm;
-  kl_slice<D, false, CPOL, DW, WS>(p, blockIdx.x, Wt, sm);
+  kl_slice<D, false, CPOL, DW, WS>(p, cc_slice_of_block(blockIdx.x, gridDim.x), Wt, sm);
 }
 
 // (Measured and dropped, round 6: the main pass with the MFMA operands swapped as in the stats

@@ -2,6 +2,9 @@
 """Per-launch HBM traffic of one kernel from the reduced PMC passes (tools/prof_collect.py pmc
 outputs of separate FETCH_SIZE and WRITE_SIZE runs): bytes = 2 x FETCH_SIZE x 1024 (gfx950: FETCH_SIZE
 counts half the bytes of 16-B/lane streaming reads; KB) + WRITE_SIZE x 1024 (MI355X_MICROARCH.md §HBM).
+The x2 holds for these kernels' reads: request-size-resolved counters show every TCC_EA0_RDREQ a
+128-B request (TCC_EA0_RDREQ_32B = 0, TCC_BUBBLE ~0), and a contiguous 16-B/lane read of a known
+11.26 MB gives RDREQ x 128 B = its bytes (tools/micro/d1_fetch_cal.hip, profiles/r06o_d1cal_*.json).
 
 usage: traffic_from_pmc.py <fetch.json> <write.json> <out.json> <kernel-substring>:<key> [...]
 """
@@ -29,8 +32,9 @@ def main():
         res[key] = {'bytes_per_launch': fetch + write, 'fetch_bytes': fetch, 'write_bytes': write,
                     'kernel': kn, 'dispatches': f.get('dispatches'),
                     'method': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes '
-                              '(tools/gpu_r03x.sh); FETCH_SIZE x2 (gfx950 16-B/lane read correction), '
-                              'x1024 (KB); per-dispatch averages'}
+                              '(tools/gpu_run.sh pmc steps); FETCH_SIZE x2 (every TCC_EA0_RDREQ a 128-B request, '
+                              'tallied at 64 B: calibrated in tools/micro/d1_fetch_cal.hip), x1024 (KB); '
+                              'per-dispatch averages'}
     json.dump(res, open(out, 'w'), indent=1)
     print(json.dumps(res))
 
