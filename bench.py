@@ -74,7 +74,7 @@ def parse():
                     help="collective backend for --gpus > 1 (nccl = RCCL; gloo only to rehearse the "
                          "data-parallel path with several ranks on one GPU)")
     ap.add_argument('--traffic-json', default=os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                                           'profiles', 'traffic_r04z.json'))
+                                                           'profiles', 'traffic_r06.json'))
     return ap.parse_args()
 
 
