@@ -15,7 +15,6 @@
 
 #include "adam.hpp"
 #include "common.hpp"
-#include "ts_probe.hpp"
 #include "xt.hpp"
 
 // build knobs (A/B builds: CCREC_EXTRA_FLAGS=-D..., a tagged library; the library reads no
@@ -40,8 +39,6 @@
 #ifndef EG_PROBE
 #define EG_PROBE(k)
 #endif
-
-TS_PROBE_DEFINE(embed)
 
 namespace {
 
@@ -269,7 +266,6 @@ __global__ __launch_bounds__(64 * GWN) void gather_xcd_kernel(const bf16_t *__re
                                                              const int32_t *__restrict__ x_idx, int x_cap,
                                                              bf16_t *__restrict__ out, const void *warm,
                                                              int64_t warm_bytes, int64_t *state, int64_t bpe) {
-  if (state) TS_PROBE_FIRST(embed, state[0]);
   if (state && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {  // the previous step's counters
     state[0] += 1;
     state[1] += 1;

@@ -20,11 +20,8 @@
 
 #include "adam.hpp"
 #include "common.hpp"
-#include "ts_probe.hpp"
 #include "detmath.hpp"
 #include "noise_dev.hpp"
-
-TS_PROBE_DEFINE(noise)
 
 namespace {
 
@@ -104,7 +101,6 @@ __global__ __launch_bounds__(NT) void adam_noise_kernel(cc_adam::Args ad, cc_noi
   // start at once, the Adam blocks (of the first flat range, then of the second, if any) stream
   // around them
   const int64_t step = a.state[0];
-  TS_PROBE_FIRST(noise, step);
   if ((int)blockIdx.x >= nf + nadam) {
     cc_adam::range(ad1, step, (int)blockIdx.x - nf - nadam, nadam1, PACK ? &pk : nullptr);
   } else if ((int)blockIdx.x >= nf) {
@@ -117,7 +113,6 @@ __global__ __launch_bounds__(NT) void adam_noise_kernel(cc_adam::Args ad, cc_noi
     }
     noise_block(a, smem, s_k, blockIdx.x, step + 1, batch, epoch);
   }
-  TS_PROBE_LAST(noise, step);
 }
 
 }  // namespace

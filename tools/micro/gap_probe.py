@@ -5,6 +5,9 @@ stamps csrc/ts_probe.hpp leaves per step: the Adam + next-F launch's first block
 block end, and the next step's E1 gather's first block start.  Prints the distribution of the
 boundary gap (gather start - Adam end) and of the Adam launch's duration, in us.
 
+(The probe macros were removed from the product kernels after the measurement; rebuild the probe
+library from commit c87345e.)
+
 usage: CCREC_LIB=$PWD/cubecobrarecommender_amd/libccrec_hip_ts.so python tools/micro/gap_probe.py [bench args]
 """
 import ctypes as C
