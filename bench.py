@@ -43,7 +43,7 @@ def parse():
                          '--steps and is <= --warmup, so warmup has replayed every graph the timed region '
                          'replays: a graph\'s first replay costs extra)')
     ap.add_argument('--V', type=int, default=22000)
-    ap.add_argument('--d', type=int, default=256)
+    ap.add_argument('--d', '--dim', dest='d', type=int, default=256)
     ap.add_argument('--batch', type=int, default=512)
     ap.add_argument('--cubes', type=int, default=65536)
     ap.add_argument('--reg', type=float, default=0.0)
@@ -78,6 +78,21 @@ def parse():
     return ap.parse_args()
 
 
+def child_argv(argv):
+    """bench.py's arguments as the ranks receive them through torch.distributed.run, whose parser
+    rejects an option that abbreviates several of its own before handing the rest to the script
+    (`--d` would abbreviate --duplicate-stdout-filters / --duplicate-stderr-filters): `--d` is
+    passed as its long form `--dim`."""
+    out = []
+    for a in argv:
+        if a == '--d':
+            a = '--dim'
+        elif a.startswith('--d='):
+            a = '--dim=' + a[4:]
+        out.append(a)
+    return out
+
+
 def launch_ranks(args):
     """--gpus N > 1 without a torch.distributed.run environment: start one rank per GPU as CHILD
     processes (torch.distributed.run, rendezvous on 127.0.0.1) and exit with their status.  This
@@ -92,7 +107,8 @@ def launch_ranks(args):
     env = dict(os.environ)
     env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
-           '--master-addr', '127.0.0.1', f'--master-port={port}', os.path.abspath(__file__), *sys.argv[1:]]
+           '--master-addr', '127.0.0.1', f'--master-port={port}', os.path.abspath(__file__),
+           *child_argv(sys.argv[1:])]
     sys.exit(subprocess.run(cmd, env=env).returncode)
 
 

@@ -119,3 +119,23 @@ def test_dp_layout_w1_chunks_any_world():
                 assert (hi - lo) % (64 * world) == 0, (world, d, name)
             assert all(r0 % 64 == 0 for r0, _ in lay.w1_chunks)
             assert lay.w1_chunks[0][0] == 0 and lay.w1_chunks[-1][1] == 22000
+
+
+def test_bench_rank_argv_passes_torchrun_parser(monkeypatch):
+    """bench.py --gpus N starts its ranks through torch.distributed.run, whose parser rejects an
+    ambiguous abbreviation of its own options before the script's arguments: `--d` is renamed."""
+    import sys
+
+    import pytest
+    from torch.distributed.run import get_args_parser
+
+    import bench
+    argv = ['--gpus', '4', '--d', '1024', '--dtype', 'fp8', '--reg', '0.1', '--d=512']
+    out = bench.child_argv(argv)
+    assert out == ['--gpus', '4', '--dim', '1024', '--dtype', 'fp8', '--reg', '0.1', '--dim=512']
+    ns = get_args_parser().parse_args(['--nnodes=1', '--nproc-per-node=4', 'bench.py', *out])
+    assert ns.training_script_args == out
+    with pytest.raises(SystemExit):       # the unrenamed form is what failed
+        get_args_parser().parse_args(['--nnodes=1', 'bench.py', *argv])
+    monkeypatch.setattr(sys, 'argv', ['bench.py', *out])
+    assert bench.parse().d == 512
