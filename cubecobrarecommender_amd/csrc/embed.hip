@@ -820,6 +820,12 @@ struct CsReg {
   int card0;           // card of this launch's W1 row 0 (a row chunk's first row)
 };
 constexpr int CS_REG_MAX = 512;   // (one 32-bit mask of reg k-steps per tile)
+// (Measured and dropped, round 6, tools/micro/eg_reg_probe.hip: per wave, a tile of popular cards
+// or the bias tile takes many reg k-steps and ends its wave ~10 us after the rest.  Neither the
+// chunks interleaved over the blocks (+14 us on the + KL step: the bias tile then shares a wave
+// with two full tiles; BCE +1, config 5 +20-35 us, profiles/r06y_w1_tstride_ab.txt) nor the reg
+// k-steps' B fragments staged in LDS (with half the LUT copies to make room: + KL +3 us,
+// profiles/r06z_w1_reg_lds_ab.txt) beat the code below.)
 
 template <bool PK, int XWM, bool VEC, bool ADAM, bool REG = false>
 __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *__restrict__ gsrc, int V, int d, int R,

@@ -1,6 +1,7 @@
 """W1 gradient + Adam in isolation (dev tool): the cube rows only (R = 512), the reg rows by index
 (cc_embed_grad_cs_adam_reg, nreg = 512 cards drawn from the bench's neg_sampler) and the reg rows as
-bits (R = 1024), at V = 22,000, d = 256; HIP-event averages per variant, interleaved."""
+bits (R = 1024), at V = 22,000, d = 256, with and without the bias row; HIP-event averages per
+variant, interleaved; --warm: no cache eviction between launches."""
 import os
 import sys
 
@@ -39,7 +40,18 @@ def main():
     bg = torch.zeros(d, device='cuda')
     st = torch.zeros(4, dtype=torch.int64, device='cuda')
     s = L.stream_ptr()
+    def reg_call(bias):
+        return lambda: L.call('cc_embed_grad_cs_adam_reg', L.ptr(gP), 1, V, d, B, RP, L.ptr(xb1),
+                              L.ptr(bg) if bias else None, None, L.ptr(p), L.ptr(m), L.ptr(v), L.ptr(sh),
+                              L.ptr(st), 1e-3, 0.9, 0.999, 1e-7, L.ptr(rid), B, B // 16, s)
+
+    def cube_call(bias):
+        return lambda: L.call('cc_embed_grad_cs_adam', L.ptr(gP), 1, V, d, B, RP, L.ptr(xb1),
+                              L.ptr(bg) if bias else None, None, L.ptr(p), L.ptr(m), L.ptr(v), L.ptr(sh),
+                              L.ptr(st), 1e-3, 0.9, 0.999, 1e-7, s)
     variants = {
+        'cubes_only_nobias': cube_call(False),
+        'reg_by_index_nobias': reg_call(False),
         'cubes_only_R512': lambda: L.call('cc_embed_grad_cs_adam', L.ptr(gP), 1, V, d, B, RP, L.ptr(xb1), L.ptr(bg),
                                           None, L.ptr(p), L.ptr(m), L.ptr(v), L.ptr(sh), L.ptr(st), 1e-3, 0.9,
                                           0.999, 1e-7, s),
@@ -52,9 +64,11 @@ def main():
     }
     times = {k: [] for k in variants}
     big = torch.empty(256 << 20, device='cuda')   # evicts the MALL between launches, as a step does
+    warm = '--warm' in sys.argv                    # (or not: p / m / v stay in the MALL)
     for rep in range(40):
         for k, f in variants.items():
-            big.mul_(1.0)
+            if not warm:
+                big.mul_(1.0)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             f()
