@@ -825,7 +825,8 @@ constexpr int CS_REG_MAX = 512;   // (one 32-bit mask of reg k-steps per tile)
 // chunks interleaved over the blocks (+14 us on the + KL step: the bias tile then shares a wave
 // with two full tiles; BCE +1, config 5 +20-35 us, profiles/r06y_w1_tstride_ab.txt) nor the reg
 // k-steps' B fragments staged in LDS (with half the LUT copies to make room: + KL +3 us,
-// profiles/r06z_w1_reg_lds_ab.txt) beat the code below.)
+// profiles/r06z_w1_reg_lds_ab.txt) nor each batch's rid reads / A bytes / LUT reads / MFMAs issued
+// phase by phase (neutral, profiles/r06g_w1_reg_pipe_ab.txt) beat the code below.)
 
 template <bool PK, int XWM, bool VEC, bool ADAM, bool REG = false>
 __global__ __launch_bounds__(CS_NT, 1) void embed_grad_cs_kernel(const bf16_t *__restrict__ gsrc, int V, int d, int R,
