@@ -13,7 +13,9 @@ from cubecobrarecommender_amd import _lib as L  # noqa: E402
 
 
 def main():
-    V, d, B = 22000, 256, 512
+    V, B = 22000, 512
+    d = int(sys.argv[sys.argv.index('--d') + 1]) if '--d' in sys.argv else 256
+    pk = int(sys.argv[sys.argv.index('--packed') + 1]) if '--packed' in sys.argv else 1
     from cubecobrarecommender_amd.synthetic import synthetic_cubes, neg_sampler_from_csr
     ip, ix = synthetic_cubes(65536, V, seed=20250301, device='cpu')
     ns = np.asarray(neg_sampler_from_csr(ip, ix, V), np.float64)
@@ -31,7 +33,8 @@ def main():
     xb1 = torch.from_numpy(xt1.view(np.int32)).cuda()
     xb2 = torch.from_numpy(xt2.view(np.int32)).cuda()
     g = (torch.randn(RP, d, device='cuda') * 0.1).to(torch.bfloat16)
-    gP = g.view(RP // 16, 2, 8, d // 32, 32).permute(3, 0, 1, 4, 2).contiguous()
+    gP = (g.view(RP // 16, 2, 8, d // 32, 32).permute(3, 0, 1, 4, 2).contiguous() if pk else
+          g.t().contiguous())   # packed fragment image, or dPre1^T [d][RP]
     rid = torch.from_numpy(reg).cuda()
     p = torch.randn(V * d, device='cuda') * 0.02
     m = torch.zeros_like(p)
@@ -41,24 +44,24 @@ def main():
     st = torch.zeros(4, dtype=torch.int64, device='cuda')
     s = L.stream_ptr()
     def reg_call(bias):
-        return lambda: L.call('cc_embed_grad_cs_adam_reg', L.ptr(gP), 1, V, d, B, RP, L.ptr(xb1),
+        return lambda: L.call('cc_embed_grad_cs_adam_reg', L.ptr(gP), pk, V, d, B, RP, L.ptr(xb1),
                               L.ptr(bg) if bias else None, None, L.ptr(p), L.ptr(m), L.ptr(v), L.ptr(sh),
                               L.ptr(st), 1e-3, 0.9, 0.999, 1e-7, L.ptr(rid), B, B // 16, s)
 
     def cube_call(bias):
-        return lambda: L.call('cc_embed_grad_cs_adam', L.ptr(gP), 1, V, d, B, RP, L.ptr(xb1),
+        return lambda: L.call('cc_embed_grad_cs_adam', L.ptr(gP), pk, V, d, B, RP, L.ptr(xb1),
                               L.ptr(bg) if bias else None, None, L.ptr(p), L.ptr(m), L.ptr(v), L.ptr(sh),
                               L.ptr(st), 1e-3, 0.9, 0.999, 1e-7, s)
     variants = {
         'cubes_only_nobias': cube_call(False),
         'reg_by_index_nobias': reg_call(False),
-        'cubes_only_R512': lambda: L.call('cc_embed_grad_cs_adam', L.ptr(gP), 1, V, d, B, RP, L.ptr(xb1), L.ptr(bg),
+        'cubes_only_R512': lambda: L.call('cc_embed_grad_cs_adam', L.ptr(gP), pk, V, d, B, RP, L.ptr(xb1), L.ptr(bg),
                                           None, L.ptr(p), L.ptr(m), L.ptr(v), L.ptr(sh), L.ptr(st), 1e-3, 0.9,
                                           0.999, 1e-7, s),
-        'reg_by_index': lambda: L.call('cc_embed_grad_cs_adam_reg', L.ptr(gP), 1, V, d, B, RP, L.ptr(xb1), L.ptr(bg),
+        'reg_by_index': lambda: L.call('cc_embed_grad_cs_adam_reg', L.ptr(gP), pk, V, d, B, RP, L.ptr(xb1), L.ptr(bg),
                                        None, L.ptr(p), L.ptr(m), L.ptr(v), L.ptr(sh), L.ptr(st), 1e-3, 0.9, 0.999,
                                        1e-7, L.ptr(rid), B, B // 16, s),
-        'reg_as_bits_R1024': lambda: L.call('cc_embed_grad_cs_adam', L.ptr(gP), 1, V, d, R2, RP, L.ptr(xb2),
+        'reg_as_bits_R1024': lambda: L.call('cc_embed_grad_cs_adam', L.ptr(gP), pk, V, d, R2, RP, L.ptr(xb2),
                                             L.ptr(bg), None, L.ptr(p), L.ptr(m), L.ptr(v), L.ptr(sh), L.ptr(st),
                                             1e-3, 0.9, 0.999, 1e-7, s),
     }
