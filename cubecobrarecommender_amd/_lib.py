@@ -60,6 +60,7 @@ class TowerArgs(C.Structure):
         ('hpt', C.c_void_p * 6), ('gpt', C.c_void_p * 6), ('gpre1p', C.c_void_p),
         ('x_bits', C.c_void_p), ('xt_bits', C.c_void_p), ('xt_V', C.c_int32), ('xt_rows', C.c_int32),
         ('d3q', C.c_void_p), ('d3qs', C.c_void_p), ('d3tq', C.c_void_p), ('d3tqs', C.c_void_p),
+        ('y_bits', C.c_void_p), ('y_img', C.c_void_p), ('y_V', C.c_int32),
     ]
 
 
@@ -116,6 +117,8 @@ SIGNATURES = {
     'cc_dec_bce_dw': (C.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _F64, _P, _P]),
     'cc_dec_bce_dw_ld': (C.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _P,
                                    _P, _F64, _P, _P]),
+    'cc_dec_bce_dw_img': (C.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _I32, _P, _P,
+                                    _P, _P, _F64, _P, _P]),
     'cc_dec_bce_dw_blocks': (_I32, [_I32]),
     'cc_dec_softmax_kl_fused': (C.c_int, [_I32, _P, _I32, _I32, _P, _P, _F32, _P, _P, _P]),
     'cc_reduce_loss': (C.c_int, [_P, _I32, _F64, _P, _P]),
@@ -161,6 +164,8 @@ SIGNATURES = {
     'cc_noise_next': (C.c_int, [C.POINTER(NoiseArgs), _I64, _P]),
     'cc_tower_slab_elems': (_I64, [_I32]),
     'cc_tower_fwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
+    'cc_tower_fwd_adam': (C.c_int, [C.POINTER(TowerArgs), _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _P, _I64,
+                                    _F32, _F32, _F32, _F32, _P]),
     'cc_tower_bwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_bwd_chain': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_bwd_chain_adam': (C.c_int, [C.POINTER(TowerArgs), _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _P,
@@ -202,7 +207,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.cc_abi_version() != 1:
+        if L.cc_abi_version() != 2:
             raise CCError('libccrec_hip ABI version mismatch')
         _lib = L
     return _lib

@@ -52,6 +52,7 @@ struct DecOutP {
   const bf16_t *Wo;        // [d][V] (the bf16 shadow of the reconstruct kernel)
   const float *bo;         // [V]
   const uint32_t *y_bits;  // [B][ceil(V/32)]
+  const uint32_t *y_img;   // or null: y_bits as cc_tower_args.y_img ([ceil(V/32)][B], register row order)
   bf16_t *dZ;              // [B][V]
   float *gW;               // [d][V]
   float *gb;               // [V]
@@ -60,6 +61,7 @@ struct DecOutP {
   uint32_t *ticket;
   double loss_scale;
   float scale;
+  float log2e;             // log2(e), passed in (an SGPR operand of the packed multiply)
   int V, ldt;
   int ldz;                 // dZ row pitch (elements, >= V; a multiple of 64 keeps every dZ row 128-B aligned)
 };
@@ -99,7 +101,7 @@ __device__ __forceinline__ uint32_t bf16_pack2(float a, float b) {
 // epilogue's strided reads cost more than the staging saved — and phase 2 with the operands swapped
 // for 16-B dWo stores: 32 rows x 32 B per store instruction ran slower than 2 x 128-B rows of
 // 4-B stores; tools/micro/dec_probe2.hip)
-template <int D, int BB, bool DMA>
+template <int D, int BB, bool DMA, bool IMG = false>
 __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   constexpr int d = D, B = BB;
   constexpr int NB = nb_of<D>(), NJ = NB / 32;    // slice columns, 32-column accumulators per wave
@@ -116,11 +118,11 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   // a ring of 16 through the pass's 32 k-steps
   constexpr bool RING1 = nkk > 16;
   constexpr int NAF = RING1 ? 16 : nkk;
-  // LDS map (bytes): the Wo^T slice [NB][d] (DMA: Wo rows [d][NB]); dZ^T [NB][B]; the target bits
-  // [NJ][B] (DMA: [B][NJ])
+  // LDS map (bytes): the Wo^T slice [NB][d] (DMA: Wo rows [d][NB]); dZ^T [NB][B].  The target bits
+  // never enter the LDS: the epilogue uses them as lane masks straight from SGPRs (below)
   static_assert(!DMA || NB == 96, "dec_bce_dw_kernel: the DMA staging assumes 96-column slices");
   constexpr int ZT_OFF = NB * d * 2, ZT_BYTES = NB * B * 2;
-  constexpr int YS_OFF = ZT_OFF + ZT_BYTES, LDS_BYTES = YS_OFF + B * NJ * 4;
+  constexpr int LDS_BYTES = ZT_OFF + ZT_BYTES;
   static_assert(LDS_BYTES <= 150 * 1024, "dec_bce_dw_kernel: LDS");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
   __shared__ float red_cs[NTH / 64][NB];
@@ -133,8 +135,8 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   __shared__ __attribute__((aligned(16))) bf16_t bfr[NJ * 64 * 8];
   bf16_t *Wt = reinterpret_cast<bf16_t *>(smem);                 // [NB][d]
   bf16_t *Zt = reinterpret_cast<bf16_t *>(smem + ZT_OFF);        // [NB][B]
-  uint32_t *ys = reinterpret_cast<uint32_t *>(smem + YS_OFF);    // [NJ][B]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5;
+  const int wu = __builtin_amdgcn_readfirstlane(w);   // the wave index as a scalar (uniform addresses)
   // the slice from an XCD-contiguous run (common.hpp): the target words' lines (32 words = ~10
   // slices) and the Wo lines two slices share are then fetched into one L2, not all 8
   // (tools/micro/d1_fetch_cal.hip: 11.2 + 17.0 of the launch's 32.8 MB of line fetches)
@@ -145,16 +147,25 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   DEC_PROBE(0);
   // pass 0's A fragments first: their L2 round trip overlaps the resident staging below
   bf16x8_t af[RING1 ? 1 : 2][NAF];
-  // fragment (row block, kk): packed = 1 KB contiguous (whole cache lines per wave load)
-  const int astr = p.D3p ? 512 : 16;
-  auto a_src = [&](int pass) -> const bf16_t * {
-    if (p.D3p) return p.D3p + ((int64_t)min(pass * 8 + w, B / 32 - 1) * nkk * 64 + lane) * 8;
-    return p.D3 + (int64_t)min(pass * 256 + w * 32 + (lane & 31), B - 1) * d + 8 * half;
+  // fragment (row block, kk): packed = 1 KB contiguous (whole cache lines per wave load).  Buffer
+  // loads: the lane part is one VGPR offset computed once, the row block and k step ride in the
+  // scalar offset (no per-load 64-bit address arithmetic on the VALU the epilogue is bound by)
+  const bool pka = p.D3p != nullptr;
+  const __amdgpu_buffer_rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(pka ? p.D3p : p.D3), (short)0, (uint32_t)B * (uint32_t)d * 2u, 0x00020000);
+  const int astr = pka ? 1024 : 32;   // bytes per 16-k step
+  const uint32_t a_vo = pka ? (uint32_t)lane * 16u : (uint32_t)((lane & 31) * d + 8 * half) * 2u;
+  auto a_so = [&](int pass) -> uint32_t {   // (uniform) byte offset of the pass's row block
+    return pka ? (uint32_t)min(pass * 8 + wu, B / 32 - 1) * (uint32_t)(nkk * 1024)
+               : (uint32_t)min(pass * 256 + wu * 32, B - 32) * (uint32_t)(d * 2);
+  };
+  auto a_ld = [&](uint32_t so, int kk) -> bf16x8_t {
+    return __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(a_rs, a_vo, so + (uint32_t)(kk * astr), 0));
   };
   auto load_a = [&](bf16x8_t (&dst)[NAF], int pass) {
-    const bf16_t *src = a_src(pass);
+    const uint32_t so = a_so(pass);
 #pragma unroll
-    for (int kk = 0; kk < NAF; ++kk) dst[kk] = *reinterpret_cast<const bf16x8_t *>(src + kk * astr);
+    for (int kk = 0; kk < NAF; ++kk) dst[kk] = a_ld(so, kk);
     // keep the whole batch in flight: without this fence the scheduler sinks each load to its
     // MFMA and the pass becomes a chain of dependent L2 round trips
     __builtin_amdgcn_sched_barrier(0);
@@ -176,26 +187,35 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
                                                (uint32_t)((k * V + n0 + 8 * c) * 2), 0, 0, 0);
     }
   }
-  // YS_LATE (DMA, B >= 256: every wave has rows in pass 0): the target words are loaded last and
-  // written to LDS only after pass 0's logits MFMAs, so the first barrier waits for the Wo slice and
-  // the A fragments but not for the 1.5-K strided word loads
-  constexpr bool YS_LATE = DMA && B >= 256;
-  constexpr int NY = (B * NJ + NTH - 1) / NTH;
-  uint32_t yv[NY];
-  auto load_ys = [&]() {
+  // The target bits as lane masks: word (row, n0 / 32 + j) of y_bits holds exactly the bits of
+  // the 32 columns of accumulator tile j, lane l <-> column n0 + 32 j + l.  Accumulator register r
+  // of tile j holds row acc_row(r, lane) — rows rl and rl + 4 in the two lane halves — so ONE 64-bit
+  // scalar (word(rl) | word(rl + 4) << 32) is that register's target mask, used directly as the
+  // lane mask of v_cndmask / s_xor (inverse ballot): no per-element shift or bit extraction on
+  // the VALU.  Scalar loads through the constant address space (uniform addresses; F wrote the
+  // words in an earlier launch).
+  typedef __attribute__((address_space(4))) const uint32_t cu32_t;
+  cu32_t *yc = (cu32_t *)p.y_bits;
+  // (tiles past the last word read the last word: their columns are past |V|, where the targets
+  // change nothing that is kept)
+  // With the image (cc_tower_args.y_img, written by the tower forward launch) a tile's 16 masks are
+  // 128 contiguous bytes: two scalar 64-B loads from one address.  Without it: 32 scattered words.
+  typedef __attribute__((address_space(4))) const uint64_t cu64_t;
+  auto load_masks = [&](int pass, int j, uint64_t (&m)[16]) {
+    const uint32_t gw = (uint32_t)min((n0 >> 5) + j, VW - 1), r0 = (uint32_t)(pass * 256 + wu * 32);
+    if constexpr (IMG) {
+      cu64_t *q = (cu64_t *)((cu32_t *)p.y_img + (gw * (uint32_t)B + r0));
 #pragma unroll
-    for (int q = 0; q < NY; ++q) {
-      const int i = tid + NTH * q, r = min(i / NJ, B - 1), gw = (n0 >> 5) + i % NJ;
-      yv[q] = gw < VW ? p.y_bits[(int64_t)r * VW + gw] : 0u;
+      for (int r = 0; r < 16; ++r) m[r] = q[r];
+      return;
     }
-  };
-  auto store_ys = [&]() {
+    const uint32_t base = r0 * (uint32_t)VW + gw;
 #pragma unroll
-    for (int q = 0; q < NY; ++q)
-      if (tid + NTH * q < B * NJ) {  // target words column-tile-major: ys[j][row]
-        const int i = tid + NTH * q;
-        ys[(i % NJ) * B + i / NJ] = yv[q];
-      }
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t rl = (uint32_t)((r & 3) + 8 * (r >> 2));
+      const uint32_t lo = yc[base + rl * (uint32_t)VW], hi = yc[base + (rl + 4) * (uint32_t)VW];
+      m[r] = (uint64_t)lo | ((uint64_t)hi << 32);
+    }
   };
   {
     constexpr int NW = NB * CHD / NTH;
@@ -237,7 +257,6 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         }
       }
     }
-    if (!YS_LATE) load_ys();
     __builtin_amdgcn_sched_barrier(0);
     if (!STAGE) {
     } else if (!fromWo) {
@@ -260,7 +279,6 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         }
       }
     }
-    if (!YS_LATE) store_ys();
   }
 
   // ---- phase 1: logits, BCE, dZ (global + LDS dZ^T), bias-gradient partial, loss.  Wave w owns
@@ -292,31 +310,25 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     cnt_z = 0;
   }
   // LDS-only barrier: __syncthreads would also wait for pass 0's A fragments (vmcnt counts loads).
-  // DMA: the wave's own DMAs (issued after pass 0's A fragments) must have landed first — and with
-  // YS_LATE only they: the NY target-word loads, issued last, stay in flight
-  if constexpr (YS_LATE) {
-    // (the builtin, not inline asm: the compiler's wait insertion then knows the Wo slice's DMA has
-    // landed and does not wait for every older load, the target words included, at the first LDS
-    // read.  s_waitcnt encoding: vmcnt[3:0], expcnt[6:4] (7: none), lgkmcnt[11:8] (0))
-    static_assert(NY <= 15, "dec_bce_dw_kernel: vmcnt immediate");
-    __builtin_amdgcn_s_waitcnt(7 << 4);
-    __builtin_amdgcn_s_barrier();
-  } else if constexpr (DMA) {
+  // DMA: the wave's own DMAs (issued after pass 0's A fragments) must have landed first
+  if constexpr (DMA) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   } else {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   DEC_PROBE(1);
   const float scale = p.scale;
+  const f32x2_t l2e = {p.log2e, p.log2e};   // (a kernel argument: the packed multiply takes it from SGPRs)
   // dZ and gW through buffer descriptors: a 32-bit byte offset per store instead of a 64-bit
-  // address (dZ = B x V x 2 B and gW = d x V x 4 B stay below 4 GB: checked on the host)
+  // address (dZ = B x V x 2 B < 2 GB and gW = d x V x 4 B < 4 GB: checked on the host)
   const __amdgpu_buffer_rsrc_t dz_rs =
       __builtin_amdgcn_make_buffer_rsrc((void *)p.dZ, (short)0, (uint32_t)B * (uint32_t)p.ldz * 2u, 0x00020000);
   const int LZ = p.ldz;
   // dz of rows (r2, r2 + 1) as one packed bf16 pair -> two 2-B stores (row offsets as the scalar
   // soffset); the odd row by buffer_store_short_d16_hi straight from the pair (inline asm: the
   // compiler counts no vmcnt for it — a later counted wait can only over-wait, never under-wait,
-  // since this store is younger than every load it counts)
+  // since this store is younger than every load it counts).  Lanes of columns past |V| carry an
+  // offset beyond the descriptor's range: the hardware drops their stores (no branch)
 #ifdef DEC_DIAG_NODZ   // diagnostic builds only (tools/micro/dec_probe2.hip): no dz stores
 #define DEC_STORE_PAIR(PK, R2) do { (void)(PK); } while (0)
 #else
@@ -332,18 +344,13 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 #pragma unroll
   for (int ps = 0; ps < npass; ++ps) {
     if (!RING1 && ps + 1 < npass) load_a(af[(ps + 1) & 1], ps + 1);
-    if constexpr (YS_LATE) {
-#ifndef DEC_DIAG_NOY
-      if (ps == 0) load_ys();   // the youngest loads: nothing before pass 0's epilogue waits for them
-#endif
-    }
     if (ps * 256 + w * 32 >= B) continue;          // wave-uniform: rows beyond B
     f32x16_t acc[NJ];  // starts at the bias (exactly): z = bo + sum_k D3 Wo accumulates in the MFMA
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
       acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, *reinterpret_cast<const bf16x8_t *>(bfr + (j * 64 + lane) * 8),
                                                        f32x16_t{}, 0, 0, 0);
-    const bf16_t *asrc = a_src(ps);
+    const uint32_t aso = a_so(ps);
 #pragma unroll
     for (int kk = 0; kk < nkk; ++kk) {
 #pragma unroll
@@ -359,17 +366,9 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         }
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[RING1 ? 0 : ps & 1][kk % NAF], b, acc[j], 0, 0, 0);
       }
-      if (RING1 && kk + NAF < nkk) af[0][kk % NAF] = *reinterpret_cast<const bf16x8_t *>(asrc + (kk + NAF) * astr);
+      if (RING1 && kk + NAF < nkk) af[0][kk % NAF] = a_ld(aso, kk + NAF);
     }
     if (RING1 && ps + 1 < npass) load_a(af[0], ps + 1);   // the next pass's head under this epilogue
-#ifndef DEC_DIAG_NOY
-    if constexpr (YS_LATE) {
-      if (ps == 0) {   // (every wave is here: B >= 256)
-        store_ys();
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      }
-    }
-#endif
     DEC_PROBE(2 + 2 * ps);
     if constexpr (SPLIT2) {
       if (ps == npass - 1) {   // this wave reads the Wo slice no more (its fragment reads returned)
@@ -378,8 +377,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
       }
     }
     if constexpr (DMA && npass > 1) {   // the half (w >> 2) == (ps & 1) leads pass ps (wave-uniform)
-      const int hw = __builtin_amdgcn_readfirstlane(w) >> 2;
-      if (hw == (ps & 1))
+      if ((wu >> 2) == (ps & 1))
         __builtin_amdgcn_s_setprio(1);
       else
         __builtin_amdgcn_s_setprio(0);
@@ -387,70 +385,60 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
     const int rb = ps * 256 + w * 32;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
+      uint64_t mk[16];   // this tile's target masks (the other wave of the SIMD covers their latency)
+      load_masks(ps, j, mk);
       const int col = j * 32 + (lane & 31);
       uint32_t tt[8];  // dz of rows (r, r+1) as one packed bf16 pair (one v_cvt_pk_bf16_f32)
-      if (valid[j]) {
-        // sigmoid_cross_entropy_with_logits (TF 2.5 Keras BCE on a sigmoid output):
-        //   loss = max(z, 0) - z y + log1p(exp(-|z|)),  dz = (sigmoid(z) - y) / (B V)
-        // in the target-signed logit s = (1 - 2y) z (the sign bit of z flipped where y = 1):
-        //   loss = max(s, 0) + log1p(exp(-|s|)),  dz = (1 - 2y) sigmoid(s) / (B V)
-        // (sigmoid(z) - 1 = -sigmoid(-z)), so the target bit enters as one sign mask shared by s
-        // and dz — two 3-input bit ops — and sigmoid(s) never cancels against y.  a = exp(-|s|)
-        // once; log1p and 1/(1+a) from it.  The 16 factors 1 + a in (1, 2] of a lane's column are
-        // multiplied (<= 2^16) and one log2 per column taken: the log is a quarter-rate
-        // instruction; summed log2 scaled by ln 2 at the end
-        // store offsets: the lane part in a VGPR, the row part (r) as the scalar soffset
-        const uint32_t zv = 2u * (uint32_t)((rb + 4 * half) * LZ + n0 + col);
-        f32x2_t lprod = {1.f, 1.f}, rs2 = {0.f, 0.f}, cs2 = {0.f, 0.f};  // even / odd rows: packed math
-        // the 16 rows' target words: 4 runs of 4 consecutive rows -> 4 LDS reads of 16 B
-        uint4 yw[4];
+      // sigmoid_cross_entropy_with_logits (TF 2.5 Keras BCE on a sigmoid output):
+      //   loss = max(z, 0) - z y + log1p(exp(-|z|)),  dz = (sigmoid(z) - y) / (B V)
+      // in the target-signed logit s = (1 - 2y) z:
+      //   loss = max(s, 0) + log1p(exp(-|s|)),  dz = (1 - 2y) sigmoid(s) / (B V)
+      // (sigmoid(z) - 1 = -sigmoid(-z)), so sigmoid(s) never cancels against y.  The sign of s is
+      // a lane mask: [z < 0] (one compare into SGPRs) xor the target mask (a scalar op); then
+      // max(s, 0) = s < 0 ? 0 : |z|, sigmoid(s) = s < 0 ? a / (1 + a) : 1 / (1 + a) and dz's sign
+      // are one v_cndmask each (|z|, -x as source modifiers).  a = exp(-|z|) = exp2(-|z log2 e|)
+      // (the product packed for two rows, abs / neg folded into v_exp); log1p and 1/(1+a) from it.
+      // The 16 factors 1 + a in (1, 2] of a lane's column are multiplied (<= 2^16) and one log2
+      // per column taken: the log is a quarter-rate instruction; summed log2 scaled by ln 2 at the
+      // end.  Columns past |V| (the last slice) compute on clamped operands: their stores are
+      // dropped (zv) and their loss is masked per tile; their dZ^T columns feed only dWo columns
+      // that are never stored
+      // store offsets: the lane part in a VGPR, the row part (r) as the scalar soffset
+      const uint32_t zv = valid[j] ? 2u * (uint32_t)((rb + 4 * half) * LZ + n0 + col) : 0x80000000u;
+      f32x2_t lprod = {1.f, 1.f}, rs2 = {0.f, 0.f}, cs2 = {0.f, 0.f};  // even / odd rows: packed math
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-#ifdef DEC_DIAG_NOY   // diagnostic builds only: targets taken as all zero (no staging, no barrier)
-          yw[g] = make_uint4(0u, 0u, 0u, 0u);
-#else
-          yw[g] = *reinterpret_cast<const uint4 *>(ys + j * B + rb + 8 * g + 4 * half);
-#endif
+      for (int r2 = 0; r2 < 16; r2 += 2) {
+        const f32x2_t z2 = {acc[j][r2], acc[j][r2 + 1]};
+        const f32x2_t zl = z2 * l2e;
+        f32x2_t a2, rl2, sel2, dzp;
+        bool yb[2], sn[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          yb[e] = __builtin_amdgcn_inverse_ballot_w64(mk[r2 + e]);
+          sn[e] = (z2[e] < 0.f) != yb[e];   // s < 0
+          a2[e] = __builtin_amdgcn_exp2f(-fabsf(zl[e]));
+          rl2[e] = sn[e] ? 0.f : fabsf(z2[e]);
         }
-        const uint32_t ysh = 31u - (uint32_t)(lane & 31);   // the lane's target bit -> bit 31
+        const f32x2_t opa2 = 1.f + a2;
+        f32x2_t rp2;
 #pragma unroll
-        for (int r2 = 0; r2 < 16; r2 += 2) {
-          f32x2_t s2, a2, opa2, rp2, sel2, rl2;
-          uint32_t ym[2];
+        for (int e = 0; e < 2; ++e) rp2[e] = __builtin_amdgcn_rcpf(opa2[e]);
+        lprod *= opa2;
+        rs2 += rl2;
+        const f32x2_t arp2 = a2 * rp2;
 #pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const int r = r2 + e;
-            const uint32_t ywr = (r & 3) == 0 ? yw[r >> 2].x : (r & 3) == 1 ? yw[r >> 2].y : (r & 3) == 2 ? yw[r >> 2].z : yw[r >> 2].w;
-            ym[e] = ywr << ysh;
-            const float z = acc[j][r];
-            s2[e] = __uint_as_float(xor_sign(__float_as_uint(z), ym[e]));
-            a2[e] = __builtin_amdgcn_exp2f(-fabsf(z) * LOG2E);
-            rl2[e] = fmaxf(s2[e], 0.f);
-          }
-          opa2 = 1.f + a2;
+        for (int e = 0; e < 2; ++e) sel2[e] = sn[e] ? arp2[e] : rp2[e];   // sigmoid(s)
+        const f32x2_t mag2 = sel2 * scale;
 #pragma unroll
-          for (int e = 0; e < 2; ++e) rp2[e] = __builtin_amdgcn_rcpf(opa2[e]);
-          lprod *= opa2;
-          rs2 += rl2;
-          const f32x2_t arp2 = a2 * rp2;
-#pragma unroll
-          for (int e = 0; e < 2; ++e) sel2[e] = s2[e] >= 0.f ? rp2[e] : arp2[e];   // sigmoid(s)
-          const f32x2_t mag2 = sel2 * scale;
-          f32x2_t dzp;
-#pragma unroll
-          for (int e = 0; e < 2; ++e) dzp[e] = __uint_as_float(xor_sign(__float_as_uint(mag2[e]), ym[e]));
-          cs2 += dzp;   // the bias gradient sums the fp32 dz (the reference's arithmetic)
-          const uint32_t pk = bf16_pack2(dzp[0], dzp[1]);
-          tt[r2 >> 1] = pk;
-          DEC_STORE_PAIR(pk, r2);
-        }
-        lsum += __builtin_amdgcn_logf(lprod[0] * lprod[1]);
-        rsum += rs2[0] + rs2[1];
-        cs[j] += cs2[0] + cs2[1];
-      } else {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) tt[r] = 0;
+        for (int e = 0; e < 2; ++e) dzp[e] = yb[e] ? -mag2[e] : mag2[e];
+        cs2 += dzp;   // the bias gradient sums the fp32 dz (the reference's arithmetic)
+        const uint32_t pk = bf16_pack2(dzp[0], dzp[1]);
+        tt[r2 >> 1] = pk;
+        DEC_STORE_PAIR(pk, r2);
       }
+      lsum += valid[j] ? __builtin_amdgcn_logf(lprod[0] * lprod[1]) : 0.f;
+      rsum += valid[j] ? rs2[0] + rs2[1] : 0.f;
+      cs[j] += cs2[0] + cs2[1];
       // dZ^T image: registers 4g..4g+3 = 4 consecutive rows -> one 8-byte LDS store
 #pragma unroll
       for (int g = 0; g < 4; ++g)
@@ -477,39 +465,30 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   const bool pk = p.D3tp != nullptr;
   if constexpr (SPLIT2) {
     // A fragment (chunk kc, step kk) of d tile t: 1 KB contiguous from the packed D3^T image, or
-    // row-strided from D3^T
-    auto arow_t = [&](int t) -> const bf16_t * {
-      return pk ? p.D3tp + ((int64_t)t * (p.ldt / 16) * 64 + lane) * 8
-                : p.D3t + (int64_t)(t * 32 + (lane & 31)) * p.ldt + 8 * half;
+    // row-strided from D3^T (buffer loads: lane part in one VGPR, tile / chunk / step as the
+    // scalar offset — both layouts put tile t at t * ldt * 64 bytes)
+    const __amdgpu_buffer_rsrc_t t_rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(pk ? p.D3tp : p.D3t), (short)0, (uint32_t)d * (uint32_t)p.ldt * 2u, 0x00020000);
+    const uint32_t t_vo = pk ? (uint32_t)lane * 16u : (uint32_t)((lane & 31) * p.ldt + 8 * half) * 2u;
+    auto af_t = [&](int t, int kc, int kk) -> bf16x8_t {
+      const uint32_t so = (uint32_t)t * (uint32_t)p.ldt * 64u + (pk ? (uint32_t)(kc * 4 + kk) * 1024u : (uint32_t)(kc * BK + kk * 16) * 2u);
+      return __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(t_rs, t_vo, so, 0));
     };
-    auto af_t = [&](const bf16_t *ar, int kc, int kk) {
-      return *reinterpret_cast<const bf16x8_t *>(ar + (pk ? (kc * 4 + kk) * 512 : kc * BK + kk * 16));
-    };
-    const bool fast = __builtin_amdgcn_readfirstlane(w) < 4;   // (wave-uniform)
-    const bf16_t *ar = arow_t(w);
+    const bool fast = wu < 4;   // (wave-uniform)
     f32x16_t acc2[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
     // the partner's partial: 16 x 64 fp32 per 32-column tile, [j][group g][lane][4]
     float *part = reinterpret_cast<float *>(smem) + (w & 3) * (NJ * 16 * 64);
     static_assert(4 * NJ * 16 * 64 * 4 <= ZT_OFF, "dec_bce_dw_kernel: partials fit the Wo slice's LDS");
     if (fast) {
-      const bf16_t *arx = arow_t(w + 4);
       f32x16_t accx[NJ];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) accx[j][r] = 0.f;
       constexpr int KF[4] = {0, 1, 4, 5};
       bf16x8_t fa[2][4], fx[2][4];   // two chunks in flight
 #pragma unroll
       for (int q = 0; q < 2; ++q)
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
-          fa[q][kk] = af_t(ar, KF[q], kk);
-          fx[q][kk] = af_t(arx, KF[q], kk);
+          fa[q][kk] = af_t(wu, KF[q], kk);
+          fx[q][kk] = af_t(wu + 4, KF[q], kk);
         }
       while (__hip_atomic_load(&cnt_z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4) __builtin_amdgcn_s_sleep(1);
 #pragma unroll
@@ -520,14 +499,15 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 #pragma unroll
           for (int j = 0; j < NJ; ++j) {
             const bf16x8_t b = frag(Zt, sw_off(j * 32 + (lane & 31), kc * BK + kk * 16 + 8 * half, CHB));
-            acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q][kk], b, acc2[j], 0, 0, 0);
-            accx[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fx[q][kk], b, accx[j], 0, 0, 0);
+            const bool first = c == 0 && kk == 0;   // (static: the accumulators start at zero)
+            acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q][kk], b, first ? f32x16_t{} : acc2[j], 0, 0, 0);
+            accx[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fx[q][kk], b, first ? f32x16_t{} : accx[j], 0, 0, 0);
           }
         if (c + 2 < 4) {
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) {
-            fa[q][kk] = af_t(ar, KF[c + 2], kk);
-            fx[q][kk] = af_t(arx, KF[c + 2], kk);
+            fa[q][kk] = af_t(wu, KF[c + 2], kk);
+            fx[q][kk] = af_t(wu + 4, KF[c + 2], kk);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -540,6 +520,11 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
         for (int g = 0; g < 4; ++g)
           *reinterpret_cast<f32x4_t *>(part + ((j * 4 + g) * 64 + lane) * 4) =
               f32x4_t{accx[j][4 * g], accx[j][4 * g + 1], accx[j][4 * g + 2], accx[j][4 * g + 3]};
+    } else {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
     }
     // this wave's own tile, the slow half's chunks: fragments in flight across the barrier
     constexpr int KS[4] = {2, 3, 6, 7};
@@ -547,7 +532,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) fs[c][kk] = af_t(ar, KS[c], kk);
+      for (int kk = 0; kk < 4; ++kk) fs[c][kk] = af_t(wu, KS[c], kk);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // dZ^T rows, partials, red_cs, red_loss
     DEC_PROBE(6);
     if (tid < NB && n0 + tid < V) {
@@ -598,15 +583,16 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
   constexpr int P2D = 4;
   constexpr int nk2 = B / BK;
   constexpr int ND2 = (d + 255) / 256;   // 32-row d tiles per wave: w (and w + 8 at d = 512)
-  // A fragment (kc, kk) of d tile dt: row-strided from D3^T, or 1 KB contiguous from the packed image
-  auto arow_of = [&](int dt) -> const bf16_t * {
-    const int t = min(w + 8 * dt, d / 32 - 1);
-    return pk ? p.D3tp + ((int64_t)t * (p.ldt / 16) * 64 + lane) * 8
-              : p.D3t + (int64_t)(t * 32 + (lane & 31)) * p.ldt + 8 * half;
-  };
-  const bf16_t *arow = arow_of(0);
-  auto afrag = [&](int kc, int kk) {
-    return *reinterpret_cast<const bf16x8_t *>(arow + (pk ? (kc * 4 + kk) * 512 : kc * BK + kk * 16));
+  // A fragment (kc, kk) of d tile dt: row-strided from D3^T, or 1 KB contiguous from the packed
+  // image (buffer loads: lane part in one VGPR, tile / chunk / step as the scalar offset — both
+  // layouts put tile t at t * ldt * 64 bytes)
+  const __amdgpu_buffer_rsrc_t t_rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(pk ? p.D3tp : p.D3t), (short)0, (uint32_t)d * (uint32_t)p.ldt * 2u, 0x00020000);
+  const uint32_t t_vo = pk ? (uint32_t)lane * 16u : (uint32_t)((lane & 31) * p.ldt + 8 * half) * 2u;
+  uint32_t t_so = (uint32_t)min(wu, d / 32 - 1) * (uint32_t)p.ldt * 64u;
+  auto afrag = [&](int kc, int kk) -> bf16x8_t {
+    const uint32_t so = t_so + (pk ? (uint32_t)(kc * 4 + kk) * 1024u : (uint32_t)(kc * BK + kk * 16) * 2u);
+    return __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(t_rs, t_vo, so, 0));
   };
   bf16x8_t ring[P2D][4];
   auto fill_ring = [&]() {
@@ -632,7 +618,7 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 #pragma unroll 1
   for (int dt = 0; dt < ND2 && (w + 8 * dt) * 32 < d; ++dt) {
     if (dt > 0) {
-      arow = arow_of(dt);
+      t_so = (uint32_t)min(wu + 8 * dt, d / 32 - 1) * (uint32_t)p.ldt * 64u;
       fill_ring();
     }
     const int dr0 = (w + 8 * dt) * 32;   // this tile's first row of dWo
@@ -717,12 +703,13 @@ __global__ __launch_bounds__(NTH) void dec_bce_dw_kernel(DecOutP p) {
 
 }  // namespace
 
-extern "C" int cc_dec_bce_dw_ld(const void *D3, const void *D3t, int32_t ldt, const void *D3p,
-                                const void *D3tp, const void *WoT, const void *Wo,
-                                const float *bo, int32_t B, int32_t d, int32_t V, const uint32_t *y_bits,
-                                void *dZ, int32_t ldz, float *gW, float *gb, double *loss_partials,
-                                double *loss_out, double loss_scale, uint32_t *ticket, void *stream) {
-  CC_REQUIRE(ldz >= V && (int64_t)B * ldz * 2 <= 0xFFFFFFFFll, "cc_dec_bce_dw: ldz >= V, dZ below 4 GB");
+static int dec_bce_dw_launch(const void *D3, const void *D3t, int32_t ldt, const void *D3p, const void *D3tp,
+                             const void *WoT, const void *Wo, const float *bo, int32_t B, int32_t d, int32_t V,
+                             const uint32_t *y_bits, const uint32_t *y_img, void *dZ, int32_t ldz, float *gW,
+                             float *gb, double *loss_partials, double *loss_out, double loss_scale,
+                             uint32_t *ticket, void *stream) {
+  // (dZ below 2 GB: the stores of columns past |V| carry the byte offset 2^31, beyond the range)
+  CC_REQUIRE(ldz >= V && (int64_t)B * ldz * 2 <= 0x7FFFFFFFll, "cc_dec_bce_dw: ldz >= V, dZ below 2 GB");
   CC_REQUIRE(D3 && D3t && (WoT || Wo) && bo && y_bits && dZ && gW && gb && loss_partials,
              "cc_dec_bce_dw: null pointer");
   CC_REQUIRE(B == 128 || B == 256 || B == 512, "cc_dec_bce_dw: B must be 128, 256 or 512");
@@ -743,6 +730,8 @@ extern "C" int cc_dec_bce_dw_ld(const void *D3, const void *D3t, int32_t ldt, co
   p.Wo = (const bf16_t *)Wo;
   p.bo = bo;
   p.y_bits = y_bits;
+  CC_REQUIRE((((uintptr_t)y_img) & 127) == 0, "cc_dec_bce_dw: y_img 128-B aligned");
+  p.y_img = y_img;
   p.dZ = (bf16_t *)dZ;
   p.gW = gW;
   p.gb = gb;
@@ -751,6 +740,7 @@ extern "C" int cc_dec_bce_dw_ld(const void *D3, const void *D3t, int32_t ldt, co
   p.ticket = ticket;
   p.loss_scale = loss_scale;
   p.scale = 1.0f / ((float)B * (float)V);
+  p.log2e = LOG2E;
   p.V = V;
   p.ldt = ldt;
   p.ldz = ldz;
@@ -762,7 +752,9 @@ extern "C" int cc_dec_bce_dw_ld(const void *D3, const void *D3t, int32_t ldt, co
                    (int64_t)d * V * 2 <= 0xFFFFFFFFll && (int64_t)B * ((V + 31) / 32) * 4 <= 0xFFFFFFFFll;
 #define DO_LAUNCH(DD, BBB)                                                                    \
   if (d == DD && B == BBB) {                                                                  \
-    if (dma && DD <= 256)                                                                     \
+    if (dma && DD <= 256 && p.y_img)                                                          \
+      hipLaunchKernelGGL((dec_bce_dw_kernel<DD, BBB, DD <= 256, true>), grid, block, 0, s, p); \
+    else if (dma && DD <= 256)                                                                \
       hipLaunchKernelGGL((dec_bce_dw_kernel<DD, BBB, DD <= 256>), grid, block, 0, s, p);      \
     else                                                                                      \
       hipLaunchKernelGGL((dec_bce_dw_kernel<DD, BBB, false>), grid, block, 0, s, p);          \
@@ -773,6 +765,26 @@ extern "C" int cc_dec_bce_dw_ld(const void *D3, const void *D3t, int32_t ldt, co
 #undef DO_LAUNCH
   CC_LAUNCH_CHECK("dec_bce_dw_kernel");
   return CC_OK;
+}
+
+extern "C" int cc_dec_bce_dw_ld(const void *D3, const void *D3t, int32_t ldt, const void *D3p,
+                                const void *D3tp, const void *WoT, const void *Wo,
+                                const float *bo, int32_t B, int32_t d, int32_t V, const uint32_t *y_bits,
+                                void *dZ, int32_t ldz, float *gW, float *gb, double *loss_partials,
+                                double *loss_out, double loss_scale, uint32_t *ticket, void *stream) {
+  return dec_bce_dw_launch(D3, D3t, ldt, D3p, D3tp, WoT, Wo, bo, B, d, V, y_bits, nullptr, dZ, ldz, gW, gb,
+                           loss_partials, loss_out, loss_scale, ticket, stream);
+}
+
+extern "C" int cc_dec_bce_dw_img(const void *D3, const void *D3t, int32_t ldt, const void *D3p,
+                                 const void *D3tp, const void *WoT, const void *Wo,
+                                 const float *bo, int32_t B, int32_t d, int32_t V, const uint32_t *y_bits,
+                                 const uint32_t *y_img, void *dZ, int32_t ldz, float *gW, float *gb,
+                                 double *loss_partials, double *loss_out, double loss_scale, uint32_t *ticket,
+                                 void *stream) {
+  CC_REQUIRE(y_img, "cc_dec_bce_dw_img: null y_img");
+  return dec_bce_dw_launch(D3, D3t, ldt, D3p, D3tp, WoT, Wo, bo, B, d, V, y_bits, y_img, dZ, ldz, gW, gb,
+                           loss_partials, loss_out, loss_scale, ticket, stream);
 }
 
 extern "C" int cc_dec_bce_dw(const void *D3, const void *D3t, int32_t ldt, const void *D3p,

@@ -52,6 +52,9 @@ struct TowerP {
   uint32_t *xt;
   int xt_V, xt_rows;
   uint8_t *d3q, *d3qs, *d3tq, *d3tqs;  // D3's MX-FP8 operand images (config 5; wide forward only, or null)
+  const uint32_t *yb;       // y row bitmasks [B][y_VW] -> yimg (fast forward's extra blocks; or null)
+  uint32_t *yimg;
+  int y_VW;
   bool packed, dwpacked;
 };
 
@@ -450,8 +453,50 @@ __device__ __forceinline__ int bias_off(int i) {
 // layer's prefetched weight fragments, the copy-out stores) at each layer boundary.
 __device__ __forceinline__ void fast_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int D>
-__global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p) {
+// The fused D1 kernel's target-mask image (cc_tower_args.y_img, decout.hip): word column gw of the
+// y row bitmasks, rows in the order the MFMA accumulator registers hold them — within every 32-row
+// block, dword 2r + h = row (r & 3) + 8 (r >> 2) + 4h — so the 16 lane masks of one accumulator
+// tile are 128 contiguous bytes (two scalar 64-B loads).  One block per (32-row block, 64 word
+// columns): coalesced 256-B row reads into LDS, coalesced 128-B column writes.
+constexpr int YI_W = 64;
+__host__ __device__ inline int yimg_blocks(int B, int VW) { return (B / 32) * ((VW + YI_W - 1) / YI_W); }
+__device__ __forceinline__ void yimg_block(const uint32_t *__restrict__ yb, int VW, int B, uint32_t *__restrict__ yimg,
+                                           int tb) {
+  extern __shared__ uint32_t ysm[];   // [32][YI_W + 1] (the launch's dynamic LDS)
+  const int nrb = B / 32, rb = tb % nrb, w0 = (tb / nrb) * YI_W;
+  for (int i = threadIdx.x; i < 32 * YI_W; i += blockDim.x) {
+    const int row = i / YI_W, c = i % YI_W;
+    ysm[row * (YI_W + 1) + c] = w0 + c < VW ? yb[(int64_t)(rb * 32 + row) * VW + w0 + c] : 0u;
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < 32 * YI_W; o += blockDim.x) {
+    const int j = o / 32, pos = o % 32;
+    const int row = 8 * (pos >> 3) + 4 * (pos & 1) + ((pos >> 1) & 3);
+    if (w0 + j < VW) yimg[(int64_t)(w0 + j) * B + rb * 32 + pos] = ysm[row * (YI_W + 1) + j];
+  }
+}
+
+// ADAM (cc_tower_fwd_adam): blocks past the chains and the xt transposes run TF Adam over two flat
+// ranges — the previous step's deferred part of the output layers (their gradients final since
+// that step's output-layer kernels; nothing in this forward reads their bf16 shadows before the
+// output-layer kernel that follows this launch) — at step state[0] + step_off (the E1 gather of
+// this step has already advanced the counter: step_off = -1)
+template <int D, bool ADAM = false>
+__global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p, cc_adam::Args ad = {}, cc_adam::Args ad1 = {},
+                                                             const int64_t *ad_state = nullptr, int64_t step_off = 0,
+                                                             int nxt = 0) {
+  const int nyi = p.yimg ? yimg_blocks(p.B, p.y_VW) : 0;
+  if (ADAM && (int)blockIdx.x >= p.R / RB + nxt + nyi) {
+    const int b = (int)blockIdx.x - p.R / RB - nxt - nyi, nb = (int)gridDim.x - p.R / RB - nxt - nyi;
+    const int64_t step = ad_state[0] + step_off;
+    cc_adam::range_u<4>(ad, step, b, nb);
+    if (ad1.n > 0) cc_adam::range_u<4>(ad1, step, b, nb);
+    return;
+  }
+  if ((int)blockIdx.x >= p.R / RB + nxt) {  // then the target-mask image
+    yimg_block(p.yb, p.y_VW, p.B, p.yimg, (int)blockIdx.x - p.R / RB - nxt);
+    return;
+  }
   if ((int)blockIdx.x >= p.R / RB) {  // blocks past the chains: the xt transpose on the idle CUs
     xt_transpose_block(p.xb, p.xt_V, p.xt, p.xt_rows, (int)blockIdx.x - p.R / RB);
     return;
@@ -1313,6 +1358,9 @@ int make_params(const cc_tower_args *t, TowerP &p) {
   p.gpre1 = t->gpre1;
   p.gpre1t = t->dtype == CC_BF16 ? t->gpre1t : nullptr;
   p.gpre1p = t->dtype == CC_BF16 && t->d <= 256 ? static_cast<bf16_t *>(t->gpre1p) : nullptr;
+  p.yb = static_cast<const uint32_t *>(t->y_bits);
+  p.yimg = static_cast<uint32_t *>(t->y_img);
+  p.y_VW = t->y_V > 0 ? (t->y_V + 31) / 32 : 0;
   p.xb = static_cast<const uint32_t *>(t->x_bits);
   p.xt = static_cast<uint32_t *>(t->xt_bits);
   p.xt_V = t->xt_V;
@@ -1361,24 +1409,92 @@ int make_params(const cc_tower_args *t, TowerP &p) {
 
 extern "C" int64_t cc_tower_slab_elems(int32_t d) { return slab_off(d, 6); }
 
+// y_img (the fused D1 kernel's target-mask image) rides in the fast forward only
+static int check_yimg(const TowerP &p) {
+  CC_REQUIRE(!p.yimg || (p.yb && p.y_VW > 0 && p.d <= 256 && !p.d3q),
+             "cc_tower_fwd: y_img needs y_bits, y_V > 0 and the bf16 fast chains (d <= 256)");
+  CC_REQUIRE(!p.yimg || (size_t)2 * RB * (p.maxw + 8) * 2 >= (size_t)32 * (YI_W + 1) * 4,
+             "cc_tower_fwd: y_img transpose LDS");
+  return CC_OK;
+}
+
+static int cus_of_device() {
+  static int cus = 0;
+  if (cus <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+extern "C" int cc_tower_fwd_adam(const cc_tower_args *t, float *pp, float *m, float *v, const float *g,
+                                 uint16_t *shadow, int64_t lo0, int64_t n0, int64_t lo1, int64_t n1,
+                                 const int64_t *state, int64_t step_off, float lr, float beta1, float beta2,
+                                 float eps, void *stream) {
+  CC_REQUIRE(t && t->dtype == CC_BF16 && t->d <= 256, "cc_tower_fwd_adam: the bf16 fast chains (d <= 256) only");
+  CC_REQUIRE(pp && m && v && g && state, "cc_tower_fwd_adam: null pointer");
+  CC_REQUIRE(((uintptr_t)pp | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g) % 16 == 0 && lo0 % 4 == 0 && lo1 % 4 == 0,
+             "cc_tower_fwd_adam: buffers must be 16-byte aligned, range starts multiples of 4");
+  CC_REQUIRE(!shadow || (uintptr_t)shadow % 8 == 0, "cc_tower_fwd_adam: shadow must be 8-byte aligned");
+  CC_REQUIRE(lo0 >= 0 && n0 >= 0 && n1 >= 0 && (n1 == 0 || lo1 >= lo0 + n0), "cc_tower_fwd_adam: ranges");
+  CC_REQUIRE(step_off == 0 || step_off == -1, "cc_tower_fwd_adam: step_off is 0 or -1");
+  const int64_t n = n0 + n1;
+  if (n == 0) return cc_tower_fwd(t, stream);
+  TowerP p;
+  int rc = make_params(t, p);
+  if (rc) return rc;
+  CC_REQUIRE(!p.xt || (p.xb && p.xt_V > 0 && p.xt_rows >= 1 && p.xt_rows <= p.R),
+             "cc_tower_fwd_adam: xt_bits needs x_bits and 1 <= xt_rows <= R");
+  const cc_adam::Args a{pp + lo0, m + lo0, v + lo0, g + lo0, shadow ? (bf16_t *)shadow + lo0 : nullptr, n0,
+                        lr, beta1, beta2, eps, lo0};
+  const cc_adam::Args a1{pp + lo1, m + lo1, v + lo1, g + lo1, shadow ? (bf16_t *)shadow + lo1 : nullptr, n1,
+                         lr, beta1, beta2, eps, lo1};
+  const size_t lds = (size_t)2 * RB * (p.maxw + 8) * 2;
+  rc = check_yimg(p);
+  if (rc) return rc;
+  const int nxt = p.xt ? (int)cdiv((p.xt_V + 31) / 32, XT_TJ) : 0;
+  const int nyi = p.yimg ? yimg_blocks(p.B, p.y_VW) : 0;
+  // one 512-thread Adam block per CU the chains leave (dispatched after the chains and the
+  // transposes), capped so no block runs out of work
+  const int64_t want = cdiv(cdiv(n, 4), (int64_t)FNT * 4);
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(cus_of_device() - p.R / RB, 8)));
+  const dim3 gr((unsigned)(p.R / RB + nxt + nyi + blocks)), b(FNT);
+  hipStream_t s = as_stream(stream);
+  switch (p.d) {
+    case 64: hipLaunchKernelGGL((tower_fwd_fast_kernel<64, true>), gr, b, lds, s, p, a, a1, state, step_off, nxt); break;
+    case 128: hipLaunchKernelGGL((tower_fwd_fast_kernel<128, true>), gr, b, lds, s, p, a, a1, state, step_off, nxt); break;
+    case 192: hipLaunchKernelGGL((tower_fwd_fast_kernel<192, true>), gr, b, lds, s, p, a, a1, state, step_off, nxt); break;
+    default: hipLaunchKernelGGL((tower_fwd_fast_kernel<256, true>), gr, b, lds, s, p, a, a1, state, step_off, nxt); break;
+  }
+  CC_LAUNCH_CHECK("tower_fwd_fast_kernel (+ Adam)");
+  return CC_OK;
+}
+
 extern "C" int cc_tower_fwd(const cc_tower_args *t, void *stream) {
   TowerP p;
   int rc = make_params(t, p);
   if (rc) return rc;
   const int es = t->dtype == CC_BF16 ? 2 : 4;
   const size_t lds = (size_t)2 * RB * (p.maxw + 16 / es) * es;
+  rc = check_yimg(p);
+  if (rc) return rc;
+  CC_REQUIRE(!p.yimg || t->dtype == CC_BF16, "cc_tower_fwd: y_img needs the bf16 fast chains");
   CC_REQUIRE(!p.xt || (p.xb && t->dtype == CC_BF16 && p.d <= 256 && p.xt_V > 0 && p.xt_rows >= 1 &&
                        p.xt_rows <= p.R),
              "cc_tower_fwd: xt_bits needs x_bits, bf16, d <= 256 and 1 <= xt_rows <= R");
   if (t->dtype == CC_BF16 && p.d <= 256) {
     const int nxt = p.xt ? (int)cdiv((p.xt_V + 31) / 32, XT_TJ) : 0;
-    const dim3 g((unsigned)(p.R / RB + nxt)), b(FNT);
+    const int nyi = p.yimg ? yimg_blocks(p.B, p.y_VW) : 0;
+    const dim3 g((unsigned)(p.R / RB + nxt + nyi)), b(FNT);
     hipStream_t s = as_stream(stream);
+    const cc_adam::Args a0{};
     switch (p.d) {
-      case 64: hipLaunchKernelGGL(tower_fwd_fast_kernel<64>, g, b, lds, s, p); break;
-      case 128: hipLaunchKernelGGL(tower_fwd_fast_kernel<128>, g, b, lds, s, p); break;
-      case 192: hipLaunchKernelGGL(tower_fwd_fast_kernel<192>, g, b, lds, s, p); break;
-      default: hipLaunchKernelGGL(tower_fwd_fast_kernel<256>, g, b, lds, s, p); break;
+      case 64: hipLaunchKernelGGL(tower_fwd_fast_kernel<64>, g, b, lds, s, p, a0, a0, nullptr, (int64_t)0, nxt); break;
+      case 128: hipLaunchKernelGGL(tower_fwd_fast_kernel<128>, g, b, lds, s, p, a0, a0, nullptr, (int64_t)0, nxt); break;
+      case 192: hipLaunchKernelGGL(tower_fwd_fast_kernel<192>, g, b, lds, s, p, a0, a0, nullptr, (int64_t)0, nxt); break;
+      default: hipLaunchKernelGGL(tower_fwd_fast_kernel<256>, g, b, lds, s, p, a0, a0, nullptr, (int64_t)0, nxt); break;
     }
   }
   else if (t->dtype == CC_BF16 && p.packed)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CC_ABI_VERSION 1
+#define CC_ABI_VERSION 2   /* 2: cc_tower_args gained y_bits, y_img, y_V */
 
 enum cc_status {
   CC_OK = 0,
@@ -421,9 +421,26 @@ typedef struct cc_tower_args {
    * with d3qs [R][d/32] E8M0 scales (K = d), d3tq [d][R] with d3tqs [d][R/32] (K = batch rows) —
    * from the LDS copy it already holds (all four set, or none). */
   void *d3q, *d3qs, *d3tq, *d3tqs;
+  /* optional (bf16 fast chains, d <= 256): cc_tower_fwd also writes y_img [ceil(y_V/32)][B] uint32,
+   * the target row bitmasks y_bits [B][ceil(y_V/32)] transposed for the fused D1 kernel's lane masks
+   * (cc_dec_bce_dw_img): word column w, then the B rows with every 32-row block in accumulator-
+   * register order — dword 2r + h of a block = its row (r & 3) + 8 (r >> 2) + 4h — in extra blocks
+   * beside the chains (NULL: no). */
+  const void *y_bits;
+  void *y_img;
+  int32_t y_V;
 } cc_tower_args;
 int64_t cc_tower_slab_elems(int32_t d);
 int cc_tower_fwd(const cc_tower_args *t, void *stream);
+/* cc_tower_fwd (the bf16 fast chains, d <= 256, with their optional xt transposes) plus, in extra
+ * workgroups of the same launch after the chains and the transposes, exactly cc_adam_dense over
+ * [lo0, lo0 + n0) and [lo1, lo1 + n1) of p, m, v, g, shadow at step state[0] + step_off (step_off
+ * 0 or -1) — the previous step's deferred Adam on the decoder output layers' leading parts: their
+ * gradients are final, and the forward reads neither them nor their shadows (the trainer's
+ * TrainConfig.wo_adam_in_fwd; the reference's update is train.py:84 ResourceApplyAdam). */
+int cc_tower_fwd_adam(const cc_tower_args *t, float *p, float *m, float *v, const float *g, uint16_t *shadow,
+                      int64_t lo0, int64_t n0, int64_t lo1, int64_t n1, const int64_t *state, int64_t step_off,
+                      float lr, float beta1, float beta2, float eps, void *stream);
 int cc_tower_bwd(const cc_tower_args *t, void *stream);
 /* cc_tower_bwd = cc_tower_bwd_chain (dX chain; writes gpre1 and every layer's dPre) followed by
  * cc_tower_bwd_dw (per-block dW/db slabs); split so the slabs can overlap the E1 scatter. */
@@ -486,6 +503,13 @@ int cc_dec_bce_dw_ld(const void *D3, const void *D3t, int32_t ldt, const void *D
                      const void *WoT, const void *Wo, const float *bo, int32_t B, int32_t d, int32_t V,
                      const uint32_t *y_bits, void *dZ, int32_t ldz, float *gW, float *gb, double *loss_partials,
                      double *loss_out, double loss_scale, uint32_t *ticket, void *stream);
+/* cc_dec_bce_dw_ld with the targets also as y_img (cc_tower_args.y_img, 128-B aligned, written from
+ * this y_bits by the tower forward launch): the epilogue's lane masks then come in two scalar 64-B
+ * loads per 32-column tile instead of 32 scattered word loads.  Same results, bit for bit. */
+int cc_dec_bce_dw_img(const void *D3, const void *D3t, int32_t ldt, const void *D3p, const void *D3tp,
+                      const void *WoT, const void *Wo, const float *bo, int32_t B, int32_t d, int32_t V,
+                      const uint32_t *y_bits, const uint32_t *y_img, void *dZ, int32_t ldz, float *gW, float *gb,
+                      double *loss_partials, double *loss_out, double loss_scale, uint32_t *ticket, void *stream);
 int32_t cc_dec_bce_dw_blocks(int32_t V);
 /* D2 softmax + KL on materialised fp32 logits Z2 [B][V] (model.py:98, train.py:85, TF 2.5 clip
  * semantics): row b uses the M~ row y_reg + reg_idx[b] * V; dZ[b] = scale * ([p >= 1e-7](-t) +

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
         assert s in L.SIGNATURES, f'{s} not bound in _lib.SIGNATURES'
-    assert lib.cc_abi_version() == 1
+    assert lib.cc_abi_version() == 2
 
 
 def test_param_layout_matches_python_mirror():

@@ -518,6 +518,17 @@ def test_dec_bce_dw_matches_unfused(B, d, V):
            L.stream_ptr())
     torch.cuda.synchronize()
     assert torch.equal(dZ, dZw) and torch.equal(gW, gWw) and torch.equal(gb, gbw) and torch.equal(loss, lossw)
+    # ... and so does the target-mask image (cc_tower_args.y_img; the trainer's call): the epilogue's
+    # lane masks from two scalar loads per tile instead of 32 scattered target words
+    pos = torch.arange(32)
+    row = 8 * (pos >> 3) + 4 * (pos & 1) + ((pos >> 1) & 3)
+    yimg = ybits[(torch.arange(B // 32)[:, None] * 32 + row[None, :]).reshape(-1).cuda()].t().contiguous()
+    dZi, gWi, gbi, lossi = torch.zeros_like(dZ), torch.zeros_like(gW), torch.zeros_like(gb), torch.zeros_like(loss)
+    L.call('cc_dec_bce_dw_img', L.ptr(D3), L.ptr(D3t), B, L.ptr(D3p), L.ptr(D3tp), None, L.ptr(Wo), L.ptr(bo), B, d,
+           V, L.ptr(ybits), L.ptr(yimg), L.ptr(dZi), V, L.ptr(gWi), L.ptr(gbi), L.ptr(part), L.ptr(lossi), scale,
+           L.ptr(tick), L.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dZ, dZi) and torch.equal(gW, gWi) and torch.equal(gb, gbi) and torch.equal(loss, lossi)
     # unfused
     dZ2 = torch.zeros(B, V, **bf)
     dZt = torch.zeros(V, B, **bf)
