@@ -29,11 +29,6 @@ def parse():
     ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--wo-tower-frac', type=float, default=-1.0,
                     help="the trailing fraction of Wo's Adam run in the tower backward launch (-1: TrainConfig's default)")
-    ap.add_argument('--wo-fwd', type=int, default=1, choices=(0, 1),
-                    help="one process: the Adam launch's share of the output layers in the next step's tower "
-                         "forward launch (1) or the Adam launch (0)")
-    ap.add_argument("--wo-fwd-frac", type=float, default=0.3,
-                    help='... the trailing fraction of that share moved (TrainConfig.wo_fwd_frac)')
     ap.add_argument('--f-in-tower', type=int, default=0,
                     help='one process: the next step\'s F in the tower backward launch (1) or the Adam launch (0)')
     ap.add_argument('--dx-packed-wo', type=int, default=1,
@@ -171,8 +166,6 @@ def roofline_for(name, ms, tr):
             n -= tr.w1_off
         for lo, hi in (getattr(tr, 'wo_ranges', None) or ()):   # (the output layers' tails: in the
             n -= hi - lo                                          # tower backward launch)
-        for lo, hi in (getattr(tr, 'fwd_ranges', None) or ()):  # (their leading parts: in the next
-            n -= hi - lo                                          # step's tower forward launch)
         byt = n * (16 + 12 + 2)                    # read p,m,v,g; write p,m,v; write bf16 shadow
         what = ('adam_noise_kernel (TF Adam over the parameters not updated elsewhere + F of the next step; '
                 'bytes counted are Adam\'s only, F adds <2%)' if getattr(tr, 'prefetch', False)
@@ -511,7 +504,6 @@ def main():
                       fuse_w1_adam=True,   # one process: W1's Adam in its gradient kernel, and (BCE
                       wo_adam_in_tower=True,   # only) Wo's in the tower backward launch, with the next
                       f_in_tower=bool(args.f_in_tower),   # step's F (parity:
-                      wo_adam_in_fwd=bool(args.wo_fwd), wo_fwd_frac=args.wo_fwd_frac,
                       dx_packed_wo=bool(args.dx_packed_wo))
     #                                        tests/test_gpu_train.py::test_fused_w1_adam_matches_unfused)
     tr = Trainer(cfg, data, params_flat=glorot_flat(V, d, seed=42), device=dev)

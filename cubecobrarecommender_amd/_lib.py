@@ -164,8 +164,6 @@ SIGNATURES = {
     'cc_noise_next': (C.c_int, [C.POINTER(NoiseArgs), _I64, _P]),
     'cc_tower_slab_elems': (_I64, [_I32]),
     'cc_tower_fwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
-    'cc_tower_fwd_adam': (C.c_int, [C.POINTER(TowerArgs), _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _P, _I64,
-                                    _F32, _F32, _F32, _F32, _P]),
     'cc_tower_bwd': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_bwd_chain': (C.c_int, [C.POINTER(TowerArgs), _P]),
     'cc_tower_bwd_chain_adam': (C.c_int, [C.POINTER(TowerArgs), _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _P,

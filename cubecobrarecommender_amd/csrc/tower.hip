@@ -476,23 +476,9 @@ __device__ __forceinline__ void yimg_block(const uint32_t *__restrict__ yb, int 
   }
 }
 
-// ADAM (cc_tower_fwd_adam): blocks past the chains and the xt transposes run TF Adam over two flat
-// ranges — the previous step's deferred part of the output layers (their gradients final since
-// that step's output-layer kernels; nothing in this forward reads their bf16 shadows before the
-// output-layer kernel that follows this launch) — at step state[0] + step_off (the E1 gather of
-// this step has already advanced the counter: step_off = -1)
-template <int D, bool ADAM = false>
-__global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p, cc_adam::Args ad = {}, cc_adam::Args ad1 = {},
-                                                             const int64_t *ad_state = nullptr, int64_t step_off = 0,
-                                                             int nxt = 0) {
-  const int nyi = p.yimg ? yimg_blocks(p.B, p.y_VW) : 0;
-  if (ADAM && (int)blockIdx.x >= p.R / RB + nxt + nyi) {
-    const int b = (int)blockIdx.x - p.R / RB - nxt - nyi, nb = (int)gridDim.x - p.R / RB - nxt - nyi;
-    const int64_t step = ad_state[0] + step_off;
-    cc_adam::range_u<4>(ad, step, b, nb);
-    if (ad1.n > 0) cc_adam::range_u<4>(ad1, step, b, nb);
-    return;
-  }
+// blocks [R/RB, R/RB + nxt): the xt transposes; then the target-mask image's blocks
+template <int D>
+__global__ __launch_bounds__(FNT) void tower_fwd_fast_kernel(TowerP p, int nxt) {
   if ((int)blockIdx.x >= p.R / RB + nxt) {  // then the target-mask image
     yimg_block(p.yb, p.y_VW, p.B, p.yimg, (int)blockIdx.x - p.R / RB - nxt);
     return;
@@ -1418,60 +1404,6 @@ static int check_yimg(const TowerP &p) {
   return CC_OK;
 }
 
-static int cus_of_device() {
-  static int cus = 0;
-  if (cus <= 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-  }
-  return cus;
-}
-
-extern "C" int cc_tower_fwd_adam(const cc_tower_args *t, float *pp, float *m, float *v, const float *g,
-                                 uint16_t *shadow, int64_t lo0, int64_t n0, int64_t lo1, int64_t n1,
-                                 const int64_t *state, int64_t step_off, float lr, float beta1, float beta2,
-                                 float eps, void *stream) {
-  CC_REQUIRE(t && t->dtype == CC_BF16 && t->d <= 256, "cc_tower_fwd_adam: the bf16 fast chains (d <= 256) only");
-  CC_REQUIRE(pp && m && v && g && state, "cc_tower_fwd_adam: null pointer");
-  CC_REQUIRE(((uintptr_t)pp | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g) % 16 == 0 && lo0 % 4 == 0 && lo1 % 4 == 0,
-             "cc_tower_fwd_adam: buffers must be 16-byte aligned, range starts multiples of 4");
-  CC_REQUIRE(!shadow || (uintptr_t)shadow % 8 == 0, "cc_tower_fwd_adam: shadow must be 8-byte aligned");
-  CC_REQUIRE(lo0 >= 0 && n0 >= 0 && n1 >= 0 && (n1 == 0 || lo1 >= lo0 + n0), "cc_tower_fwd_adam: ranges");
-  CC_REQUIRE(step_off == 0 || step_off == -1, "cc_tower_fwd_adam: step_off is 0 or -1");
-  const int64_t n = n0 + n1;
-  if (n == 0) return cc_tower_fwd(t, stream);
-  TowerP p;
-  int rc = make_params(t, p);
-  if (rc) return rc;
-  CC_REQUIRE(!p.xt || (p.xb && p.xt_V > 0 && p.xt_rows >= 1 && p.xt_rows <= p.R),
-             "cc_tower_fwd_adam: xt_bits needs x_bits and 1 <= xt_rows <= R");
-  const cc_adam::Args a{pp + lo0, m + lo0, v + lo0, g + lo0, shadow ? (bf16_t *)shadow + lo0 : nullptr, n0,
-                        lr, beta1, beta2, eps, lo0};
-  const cc_adam::Args a1{pp + lo1, m + lo1, v + lo1, g + lo1, shadow ? (bf16_t *)shadow + lo1 : nullptr, n1,
-                         lr, beta1, beta2, eps, lo1};
-  const size_t lds = (size_t)2 * RB * (p.maxw + 8) * 2;
-  rc = check_yimg(p);
-  if (rc) return rc;
-  const int nxt = p.xt ? (int)cdiv((p.xt_V + 31) / 32, XT_TJ) : 0;
-  const int nyi = p.yimg ? yimg_blocks(p.B, p.y_VW) : 0;
-  // one 512-thread Adam block per CU the chains leave (dispatched after the chains and the
-  // transposes), capped so no block runs out of work
-  const int64_t want = cdiv(cdiv(n, 4), (int64_t)FNT * 4);
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::max(cus_of_device() - p.R / RB, 8)));
-  const dim3 gr((unsigned)(p.R / RB + nxt + nyi + blocks)), b(FNT);
-  hipStream_t s = as_stream(stream);
-  switch (p.d) {
-    case 64: hipLaunchKernelGGL((tower_fwd_fast_kernel<64, true>), gr, b, lds, s, p, a, a1, state, step_off, nxt); break;
-    case 128: hipLaunchKernelGGL((tower_fwd_fast_kernel<128, true>), gr, b, lds, s, p, a, a1, state, step_off, nxt); break;
-    case 192: hipLaunchKernelGGL((tower_fwd_fast_kernel<192, true>), gr, b, lds, s, p, a, a1, state, step_off, nxt); break;
-    default: hipLaunchKernelGGL((tower_fwd_fast_kernel<256, true>), gr, b, lds, s, p, a, a1, state, step_off, nxt); break;
-  }
-  CC_LAUNCH_CHECK("tower_fwd_fast_kernel (+ Adam)");
-  return CC_OK;
-}
-
 extern "C" int cc_tower_fwd(const cc_tower_args *t, void *stream) {
   TowerP p;
   int rc = make_params(t, p);
@@ -1489,12 +1421,11 @@ extern "C" int cc_tower_fwd(const cc_tower_args *t, void *stream) {
     const int nyi = p.yimg ? yimg_blocks(p.B, p.y_VW) : 0;
     const dim3 g((unsigned)(p.R / RB + nxt + nyi)), b(FNT);
     hipStream_t s = as_stream(stream);
-    const cc_adam::Args a0{};
     switch (p.d) {
-      case 64: hipLaunchKernelGGL(tower_fwd_fast_kernel<64>, g, b, lds, s, p, a0, a0, nullptr, (int64_t)0, nxt); break;
-      case 128: hipLaunchKernelGGL(tower_fwd_fast_kernel<128>, g, b, lds, s, p, a0, a0, nullptr, (int64_t)0, nxt); break;
-      case 192: hipLaunchKernelGGL(tower_fwd_fast_kernel<192>, g, b, lds, s, p, a0, a0, nullptr, (int64_t)0, nxt); break;
-      default: hipLaunchKernelGGL(tower_fwd_fast_kernel<256>, g, b, lds, s, p, a0, a0, nullptr, (int64_t)0, nxt); break;
+      case 64: hipLaunchKernelGGL(tower_fwd_fast_kernel<64>, g, b, lds, s, p, nxt); break;
+      case 128: hipLaunchKernelGGL(tower_fwd_fast_kernel<128>, g, b, lds, s, p, nxt); break;
+      case 192: hipLaunchKernelGGL(tower_fwd_fast_kernel<192>, g, b, lds, s, p, nxt); break;
+      default: hipLaunchKernelGGL(tower_fwd_fast_kernel<256>, g, b, lds, s, p, nxt); break;
     }
   }
   else if (t->dtype == CC_BF16 && p.packed)

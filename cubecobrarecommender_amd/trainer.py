@@ -48,11 +48,6 @@ class TrainConfig:
     wo_tower_frac: float = -1.0    # ... on this trailing fraction of each; the rest stays in the Adam + F
     #                                launch (< 0: measured per mode — 0.6 BCE only, 0.55 with the
     #                                sampled regulariser; bench.py --wo-tower-frac sweeps)
-    wo_adam_in_fwd: bool = False   # with wo_adam_in_tower: the Adam + F launch's share of the output layers
-    #                                (their leading parts) deferred to the NEXT step's tower forward launch
-    #                                (cc_tower_fwd_adam, beside its 16-32 latency-bound chain blocks); flush()
-    #                                applies a pending one (bench.py)
-    wo_fwd_frac: float = 1.0       # ... the trailing fraction of that share (the rest stays in the Adam launch)
     dx_splits: int = 0             # decoder dX K-splits (0: measured default, 32 bf16 / 16 fp8)
     dx_splits_reg: int = 0         # ... of the full-mode regulariser branch (0: 4)
     dx_packed_wo: bool = True      # full-mode regulariser dX from Wo's fragment image (cc_gemm_dx_splitk_pk)
@@ -530,24 +525,6 @@ class Trainer:
                     lo = b
                 self.rest_ranges = rest
         self.wo_range = self.wo_ranges[0] if self.wo_ranges else None   # (tests: is the placement on)
-        # the Adam launch's share of the output layers (Wo from its first element up to the tower
-        # launch's range; with the regulariser the same for Wo_reg) deferred — its trailing
-        # wo_fwd_frac — to the next step's tower forward launch (cc_tower_fwd_adam): nothing from
-        # the Adam launch to that forward's output-layer kernel reads these parameters, their
-        # moments, their gradients or their bf16 shadows.  fwd_ranges: the deferred [lo, hi)
-        # ranges; rest_ranges shrinks to what is left
-        self.fwd_ranges = None
-        if cfg.wo_adam_in_fwd and self.wo_ranges is not None:
-            lay = self.layout
-            heads = [lay.offset('decoder/reconstruct/kernel')]
-            if self.use_reg:
-                heads.append(lay.offset('decoder_for_reg/reconstruct/kernel'))
-            ff = min(max(float(cfg.wo_fwd_frac), 0.0), 1.0)
-            fwd = [(a - int((a - h) * ff) // 256 * 256, a) for h, (a, _) in zip(heads, self.wo_ranges)]
-            if all(lo < hi for lo, hi in fwd):
-                self.fwd_ranges = fwd
-                self.rest_ranges = [(lo, f0) for (lo, _), (f0, _) in zip(self.rest_ranges, fwd)]
-        self._fwd_adam_pending = False   # the previous step's deferred output-layer Adam rides in the tower forward
         # the next step's F in the tower backward launch: one process with F prefetched (xt bits by
         # the tower forward's transpose, so F sets none the W1 gradient still reads), the packed
         # Adam launch, the fast bf16 chains
@@ -917,19 +894,11 @@ class Trainer:
                L.ptr(self.state) if self._adv_deferred else None, self.batches_per_epoch,
                L.ptr(self.x_bits) if self.xt_in_gather and not self.xt_in_tower else None,
                L.ptr(self.xt_bits) if self.xt_in_gather and not self.xt_in_tower else None, self.xt_rows, s)
-        adv, self._adv_deferred = self._adv_deferred, False   # (the counter now counts this step)
+        self._adv_deferred = False
         t()
         branches = self.branches()
         Br = self.Breg
-        if self.fused_tower and self._fwd_adam_pending:   # + the previous step's deferred output-layer Adam
-            self._fwd_adam_pending = False
-            t = self._tick('cc_tower_fwd')
-            (a0, b0), (a1, b1) = self.fwd_ranges[0], (list(self.fwd_ranges[1:]) + [(0, 0)])[0]
-            L.call('cc_tower_fwd_adam', L.C.byref(self.targs), L.ptr(self.params), L.ptr(self.m), L.ptr(self.v),
-                   L.ptr(self.grads), L.ptr(self.shadow), a0, b0 - a0, a1, b1 - a1, L.ptr(self.state),
-                   -1 if adv else 0, cfg.lr, cfg.beta1, cfg.beta2, cfg.eps, s)
-            t()
-        elif self.fused_tower:
+        if self.fused_tower:
             t = self._tick('cc_tower_fwd')
             L.call('cc_tower_fwd', L.C.byref(self.targs), s)
             t()
@@ -1341,17 +1310,9 @@ class Trainer:
         (the decoder's Wo^T on the side stream, concurrently)."""
         if self.adam_packs:   # packed tower images already written by the Adam launch
             self.refresh_decoder_operands(L.stream_ptr(stream))
-            if defer:         # counters: in the next forward's E1 gather launch (and the deferred
-                self._adv_deferred = True   # output-layer Adam in its tower forward launch)
-                self._fwd_adam_pending = self.fwd_ranges is not None
+            if defer:         # counters: in the next forward's E1 gather launch
+                self._adv_deferred = True
             else:
-                if self.fwd_ranges is not None:   # the deferred output-layer Adam, at this step's count
-                    self._fwd_adam_pending = False
-                    cfg = self.cfg
-                    for lo, hi in self.fwd_ranges:
-                        L.call('cc_adam_dense', L.ptr(self.params[lo:]), L.ptr(self.m[lo:]), L.ptr(self.v[lo:]),
-                               L.ptr(self.grads[lo:]), L.ptr(self.shadow[lo:]), hi - lo, L.ptr(self.state),
-                               cfg.lr, cfg.beta1, cfg.beta2, cfg.eps, L.stream_ptr(stream))
                 L.call('cc_state_advance', L.ptr(self.state), self.batches_per_epoch, L.stream_ptr(stream))
             return
         if self.fused_tower and stream is None:

@@ -432,15 +432,6 @@ typedef struct cc_tower_args {
 } cc_tower_args;
 int64_t cc_tower_slab_elems(int32_t d);
 int cc_tower_fwd(const cc_tower_args *t, void *stream);
-/* cc_tower_fwd (the bf16 fast chains, d <= 256, with their optional xt transposes) plus, in extra
- * workgroups of the same launch after the chains and the transposes, exactly cc_adam_dense over
- * [lo0, lo0 + n0) and [lo1, lo1 + n1) of p, m, v, g, shadow at step state[0] + step_off (step_off
- * 0 or -1) — the previous step's deferred Adam on the decoder output layers' leading parts: their
- * gradients are final, and the forward reads neither them nor their shadows (the trainer's
- * TrainConfig.wo_adam_in_fwd; the reference's update is train.py:84 ResourceApplyAdam). */
-int cc_tower_fwd_adam(const cc_tower_args *t, float *p, float *m, float *v, const float *g, uint16_t *shadow,
-                      int64_t lo0, int64_t n0, int64_t lo1, int64_t n1, const int64_t *state, int64_t step_off,
-                      float lr, float beta1, float beta2, float eps, void *stream);
 int cc_tower_bwd(const cc_tower_args *t, void *stream);
 /* cc_tower_bwd = cc_tower_bwd_chain (dX chain; writes gpre1 and every layer's dPre) followed by
  * cc_tower_bwd_dw (per-block dW/db slabs); split so the slabs can overlap the E1 scatter. */

@@ -81,12 +81,11 @@ def test_bench_configuration_matches_oracle(reg):
     y_mtx = adjacency_normalised_gpu(indptr, indices, V, device='cuda') if reg > 0 else None
     data = DeviceDataset(csr=(indptr, indices), num_cards=V, neg_sampler=ns, y_mtx=y_mtx, device='cuda')
     cfg = TrainConfig(V=V, d=d, batch_size=B, reg=reg, dtype='bf16', seed=1234,
-                      fuse_w1_adam=True, wo_adam_in_tower=True, wo_adam_in_fwd=True)   # exactly bench.py's
-    flat = glorot_flat(V, d, seed=42)                                                       # TrainConfig
+                      fuse_w1_adam=True, wo_adam_in_tower=True)    # exactly bench.py's TrainConfig
+    flat = glorot_flat(V, d, seed=42)
     tr = Trainer(cfg, data, params_flat=flat)
     assert tr.fused_out and tr.adam_packs and tr.prefetch and tr.wpack is not None and tr.fuse_w1
     assert tr.wo_ranges is not None and len(tr.wo_ranges) == (2 if reg > 0 else 1)
-    assert tr.fwd_ranges is not None and len(tr.fwd_ranges) == (2 if reg > 0 else 1)
     perm = np.random.default_rng(99).permutation(C).astype(np.int32)
     tr.set_epoch_permutations(perm[None, :])
     tr.capture()
@@ -99,7 +98,6 @@ def test_bench_configuration_matches_oracle(reg):
     lay = Layout(V, d)
     n1 = V * d
     for step in range(3):
-        tr.flush()   # (the previous step's deferred output-layer Adam: the parameters this step sees)
         P = lay.unpack(tr.standard(tr.params))
         m0 = tr.m[:n1].double().cpu().numpy()
         v0 = tr.v[:n1].double().cpu().numpy()

@@ -338,26 +338,19 @@ def test_fused_w1_adam_matches_unfused(reg):
     backward launch (cc_tower_bwd_chain_adam, cc_adam::range_u) and the rest in two ranges of the
     Adam + F launch (cc_adam_noise_pack2) — the same bits again; and with f_in_tower, the next step's
     F drawn by the tower backward launch (cc_tower_bwd_chain_noise, two cubes per workgroup) and the
-    Adam launch without it (cc_adam_pack2).  With wo_adam_in_fwd (bench.py): the Adam launch's share
-    of the output layers deferred to the next step's tower forward launch (cc_tower_fwd_adam, at the
-    step count before the E1 gather's advance) or, when no step follows, to flush() — the same bits
-    (wo_fwd_frac 0.5: half of that share moved, the rest in the Adam launch)."""
+    Adam launch without it (cc_adam_pack2)."""
     out = {}
-    keys = ((False, False, False, 0.0), (True, False, False, 0.0), (True, True, False, 0.0), (True, True, True, 0.0),
-            (True, False, True, 0.0), (True, True, False, 1.0), (True, True, True, 1.0), (True, True, False, 0.5))
-    for fuse, wo, ft, fw in keys:
+    for fuse, wo, ft in ((False, False, False), (True, False, False), (True, True, False), (True, True, True),
+                         (True, False, True)):
         lists, Mt, ns = problem(11, 1024, 2500, (20, 40, 80))
         P = model_ref.init_params(2500, 256, seed=11, bias_std=0.01)
         lay = Layout(2500, 256)
         cfg = TrainConfig(V=2500, d=256, batch_size=256, reg=reg, dtype='bf16', seed=11, fuse_w1_adam=fuse,
-                          wo_adam_in_tower=wo, f_in_tower=ft, wo_adam_in_fwd=fw > 0, wo_fwd_frac=fw)
+                          wo_adam_in_tower=wo, f_in_tower=ft)
         tr = Trainer(cfg, DeviceDataset(lists, 2500, y_mtx=Mt.astype(np.float32) if reg > 0 else None,
                                         neg_sampler=ns), params_flat=lay.pack(P))
         tr.set_epoch_permutation(np.random.default_rng(11).permutation(1024).astype(np.int32))
         assert tr.fuse_w1 == fuse and tr.adam_packs and (tr.wo_range is not None) == wo and tr.f_in_tower == ft
-        assert (tr.fwd_ranges is not None) == (fw > 0)
-        if fw > 0:
-            assert len(tr.fwd_ranges) == (2 if reg > 0 else 1)
         losses = []
         for _ in range(2):
             tr.step()
@@ -368,29 +361,27 @@ def test_fused_w1_adam_matches_unfused(reg):
             losses.append(tr.losses())
         tr.flush()
         torch.cuda.synchronize()
-        out[fuse, wo, ft, fw] = (tr.params.cpu(), tr.m.cpu(), tr.v.cpu(), tr.shadow.cpu(), losses)
-    base = out[keys[0]]
-    for key in keys[1:]:
+        out[fuse, wo, ft] = (tr.params.cpu(), tr.m.cpu(), tr.v.cpu(), tr.shadow.cpu(), losses)
+    base = out[False, False, False]
+    for key in ((True, False, False), (True, True, False), (True, True, True), (True, False, True)):
         for a, b in zip(base[:4], out[key][:4]):
             assert torch.equal(a, b), key
         assert base[4] == out[key][4], key
 
 
-@pytest.mark.parametrize('reg,ft,fw', [(0.0, False, False), (0.1, False, False), (0.0, True, False), (0.1, True, False),
-                                       (0.0, False, True), (0.1, False, True)])
-def test_step_many_multi_graph_matches_single_steps(reg, ft, fw):
+@pytest.mark.parametrize('reg,ft', [(0.0, False), (0.1, False), (0.0, True), (0.1, True)])
+def test_step_many_multi_graph_matches_single_steps(reg, ft):
     """step_many — graph_steps (here 4; remainders by the graphs of its halves) whole steps per captured graph replay, the loss
     accumulated inside the graph — gives bit-identical parameters, moments, shadow, device
     counters and accumulated losses to the same number of single step() calls (bench.py's
-    configuration: fused W1 / Wo Adam placement, and the deferred output-layer Adam in the next
-    tower forward launch)."""
+    configuration: fused W1 / Wo Adam placement)."""
     out = {}
     for multi in (False, True):
         lists, Mt, ns = problem(13, 1024, 2500, (20, 40, 80))
         P = model_ref.init_params(2500, 256, seed=13, bias_std=0.01)
         lay = Layout(2500, 256)
         cfg = TrainConfig(V=2500, d=256, batch_size=128, reg=reg, dtype='bf16', seed=13, fuse_w1_adam=True,
-                          wo_adam_in_tower=True, f_in_tower=ft, graph_steps=4 if multi else 1, wo_adam_in_fwd=fw)
+                          wo_adam_in_tower=True, f_in_tower=ft, graph_steps=4 if multi else 1)
         tr = Trainer(cfg, DeviceDataset(lists, 2500, y_mtx=Mt.astype(np.float32) if reg > 0 else None,
                                         neg_sampler=ns), params_flat=lay.pack(P))
         tr.set_epoch_permutation(np.random.default_rng(13).permutation(1024).astype(np.int32))
@@ -664,7 +655,7 @@ def test_reg_rows_by_index_bit_identical(d, dtype, fused):
     np.testing.assert_array_equal(v1, v0)
 
 
-@pytest.mark.parametrize('V,B', [(2500, 128), (2504, 256), (700, 64)])
+@pytest.mark.parametrize('V,B', [(2500, 128), (2504, 256), (700, 512)])
 def test_tower_forward_writes_target_mask_image(V, B):
     """The tower forward launch's extra blocks write the fused D1 kernel's target-mask image
     (cc_tower_args.y_img): y_bits word-column major, every 32-row block's rows in accumulator-
