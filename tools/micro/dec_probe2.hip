@@ -53,10 +53,18 @@ int main() {
   (void)hipMalloc(&bo, V * 4);
   (void)hipMemset(bo, 0, V * 4);
   (void)hipMalloc(&yb, (size_t)B * VW * 4);
+  void *yi;   // the target-mask image (cc_tower_args.y_img): the trainer's call, cc_dec_bce_dw_img
+  (void)hipMalloc(&yi, (size_t)B * VW * 4);
   {
-    std::vector<uint32_t> y((size_t)B * VW);
+    std::vector<uint32_t> y((size_t)B * VW), img((size_t)B * VW);
     for (auto &x : y) x = (rng() & rng() & rng() & rng() & rng()) ;  // ~3 % ones
+    for (int w = 0; w < VW; ++w)
+      for (int r = 0; r < B; ++r) {
+        const int pos = r & 31, row = (r & ~31) + 8 * (pos >> 3) + 4 * (pos & 1) + ((pos >> 1) & 3);
+        img[(size_t)w * B + r] = y[(size_t)row * VW + w];
+      }
     (void)hipMemcpy(yb, y.data(), y.size() * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(yi, img.data(), img.size() * 4, hipMemcpyHostToDevice);
   }
   (void)hipMalloc(&dZ, (size_t)B * V * 2);
   (void)hipMalloc(&gW, (size_t)d * V * 4);
@@ -74,8 +82,9 @@ int main() {
     std::vector<float> ts;
     for (int rep = 0; rep < 200; ++rep) {
       (void)hipEventRecord(e0, nullptr);
-      cc_dec_bce_dw(D3, D3t, B, D3p, D3tp, nullptr, Wo, (const float *)bo, B, d, V, (const uint32_t *)yb, dZ,
-                    (float *)gW, (float *)gb, (double *)part, (double *)loss, 1.0 / (B * V), (uint32_t *)tick, nullptr);
+      cc_dec_bce_dw_img(D3, D3t, B, D3p, D3tp, nullptr, Wo, (const float *)bo, B, d, V, (const uint32_t *)yb,
+                        (const uint32_t *)yi, dZ, V, (float *)gW, (float *)gb, (double *)part, (double *)loss,
+                        1.0 / (B * V), (uint32_t *)tick, nullptr);
       (void)hipEventRecord(e1, nullptr);
       (void)hipEventSynchronize(e1);
       float ms = 0.f;
@@ -90,9 +99,9 @@ int main() {
 #endif
   for (int rep = 0; rep < 6; ++rep) {
     (void)hipEventRecord(e0, nullptr);
-    int rc = cc_dec_bce_dw(D3, D3t, B, D3p, D3tp, nullptr, Wo, (const float *)bo, B, d, V, (const uint32_t *)yb, dZ,
-                           (float *)gW, (float *)gb, (double *)part, (double *)loss, 1.0 / (B * V), (uint32_t *)tick,
-                           nullptr);
+    int rc = cc_dec_bce_dw_img(D3, D3t, B, D3p, D3tp, nullptr, Wo, (const float *)bo, B, d, V, (const uint32_t *)yb,
+                               (const uint32_t *)yi, dZ, V, (float *)gW, (float *)gb, (double *)part, (double *)loss,
+                               1.0 / (B * V), (uint32_t *)tick, nullptr);
     (void)hipEventRecord(e1, nullptr);
     (void)hipDeviceSynchronize();
     float ms = 0.f;
