@@ -23,9 +23,11 @@ FLAGS = ['-O3', '-fPIC', '-std=c++17', f'--offload-arch={ARCH}', '-I', INC, '-I'
          '-Wall', '-Wno-unused-function', '-Wno-unused-variable'] + os.environ.get('CCREC_EXTRA_FLAGS', '').split()
 
 
-# per-file flags: the fused D1 kernel's inputs are finite logits; without NaN semantics its max()
-# needs no canonicalising v_max (one VALU op per logit in a VALU-bound epilogue)
-FILE_FLAGS = {'decout.hip': ['-fno-honor-nans']}
+# per-file flags: the fused output-layer kernels' inputs are finite (logits, M~ rows, row stats;
+# the KL's clipped targets never meet an infinite log); without NaN semantics their min / max need
+# no canonicalising v_max (one VALU op per logit in VALU-bound epilogues; decreg.hip: the sampled
+# main pass's scratch spill goes too)
+FILE_FLAGS = {'decout.hip': ['-fno-honor-nans'], 'decreg.hip': ['-fno-honor-nans']}
 
 
 def sources():

@@ -28,13 +28,7 @@
 
 namespace {
 
-#ifndef CCREC_DX_ST   // dev knob (A/B builds): LDS stages of the split-K pipeline
-#define CCREC_DX_ST 4
-#endif
-#ifndef DX_DIAG        // dev diagnostics only: 1 no MFMAs, 2 no DMA (0 in the library)
-#define DX_DIAG 0
-#endif
-constexpr int XBM = 128, XBN = 128, XBK = 64, XST = CCREC_DX_ST, XNT = 256;
+constexpr int XBM = 128, XBN = 128, XBK = 64, XST = 4, XNT = 256;
 constexpr int XTILE_BYTES = (XBM + XBN) * XBK * 2;  // one stage: A then B, 32 KB
 constexpr int XLDS = XST * XTILE_BYTES;             // 128 KB
 
@@ -62,7 +56,6 @@ __device__ __forceinline__ void dma_tile(const DxP &p, const __amdgpu_buffer_rsr
   char *sa = smem + st * XTILE_BYTES, *sb = sa + XBM * XBK * 2;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    if constexpr (DX_DIAG & 2) break;
     const int i = w * 4 + u;       // instruction index: rows 8i .. 8i + 7
     const int row = 8 * i + rl;
     const int c = slot ^ ((row >> 1) & 7);
@@ -76,11 +69,7 @@ __device__ __forceinline__ void dma_tile(const DxP &p, const __amdgpu_buffer_rsr
 
 template <int N_OUT>
 __device__ __forceinline__ void wait_vm() {
-  if constexpr (N_OUT == 32)
-    asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-  else if constexpr (N_OUT == 24)
-    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-  else if constexpr (N_OUT == 16)
+  if constexpr (N_OUT == 16)
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else if constexpr (N_OUT == 8)
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -120,11 +109,7 @@ __global__ __launch_bounds__(XNT) void dx_splitk_kernel(DxP p) {
     // tile t landed in every wave (own DMAs counted, then the barrier); 8 DMA instructions per
     // wave per tile, min(2, nk - 1 - t) tiles issued after t may stay in flight
     const int after = min(XST - 2, nk - 1 - t);
-    if (after >= 4)
-      wait_vm<32>();
-    else if (after == 3)
-      wait_vm<24>();
-    else if (after == 2)
+    if (after >= 2)
       wait_vm<16>();
     else if (after == 1)
       wait_vm<8>();
@@ -140,11 +125,6 @@ __global__ __launch_bounds__(XNT) void dx_splitk_kernel(DxP p) {
       const int c = 2 * kk + half;
       const bf16x8_t a0 = frag(sa, ar, c), a1 = frag(sa, ar + 32, c);
       const bf16x8_t b0 = frag(sb, br, c), b1 = frag(sb, br + 32, c);
-      if constexpr (DX_DIAG & 1) {
-        acc[0][0][0] += (float)a0[0] + (float)b0[0];
-        acc[1][1][0] += (float)a1[0] + (float)b1[0];
-        continue;
-      }
       acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
       acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
       acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
@@ -252,11 +232,6 @@ __global__ __launch_bounds__(WNT) void dx_wide_kernel(DxP p) {
       const int c = 2 * kk + half;
       const bf16x8_t a0 = frag(sa, ar, c), a1 = frag(sa, ar + 32, c);
       const bf16x8_t b0 = frag(sb, br, c), b1 = frag(sb, br + 32, c);
-      if constexpr (DX_DIAG & 1) {
-        acc[0][0][0] += (float)a0[0] + (float)b0[0];
-        acc[1][1][0] += (float)a1[0] + (float)b1[0];
-        continue;
-      }
       acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
       acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
       acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
